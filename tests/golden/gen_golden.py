@@ -1,0 +1,519 @@
+"""Generate golden input/output vectors from the reference's OWN hot-path code.
+
+Test infrastructure only.  Runs in the build container (where the read-only
+reference checkout lives at /root/reference); skips cleanly when it is absent.
+Nothing from the reference is copied: the reference source files are executed
+in place (path-loaded, bytecode writing disabled) with ``sys.modules`` stubs
+for the third-party imports that are not installed here (gymnasium,
+tensordict, pettingzoo) and for the agilerl sub-packages these files import
+but the exercised methods never touch.  Only seeded inputs and the outputs the
+reference produced are written, as small ``.npz`` files beside this script.
+
+Reference functions exercised (paths relative to /root/reference):
+  * agilerl/components/rollout_buffer.py:413-481  RolloutBuffer.compute_returns_and_advantages
+  * agilerl/components/segment_tree.py            SumSegmentTree / MinSegmentTree
+  * agilerl/components/replay_buffer.py:261-428   PrioritizedReplayBuffer (_update_priority,
+                                                  _sample_proportional, _calculate_weights,
+                                                  update_priorities)
+  * agilerl/algorithms/ppo.py:814-921             PPO._learn_from_rollout_buffer_flat (loss math)
+  * agilerl/algorithms/dqn.py:274-324             DQN.update (TD target)
+  * agilerl/algorithms/dqn_rainbow.py:284-367     RainbowDQN._dqn_loss (C51 projection)
+  * agilerl/hpo/tournament.py:41-119              TournamentSelection
+
+Usage:  python tests/golden/gen_golden.py  [--ref /root/reference]
+"""
+
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True  # never write __pycache__ into the read-only reference
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+# --------------------------------------------------------------------------- #
+# import stubs                                                                #
+# --------------------------------------------------------------------------- #
+class _StubMeta(type):
+    """Placeholder classes answer any class attribute (enum members, ...)."""
+
+    def __getattr__(cls, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        return f"<stub {cls.__name__}.{name}>"
+
+
+class _StubModule(types.ModuleType):
+    """Module whose every attribute is a fresh placeholder class."""
+
+    def __getattr__(self, name):  # noqa: D401
+        if name.startswith("__"):
+            raise AttributeError(name)
+        cls = _StubMeta(name, (), {"__init__": lambda self, *a, **k: None})
+        setattr(self, name, cls)
+        return cls
+
+
+def _stub(name: str) -> types.ModuleType:
+    mod = _StubModule(name)
+    mod.__path__ = []  # behave like a package
+    sys.modules[name] = mod
+    return mod
+
+
+def _install_stubs() -> None:
+    for name in [
+        "gymnasium",
+        "gymnasium.spaces",
+        "tensordict",
+        "tensordict.nn",
+        "pettingzoo",
+        "agilerl",
+        "agilerl.typing",
+        "agilerl.protocols",
+        "agilerl.utils",
+        "agilerl.utils.algo_utils",
+        "agilerl.algorithms",
+        "agilerl.algorithms.core",
+        "agilerl.algorithms.core.base",
+        "agilerl.algorithms.core.registry",
+        "agilerl.modules",
+        "agilerl.modules.base",
+        "agilerl.modules.configs",
+        "agilerl.networks",
+        "agilerl.networks.value_networks",
+        "agilerl.networks.q_networks",
+        "agilerl.wrappers",
+        "agilerl.wrappers.make_evolvable",
+        "agilerl.components",
+    ]:
+        _stub(name)
+    sys.modules["gymnasium"].spaces = sys.modules["gymnasium.spaces"]
+
+
+def _load(ref: str, modname: str, relpath: str):
+    path = os.path.join(ref, relpath)
+    spec = importlib.util.spec_from_file_location(modname, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[modname] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+# --------------------------------------------------------------------------- #
+# GAE                                                                         #
+# --------------------------------------------------------------------------- #
+def gen_gae(rb_mod, out: dict) -> None:
+    RolloutBuffer = rb_mod.RolloutBuffer
+    cases = [
+        # (T, N, p_done, use_gae, gamma, lam, seed)
+        (16, 128, 0.01, True, 0.99, 0.95, 0),   # config-2 shape (one agent)
+        (64, 33, 0.05, True, 0.99, 0.95, 1),    # ragged N
+        (1, 7, 0.5, True, 0.99, 0.95, 2),       # T == 1: only the bootstrap branch
+        (40, 16, 0.3, True, 0.97, 0.9, 3),      # dense dones, other gamma/lambda
+        (512, 128, 0.01, True, 0.99, 0.95, 4),  # long scan
+        (32, 64, 0.05, False, 0.99, 0.95, 5),   # Monte-Carlo branch
+        (24, 5, 1.0, True, 0.99, 0.95, 6),      # every step terminal
+        (24, 5, 0.0, True, 0.99, 1.0, 7),       # no terminal, lambda 1
+    ]
+    for k, (T, N, pd, use_gae, gamma, lam, seed) in enumerate(cases):
+        rng = np.random.default_rng(seed)
+        r = rng.standard_normal((T, N)).astype(np.float32)
+        v = rng.standard_normal((T, N)).astype(np.float32)
+        d = rng.random((T, N)) < pd
+        lv = rng.standard_normal(N).astype(np.float32)
+        ld = rng.random(N) < pd
+        rb = object.__new__(RolloutBuffer)
+        rb.capacity, rb.num_envs, rb.full, rb.pos = T, N, True, T
+        rb.use_gae, rb.gamma, rb.gae_lambda = use_gae, gamma, lam
+        rb.buffer = {
+            "rewards": torch.from_numpy(r.copy()),
+            "dones": torch.from_numpy(d.copy()),
+            "values": torch.from_numpy(v.copy()),
+            "advantages": torch.zeros(T, N),
+            "returns": torch.zeros(T, N),
+        }
+        rb.compute_returns_and_advantages(torch.from_numpy(lv), torch.from_numpy(ld))
+        out[f"gae{k}"] = dict(
+            rewards=r, values=v, dones=d.astype(np.uint8), last_value=lv,
+            last_done=ld.astype(np.uint8), gamma=np.float64(gamma), lam=np.float64(lam),
+            use_gae=np.int32(use_gae),
+            advantages=rb.buffer["advantages"].numpy().copy(),
+            returns=rb.buffer["returns"].numpy().copy(),
+        )
+
+
+# --------------------------------------------------------------------------- #
+# segment tree + PER                                                          #
+# --------------------------------------------------------------------------- #
+def gen_segment_tree(st_mod, out: dict) -> None:
+    Sum, Min = st_mod.SumSegmentTree, st_mod.MinSegmentTree
+    rng = np.random.default_rng(11)
+    cap = 64
+    s, m = Sum(cap), Min(cap)
+    idx = rng.integers(0, cap, 300)
+    val = np.abs(rng.standard_normal(300)) + 1e-3
+    for i, x in zip(idx, val):
+        s[int(i)] = float(x)
+        m[int(i)] = float(x)
+    q = np.concatenate([rng.random(200) * s.sum(), [0.0, s.sum(), s.sum() * 0.5]])
+    ret = np.array([s.retrieve(float(u)) for u in q], dtype=np.int64)
+    ranges = [(0, 0), (3, 17), (0, 63), (10, 11), (5, -1), (31, 33)]
+    sums = np.array([s.sum(a, b) for a, b in ranges])
+    mins = np.array([m.min(a, b) for a, b in ranges])
+    out["segtree"] = dict(
+        cap=np.int64(cap), set_idx=idx.astype(np.int64), set_val=val,
+        sum_tree=np.array(s.tree), min_tree=np.array(m.tree), queries=q,
+        retrieve=ret, ranges=np.array(ranges, dtype=np.int64), range_sum=sums, range_min=mins,
+    )
+
+
+def _per_add(buf, n: int) -> None:
+    """The priority half of PrioritizedReplayBuffer.add (replay_buffer.py:296-309);
+    the TensorDict storage half is not needed for the tree."""
+    for _ in range(n):
+        buf._update_priority(buf.tree_ptr, buf.max_priority)
+        buf.tree_ptr = (buf.tree_ptr + 1) % buf.max_size
+    buf._size = min(buf._size + n, buf.max_size)
+
+
+def gen_per(rp_mod, out: dict) -> None:
+    PER = rp_mod.PrioritizedReplayBuffer
+    cases = [
+        # (max_size, n_add, B, beta, alpha, rounds, seed)
+        (100, 60, 32, 0.4, 0.6, 3, 21),
+        (1000, 1000, 64, 0.4, 0.6, 4, 22),     # full buffer, config-3 batch
+        (5000, 7321, 64, 0.6, 0.6, 3, 23),     # wrapped ring, non-pow2 max_size
+        (4096, 3000, 256, 0.4, 0.5, 2, 24),    # pow2 capacity, partial fill
+    ]
+    for k, (max_size, n_add, B, beta, alpha, rounds, seed) in enumerate(cases):
+        torch.manual_seed(seed)
+        rng = np.random.default_rng(seed)
+        buf = PER(max_size, alpha=alpha)
+        _per_add(buf, n_add)
+        rec = {"max_size": np.int64(max_size), "n_add": np.int64(n_add), "B": np.int64(B),
+               "beta": np.float64(beta), "alpha": np.float64(alpha), "seed": np.int64(seed),
+               "rounds": np.int64(rounds)}
+        # record the uniform stream the sampler consumes (global torch CPU generator)
+        for rd in range(rounds):
+            state = torch.get_rng_state()
+            u = torch.rand(B).numpy().copy()
+            torch.set_rng_state(state)
+            idxs = buf._sample_proportional(B)
+            w = buf._calculate_weights(idxs, beta)
+            pri = (np.abs(rng.standard_normal(B)) * (0.1 if rd == 1 else 1.0)).astype(np.float32)
+            if rd == 2:
+                pri[: B // 4] = 1e-9  # hits the 1e-5 floor
+            buf.update_priorities(idxs.unsqueeze(1), torch.from_numpy(pri))
+            extra = 7 + 3 * rd
+            _per_add(buf, extra)  # interleaved inserts at max priority
+            rec[f"u{rd}"] = u
+            rec[f"idx{rd}"] = idxs.numpy().astype(np.int64)
+            rec[f"w{rd}"] = w.numpy().astype(np.float32)
+            rec[f"pri{rd}"] = pri
+            rec[f"extra{rd}"] = np.int64(extra)
+            rec[f"sum_tree{rd}"] = np.array(buf.sum_tree.tree)
+            rec[f"min_tree{rd}"] = np.array(buf.min_tree.tree)
+            rec[f"max_priority{rd}"] = np.float64(buf.max_priority)
+            rec[f"tree_ptr{rd}"] = np.int64(buf.tree_ptr)
+            rec[f"size{rd}"] = np.int64(buf._size)
+        out[f"per{k}"] = rec
+
+
+# --------------------------------------------------------------------------- #
+# PPO clipped-surrogate loss                                                  #
+# --------------------------------------------------------------------------- #
+class _FakeTD(dict):
+    def is_empty(self):
+        return len(self) == 0
+
+    def get(self, key, default=None):
+        return dict.get(self, key, default)
+
+    def __getitem__(self, key):
+        if isinstance(key, str):
+            return dict.__getitem__(self, key)
+        idx = torch.as_tensor(np.asarray(key))
+        return _FakeTD({k: v[idx] for k, v in self.items()})
+
+
+def gen_ppo(ppo_mod, spaces_mod, out: dict) -> None:
+    PPO = ppo_mod.PPO
+    cases = [
+        # (S, batch, epochs, clip, vf, ent, seed)
+        (2048, 128, 4, 0.2, 0.5, 0.01, 31),  # config-2 rollout
+        (300, 64, 2, 0.1, 1.0, 0.05, 32),    # short last minibatch
+    ]
+    for k, (S, bs, E, clip, vf, ent, seed) in enumerate(cases):
+        rng = np.random.default_rng(seed)
+        old_logp = rng.uniform(-3, -0.05, S).astype(np.float32)
+        # per-sample "network outputs" the fake evaluate_actions returns as leaves
+        new_logp = (old_logp + rng.normal(0, 0.15, S)).astype(np.float32)
+        adv = (rng.standard_normal(S) * 2 + 0.3).astype(np.float32)
+        ret = rng.standard_normal(S).astype(np.float32)
+        old_v = rng.standard_normal(S).astype(np.float32)
+        new_v = (old_v + rng.normal(0, 0.3, S)).astype(np.float32)
+        H = rng.uniform(0, np.log(4), S).astype(np.float32)
+
+        P_logp = torch.tensor(new_logp, requires_grad=True)
+        P_v = torch.tensor(new_v, requires_grad=True)
+        P_H = torch.tensor(H, requires_grad=True)
+        snaps: list = []
+
+        class _Opt:
+            def zero_grad(self):
+                for p in (P_logp, P_v, P_H):
+                    p.grad = None
+
+            def step(self):
+                snaps.append((P_logp.grad.clone(), P_v.grad.clone(), P_H.grad.clone()))
+
+        class _Net:
+            def parameters(self):
+                return []
+
+        class _RB:
+            def size(self):
+                return S
+
+        fake = object.__new__(PPO)
+        fake.batch_size, fake.update_epochs = bs, E
+        fake.clip_coef, fake.vf_coef, fake.ent_coef = clip, vf, ent
+        fake.target_kl, fake.accelerator, fake.max_grad_norm = None, None, 0.5
+        fake.action_space = spaces_mod.Discrete()
+        fake.optimizer, fake.actor, fake.critic = _Opt(), _Net(), _Net()
+        fake.rollout_buffer = _RB()
+
+        def _eval(obs, actions, hidden_state=None, action_mask=None):
+            i = obs.long().view(-1)
+            return P_logp[i], P_H[i], P_v[i]
+
+        fake.evaluate_actions = _eval
+        td = _FakeTD(
+            observations=torch.arange(S, dtype=torch.float32).view(S, 1),
+            actions=torch.zeros(S, 1),
+            log_probs=torch.tensor(old_logp),
+            advantages=torch.tensor(adv),
+            returns=torch.tensor(ret),
+            values=torch.tensor(old_v),
+        )
+        np.random.seed(seed)
+        perm_state = np.random.get_state()
+        mean_loss = PPO._learn_from_rollout_buffer_flat(fake, buffer_td_external=td)
+        # replay the permutation stream the learner consumed
+        np.random.set_state(perm_state)
+        perms = []
+        idx = np.arange(S)
+        for _ in range(E):
+            np.random.shuffle(idx)
+            perms.append(idx.copy())
+        n_mb = len(snaps)
+        out[f"ppo{k}"] = dict(
+            S=np.int64(S), batch=np.int64(bs), epochs=np.int64(E), clip=np.float64(clip),
+            vf=np.float64(vf), ent=np.float64(ent), seed=np.int64(seed),
+            old_logp=old_logp, new_logp=new_logp, adv=adv, ret=ret, old_v=old_v,
+            new_v=new_v, H=H, adv_norm=td["advantages"].numpy().copy(),
+            perms=np.stack(perms).astype(np.int64), mean_loss=np.float64(mean_loss),
+            g_logp=np.stack([s[0].numpy() for s in snaps]),
+            g_v=np.stack([s[1].numpy() for s in snaps]),
+            g_H=np.stack([s[2].numpy() for s in snaps]),
+            n_minibatches=np.int64(n_mb),
+        )
+
+
+# --------------------------------------------------------------------------- #
+# DQN TD target                                                               #
+# --------------------------------------------------------------------------- #
+def gen_dqn(dqn_mod, out: dict) -> None:
+    DQN = dqn_mod.DQN
+    for k, (B, A, double, gamma, seed) in enumerate(
+        [(128, 2, False, 0.99, 41), (64, 6, True, 0.97, 42), (33, 4, False, 0.9, 43)]
+    ):
+        rng = np.random.default_rng(seed)
+        q_next_online = rng.standard_normal((B, A)).astype(np.float32)
+        q_next_target = rng.standard_normal((B, A)).astype(np.float32)
+        q_cur = rng.standard_normal((B, A)).astype(np.float32)
+        r = rng.standard_normal((B, 1)).astype(np.float32)
+        d = (rng.random((B, 1)) < 0.2).astype(np.float32)
+        a = rng.integers(0, A, (B, 1)).astype(np.int64)
+        obs_tag, next_tag = torch.zeros(B, 1), torch.ones(B, 1)
+        Qc = torch.tensor(q_cur, requires_grad=True)
+        rec: dict = {}
+
+        class _Actor:
+            def __call__(self, x):
+                return Qc if float(x[0, 0]) == 0 else torch.tensor(q_next_online)
+
+        class _Target:
+            def __call__(self, x):
+                return torch.tensor(q_next_target)
+
+        class _Crit:
+            def __call__(self, q_eval, y):
+                rec["q_eval"], rec["y"] = q_eval.detach().clone(), y.detach().clone()
+                return torch.nn.functional.mse_loss(q_eval, y)
+
+        class _Opt:
+            def zero_grad(self):
+                Qc.grad = None
+
+            def step(self):
+                rec["g_q"] = Qc.grad.clone()
+
+        fake = object.__new__(DQN)
+        fake.double, fake.gamma, fake.accelerator = double, gamma, None
+        fake.actor, fake.actor_target, fake.criterion, fake.optimizer = _Actor(), _Target(), _Crit(), _Opt()
+        loss = DQN.update(fake, obs_tag, torch.tensor(a), torch.tensor(r), next_tag, torch.tensor(d))
+        out[f"dqn{k}"] = dict(
+            double=np.int32(double), gamma=np.float64(gamma), q_next_online=q_next_online,
+            q_next_target=q_next_target, q_cur=q_cur, r=r, d=d, a=a,
+            y=rec["y"].numpy(), q_eval=rec["q_eval"].numpy(), loss=np.float32(loss.item()),
+            g_q=rec["g_q"].numpy(),
+        )
+
+
+# --------------------------------------------------------------------------- #
+# Rainbow C51 projection                                                      #
+# --------------------------------------------------------------------------- #
+def gen_c51(rainbow_mod, out: dict) -> None:
+    Rainbow = rainbow_mod.RainbowDQN
+    cases = [
+        # (B, A, Z, vmin, vmax, gamma, seed)
+        (64, 6, 51, -200.0, 200.0, 0.99**4, 51),   # config 3 (n-step gamma)
+        (64, 6, 51, -100.0, 100.0, 0.99, 52),      # create_population overrides
+        (40, 4, 51, 0.0, 200.0, 0.99, 53),         # class defaults
+        (17, 3, 11, -10.0, 10.0, 0.9, 54),         # small support, heavy clamping
+    ]
+    for k, (B, A, Z, vmin, vmax, gamma, seed) in enumerate(cases):
+        rng = np.random.default_rng(seed)
+        support = torch.linspace(vmin, vmax, Z)
+        q_next = rng.standard_normal((B, A)).astype(np.float32)
+        lt = torch.tensor(rng.standard_normal((B, A, Z)).astype(np.float32) * 2)
+        tdist = torch.softmax(lt, dim=-1).clamp(min=1e-3).numpy()
+        lc = torch.tensor(rng.standard_normal((B, A, Z)).astype(np.float32))
+        logp_cur = torch.log_softmax(lc, dim=-1).numpy()
+        scale = (vmax - vmin) * 0.3
+        r = (rng.standard_normal((B, 1)) * scale).astype(np.float32)
+        r[:3, 0] = [vmax * 5, vmin * 5, 0.0]  # clamp both ends
+        d = (rng.random((B, 1)) < 0.2).astype(np.float32)
+        a = rng.integers(0, A, (B, 1)).astype(np.int64)
+
+        class _Actor:
+            def __call__(self, x, q=True, log=False):
+                if float(x.reshape(-1)[0]) == 1.0:  # next obs
+                    return torch.tensor(q_next)
+                return torch.tensor(logp_cur)
+
+        class _Target:
+            def __call__(self, x, q=True, log=False):
+                return torch.tensor(tdist)
+
+        fake = object.__new__(Rainbow)
+        fake.actor, fake.actor_target = _Actor(), _Target()
+        fake.batch_size, fake.num_atoms, fake.support = B, Z, support
+        fake.v_min, fake.v_max = vmin, vmax
+        fake.delta_z = (vmax - vmin) / (Z - 1)
+        fake.device = "cpu"
+        fake.preprocess_observation = lambda o: o
+        loss = Rainbow._dqn_loss(
+            fake, torch.zeros(B, 1), torch.tensor(a), torch.tensor(r), torch.ones(B, 1),
+            torch.tensor(d), gamma,
+        )
+        out[f"c51_{k}"] = dict(
+            B=np.int64(B), A=np.int64(A), Z=np.int64(Z), vmin=np.float64(vmin),
+            vmax=np.float64(vmax), gamma=np.float64(gamma), support=support.numpy(),
+            q_next=q_next, target_dist=tdist, logp_cur=logp_cur, r=r, d=d, a=a,
+            loss=loss.numpy(),
+        )
+
+
+# --------------------------------------------------------------------------- #
+# tournament selection                                                        #
+# --------------------------------------------------------------------------- #
+def gen_tournament(tour_mod, out: dict) -> None:
+    TS = tour_mod.TournamentSelection
+
+    class _Agent:
+        def __init__(self, index, fitness):
+            self.index, self.fitness, self.parent = index, fitness, index
+
+        def clone(self, index=None, wrap=True):
+            c = _Agent(self.index if index is None else index, list(self.fitness))
+            c.parent = self.index
+            return c
+
+    for k, (P, tsize, elitism, eval_loop, seed) in enumerate(
+        [(8, 2, True, 1, 61), (8, 3, False, 2, 62), (32, 2, True, 3, 63), (5, 4, True, 1, 64)]
+    ):
+        rng = np.random.default_rng(seed)
+        fit = rng.standard_normal((P, 4)) * 50
+        fit[1] = fit[0]  # a tie
+        pop = [_Agent(i + 10 * k, list(fit[i])) for i in range(P)]
+        ts = TS(tsize, elitism, P, eval_loop)
+        ts.language_model = False
+        np.random.seed(seed)
+        elite, new_pop = ts.select(pop)
+        out[f"tour{k}"] = dict(
+            P=np.int64(P), tsize=np.int64(tsize), elitism=np.int32(elitism),
+            eval_loop=np.int64(eval_loop), seed=np.int64(seed), fitness=fit,
+            indices=np.array([a.index for a in pop], dtype=np.int64),
+            elite_parent=np.int64(elite.parent),
+            parents=np.array([a.parent for a in new_pop], dtype=np.int64),
+            new_indices=np.array([a.index for a in new_pop], dtype=np.int64),
+        )
+
+
+# --------------------------------------------------------------------------- #
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    args = ap.parse_args()
+    if not os.path.isdir(os.path.join(args.ref, "agilerl")):
+        print("reference checkout not present; nothing generated")
+        return
+    torch.set_num_threads(1)
+    _install_stubs()
+    ref = args.ref
+    st = _load(ref, "agilerl.components.segment_tree", "agilerl/components/segment_tree.py")
+    rp = _load(ref, "agilerl.components.replay_buffer", "agilerl/components/replay_buffer.py")
+    rb = _load(ref, "agilerl.components.rollout_buffer", "agilerl/components/rollout_buffer.py")
+    ppo = _load(ref, "agilerl.algorithms.ppo", "agilerl/algorithms/ppo.py")
+    dqn = _load(ref, "agilerl.algorithms.dqn", "agilerl/algorithms/dqn.py")
+    rainbow = _load(ref, "agilerl.algorithms.dqn_rainbow", "agilerl/algorithms/dqn_rainbow.py")
+    tour = _load(ref, "agilerl.hpo.tournament", "agilerl/hpo/tournament.py")
+
+    groups: dict[str, dict] = {}
+    gen_gae(rb, groups)
+    gen_segment_tree(st, groups)
+    gen_per(rp, groups)
+    gen_ppo(ppo, sys.modules["gymnasium.spaces"], groups)
+    gen_dqn(dqn, groups)
+    gen_c51(rainbow, groups)
+    gen_tournament(tour, groups)
+
+    meta = {
+        "generator": "tests/golden/gen_golden.py",
+        "torch": torch.__version__,
+        "numpy": np.__version__,
+        "python": sys.version.split()[0],
+        "reference_pins": {"torch": "2.9.0 (pyproject.toml:34)", "numpy": ">=2 (pyproject.toml:22)"},
+        "groups": sorted(groups),
+    }
+    for name, rec in groups.items():
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
+    with open(os.path.join(HERE, "META.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print("wrote", len(groups), "fixtures")
+
+
+if __name__ == "__main__":
+    main()
