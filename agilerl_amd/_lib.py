@@ -1,0 +1,95 @@
+"""ctypes binding of libagx.so (the C ABI declared in include/agx.h).
+
+This is the binding a maintainer of the reference would add (see
+INTEGRATION.md).  The product path has NO CPU fallback: if the library is
+missing or no GPU is visible, every op raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must load torch's HIP runtime before libagx binds to it)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libagx.so")
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int64
+_D = ctypes.c_double
+_F = ctypes.c_float
+_INT = ctypes.c_int
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/agx.h one-to-one
+SIGNATURES = {
+    "agx_last_error": (ctypes.c_char_p, []),
+    "agx_version": (_INT, []),
+    "agx_device_info": (_INT, [_P]),
+    "agx_gae_workspace_bytes": (_SZ, [_I, _I, _I]),
+    "agx_gae": (_INT, [_P, _P, _P, _P, _P, _I, _I, _I, _D, _D, _INT, _P, _P, _P, _P, _P]),
+    "agx_adv_normalize": (_INT, [_P, _P, _I, _I, _P]),
+    "agx_ppo_loss_fwd_bwd": (_INT, [_P] * 8 + [_I, _I, _F, _F, _F, _P, _P, _P, _P, _P]),
+    "agx_per_workspace_bytes": (_SZ, [_I, _I]),
+    "agx_per_init": (_INT, [_P, _P, _I, _P]),
+    "agx_per_add": (_INT, [_P, _P, _I, _I, _I, _I, _D, _P, _P, _P]),
+    "agx_per_update": (_INT, [_P, _P, _I, _I, _P, _P, _I, _D, _D, _P, _P, _P]),
+    "agx_per_sample": (_INT, [_P, _P, _I, _P, _I, _I, _D, _P, _P, _P, _P]),
+    "agx_per_gather": (_INT, [_P, _P, _I, _P, _P]),
+    "agx_td_target": (_INT, [_P] * 6 + [_I, _I, _D, _INT, _P, _P, _P, _P]),
+    "agx_c51_project_loss": (_INT, [_P] * 7 + [_I, _I, _I, _D, _D, _D, _P, _P, _P]),
+    "agx_adam_workspace_bytes": (_SZ, [_I, _I]),
+    "agx_clip_adam": (_INT, [_P, _P, _P, _P, _I, _I, _P, _INT, _F, _P, _F, _F, _F, _I, _P, _P]),
+    "agx_polyak": (_INT, [_P, _P, _I, _F, _P]),
+    "agx_debug_pow": (_INT, [_P, _P, _P, _I, _P]),
+}
+
+_lib = None
+
+
+class AgxError(RuntimeError):
+    pass
+
+
+def load(require_gpu: bool = True):
+    """Load libagx.so (raises if absent).  With require_gpu, also insist on a
+    visible ROCm device — the product path never runs on the CPU."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise AgxError(
+                f"{LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`"
+            )
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    if require_gpu and not torch.cuda.is_available():
+        raise AgxError("agilerl_amd needs an MI355X (ROCm device); no CPU fallback exists")
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = _lib.agx_last_error().decode(errors="replace") if _lib is not None else ""
+        raise AgxError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream(s=None) -> int:
+    s = torch.cuda.current_stream() if s is None else s
+    return s.cuda_stream
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    check(getattr(lib, name)(*args), name)

@@ -1,0 +1,211 @@
+// DQN TD target and Rainbow C51 categorical projection + cross entropy.
+//
+// TD target — agilerl/algorithms/dqn.py:296-314 (DQN.update):
+//   q_t = max_a Qtgt(s')  |  Qtgt(s')[argmax_a Q(s')] (double)
+//   y   = r + (gamma*q_t)*(1-d)        (f32, one rounding per op)
+//   loss = MSE(Q(s)[a], y);  dloss/dQ(s)[a] = 2 (Q[a]-y) / B
+//
+// C51 — agilerl/algorithms/dqn_rainbow.py:313-367 (RainbowDQN._dqn_loss), f32:
+//   a* = argmax Q_online(s') (first maximum, like torch.argmax)
+//   t_z = clamp(r + ((1-d)*gamma)*z, vmin, vmax);  b = (t_z - vmin) / f32(dz)
+//   L = floor(b), U = ceil(b); L[(U>0)&(U==L)] -= 1; U[(Z-1>L)&(U==L)] += 1
+//   proj.index_add_(L, p*(U-b)); proj.index_add_(U, p*(b-L))   (serial order)
+//   loss_i = -sum_z proj_z * log_p[a_i, z]
+// The serial index_add_ adds, per bin, all lower masses in atom order and
+// then all upper masses in atom order.  When b is monotone in z (support
+// ascending, (1-d)*gamma >= 0 — always the case in Rainbow) the atoms feeding
+// a bin form a contiguous run, found by a binary search in LDS; the bin's
+// lane then adds that run in order — bit-identical to the reference's
+// projection.  A row whose b is not monotone falls back to the full ordered
+// scan.  One wave per row, lane z <-> atom z (Z <= 64 per pass, Z <= 256).
+// Algorithmic bytes per row: 4A (q row) + 4Z (target row a*) + 4Z (log_p row
+// a_i) + 8 (r, d) + 4 (loss) = 444 B at A = 6, Z = 51.
+#include "agx_common.h"
+
+namespace agx {
+
+__global__ void td_target_kernel(const float *__restrict__ qno, const float *__restrict__ qnt,
+                                 const float *__restrict__ qc, const int64_t *__restrict__ act,
+                                 const float *__restrict__ r, const float *__restrict__ d, int64_t B,
+                                 int A, float g, int dbl, float *__restrict__ y,
+                                 float *__restrict__ g_q) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const float *tn = qnt + i * A;
+    float qt;
+    if (dbl) {
+        const float *on = qno + i * A;
+        int best = 0;
+        float bv = on[0];
+        for (int a = 1; a < A; ++a)
+            if (on[a] > bv) {
+                bv = on[a];
+                best = a;
+            }
+        qt = tn[best];
+    } else {
+        qt = tn[0];
+        for (int a = 1; a < A; ++a) qt = fmaxf(qt, tn[a]);
+    }
+    const float yi = r[i] + (g * qt) * (1.0f - d[i]);
+    y[i] = yi;
+    if (g_q) {
+        const int64_t ai = act[i];
+        const float diff = qc[i * A + ai] - yi;
+        const float scale = 2.0f / (float)B;
+        for (int a = 0; a < A; ++a) g_q[i * A + a] = (a == ai) ? diff * scale : 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(1024) void td_loss_kernel(const float *__restrict__ qc,
+                                                       const int64_t *__restrict__ act,
+                                                       const float *__restrict__ y, int64_t B,
+                                                       int A, float *__restrict__ loss) {
+    __shared__ double red[1024 / kWave];
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
+        const double diff = (double)qc[i * A + act[i]] - (double)y[i];
+        s += diff * diff;
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x / 64] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < (int)(blockDim.x / 64); ++w) t += red[w];
+        *loss = (float)(t / (double)B);
+    }
+}
+
+constexpr int kC51Waves = 4;   // rows per block
+constexpr int kC51MaxZ = 256;  // atoms per row (lane handles Z/64 of them)
+
+__device__ __forceinline__ int lower_bound_i(const int *a, int n, int key) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kC51Waves * 64) void c51_kernel(
+    const float *__restrict__ qno, const float *__restrict__ tdist, const float *__restrict__ logp,
+    const int64_t *__restrict__ act, const float *__restrict__ rew, const float *__restrict__ dn,
+    const float *__restrict__ support, int64_t B, int A, int Z, float vmin, float vmax, float dz,
+    float g, float *__restrict__ loss, float *__restrict__ proj) {
+    __shared__ int sL[kC51Waves][kC51MaxZ];
+    __shared__ int sU[kC51Waves][kC51MaxZ];
+    __shared__ float sml[kC51Waves][kC51MaxZ];
+    __shared__ float smu[kC51Waves][kC51MaxZ];
+    const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * kC51Waves + w;
+    const bool live = row < B;            // dead waves shadow the last row and store nothing,
+    const int64_t i = live ? row : B - 1;  // so every wave reaches the barrier
+    // a* = argmax_a Q_online(s'), first maximum
+    float bv = -__builtin_inff();
+    int ba = 0x7fffffff;
+    for (int a = lane; a < A; a += 64) {
+        const float q = qno[i * A + a];
+        if (q > bv || (q == bv && a < ba)) {
+            bv = q;
+            ba = a;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float q2 = __shfl_xor(bv, o, 64);
+        const int a2 = __shfl_xor(ba, o, 64);
+        if (q2 > bv || (q2 == bv && a2 < ba)) {
+            bv = q2;
+            ba = a2;
+        }
+    }
+    const int astar = ba;
+    const float k = (1.0f - dn[i]) * g;
+    const float r = rew[i];
+    const float *prow = tdist + ((size_t)i * A + astar) * Z;
+    bool mono = true;
+    for (int z = lane; z < Z; z += 64) {
+        float tz = r + k * support[z];
+        tz = fminf(fmaxf(tz, vmin), vmax);  // clamp(min=vmin, max=vmax)
+        const float b = (tz - vmin) / dz;
+        int L = (int)floorf(b), U = (int)ceilf(b);
+        if (U > 0 && U == L) L -= 1;
+        if (Z - 1 > L && U == L) U += 1;
+        L = L < 0 ? 0 : (L > Z - 1 ? Z - 1 : L);  // guard (never taken for valid inputs)
+        U = U < 0 ? 0 : (U > Z - 1 ? Z - 1 : U);
+        const float p = prow[z];
+        sL[w][z] = L;
+        sU[w][z] = U;
+        sml[w][z] = p * ((float)U - b);
+        smu[w][z] = p * (b - (float)L);
+    }
+    __syncthreads();
+    for (int z = lane; z + 1 < Z; z += 64)
+        if (sL[w][z + 1] < sL[w][z] || sU[w][z + 1] < sU[w][z]) mono = false;
+    mono = __all(mono);
+    const float *lrow = logp + ((size_t)i * A + act[i]) * Z;
+    float part = 0.0f;
+    for (int bin = lane; bin < Z; bin += 64) {
+        float acc = 0.0f;
+        if (mono) {
+            int z0 = lower_bound_i(sL[w], Z, bin), z1 = lower_bound_i(sL[w], Z, bin + 1);
+            for (int z = z0; z < z1; ++z) acc += sml[w][z];
+            z0 = lower_bound_i(sU[w], Z, bin);
+            z1 = lower_bound_i(sU[w], Z, bin + 1);
+            for (int z = z0; z < z1; ++z) acc += smu[w][z];
+        } else {
+            for (int z = 0; z < Z; ++z)
+                if (sL[w][z] == bin) acc += sml[w][z];
+            for (int z = 0; z < Z; ++z)
+                if (sU[w][z] == bin) acc += smu[w][z];
+        }
+        if (proj && live) proj[(size_t)i * Z + bin] = acc;
+        part += acc * lrow[bin];
+    }
+    part = wave_sum(part);
+    if (lane == 0 && live) loss[i] = -part;
+}
+
+}  // namespace agx
+
+using namespace agx;
+
+extern "C" int agx_td_target(const float *q_next_online, const float *q_next_target,
+                             const float *q_cur, const int64_t *actions, const float *rewards,
+                             const float *dones, int64_t B, int64_t A, double gamma, int double_q,
+                             float *y, float *g_q, float *loss, void *stream) {
+    AGX_REQUIRE(q_next_target && rewards && dones && y && B >= 0 && A > 0 && A < 65536,
+                "agx_td_target: bad arguments");
+    AGX_REQUIRE(!double_q || q_next_online, "agx_td_target: double_q needs q_next_online");
+    AGX_REQUIRE(!(g_q || loss) || (q_cur && actions), "agx_td_target: loss needs q_cur/actions");
+    if (B == 0) return AGX_OK;
+    hipStream_t s = as_stream(stream);
+    td_target_kernel<<<(unsigned)ceil_div(B, 256), 256, 0, s>>>(
+        q_next_online, q_next_target, q_cur, actions, rewards, dones, B, (int)A, (float)gamma,
+        double_q, y, g_q);
+    int rc = check_launch("agx_td_target");
+    if (rc || !loss) return rc;
+    td_loss_kernel<<<1, 1024, 0, s>>>(q_cur, actions, y, B, (int)A, loss);
+    return check_launch("agx_td_target loss");
+}
+
+extern "C" int agx_c51_project_loss(const float *q_next_online, const float *target_dist,
+                                    const float *logp_cur, const int64_t *actions,
+                                    const float *rewards, const float *dones, const float *support,
+                                    int64_t B, int64_t A, int64_t Z, double v_min, double v_max,
+                                    double gamma, float *loss, float *proj, void *stream) {
+    AGX_REQUIRE(q_next_online && target_dist && logp_cur && actions && rewards && dones && support &&
+                    loss,
+                "agx_c51_project_loss: null pointer");
+    AGX_REQUIRE(B >= 0 && A > 0 && Z >= 2 && Z <= kC51MaxZ, "agx_c51_project_loss: need 2 <= Z <= %d",
+                kC51MaxZ);
+    if (B == 0) return AGX_OK;
+    const float dz = (float)((v_max - v_min) / (double)(Z - 1));  // python float -> f32 operand
+    c51_kernel<<<(unsigned)ceil_div(B, kC51Waves), kC51Waves * 64, 0, as_stream(stream)>>>(
+        q_next_online, target_dist, logp_cur, actions, rewards, dones, support, B, (int)A, (int)Z,
+        (float)v_min, (float)v_max, dz, (float)gamma, loss, proj);
+    return check_launch("agx_c51_project_loss");
+}

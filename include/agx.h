@@ -1,0 +1,162 @@
+/*
+ * agx.h — C ABI of libagx.so, the MI355X (gfx950) hot path of a
+ * population-based RL trainer (drop-in for the mcx/AgileRL hot path).
+ *
+ * Conventions (every entry point):
+ *   - all array pointers are DEVICE pointers owned by the caller
+ *     (e.g. torch.Tensor.data_ptr()); layouts are dense, row-major;
+ *   - `stream` is a hipStream_t passed as void*; every call is asynchronous
+ *     on it, does no allocation, no host<->device copy and no synchronisation
+ *     (graph-capturable);
+ *   - scratch, where needed, is caller-provided; *_workspace_bytes() sizes it;
+ *   - return 0 (AGX_OK) or a negative status; agx_last_error() returns a
+ *     thread-local message for the last failing call on this thread;
+ *   - no C++ exception crosses the ABI; calls on distinct streams are
+ *     independent and thread-safe.
+ *
+ * Each entry point cites the reference (mcx/AgileRL 2.7.0) interface it
+ * replaces; paths are relative to the reference checkout.
+ */
+#ifndef AGX_H
+#define AGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AGX_OK 0
+#define AGX_EINVAL (-1)       /* bad shape / pointer / argument             */
+#define AGX_EHIP (-2)         /* HIP runtime error (launch or device fault) */
+#define AGX_EUNSUPPORTED (-3) /* configuration not implemented             */
+
+/* ---- library ------------------------------------------------------------ */
+const char *agx_last_error(void);
+int agx_version(void); /* major*10000 + minor*100 + patch */
+/* Device properties of the current device (CU count, HBM peak guess);
+ * fills out[0]=multiProcessorCount, out[1]=gcnArch (950), out[2]=warpSize. */
+int agx_device_info(int *out3);
+
+/* ---- GAE / Monte-Carlo returns -------------------------------------------
+ * Replaces RolloutBuffer.compute_returns_and_advantages
+ * (agilerl/components/rollout_buffer.py:413-481), batched over a population.
+ * Layout: P agents x (T, N) time-major SoA, i.e. x[p][t][n].
+ * rewards/values f32, dones u8 (the reference's torch.bool), last_value
+ * f32 [P][N], last_done u8 [P][N].  Outputs advantages/returns f32 [P][T][N],
+ * bit-exact to the reference (f64 carry, the NumPy-2 dtype flow).
+ * If adv_stats != NULL, also writes per-agent [mean, unbiased std] (f64) of
+ * the advantages, as used by PPO's normalisation (agilerl/algorithms/
+ * ppo.py:829-834); this needs `workspace` of agx_gae_workspace_bytes(). */
+size_t agx_gae_workspace_bytes(int64_t P, int64_t T, int64_t N);
+int agx_gae(const float *rewards, const uint8_t *dones, const float *values,
+            const float *last_value, const uint8_t *last_done, int64_t P, int64_t T,
+            int64_t N, double gamma, double gae_lambda, int use_gae, float *advantages,
+            float *returns, double *adv_stats, void *workspace, void *stream);
+
+/* In-place (a - mean) / (std + 1e-8) per agent (ppo.py:829-834);
+ * adv_stats as written by agx_gae.  adv is [P][count]. */
+int agx_adv_normalize(float *adv, const double *adv_stats, int64_t P, int64_t count, void *stream);
+
+/* ---- PPO clipped-surrogate loss, forward + backward ----------------------
+ * Replaces the loss block of PPO._learn_from_rollout_buffer_flat
+ * (agilerl/algorithms/ppo.py:868-902) and its autograd backward.
+ * num_minibatches contiguous minibatches of `batch` samples.  logp / value /
+ * entropy are the network outputs in minibatch order; old_logp / adv / ret /
+ * old_value are read at index[j] when index != NULL (the shuffled minibatch
+ * gather of ppo.py:842-848), else at j.
+ * Writes d loss / d{logp, value, entropy} per sample and, per minibatch,
+ * stats[m*8 + {0:loss, 1:policy_loss, 2:value_loss, 3:entropy_loss,
+ *              4:approx_kl, 5:clip_fraction}]. */
+int agx_ppo_loss_fwd_bwd(const float *logp, const float *old_logp, const float *adv,
+                         const float *ret, const float *old_value, const float *value,
+                         const float *entropy, const int64_t *index, int64_t batch,
+                         int64_t num_minibatches, float clip_coef, float vf_coef,
+                         float ent_coef, float *g_logp, float *g_value, float *g_entropy,
+                         float *stats, void *stream);
+
+/* ---- prioritized replay segment trees -----------------------------------
+ * Replaces SumSegmentTree / MinSegmentTree (agilerl/components/
+ * segment_tree.py) and the priority half of PrioritizedReplayBuffer
+ * (agilerl/components/replay_buffer.py:261-428).
+ * Trees are 1-indexed heaps of 2*capacity doubles (node k has children 2k,
+ * 2k+1; leaf i at capacity+i), capacity a power of two >= max_size.
+ * max_priority is a device f64 scalar (initialise to 1.0).
+ * Leaves hold priority**alpha computed with a correctly rounded pow; the
+ * tree is a pure function of the leaves, so batched updates are identical
+ * to the reference's sequential path walks. */
+size_t agx_per_workspace_bytes(int64_t capacity, int64_t max_batch);
+int agx_per_init(double *sum_tree, double *min_tree, int64_t capacity, void *stream);
+/* PrioritizedReplayBuffer.add (replay_buffer.py:296-309): n leaves at ring
+ * positions (start + i) % max_size get max_priority**alpha. */
+int agx_per_add(double *sum_tree, double *min_tree, int64_t capacity, int64_t max_size,
+                int64_t start, int64_t n, double alpha, const double *max_priority,
+                void *workspace, void *stream);
+/* PrioritizedReplayBuffer.update_priorities (replay_buffer.py:411-428):
+ * in order, p = max(priority, floor), leaf = p**alpha (last duplicate wins),
+ * max_priority = max(max_priority, p).  Indices must be in [0, max_size). */
+int agx_per_update(double *sum_tree, double *min_tree, int64_t capacity, int64_t max_size,
+                   const int64_t *indices, const float *priorities, int64_t n, double alpha,
+                   double floor, double *max_priority, void *workspace, void *stream);
+/* _sample_proportional (replay_buffer.py:357-381) + SumSegmentTree.retrieve
+ * (segment_tree.py:136-156): uniforms are the caller's torch.rand(B) stream.
+ * If weights != NULL also _calculate_weights (replay_buffer.py:383-409) with
+ * the buffer's current `size`.  err (device int32, may be NULL) gets the count
+ * of samples whose upper bound failed the reference's assert. */
+int agx_per_sample(const double *sum_tree, const double *min_tree, int64_t capacity,
+                   const float *uniforms, int64_t B, int64_t size, double beta,
+                   int64_t *indices, float *weights, int32_t *err, void *stream);
+/* SegmentTree.__getitem__ / reductions helper: copies tree[k] for given
+ * nodes (used for sum()/min() and leaf reads without a host round trip). */
+int agx_per_gather(const double *tree, const int64_t *nodes, int64_t n, double *out, void *stream);
+
+/* ---- DQN TD target -------------------------------------------------------
+ * Replaces DQN.update's target + loss (agilerl/algorithms/dqn.py:296-314):
+ * y = r + gamma*q_t*(1-d), q_t = max_a Qtgt(s') or Qtgt(s')[argmax Q(s')]
+ * (double_q); loss = mean((Q(s)[a] - y)^2); g_q = d loss / d Q(s) (B,A). */
+int agx_td_target(const float *q_next_online, const float *q_next_target, const float *q_cur,
+                  const int64_t *actions, const float *rewards, const float *dones, int64_t B,
+                  int64_t A, double gamma, int double_q, float *y, float *g_q, float *loss,
+                  void *stream);
+
+/* ---- Rainbow C51 projection + cross entropy ------------------------------
+ * Replaces RainbowDQN._dqn_loss (agilerl/algorithms/dqn_rainbow.py:313-367).
+ * q_next_online (B,A) picks a*; target_dist (B,A,Z) are the clamped target
+ * probabilities; logp_cur (B,A,Z) the online log-softmax on s; support (Z).
+ * Writes the elementwise loss (B) and, if proj != NULL, the projected
+ * distribution (B,Z) bit-exact to the serial index_add_. */
+int agx_c51_project_loss(const float *q_next_online, const float *target_dist,
+                         const float *logp_cur, const int64_t *actions, const float *rewards,
+                         const float *dones, const float *support, int64_t B, int64_t A,
+                         int64_t Z, double v_min, double v_max, double gamma, float *loss,
+                         float *proj, void *stream);
+
+/* ---- optimiser -----------------------------------------------------------
+ * Fused per-agent gradient-norm clip + Adam over a population's flat
+ * parameter buffers (replaces clip_grad_norm_ ppo.py:910-911 /
+ * dqn_rainbow.py:479 and torch.optim.Adam via OptimizerWrapper.step,
+ * agilerl/algorithms/core/optimizer_wrapper.py:444-452).
+ * params/grads/exp_avg/exp_avg_sq: [P][n]; the n parameters are split into
+ * G clip groups by group_offsets[0..G] (host array, G <= 8); with
+ * max_norm <= 0 nothing is clipped.  lr: device f32 [P] (per-agent learning
+ * rates, mutable by HPO without recompiling a graph); step is the 1-based
+ * Adam step count shared by the population. */
+size_t agx_adam_workspace_bytes(int64_t P, int64_t n);
+int agx_clip_adam(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t P,
+                  int64_t n, const int64_t *group_offsets, int G, float max_norm,
+                  const float *lr, float beta1, float beta2, float eps, int64_t step,
+                  void *workspace, void *stream);
+/* Polyak soft update target <- tau*online + (1-tau)*target
+ * (dqn.py:349-358, dqn_rainbow.py:492-501). */
+int agx_polyak(float *target, const float *online, int64_t n, float tau, void *stream);
+
+/* ---- diagnostics ---------------------------------------------------------
+ * out[i] = correctly rounded pow(x[i], y[i]) (the routine the PER leaves and
+ * IS weights use); for parity tests against libm / high-precision values. */
+int agx_debug_pow(const double *x, const double *y, double *out, int64_t n, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AGX_H */

@@ -1,0 +1,312 @@
+"""Parity of the HIP kernels (through the C ABI) against the CPU oracle and
+the reference's golden vectors.  Needs an MI355X."""
+
+from decimal import Decimal, getcontext
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import cref  # noqa: E402
+from oracle import dqn as odqn  # noqa: E402
+from oracle import gae as ogae  # noqa: E402
+from oracle import per as oper  # noqa: E402
+from oracle import ppo_loss as oppo  # noqa: E402
+
+DEV = torch.device("cuda:0")
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def K():
+    from agilerl_amd import kernels
+
+    return kernels
+
+
+# --------------------------------------------------------------------------- #
+# GAE — bit-exact                                                             #
+# --------------------------------------------------------------------------- #
+@pytest.mark.parametrize("case", [f"gae{i}" for i in range(8)])
+def test_gae_golden_bit_exact(golden, case):
+    g = golden(case)
+    adv, ret = K().gae(T(g["rewards"]), T(g["dones"]), T(g["values"]), T(g["last_value"]),
+                       T(g["last_done"]), float(g["gamma"]), float(g["lam"]), bool(g["use_gae"]))
+    assert np.array_equal(adv.cpu().numpy().view(np.uint32), g["advantages"].view(np.uint32))
+    assert np.array_equal(ret.cpu().numpy().view(np.uint32), g["returns"].view(np.uint32))
+
+
+@pytest.mark.parametrize("P,Tn,N,pd,use_gae", [(8, 16, 128, 0.01, True), (3, 257, 1000, 0.02, True),
+                                               (2, 33, 4099, 0.3, False), (5, 1, 64, 0.5, True),
+                                               (1, 9, 1, 0.5, True)])
+def test_gae_population_bit_exact_vs_c_oracle(P, Tn, N, pd, use_gae):
+    rng = np.random.default_rng(P * 1000 + Tn)
+    r = rng.standard_normal((P, Tn, N)).astype(np.float32)
+    v = rng.standard_normal((P, Tn, N)).astype(np.float32)
+    d = (rng.random((P, Tn, N)) < pd).astype(np.uint8)
+    lv = rng.standard_normal((P, N)).astype(np.float32)
+    ld = (rng.random((P, N)) < pd).astype(np.uint8)
+    adv, ret, stats = K().gae(T(r), T(d), T(v), T(lv), T(ld), 0.99, 0.95, use_gae, with_stats=True)
+    ea, er = cref.gae(r, v, d, lv, ld, 0.99, 0.95, use_gae, nthreads=8)
+    assert np.array_equal(adv.cpu().numpy(), ea)
+    assert np.array_equal(ret.cpu().numpy(), er)
+    st = stats.cpu().numpy()
+    for p in range(P):
+        m, s = ogae.adv_stats(ea[p])
+        assert abs(st[p, 0] - m) <= 1e-12 * max(1, abs(m)) + 1e-12
+        if Tn * N > 1:
+            assert abs(st[p, 1] - s) <= 1e-9 * s
+
+
+def test_gae_bool_dones_and_normalize():
+    rng = np.random.default_rng(7)
+    r = rng.standard_normal((2, 40, 300)).astype(np.float32)
+    v = rng.standard_normal((2, 40, 300)).astype(np.float32)
+    d = rng.random((2, 40, 300)) < 0.05
+    lv = rng.standard_normal((2, 300)).astype(np.float32)
+    ld = rng.random((2, 300)) < 0.05
+    adv, ret, stats = K().gae(T(r), T(d), T(v), T(lv), T(ld), with_stats=True)
+    ea, _ = cref.gae(r, v, d, lv, ld, 0.99, 0.95)
+    assert np.array_equal(adv.cpu().numpy(), ea)
+    K().adv_normalize_(adv, stats)
+    for p in range(2):
+        np.testing.assert_allclose(adv[p].cpu().numpy(), ogae.normalize_advantages(ea[p]), rtol=1e-5,
+                                   atol=1e-6)
+
+
+# --------------------------------------------------------------------------- #
+# PPO loss                                                                    #
+# --------------------------------------------------------------------------- #
+def _loss_inputs(S, seed):
+    rng = np.random.default_rng(seed)
+    old = rng.uniform(-3, -0.05, S).astype(np.float32)
+    lp = (old + rng.normal(0, 0.2, S)).astype(np.float32)
+    A, R, ov = (rng.standard_normal(S).astype(np.float32) for _ in range(3))
+    v = (ov + rng.normal(0, 0.3, S)).astype(np.float32)
+    H = rng.uniform(0, 1.3, S).astype(np.float32)
+    return lp, old, A, R, ov, v, H
+
+
+@pytest.mark.parametrize("b,nmb", [(128, 16), (64, 5), (256, 3), (1000, 2), (130, 4), (7, 9)])
+def test_ppo_loss_vs_oracle(b, nmb):
+    lp, old, A, R, ov, v, H = _loss_inputs(b * nmb, b)
+    g1, g2, g3, st = K().ppo_loss_fwd_bwd(*(T(x) for x in (lp, old, A, R, ov, v, H)), b, 0.2, 0.5, 0.01)
+    g1, g2, g3, st = (x.cpu().numpy() for x in (g1, g2, g3, st))
+    for m in range(nmb):
+        s = slice(m * b, (m + 1) * b)
+        loss, parts, e1, e2, e3 = oppo.minibatch_loss(lp[s], old[s], A[s], R[s], ov[s], v[s], H[s],
+                                                       0.2, 0.5, 0.01)
+        tol = 1e-5 * max(1.0, abs(loss))
+        assert abs(st[m, 0] - loss) <= tol
+        assert abs(st[m, 1] - parts["pg"]) <= 1e-5 * max(1, abs(parts["pg"]))
+        assert abs(st[m, 2] - parts["vl"]) <= 1e-5 * max(1, abs(parts["vl"]))
+        assert abs(st[m, 4] - parts["kl"]) <= 1e-6
+        assert abs(st[m, 5] - parts["clipfrac"]) <= 1e-6
+        np.testing.assert_allclose(g1[s], e1, rtol=1e-5, atol=1e-8)
+        np.testing.assert_allclose(g2[s], e2, rtol=1e-5, atol=1e-8)
+        np.testing.assert_allclose(g3[s], e3, rtol=1e-6)
+
+
+def test_ppo_loss_golden_with_index_gather(golden):
+    """The reference's own schedule: normalised advantages, numpy permutation,
+    per-minibatch gradients (ppo0: 2048 samples, b=128, 4 epochs)."""
+    g = golden("ppo0")
+    S, b = int(g["S"]), int(g["batch"])
+    k = K()
+    an = T(g["adv_norm"])
+    old, R, ov = T(g["old_logp"]), T(g["ret"]), T(g["old_v"])
+    nl, nv, H = g["new_logp"], g["new_v"], g["H"]
+    snap = 0
+    for perm in g["perms"]:
+        for s0 in range(0, S, b):
+            mb = perm[s0:s0 + b]
+            g1, g2, g3, st = k.ppo_loss_fwd_bwd(T(nl[mb]), old, an, R, ov, T(nv[mb]), T(H[mb]), len(mb),
+                                                float(g["clip"]), float(g["vf"]), float(g["ent"]),
+                                                index=T(mb.astype(np.int64)))
+            np.testing.assert_allclose(g1.cpu().numpy(), g["g_logp"][snap][mb], rtol=1e-4, atol=1e-8)
+            np.testing.assert_allclose(g2.cpu().numpy(), g["g_v"][snap][mb], rtol=1e-4, atol=1e-8)
+            np.testing.assert_allclose(g3.cpu().numpy(), g["g_H"][snap][mb], rtol=1e-5)
+            snap += 1
+    assert snap == int(g["n_minibatches"])
+
+
+# --------------------------------------------------------------------------- #
+# PER                                                                         #
+# --------------------------------------------------------------------------- #
+def _trees(cap):
+    st = torch.empty(2 * cap, dtype=torch.float64, device=DEV)
+    mt = torch.empty(2 * cap, dtype=torch.float64, device=DEV)
+    K().per_init(st, mt, cap)
+    return st, mt
+
+
+def _assert_tree_close(dev_tree, ref_tree):
+    a = dev_tree.cpu().numpy()[1:]
+    b = np.asarray(ref_tree)[1:]
+    fin = np.isfinite(b)
+    assert np.array_equal(np.isfinite(a), fin)
+    rel = np.abs(a[fin] - b[fin]) / np.maximum(np.abs(b[fin]), 1e-300)
+    assert rel.max() <= 4e-16 * 64, rel.max()  # <= 1 ulp leaves, sums stay within rounding
+    return float((a[fin] == b[fin]).mean())
+
+
+@pytest.mark.parametrize("case", [f"per{i}" for i in range(4)])
+def test_per_golden_indices_bit_exact(golden, case):
+    g = golden(case)
+    ms, alpha, beta, B = int(g["max_size"]), float(g["alpha"]), float(g["beta"]), int(g["B"])
+    cap = oper.tree_capacity(ms)
+    st, mt = _trees(cap)
+    mp = torch.ones(1, dtype=torch.float64, device=DEV)
+    k = K()
+    k.per_add(st, mt, cap, ms, 0, int(g["n_add"]), alpha, mp)
+    ptr = int(g["n_add"]) % ms
+    size = min(int(g["n_add"]), ms)
+    for rd in range(int(g["rounds"])):
+        idx, w = k.per_sample(st, mt, cap, T(g[f"u{rd}"]), size=size, beta=beta)
+        assert np.array_equal(idx.cpu().numpy(), g[f"idx{rd}"])
+        np.testing.assert_allclose(w.cpu().numpy(), g[f"w{rd}"], rtol=2e-7)
+        k.per_update(st, mt, cap, ms, idx, T(g[f"pri{rd}"]), alpha, mp)
+        n = int(g[f"extra{rd}"])
+        k.per_add(st, mt, cap, ms, ptr, n, alpha, mp)
+        ptr = (ptr + n) % ms
+        size = min(size + n, ms)
+        frac = _assert_tree_close(st, g[f"sum_tree{rd}"])
+        _assert_tree_close(mt, g[f"min_tree{rd}"])
+        assert frac > 0.95
+        assert mp.item() == float(g[f"max_priority{rd}"])
+
+
+def test_per_large_batches_vs_c_oracle():
+    """Multi-launch path (batches > 1024) incl. duplicates, cap 2^17."""
+    rng = np.random.default_rng(5)
+    ms, alpha, beta = 100_000, 0.6, 0.4
+    cap = oper.tree_capacity(ms)
+    c = cref.PERTree(ms, alpha)
+    st, mt = _trees(cap)
+    mp = torch.ones(1, dtype=torch.float64, device=DEV)
+    k = K()
+    c.add(ms)
+    k.per_add(st, mt, cap, ms, 0, ms, alpha, mp)
+    for rd in range(3):
+        idx = rng.integers(0, ms, 20_000)
+        pri = (np.abs(rng.standard_normal(20_000)) * (3 if rd == 1 else 1)).astype(np.float32)
+        pri[:50] = 1e-9
+        c.update(idx, pri)
+        k.per_update(st, mt, cap, ms, T(idx.astype(np.int64)), T(pri), alpha, mp)
+        assert mp.item() == c.max_priority
+        _assert_tree_close(st, c.sum)
+        _assert_tree_close(mt, c.min)
+        u = torch.rand(50_000, generator=torch.Generator().manual_seed(rd)).numpy()
+        eidx, bad = c.sample(u)
+        gidx, w = k.per_sample(st, mt, cap, T(u), size=ms, beta=beta)
+        assert bad == 0
+        assert np.array_equal(gidx.cpu().numpy(), eidx)
+        np.testing.assert_allclose(w.cpu().numpy(), c.weights(eidx, beta), rtol=2e-7)
+
+
+def test_per_ring_add_wraps():
+    ms, cap = 1000, 1024
+    st, mt = _trees(cap)
+    mp = torch.full((1,), 2.5, dtype=torch.float64, device=DEV)
+    K().per_add(st, mt, cap, ms, 990, 1500, 0.6, mp)  # longer than the ring
+    ref = oper.PER(ms, 0.6)
+    ref.max_priority, ref.tree_ptr = 2.5, 990
+    ref.add(1500)
+    _assert_tree_close(st, ref.sum_tree.tree)
+
+
+def test_correctly_rounded_pow():
+    getcontext().prec = 50
+    rng = np.random.default_rng(3)
+    x = np.abs(rng.standard_normal(3000)).astype(np.float32).astype(np.float64) + 1e-5
+    y = np.where(np.arange(3000) % 2 == 0, 0.6, -0.4)
+    got = K().debug_pow(T(x), T(y)).cpu().numpy()
+    cr = np.array([float((Decimal(float(b)) * Decimal(float(a)).ln()).exp()) for a, b in zip(x, y)])
+    assert np.array_equal(got, cr)
+    libm = x ** y
+    assert (libm != cr).mean() < 0.01  # libm itself is not correctly rounded
+
+
+# --------------------------------------------------------------------------- #
+# DQN TD target / Rainbow C51                                                 #
+# --------------------------------------------------------------------------- #
+@pytest.mark.parametrize("case", ["dqn0", "dqn1", "dqn2"])
+def test_td_target_golden(golden, case):
+    g = golden(case)
+    y, gq, loss = K().td_target(T(g["q_next_target"]), T(g["r"]), T(g["d"]), float(g["gamma"]),
+                                T(g["q_next_online"]), bool(g["double"]), T(g["q_cur"]), T(g["a"]))
+    assert np.array_equal(y.cpu().numpy(), g["y"])
+    np.testing.assert_allclose(gq.cpu().numpy(), g["g_q"], rtol=1e-5, atol=1e-9)
+    assert abs(loss.item() - float(g["loss"])) <= 1e-5 * abs(float(g["loss"]))
+
+
+@pytest.mark.parametrize("case", [f"c51_{i}" for i in range(4)])
+def test_c51_golden(golden, case):
+    g = golden(case)
+    loss, proj = K().c51_project_loss(T(g["q_next"]), T(g["target_dist"]), T(g["logp_cur"]), T(g["a"]),
+                                      T(g["r"]), T(g["d"]), T(g["support"]), float(g["vmin"]),
+                                      float(g["vmax"]), float(g["gamma"]), with_proj=True)
+    _, eproj = odqn.c51_project(g["q_next"], g["target_dist"], g["r"], g["d"], g["support"],
+                                float(g["vmin"]), float(g["vmax"]), float(g["gamma"]))
+    assert np.array_equal(proj.cpu().numpy(), eproj)
+    np.testing.assert_allclose(loss.cpu().numpy(), g["loss"], rtol=1e-5, atol=1e-6)
+
+
+def test_c51_large_vs_c_oracle():
+    rng = np.random.default_rng(9)
+    B, A, Z = 5000, 6, 51
+    support = torch.linspace(-200, 200, Z).numpy()
+    q = rng.standard_normal((B, A)).astype(np.float32)
+    q[:10] = 0.0  # argmax ties -> first index
+    td = torch.softmax(torch.randn(B, A, Z), -1).clamp(min=1e-3).numpy()
+    lp = torch.log_softmax(torch.randn(B, A, Z), -1).numpy()
+    a = rng.integers(0, A, B).astype(np.int64)
+    r = (rng.standard_normal(B) * 120).astype(np.float32)
+    d = (rng.random(B) < 0.1).astype(np.float32)
+    loss, proj = K().c51_project_loss(T(q), T(td), T(lp), T(a), T(r), T(d), T(support), -200, 200,
+                                      0.99 ** 4, with_proj=True)
+    eloss, eproj = cref.c51(q, td, lp, a, r, d, support, -200.0, 200.0, 0.99 ** 4)
+    assert np.array_equal(proj.cpu().numpy(), eproj)
+    np.testing.assert_allclose(loss.cpu().numpy(), eloss, rtol=1e-5, atol=1e-5)
+
+
+# --------------------------------------------------------------------------- #
+# optimiser                                                                   #
+# --------------------------------------------------------------------------- #
+def test_clip_adam_matches_torch():
+    torch.manual_seed(0)
+    P, n, split = 3, 5000, 3100
+    p0 = torch.randn(P, n)
+    grads = [torch.randn(P, n) * (5.0 if s == 0 else 0.01) for s in range(4)]
+    lr = [1e-3, 5e-4, 2e-3]
+    ref = [torch.nn.Parameter(p0[i, :split].clone()) for i in range(P)]
+    ref2 = [torch.nn.Parameter(p0[i, split:].clone()) for i in range(P)]
+    opts = [torch.optim.Adam([ref[i], ref2[i]], lr=lr[i]) for i in range(P)]
+    params = p0.clone().to(DEV)
+    opt = K().ClipAdam(params, [0, split, n], lr, max_norm=0.5)
+    for g in grads:
+        for i in range(P):
+            ref[i].grad = g[i, :split].clone()
+            ref2[i].grad = g[i, split:].clone()
+            torch.nn.utils.clip_grad_norm_([ref[i]], 0.5)
+            torch.nn.utils.clip_grad_norm_([ref2[i]], 0.5)
+            opts[i].step()
+        opt.grads.copy_(g)
+        opt.step()
+    got = params.cpu()
+    for i in range(P):
+        np.testing.assert_allclose(got[i, :split].numpy(), ref[i].detach().numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(got[i, split:].numpy(), ref2[i].detach().numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_polyak():
+    t = torch.randn(10_001)
+    o = torch.randn(10_001)
+    exp = 1e-3 * o + (1.0 - 1e-3) * t
+    td = t.to(DEV)
+    K().polyak_(td, o.to(DEV), 1e-3)
+    assert torch.equal(td.cpu(), exp)
