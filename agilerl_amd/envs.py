@@ -1,0 +1,83 @@
+"""Host-side synthetic vectorised environments (gymnasium-style API).
+
+``SyntheticVecEnv`` is a LunarLander-v2-shaped stand-in (obs 8 f32, 4
+discrete actions, reward ~ N(0,1), termination ~ Bernoulli(1/200)) whose step
+costs ~nothing, so benchmarks measure the framework, not box2d (SURVEY §8d;
+gymnasium/box2d are not installed on this image).  It returns the
+gymnasium 5-tuple ``(obs, reward, terminated, truncated, info)``.
+
+Observations/rewards/dones are written straight into caller-provided
+(pinned) host buffers when given, so the H2D copy into the HBM rollout SoA is
+a single async hipMemcpy per field per step.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+
+class Discrete:
+    def __init__(self, n: int):
+        self.n = int(n)
+        self.shape = ()
+        self.dtype = np.int64
+
+    def sample(self):
+        return np.random.randint(self.n)
+
+
+class Box:
+    def __init__(self, low, high, shape, dtype=np.float32):
+        self.shape = tuple(shape)
+        self.dtype = dtype
+        self.low = np.full(self.shape, low, dtype=dtype)
+        self.high = np.full(self.shape, high, dtype=dtype)
+
+    def sample(self):
+        return np.random.uniform(self.low, self.high).astype(self.dtype)
+
+
+class SyntheticVecEnv:
+    """``num_envs`` independent synthetic episodes; data drawn from a ring of
+    pre-generated batches (``ring`` steps) so a step is a memcpy."""
+
+    def __init__(self, num_envs: int, obs_dim: int = 8, n_actions: int = 4, p_done: float = 1 / 200,
+                 seed: int = 0, ring: int = 97):
+        self.num_envs = int(num_envs)
+        self.single_observation_space = Box(-np.inf, np.inf, (obs_dim,))
+        self.single_action_space = Discrete(n_actions)
+        self.observation_space = self.single_observation_space
+        self.action_space = self.single_action_space
+        rng = np.random.default_rng(seed)
+        self._obs = rng.standard_normal((ring, num_envs, obs_dim), dtype=np.float32)
+        self._rew = rng.standard_normal((ring, num_envs), dtype=np.float32)
+        self._term = rng.random((ring, num_envs)) < p_done
+        self._trunc = np.zeros(num_envs, dtype=bool)
+        self._k = 0
+        self._ring = ring
+        self.steps = 0
+
+    def reset(self, seed=None, options=None, out_obs: np.ndarray | None = None):
+        self._k = 0
+        obs = self._obs[0]
+        if out_obs is not None:
+            np.copyto(out_obs.reshape(obs.shape), obs)
+            obs = out_obs
+        return obs, {}
+
+    def step(self, actions, out_obs=None, out_rew=None, out_done=None):
+        self._k = (self._k + 1) % self._ring
+        self.steps += self.num_envs
+        obs, rew, term = self._obs[self._k], self._rew[self._k], self._term[self._k]
+        if out_obs is not None:
+            np.copyto(out_obs.reshape(obs.shape), obs)
+            obs = out_obs
+        if out_rew is not None:
+            np.copyto(out_rew.reshape(rew.shape), rew)
+            rew = out_rew
+        if out_done is not None:
+            np.copyto(out_done.reshape(term.shape), term)
+        return obs, rew, term, self._trunc, {}
+
+    def close(self):
+        pass

@@ -35,7 +35,7 @@ def _ws(nbytes: int, device) -> torch.Tensor:
 # GAE                                                                         #
 # --------------------------------------------------------------------------- #
 def gae(rewards, dones, values, last_value, last_done, gamma=0.99, gae_lambda=0.95, use_gae=True,
-        advantages=None, returns=None, with_stats=False, workspace=None):
+        advantages=None, returns=None, with_stats=False, workspace=None, stats_out=None):
     """rewards/values f32 [P,T,N] (or [T,N]), dones u8/bool, last_* [P,N].
     Returns (advantages, returns[, stats f64 [P,2] = mean, unbiased std])."""
     squeeze = rewards.dim() == 2
@@ -60,7 +60,8 @@ def gae(rewards, dones, values, last_value, last_done, gamma=0.99, gae_lambda=0.
     _need(ret, "returns", _f32)
     stats = None
     if with_stats:
-        stats = torch.empty(P, 2, dtype=_f64, device=r.device)
+        stats = torch.empty(P, 2, dtype=_f64, device=r.device) if stats_out is None else stats_out
+        _need(stats, "stats_out", _f64, (P, 2))
         if workspace is None:
             workspace = _ws(_lib.load().agx_gae_workspace_bytes(P, T, N), r.device)
     _lib.call("agx_gae", r.data_ptr(), d.data_ptr(), v.data_ptr(), lv.data_ptr(), ld.data_ptr(),
@@ -238,13 +239,14 @@ class ClipAdam:
     """Fused per-agent grad-norm clip + Adam over flat [P, n] buffers."""
 
     def __init__(self, params: torch.Tensor, group_offsets, lr, betas=(0.9, 0.999), eps=1e-8,
-                 max_norm=0.5):
+                 max_norm=0.5, grads: torch.Tensor | None = None):
         _need(params, "params", _f32)
         if params.dim() != 2:
             raise ValueError("params must be [P, n]")
         self.params = params
         P, n = params.shape
-        self.grads = torch.zeros_like(params)
+        self.grads = torch.zeros_like(params) if grads is None else grads
+        _need(self.grads, "grads", _f32, tuple(params.shape))
         self.exp_avg = torch.zeros_like(params)
         self.exp_avg_sq = torch.zeros_like(params)
         self.offsets = (torch.tensor(list(group_offsets), dtype=torch.int64)).contiguous()

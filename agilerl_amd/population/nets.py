@@ -1,0 +1,157 @@
+"""Population-stacked actor-critic MLPs over ONE flat parameter buffer [P, n].
+
+Architecture (what the reference builds for PPO with a shared MLP encoder,
+agilerl/utils/evolvable_networks.py:527-644 ``create_mlp`` via
+agilerl/networks/base.py:541-561, ``StochasticActor`` / ``ValueNetwork``):
+
+  encoder : [Linear -> LayerNorm(affine) -> act] per hidden size,
+            Linear(-> latent) -> LayerNorm(no affine) -> act    (output_layernorm, output_vanish off)
+  actor   : [Linear -> LayerNorm(affine) -> act] per hidden size, Linear(-> A)  (x0.1 init)
+  critic  : same on the actor's latent (share_encoders, ppo.py:487-491), Linear(-> 1)
+
+Every agent's parameters are one contiguous row of ``flat[P, n]`` laid out
+[encoder | actor head | critic head] in state-dict order (weight, bias,
+LN weight, LN bias per layer), so one kernel launch updates the whole
+population and the two clip groups of ppo.py:910-911 are the contiguous
+ranges [0, enc+actor) and [enc+actor, n).  Weights use the nn.Linear [out, in]
+layout.  Initialisation: orthogonal (gain sqrt 2), zero bias, output layers
+x0.1 (``layer_init`` / ``output_vanish``, evolvable_networks.py:410-441, 621-629).
+
+``forward`` is the plain-PyTorch fp32 path (batched over the population with
+bmm); it is the numerics reference for the fused HIP learner and the path
+for architectures the fused kernel does not cover.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn.functional as F
+
+
+@dataclass
+class Layer:
+    name: str
+    fin: int
+    fout: int
+    ln: str | None  # None | "affine" | "plain"
+    act: bool
+    w: int = 0
+    b: int = 0
+    g: int = -1
+    beta: int = -1
+    vanish: bool = False
+
+
+@dataclass
+class ActorCriticSpec:
+    obs_dim: int
+    n_actions: int
+    encoder_hidden: list[int] = field(default_factory=lambda: [64])
+    latent_dim: int = 64
+    actor_hidden: list[int] = field(default_factory=lambda: [64])
+    critic_hidden: list[int] = field(default_factory=lambda: [64])
+    layer_norm: bool = True
+
+    def __post_init__(self) -> None:
+        ln = "affine" if self.layer_norm else None
+        enc = [self.obs_dim, *self.encoder_hidden]
+        self.encoder = [Layer(f"encoder_linear_layer_{i}", enc[i - 1], enc[i], ln, True)
+                        for i in range(1, len(enc))]
+        self.encoder.append(Layer("encoder_linear_layer_output", enc[-1], self.latent_dim,
+                                  "plain" if self.layer_norm else None, True))
+        self.actor = self._head("actor", self.actor_hidden, self.n_actions, ln)
+        self.critic = self._head("critic", self.critic_hidden, 1, ln)
+        off = 0
+        for lay in self.encoder + self.actor + self.critic:
+            lay.w = off
+            off += lay.fin * lay.fout
+            lay.b = off
+            off += lay.fout
+            if lay.ln == "affine":
+                lay.g = off
+                off += lay.fout
+                lay.beta = off
+                off += lay.fout
+            if lay is self.actor[-1]:
+                self.actor_end = off
+        self.n_params = off
+        self.group_offsets = [0, self.actor_end, self.n_params]
+
+    def _head(self, name, hidden, nout, ln):
+        dims = [self.latent_dim, *hidden]
+        layers = [Layer(f"{name}_linear_layer_{i}", dims[i - 1], dims[i], ln, True)
+                  for i in range(1, len(dims))]
+        layers.append(Layer(f"{name}_linear_layer_output", dims[-1], nout, None, False, vanish=True))
+        return layers
+
+    @property
+    def layers(self) -> list[Layer]:
+        return self.encoder + self.actor + self.critic
+
+    # ------------------------------------------------------------------ #
+    def init_params(self, P: int, seeds: list[int] | None = None, device="cpu") -> torch.Tensor:
+        flat = torch.zeros(P, self.n_params, dtype=torch.float32)
+        for p in range(P):
+            gen = torch.Generator().manual_seed(int(seeds[p]) if seeds is not None else p)
+            for lay in self.layers:
+                w = torch.empty(lay.fout, lay.fin)
+                torch.nn.init.orthogonal_(w, math.sqrt(2), generator=gen)
+                if lay.vanish:
+                    w.mul_(0.1)
+                flat[p, lay.w: lay.w + w.numel()] = w.reshape(-1)
+                if lay.ln == "affine":
+                    flat[p, lay.g: lay.g + lay.fout] = 1.0
+        return flat.to(device)
+
+    def views(self, flat: torch.Tensor, lay: Layer):
+        P = flat.shape[0]
+        W = flat[:, lay.w: lay.w + lay.fin * lay.fout].view(P, lay.fout, lay.fin)
+        b = flat[:, lay.b: lay.b + lay.fout]
+        g = flat[:, lay.g: lay.g + lay.fout] if lay.ln == "affine" else None
+        be = flat[:, lay.beta: lay.beta + lay.fout] if lay.ln == "affine" else None
+        return W, b, g, be
+
+    def _run(self, flat, x, layers):
+        for lay in layers:
+            W, b, g, be = self.views(flat, lay)
+            x = torch.baddbmm(b.unsqueeze(1), x, W.transpose(1, 2))
+            if lay.ln is not None:
+                x = F.layer_norm(x, (lay.fout,), eps=1e-5)
+                if g is not None:
+                    x = x * g.unsqueeze(1) + be.unsqueeze(1)
+            if lay.act:
+                x = torch.relu(x)
+        return x
+
+    def forward(self, flat: torch.Tensor, obs: torch.Tensor):
+        """obs [P, B, obs_dim] -> (logits [P, B, A], value [P, B])."""
+        lat = self._run(flat, obs, self.encoder)
+        logits = self._run(flat, lat, self.actor)
+        value = self._run(flat, lat, self.critic).squeeze(-1)
+        return logits, value
+
+    def state_dict_keys(self) -> dict[str, tuple[int, tuple[int, ...]]]:
+        """Reference-compatible parameter names -> (offset, shape)."""
+        out = {}
+        for net, layers in (("actor.encoder.model", self.encoder), ("actor.head_net.model", self.actor),
+                            ("critic.head_net.model", self.critic)):
+            for lay in layers:
+                out[f"{net}.{lay.name}.weight"] = (lay.w, (lay.fout, lay.fin))
+                out[f"{net}.{lay.name}.bias"] = (lay.b, (lay.fout,))
+                if lay.ln == "affine":
+                    ln_name = lay.name.replace("linear_layer", "layer_norm")
+                    out[f"{net}.{ln_name}.weight"] = (lay.g, (lay.fout,))
+                    out[f"{net}.{ln_name}.bias"] = (lay.beta, (lay.fout,))
+        return out
+
+
+def categorical(logits: torch.Tensor):
+    """log-softmax and entropy as ``agilerl/utils/torch_utils.py:142-199``:
+    H = -sum p * log(p + 1e-8)."""
+    logp_all = torch.log_softmax(logits, dim=-1)
+    p = torch.softmax(logits, dim=-1)
+    ent = -(p * torch.log(p + 1e-8)).sum(-1)
+    return logp_all, ent

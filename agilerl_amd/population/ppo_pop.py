@@ -1,0 +1,192 @@
+"""A PPO population resident in HBM: stacked networks, SoA rollout storage,
+batched rollout inference and a batched learner.
+
+Reference behaviour mirrored per agent:
+  * rollout collection  agilerl/rollouts/on_policy.py:23-203 (done = term|trunc
+    of THIS step; bootstrap with last_done = term, :184-196)
+  * rollout storage     agilerl/components/rollout_buffer.py:137-411 (time-major
+    (T, N) SoA; here (P, T, N) on the GPU instead of CPU TensorDicts)
+  * GAE                 rollout_buffer.py:413-481 -> agx_gae (bit-exact)
+  * learner             agilerl/algorithms/ppo.py:814-921: global advantage
+    normalisation, E epochs of shuffled minibatches, clipped surrogate +
+    clipped value loss - entropy, per-group grad clip, Adam;
+    returns sum(loss)/(num_samples*epochs) (:920)
+
+The population axis replaces the reference's sequential agent loop
+(train_on_policy.py:210): every kernel processes all P agents at once.
+Sampling uses an on-device Gumbel-max draw (the reference's torch.multinomial
+stream cannot be reproduced on a GPU generator anyway).
+
+Two learner back ends share this state:
+  * ``fused=True``  one persistent HIP workgroup per agent runs all E x M
+                    minibatch updates (agx_ppo_learn, f32 MFMA GEMMs) —
+                    the production path;
+  * ``fused=False`` plain-PyTorch fp32 autograd over the stacked networks with
+                    the HIP loss / clip+Adam kernels — the numerics reference
+                    for the fused kernel and the path for architectures it does
+                    not cover.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import kernels as K
+from .nets import ActorCriticSpec, categorical
+
+
+class _PPOLossFn(torch.autograd.Function):
+    """Clipped surrogate loss for P minibatches at once (HIP fwd+bwd)."""
+
+    @staticmethod
+    def forward(ctx, logp, value, entropy, old_logp, adv, ret, old_v, gidx, b, clip, vf, ent):
+        g1, g2, g3, stats = K.ppo_loss_fwd_bwd(
+            logp.contiguous().view(-1), old_logp, adv, ret, old_v, value.contiguous().view(-1),
+            entropy.contiguous().view(-1), b, clip, vf, ent, index=gidx)
+        ctx.save_for_backward(g1, g2, g3)
+        ctx.shape = logp.shape
+        ctx.mark_non_differentiable(stats)
+        return stats[:, 0].sum(), stats
+
+    @staticmethod
+    def backward(ctx, gl, _gs):
+        g1, g2, g3 = ctx.saved_tensors
+        s = ctx.shape
+        return (g1.view(s) * gl, g2.view(s) * gl, g3.view(s) * gl) + (None,) * 9
+
+
+class PPOPopulation:
+    def __init__(self, spec: ActorCriticSpec, pop_size: int, num_envs: int, *, learn_step=2048,
+                 batch_size=128, lr=1e-3, gamma=0.99, gae_lambda=0.95, clip_coef=0.2, ent_coef=0.01,
+                 vf_coef=0.5, max_grad_norm=0.5, update_epochs=4, target_kl=None, seeds=None,
+                 device="cuda", fused=True):
+        self.spec = spec
+        self.P, self.N = int(pop_size), int(num_envs)
+        self.T = -(learn_step // -self.N)  # capacity = ceil(learn_step / num_envs), ppo.py:363
+        self.S = self.T * self.N
+        self.batch_size = int(batch_size)
+        self.gamma, self.gae_lambda = float(gamma), float(gae_lambda)
+        self.clip_coef, self.ent_coef, self.vf_coef = float(clip_coef), float(ent_coef), float(vf_coef)
+        self.max_grad_norm = float(max_grad_norm)
+        self.update_epochs = int(update_epochs)
+        self.target_kl = target_kl
+        self.device = torch.device(device)
+        seeds = list(range(self.P)) if seeds is None else list(seeds)
+        self.seeds = seeds
+        self.params = torch.nn.Parameter(spec.init_params(self.P, seeds, self.device))
+        self.params.grad = torch.zeros_like(self.params)
+        lr_list = [float(lr)] * self.P if not isinstance(lr, (list, tuple)) else [float(x) for x in lr]
+        self.opt = K.ClipAdam(self.params.data, spec.group_offsets, lr_list, max_norm=self.max_grad_norm,
+                              grads=self.params.grad)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(int(seeds[0]) * 7919 + 17)
+        self.fused = fused
+        self._alloc_rollout()
+        self.learn_steps = 0
+
+    # ------------------------------------------------------------------ #
+    def _alloc_rollout(self):
+        P, T, N, D, dev = self.P, self.T, self.N, self.spec.obs_dim, self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.obs = torch.zeros(P, T, N, D, **f32)
+        self.actions = torch.zeros(P, T, N, dtype=torch.int64, device=dev)
+        self.rewards = torch.zeros(P, T, N, **f32)
+        self.dones = torch.zeros(P, T, N, dtype=torch.uint8, device=dev)
+        self.values = torch.zeros(P, T, N, **f32)
+        self.log_probs = torch.zeros(P, T, N, **f32)
+        self.advantages = torch.zeros(P, T, N, **f32)
+        self.returns = torch.zeros(P, T, N, **f32)
+        self.adv_stats = torch.zeros(P, 2, dtype=torch.float64, device=dev)
+        self.gae_ws = torch.empty(max(16, K._lib.load().agx_gae_workspace_bytes(P, T, N)), dtype=torch.uint8,
+                                  device=dev)
+
+    # ------------------------------------------------------------------ #
+    @torch.no_grad()
+    def act(self, obs: torch.Tensor):
+        """obs [P, N, D] (device) -> action, log_prob, entropy, value, each [P, N]."""
+        logits, value = self.spec.forward(self.params.data, obs)
+        logp_all, ent = categorical(logits)
+        u = torch.rand(logits.shape, generator=self.gen, device=self.device).clamp_(min=1e-20)
+        action = torch.argmax(logits - torch.log(-torch.log(u)), dim=-1)
+        logp = logp_all.gather(-1, action.unsqueeze(-1)).squeeze(-1)
+        return action, logp, ent, value
+
+    @torch.no_grad()
+    def store(self, t: int, obs, action, reward, done, value, logp):
+        self.obs[:, t].copy_(obs, non_blocking=True)
+        self.actions[:, t].copy_(action, non_blocking=True)
+        self.rewards[:, t].copy_(reward, non_blocking=True)
+        self.dones[:, t].copy_(done, non_blocking=True)
+        self.values[:, t].copy_(value, non_blocking=True)
+        self.log_probs[:, t].copy_(logp, non_blocking=True)
+
+    @torch.no_grad()
+    def finish_rollout(self, last_obs: torch.Tensor, last_done: torch.Tensor):
+        """Bootstrap value + GAE (+ per-agent advantage statistics)."""
+        _, last_value = self.spec.forward(self.params.data, last_obs)
+        K.gae(self.rewards, self.dones, self.values, last_value.contiguous(), last_done.contiguous(),
+              self.gamma, self.gae_lambda, True, advantages=self.advantages, returns=self.returns,
+              with_stats=True, workspace=self.gae_ws, stats_out=self.adv_stats)
+
+    # ------------------------------------------------------------------ #
+    def learn(self) -> torch.Tensor:
+        """One PPO update of every agent; returns the reference's mean_loss per
+        agent (device tensor [P], no host sync)."""
+        self.learn_steps += 1
+        if self.fused:
+            from .learner import fused_learn
+
+            return fused_learn(self)
+        return self._learn_torch()
+
+    def minibatch_plan(self):
+        b = self.batch_size
+        return [(s, min(s + b, self.S)) for s in range(0, self.S, b)]
+
+    def permutations(self) -> torch.Tensor:
+        """[E, P, S] int64 per-agent shuffles (the reference's np.random.shuffle
+        per epoch, ppo.py:842), drawn on the device."""
+        keys = torch.rand(self.update_epochs, self.P, self.S, generator=self.gen, device=self.device)
+        return torch.argsort(keys, dim=-1)
+
+    def _learn_torch(self, perms: torch.Tensor | None = None) -> torch.Tensor:
+        P, S, D = self.P, self.S, self.spec.obs_dim
+        K.adv_normalize_(self.advantages, self.adv_stats)
+        obs = self.obs.view(P, S, D)
+        act = self.actions.view(P, S)
+        old_logp = self.log_probs.view(-1)
+        adv = self.advantages.view(-1)
+        ret = self.returns.view(-1)
+        old_v = self.values.view(-1)
+        base = (torch.arange(P, device=self.device) * S).unsqueeze(1)
+        if perms is None:
+            perms = self.permutations()
+        total = torch.zeros(P, dtype=torch.float32, device=self.device)
+        for e in range(self.update_epochs):
+            for s0, s1 in self.minibatch_plan():
+                idx = perms[e][:, s0:s1]  # [P, b]
+                ob = torch.gather(obs, 1, idx.unsqueeze(-1).expand(-1, -1, D))
+                ac = torch.gather(act, 1, idx)
+                logits, value = self.spec.forward(self.params, ob)
+                logp_all, ent = categorical(logits)
+                logp = logp_all.gather(-1, ac.unsqueeze(-1)).squeeze(-1)
+                gidx = (idx + base).reshape(-1).contiguous()
+                loss, stats = _PPOLossFn.apply(logp, value, ent, old_logp, adv, ret, old_v, gidx,
+                                               s1 - s0, self.clip_coef, self.vf_coef, self.ent_coef)
+                self.params.grad.zero_()
+                loss.backward()
+                self.opt.step()
+                total += stats[:, 0]
+        return total / (S * self.update_epochs)
+
+    # ------------------------------------------------------------------ #
+    @torch.no_grad()
+    def evaluate(self, obs: torch.Tensor) -> torch.Tensor:
+        """Greedy actions (mode of the categorical) for fitness evaluation."""
+        logits, _ = self.spec.forward(self.params.data, obs)
+        return torch.argmax(logits, dim=-1)
+
+    def n_minibatches(self) -> int:
+        return math.ceil(self.S / self.batch_size)

@@ -1,0 +1,296 @@
+"""Benchmark: population env-steps/s (+ learner updates/s) of an 8-agent PPO
+population (config 2: LunarLander-shaped, 128 vec envs per agent, T=16,
+B=128, E=4), plus the GAE + clipped-loss kernel roofline at the SURVEY §8d
+synthetic shape, plus the reference-style CPU baseline.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: launched by torch.distributed.run, one rank per GPU over RCCL)
+
+A "step" = one PPO iteration of the whole per-GPU population: T vector steps
+of rollout for every agent (host env + HBM rollout SoA), bootstrap + GAE,
+and E x M minibatch learner updates per agent.  Scaling is weak: every GPU
+runs its own 8-agent population (a shard of an 8N-agent population); ranks
+exchange only fitness scalars (RCCL all-gather) and the selected parents'
+parameters at generation boundaries (--evo-every).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+GAE_BYTES = 17          # per transition   
+LOSS_BYTES = 40         # per sample·epoch
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md, chip-level parameters (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pop", type=int, default=8, help="agents per GPU")
+    ap.add_argument("--num-envs", type=int, default=128)
+    ap.add_argument("--learn-step", type=int, default=2048)
+    ap.add_argument("--batch-size", type=int, default=128)
+    ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--evo-every", type=int, default=5, help="iterations per generation (0: never)")
+    ap.add_argument("--learner", choices=["fused", "torch"], default="fused")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--roof-reps", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+# --------------------------------------------------------------------------- #
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# --------------------------------------------------------------------------- #
+def population_leg(args, world, rank):
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.population_sync import PopulationSync
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+    from agilerl_amd.population.runner import PopulationRunner
+
+    spec = ActorCriticSpec(obs_dim=8, n_actions=4, encoder_hidden=[64], latent_dim=64,
+                           actor_hidden=[64], critic_hidden=[64])
+    P, N = args.pop, args.num_envs
+    seeds = [rank * P + i for i in range(P)]
+    pop = PPOPopulation(spec, P, N, learn_step=args.learn_step, batch_size=args.batch_size, lr=1e-3,
+                        update_epochs=args.epochs, seeds=seeds, device="cuda",
+                        fused=args.learner == "fused")
+    env = SyntheticVecEnv(P * N, seed=1000 + rank)
+    runner = PopulationRunner(pop, env)
+    sync = PopulationSync(pop, runner, world, rank, seed=42) if args.evo_every > 0 else None
+
+    def step(i):
+        runner.iteration()
+        if sync is not None and (i + 1) % args.evo_every == 0:
+            sync.generation()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    env_steps = world * P * pop.S * args.steps
+    updates = world * P * args.epochs * pop.n_minibatches() * args.steps
+    return dict(dt=dt, env_steps=env_steps, updates=updates, S=pop.S, T=pop.T,
+                generations=(args.steps // args.evo_every) if args.evo_every else 0)
+
+
+# --------------------------------------------------------------------------- #
+def measure_copy_peak():
+    n = 512 * 1024 * 1024 // 4  # 512 MiB per side
+    a = torch.empty(n, dtype=torch.float32, device="cuda").uniform_()
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    reps = 10
+    for _ in range(reps):
+        b.copy_(a)
+    e.record()
+    e.synchronize()
+    ms = s.elapsed_time(e) / reps
+    del a, b
+    return 2 * n * 4 / (ms * 1e-3) / 1e9
+
+
+def roofline_leg(args):
+    """GAE (P=8, T=1024, N=8192) + E=4 passes of the loss fwd+bwd over the same
+    67.1 M samples (b = 128), timed per kernel with HIP events on the launch
+    stream (torch's current stream: libagx launches there)."""
+    from agilerl_amd import kernels as K
+
+    P, T, N, E, b = 8, 1024, 8192, 4, 128
+    S = P * T * N
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+    r = torch.randn(P, T, N, device=dev, generator=g)
+    v = torch.randn(P, T, N, device=dev, generator=g)
+    d = (torch.rand(P, T, N, device=dev, generator=g) < 0.01).to(torch.uint8)
+    lv = torch.randn(P, N, device=dev, generator=g)
+    ld = (torch.rand(P, N, device=dev, generator=g) < 0.01).to(torch.uint8)
+    adv = torch.empty_like(r)
+    ret = torch.empty_like(r)
+    stats = torch.empty(P, 2, dtype=torch.float64, device=dev)
+    ws = torch.empty(max(16, K._lib.load().agx_gae_workspace_bytes(P, T, N)), dtype=torch.uint8, device=dev)
+    g1 = torch.Generator(device=dev).manual_seed(1)
+    old_logp = torch.rand(S, device=dev, generator=g1) * -2.95 - 0.05
+    logp = old_logp + 0.05 * torch.randn(S, device=dev, generator=g1)
+    newv = v.view(-1) + 0.1 * torch.randn(S, device=dev, generator=g1)
+    H = torch.rand(S, device=dev, generator=g1) * float(np.log(4))
+    out = tuple(torch.empty(S, device=dev) for _ in range(3))
+    lstats = torch.empty(S // b, 8, device=dev)
+
+    def run_gae():
+        K.gae(r, d, v, lv, ld, 0.99, 0.95, True, advantages=adv, returns=ret, with_stats=True,
+              workspace=ws, stats_out=stats)
+
+    def run_loss():
+        K.ppo_loss_fwd_bwd(logp, old_logp, adv.view(-1), ret.view(-1), v.view(-1), newv, H, b, 0.2, 0.5,
+                           0.01, out=out, stats=lstats)
+
+    for _ in range(2):
+        run_gae()
+        run_loss()
+    torch.cuda.synchronize()
+    t_gae, t_loss = [], []
+    for _ in range(args.roof_reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        run_gae()
+        e1.record()
+        evs = []
+        for _ in range(E):
+            a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a0.record()
+            run_loss()
+            a1.record()
+            evs.append((a0, a1))
+        torch.cuda.synchronize()
+        t_gae.append(e0.elapsed_time(e1) * 1e-3)
+        t_loss += [x.elapsed_time(y) * 1e-3 for x, y in evs]
+    tg = float(np.mean(t_gae))
+    tl = float(np.mean(t_loss))
+    peak_meas = measure_copy_peak()
+    fused_bytes = (GAE_BYTES + E * LOSS_BYTES) * S
+    fused_t = tg + E * tl
+    ach = fused_bytes / fused_t / 1e9
+    res = dict(
+        bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+        frac=round(ach / HBM_PEAK_GBS, 4), traffic=None,
+        kernel="agx_gae + 4 x agx_ppo_loss_fwd_bwd (GAE+loss, E=4)",
+        units="transitions P=8 T=1024 N=8192 (67.1M), 177 B each (17 GAE + 4x40 loss)",
+        gae_ms=round(tg * 1e3, 3), loss_ms=round(tl * 1e3, 3),
+        gae_gbs=round(GAE_BYTES * S / tg / 1e9, 1), loss_gbs=round(LOSS_BYTES * S / tl / 1e9, 1),
+        peak_measured_copy=round(peak_meas, 1), frac_of_measured=round(ach / peak_meas, 4),
+    )
+    del r, v, d, adv, ret, old_logp, logp, newv, H, out
+    torch.cuda.empty_cache()
+    return res
+
+
+# --------------------------------------------------------------------------- #
+def cpu_baseline_leg(args, S_per_agent):
+    """The reference-style CPU PPO iteration (oracle/ppo_cpu.py), one agent at a
+    time like train_on_policy.py:210, on a bounded sample: whole agent
+    iterations until --cpu-seconds elapse (at least one)."""
+    from agilerl_amd.envs import SyntheticVecEnv
+    from oracle.ppo_cpu import CpuPPOAgent
+
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    agent = CpuPPOAgent(num_envs=args.num_envs, learn_step=args.learn_step, batch_size=args.batch_size,
+                        update_epochs=args.epochs)
+    env = SyntheticVecEnv(args.num_envs, seed=7)
+    t0 = time.perf_counter()
+    n = 0
+    steps = 0
+    while True:
+        steps += agent.iteration(env)
+        n += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    torch.set_num_threads(threads)
+    return dict(value=round(steps / dt, 1), unit="env-steps/s", cores=1, kind="port",
+                sample=f"{n} single-agent PPO iterations (T={agent.T}, N={args.num_envs}, "
+                       f"E={args.epochs}, B={args.batch_size}) of oracle/ppo_cpu.py on 1 host thread "
+                       f"({os.cpu_count()} CPUs visible), {dt:.1f}s; reference trains agents sequentially, "
+                       f"so population env-steps/s = per-agent rate")
+
+
+# --------------------------------------------------------------------------- #
+def main():
+    args = parse()
+    world, rank, local = setup_dist()
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    from agilerl_amd import _lib
+
+    _lib.load()
+    res = population_leg(args, world, rank)
+    roof = None
+    if not args.no_roofline:
+        roof = roofline_leg(args)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline_leg(args, res["S"])
+    if rank == 0:
+        value = res["env_steps"] / res["dt"]
+        line = {
+            "metric": "population env-steps/sec (8-agent PPO per GPU, LunarLander-shaped synthetic envs)",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(res["dt"] / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (GAE carry f64)",
+            "data": "synthetic (host SyntheticVecEnv: obs 8 f32, 4 actions, r~N(0,1), done~Bern(1/200))",
+            "config": {
+                "workload": "config 2: PPO pop=8 per GPU x 128 vec envs, T=16, batch 128, 4 epochs, "
+                            "MLP enc[64]->64 + heads[64] (shared encoder), tournament every "
+                            f"{args.evo_every} iterations",
+                "pop_per_gpu": args.pop, "num_envs": args.num_envs, "learn_step": args.learn_step,
+                "batch_size": args.batch_size, "update_epochs": args.epochs, "learner": args.learner,
+                "parallelism": f"population-sharded x{world}",
+            },
+            "learner_updates_per_s": round(res["updates"] / res["dt"], 1),
+            "generations": res["generations"],
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
