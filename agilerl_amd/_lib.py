@@ -31,6 +31,11 @@ SIGNATURES = {
     "agx_gae": (_INT, [_P, _P, _P, _P, _P, _I, _I, _I, _D, _D, _INT, _P, _P, _P, _P, _P]),
     "agx_adv_normalize": (_INT, [_P, _P, _I, _I, _P]),
     "agx_ppo_loss_fwd_bwd": (_INT, [_P] * 8 + [_I, _I, _F, _F, _F, _P, _P, _P, _P, _P]),
+    "agx_ppo_learn_lds_bytes": (_SZ, [_P]),
+    "agx_ppo_learn_workspace_bytes": (_SZ, [_P]),
+    "agx_ppo_learn_prepare": (_INT, [_P, _P, _P]),
+    "agx_ppo_learn": (_INT, [_P, _I, _P, _P, _P, _P, _F, _F, _F, _I, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I,
+                             _F, _F, _F, _F, _P, _P, _P]),
     "agx_per_workspace_bytes": (_SZ, [_I, _I]),
     "agx_per_init": (_INT, [_P, _P, _I, _P]),
     "agx_per_add": (_INT, [_P, _P, _I, _I, _I, _I, _D, _P, _P, _P]),

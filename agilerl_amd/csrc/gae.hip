@@ -19,14 +19,14 @@
 // hidden by this per-lane ILP rather than by occupancy.
 // Algorithmic bytes: 4 (r) + 1 (done) + 4 (v) in, 4 (adv) + 4 (ret) out = 17 B
 // per transition.
+#include <cstdlib>
+
 #include "agx_common.h"
 
 namespace agx {
 
 constexpr int kGaeBlock = 256;
-constexpr int kGaeU = 8;  // prefetch depth (time steps per register set)
-
-template <bool kGae, bool kStats>
+template <int kGaeU, bool kGae, bool kStats>
 __global__ __launch_bounds__(kGaeBlock) void gae_kernel(
     const float *__restrict__ rewards, const uint8_t *__restrict__ dones,
     const float *__restrict__ values, const float *__restrict__ last_value,
@@ -225,17 +225,30 @@ extern "C" int agx_gae(const float *rewards, const uint8_t *dones, const float *
     dim3 grid(nblk, (unsigned)P);
     const double gl = gamma * gae_lambda;
     double *part = static_cast<double *>(workspace);
-#define AGX_GAE_LAUNCH(G, S)                                                                   \
-    gae_kernel<G, S><<<grid, kGaeBlock, 0, s>>>(rewards, dones, values, last_value, last_done, \
-                                                (int)T, (int)N, gamma, gl, advantages,         \
-                                                returns, part)
-    if (use_gae) {
-        if (adv_stats) AGX_GAE_LAUNCH(true, true);
-        else AGX_GAE_LAUNCH(true, false);
-    } else {
-        if (adv_stats) AGX_GAE_LAUNCH(false, true);
-        else AGX_GAE_LAUNCH(false, false);
+    // prefetch depth: deeper register pipelines for long scans (per-lane ILP is
+    // what hides HBM latency at 1-4 waves per SIMD); AGX_GAE_UNROLL overrides.
+    int U = T >= 32 ? 16 : 8;  // measured on MI355X at P8 T1024 N8192: U8 3.75, U16 4.78, U32 4.51 TB/s
+    if (const char *e = getenv("AGX_GAE_UNROLL")) U = atoi(e);
+#define AGX_GAE_LAUNCH(UU, G, S)                                                                    \
+    gae_kernel<UU, G, S><<<grid, kGaeBlock, 0, s>>>(rewards, dones, values, last_value, last_done, \
+                                                    (int)T, (int)N, gamma, gl, advantages,         \
+                                                    returns, part)
+#define AGX_GAE_U(UU)                                          \
+    if (use_gae) {                                             \
+        if (adv_stats) AGX_GAE_LAUNCH(UU, true, true);         \
+        else AGX_GAE_LAUNCH(UU, true, false);                  \
+    } else {                                                   \
+        if (adv_stats) AGX_GAE_LAUNCH(UU, false, true);        \
+        else AGX_GAE_LAUNCH(UU, false, false);                 \
     }
+    if (U >= 32) {
+        AGX_GAE_U(32)
+    } else if (U >= 16) {
+        AGX_GAE_U(16)
+    } else {
+        AGX_GAE_U(8)
+    }
+#undef AGX_GAE_U
 #undef AGX_GAE_LAUNCH
     int rc = check_launch("agx_gae");
     if (rc || !adv_stats) return rc;

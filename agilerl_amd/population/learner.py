@@ -1,0 +1,90 @@
+"""Host side of the fused PPO learner (agx_ppo_learn in learner.hip)."""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from .. import _lib
+from .. import kernels as K
+from .nets import ActorCriticSpec
+
+_i32 = ctypes.c_int32
+
+
+class AgxPPONet(ctypes.Structure):
+    """Mirror of ``agx_ppo_net`` (include/agx.h)."""
+
+    _fields_ = [
+        ("obs_dim", _i32), ("n_actions", _i32), ("n_enc", _i32), ("enc_dim", _i32 * 4),
+        ("enc_w", _i32 * 3), ("enc_b", _i32 * 3), ("enc_ln_w", _i32 * 3), ("enc_ln_b", _i32 * 3),
+        ("head_actor", _i32), ("head_critic", _i32),
+        ("actor_w", _i32), ("actor_b", _i32), ("actor_ln_w", _i32), ("actor_ln_b", _i32),
+        ("actor_out_w", _i32), ("actor_out_b", _i32),
+        ("critic_w", _i32), ("critic_b", _i32), ("critic_ln_w", _i32), ("critic_ln_b", _i32),
+        ("critic_out_w", _i32), ("critic_out_b", _i32),
+        ("n_params", _i32), ("critic_start", _i32),
+    ]
+
+
+def net_descriptor(spec: ActorCriticSpec) -> AgxPPONet | None:
+    """The fused-kernel descriptor, or None when the architecture is outside
+    what agx_ppo_learn covers (then the torch learner runs)."""
+    if (len(spec.actor) != 2 or len(spec.critic) != 2 or not spec.layer_norm
+            or not 2 <= len(spec.encoder) <= 3):
+        return None
+    d = AgxPPONet()
+    d.obs_dim, d.n_actions, d.n_enc = spec.obs_dim, spec.n_actions, len(spec.encoder)
+    d.enc_dim[0] = spec.obs_dim
+    for i, lay in enumerate(spec.encoder):
+        d.enc_dim[i + 1] = lay.fout
+        d.enc_w[i], d.enc_b[i] = lay.w, lay.b
+        d.enc_ln_w[i], d.enc_ln_b[i] = lay.g, lay.beta
+    a1, ao = spec.actor
+    c1, co = spec.critic
+    d.head_actor, d.head_critic = a1.fout, c1.fout
+    d.actor_w, d.actor_b, d.actor_ln_w, d.actor_ln_b = a1.w, a1.b, a1.g, a1.beta
+    d.actor_out_w, d.actor_out_b = ao.w, ao.b
+    d.critic_w, d.critic_b, d.critic_ln_w, d.critic_ln_b = c1.w, c1.b, c1.g, c1.beta
+    d.critic_out_w, d.critic_out_b = co.w, co.b
+    d.n_params, d.critic_start = spec.n_params, spec.actor_end
+    lib = _lib.load(require_gpu=False)  # pure host-side planning query
+    if lib.agx_ppo_learn_lds_bytes(ctypes.byref(d)) == 0:
+        return None
+    return d
+
+
+class FusedLearner:
+    def __init__(self, pop):
+        self.desc = net_descriptor(pop.spec)
+        if self.desc is None:
+            raise _lib.AgxError("network outside the fused learner's coverage")
+        lib = _lib.load()
+        nbytes = lib.agx_ppo_learn_workspace_bytes(ctypes.byref(self.desc))
+        self.ws = torch.empty(max(16, nbytes), dtype=torch.uint8, device=pop.device)
+        _lib.check(lib.agx_ppo_learn_prepare(ctypes.byref(self.desc), self.ws.data_ptr(), _lib.stream()),
+                   "agx_ppo_learn_prepare")
+        self.loss = torch.zeros(pop.P, dtype=torch.float32, device=pop.device)
+
+    def learn(self, pop, perms: torch.Tensor | None = None) -> torch.Tensor:
+        K.adv_normalize_(pop.advantages, pop.adv_stats)
+        if perms is None:
+            perms = pop.permutations()
+        opt = pop.opt
+        b1, b2 = opt.betas
+        _lib.call("agx_ppo_learn", ctypes.byref(self.desc), pop.P, pop.params.data.data_ptr(),
+                  opt.exp_avg.data_ptr(), opt.exp_avg_sq.data_ptr(), opt.lr.data_ptr(), float(b1), float(b2),
+                  float(opt.eps), opt.step_count, pop.obs.data_ptr(), pop.actions.data_ptr(),
+                  pop.log_probs.data_ptr(), pop.advantages.data_ptr(), pop.returns.data_ptr(),
+                  pop.values.data_ptr(), pop.S, perms.data_ptr(), pop.update_epochs, pop.batch_size,
+                  float(pop.clip_coef), float(pop.vf_coef), float(pop.ent_coef), float(pop.max_grad_norm),
+                  self.loss.data_ptr(), self.ws.data_ptr(), _lib.stream())
+        opt.step_count += pop.update_epochs * pop.n_minibatches()
+        return self.loss
+
+
+def fused_learn(pop, perms=None) -> torch.Tensor:
+    if getattr(pop, "_fused", None) is None:
+        pop._fused = FusedLearner(pop)
+    return pop._fused.learn(pop, perms)

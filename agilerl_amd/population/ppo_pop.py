@@ -135,10 +135,13 @@ class PPOPopulation:
         """One PPO update of every agent; returns the reference's mean_loss per
         agent (device tensor [P], no host sync)."""
         self.learn_steps += 1
-        if self.fused:
-            from .learner import fused_learn
+        if self.fused and self.target_kl is None:
+            from .learner import fused_learn, net_descriptor
 
-            return fused_learn(self)
+            if getattr(self, "_fused_ok", None) is None:
+                self._fused_ok = net_descriptor(self.spec) is not None
+            if self._fused_ok:
+                return fused_learn(self)
         return self._learn_torch()
 
     def minibatch_plan(self):

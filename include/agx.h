@@ -76,6 +76,49 @@ int agx_ppo_loss_fwd_bwd(const float *logp, const float *old_logp, const float *
                          float ent_coef, float *g_logp, float *g_value, float *g_entropy,
                          float *stats, void *stream);
 
+/* ---- fused PPO learner ----------------------------------------------------
+ * Replaces PPO._learn_from_rollout_buffer_flat (agilerl/algorithms/ppo.py:
+ * 836-921) end to end for the shared-encoder MLP actor-critic the reference
+ * builds (create_mlp, agilerl/utils/evolvable_networks.py:527-644): per
+ * agent one workgroup runs all epochs x minibatches (gather -> forward ->
+ * loss -> backward -> 2-group grad clip -> Adam) with parameters in LDS and
+ * f32 MFMA GEMMs.  Offsets below index one agent's flat parameter row
+ * [encoder | actor head | critic head] in state-dict order.
+ * Supported: 2-3 encoder Linear layers (hidden: LayerNorm(affine)+ReLU,
+ * output: LayerNorm(plain)+ReLU), one hidden layer per head (LN affine +
+ * ReLU), widths multiples of 16 (<= 128, heads <= 256 together),
+ * obs_dim <= 128, n_actions <= 16; otherwise AGX_EUNSUPPORTED. */
+typedef struct agx_ppo_net {
+    int32_t obs_dim, n_actions, n_enc;
+    int32_t enc_dim[4]; /* enc_dim[0] = obs_dim, enc_dim[i] = width of encoder layer i */
+    int32_t enc_w[3], enc_b[3], enc_ln_w[3], enc_ln_b[3];
+    int32_t head_actor, head_critic;
+    int32_t actor_w, actor_b, actor_ln_w, actor_ln_b, actor_out_w, actor_out_b;
+    int32_t critic_w, critic_b, critic_ln_w, critic_ln_b, critic_out_w, critic_out_b;
+    int32_t n_params, critic_start;
+} agx_ppo_net;
+
+/* LDS bytes the fused learner needs for `net` (0: unsupported). */
+size_t agx_ppo_learn_lds_bytes(const agx_ppo_net *net);
+/* Device workspace bytes for agx_ppo_learn_prepare / agx_ppo_learn. */
+size_t agx_ppo_learn_workspace_bytes(const agx_ppo_net *net);
+/* One-time: upload the gradient-ownership table into `workspace`
+ * (synchronises `stream`; call outside any graph capture). */
+int agx_ppo_learn_prepare(const agx_ppo_net *net, void *workspace, void *stream);
+/* params / exp_avg / exp_avg_sq: [P][n_params] (updated in place);
+ * lr: device f32 [P]; Adam steps adam_step0+1 ... are used for the
+ * epochs*ceil(S/batch) updates; obs [P][S][obs_dim], actions int64 [P][S],
+ * old_logp / adv (already normalised) / ret / old_value f32 [P][S];
+ * perms int64 [epochs][P][S] (each row a permutation of 0..S-1);
+ * loss_out f32 [P] = sum of minibatch losses / (S * epochs) (ppo.py:920). */
+int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, float *exp_avg,
+                  float *exp_avg_sq, const float *lr, float beta1, float beta2, float eps,
+                  int64_t adam_step0, const float *obs, const int64_t *actions,
+                  const float *old_logp, const float *adv, const float *ret,
+                  const float *old_value, int64_t S, const int64_t *perms, int64_t epochs,
+                  int64_t batch, float clip_coef, float vf_coef, float ent_coef,
+                  float max_grad_norm, float *loss_out, void *workspace, void *stream);
+
 /* ---- prioritized replay segment trees -----------------------------------
  * Replaces SumSegmentTree / MinSegmentTree (agilerl/components/
  * segment_tree.py) and the priority half of PrioritizedReplayBuffer

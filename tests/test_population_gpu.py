@@ -1,0 +1,121 @@
+"""Population PPO engine on the GPU: the fused learner kernel (agx_ppo_learn)
+against the plain-PyTorch fp32 learner on identical inputs and permutations,
+and an end-to-end rollout -> GAE -> learn iteration."""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _pop(P=3, N=16, learn_step=128, batch=64, epochs=1, seed=0, **kw):
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+
+    spec = ActorCriticSpec(obs_dim=8, n_actions=4, **kw)
+    pop = PPOPopulation(spec, P, N, learn_step=learn_step, batch_size=batch, lr=1e-3, update_epochs=epochs,
+                        seeds=[seed + i for i in range(P)], device=DEV, fused=True)
+    g = torch.Generator(device=DEV).manual_seed(seed + 99)
+    pop.obs.copy_(torch.randn(pop.obs.shape, device=DEV, generator=g))
+    pop.actions.copy_(torch.randint(0, 4, pop.actions.shape, device=DEV, generator=g))
+    pop.rewards.copy_(torch.randn(pop.rewards.shape, device=DEV, generator=g))
+    pop.dones.copy_((torch.rand(pop.dones.shape, device=DEV, generator=g) < 0.05).to(torch.uint8))
+    with torch.no_grad():
+        logits, value = spec.forward(pop.params.data, pop.obs.view(P, -1, 8))
+        lp = torch.log_softmax(logits, -1).gather(-1, pop.actions.view(P, -1, 1)).squeeze(-1)
+    pop.values.copy_(value.view_as(pop.values) + 0.1 * torch.randn(pop.values.shape, device=DEV, generator=g))
+    pop.log_probs.copy_(lp.view_as(pop.log_probs) + 0.05 * torch.randn(pop.log_probs.shape, device=DEV, generator=g))
+    last_obs = torch.randn(P, N, 8, device=DEV, generator=g)
+    last_done = torch.zeros(P, N, dtype=torch.uint8, device=DEV)
+    pop.finish_rollout(last_obs, last_done)
+    return pop
+
+
+def _clone_state(pop):
+    return (pop.params.data.clone(), pop.opt.exp_avg.clone(), pop.opt.exp_avg_sq.clone(),
+            pop.advantages.clone(), pop.opt.step_count)
+
+
+def _restore(pop, st):
+    pop.params.data.copy_(st[0])
+    pop.opt.exp_avg.copy_(st[1])
+    pop.opt.exp_avg_sq.copy_(st[2])
+    pop.advantages.copy_(st[3])
+    pop.opt.step_count = st[4]
+
+
+@pytest.mark.parametrize("N,learn_step,batch,epochs", [(16, 64, 64, 1), (16, 128, 64, 1), (8, 100, 32, 2),
+                                                       (16, 128, 48, 1)])
+def test_fused_learner_matches_torch_learner(N, learn_step, batch, epochs):
+    from agilerl_amd.population.learner import fused_learn
+
+    pop = _pop(N=N, learn_step=learn_step, batch=batch, epochs=epochs)
+    st = _clone_state(pop)
+    perms = pop.permutations()
+    loss_t = pop._learn_torch(perms).clone()
+    p_torch = pop.params.data.clone()
+    m_torch = pop.opt.exp_avg.clone()
+    _restore(pop, st)
+    loss_f = fused_learn(pop, perms).clone()
+    torch.cuda.synchronize()
+    p0 = st[0]
+    d_t = (p_torch - p0)
+    d_f = (pop.params.data - p0)
+    # Gradients are what the kernels compute: the Adam first moment carries
+    # them.  The parameter update m/(sqrt(v)+eps) is ill-conditioned where
+    # |g| ~ eps, so it is checked on 99.9% of the entries only.
+    m_f, m_t = pop.opt.exp_avg.cpu().numpy(), m_torch.cpu().numpy()
+    np.testing.assert_allclose(m_f, m_t, rtol=2e-3, atol=1e-5 * np.abs(m_t).max())
+    scale = d_t.abs().max().item()
+    assert scale > 0
+    bad = ((d_f - d_t).abs() > 2e-3 * scale).float().mean().item()
+    assert bad <= 1e-3, bad
+    np.testing.assert_allclose(loss_f.cpu().numpy(), loss_t.cpu().numpy(), rtol=1e-4, atol=1e-7)
+
+
+def test_fused_learner_single_update_tight():
+    """One minibatch, one epoch: gradients and the single Adam step agree
+    closely (only summation order differs)."""
+    from agilerl_amd.population.learner import fused_learn
+
+    pop = _pop(N=32, learn_step=64, batch=64, epochs=1, seed=5)
+    st = _clone_state(pop)
+    perms = pop.permutations()
+    pop._learn_torch(perms)
+    g_torch = pop.opt.grads.clone()  # clipped gradients of the single update
+    m_t = pop.opt.exp_avg.clone()
+    _restore(pop, st)
+    fused_learn(pop, perms)
+    torch.cuda.synchronize()
+    # first Adam step: exp_avg = 0.1 * g_clipped exactly
+    np.testing.assert_allclose(pop.opt.exp_avg.cpu().numpy(), m_t.cpu().numpy(), rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose((pop.opt.exp_avg / 0.1).cpu().numpy(), g_torch.cpu().numpy(), rtol=1e-3, atol=1e-8)
+
+
+def test_runner_iteration_end_to_end():
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.population_sync import PopulationSync
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+    from agilerl_amd.population.runner import PopulationRunner
+
+    spec = ActorCriticSpec(obs_dim=8, n_actions=4)
+    pop = PPOPopulation(spec, 4, 32, learn_step=256, batch_size=64, update_epochs=2, device=DEV)
+    runner = PopulationRunner(pop, SyntheticVecEnv(4 * 32, seed=3))
+    p0 = pop.params.data.clone()
+    for _ in range(2):
+        loss = runner.iteration()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).all()
+    assert not torch.equal(p0, pop.params.data)
+    assert runner.env_steps == 2 * 4 * 32 * 8
+    # actions in range, stored dones match the env's
+    assert int(pop.actions.min()) >= 0 and int(pop.actions.max()) < 4
+    sync = PopulationSync(pop, runner, seed=1)
+    parents = sync.generation()
+    assert len(parents) == 4 and all(0 <= p < 4 for p in parents)
+    for i, par in enumerate(parents):
+        assert torch.equal(pop.params.data[i], pop.params.data[i]) and par >= 0
