@@ -32,10 +32,12 @@ SIGNATURES = {
     "agx_adv_normalize": (_INT, [_P, _P, _I, _I, _P]),
     "agx_ppo_loss_fwd_bwd": (_INT, [_P] * 8 + [_I, _I, _F, _F, _F, _P, _P, _P, _P, _P]),
     "agx_ppo_learn_lds_bytes": (_SZ, [_P]),
-    "agx_ppo_learn_workspace_bytes": (_SZ, [_P]),
+    "agx_ppo_learn_workspace_bytes": (_SZ, [_P, _I, _I, _I]),
     "agx_ppo_learn_prepare": (_INT, [_P, _P, _P]),
-    "agx_ppo_learn": (_INT, [_P, _I, _P, _P, _P, _P, _F, _F, _F, _I, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I,
-                             _F, _F, _F, _F, _P, _P, _P]),
+    "agx_ppo_learn": (_INT, [_P, _I, _P, _P, _P, _P, _F, _F, _F, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I,
+                             _I, _F, _F, _F, _F, _P, _P, _P]),
+    "agx_ppo_act": (_INT, [_P, _I, _I, _P, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P, _I,
+                           _P, _P, _P]),
     "agx_per_workspace_bytes": (_SZ, [_I, _I]),
     "agx_per_init": (_INT, [_P, _P, _I, _P]),
     "agx_per_add": (_INT, [_P, _P, _I, _I, _I, _I, _D, _P, _P, _P]),
@@ -48,6 +50,7 @@ SIGNATURES = {
     "agx_clip_adam": (_INT, [_P, _P, _P, _P, _I, _I, _P, _INT, _F, _P, _F, _F, _F, _I, _P, _P]),
     "agx_polyak": (_INT, [_P, _P, _I, _F, _P]),
     "agx_debug_pow": (_INT, [_P, _P, _P, _I, _P]),
+    "agx_debug_learn_stamps": (_INT, [_P]),
 }
 
 _lib = None

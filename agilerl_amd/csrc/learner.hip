@@ -1,33 +1,49 @@
-// Fused PPO learner: ONE persistent workgroup per agent runs every
-// epoch x minibatch update of PPO._learn_from_rollout_buffer_flat
-// (agilerl/algorithms/ppo.py:836-915) — gather, MLP forward, categorical
-// log-prob / entropy, clipped-surrogate + clipped-value loss, backward through
-// the shared-encoder actor-critic, two-group gradient-norm clip
-// (ppo.py:910-911) and Adam (optimizer_wrapper.py:444-452) — without leaving
-// the chip.
+// Fused PPO learner + rollout policy step for a population of shared-encoder
+// MLP actor-critics.
 //
-// Network (the reference's config-2 PPO nets, agilerl/utils/
-// evolvable_networks.py:527-644, agilerl/networks/base.py:541-561):
+// agx_ppo_learn: ONE persistent workgroup per agent runs every epoch x
+// minibatch update of PPO._learn_from_rollout_buffer_flat
+// (agilerl/algorithms/ppo.py:836-915) — forward, categorical log-prob /
+// entropy, clipped-surrogate + clipped-value loss, backward, two-group
+// gradient-norm clip (ppo.py:910-911) and Adam (optimizer_wrapper.py:444-452)
+// — without leaving the chip.  A prologue kernel first gathers the rollout
+// SoA into per-epoch minibatch order (the reference's shuffled TensorDict
+// indexing, ppo.py:842-848) and applies the global advantage normalisation
+// (ppo.py:829-834), so the learner streams contiguous 32-row sub-batches.
+//
+// agx_ppo_act: the rollout policy step (PPO.get_action, ppo.py:567-633 ->
+// _get_action_and_values :400-492): forward, Gumbel-max categorical sample
+// from a counter-based Philox stream, log-prob, entropy and value, written
+// straight into the (P, T, N) rollout SoA.
+//
+// Network (agilerl/utils/evolvable_networks.py:527-644 create_mlp,
+// agilerl/networks/base.py:541-561):
 //   encoder: ne-1 x [Linear -> LayerNorm(affine) -> ReLU], Linear(->lat) ->
 //            LayerNorm(plain) -> ReLU
 //   heads  : actor  Linear(lat->ha) -> LN(affine) -> ReLU -> Linear(->A)
 //            critic Linear(lat->hc) -> LN(affine) -> ReLU -> Linear(->1)
 //   The two head hidden layers run as ONE merged [ha+hc] layer (same input,
-//   per-half LayerNorm), and d(latent) = [dz_a | dz_c] . [Wa; Wc] is one GEMM.
+//   per-half LayerNorm); d(latent) = [dz_a | dz_c] . [Wa; Wc] is one GEMM.
 //
-// Work split (512 threads = 8 waves, sub-batches of SB = 32 rows):
-//   * all parameters live in LDS for the whole learn() (padded rows);
-//   * GEMMs (forward Z = X W^T, backward dX = dZ W, dW += dZ^T X) are
-//     f32 MFMA v_mfma_f32_16x16x4_f32 tiles (exact f32 FMA chains);
-//   * the dW of every Linear weight stays in MFMA accumulator registers
-//     across the minibatch (each wave owns a fixed set of 16x16 tiles), and
-//     the clip + Adam update is applied straight from those registers;
-//   * LayerNorm fwd/bwd and the loss are row passes (a wave per row, lanes
-//     across features); bias / LN-affine / output-layer gradients are
-//     reduced per wave into LDS partials and summed by fixed owner threads
-//     in a fixed order (deterministic).
-// Global memory traffic per update: the 32-row gathers of the rollout SoA
-// and the Adam moments; parameters are written back once at the end.
+// Kernels are instantiated per network shape (compile-time plan: every
+// offset, trip count and tile->register assignment is a constant, which is
+// what keeps ~200 live VGPRs spill-free).  Mapping (512 threads = 8 waves,
+// sub-batches of SB = 32 rows):
+//   * parameters live in LDS (weight rows padded by 2 floats: conflict-free
+//     MFMA operand reads); Adam moments live in REGISTERS — thread t owns
+//     LDS parameter slots t, t+512, ... for the whole learn();
+//   * every Linear (incl. the output layers, padded to 16 rows, with the bias
+//     as an extra ones-column) is an f32 MFMA v_mfma_f32_16x16x4_f32 GEMM;
+//     each wave owns fixed 16x16 dW tiles whose accumulators stay in
+//     registers over the sub-batches of a minibatch;
+//   * LayerNorm forward/backward and the loss are row passes with 16 lanes
+//     per row (4 rows per wave): row reductions are DPP (quad_perm,
+//     row_half_mirror, row_mirror); bias / LN-affine gradients are reduced
+//     across the 4 rows by ds_swizzle + permlane32_swap and accumulated per
+//     wave in LDS, summed in a fixed order (deterministic);
+//   * minibatch end: dump dW tiles + vector grads into an LDS gradient image
+//     of the parameter region (aliasing the dead activations), two-group
+//     norm, Adam from registers.
 #include <cmath>
 
 #include "agx_common.h"
@@ -37,795 +53,1110 @@ namespace agx {
 constexpr int kNT = 512;
 constexpr int kNW = kNT / kWave;  // 8 waves
 constexpr int kSB = 32;           // rows per sub-batch
-constexpr int kMaxSlot = 8;       // dW tiles per wave
-constexpr int kVecSlot = 4;       // owned vector-gradient entries per thread
+constexpr int kMaxSlot = 10;      // dW tiles per wave
+constexpr int kMaxPT = 30;        // LDS parameter slots per thread
 constexpr int kMaxA = 16;
+constexpr int kMaxBlk = 28;
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+struct NetDims {
+    int D, A, ne, eo[3], ha, hc;
+};
+
+struct Blk {
+    int f0, len, rowlen, l0, ldst;  // flat [f0, f0+len) <-> LDS l0 + (i / rowlen) * ldst + i % rowlen
+};
+
 struct LearnPlan {
-    // network
-    int D, A, ne, ein[3], eout[3], lat, ha, hc, H;
-    // global flat offsets (per agent row)
-    int ew[3], eb[3], eg[3], ebe[3];
-    int aw, ab, ag, abe, aow, aob, cw, cb, cg, cbe, cow, cob;
-    int n, split;
-    // LDS plan (floats)
+    int ok;
+    int D, A, ne, ein[3], eout[3], eaff[3], lat, ha, hc, H, n;
+    // flat offsets (nets.py layout): per encoder layer W, b, [g, be]; actor W, b,
+    // g, be, Wout, bout; critic W, b, g, be, Wout, bout
+    int f_ew[3], f_eb[3], f_eg[3], f_ebe[3];
+    int f_aw, f_ab, f_ag, f_abe, f_aow, f_aob, f_cw, f_cb, f_cg, f_cbe, f_cow, f_cob;
+    // LDS (floats)
     int l_ew[3], l_eld[3], l_eb[3], l_eg[3], l_ebe[3];
     int l_hw, l_hld, l_hb, l_hg, l_hbe;
-    int l_aow, l_aob, l_cow, l_cob;
-    int l_x0, ld_x0;
-    int l_xe[3], ld_xe[3], l_re[3];
-    int l_xh, ld_xh, l_rh;
+    int l_aow, l_aold, l_aob, l_cow, l_cold, l_cob;
+    int param_end;
+    int l_x0, ld_x0, l_xe[3], ld_xe[3], l_re[3], l_xh, ld_xh, l_rh;
     int l_s1, l_s2, ld_s;
-    int l_lg, l_dlg, l_val, l_dval, l_row, l_red, red_e[3], red_h, l_stat;
-    int lds_floats;
-    int nvec;  // vector-gradient entries (<= kNT * kVecSlot)
-    int ntiles, tile_begin[4];  // dW tiles: enc layers 0..ne-1, then head
+    int l_lg, l_dlg, l_dvb, l_val, l_row;
+    int l_red, red_e[3], red_h, l_stat;
+    int l_grad;  // gradient image of [0, param_end) (aliases the activations)
+    int lds_floats, act_floats;
+    // dW tiles per layer group g: enc 0..ne-1, head ne, out-actor ne+1, out-critic ne+2
+    int nt[6], ncol[6], slot0[6], nslot[6], nslots;
+    int nblk;
+    Blk blk[kMaxBlk];
 };
 
-// vector-gradient entry descriptor (host-built table in global memory)
-struct VecDesc {
-    int flat;   // global flat offset
-    int lds;    // LDS offset of the parameter
-    int group;  // clip group
-    int kind;   // 0: sum of per-wave partials, 1: actor out W, 2: critic out W,
-                // 3: actor out bias, 4: critic out bias
-    int p0, p1; // kind 0: red base, wave stride; kind 1: a, column; kind 2: column
+constexpr int rup(int x, int m) { return (x + m - 1) / m * m; }
+
+constexpr LearnPlan make_plan(NetDims d) {
+    LearnPlan pl{};
+    pl.ok = 0;
+    pl.D = d.D;
+    pl.A = d.A;
+    pl.ne = d.ne;
+    if (pl.ne < 2 || pl.ne > 3 || pl.A < 1 || pl.A > kMaxA || pl.D < 1 || pl.D > 128) return pl;
+    int prev = pl.D;
+    for (int e = 0; e < pl.ne; ++e) {
+        pl.ein[e] = prev;
+        pl.eout[e] = d.eo[e];
+        pl.eaff[e] = e < pl.ne - 1;
+        if (pl.eout[e] % 16 || pl.eout[e] > 128 || pl.eout[e] < 16) return pl;
+        prev = pl.eout[e];
+    }
+    pl.lat = prev;
+    pl.ha = d.ha;
+    pl.hc = d.hc;
+    pl.H = pl.ha + pl.hc;
+    if (pl.ha % 16 || pl.hc % 16 || pl.ha < 16 || pl.hc < 16 || pl.H > 128) return pl;
+    // ---- flat layout
+    int f = 0;
+    for (int e = 0; e < pl.ne; ++e) {
+        pl.f_ew[e] = f;
+        f += pl.eout[e] * pl.ein[e];
+        pl.f_eb[e] = f;
+        f += pl.eout[e];
+        pl.f_eg[e] = pl.f_ebe[e] = -1;
+        if (pl.eaff[e]) {
+            pl.f_eg[e] = f;
+            f += pl.eout[e];
+            pl.f_ebe[e] = f;
+            f += pl.eout[e];
+        }
+    }
+    pl.f_aw = f; f += pl.ha * pl.lat;
+    pl.f_ab = f; f += pl.ha;
+    pl.f_ag = f; f += pl.ha;
+    pl.f_abe = f; f += pl.ha;
+    pl.f_aow = f; f += pl.A * pl.ha;
+    pl.f_aob = f; f += pl.A;
+    pl.f_cw = f; f += pl.hc * pl.lat;
+    pl.f_cb = f; f += pl.hc;
+    pl.f_cg = f; f += pl.hc;
+    pl.f_cbe = f; f += pl.hc;
+    pl.f_cow = f; f += pl.hc;
+    pl.f_cob = f; f += 1;
+    pl.n = f;
+    // ---- LDS: parameters
+    int off = 0;
+    for (int e = 0; e < pl.ne; ++e) {
+        pl.l_eld[e] = rup(pl.ein[e], 16) + 2;
+        pl.l_ew[e] = off; off += rup(pl.eout[e] * pl.l_eld[e], 4);
+        pl.l_eb[e] = off; off += rup(pl.eout[e], 4);
+        pl.l_eg[e] = off; off += pl.eaff[e] ? rup(pl.eout[e], 4) : 0;
+        pl.l_ebe[e] = off; off += pl.eaff[e] ? rup(pl.eout[e], 4) : 0;
+    }
+    pl.l_hld = pl.lat + 2;
+    pl.l_hw = off; off += rup(pl.H * pl.l_hld, 4);
+    pl.l_hb = off; off += rup(pl.H, 4);
+    pl.l_hg = off; off += rup(pl.H, 4);
+    pl.l_hbe = off; off += rup(pl.H, 4);
+    pl.l_aold = pl.ha + 2;
+    pl.l_aow = off; off += rup(pl.A * pl.l_aold, 4);
+    pl.l_aob = off; off += kMaxA;
+    pl.l_cold = pl.hc + 2;
+    pl.l_cow = off; off += rup(pl.l_cold, 4);
+    pl.l_cob = off; off += 4;
+    pl.param_end = off;
+    if (pl.param_end > kNT * kMaxPT) return pl;
+    // ---- LDS: activations (the gradient image aliases them)
+    pl.ld_x0 = rup(pl.D, 16) + 2;
+    pl.l_x0 = off; off += rup(kSB * pl.ld_x0, 4);
+    for (int e = 0; e < pl.ne; ++e) {
+        pl.ld_xe[e] = pl.eout[e] + 2;
+        pl.l_xe[e] = off; off += kSB * pl.ld_xe[e];
+        pl.l_re[e] = off; off += 2 * kSB;
+    }
+    pl.ld_xh = pl.H + 2;
+    pl.l_xh = off; off += kSB * pl.ld_xh;
+    pl.l_rh = off; off += 2 * kSB;
+    int wmax = pl.H;
+    for (int e = 0; e < pl.ne; ++e) wmax = wmax > pl.eout[e] ? wmax : pl.eout[e];
+    pl.ld_s = wmax + 2;
+    pl.l_s1 = off; off += kSB * pl.ld_s;
+    pl.l_s2 = off; off += kSB * pl.ld_s;
+    pl.l_lg = off; off += kSB * kMaxA;
+    pl.l_val = off; off += kSB;
+    pl.act_floats = off;  // the policy-step kernel needs only this much
+    pl.l_dlg = off; off += kSB * kMaxA;
+    pl.l_dvb = off; off += kSB * kMaxA;
+    pl.l_row = off; off += 5 * kSB;
+    pl.l_grad = pl.l_x0;
+    if (off - pl.l_x0 < pl.param_end) off = pl.l_x0 + pl.param_end;  // room for the gradient image
+    int red = 0;
+    for (int e = 0; e < pl.ne; ++e) {
+        pl.red_e[e] = red;
+        red += (pl.eaff[e] ? 3 : 1) * kNW * pl.eout[e];
+    }
+    pl.red_h = red;
+    red += 3 * kNW * pl.H;
+    pl.l_red = off; off += red;
+    pl.l_stat = off; off += 4 * kNW;
+    pl.lds_floats = off;
+    if (pl.lds_floats * 4 > 160 * 1024) return pl;
+    // ---- dW tile groups
+    int slot = 0;
+    for (int g = 0; g < pl.ne + 3; ++g) {
+        int fo = 0, fi = 0;
+        if (g < pl.ne) { fo = pl.eout[g]; fi = pl.ein[g]; }
+        else if (g == pl.ne) { fo = pl.H; fi = pl.lat; }
+        else if (g == pl.ne + 1) { fo = 16; fi = pl.ha + 1; }   // + bias column
+        else { fo = 16; fi = pl.hc + 1; }
+        pl.ncol[g] = (fi + 15) / 16;
+        pl.nt[g] = (fo / 16) * pl.ncol[g];
+        pl.slot0[g] = slot;
+        pl.nslot[g] = (pl.nt[g] + kNW - 1) / kNW;
+        slot += pl.nslot[g];
+    }
+    pl.nslots = slot;
+    if (slot > kMaxSlot) return pl;
+    // ---- flat <-> LDS blocks
+    int nb = 0;
+    auto blk = [&](int f0, int len, int rowlen, int l0, int ldst) {
+        if (len > 0) pl.blk[nb++] = Blk{f0, len, rowlen, l0, ldst};
+    };
+    for (int e = 0; e < pl.ne; ++e) {
+        const int fo = pl.eout[e], fi = pl.ein[e];
+        blk(pl.f_ew[e], fo * fi, fi, pl.l_ew[e], pl.l_eld[e]);
+        blk(pl.f_eb[e], fo, fo, pl.l_eb[e], fo);
+        if (pl.eaff[e]) {
+            blk(pl.f_eg[e], fo, fo, pl.l_eg[e], fo);
+            blk(pl.f_ebe[e], fo, fo, pl.l_ebe[e], fo);
+        }
+    }
+    blk(pl.f_aw, pl.ha * pl.lat, pl.lat, pl.l_hw, pl.l_hld);
+    blk(pl.f_ab, pl.ha, pl.ha, pl.l_hb, pl.ha);
+    blk(pl.f_ag, pl.ha, pl.ha, pl.l_hg, pl.ha);
+    blk(pl.f_abe, pl.ha, pl.ha, pl.l_hbe, pl.ha);
+    blk(pl.f_aow, pl.A * pl.ha, pl.ha, pl.l_aow, pl.l_aold);
+    blk(pl.f_aob, pl.A, pl.A, pl.l_aob, pl.A);
+    blk(pl.f_cw, pl.hc * pl.lat, pl.lat, pl.l_hw + pl.ha * pl.l_hld, pl.l_hld);
+    blk(pl.f_cb, pl.hc, pl.hc, pl.l_hb + pl.ha, pl.hc);
+    blk(pl.f_cg, pl.hc, pl.hc, pl.l_hg + pl.ha, pl.hc);
+    blk(pl.f_cbe, pl.hc, pl.hc, pl.l_hbe + pl.ha, pl.hc);
+    blk(pl.f_cow, pl.hc, pl.hc, pl.l_cow, pl.l_cold);
+    blk(pl.f_cob, 1, 1, pl.l_cob, 1);
+    pl.nblk = nb;
+    pl.ok = 1;
+    return pl;
+}
+
+// ---------------------------------------------------------------------------
+// instantiated shapes: (obs_dim, actions, encoder widths..., head_actor, head_critic)
+// ---------------------------------------------------------------------------
+#define AGX_PPO_SHAPES(X)                 \
+    X(8, 4, 2, 64, 64, 0, 64, 64)  /* LunarLander config 2 (ppo.yaml) */ \
+    X(4, 2, 2, 64, 64, 0, 64, 64)  /* CartPole */                        \
+    X(6, 3, 2, 64, 64, 0, 64, 64)  /* Acrobot */
+
+template <int D_, int A_, int NE_, int E0, int E1, int E2, int HA, int HC>
+struct Shape {
+    static constexpr NetDims dims{D_, A_, NE_, {E0, E1, E2}, HA, HC};
+    static constexpr LearnPlan plan = make_plan(dims);
 };
 
-struct LearnArgs {
-    const LearnPlan *plan;  // device copy (workspace), read through scalar loads
-    const VecDesc *vec;
-    float *params, *m, *v;
-    const float *lr;
-    float b1, b2, eps;
-    long long step0;
-    const float *obs;
-    const long long *act;
-    const float *old_logp, *adv, *ret, *old_v;
-    long long S;
-    const long long *perms;
-    int E, B, P;
-    float clip, vf, ent, max_norm;
-    float *loss_out;
-};
+// ---------------------------------------------------------------------------
+// cross-lane helpers
+// ---------------------------------------------------------------------------
+template <int C>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), C, 0xf, 0xf, true));
+}
+// sum / max over the 16 lanes of a DPP row; result in every lane of the row
+__device__ __forceinline__ float row_sum(float v) {
+    v += dpp<0xb1>(v);   // quad_perm [1,0,3,2]
+    v += dpp<0x4e>(v);   // quad_perm [2,3,0,1]
+    v += dpp<0x141>(v);  // row_half_mirror
+    v += dpp<0x140>(v);  // row_mirror
+    return v;
+}
+__device__ __forceinline__ float row_max(float v) {
+    v = fmaxf(v, dpp<0xb1>(v));
+    v = fmaxf(v, dpp<0x4e>(v));
+    v = fmaxf(v, dpp<0x141>(v));
+    v = fmaxf(v, dpp<0x140>(v));
+    return v;
+}
+// sum over the 4 row-groups (lanes l, l^16, l^32, l^48) of a wave
+__device__ __forceinline__ float rowgroup_sum(float v) {
+    // ds_swizzle bit mode (offset[15] = 0): and_mask 0x1f, xor_mask 0x10 -> lane ^ 16
+    v += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401f));
+    // lane ^ 32 through the LDS crossbar (v_permlane32_swap's second result is
+    // mis-allocated by this toolchain's builtin lowering: both results land in
+    // one register)
+    const int l = (int)(threadIdx.x & 63);
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((l ^ 32) << 2, __builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+// Lane / wave ids re-derived through an opaque asm at the start of each phase:
+// otherwise LICM hoists every lane-dependent LDS address of the whole
+// learner out of the epoch/minibatch loops and they all stay live (spills).
+__device__ __forceinline__ int vlane() {
+    int v = (int)threadIdx.x;
+    asm volatile("" : "+v"(v));
+    return v & 63;
+}
+__device__ __forceinline__ int vtid() {
+    int v = (int)threadIdx.x;
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ int swave() {
+    int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    asm volatile("" : "+s"(w));
+    return w;
+}
+#define AGX_IDS                                             \
+    const int lane = vlane(), wave = swave();               \
+    const int lr16 = lane & 15, lq = lane >> 4;             \
+    const int rrow = wave * 4 + lq, sub = lr16;             \
+    (void)lr16, (void)lq, (void)rrow, (void)sub, (void)lane
+
+// workgroup-uniform sum (fixed order); uses stat[slot*kNW .. +kNW)
+__device__ __forceinline__ float block_sum(float v, float *stat, int slot, int lane, int wave) {
+    v = row_sum(v);
+    const float w = readlane_f(v, 0) + readlane_f(v, 16) + readlane_f(v, 32) + readlane_f(v, 48);
+    if (lane == 0) stat[slot * kNW + wave] = w;
+    __syncthreads();
+    float t = 0.f;
+    for (int i = 0; i < kNW; ++i) t += stat[slot * kNW + i];
+    return t;
+}
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
-// C[16x16] += A[16 x K] B[K x 16]; A(m,k) / B(k,n) fetched by functors
-template <class FA, class FB>
-__device__ __forceinline__ f4 mfma_tile(f4 acc, int K, FA a, FB b) {
-    const int lane = threadIdx.x & 63;
+// C[16x16] += A[16 x K] B[K x 16], K % 16 == 0 (operands batched 4 k-steps
+// at a time so LDS latency overlaps the MFMA chain)
+template <int K, class FA, class FB>
+__device__ __forceinline__ f4 mfma_tile(f4 acc, FA a, FB b) {
+    const int lane = vlane();
     const int r = lane & 15, q = lane >> 4;
-    for (int k0 = 0; k0 < K; k0 += 4) {
-        const float av = a(r, k0 + q);
-        const float bv = b(k0 + q, r);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+#pragma unroll
+    for (int k0 = 0; k0 < K; k0 += 16) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            av[j] = a(r, k0 + 4 * j + q);
+            bv[j] = b(k0 + 4 * j + q, r);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
     }
     return acc;
 }
 
+// flat parameter index -> LDS offset (compile-time block table)
+template <class C>
+__device__ __forceinline__ int flat_to_lds(int f) {
+    constexpr LearnPlan pl = C::plan;
+    int l = 0;
+#pragma unroll
+    for (int b = 0; b < pl.nblk; ++b) {
+        constexpr int dummy = 0;
+        (void)dummy;
+        const Blk k = pl.blk[b];
+        if (f >= k.f0 && f < k.f0 + k.len) {
+            const int i = f - k.f0;
+            l = k.l0 + (i / k.rowlen) * k.ldst + i % k.rowlen;
+        }
+    }
+    return l;
+}
+// LDS offset -> flat index (-1 for padding) and clip group
+template <class C>
+__device__ __forceinline__ int lds_to_flat(int l, int &group) {
+    constexpr LearnPlan pl = C::plan;
+    int f = -1;
+    group = 0;
+#pragma unroll
+    for (int b = 0; b < pl.nblk; ++b) {
+        const Blk k = pl.blk[b];
+        const int rows = k.len / k.rowlen;
+        if (l >= k.l0 && l < k.l0 + rows * k.ldst) {
+            const int i = l - k.l0;
+            const int c = i % k.ldst;
+            if (c < k.rowlen) {
+                f = k.f0 + (i / k.ldst) * k.rowlen + c;
+                group = f >= pl.f_cw ? 1 : 0;
+            }
+        }
+    }
+    return f;
+}
+
+// ---------------------------------------------------------------------------
+// shared forward (X0 in LDS -> y_h in S1, logits in lg, value in val)
+// ---------------------------------------------------------------------------
+template <class C>
+struct Fwd {
+    static constexpr LearnPlan pl = C::plan;
+    float *sm;
+
+    // LayerNorm(+affine)+ReLU of Z (S2, width F; LN groups [0,split), [split,F))
+    // -> xhat to xb (stride ldx), y to S1, rstd to rb[2r + group]
+    template <int F, int split, int xb, int ldx, int rb, int gb, int bb>
+    __device__ __forceinline__ void ln_rows() {
+        constexpr int NC = F / 16;
+        constexpr int F0 = split < F ? split : F, F1 = F - F0;
+        AGX_IDS;
+        const int r = rrow;
+        float z[NC];
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+            z[i] = sm[pl.l_s2 + r * pl.ld_s + sub + 16 * i];
+            if (16 * i < split) s0 += z[i];
+            else s1 += z[i];
+        }
+        const float m0 = row_sum(s0) * (1.f / (float)F0);
+        const float m1 = F1 > 0 ? row_sum(s1) * (1.f / (float)(F1 > 0 ? F1 : 1)) : 0.f;
+        float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+            if (16 * i < split) v0 += (z[i] - m0) * (z[i] - m0);
+            else v1 += (z[i] - m1) * (z[i] - m1);
+        }
+        const float r0 = 1.f / sqrtf(row_sum(v0) / (float)F0 + 1e-5f);
+        const float r1 = F1 > 0 ? 1.f / sqrtf(row_sum(v1) / (float)(F1 > 0 ? F1 : 1) + 1e-5f) : 0.f;
+        if ((lane & 15) == 0) {
+            sm[rb + 2 * r] = r0;
+            sm[rb + 2 * r + 1] = r1;
+        }
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+            const int j = sub + 16 * i;
+            const float xh = 16 * i < split ? (z[i] - m0) * r0 : (z[i] - m1) * r1;
+            sm[xb + r * ldx + j] = xh;
+            sm[pl.l_s1 + r * pl.ld_s + j] = gb >= 0 ? relu(xh * sm[gb + j] + sm[bb + j]) : relu(xh);
+        }
+    }
+
+    // Z[SB x fout] = X W^T + b  -> S2
+    template <int xb, int ldx, int K, int wb, int ldw, int bias, int fout>
+    __device__ __forceinline__ void gemm_fwd() {
+        constexpr int nt = (kSB / 16) * (fout / 16);
+        AGX_IDS;
+        for (int t = wave; t < nt; t += kNW) {
+            const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
+            f4 c = f4{0.f, 0.f, 0.f, 0.f};
+            c = mfma_tile<K>(c, [&](int m, int k) { return sm[xb + (m0 + m) * ldx + k]; },
+                             [&](int k, int n) { return sm[wb + (n0 + n) * ldw + k]; });
+            const float bv = sm[bias + n0 + lr16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sm[pl.l_s2 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i] + bv;
+        }
+    }
+
+    template <int L>
+    __device__ __forceinline__ void enc_layer() {
+        constexpr int K = rup(pl.ein[L], 16);
+        gemm_fwd<L == 0 ? pl.l_x0 : pl.l_s1, L == 0 ? pl.ld_x0 : pl.ld_s, K, pl.l_ew[L], pl.l_eld[L], pl.l_eb[L],
+                 pl.eout[L]>();
+        __syncthreads();
+        ln_rows<pl.eout[L], pl.eout[L], pl.l_xe[L], pl.ld_xe[L], pl.l_re[L], pl.eaff[L] ? pl.l_eg[L] : -1,
+                pl.l_ebe[L]>();
+        __syncthreads();
+        if constexpr (L + 1 < pl.ne) enc_layer<L + 1>();
+    }
+
+    __device__ __forceinline__ void run() {
+        enc_layer<0>();
+        gemm_fwd<pl.l_s1, pl.ld_s, pl.lat, pl.l_hw, pl.l_hld, pl.l_hb, pl.H>();
+        __syncthreads();
+        ln_rows<pl.H, pl.ha, pl.l_xh, pl.ld_xh, pl.l_rh, pl.l_hg, pl.l_hbe>();
+        __syncthreads();
+        // output layers: 2 row tiles x {actor logits, critic value}
+        AGX_IDS;
+        if (wave < 2) {
+            const int m0 = wave * 16;
+            f4 c = f4{0.f, 0.f, 0.f, 0.f};
+            c = mfma_tile<pl.ha>(c, [&](int m, int k) { return sm[pl.l_s1 + (m0 + m) * pl.ld_s + k]; },
+                                 [&](int k, int n) { return n < pl.A ? sm[pl.l_aow + n * pl.l_aold + k] : 0.f; });
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (lr16 < pl.A) sm[pl.l_lg + (m0 + lq * 4 + i) * kMaxA + lr16] = c[i] + sm[pl.l_aob + lr16];
+        } else if (wave < 4) {
+            const int m0 = (wave - 2) * 16;
+            f4 c = f4{0.f, 0.f, 0.f, 0.f};
+            c = mfma_tile<pl.hc>(c, [&](int m, int k) { return sm[pl.l_s1 + (m0 + m) * pl.ld_s + pl.ha + k]; },
+                                 [&](int k, int n) { return n == 0 ? sm[pl.l_cow + k] : 0.f; });
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (lr16 == 0) sm[pl.l_val + m0 + lq * 4 + i] = c[i] + sm[pl.l_cob];
+        }
+        __syncthreads();
+    }
+};
+
+template <class C>
+__device__ void load_params(float *sm, const float *gp, int tid) {
+    constexpr LearnPlan pl = C::plan;
+    for (int f = tid; f < pl.n; f += kNT) sm[flat_to_lds<C>(f)] = gp[f];
+}
+
+struct LearnArgs {
+    float *params, *m, *v;
+    const float *lr;
+    float b1, b2, eps;
+    long long step0;
+    const float *gobs;  // [E][P][S][D] minibatch-ordered
+    const int *gact;    // [E][P][S]
+    const float *grow;  // [E][P][4][S]: old_logp, adv_norm, ret, old_v
+    long long S;
+    int E, B, P;
+    float clip, vf, ent, max_norm;
+    float *loss_out;
+    long long *stamps;
+};
+
+#define AGX_STAMP(slot)                                                          \
+    do {                                                                         \
+        if (g.stamps && p == 0 && e == 0 && mb == 0 && tid == 0 && (slot) < 80) \
+            g.stamps[(slot)] = (long long)__builtin_readcyclecounter(); \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// learner
+// ---------------------------------------------------------------------------
+template <class C>
 __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const LearnPlan &pl = *g.plan;
+    constexpr LearnPlan pl = C::plan;
     const int p = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int lr16 = lane & 15, lq = lane >> 4;
+    const int tid = threadIdx.x;
     float *gp = g.params + (size_t)p * pl.n;
     float *gm = g.m + (size_t)p * pl.n;
     float *gv = g.v + (size_t)p * pl.n;
     const long long S = g.S;
+    Fwd<C> fw{sm};
 
-    // ---------------- load parameters into LDS (zero padding) -------------
     for (int i = tid; i < pl.lds_floats; i += kNT) sm[i] = 0.f;
     __syncthreads();
-    for (int e = 0; e < pl.ne; ++e) {
-        const int fin = pl.ein[e], fout = pl.eout[e];
-        for (int i = tid; i < fin * fout; i += kNT) sm[pl.l_ew[e] + (i / fin) * pl.l_eld[e] + i % fin] = gp[pl.ew[e] + i];
-        for (int i = tid; i < fout; i += kNT) {
-            sm[pl.l_eb[e] + i] = gp[pl.eb[e] + i];
-            if (pl.eg[e] >= 0) {
-                sm[pl.l_eg[e] + i] = gp[pl.eg[e] + i];
-                sm[pl.l_ebe[e] + i] = gp[pl.ebe[e] + i];
-            }
-        }
-    }
-    for (int i = tid; i < pl.lat * pl.H; i += kNT) {
-        const int o = i / pl.lat, c = i % pl.lat;
-        const float w = o < pl.ha ? gp[pl.aw + o * pl.lat + c] : gp[pl.cw + (o - pl.ha) * pl.lat + c];
-        sm[pl.l_hw + o * pl.l_hld + c] = w;
-    }
-    for (int o = tid; o < pl.H; o += kNT) {
-        const bool a = o < pl.ha;
-        const int oo = a ? o : o - pl.ha;
-        sm[pl.l_hb + o] = gp[(a ? pl.ab : pl.cb) + oo];
-        sm[pl.l_hg + o] = gp[(a ? pl.ag : pl.cg) + oo];
-        sm[pl.l_hbe + o] = gp[(a ? pl.abe : pl.cbe) + oo];
-    }
-    for (int i = tid; i < pl.A * pl.ha; i += kNT) sm[pl.l_aow + i] = gp[pl.aow + i];
-    for (int i = tid; i < pl.A; i += kNT) sm[pl.l_aob + i] = gp[pl.aob + i];
-    for (int i = tid; i < pl.hc; i += kNT) sm[pl.l_cow + i] = gp[pl.cow + i];
-    if (tid == 0) sm[pl.l_cob] = gp[pl.cob];
-
-    // ---------------- ownership: dW tiles (MFMA accumulators) --------------
-    // tile (layer, o0, i0) packed as (L+1) << 16 | o0/16 << 8 | i0/16; 0 = none
-    int tpk[kMaxSlot];
+    load_params<C>(sm, gp, tid);
+    // Adam moments of the owned LDS parameter slots -> registers; group bits
+    float am[kMaxPT], av[kMaxPT];
+    unsigned gbits = 0, vbits = 0;
 #pragma unroll
-    for (int s = 0; s < kMaxSlot; ++s) {
-        const int t = wave + kNW * s;
-        tpk[s] = 0;
-        if (t < pl.ntiles) {
-            int L = 0;
-            while (L < pl.ne && t >= pl.tile_begin[L + 1]) ++L;
-            const int local = t - pl.tile_begin[L];
-            const int fin = L < pl.ne ? pl.ein[L] : pl.lat;
-            const int ncol = (fin + 15) / 16;
-            tpk[s] = ((L + 1) << 16) | ((local / ncol) << 8) | (local % ncol);  // L == ne: merged head
-        }
+    for (int i = 0; i < kMaxPT; ++i) {
+        const int l = tid + kNT * i;
+        int grp = 0;
+        const int f = l < pl.param_end ? lds_to_flat<C>(l, grp) : -1;
+        am[i] = f >= 0 ? gm[f] : 0.f;
+        av[i] = f >= 0 ? gv[f] : 0.f;
+        if (f >= 0) vbits |= 1u << i;
+        if (grp) gbits |= 1u << i;
     }
-#define T_LAYER(s) ((tpk[s] >> 16) - 1)
-#define T_O0(s) (((tpk[s] >> 8) & 255) * 16)
-#define T_I0(s) ((tpk[s] & 255) * 16)
+    // keep the ownership bits as plain VGPR data: left transparent, the compiler
+    // re-materialises them as 60 live SGPR-pair lane masks (SGPR spills)
+    asm volatile("" : "+v"(vbits), "+v"(gbits));
     __syncthreads();
 
+    constexpr int nmb_dummy = 0;
+    (void)nmb_dummy;
     const int nmb = (int)((S + g.B - 1) / g.B);
     float loss_total = 0.f;
     long long step = g.step0;
-    float *rowf = sm + pl.l_row;  // [5][SB]: act (bits), old_logp, adv, ret, old_v
-    int *rowi = reinterpret_cast<int *>(rowf);
+    float *rowf = sm + pl.l_row;  // [4][SB]: old_logp, adv, ret, old_v
+    float *stat = sm + pl.l_stat;
+    int *acts = reinterpret_cast<int *>(sm + pl.l_row + 4 * kSB);
 
     for (int e = 0; e < g.E; ++e) {
-        const long long *perm = g.perms + ((size_t)e * g.P + p) * S;
+        const float *eobs = g.gobs + ((size_t)e * g.P + p) * S * pl.D;
+        const int *eact = g.gact + ((size_t)e * g.P + p) * S;
+        const float *erow = g.grow + ((size_t)e * g.P + p) * 4 * S;
         for (int mb = 0; mb < nmb; ++mb) {
             const long long s0 = (long long)mb * g.B;
             const int bsz = (int)((s0 + g.B <= S) ? g.B : S - s0);
             const float inv_b = 1.f / (float)bsz;
+            const int tid = vtid();
             f4 acc[kMaxSlot];
 #pragma unroll
             for (int s = 0; s < kMaxSlot; ++s) acc[s] = f4{0.f, 0.f, 0.f, 0.f};
-            float vacc[kVecSlot] = {0.f, 0.f, 0.f, 0.f};
-            float lsum = 0.f;  // per-thread loss partial (row threads)
+            for (int i = tid; i < pl.l_stat - pl.l_red; i += kNT) sm[pl.l_red + i] = 0.f;
+            float lsum = 0.f;
 
             for (int sb = 0; sb < bsz; sb += kSB) {
                 const int nrow = bsz - sb < kSB ? bsz - sb : kSB;
-                // ---- P0: gather rows ------------------------------------------
-                for (int i = tid; i < kSB * pl.ld_x0; i += kNT) sm[pl.l_x0 + i] = 0.f;
-                __syncthreads();
-                for (int i = tid; i < kSB * pl.D; i += kNT) {
-                    const int r = i / pl.D, d = i % pl.D;
-                    if (r < nrow) {
-                        const long long src = perm[s0 + sb + r];
-                        sm[pl.l_x0 + r * pl.ld_x0 + d] = g.obs[((size_t)p * S + src) * pl.D + d];
-                    }
+                const int stb = sb < 4 * kSB ? (sb / kSB) * 16 : 80;
+                const int tid = vtid();
+                AGX_STAMP(stb + 0);
+                // ---- P0: contiguous gather of the sub-batch -------------------
+                // (padding columns rewritten too: the gradient image aliases them)
+                for (int i = tid; i < kSB * pl.ld_x0; i += kNT) {
+                    const int r = i / pl.ld_x0, dd = i % pl.ld_x0;
+                    sm[pl.l_x0 + i] = (r < nrow && dd < pl.D) ? eobs[(s0 + sb + r) * pl.D + dd] : 0.f;
                 }
-                if (tid < kSB) {
-                    const int r = tid;
-                    if (r < nrow) {
-                        const long long src = (size_t)p * S + perm[s0 + sb + r];
-                        rowi[r] = (int)g.act[src];
-                        rowf[kSB + r] = g.old_logp[src];
-                        rowf[2 * kSB + r] = g.adv[src];
-                        rowf[3 * kSB + r] = g.ret[src];
-                        rowf[4 * kSB + r] = g.old_v[src];
-                    } else {
-                        rowi[r] = 0;
-                        rowf[kSB + r] = rowf[2 * kSB + r] = rowf[3 * kSB + r] = rowf[4 * kSB + r] = 0.f;
-                    }
+                if (tid < 4 * kSB) {
+                    const int k = tid / kSB, r = tid % kSB;
+                    rowf[k * kSB + r] = r < nrow ? erow[(size_t)k * S + s0 + sb + r] : 0.f;
+                } else if (tid < 5 * kSB) {
+                    const int r = tid - 4 * kSB;
+                    acts[r] = r < nrow ? eact[s0 + sb + r] : 0;
                 }
                 __syncthreads();
+                AGX_STAMP(stb + 1);
 
-                // ---- P1: encoder forward ----------------------------------------
-                for (int L = 0; L < pl.ne; ++L) {
-                    const int fin = pl.ein[L], fout = pl.eout[L];
-                    const int K = (fin + 3) & ~3;
-                    const int xb = L == 0 ? pl.l_x0 : pl.l_s1;
-                    const int ldx = L == 0 ? pl.ld_x0 : pl.ld_s;
-                    const int wb = pl.l_ew[L], ldw = pl.l_eld[L];
-                    const int nt = (kSB / 16) * (fout / 16);
+                // ---- P1-P3: forward ------------------------------------------
+                fw.run();
+                AGX_STAMP(stb + 2);
+
+                // ---- P4: loss + d(logits), d(value); 16 lanes per row ------------
+                {
+                    AGX_IDS;
+                    const int r = rrow, a = sub;
+                    const bool live = r < nrow;
+                    const float lg = a < pl.A ? sm[pl.l_lg + r * kMaxA + a] : -3.0e38f;
+                    const float mx = row_max(lg);
+                    const float ex = a < pl.A ? expf(lg - mx) : 0.f;
+                    const float lse = mx + logf(row_sum(ex));
+                    const float pa = a < pl.A ? expf(lg - lse) : 0.f;
+                    const float lpe = logf(pa + 1e-8f);
+                    const float Hs = -row_sum(a < pl.A ? pa * lpe : 0.f);  // H = -sum p log(p+1e-8)
+                    const float gh = -(lpe + pa / (pa + 1e-8f));            // dH/dp_a
+                    const float pg_dot = row_sum(a < pl.A ? pa * gh : 0.f);
+                    const int a_t = acts[r];
+                    const float logp = __builtin_bit_cast(
+                                           float, __builtin_amdgcn_ds_bpermute((lane - sub + a_t) * 4,
+                                                                               __builtin_bit_cast(int, lg))) -
+                                       lse;
+                    const float olp = rowf[r], A = rowf[kSB + r], R = rowf[2 * kSB + r], ov = rowf[3 * kSB + r];
+                    const float v = sm[pl.l_val + r];
+                    const float lo = 1.f - g.clip, hi = 1.f + g.clip;
+                    const float lrt = logp - olp;
+                    const float ratio = expf(lrt);
+                    const float rcl = fminf(fmaxf(ratio, lo), hi);
+                    const float p1 = -A * ratio, p2 = -A * rcl;
+                    const float g1 = p1 > p2 ? 1.f : (p1 == p2 ? 0.5f : 0.f);
+                    const float g2 = p2 > p1 ? 1.f : (p1 == p2 ? 0.5f : 0.f);
+                    const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+                    const float g_logp = ((g1 * -A + g2 * -A * inr) * inv_b) * ratio;
+                    const float dv = v - ov;
+                    const float vcl = ov + fminf(fmaxf(dv, -g.clip), g.clip);
+                    const float eu = v - R, ec = vcl - R;
+                    const float lu = eu * eu, lc = ec * ec;
+                    const float gu = lu > lc ? 1.f : (lu == lc ? 0.5f : 0.f);
+                    const float gc = lc > lu ? 1.f : (lu == lc ? 0.5f : 0.f);
+                    const float inv = (dv >= -g.clip && dv <= g.clip) ? 1.f : 0.f;
+                    const float g_H = -g.ent * inv_b;
+                    const float dl = g_logp * ((a == a_t ? 1.f : 0.f) - pa) + g_H * pa * (gh - pg_dot);
+                    if (a < pl.A) sm[pl.l_dlg + r * kMaxA + a] = live ? dl : 0.f;
+                    if (a == 0) {
+                        sm[pl.l_dvb + r * kMaxA] =
+                            live ? g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv) : 0.f;
+                        if (live) lsum += (fmaxf(p1, p2) + g.vf * 0.5f * fmaxf(lu, lc) - g.ent * Hs) * inv_b;
+                    }
+                }
+                __syncthreads();
+                AGX_STAMP(stb + 3);
+
+                // ---- P5: output-layer dW (bias = ones column); dY_h = dOut . W_out -> S2
+                {
+                    AGX_IDS;
+                    constexpr int ga = pl.ne + 1, gc = pl.ne + 2;
+#pragma unroll
+                    for (int j = 0; j < pl.nslot[ga]; ++j) {
+                        const int t = wave + kNW * j;
+                        if (t < pl.nt[ga]) {
+                            const int i0 = (t % pl.ncol[ga]) * 16;
+                            acc[pl.slot0[ga] + j] = mfma_tile<kSB>(
+                                acc[pl.slot0[ga] + j], [&](int m, int k) { return sm[pl.l_dlg + k * kMaxA + m]; },
+                                [&](int k, int n) {
+                                    const int c = i0 + n;
+                                    return c < pl.ha ? sm[pl.l_s1 + k * pl.ld_s + c] : (c == pl.ha ? 1.f : 0.f);
+                                });
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < pl.nslot[gc]; ++j) {
+                        const int t = wave + kNW * j;
+                        if (t < pl.nt[gc]) {
+                            const int i0 = (t % pl.ncol[gc]) * 16;
+                            acc[pl.slot0[gc] + j] = mfma_tile<kSB>(
+                                acc[pl.slot0[gc] + j], [&](int m, int k) { return sm[pl.l_dvb + k * kMaxA + m]; },
+                                [&](int k, int n) {
+                                    const int c = i0 + n;
+                                    return c < pl.hc ? sm[pl.l_s1 + k * pl.ld_s + pl.ha + c] : (c == pl.hc ? 1.f : 0.f);
+                                });
+                        }
+                    }
+                    constexpr int nt = (kSB / 16) * (pl.H / 16);
                     for (int t = wave; t < nt; t += kNW) {
                         const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
                         f4 c = f4{0.f, 0.f, 0.f, 0.f};
-                        c = mfma_tile(c, K, [&](int m, int k) { return sm[xb + (m0 + m) * ldx + k]; },
-                                      [&](int k, int n) { return sm[wb + (n0 + n) * ldw + k]; });
-                        const float bias = sm[pl.l_eb[L] + n0 + lr16];
+                        if (n0 < pl.ha) {
+                            c = mfma_tile<16>(c, [&](int m, int k) { return sm[pl.l_dlg + (m0 + m) * kMaxA + k]; },
+                                              [&](int k, int n) {
+                                                  return k < pl.A ? sm[pl.l_aow + k * pl.l_aold + n0 + n] : 0.f;
+                                              });
+                        } else {
+                            c = mfma_tile<16>(c, [&](int m, int k) { return sm[pl.l_dvb + (m0 + m) * kMaxA + k]; },
+                                              [&](int k, int n) {
+                                                  return k == 0 ? sm[pl.l_cow + n0 - pl.ha + n] : 0.f;
+                                              });
+                        }
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) sm[pl.l_s2 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i] + bias;
+                        for (int i = 0; i < 4; ++i) sm[pl.l_s2 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i];
                     }
-                    __syncthreads();
-                    // LayerNorm + ReLU row pass: wave handles rows wave*4 .. +3
-                    const bool affine = pl.eg[L] >= 0;
-                    for (int rr = 0; rr < kSB / kNW; ++rr) {
-                        const int r = wave * (kSB / kNW) + rr;
-                        float z0 = lane < fout ? sm[pl.l_s2 + r * pl.ld_s + lane] : 0.f;
-                        float z1 = lane + 64 < fout ? sm[pl.l_s2 + r * pl.ld_s + lane + 64] : 0.f;
-                        const float mean = wave_sum(z0 + z1) / (float)fout;
-                        const float d0 = lane < fout ? z0 - mean : 0.f;
-                        const float d1 = lane + 64 < fout ? z1 - mean : 0.f;
-                        const float var = wave_sum(d0 * d0 + d1 * d1) / (float)fout;
-                        const float rstd = 1.f / sqrtf(var + 1e-5f);
-                        if (lane == 0) sm[pl.l_re[L] + r] = rstd;
+                }
+                __syncthreads();
+                AGX_STAMP(stb + 4);
+
+                // backward row pass through LN(+affine)+ReLU: S2 (dY) -> S2 (dZ)
+                auto ln_bwd = [&](auto Fc, auto splitc, auto xbc, auto ldxc, auto rbc, auto gbc, auto bbc, auto redc,
+                                  auto affc) {
+                    constexpr int F = decltype(Fc)::value, split = decltype(splitc)::value;
+                    constexpr int xb = decltype(xbc)::value, ldx = decltype(ldxc)::value;
+                    constexpr int rb = decltype(rbc)::value, gb = decltype(gbc)::value, bb = decltype(bbc)::value;
+                    constexpr int red = decltype(redc)::value;
+                    constexpr bool aff = decltype(affc)::value;
+                    constexpr int NC = F / 16;
+                    constexpr int F0 = split < F ? split : F, F1 = F - F0;
+                    AGX_IDS;
+                    const int r = rrow;
+                    float xh[NC], dxh[NC], dyp[NC];
+                    float a1 = 0.f, a2 = 0.f, c1 = 0.f, c2 = 0.f;
+                    const float rs0 = sm[rb + 2 * r], rs1 = sm[rb + 2 * r + 1];
 #pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const int j = lane + 64 * h;
-                            if (j < fout) {
-                                const float xh = (h ? d1 : d0) * rstd;
-                                sm[pl.l_xe[L] + r * pl.ld_xe[L] + j] = xh;
-                                const float y = affine ? relu(xh * sm[pl.l_eg[L] + j] + sm[pl.l_ebe[L] + j]) : relu(xh);
-                                sm[pl.l_s1 + r * pl.ld_s + j] = y;
+                    for (int i = 0; i < NC; ++i) {
+                        const int j = sub + 16 * i;
+                        const float dy = sm[pl.l_s2 + r * pl.ld_s + j];
+                        xh[i] = sm[xb + r * ldx + j];
+                        const float gam = aff ? sm[gb + j] : 1.f;
+                        const float y = aff ? xh[i] * gam + sm[bb + j] : xh[i];
+                        dyp[i] = y > 0.f ? dy : 0.f;
+                        dxh[i] = dyp[i] * gam;
+                        if (16 * i < split) {
+                            a1 += dxh[i];
+                            a2 += dxh[i] * xh[i];
+                        } else {
+                            c1 += dxh[i];
+                            c2 += dxh[i] * xh[i];
+                        }
+                    }
+                    const float ma1 = row_sum(a1) * (1.f / (float)F0), ma2 = row_sum(a2) * (1.f / (float)F0);
+                    const float mc1 = F1 > 0 ? row_sum(c1) * (1.f / (float)(F1 > 0 ? F1 : 1)) : 0.f;
+                    const float mc2 = F1 > 0 ? row_sum(c2) * (1.f / (float)(F1 > 0 ? F1 : 1)) : 0.f;
+                    float *rd = sm + pl.l_red + red;
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) {
+                        const int j = sub + 16 * i;
+                        const bool g0 = 16 * i < split;
+                        const float dz = (g0 ? rs0 : rs1) * (dxh[i] - (g0 ? ma1 : mc1) - xh[i] * (g0 ? ma2 : mc2));
+                        sm[pl.l_s2 + r * pl.ld_s + j] = dz;
+                        const float sdz = rowgroup_sum(dz);
+                        if (lane < 16) rd[(0 * kNW + wave) * F + j] += sdz;
+                        if (aff) {
+                            const float sg = rowgroup_sum(dyp[i] * xh[i]);
+                            const float sbt = rowgroup_sum(dyp[i]);
+                            if (lane < 16) {
+                                rd[(1 * kNW + wave) * F + j] += sg;
+                                rd[(2 * kNW + wave) * F + j] += sbt;
                             }
                         }
                     }
-                    __syncthreads();
-                }
+                };
+#define IC(x) std::integral_constant<int, (x)>()
+#define BC(x) std::integral_constant<bool, (x)>()
 
-                // ---- P2: merged head forward --------------------------------------
+                // ---- P6: head LN backward (dY_h in S2 -> dZ_h in S2) ----------
+                ln_bwd(IC(pl.H), IC(pl.ha), IC(pl.l_xh), IC(pl.ld_xh), IC(pl.l_rh), IC(pl.l_hg), IC(pl.l_hbe),
+                       IC(pl.red_h), BC(true));
+                __syncthreads();
+                AGX_STAMP(stb + 5);
+
+                // ---- P7: head dW += dZ^T latent; d(latent) = dZ . W_h -> S1 --------
                 {
-                    const int nt = (kSB / 16) * (pl.H / 16);
+                    AGX_IDS;
+                    constexpr int gh = pl.ne, Le = pl.ne - 1;
+#pragma unroll
+                    for (int j = 0; j < pl.nslot[gh]; ++j) {
+                        const int t = wave + kNW * j;
+                        if (t < pl.nt[gh]) {
+                            const int o0 = (t / pl.ncol[gh]) * 16, i0 = (t % pl.ncol[gh]) * 16;
+                            acc[pl.slot0[gh] + j] = mfma_tile<kSB>(
+                                acc[pl.slot0[gh] + j], [&](int m, int k) { return sm[pl.l_s2 + k * pl.ld_s + o0 + m]; },
+                                [&](int k, int n) { return relu(sm[pl.l_xe[Le] + k * pl.ld_xe[Le] + i0 + n]); });
+                        }
+                    }
+                    constexpr int nt = (kSB / 16) * (pl.lat / 16);
                     for (int t = wave; t < nt; t += kNW) {
                         const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
                         f4 c = f4{0.f, 0.f, 0.f, 0.f};
-                        c = mfma_tile(c, pl.lat, [&](int m, int k) { return sm[pl.l_s1 + (m0 + m) * pl.ld_s + k]; },
-                                      [&](int k, int n) { return sm[pl.l_hw + (n0 + n) * pl.l_hld + k]; });
-                        const float bias = sm[pl.l_hb + n0 + lr16];
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) sm[pl.l_s2 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i] + bias;
-                    }
-                    __syncthreads();
-                    for (int rr = 0; rr < kSB / kNW; ++rr) {
-                        const int r = wave * (kSB / kNW) + rr;
-                        float z[4], sa = 0.f, sc = 0.f;
-#pragma unroll
-                        for (int h = 0; h < 4; ++h) {
-                            const int j = lane + 64 * h;
-                            z[h] = j < pl.H ? sm[pl.l_s2 + r * pl.ld_s + j] : 0.f;
-                            if (j < pl.ha) sa += z[h];
-                            else if (j < pl.H) sc += z[h];
-                        }
-                        const float ma = wave_sum(sa) / (float)pl.ha, mc = wave_sum(sc) / (float)pl.hc;
-                        float va = 0.f, vc = 0.f;
-#pragma unroll
-                        for (int h = 0; h < 4; ++h) {
-                            const int j = lane + 64 * h;
-                            if (j < pl.ha) va += (z[h] - ma) * (z[h] - ma);
-                            else if (j < pl.H) vc += (z[h] - mc) * (z[h] - mc);
-                        }
-                        const float ra = 1.f / sqrtf(wave_sum(va) / (float)pl.ha + 1e-5f);
-                        const float rc = 1.f / sqrtf(wave_sum(vc) / (float)pl.hc + 1e-5f);
-                        if (lane == 0) {
-                            sm[pl.l_rh + 2 * r] = ra;
-                            sm[pl.l_rh + 2 * r + 1] = rc;
-                        }
-#pragma unroll
-                        for (int h = 0; h < 4; ++h) {
-                            const int j = lane + 64 * h;
-                            if (j < pl.H) {
-                                const float xh = j < pl.ha ? (z[h] - ma) * ra : (z[h] - mc) * rc;
-                                sm[pl.l_xh + r * pl.ld_xh + j] = xh;
-                                sm[pl.l_s1 + r * pl.ld_s + j] = relu(xh * sm[pl.l_hg + j] + sm[pl.l_hbe + j]);
-                            }
-                        }
-                    }
-                    __syncthreads();
-                }
-
-                // ---- P3: output layers (VALU dots) ---------------------------------
-                for (int idx = tid; idx < kSB * (pl.A + 1); idx += kNT) {
-                    const int r = idx % kSB, j = idx / kSB;
-                    const float *y = sm + pl.l_s1 + r * pl.ld_s;
-                    float s;
-                    if (j < pl.A) {
-                        s = sm[pl.l_aob + j];
-                        const float *w = sm + pl.l_aow + j * pl.ha;
-                        for (int o = 0; o < pl.ha; ++o) s += y[o] * w[o];
-                        sm[pl.l_lg + r * kMaxA + j] = s;
-                    } else {
-                        s = sm[pl.l_cob];
-                        const float *w = sm + pl.l_cow;
-                        for (int o = 0; o < pl.hc; ++o) s += y[pl.ha + o] * w[o];
-                        sm[pl.l_val + r] = s;
-                    }
-                }
-                __syncthreads();
-
-                // ---- P4: loss + d(logits), d(value) per row ------------------------
-                if (tid < kSB) {
-                    const int r = tid;
-                    float *dl = sm + pl.l_dlg + r * kMaxA;
-                    if (r < nrow) {
-                        const float *lg = sm + pl.l_lg + r * kMaxA;
-                        float mx = lg[0];
-                        for (int a = 1; a < pl.A; ++a) mx = fmaxf(mx, lg[a]);
-                        float se = 0.f;
-                        for (int a = 0; a < pl.A; ++a) se += expf(lg[a] - mx);
-                        const float lse = mx + logf(se);
-                        const int a_t = rowi[r];
-                        const float logp = lg[a_t] - lse;
-                        // entropy H = -sum p log(p + 1e-8)  (torch_utils.py:188-199)
-                        float Hs = 0.f, pg_dot = 0.f;
-                        for (int a = 0; a < pl.A; ++a) {
-                            const float pa = expf(lg[a] - lse);
-                            const float lpe = logf(pa + 1e-8f);
-                            Hs -= pa * lpe;
-                            pg_dot += pa * -(lpe + pa / (pa + 1e-8f));  // sum_a p_a dH/dp_a
-                        }
-                        const float olp = rowf[kSB + r], A = rowf[2 * kSB + r], R = rowf[3 * kSB + r];
-                        const float ov = rowf[4 * kSB + r], v = sm[pl.l_val + r];
-                        const float lo = 1.f - g.clip, hi = 1.f + g.clip;
-                        const float lrt = logp - olp;
-                        const float ratio = expf(lrt);
-                        const float rcl = fminf(fmaxf(ratio, lo), hi);
-                        const float p1 = -A * ratio, p2 = -A * rcl;
-                        const float g1 = p1 > p2 ? 1.f : (p1 == p2 ? 0.5f : 0.f);
-                        const float g2 = p2 > p1 ? 1.f : (p1 == p2 ? 0.5f : 0.f);
-                        const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
-                        const float g_logp = ((g1 * -A + g2 * -A * inr) * inv_b) * ratio;
-                        const float dv = v - ov;
-                        const float vcl = ov + fminf(fmaxf(dv, -g.clip), g.clip);
-                        const float eu = v - R, ec = vcl - R;
-                        const float lu = eu * eu, lc = ec * ec;
-                        const float gu = lu > lc ? 1.f : (lu == lc ? 0.5f : 0.f);
-                        const float gc = lc > lu ? 1.f : (lu == lc ? 0.5f : 0.f);
-                        const float inv = (dv >= -g.clip && dv <= g.clip) ? 1.f : 0.f;
-                        sm[pl.l_dval + r] = g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv);
-                        const float g_H = -g.ent * inv_b;
-                        for (int a = 0; a < pl.A; ++a) {
-                            const float pa = expf(lg[a] - lse);
-                            const float gh = -(logf(pa + 1e-8f) + pa / (pa + 1e-8f));  // dH/dp_a
-                            dl[a] = g_logp * ((a == a_t ? 1.f : 0.f) - pa) + g_H * pa * (gh - pg_dot);
-                        }
-                        lsum += (fmaxf(p1, p2) + g.vf * 0.5f * fmaxf(lu, lc) - g.ent * Hs) * inv_b;
-                    } else {
-                        for (int a = 0; a < pl.A; ++a) dl[a] = 0.f;
-                        sm[pl.l_dval + r] = 0.f;
-                    }
-                }
-                __syncthreads();
-
-                // ---- P5: head hidden backward row pass -----------------------------
-                {
-                    float pb[4] = {0.f, 0.f, 0.f, 0.f}, pgm[4] = {0.f, 0.f, 0.f, 0.f}, pbe[4] = {0.f, 0.f, 0.f, 0.f};
-                    for (int rr = 0; rr < kSB / kNW; ++rr) {
-                        const int r = wave * (kSB / kNW) + rr;
-                        const float ra = sm[pl.l_rh + 2 * r], rc = sm[pl.l_rh + 2 * r + 1];
-                        float xh[4], dxh[4], dyp[4];
-                        float sa1 = 0.f, sa2 = 0.f, sc1 = 0.f, sc2 = 0.f;
-#pragma unroll
-                        for (int h = 0; h < 4; ++h) {
-                            const int j = lane + 64 * h;
-                            xh[h] = dxh[h] = dyp[h] = 0.f;
-                            if (j < pl.H) {
-                                float dy;
-                                if (j < pl.ha) {
-                                    dy = 0.f;
-                                    for (int a = 0; a < pl.A; ++a) dy += sm[pl.l_dlg + r * kMaxA + a] * sm[pl.l_aow + a * pl.ha + j];
-                                } else {
-                                    dy = sm[pl.l_dval + r] * sm[pl.l_cow + j - pl.ha];
-                                }
-                                xh[h] = sm[pl.l_xh + r * pl.ld_xh + j];
-                                const float gam = sm[pl.l_hg + j];
-                                const float y = xh[h] * gam + sm[pl.l_hbe + j];
-                                dyp[h] = y > 0.f ? dy : 0.f;
-                                dxh[h] = dyp[h] * gam;
-                                if (j < pl.ha) {
-                                    sa1 += dxh[h];
-                                    sa2 += dxh[h] * xh[h];
-                                } else {
-                                    sc1 += dxh[h];
-                                    sc2 += dxh[h] * xh[h];
-                                }
-                            }
-                        }
-                        const float ma1 = wave_sum(sa1) / (float)pl.ha, ma2 = wave_sum(sa2) / (float)pl.ha;
-                        const float mc1 = wave_sum(sc1) / (float)pl.hc, mc2 = wave_sum(sc2) / (float)pl.hc;
-#pragma unroll
-                        for (int h = 0; h < 4; ++h) {
-                            const int j = lane + 64 * h;
-                            if (j < pl.H) {
-                                const bool isa = j < pl.ha;
-                                const float dz = (isa ? ra : rc) * (dxh[h] - (isa ? ma1 : mc1) - xh[h] * (isa ? ma2 : mc2));
-                                sm[pl.l_s2 + r * pl.ld_s + j] = dz;
-                                pb[h] += dz;
-                                pgm[h] += dyp[h] * xh[h];
-                                pbe[h] += dyp[h];
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int h = 0; h < 4; ++h) {
-                        const int j = lane + 64 * h;
-                        if (j < pl.H) {
-                            float *red = sm + pl.l_red + pl.red_h;
-                            red[(0 * kNW + wave) * pl.H + j] = pb[h];
-                            red[(1 * kNW + wave) * pl.H + j] = pgm[h];
-                            red[(2 * kNW + wave) * pl.H + j] = pbe[h];
-                        }
-                    }
-                }
-                __syncthreads();
-
-                // ---- P6: head dW (MFMA acc) and d(latent) = dZ . W_h -> S1 --------
-                {
-                    const int Le = pl.ne - 1;  // latent = relu(xhat of the last encoder layer)
-                    const int xeb = pl.l_xe[Le], ldxe = pl.ld_xe[Le];
-#pragma unroll
-                    for (int s = 0; s < kMaxSlot; ++s) {
-                        if (T_LAYER(s) == pl.ne) {
-                            const int o0 = T_O0(s), i0 = T_I0(s);
-                            acc[s] = mfma_tile(acc[s], kSB,
-                                               [&](int m, int k) { return sm[pl.l_s2 + k * pl.ld_s + o0 + m]; },
-                                               [&](int k, int n) { return relu(sm[xeb + k * ldxe + i0 + n]); });
-                        }
-                    }
-                    const int nt = (kSB / 16) * (pl.lat / 16);
-                    for (int t = wave; t < nt; t += kNW) {
-                        const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
-                        f4 c = f4{0.f, 0.f, 0.f, 0.f};
-                        c = mfma_tile(c, pl.H, [&](int m, int k) { return sm[pl.l_s2 + (m0 + m) * pl.ld_s + k]; },
-                                      [&](int k, int n) { return sm[pl.l_hw + k * pl.l_hld + n0 + n]; });
+                        c = mfma_tile<pl.H>(c, [&](int m, int k) { return sm[pl.l_s2 + (m0 + m) * pl.ld_s + k]; },
+                                            [&](int k, int n) { return sm[pl.l_hw + k * pl.l_hld + n0 + n]; });
 #pragma unroll
                         for (int i = 0; i < 4; ++i) sm[pl.l_s1 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i];
                     }
                 }
                 __syncthreads();
+                AGX_STAMP(stb + 6);
 
-                // ---- P7: encoder backward, last layer first --------------------------
-                for (int L = pl.ne - 1; L >= 0; --L) {
-                    const int fin = pl.ein[L], fout = pl.eout[L];
-                    const bool affine = pl.eg[L] >= 0;
-                    {
-                        float pb[2] = {0.f, 0.f}, pgm[2] = {0.f, 0.f}, pbe[2] = {0.f, 0.f};
-                        for (int rr = 0; rr < kSB / kNW; ++rr) {
-                            const int r = wave * (kSB / kNW) + rr;
-                            const float rstd = sm[pl.l_re[L] + r];
-                            float xh[2], dxh[2], dyp[2], s1 = 0.f, s2 = 0.f;
+                // ---- P8: encoder backward, last layer first ----------------------
+                auto enc_bwd = [&](auto Lc) {
+                    constexpr int L = decltype(Lc)::value;
+                    constexpr int fin = pl.ein[L], fout = pl.eout[L];
+                    AGX_IDS;
+                    {  // dY (S1) -> S2: the row pass works in place on S2
+                        const int r = rrow;
 #pragma unroll
-                            for (int h = 0; h < 2; ++h) {
-                                const int j = lane + 64 * h;
-                                xh[h] = dxh[h] = dyp[h] = 0.f;
-                                if (j < fout) {
-                                    const float dy = sm[pl.l_s1 + r * pl.ld_s + j];
-                                    xh[h] = sm[pl.l_xe[L] + r * pl.ld_xe[L] + j];
-                                    const float gam = affine ? sm[pl.l_eg[L] + j] : 1.f;
-                                    const float y = affine ? xh[h] * gam + sm[pl.l_ebe[L] + j] : xh[h];
-                                    dyp[h] = y > 0.f ? dy : 0.f;
-                                    dxh[h] = dyp[h] * gam;
-                                    s1 += dxh[h];
-                                    s2 += dxh[h] * xh[h];
-                                }
-                            }
-                            const float m1 = wave_sum(s1) / (float)fout, m2 = wave_sum(s2) / (float)fout;
-#pragma unroll
-                            for (int h = 0; h < 2; ++h) {
-                                const int j = lane + 64 * h;
-                                if (j < fout) {
-                                    const float dz = rstd * (dxh[h] - m1 - xh[h] * m2);
-                                    sm[pl.l_s2 + r * pl.ld_s + j] = dz;
-                                    pb[h] += dz;
-                                    pgm[h] += dyp[h] * xh[h];
-                                    pbe[h] += dyp[h];
-                                }
-                            }
+                        for (int i = 0; i < fout / 16; ++i) {
+                            const int j = sub + 16 * i;
+                            sm[pl.l_s2 + r * pl.ld_s + j] = sm[pl.l_s1 + r * pl.ld_s + j];
                         }
+                    }
+                    ln_bwd(IC(fout), IC(fout), IC(pl.l_xe[L]), IC(pl.ld_xe[L]), IC(pl.l_re[L]), IC(pl.l_eg[L]),
+                           IC(pl.l_ebe[L]), IC(pl.red_e[L]), BC(pl.eaff[L] != 0));
+                    __syncthreads();
+                    constexpr bool in_aff = L > 0 && pl.eaff[L > 0 ? L - 1 : 0];
+                    constexpr int xb = L == 0 ? pl.l_x0 : pl.l_xe[L > 0 ? L - 1 : 0];
+                    constexpr int ldx = L == 0 ? pl.ld_x0 : pl.ld_xe[L > 0 ? L - 1 : 0];
+                    constexpr int gbase = L > 0 ? pl.l_eg[L > 0 ? L - 1 : 0] : 0;
+                    constexpr int bbase = L > 0 ? pl.l_ebe[L > 0 ? L - 1 : 0] : 0;
 #pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const int j = lane + 64 * h;
-                            if (j < fout) {
-                                float *red = sm + pl.l_red + pl.red_e[L];
-                                red[(0 * kNW + wave) * fout + j] = pb[h];
-                                if (affine) {
-                                    red[(1 * kNW + wave) * fout + j] = pgm[h];
-                                    red[(2 * kNW + wave) * fout + j] = pbe[h];
-                                }
-                            }
+                    for (int j = 0; j < pl.nslot[L]; ++j) {
+                        const int t = wave + kNW * j;
+                        if (t < pl.nt[L]) {
+                            const int o0 = (t / pl.ncol[L]) * 16, i0 = (t % pl.ncol[L]) * 16;
+                            const int col = i0 + lr16;
+                            const bool cv = col < fin;
+                            const float gam = (in_aff && cv) ? sm[gbase + col] : 1.f;
+                            const float bet = (in_aff && cv) ? sm[bbase + col] : 0.f;
+                            acc[pl.slot0[L] + j] = mfma_tile<kSB>(
+                                acc[pl.slot0[L] + j], [&](int m, int k) { return sm[pl.l_s2 + k * pl.ld_s + o0 + m]; },
+                                [&](int k, int n) {
+                                    const float x = sm[xb + k * ldx + i0 + n];
+                                    if constexpr (L == 0) return x;
+                                    else return cv ? relu(x * gam + bet) : 0.f;
+                                });
+                        }
+                    }
+                    if constexpr (L > 0) {
+                        constexpr int nt = (kSB / 16) * (fin / 16);
+                        for (int t = wave; t < nt; t += kNW) {
+                            const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
+                            f4 c = f4{0.f, 0.f, 0.f, 0.f};
+                            c = mfma_tile<fout>(c, [&](int m, int k) { return sm[pl.l_s2 + (m0 + m) * pl.ld_s + k]; },
+                                                [&](int k, int n) { return sm[pl.l_ew[L] + k * pl.l_eld[L] + n0 + n]; });
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) sm[pl.l_s1 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i];
                         }
                     }
                     __syncthreads();
-                    // dW_L += dZ^T X_in ; X_in = obs (L == 0) or y of layer L-1 (recomputed)
-                    {
-                        const bool in_aff = L > 0 && pl.eg[L - 1] >= 0;
-                        const int xb = L == 0 ? pl.l_x0 : pl.l_xe[L - 1];
-                        const int ldx = L == 0 ? pl.ld_x0 : pl.ld_xe[L - 1];
-#pragma unroll
-                        for (int s = 0; s < kMaxSlot; ++s) {
-                            if (T_LAYER(s) == L) {
-                                const int o0 = T_O0(s), i0 = T_I0(s);
-                                const int col = i0 + lr16;
-                                const bool cv = col < fin;
-                                const float gam = (L > 0 && cv && in_aff) ? sm[pl.l_eg[L - 1] + col] : 1.f;
-                                const float bet = (L > 0 && cv && in_aff) ? sm[pl.l_ebe[L - 1] + col] : 0.f;
-                                acc[s] = mfma_tile(
-                                    acc[s], kSB, [&](int m, int k) { return sm[pl.l_s2 + k * pl.ld_s + o0 + m]; },
-                                    [&](int k, int n) {
-                                        const float x = sm[xb + k * ldx + i0 + n];
-                                        return L == 0 ? x : (cv ? relu(x * gam + bet) : 0.f);
-                                    });
-                            }
-                        }
-                        if (L > 0) {  // dX = dZ . W_L -> S1 (d of layer L-1's output)
-                            const int nt = (kSB / 16) * (fin / 16);
-                            for (int t = wave; t < nt; t += kNW) {
-                                const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
-                                f4 c = f4{0.f, 0.f, 0.f, 0.f};
-                                c = mfma_tile(c, fout, [&](int m, int k) { return sm[pl.l_s2 + (m0 + m) * pl.ld_s + k]; },
-                                              [&](int k, int n) { return sm[pl.l_ew[L] + k * pl.l_eld[L] + n0 + n]; });
-#pragma unroll
-                                for (int i = 0; i < 4; ++i) sm[pl.l_s1 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i];
-                            }
-                        }
-                    }
-                    __syncthreads();
-                }
-
-                // ---- P8: owners accumulate vector gradients (fixed order) ---------
-#pragma unroll
-                for (int s = 0; s < kVecSlot; ++s) {
-                    const int vi = tid + kNT * s;
-                    if (vi >= pl.nvec) continue;
-                    const VecDesc d = g.vec[vi];
-                    float x = 0.f;
-                    if (d.kind == 0) {
-                        for (int w = 0; w < kNW; ++w) x += sm[pl.l_red + d.p0 + w * d.p1];
-                    } else if (d.kind == 1 || d.kind == 2) {  // out weight: sum_r dZout[r] * y_h[r][col]
-                        const int col = d.p1;
-                        const float gam = sm[pl.l_hg + col], bet = sm[pl.l_hbe + col];
-                        for (int r = 0; r < kSB; ++r) {
-                            const float dz = d.kind == 1 ? sm[pl.l_dlg + r * kMaxA + d.p0] : sm[pl.l_dval + r];
-                            x += dz * relu(sm[pl.l_xh + r * pl.ld_xh + col] * gam + bet);
-                        }
-                    } else if (d.kind == 3) {
-                        for (int r = 0; r < kSB; ++r) x += sm[pl.l_dlg + r * kMaxA + d.p0];
-                    } else if (d.kind == 4) {
-                        for (int r = 0; r < kSB; ++r) x += sm[pl.l_dval + r];
-                    }
-                    vacc[s] += x;
-                }
-                __syncthreads();
+                };
+                if constexpr (pl.ne == 3) enc_bwd(IC(2));
+                enc_bwd(IC(1));
+                enc_bwd(IC(0));
+                AGX_STAMP(stb + 7);
             }  // sub-batches
 
-            // ---- P9: two-group gradient norms ---------------------------------
-            float n0 = 0.f, n1 = 0.f;
+            // ---- P9: dump gradients into the LDS image of the parameter region --
+            float *G = sm + pl.l_grad;
+            auto dump = [&](auto gc) {
+                constexpr int gg = decltype(gc)::value;
+                AGX_IDS;
 #pragma unroll
-            for (int s = 0; s < kMaxSlot; ++s) {
-                const int L = T_LAYER(s);
-                if (L >= 0) {
-                    const int fin = L < pl.ne ? pl.ein[L] : pl.lat;
-                    const int fout = L < pl.ne ? pl.eout[L] : pl.H;
-                    const int col = T_I0(s) + lr16;
+                for (int j = 0; j < pl.nslot[gg]; ++j) {
+                    const int t = wave + kNW * j;
+                    if (t < pl.nt[gg]) {
+                        const int o0 = (t / pl.ncol[gg]) * 16, i0 = (t % pl.ncol[gg]) * 16;
+                        const int col = i0 + lr16;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int o = T_O0(s) + lq * 4 + i;
-                        if (col < fin && o < fout) {
-                            const float x = acc[s][i];
-                            if (L == pl.ne && o >= pl.ha) n1 += x * x;
-                            else n0 += x * x;
+                        for (int i = 0; i < 4; ++i) {
+                            const int o = o0 + lq * 4 + i;
+                            const float x = acc[pl.slot0[gg] + j][i];
+                            if constexpr (gg < pl.ne) {
+                                if (col < pl.ein[gg]) G[pl.l_ew[gg] + o * pl.l_eld[gg] + col] = x;
+                            } else if constexpr (gg == pl.ne) {
+                                G[pl.l_hw + o * pl.l_hld + col] = x;
+                            } else if constexpr (gg == pl.ne + 1) {
+                                if (o < pl.A) {
+                                    if (col < pl.ha) G[pl.l_aow + o * pl.l_aold + col] = x;
+                                    else if (col == pl.ha) G[pl.l_aob + o] = x;
+                                }
+                            } else {
+                                if (o == 0) {
+                                    if (col < pl.hc) G[pl.l_cow + col] = x;
+                                    else if (col == pl.hc) G[pl.l_cob] = x;
+                                }
+                            }
                         }
                     }
                 }
-            }
+            };
+            dump(IC(0));
+            dump(IC(1));
+            if constexpr (pl.ne == 3) dump(IC(2));
+            dump(IC(pl.ne));
+            dump(IC(pl.ne + 1));
+            dump(IC(pl.ne + 2));
+            // LN / bias vectors: fixed-order sums of the per-wave partials
+            auto vdump = [&](auto Lc) {
+                constexpr int L = decltype(Lc)::value;
+                constexpr int F = L < pl.ne ? pl.eout[L < pl.ne ? L : 0] : pl.H;
+                constexpr int nv = (L < pl.ne && !pl.eaff[L < pl.ne ? L : 0]) ? 1 : 3;
+                constexpr int red = L < pl.ne ? pl.red_e[L < pl.ne ? L : 0] : pl.red_h;
+                const int tid = vtid();
+                for (int idx = tid; idx < nv * F; idx += kNT) {
+                    const int k = idx / F, j = idx % F;
+                    float x = 0.f;
 #pragma unroll
-            for (int s = 0; s < kVecSlot; ++s) {
-                const int vi = tid + kNT * s;
-                if (vi < pl.nvec) {
-                    if (g.vec[vi].group) n1 += vacc[s] * vacc[s];
-                    else n0 += vacc[s] * vacc[s];
+                    for (int w = 0; w < kNW; ++w) x += sm[pl.l_red + red + (k * kNW + w) * F + j];
+                    int l;
+                    if constexpr (L < pl.ne) {
+                        l = (k == 0 ? pl.l_eb[L < pl.ne ? L : 0] : (k == 1 ? pl.l_eg[L < pl.ne ? L : 0] : pl.l_ebe[L < pl.ne ? L : 0])) + j;
+                    } else {
+                        l = (k == 0 ? pl.l_hb : (k == 1 ? pl.l_hg : pl.l_hbe)) + j;
+                    }
+                    G[l] = x;
+                }
+            };
+            vdump(IC(0));
+            vdump(IC(1));
+            if constexpr (pl.ne == 3) vdump(IC(2));
+            vdump(IC(pl.ne));
+            AGX_STAMP(64 + 9);
+            __syncthreads();
+
+            // ---- P10: two-group norm, Adam from registers -------------------------
+            float n0 = 0.f, n1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < kMaxPT; ++i) {
+                const int l = tid + kNT * i;
+                if ((vbits >> i) & 1u) {
+                    const float x = G[l];
+                    if ((gbits >> i) & 1u) n1 += x * x;
+                    else n0 += x * x;
                 }
             }
-            n0 = wave_sum(n0);
-            n1 = wave_sum(n1);
-            // minibatch loss from the row threads (wave 0)
-            const float lmb = wave_sum(lsum);
-            float *stat = sm + pl.l_stat;
-            if (lane == 0) {
-                stat[2 * wave] = n0;
-                stat[2 * wave + 1] = n1;
-            }
-            __syncthreads();
-            float t0 = 0.f, t1 = 0.f;
-            for (int w = 0; w < kNW; ++w) {
-                t0 += stat[2 * w];
-                t1 += stat[2 * w + 1];
-            }
+            AGX_IDS;
+            const float t0 = block_sum(n0, stat, 0, lane, wave);
+            const float t1 = block_sum(n1, stat, 1, lane, wave);
+            const float lmb = block_sum(lsum, stat, 2, lane, wave);
             if (tid == 0) loss_total += lmb;
             const float c0 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t0) + 1e-6f), 1.f) : 1.f;
             const float c1 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t1) + 1e-6f), 1.f) : 1.f;
-
-            // ---- P10: Adam on owned entries --------------------------------------
             ++step;
             const float bc1 = (float)(1.0 - pow((double)g.b1, (double)step));
             const float bc2s = (float)sqrt(1.0 - pow((double)g.b2, (double)step));
             const float step_size = g.lr[p] / bc1;
-            auto adam = [&](int flat, int lds, float gr) {
-                float mm = gm[flat], vv = gv[flat];
-                mm = mm + (1.f - g.b1) * (gr - mm);
-                vv = vv * g.b2 + (1.f - g.b2) * gr * gr;
-                gm[flat] = mm;
-                gv[flat] = vv;
-                const float denom = sqrtf(vv) / bc2s + g.eps;
-                sm[lds] = sm[lds] - step_size * (mm / denom);
-            };
 #pragma unroll
-            for (int s = 0; s < kMaxSlot; ++s) {
-                const int L = T_LAYER(s);
-                if (L >= 0) {
-                    const int col = T_I0(s) + lr16;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int o = T_O0(s) + lq * 4 + i;
-                        if (L < pl.ne) {
-                            if (col < pl.ein[L] && o < pl.eout[L])
-                                adam(pl.ew[L] + o * pl.ein[L] + col, pl.l_ew[L] + o * pl.l_eld[L] + col, acc[s][i] * c0);
-                        } else if (col < pl.lat && o < pl.H) {
-                            const bool isa = o < pl.ha;
-                            const int flat = isa ? pl.aw + o * pl.lat + col : pl.cw + (o - pl.ha) * pl.lat + col;
-                            adam(flat, pl.l_hw + o * pl.l_hld + col, acc[s][i] * (isa ? c0 : c1));
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < kVecSlot; ++s) {
-                const int vi = tid + kNT * s;
-                if (vi < pl.nvec) {
-                    const VecDesc d = g.vec[vi];
-                    adam(d.flat, d.lds, vacc[s] * (d.group ? c1 : c0));
+            for (int i = 0; i < kMaxPT; ++i) {
+                const int l = tid + kNT * i;
+                if ((vbits >> i) & 1u) {  // G (activation alias) and the parameters are disjoint
+                    const float gr = G[l] * (((gbits >> i) & 1u) ? c1 : c0);
+                    am[i] = am[i] + (1.f - g.b1) * (gr - am[i]);
+                    av[i] = av[i] * g.b2 + (1.f - g.b2) * gr * gr;
+                    const float denom = sqrtf(av[i]) / bc2s + g.eps;
+                    sm[l] = sm[l] - step_size * (am[i] / denom);
                 }
             }
             __syncthreads();
+            AGX_STAMP(64 + 10);
         }  // minibatches
     }      // epochs
 
-    // ---------------- write parameters back ---------------------------------
-    for (int e = 0; e < pl.ne; ++e) {
-        const int fin = pl.ein[e], fout = pl.eout[e];
-        for (int i = tid; i < fin * fout; i += kNT) gp[pl.ew[e] + i] = sm[pl.l_ew[e] + (i / fin) * pl.l_eld[e] + i % fin];
-        for (int i = tid; i < fout; i += kNT) {
-            gp[pl.eb[e] + i] = sm[pl.l_eb[e] + i];
-            if (pl.eg[e] >= 0) {
-                gp[pl.eg[e] + i] = sm[pl.l_eg[e] + i];
-                gp[pl.ebe[e] + i] = sm[pl.l_ebe[e] + i];
-            }
+    // ---- write parameters and moments back --------------------------------------
+#pragma unroll
+    for (int i = 0; i < kMaxPT; ++i) {
+        const int l = tid + kNT * i;
+        if ((vbits >> i) & 1u) {
+            int grp;
+            const int f = lds_to_flat<C>(l, grp);
+            gp[f] = sm[l];
+            gm[f] = am[i];
+            gv[f] = av[i];
         }
     }
-    for (int i = tid; i < pl.lat * pl.H; i += kNT) {
-        const int o = i / pl.lat, c = i % pl.lat;
-        const float w = sm[pl.l_hw + o * pl.l_hld + c];
-        if (o < pl.ha) gp[pl.aw + o * pl.lat + c] = w;
-        else gp[pl.cw + (o - pl.ha) * pl.lat + c] = w;
+    if (tid == 0 && g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)g.E);
+#undef IC
+#undef BC
+}
+
+// ---------------------------------------------------------------------------
+// prologue: permute the rollout SoA into minibatch order, normalise advantages
+// ---------------------------------------------------------------------------
+__global__ void ppo_gather_kernel(const float *__restrict__ obs, const long long *__restrict__ act,
+                                  const float *__restrict__ old_logp, const float *__restrict__ adv,
+                                  const float *__restrict__ ret, const float *__restrict__ old_v,
+                                  const double *__restrict__ adv_stats, const long long *__restrict__ perms,
+                                  long long S, int D, int P, float *__restrict__ gobs, int *__restrict__ gact,
+                                  float *__restrict__ grow) {
+    const int ep = blockIdx.y;  // e * P + p
+    const int p = ep % P;
+    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= S) return;
+    const long long src = perms[(size_t)ep * S + j];
+    const size_t sp = (size_t)p * S + src;
+    for (int d = 0; d < D; ++d) gobs[((size_t)ep * S + j) * D + d] = obs[sp * D + d];
+    gact[(size_t)ep * S + j] = (int)act[sp];
+    float *gr = grow + (size_t)ep * 4 * S;
+    double a = adv[sp];
+    if (adv_stats) a = (a - adv_stats[2 * p]) * (1.0 / (adv_stats[2 * p + 1] + 1e-8));  // == adv_normalize_kernel
+    gr[j] = old_logp[sp];
+    gr[S + j] = (float)a;
+    gr[2 * S + j] = ret[sp];
+    gr[3 * S + j] = old_v[sp];
+}
+
+// ---------------------------------------------------------------------------
+// rollout policy step
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned mulhilo(unsigned a, unsigned b, unsigned &hi) {
+    const unsigned long long prod = (unsigned long long)a * b;
+    hi = (unsigned)(prod >> 32);
+    return (unsigned)prod;
+}
+// Philox4x32-10 (Salmon et al., SC'11)
+__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        unsigned h0, h1;
+        const unsigned l0 = mulhilo(0xD2511F53u, c.x, h0);
+        const unsigned l1 = mulhilo(0xCD9E8D57u, c.z, h1);
+        c = make_uint4(h1 ^ c.y ^ k.x, l1, h0 ^ c.w ^ k.y, l0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
     }
-    for (int o = tid; o < pl.H; o += kNT) {
-        const bool a = o < pl.ha;
-        const int oo = a ? o : o - pl.ha;
-        gp[(a ? pl.ab : pl.cb) + oo] = sm[pl.l_hb + o];
-        gp[(a ? pl.ag : pl.cg) + oo] = sm[pl.l_hg + o];
-        gp[(a ? pl.abe : pl.cbe) + oo] = sm[pl.l_hbe + o];
+    return c;
+}
+
+struct ActArgs {
+    const float *params;
+    const float *obs;  // agent p, env n at obs + p*obs_pstride + n*D
+    long long obs_pstride;
+    int N, P, sample;
+    unsigned long long seed, counter;
+    long long *act_out;  // agent p, env n at + p*out_pstride + n (each may be null)
+    float *logp_out, *value_out, *ent_out;
+    long long out_pstride;
+    long long *act_flat;  // [P*N] contiguous copy (host staging) or null
+};
+
+template <class C>
+__global__ __launch_bounds__(kNT, 1) void ppo_act_kernel(ActArgs g) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    constexpr LearnPlan pl = C::plan;
+    const int p = blockIdx.y, n0 = blockIdx.x * kSB;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < pl.act_floats; i += kNT) sm[i] = 0.f;
+    __syncthreads();
+    load_params<C>(sm, g.params + (size_t)p * pl.n, tid);
+    const int nrow = g.N - n0 < kSB ? g.N - n0 : kSB;
+    const float *ob = g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * pl.D;
+    for (int i = tid; i < kSB * pl.D; i += kNT) {
+        const int r = i / pl.D, d = i % pl.D;
+        sm[pl.l_x0 + r * pl.ld_x0 + d] = r < nrow ? ob[i] : 0.f;
     }
-    for (int i = tid; i < pl.A * pl.ha; i += kNT) gp[pl.aow + i] = sm[pl.l_aow + i];
-    for (int i = tid; i < pl.A; i += kNT) gp[pl.aob + i] = sm[pl.l_aob + i];
-    for (int i = tid; i < pl.hc; i += kNT) gp[pl.cow + i] = sm[pl.l_cow + i];
-    if (tid == 0) {
-        gp[pl.cob] = sm[pl.l_cob];
-        if (g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)g.E);
+    __syncthreads();
+    Fwd<C> fw{sm};
+    fw.run();
+    // categorical over 16 lanes per row
+    const int r = wave * 4 + (lane >> 4), a = lane & 15;
+    const bool live = r < nrow;
+    const float lg = a < pl.A ? sm[pl.l_lg + r * kMaxA + a] : -3.0e38f;
+    const float mx = row_max(lg);
+    const float lse = mx + logf(row_sum(a < pl.A ? expf(lg - mx) : 0.f));
+    const float pa = a < pl.A ? expf(lg - lse) : 0.f;
+    const float H = -row_sum(a < pl.A ? pa * logf(pa + 1e-8f) : 0.f);
+    float score = lg;
+    if (g.sample) {
+        const unsigned long long env = (unsigned long long)p * g.N + n0 + r;
+        const uint4 rnd = philox(make_uint4((unsigned)env, (unsigned)(env >> 32), (unsigned)g.counter,
+                                            (unsigned)(g.counter >> 32) ^ ((unsigned)(a >> 2) << 24)),
+                                 make_uint2((unsigned)g.seed, (unsigned)(g.seed >> 32)));
+        const unsigned w = (a & 3) == 0 ? rnd.x : (a & 3) == 1 ? rnd.y : (a & 3) == 2 ? rnd.z : rnd.w;
+        const float u = ((float)(w >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+        score = a < pl.A ? lg - logf(-logf(u)) : -3.0e38f;                  // Gumbel-max
+    }
+    const float best = row_max(score);
+    const unsigned long long ball = __ballot(score == best);
+    const int choice = __builtin_ctz((unsigned)((ball >> (lane & ~15)) & 0xffffu));  // first maximum
+    const float lgc = __builtin_bit_cast(
+        float, __builtin_amdgcn_ds_bpermute(((lane & ~15) + choice) * 4, __builtin_bit_cast(int, lg)));
+    if (live && a == 0) {
+        const size_t o = (size_t)p * g.out_pstride + n0 + r;
+        if (g.act_out) g.act_out[o] = choice;
+        if (g.logp_out) g.logp_out[o] = lgc - lse;
+        if (g.ent_out) g.ent_out[o] = H;
+        if (g.value_out) g.value_out[o] = sm[pl.l_val + r];
+        if (g.act_flat) g.act_flat[(size_t)p * g.N + n0 + r] = choice;
     }
 }
 
 // ---------------------------------------------------------------------------
-// host-side planning
+// host-side dispatch over the instantiated shapes
 // ---------------------------------------------------------------------------
-static int plan_learner(const agx_ppo_net *net, LearnPlan &pl, VecDesc *vec, int vec_cap) {
-    pl = LearnPlan{};
-    pl.D = net->obs_dim;
-    pl.A = net->n_actions;
-    pl.ne = net->n_enc;
-    if (pl.ne < 2 || pl.ne > 3 || pl.A < 1 || pl.A > kMaxA || pl.D < 1 || pl.D > 128) return -1;
-    int prev = pl.D;
+static bool same_layout(const agx_ppo_net *net, const LearnPlan &pl) {
+    if (!pl.ok || net->n_params != pl.n || net->critic_start != pl.f_cw) return false;
     for (int e = 0; e < pl.ne; ++e) {
-        pl.ein[e] = prev;
-        pl.eout[e] = net->enc_dim[e + 1];
-        if (pl.eout[e] % 16 || pl.eout[e] > 128 || pl.eout[e] < 16) return -1;
-        if (e > 0 && pl.ein[e] % 16) return -1;
-        pl.ew[e] = net->enc_w[e];
-        pl.eb[e] = net->enc_b[e];
-        pl.eg[e] = e < pl.ne - 1 ? net->enc_ln_w[e] : -1;
-        pl.ebe[e] = e < pl.ne - 1 ? net->enc_ln_b[e] : -1;
-        prev = pl.eout[e];
+        if (net->enc_w[e] != pl.f_ew[e] || net->enc_b[e] != pl.f_eb[e]) return false;
+        if (pl.eaff[e] && (net->enc_ln_w[e] != pl.f_eg[e] || net->enc_ln_b[e] != pl.f_ebe[e])) return false;
     }
-    pl.lat = prev;
-    pl.ha = net->head_actor;
-    pl.hc = net->head_critic;
-    pl.H = pl.ha + pl.hc;
-    if (pl.ha % 16 || pl.hc % 16 || pl.ha < 16 || pl.hc < 16 || pl.H > 256) return -1;
-    pl.aw = net->actor_w; pl.ab = net->actor_b; pl.ag = net->actor_ln_w; pl.abe = net->actor_ln_b;
-    pl.aow = net->actor_out_w; pl.aob = net->actor_out_b;
-    pl.cw = net->critic_w; pl.cb = net->critic_b; pl.cg = net->critic_ln_w; pl.cbe = net->critic_ln_b;
-    pl.cow = net->critic_out_w; pl.cob = net->critic_out_b;
-    pl.n = net->n_params;
-    pl.split = net->critic_start;
-    // ---- LDS plan
-    int off = 0;
-    auto take = [&](int n) { const int o = off; off += (n + 3) & ~3; return o; };
-    for (int e = 0; e < pl.ne; ++e) {
-        pl.l_eld[e] = ((pl.ein[e] + 3) & ~3) + 2;
-        pl.l_ew[e] = take(pl.eout[e] * pl.l_eld[e]);
-        pl.l_eb[e] = take(pl.eout[e]);
-        pl.l_eg[e] = pl.eg[e] >= 0 ? take(pl.eout[e]) : -1;
-        pl.l_ebe[e] = pl.eg[e] >= 0 ? take(pl.eout[e]) : -1;
+    return net->actor_w == pl.f_aw && net->actor_b == pl.f_ab && net->actor_ln_w == pl.f_ag &&
+           net->actor_ln_b == pl.f_abe && net->actor_out_w == pl.f_aow && net->actor_out_b == pl.f_aob &&
+           net->critic_w == pl.f_cw && net->critic_b == pl.f_cb && net->critic_ln_w == pl.f_cg &&
+           net->critic_ln_b == pl.f_cbe && net->critic_out_w == pl.f_cow && net->critic_out_b == pl.f_cob;
+}
+
+static bool dims_match(const agx_ppo_net *net, const NetDims &d) {
+    if (net->obs_dim != d.D || net->n_actions != d.A || net->n_enc != d.ne) return false;
+    if (net->enc_dim[0] != d.D) return false;
+    for (int e = 0; e < d.ne; ++e)
+        if (net->enc_dim[e + 1] != d.eo[e]) return false;
+    return net->head_actor == d.ha && net->head_critic == d.hc;
+}
+
+struct Launcher {
+    const LearnPlan *plan;
+    void (*learn)(const LearnArgs &, int P, size_t lds, hipStream_t);
+    void (*act)(const ActArgs &, dim3 grid, size_t lds, hipStream_t);
+};
+
+template <class C>
+static void launch_learn(const LearnArgs &a, int P, size_t lds, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
     }
-    pl.l_hld = pl.lat + 2;
-    pl.l_hw = take(pl.H * pl.l_hld);
-    pl.l_hb = take(pl.H);
-    pl.l_hg = take(pl.H);
-    pl.l_hbe = take(pl.H);
-    pl.l_aow = take(pl.A * pl.ha);
-    pl.l_aob = take(pl.A);
-    pl.l_cow = take(pl.hc);
-    pl.l_cob = take(1);
-    pl.ld_x0 = ((pl.D + 15) & ~15) + 2;
-    pl.l_x0 = take(kSB * pl.ld_x0);
-    for (int e = 0; e < pl.ne; ++e) {
-        pl.ld_xe[e] = pl.eout[e] + 2;
-        pl.l_xe[e] = take(kSB * pl.ld_xe[e]);
-        pl.l_re[e] = take(kSB);
+    ppo_learn_kernel<C><<<(unsigned)P, kNT, lds, s>>>(a);
+}
+template <class C>
+static void launch_act(const ActArgs &a, dim3 grid, size_t lds, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)ppo_act_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
     }
-    pl.ld_xh = pl.H + 2;
-    pl.l_xh = take(kSB * pl.ld_xh);
-    pl.l_rh = take(2 * kSB);
-    int wmax = pl.H;
-    for (int e = 0; e < pl.ne; ++e) wmax = wmax > pl.eout[e] ? wmax : pl.eout[e];
-    pl.ld_s = wmax + 2;
-    pl.l_s1 = take(kSB * pl.ld_s);
-    pl.l_s2 = take(kSB * pl.ld_s);
-    pl.l_lg = take(kSB * kMaxA);
-    pl.l_dlg = take(kSB * kMaxA);
-    pl.l_val = take(kSB);
-    pl.l_dval = take(kSB);
-    pl.l_row = take(5 * kSB);
-    pl.l_stat = take(4 * kNW);
-    // partial buffers: [3][NW][width] per layer (plain LN layer: bias only)
-    int red = 0;
-    for (int e = 0; e < pl.ne; ++e) {
-        pl.red_e[e] = red;
-        red += (pl.eg[e] >= 0 ? 3 : 1) * kNW * pl.eout[e];
+    ppo_act_kernel<C><<<grid, kNT, lds, s>>>(a);
+}
+
+static bool find_launcher(const agx_ppo_net *net, Launcher &out) {
+    if (!net) return false;
+#define AGX_TRY(D_, A_, NE_, E0, E1, E2, HA, HC)                                                      \
+    {                                                                                                 \
+        using C = Shape<D_, A_, NE_, E0, E1, E2, HA, HC>;                                             \
+        static_assert(C::plan.ok, "instantiated PPO shape must have a valid plan");                   \
+        if (dims_match(net, C::dims) && same_layout(net, C::plan)) {                                  \
+            out = Launcher{&C::plan, &launch_learn<C>, &launch_act<C>};                               \
+            return true;                                                                              \
+        }                                                                                             \
     }
-    pl.red_h = red;
-    red += 3 * kNW * pl.H;
-    pl.l_red = take(red);
-    pl.lds_floats = off;
-    // ---- dW tiles
-    pl.tile_begin[0] = 0;
-    for (int e = 0; e < pl.ne; ++e) pl.tile_begin[e + 1] = pl.tile_begin[e] + (pl.eout[e] / 16) * ((pl.ein[e] + 15) / 16);
-    pl.ntiles = pl.tile_begin[pl.ne] + (pl.H / 16) * (pl.lat / 16);
-    if (pl.ntiles > kNW * kMaxSlot) return -2;
-    // ---- vector gradients
-    int nv = 0;
-    auto add = [&](int flat, int lds, int group, int kind, int p0, int p1) {
-        if (nv < vec_cap) vec[nv] = VecDesc{flat, lds, group, kind, p0, p1};
-        ++nv;
-    };
-    for (int e = 0; e < pl.ne; ++e) {
-        const int F = pl.eout[e];
-        for (int j = 0; j < F; ++j) add(pl.eb[e] + j, pl.l_eb[e] + j, 0, 0, pl.red_e[e] + j, F);
-        if (pl.eg[e] >= 0) {
-            for (int j = 0; j < F; ++j) add(pl.eg[e] + j, pl.l_eg[e] + j, 0, 0, pl.red_e[e] + kNW * F + j, F);
-            for (int j = 0; j < F; ++j) add(pl.ebe[e] + j, pl.l_ebe[e] + j, 0, 0, pl.red_e[e] + 2 * kNW * F + j, F);
-        }
-    }
-    for (int j = 0; j < pl.H; ++j) {
-        const bool a = j < pl.ha;
-        const int jj = a ? j : j - pl.ha;
-        const int grp = a ? 0 : 1;
-        add((a ? pl.ab : pl.cb) + jj, pl.l_hb + j, grp, 0, pl.red_h + j, pl.H);
-        add((a ? pl.ag : pl.cg) + jj, pl.l_hg + j, grp, 0, pl.red_h + kNW * pl.H + j, pl.H);
-        add((a ? pl.abe : pl.cbe) + jj, pl.l_hbe + j, grp, 0, pl.red_h + 2 * kNW * pl.H + j, pl.H);
-    }
-    for (int a = 0; a < pl.A; ++a)
-        for (int o = 0; o < pl.ha; ++o) add(pl.aow + a * pl.ha + o, pl.l_aow + a * pl.ha + o, 0, 1, a, o);
-    for (int o = 0; o < pl.hc; ++o) add(pl.cow + o, pl.l_cow + o, 1, 2, 0, pl.ha + o);
-    for (int a = 0; a < pl.A; ++a) add(pl.aob + a, pl.l_aob + a, 0, 3, a, 0);
-    add(pl.cob, pl.l_cob, 1, 4, 0, 0);
-    pl.nvec = nv;
-    if (nv > kNT * kVecSlot) return -3;
-    return 0;
+    AGX_PPO_SHAPES(AGX_TRY)
+#undef AGX_TRY
+    return false;
+}
+
+static long long *&g_stamps_ptr() {
+    static long long *p = nullptr;
+    return p;
 }
 
 }  // namespace agx
@@ -833,40 +1164,32 @@ static int plan_learner(const agx_ppo_net *net, LearnPlan &pl, VecDesc *vec, int
 using namespace agx;
 
 extern "C" size_t agx_ppo_learn_lds_bytes(const agx_ppo_net *net) {
-    LearnPlan pl;
-    if (!net || plan_learner(net, pl, nullptr, 0) != 0) return 0;
-    return (size_t)pl.lds_floats * sizeof(float);
+    Launcher L;
+    if (!find_launcher(net, L)) return 0;
+    return (size_t)L.plan->lds_floats * sizeof(float);
 }
 
-constexpr size_t kPlanBytes = (sizeof(LearnPlan) + 255) & ~(size_t)255;
+extern "C" size_t agx_ppo_learn_workspace_bytes(const agx_ppo_net *net, int64_t P, int64_t S, int64_t epochs) {
+    Launcher L;
+    if (!find_launcher(net, L)) return 0;
+    const size_t per = (size_t)epochs * P * S;
+    return 256 + per * (size_t)L.plan->D * 4 + ((per * 4 + 255) & ~(size_t)255) + per * 4 * 4;
+}
 
-extern "C" size_t agx_ppo_learn_workspace_bytes(const agx_ppo_net *net) {
-    LearnPlan pl;
-    if (!net || plan_learner(net, pl, nullptr, 0) != 0) return 0;
-    return kPlanBytes + (size_t)pl.nvec * sizeof(VecDesc);
+extern "C" int agx_debug_learn_stamps(int64_t *buf) {
+    static_assert(sizeof(long long) == sizeof(int64_t), "");
+    g_stamps_ptr() = reinterpret_cast<long long *>(buf);
+    return AGX_OK;
 }
 
 extern "C" int agx_ppo_learn_prepare(const agx_ppo_net *net, void *workspace, void *stream) {
-    AGX_REQUIRE(net && workspace, "agx_ppo_learn_prepare: null pointer");
-    LearnPlan pl;
-    static thread_local VecDesc vec[kNT * kVecSlot];
-    const int rc = plan_learner(net, pl, vec, kNT * kVecSlot);
-    if (rc != 0) {
-        set_error("agx_ppo_learn_prepare: network not supported by the fused learner (code %d)", rc);
+    (void)workspace;
+    (void)stream;
+    AGX_REQUIRE(net, "agx_ppo_learn_prepare: null pointer");
+    Launcher L;
+    if (!find_launcher(net, L)) {
+        set_error("agx_ppo_learn_prepare: network shape not instantiated for the fused learner");
         return AGX_EUNSUPPORTED;
-    }
-    // one-time upload of the plan + ownership table; synchronous so the host
-    // copies may be reused immediately
-    static thread_local LearnPlan plan_copy;
-    plan_copy = pl;
-    hipError_t e = hipMemcpyAsync(workspace, &plan_copy, sizeof(LearnPlan), hipMemcpyHostToDevice, as_stream(stream));
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(static_cast<char *>(workspace) + kPlanBytes, vec, (size_t)pl.nvec * sizeof(VecDesc),
-                           hipMemcpyHostToDevice, as_stream(stream));
-    if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
-    if (e != hipSuccess) {
-        set_error("agx_ppo_learn_prepare: %s", hipGetErrorString(e));
-        return AGX_EHIP;
     }
     return AGX_OK;
 }
@@ -874,32 +1197,34 @@ extern "C" int agx_ppo_learn_prepare(const agx_ppo_net *net, void *workspace, vo
 extern "C" int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, float *exp_avg,
                              float *exp_avg_sq, const float *lr, float beta1, float beta2, float eps,
                              int64_t adam_step0, const float *obs, const int64_t *actions,
-                             const float *old_logp, const float *adv, const float *ret,
-                             const float *old_value, int64_t S, const int64_t *perms, int64_t epochs,
-                             int64_t batch, float clip_coef, float vf_coef, float ent_coef,
+                             const float *old_logp, const float *adv, const double *adv_stats,
+                             const float *ret, const float *old_value, int64_t S, const int64_t *perms,
+                             int64_t epochs, int64_t batch, float clip_coef, float vf_coef, float ent_coef,
                              float max_grad_norm, float *loss_out, void *workspace, void *stream) {
     AGX_REQUIRE(net && params && exp_avg && exp_avg_sq && lr && obs && actions && old_logp && adv && ret &&
                     old_value && perms && workspace,
                 "agx_ppo_learn: null pointer");
-    AGX_REQUIRE(P > 0 && P <= 65535 && S > 0 && epochs > 0 && batch > 0, "agx_ppo_learn: bad sizes");
-    LearnPlan pl;
-    const int rc = plan_learner(net, pl, nullptr, 0);
-    if (rc != 0) {
-        set_error("agx_ppo_learn: network not supported by the fused learner (code %d)", rc);
+    AGX_REQUIRE(P > 0 && P <= 65535 && S > 0 && epochs > 0 && batch > 0 && epochs * P <= 65535,
+                "agx_ppo_learn: bad sizes");
+    Launcher L;
+    if (!find_launcher(net, L)) {
+        set_error("agx_ppo_learn: network shape not instantiated for the fused learner");
         return AGX_EUNSUPPORTED;
     }
-    const size_t lds = (size_t)pl.lds_floats * sizeof(float);
-    AGX_REQUIRE(lds <= 160 * 1024, "agx_ppo_learn: network needs %zu B of LDS (> 160 KiB)", lds);
-    AGX_REQUIRE(pl.n == net->n_params, "agx_ppo_learn: inconsistent parameter count");
+    const LearnPlan &pl = *L.plan;
     hipStream_t s = as_stream(stream);
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipFuncSetAttribute((const void *)ppo_learn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_set = true;
-    }
+    const size_t per = (size_t)epochs * P * S;
+    char *ws = static_cast<char *>(workspace);
+    float *gobs = reinterpret_cast<float *>(ws + 256);
+    int *gact = reinterpret_cast<int *>(ws + 256 + per * pl.D * 4);
+    float *grow = reinterpret_cast<float *>(ws + 256 + per * pl.D * 4 + ((per * 4 + 255) & ~(size_t)255));
+    dim3 ggrid((unsigned)ceil_div(S, 256), (unsigned)(epochs * P));
+    ppo_gather_kernel<<<ggrid, 256, 0, s>>>(obs, reinterpret_cast<const long long *>(actions), old_logp, adv, ret,
+                                            old_value, adv_stats, reinterpret_cast<const long long *>(perms), S,
+                                            pl.D, (int)P, gobs, gact, grow);
+    const int rc2 = check_launch("agx_ppo_learn gather");
+    if (rc2) return rc2;
     LearnArgs a;
-    a.plan = static_cast<const LearnPlan *>(workspace);
-    a.vec = reinterpret_cast<const VecDesc *>(static_cast<const char *>(workspace) + kPlanBytes);
     a.params = params;
     a.m = exp_avg;
     a.v = exp_avg_sq;
@@ -908,14 +1233,10 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, f
     a.b2 = beta2;
     a.eps = eps;
     a.step0 = adam_step0;
-    a.obs = obs;
-    a.act = reinterpret_cast<const long long *>(actions);
-    a.old_logp = old_logp;
-    a.adv = adv;
-    a.ret = ret;
-    a.old_v = old_value;
+    a.gobs = gobs;
+    a.gact = gact;
+    a.grow = grow;
     a.S = S;
-    a.perms = reinterpret_cast<const long long *>(perms);
     a.E = (int)epochs;
     a.B = (int)batch;
     a.P = (int)P;
@@ -924,6 +1245,38 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, f
     a.ent = ent_coef;
     a.max_norm = max_grad_norm;
     a.loss_out = loss_out;
-    ppo_learn_kernel<<<(unsigned)P, kNT, lds, s>>>(a);
+    a.stamps = g_stamps_ptr();
+    L.learn(a, (int)P, (size_t)pl.lds_floats * sizeof(float), s);
     return check_launch("agx_ppo_learn");
+}
+
+extern "C" int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const float *params, const float *obs,
+                           int64_t obs_agent_stride, int sample, uint64_t seed, uint64_t counter,
+                           int64_t *actions, float *log_probs, float *values, float *entropy,
+                           int64_t out_agent_stride, int64_t *actions_flat, void *workspace, void *stream) {
+    (void)workspace;
+    AGX_REQUIRE(net && params && obs && P > 0 && N > 0 && P <= 65535, "agx_ppo_act: bad arguments");
+    Launcher L;
+    if (!find_launcher(net, L)) {
+        set_error("agx_ppo_act: network shape not instantiated");
+        return AGX_EUNSUPPORTED;
+    }
+    ActArgs a;
+    a.params = params;
+    a.obs = obs;
+    a.obs_pstride = obs_agent_stride;
+    a.N = (int)N;
+    a.P = (int)P;
+    a.sample = sample;
+    a.seed = seed;
+    a.counter = counter;
+    a.act_out = reinterpret_cast<long long *>(actions);
+    a.logp_out = log_probs;
+    a.value_out = values;
+    a.ent_out = entropy;
+    a.out_pstride = out_agent_stride;
+    a.act_flat = reinterpret_cast<long long *>(actions_flat);
+    dim3 grid((unsigned)ceil_div(N, kSB), (unsigned)P);
+    L.act(a, grid, (size_t)L.plan->act_floats * sizeof(float), as_stream(stream));
+    return check_launch("agx_ppo_act");
 }

@@ -61,14 +61,16 @@ class FusedLearner:
         if self.desc is None:
             raise _lib.AgxError("network outside the fused learner's coverage")
         lib = _lib.load()
-        nbytes = lib.agx_ppo_learn_workspace_bytes(ctypes.byref(self.desc))
+        nbytes = lib.agx_ppo_learn_workspace_bytes(ctypes.byref(self.desc), pop.P, pop.S, pop.update_epochs)
         self.ws = torch.empty(max(16, nbytes), dtype=torch.uint8, device=pop.device)
         _lib.check(lib.agx_ppo_learn_prepare(ctypes.byref(self.desc), self.ws.data_ptr(), _lib.stream()),
                    "agx_ppo_learn_prepare")
         self.loss = torch.zeros(pop.P, dtype=torch.float32, device=pop.device)
 
     def learn(self, pop, perms: torch.Tensor | None = None) -> torch.Tensor:
-        K.adv_normalize_(pop.advantages, pop.adv_stats)
+        """All epochs x minibatches of every agent in two launches (gather +
+        learner).  Advantages are normalised on the fly from pop.adv_stats
+        (ppo.py:829-834); pop.advantages itself is left untouched."""
         if perms is None:
             perms = pop.permutations()
         opt = pop.opt
@@ -76,10 +78,10 @@ class FusedLearner:
         _lib.call("agx_ppo_learn", ctypes.byref(self.desc), pop.P, pop.params.data.data_ptr(),
                   opt.exp_avg.data_ptr(), opt.exp_avg_sq.data_ptr(), opt.lr.data_ptr(), float(b1), float(b2),
                   float(opt.eps), opt.step_count, pop.obs.data_ptr(), pop.actions.data_ptr(),
-                  pop.log_probs.data_ptr(), pop.advantages.data_ptr(), pop.returns.data_ptr(),
-                  pop.values.data_ptr(), pop.S, perms.data_ptr(), pop.update_epochs, pop.batch_size,
-                  float(pop.clip_coef), float(pop.vf_coef), float(pop.ent_coef), float(pop.max_grad_norm),
-                  self.loss.data_ptr(), self.ws.data_ptr(), _lib.stream())
+                  pop.log_probs.data_ptr(), pop.advantages.data_ptr(), pop.adv_stats.data_ptr(),
+                  pop.returns.data_ptr(), pop.values.data_ptr(), pop.S, perms.data_ptr(), pop.update_epochs,
+                  pop.batch_size, float(pop.clip_coef), float(pop.vf_coef), float(pop.ent_coef),
+                  float(pop.max_grad_norm), self.loss.data_ptr(), self.ws.data_ptr(), _lib.stream())
         opt.step_count += pop.update_epochs * pop.n_minibatches()
         return self.loss
 
@@ -88,3 +90,12 @@ def fused_learn(pop, perms=None) -> torch.Tensor:
     if getattr(pop, "_fused", None) is None:
         pop._fused = FusedLearner(pop)
     return pop._fused.learn(pop, perms)
+
+
+def policy_step(pop, desc: AgxPPONet, obs: torch.Tensor, obs_agent_stride: int, *, sample: bool, counter: int,
+                actions=None, log_probs=None, values=None, entropy=None, out_agent_stride: int = 0,
+                actions_flat=None) -> None:
+    """agx_ppo_act over all P agents x N envs (PPO.get_action, ppo.py:567-633)."""
+    _lib.call("agx_ppo_act", ctypes.byref(desc), pop.P, pop.N, pop.params.data.data_ptr(), obs.data_ptr(),
+              obs_agent_stride, 1 if sample else 0, pop.act_seed, counter, _lib.ptr(actions), _lib.ptr(log_probs),
+              _lib.ptr(values), _lib.ptr(entropy), out_agent_stride, _lib.ptr(actions_flat), None, _lib.stream())

@@ -83,6 +83,9 @@ class PPOPopulation:
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(int(seeds[0]) * 7919 + 17)
         self.fused = fused
+        self.act_seed = (int(seeds[0]) * 0x9E3779B97F4A7C15 + 0x5851F42D) & 0xFFFFFFFFFFFFFFFF
+        self.act_counter = 0
+        self._desc = None
         self._alloc_rollout()
         self.learn_steps = 0
 
@@ -113,6 +116,39 @@ class PPOPopulation:
         logp = logp_all.gather(-1, action.unsqueeze(-1)).squeeze(-1)
         return action, logp, ent, value
 
+    def fused_descriptor(self):
+        """agx_ppo_net for this architecture, or None when the fused kernels do
+        not cover it (then the plain-PyTorch forward / learner run)."""
+        if not self.fused:
+            return None
+        if self._desc is None:
+            from .learner import net_descriptor
+
+            self._desc = net_descriptor(self.spec) or False
+        return self._desc or None
+
+    @torch.no_grad()
+    def act_into(self, t: int, actions_flat: torch.Tensor | None = None) -> None:
+        """Rollout policy step for slot t: reads obs[:, t], writes actions /
+        log_probs / values[:, t] in place (and a contiguous [P*N] copy of the
+        actions for the host env step)."""
+        desc = self.fused_descriptor()
+        if desc is None:
+            action, logp, _ent, value = self.act(self.obs[:, t])
+            self.actions[:, t].copy_(action)
+            self.values[:, t].copy_(value)
+            self.log_probs[:, t].copy_(logp)
+            if actions_flat is not None:
+                actions_flat.copy_(action.view(-1))
+            return
+        from .learner import policy_step
+
+        self.act_counter += 1
+        TN = self.T * self.N
+        policy_step(self, desc, self.obs[:, t], TN * self.spec.obs_dim, sample=True, counter=self.act_counter,
+                    actions=self.actions[:, t], log_probs=self.log_probs[:, t], values=self.values[:, t],
+                    out_agent_stride=TN, actions_flat=actions_flat)
+
     @torch.no_grad()
     def store(self, t: int, obs, action, reward, done, value, logp):
         self.obs[:, t].copy_(obs, non_blocking=True)
@@ -135,13 +171,10 @@ class PPOPopulation:
         """One PPO update of every agent; returns the reference's mean_loss per
         agent (device tensor [P], no host sync)."""
         self.learn_steps += 1
-        if self.fused and self.target_kl is None:
-            from .learner import fused_learn, net_descriptor
+        if self.target_kl is None and self.fused_descriptor() is not None:
+            from .learner import fused_learn
 
-            if getattr(self, "_fused_ok", None) is None:
-                self._fused_ok = net_descriptor(self.spec) is not None
-            if self._fused_ok:
-                return fused_learn(self)
+            return fused_learn(self)
         return self._learn_torch()
 
     def minibatch_plan(self):

@@ -26,6 +26,7 @@ class PopulationRunner:
         self.done_h = torch.zeros(P * N, dtype=torch.bool, **pin)
         self.term_h = torch.zeros(P * N, dtype=torch.bool, **pin)
         self.act_h = torch.zeros(P * N, dtype=torch.int64, **pin)
+        self.act_d = torch.zeros(P * N, dtype=torch.int64, device=pop.device)
         self.last_obs = torch.zeros(P, N, D, dtype=torch.float32, device=pop.device)
         self.last_done = torch.zeros(P, N, dtype=torch.uint8, device=pop.device)
         self.ev = torch.cuda.Event()
@@ -48,13 +49,9 @@ class PopulationRunner:
             self.started = True
         pop.obs[:, 0].copy_(self.last_obs)
         for t in range(T):
-            cur = pop.obs[:, t]
-            action, logp, _ent, value = pop.act(cur)
-            self.act_h.copy_(action.view(-1), non_blocking=True)
+            pop.act_into(t, self.act_d)
+            self.act_h.copy_(self.act_d, non_blocking=True)
             self.ev.record()
-            pop.actions[:, t].copy_(action)
-            pop.values[:, t].copy_(value)
-            pop.log_probs[:, t].copy_(logp)
             self.ev.synchronize()
             _, _, term, trunc, _ = env.step(self.act_h.numpy(), out_obs=self.obs_h.numpy(),
                                             out_rew=self.rew_h.numpy(), out_done=self.done_h.numpy())

@@ -86,8 +86,9 @@ int agx_ppo_loss_fwd_bwd(const float *logp, const float *old_logp, const float *
  * [encoder | actor head | critic head] in state-dict order.
  * Supported: 2-3 encoder Linear layers (hidden: LayerNorm(affine)+ReLU,
  * output: LayerNorm(plain)+ReLU), one hidden layer per head (LN affine +
- * ReLU), widths multiples of 16 (<= 128, heads <= 256 together),
- * obs_dim <= 128, n_actions <= 16; otherwise AGX_EUNSUPPORTED. */
+ * ReLU), widths multiples of 16 (<= 128, heads <= 128 together),
+ * obs_dim <= 128, n_actions <= 16, <= 14336 parameters and the LDS plan
+ * within 160 KiB; otherwise AGX_EUNSUPPORTED. */
 typedef struct agx_ppo_net {
     int32_t obs_dim, n_actions, n_enc;
     int32_t enc_dim[4]; /* enc_dim[0] = obs_dim, enc_dim[i] = width of encoder layer i */
@@ -100,24 +101,39 @@ typedef struct agx_ppo_net {
 
 /* LDS bytes the fused learner needs for `net` (0: unsupported). */
 size_t agx_ppo_learn_lds_bytes(const agx_ppo_net *net);
-/* Device workspace bytes for agx_ppo_learn_prepare / agx_ppo_learn. */
-size_t agx_ppo_learn_workspace_bytes(const agx_ppo_net *net);
-/* One-time: upload the gradient-ownership table into `workspace`
- * (synchronises `stream`; call outside any graph capture). */
+/* Device workspace bytes for agx_ppo_learn (plan + minibatch-ordered copy
+ * of the rollout for `epochs` epochs of P agents x S samples). */
+size_t agx_ppo_learn_workspace_bytes(const agx_ppo_net *net, int64_t P, int64_t S, int64_t epochs);
+/* One-time: upload the kernel plan into `workspace` (synchronises `stream`;
+ * call outside any graph capture).  Also required by agx_ppo_act. */
 int agx_ppo_learn_prepare(const agx_ppo_net *net, void *workspace, void *stream);
 /* params / exp_avg / exp_avg_sq: [P][n_params] (updated in place);
  * lr: device f32 [P]; Adam steps adam_step0+1 ... are used for the
  * epochs*ceil(S/batch) updates; obs [P][S][obs_dim], actions int64 [P][S],
- * old_logp / adv (already normalised) / ret / old_value f32 [P][S];
- * perms int64 [epochs][P][S] (each row a permutation of 0..S-1);
- * loss_out f32 [P] = sum of minibatch losses / (S * epochs) (ppo.py:920). */
+ * old_logp / adv / ret / old_value f32 [P][S]; adv_stats f64 [P][2]
+ * (mean, unbiased std from agx_gae) normalises adv on the fly, or NULL when
+ * adv is already normalised; perms int64 [epochs][P][S] (each row a
+ * permutation of 0..S-1); loss_out f32 [P] = sum of minibatch losses /
+ * (S * epochs) (ppo.py:920). */
 int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, float *exp_avg,
                   float *exp_avg_sq, const float *lr, float beta1, float beta2, float eps,
                   int64_t adam_step0, const float *obs, const int64_t *actions,
-                  const float *old_logp, const float *adv, const float *ret,
-                  const float *old_value, int64_t S, const int64_t *perms, int64_t epochs,
-                  int64_t batch, float clip_coef, float vf_coef, float ent_coef,
+                  const float *old_logp, const float *adv, const double *adv_stats,
+                  const float *ret, const float *old_value, int64_t S, const int64_t *perms,
+                  int64_t epochs, int64_t batch, float clip_coef, float vf_coef, float ent_coef,
                   float max_grad_norm, float *loss_out, void *workspace, void *stream);
+/* Rollout policy step (PPO.get_action / _get_action_and_values, ppo.py:
+ * 400-633) for all P agents x N envs: obs of agent p, env n at
+ * obs + p*obs_agent_stride + n*obs_dim; writes (each output may be NULL)
+ * actions int64, log_probs, values, entropy at + p*out_agent_stride + n and
+ * actions_flat[p*N + n].  sample=1: Gumbel-max draw from Philox4x32-10
+ * keyed by seed, counter = (env index, step counter); sample=0: argmax.
+ * `workspace` as prepared by agx_ppo_learn_prepare. */
+int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
+                const float *obs, int64_t obs_agent_stride, int sample, uint64_t seed,
+                uint64_t counter, int64_t *actions, float *log_probs, float *values,
+                float *entropy, int64_t out_agent_stride, int64_t *actions_flat,
+                void *workspace, void *stream);
 
 /* ---- prioritized replay segment trees -----------------------------------
  * Replaces SumSegmentTree / MinSegmentTree (agilerl/components/
@@ -198,6 +214,11 @@ int agx_polyak(float *target, const float *online, int64_t n, float tau, void *s
  * out[i] = correctly rounded pow(x[i], y[i]) (the routine the PER leaves and
  * IS weights use); for parity tests against libm / high-precision values. */
 int agx_debug_pow(const double *x, const double *y, double *out, int64_t n, void *stream);
+/* Fused-learner phase timing: subsequent agx_ppo_learn calls write shader
+ * cycle stamps of agent 0's first minibatch into buf (device int64[80]:
+ * [sub_batch*16 + phase], phases 0-8 per sub-batch, 9-11 at slot 64+);
+ * buf = NULL disables. */
+int agx_debug_learn_stamps(int64_t *buf);
 
 #ifdef __cplusplus
 }

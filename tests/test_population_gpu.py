@@ -119,3 +119,71 @@ def test_runner_iteration_end_to_end():
     assert len(parents) == 4 and all(0 <= p < 4 for p in parents)
     for i, par in enumerate(parents):
         assert torch.equal(pop.params.data[i], pop.params.data[i]) and par >= 0
+
+
+@pytest.mark.parametrize("P,N", [(3, 16), (2, 45), (8, 1)])
+def test_policy_step_matches_torch_forward(P, N):
+    """agx_ppo_act vs the plain-PyTorch forward of the stacked networks:
+    values, entropy, log-prob of the chosen action; greedy mode = argmax."""
+    from agilerl_amd.population.learner import policy_step
+    from agilerl_amd.population.nets import categorical
+
+    pop = _pop(P=P, N=N, learn_step=4 * N, batch=4 * N)
+    desc = pop.fused_descriptor()
+    assert desc is not None
+    obs = torch.randn(P, N, 8, device=DEV)
+    logits, value = pop.spec.forward(pop.params.data, obs)
+    logp_all, ent = categorical(logits)
+    outs = dict(actions=torch.empty(P, N, dtype=torch.int64, device=DEV),
+                log_probs=torch.empty(P, N, device=DEV), values=torch.empty(P, N, device=DEV),
+                entropy=torch.empty(P, N, device=DEV), actions_flat=torch.empty(P * N, dtype=torch.int64, device=DEV))
+    for sample in (False, True):
+        policy_step(pop, desc, obs, N * 8, sample=sample, counter=7, out_agent_stride=N, **outs)
+        torch.cuda.synchronize()
+        a = outs["actions"]
+        assert torch.equal(a.view(-1), outs["actions_flat"])
+        if not sample:
+            assert torch.equal(a, logits.argmax(-1))
+        lp = logp_all.gather(-1, a.unsqueeze(-1)).squeeze(-1)
+        torch.testing.assert_close(outs["log_probs"], lp, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(outs["values"], value, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(outs["entropy"], ent, rtol=1e-4, atol=1e-5)
+
+
+def test_policy_step_sampling_distribution():
+    """Gumbel-max draws follow softmax(logits): chi-square over many counters."""
+    from agilerl_amd.population.learner import policy_step
+
+    P, N = 2, 256
+    pop = _pop(P=P, N=N, learn_step=N, batch=N)
+    desc = pop.fused_descriptor()
+    obs = torch.randn(P, 1, 8, device=DEV).expand(P, N, 8).contiguous()
+    probs = torch.softmax(pop.spec.forward(pop.params.data, obs[:, :1])[0], -1)[:, 0]  # [P, A]
+    counts = torch.zeros(P, 4, device=DEV)
+    act = torch.empty(P, N, dtype=torch.int64, device=DEV)
+    R = 64
+    for c in range(R):
+        policy_step(pop, desc, obs, N * 8, sample=True, counter=1000 + c, actions=act, out_agent_stride=N)
+        counts += torch.nn.functional.one_hot(act, 4).sum(1).float()
+    n = R * N
+    exp = probs * n
+    chi2 = (((counts - exp) ** 2) / exp).sum(-1).cpu().numpy()
+    assert (chi2 < 25.0).all(), (chi2, probs)  # 3 dof: P(chi2 > 25) ~ 1.6e-5
+
+
+def test_policy_step_rejects_unsupported_shape():
+    from agilerl_amd import _lib
+    from agilerl_amd.population.learner import AgxPPONet
+
+    d = AgxPPONet()
+    d.obs_dim, d.n_actions, d.n_enc = 7, 3, 2
+    lib = _lib.load()
+    rc = lib.agx_ppo_act(ctypes_byref(d), 1, 1, None, None, 0, 0, 0, 0, None, None, None, None, 0, None, None,
+                         None)
+    assert rc != 0
+
+
+def ctypes_byref(x):
+    import ctypes
+
+    return ctypes.byref(x)

@@ -1,0 +1,44 @@
+"""Phase timing of the fused learner (diagnostic; uses agx_debug_learn_stamps).
+
+Slots (learner.hip AGX_STAMP): sub-batch k of agent 0's first minibatch at
+k*16 + {0 start, 1 gathered, 2 forward, 3 loss, 4 out-layer bwd, 5 head LN bwd,
+6 head dW/dX, 7 encoder bwd}; 64+9 gradients dumped, 64+10 Adam done."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from agilerl_amd import _lib  # noqa: E402
+from agilerl_amd.envs import SyntheticVecEnv  # noqa: E402
+from agilerl_amd.population.nets import ActorCriticSpec  # noqa: E402
+from agilerl_amd.population.ppo_pop import PPOPopulation  # noqa: E402
+from agilerl_amd.population.runner import PopulationRunner  # noqa: E402
+
+P, N = int(os.environ.get("P", 8)), int(os.environ.get("N", 128))
+spec = ActorCriticSpec(obs_dim=8, n_actions=4)
+pop = PPOPopulation(spec, P, N, learn_step=2048, batch_size=128, update_epochs=4, device="cuda")
+runner = PopulationRunner(pop, SyntheticVecEnv(P * N))
+runner.iteration()
+buf = torch.zeros(80, dtype=torch.int64, device="cuda")
+lib = _lib.load()
+lib.agx_debug_learn_stamps(buf.data_ptr())
+runner.collect()
+pop.finish_rollout(runner.last_obs, runner.last_done)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+pop.learn()
+torch.cuda.synchronize()
+t1 = time.perf_counter()
+lib.agx_debug_learn_stamps(None)
+st = buf.cpu().tolist()
+nmb = pop.update_epochs * pop.n_minibatches()
+print(f"learn() wall {1e3 * (t1 - t0):.3f} ms  ({nmb} minibatch updates per agent, {P} agents)")
+names = ["gather", "fwd", "loss", "out bwd", "head LN bwd", "head dW+dX", "enc bwd"]
+for sb in range(4):
+    row = st[sb * 16: sb * 16 + 8]
+    seg = [row[i + 1] - row[i] for i in range(7)]
+    print(f"sb{sb}: " + "  ".join(f"{n}={c}" for n, c in zip(names, seg)) + f"  total={row[7] - row[0]}")
+print("dump", st[64 + 9] - st[3 * 16 + 7], "norm+adam", st[64 + 10] - st[64 + 9],
+      "minibatch total cycles", st[64 + 10] - st[0])
