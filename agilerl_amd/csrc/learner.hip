@@ -45,6 +45,7 @@
 //     of the parameter region (aliasing the dead activations), two-group
 //     norm, Adam from registers.
 #include <cmath>
+#include <cstdlib>
 
 #include "agx_common.h"
 
@@ -86,6 +87,7 @@ struct LearnPlan {
     int l_red, red_e[3], red_h, l_stat;
     int l_grad;  // gradient image of [0, param_end) (aliases the activations)
     int lds_floats, act_floats;
+    int slab;  // floats per cross-workgroup gradient slab (parameter image + loss)
     // dW tiles per layer group g: enc 0..ne-1, head ne, out-actor ne+1, out-critic ne+2
     int nt[6], ncol[6], slot0[6], nslot[6], nslots;
     int nblk;
@@ -199,6 +201,7 @@ constexpr LearnPlan make_plan(NetDims d) {
     pl.l_stat = off; off += 4 * kNW;
     pl.lds_floats = off;
     if (pl.lds_floats * 4 > 160 * 1024) return pl;
+    pl.slab = rup(pl.param_end + 1, 64);
     // ---- dW tile groups
     int slot = 0;
     for (int g = 0; g < pl.ne + 3; ++g) {
@@ -514,11 +517,16 @@ struct LearnArgs {
     float clip, vf, ent, max_norm;
     float *loss_out;
     long long *stamps;
+    int K;                // workgroups per agent (data-parallel over sub-batches)
+    float *slabs;         // [P][2][K][slab] gradient hand-off (double-buffered)
+    unsigned *cnt;        // [P] arrival counters, [P] = timeout word (zeroed per call)
 };
+
+constexpr unsigned kSpinMax = 1u << 22;  // ~ seconds of s_sleep polling: a missing partner is a bug
 
 #define AGX_STAMP(slot)                                                          \
     do {                                                                         \
-        if (g.stamps && p == 0 && e == 0 && mb == 0 && tid == 0 && (slot) < 80) \
+        if (g.stamps && b == 0 && e == 0 && mb == 0 && tid == 0 && (slot) < 80) \
             g.stamps[(slot)] = (long long)__builtin_readcyclecounter(); \
     } while (0)
 
@@ -529,7 +537,10 @@ template <class C>
 __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     constexpr LearnPlan pl = C::plan;
-    const int p = blockIdx.x;
+    // block b -> agent b % P, partner kk = b / P: with P % 8 == 0 an agent's K
+    // workgroups share an XCD under round-robin dispatch (speed only)
+    const int b = blockIdx.x;
+    const int p = b % g.P, kk = b / g.P;
     const int tid = threadIdx.x;
     float *gp = g.params + (size_t)p * pl.n;
     float *gm = g.m + (size_t)p * pl.n;
@@ -582,9 +593,10 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             for (int i = tid; i < pl.l_stat - pl.l_red; i += kNT) sm[pl.l_red + i] = 0.f;
             float lsum = 0.f;
 
-            for (int sb = 0; sb < bsz; sb += kSB) {
+            for (int sb = kk * kSB; sb < bsz; sb += g.K * kSB) {
                 const int nrow = bsz - sb < kSB ? bsz - sb : kSB;
-                const int stb = sb < 4 * kSB ? (sb / kSB) * 16 : 80;
+                const int jsb = (sb / kSB) / g.K;
+                const int stb = jsb < 4 ? jsb * 16 : 80;
                 const int tid = vtid();
                 AGX_STAMP(stb + 0);
                 // ---- P0: contiguous gather of the sub-batch -------------------
@@ -923,6 +935,60 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             vdump(IC(pl.ne));
             AGX_STAMP(64 + 9);
             __syncthreads();
+            float lmb;
+            {
+                AGX_IDS;
+                lmb = block_sum(lsum, stat, 2, lane, wave);
+            }
+            if (g.K > 1) {
+                // ---- P9b: exchange partial gradients with the agent's partners --------
+                // (MI355X_MICROARCH visibility rules: plain stores -> vmcnt drain ->
+                // barrier -> agent release -> ticket; relaxed poll -> ONE agent acquire)
+                const int upd = e * nmb + mb;
+                float *base = g.slabs + ((size_t)p * 2 + (upd & 1)) * g.K * pl.slab;
+                float *mine = base + (size_t)kk * pl.slab;
+                for (int i = tid; i < pl.param_end / 4; i += kNT)
+                    reinterpret_cast<f4 *>(mine)[i] = reinterpret_cast<const f4 *>(G)[i];
+                if (tid == 0) mine[pl.param_end] = lmb;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_fetch_add(g.cnt + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned target = (unsigned)(g.K * (upd + 1));
+                    unsigned spins = 0;
+                    int ok = 1;
+                    while (__hip_atomic_load(g.cnt + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++spins > kSpinMax) {
+                            __hip_atomic_store(g.cnt + g.P, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            ok = 0;
+                            break;
+                        }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    stat[3 * kNW] = ok ? 1.f : 0.f;
+                }
+                __syncthreads();
+                if (stat[3 * kNW] == 0.f) return;  // partner never arrived: timeout word set, whole block exits
+                // fixed-order sum over partners: every workgroup of the agent computes
+                // bit-identical totals, hence bit-identical parameters after Adam
+                for (int i = tid; i < pl.param_end / 4; i += kNT) {
+                    f4 t = reinterpret_cast<const f4 *>(base)[i];
+                    for (int q = 1; q < g.K; ++q) t += reinterpret_cast<const f4 *>(base + (size_t)q * pl.slab)[i];
+                    reinterpret_cast<f4 *>(G)[i] = t;
+                }
+                // (loss words via vector atomics: a uniform plain load would take the
+                // scalar-cache path, which the acquire does not invalidate)
+                float lt = __hip_atomic_load(base + pl.param_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (int q = 1; q < g.K; ++q)
+                    lt += __hip_atomic_load(base + (size_t)q * pl.slab + pl.param_end, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+                lmb = lt;
+                __syncthreads();
+            }
 
             // ---- P10: two-group norm, Adam from registers -------------------------
             float n0 = 0.f, n1 = 0.f;
@@ -938,7 +1004,6 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             AGX_IDS;
             const float t0 = block_sum(n0, stat, 0, lane, wave);
             const float t1 = block_sum(n1, stat, 1, lane, wave);
-            const float lmb = block_sum(lsum, stat, 2, lane, wave);
             if (tid == 0) loss_total += lmb;
             const float c0 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t0) + 1e-6f), 1.f) : 1.f;
             const float c1 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t1) + 1e-6f), 1.f) : 1.f;
@@ -962,7 +1027,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
         }  // minibatches
     }      // epochs
 
-    // ---- write parameters and moments back --------------------------------------
+    // ---- write parameters and moments back (partners hold identical copies) ------
+    if (kk != 0) return;
 #pragma unroll
     for (int i = 0; i < kMaxPT; ++i) {
         const int l = tid + kNT * i;
@@ -1115,18 +1181,18 @@ static bool dims_match(const agx_ppo_net *net, const NetDims &d) {
 
 struct Launcher {
     const LearnPlan *plan;
-    void (*learn)(const LearnArgs &, int P, size_t lds, hipStream_t);
+    void (*learn)(const LearnArgs &, int nblocks, size_t lds, hipStream_t);
     void (*act)(const ActArgs &, dim3 grid, size_t lds, hipStream_t);
 };
 
 template <class C>
-static void launch_learn(const LearnArgs &a, int P, size_t lds, hipStream_t s) {
+static void launch_learn(const LearnArgs &a, int nblocks, size_t lds, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    ppo_learn_kernel<C><<<(unsigned)P, kNT, lds, s>>>(a);
+    ppo_learn_kernel<C><<<(unsigned)nblocks, kNT, lds, s>>>(a);
 }
 template <class C>
 static void launch_act(const ActArgs &a, dim3 grid, size_t lds, hipStream_t s) {
@@ -1169,11 +1235,50 @@ extern "C" size_t agx_ppo_learn_lds_bytes(const agx_ppo_net *net) {
     return (size_t)L.plan->lds_floats * sizeof(float);
 }
 
+// Workgroups per agent: the learner spreads an agent's sub-batches over up to
+// 4 partner workgroups (one CU each) when the population leaves CUs idle.
+static int cu_count() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                ? prop.multiProcessorCount
+                : 256;
+        if (n <= 0) n = 256;
+    }
+    return n;
+}
+static int max_partners(int64_t P) {
+    int k = 4;
+    if (const char *e = getenv("AGX_LEARN_SPLIT")) k = atoi(e);
+    if (k < 1) k = 1;
+    if (k > 8) k = 8;
+    const int64_t fit = cu_count() / (P > 0 ? P : 1);  // all partners co-resident, 1 block per CU
+    if (fit < k) k = fit < 1 ? 1 : (int)fit;
+    return k;
+}
+struct LearnWs {
+    size_t cnt, gobs, gact, grow, slabs, total;
+};
+static LearnWs learn_ws(const LearnPlan &pl, int64_t P, int64_t S, int64_t epochs) {
+    LearnWs w;
+    const size_t per = (size_t)epochs * P * S;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    w.cnt = 0;
+    w.gobs = up(((size_t)P + 1) * 4);
+    w.gact = w.gobs + up(per * pl.D * 4);
+    w.grow = w.gact + up(per * 4);
+    w.slabs = w.grow + up(per * 4 * 4);
+    const int K = max_partners(P);
+    w.total = w.slabs + (K > 1 ? (size_t)P * 2 * K * pl.slab * 4 : 0);
+    return w;
+}
+
 extern "C" size_t agx_ppo_learn_workspace_bytes(const agx_ppo_net *net, int64_t P, int64_t S, int64_t epochs) {
     Launcher L;
-    if (!find_launcher(net, L)) return 0;
-    const size_t per = (size_t)epochs * P * S;
-    return 256 + per * (size_t)L.plan->D * 4 + ((per * 4 + 255) & ~(size_t)255) + per * 4 * 4;
+    if (!find_launcher(net, L) || P <= 0 || S <= 0 || epochs <= 0) return 0;
+    return learn_ws(*L.plan, P, S, epochs).total;
 }
 
 extern "C" int agx_debug_learn_stamps(int64_t *buf) {
@@ -1213,11 +1318,19 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, f
     }
     const LearnPlan &pl = *L.plan;
     hipStream_t s = as_stream(stream);
-    const size_t per = (size_t)epochs * P * S;
+    const LearnWs w = learn_ws(pl, P, S, epochs);
     char *ws = static_cast<char *>(workspace);
-    float *gobs = reinterpret_cast<float *>(ws + 256);
-    int *gact = reinterpret_cast<int *>(ws + 256 + per * pl.D * 4);
-    float *grow = reinterpret_cast<float *>(ws + 256 + per * pl.D * 4 + ((per * 4 + 255) & ~(size_t)255));
+    float *gobs = reinterpret_cast<float *>(ws + w.gobs);
+    int *gact = reinterpret_cast<int *>(ws + w.gact);
+    float *grow = reinterpret_cast<float *>(ws + w.grow);
+    const int64_t nsb = (batch + kSB - 1) / kSB;
+    int K = max_partners(P);
+    if (K > nsb) K = (int)nsb;
+    AGX_REQUIRE(P * K <= 65535, "agx_ppo_learn: too many workgroups");
+    if (K > 1) {
+        // counters + timeout word: one 16-byte-multiple block at the workspace start
+        if (hipMemsetAsync(ws, 0, w.gobs, s) != hipSuccess) return check_launch("agx_ppo_learn memset");
+    }
     dim3 ggrid((unsigned)ceil_div(S, 256), (unsigned)(epochs * P));
     ppo_gather_kernel<<<ggrid, 256, 0, s>>>(obs, reinterpret_cast<const long long *>(actions), old_logp, adv, ret,
                                             old_value, adv_stats, reinterpret_cast<const long long *>(perms), S,
@@ -1246,7 +1359,10 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, f
     a.max_norm = max_grad_norm;
     a.loss_out = loss_out;
     a.stamps = g_stamps_ptr();
-    L.learn(a, (int)P, (size_t)pl.lds_floats * sizeof(float), s);
+    a.K = K;
+    a.slabs = reinterpret_cast<float *>(ws + w.slabs);
+    a.cnt = reinterpret_cast<unsigned *>(ws);
+    L.learn(a, (int)(P * K), (size_t)pl.lds_floats * sizeof(float), s);
     return check_launch("agx_ppo_learn");
 }
 
