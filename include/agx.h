@@ -101,11 +101,14 @@ typedef struct agx_ppo_net {
 
 /* LDS bytes the fused learner needs for `net` (0: unsupported). */
 size_t agx_ppo_learn_lds_bytes(const agx_ppo_net *net);
-/* Device workspace bytes for agx_ppo_learn (plan + minibatch-ordered copy
- * of the rollout for `epochs` epochs of P agents x S samples). */
+/* Device workspace bytes for agx_ppo_learn: arrival counters, the
+ * minibatch-ordered copy of the rollout for `epochs` epochs of P agents x S
+ * samples, and the gradient hand-off slabs of the partner workgroups (an
+ * agent's sub-batches are spread over up to 4 workgroups when P leaves CUs
+ * idle; AGX_LEARN_SPLIT=1..8 overrides the cap). */
 size_t agx_ppo_learn_workspace_bytes(const agx_ppo_net *net, int64_t P, int64_t S, int64_t epochs);
-/* One-time: upload the kernel plan into `workspace` (synchronises `stream`;
- * call outside any graph capture).  Also required by agx_ppo_act. */
+/* Validates that `net` is one of the instantiated shapes (the kernel plan is
+ * compile-time); no device work.  AGX_EUNSUPPORTED otherwise. */
 int agx_ppo_learn_prepare(const agx_ppo_net *net, void *workspace, void *stream);
 /* params / exp_avg / exp_avg_sq: [P][n_params] (updated in place);
  * lr: device f32 [P]; Adam steps adam_step0+1 ... are used for the
@@ -128,7 +131,7 @@ int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, float *exp_a
  * actions int64, log_probs, values, entropy at + p*out_agent_stride + n and
  * actions_flat[p*N + n].  sample=1: Gumbel-max draw from Philox4x32-10
  * keyed by seed, counter = (env index, step counter); sample=0: argmax.
- * `workspace` as prepared by agx_ppo_learn_prepare. */
+ * `workspace` is unused (may be NULL). */
 int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
                 const float *obs, int64_t obs_agent_stride, int sample, uint64_t seed,
                 uint64_t counter, int64_t *actions, float *log_probs, float *values,
