@@ -38,6 +38,7 @@ SIGNATURES = {
                              _I, _F, _F, _F, _F, _P, _P, _P]),
     "agx_ppo_act": (_INT, [_P, _I, _I, _P, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P, _I,
                            _P, _P, _P]),
+    "agx_ppo_rollout_step": (_INT, [_P, _I, _I, _P, _P, _INT, _INT, ctypes.c_uint64, ctypes.c_uint64, _P]),
     "agx_per_workspace_bytes": (_SZ, [_I, _I]),
     "agx_per_init": (_INT, [_P, _P, _I, _P]),
     "agx_per_add": (_INT, [_P, _P, _I, _I, _I, _I, _D, _P, _P, _P]),

@@ -501,6 +501,7 @@ struct Fwd {
 template <class C>
 __device__ void load_params(float *sm, const float *gp, int tid) {
     constexpr LearnPlan pl = C::plan;
+#pragma unroll 8
     for (int f = tid; f < pl.n; f += kNT) sm[flat_to_lds<C>(f)] = gp[f];
 }
 
@@ -1103,6 +1104,18 @@ struct ActArgs {
     float *logp_out, *value_out, *ent_out;
     long long out_pstride;
     long long *act_flat;  // [P*N] contiguous copy (host staging) or null
+    int act;              // 0: scatter only (the step after the last action)
+    // rollout bookkeeping fused into the policy step (agx_ppo_rollout_step)
+    float *obs_copy;      // obs also written here (rollout slot t), agent stride obs_copy_pstride
+    long long obs_copy_pstride;
+    const float *st_rew;  // [P*N] reward / done of the previous vector step, or null
+    const unsigned char *st_done;
+    float *rew_prev;      // rollout slot t-1, agent stride prev_pstride
+    unsigned char *done_prev;
+    long long prev_pstride;
+    float *scores;        // [P*N] running episode score (on_policy.py:147-172), or null
+    double *ret_sum;      // [P*N] sum of finished-episode returns
+    long long *episodes;  // [P*N] finished-episode count
 };
 
 template <class C>
@@ -1111,11 +1124,33 @@ __global__ __launch_bounds__(kNT, 1) void ppo_act_kernel(ActArgs g) {
     constexpr LearnPlan pl = C::plan;
     const int p = blockIdx.y, n0 = blockIdx.x * kSB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nrow = g.N - n0 < kSB ? g.N - n0 : kSB;
+    if (g.st_rew && tid < nrow) {  // reward/done of the previous step -> slot t-1, episode accounting
+        const int env = n0 + tid;
+        const size_t idx = (size_t)p * g.N + env;
+        const float rw = g.st_rew[idx];
+        const unsigned char dn = g.st_done[idx];
+        g.rew_prev[(size_t)p * g.prev_pstride + env] = rw;
+        g.done_prev[(size_t)p * g.prev_pstride + env] = dn;
+        if (g.scores) {
+            float sc = g.scores[idx] + rw;
+            if (dn) {
+                g.ret_sum[idx] += (double)sc;
+                g.episodes[idx] += 1;
+                sc = 0.f;
+            }
+            g.scores[idx] = sc;
+        }
+    }
+    const float *ob = g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * pl.D;
+    if (g.obs_copy) {
+        float *oc = g.obs_copy + (size_t)p * g.obs_copy_pstride + (size_t)n0 * pl.D;
+        for (int i = tid; i < nrow * pl.D; i += kNT) oc[i] = ob[i];
+    }
+    if (!g.act) return;
     for (int i = tid; i < pl.act_floats; i += kNT) sm[i] = 0.f;
     __syncthreads();
     load_params<C>(sm, g.params + (size_t)p * pl.n, tid);
-    const int nrow = g.N - n0 < kSB ? g.N - n0 : kSB;
-    const float *ob = g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * pl.D;
     for (int i = tid; i < kSB * pl.D; i += kNT) {
         const int r = i / pl.D, d = i % pl.D;
         sm[pl.l_x0 + r * pl.ld_x0 + d] = r < nrow ? ob[i] : 0.f;
@@ -1392,7 +1427,63 @@ extern "C" int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const f
     a.ent_out = entropy;
     a.out_pstride = out_agent_stride;
     a.act_flat = reinterpret_cast<long long *>(actions_flat);
+    a.act = 1;
+    a.obs_copy = nullptr;
+    a.obs_copy_pstride = 0;
+    a.st_rew = nullptr;
+    a.st_done = nullptr;
+    a.rew_prev = nullptr;
+    a.done_prev = nullptr;
+    a.prev_pstride = 0;
+    a.scores = nullptr;
+    a.ret_sum = nullptr;
+    a.episodes = nullptr;
     dim3 grid((unsigned)ceil_div(N, kSB), (unsigned)P);
     L.act(a, grid, (size_t)L.plan->act_floats * sizeof(float), as_stream(stream));
     return check_launch("agx_ppo_act");
+}
+
+extern "C" int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
+                                    const agx_rollout_io *io, int act, int sample, uint64_t seed,
+                                    uint64_t counter, void *stream) {
+    AGX_REQUIRE(net && io && io->stage_obs && P > 0 && N > 0 && P <= 65535, "agx_ppo_rollout_step: bad arguments");
+    AGX_REQUIRE(!act || (params && io->actions_flat), "agx_ppo_rollout_step: act needs params and actions_flat");
+    AGX_REQUIRE(!io->stage_rew || (io->stage_done && io->rewards_prev && io->dones_prev),
+                "agx_ppo_rollout_step: previous-step scatter needs rewards/dones slots");
+    AGX_REQUIRE(!io->scores || (io->stage_rew && io->return_sum && io->episodes),
+                "agx_ppo_rollout_step: episode accounting needs return_sum, episodes and stage rewards");
+    Launcher L;
+    if (!find_launcher(net, L)) {
+        set_error("agx_ppo_rollout_step: network shape not instantiated");
+        return AGX_EUNSUPPORTED;
+    }
+    ActArgs a;
+    a.params = params;
+    a.obs = io->stage_obs;
+    a.obs_pstride = N * (int64_t)L.plan->D;
+    a.N = (int)N;
+    a.P = (int)P;
+    a.sample = sample;
+    a.seed = seed;
+    a.counter = counter;
+    a.act_out = reinterpret_cast<long long *>(io->actions);
+    a.logp_out = io->log_probs;
+    a.value_out = io->values;
+    a.ent_out = nullptr;
+    a.out_pstride = io->slot_agent_stride;
+    a.act_flat = reinterpret_cast<long long *>(io->actions_flat);
+    a.act = act;
+    a.obs_copy = io->obs_slot;
+    a.obs_copy_pstride = io->obs_agent_stride;
+    a.st_rew = io->stage_rew;
+    a.st_done = io->stage_done;
+    a.rew_prev = io->rewards_prev;
+    a.done_prev = io->dones_prev;
+    a.prev_pstride = io->slot_agent_stride;
+    a.scores = io->scores;
+    a.ret_sum = io->return_sum;
+    a.episodes = reinterpret_cast<long long *>(io->episodes);
+    dim3 grid((unsigned)ceil_div(N, kSB), (unsigned)P);
+    L.act(a, grid, (size_t)L.plan->act_floats * sizeof(float), as_stream(stream));
+    return check_launch("agx_ppo_rollout_step");
 }

@@ -35,8 +35,7 @@ class PopulationSync:
         r = self.runner
         f = torch.where(r.episodes > 0, r.episode_return_sum / r.episodes.clamp(min=1).double(),
                         torch.full_like(r.episode_return_sum, -1e9))
-        r.episode_return_sum.zero_()
-        r.episodes.zero_()
+        r.reset_episode_stats()
         return f
 
     def _all_gather(self, x: torch.Tensor) -> torch.Tensor:

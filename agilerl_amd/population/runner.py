@@ -1,17 +1,55 @@
 """Host env workers <-> HBM rollout SoA for a whole population.
 
-One vector step of every agent = one batched inference launch sequence on the
-GPU, one pinned D2H of the actions (the only synchronisation), the host env
-step writing straight into pinned staging buffers, and async H2D copies into
-the (P, T, N) rollout arrays (reference: agilerl/rollouts/on_policy.py:23-203,
-one agent at a time through CPU TensorDicts).
+Reference: agilerl/rollouts/on_policy.py:23-203 (one agent at a time, CPU
+TensorDicts, a forward + ``.cpu()`` sync per step).  Here one vector step of
+EVERY agent is, on the fused path (agx_ppo_rollout_step):
+
+  1. ONE launch: scatter the staged obs into rollout slot t, the staged
+     reward/done of step t-1 into slot t-1 (+ episode accounting), and the
+     policy step (MFMA forward, Gumbel-max sample) writing action / log-prob /
+     value into slot t and a contiguous action copy;
+  2. ONE D2H of the P*N actions into pinned memory + an event wait (the only
+     synchronisation);
+  3. the host env step, writing obs / reward / done straight into ONE packed
+     pinned staging buffer;
+  4. ONE async H2D of that staging buffer.
+
+Architectures outside the fused kernels use the plain-PyTorch policy step
+with per-field copies (``_collect_torch``).
 """
 
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
+from .. import _lib
 from .ppo_pop import PPOPopulation
+
+
+class AgxRolloutIO(ctypes.Structure):
+    """Mirror of ``agx_rollout_io`` (include/agx.h)."""
+
+    _fields_ = [
+        ("stage_obs", ctypes.c_void_p), ("stage_rew", ctypes.c_void_p), ("stage_done", ctypes.c_void_p),
+        ("obs_slot", ctypes.c_void_p), ("obs_agent_stride", ctypes.c_int64),
+        ("rewards_prev", ctypes.c_void_p), ("dones_prev", ctypes.c_void_p),
+        ("actions", ctypes.c_void_p), ("log_probs", ctypes.c_void_p), ("values", ctypes.c_void_p),
+        ("slot_agent_stride", ctypes.c_int64), ("actions_flat", ctypes.c_void_p),
+        ("scores", ctypes.c_void_p), ("return_sum", ctypes.c_void_p), ("episodes", ctypes.c_void_p),
+    ]
+
+
+def _packed(P: int, N: int, D: int, **kw):
+    """One byte buffer [obs f32 P*N*D | reward f32 P*N | done u8 P*N] + views."""
+    n_obs, n_rew = P * N * D * 4, P * N * 4
+    nbytes = (n_obs + n_rew + P * N + 15) // 16 * 16
+    buf = torch.zeros(nbytes, dtype=torch.uint8, **kw)
+    obs = buf[:n_obs].view(torch.float32).view(P * N, D)
+    rew = buf[n_obs:n_obs + n_rew].view(torch.float32)
+    done = buf[n_obs + n_rew:n_obs + n_rew + P * N].view(torch.bool)
+    return buf, obs, rew, done
 
 
 class PopulationRunner:
@@ -20,32 +58,114 @@ class PopulationRunner:
             raise ValueError(f"env has {env.num_envs} envs, population needs P*N = {pop.P * pop.N}")
         self.pop, self.env = pop, env
         P, N, D = pop.P, pop.N, pop.spec.obs_dim
-        pin = dict(pin_memory=True)
-        self.obs_h = torch.zeros(P * N, D, dtype=torch.float32, **pin)
-        self.rew_h = torch.zeros(P * N, dtype=torch.float32, **pin)
-        self.done_h = torch.zeros(P * N, dtype=torch.bool, **pin)
-        self.term_h = torch.zeros(P * N, dtype=torch.bool, **pin)
-        self.act_h = torch.zeros(P * N, dtype=torch.int64, **pin)
-        self.act_d = torch.zeros(P * N, dtype=torch.int64, device=pop.device)
-        self.last_obs = torch.zeros(P, N, D, dtype=torch.float32, device=pop.device)
-        self.last_done = torch.zeros(P, N, dtype=torch.uint8, device=pop.device)
+        dev = pop.device
+        self.stage_h, self.obs_h, self.rew_h, self.done_h = _packed(P, N, D, pin_memory=True)
+        self.stage_d, self.obs_d, self.rew_d, self.done_d = _packed(P, N, D, device=dev)
+        self.term_h = torch.zeros(P * N, dtype=torch.bool, pin_memory=True)
+        self.act_h = torch.zeros(P * N, dtype=torch.int64, pin_memory=True)
+        self.act_d = torch.zeros(P * N, dtype=torch.int64, device=dev)
+        self.last_obs = torch.zeros(P, N, D, dtype=torch.float32, device=dev)
+        self.last_done = torch.zeros(P, N, dtype=torch.uint8, device=dev)
         self.ev = torch.cuda.Event()
         self.started = False
         self.env_steps = 0
-        self.scores = torch.zeros(P, N, dtype=torch.float32, device=pop.device)
-        self.episode_return_sum = torch.zeros(P, dtype=torch.float64, device=pop.device)
-        self.episodes = torch.zeros(P, dtype=torch.int64, device=pop.device)
+        # per-env episode accounting (on_policy.py:147-172), reduced per agent on demand
+        self.scores = torch.zeros(P * N, dtype=torch.float32, device=dev)
+        self.ret_sum_env = torch.zeros(P * N, dtype=torch.float64, device=dev)
+        self.episodes_env = torch.zeros(P * N, dtype=torch.int64, device=dev)
+        self._ios = None
 
-    def _h2d(self, dst: torch.Tensor, src: torch.Tensor) -> None:
-        dst.copy_(src.view(dst.shape), non_blocking=True)
+    # ------------------------------------------------------------------ #
+    @property
+    def episode_return_sum(self) -> torch.Tensor:
+        return self.ret_sum_env.view(self.pop.P, self.pop.N).sum(1)
+
+    @property
+    def episodes(self) -> torch.Tensor:
+        return self.episodes_env.view(self.pop.P, self.pop.N).sum(1)
+
+    def reset_episode_stats(self) -> None:
+        self.ret_sum_env.zero_()
+        self.episodes_env.zero_()
+
+    # ------------------------------------------------------------------ #
+    def _build_ios(self):
+        """agx_rollout_io for every step t = 0..T (t = T: final scatter only)."""
+        pop = self.pop
+        T, N, D = pop.T, pop.N, pop.spec.obs_dim
+        ios = []
+        for t in range(T + 1):
+            io = AgxRolloutIO()
+            io.stage_obs = self.obs_d.data_ptr()
+            if t > 0:
+                io.stage_rew = self.rew_d.data_ptr()
+                io.stage_done = self.done_d.data_ptr()
+                io.rewards_prev = pop.rewards[:, t - 1].data_ptr()
+                io.dones_prev = pop.dones[:, t - 1].data_ptr()
+                io.scores = self.scores.data_ptr()
+                io.return_sum = self.ret_sum_env.data_ptr()
+                io.episodes = self.episodes_env.data_ptr()
+            if t < T:
+                io.obs_slot = pop.obs[:, t].data_ptr()
+                io.obs_agent_stride = T * N * D
+                io.actions = pop.actions[:, t].data_ptr()
+                io.log_probs = pop.log_probs[:, t].data_ptr()
+                io.values = pop.values[:, t].data_ptr()
+                io.actions_flat = self.act_d.data_ptr()
+            else:
+                io.obs_slot = self.last_obs.data_ptr()
+                io.obs_agent_stride = N * D
+            io.slot_agent_stride = T * N
+            ios.append(io)
+        self._ios = ios
+
+    def _env_step(self) -> None:
+        _, _, term, trunc, _ = self.env.step(self.act_h.numpy(), out_obs=self.obs_h.numpy(),
+                                             out_rew=self.rew_h.numpy(), out_done=self.done_h.numpy())
+        if trunc is not None and trunc.any():  # done = term | trunc (on_policy.py:121-126)
+            self.done_h.numpy()[:] |= trunc
+        self.term_h.numpy()[:] = term
 
     @torch.no_grad()
     def collect(self) -> None:
         pop, env = self.pop, self.env
+        desc = pop.fused_descriptor()
+        if desc is None:
+            return self._collect_torch()
+        P, N, T = pop.P, pop.N, pop.T
+        if self._ios is None:
+            self._build_ios()
+        if not self.started:
+            env.reset(out_obs=self.obs_h.numpy())
+            self.stage_d.copy_(self.stage_h, non_blocking=True)
+            self.started = True
+        lib = _lib.load()
+        fn = lib.agx_ppo_rollout_step
+        dref = ctypes.byref(desc)
+        params = pop.params.data.data_ptr()
+        s = _lib.stream()
+        for t in range(T):
+            pop.act_counter += 1
+            _lib.check(fn(dref, P, N, params, ctypes.byref(self._ios[t]), 1, 1, pop.act_seed, pop.act_counter, s),
+                       "agx_ppo_rollout_step")
+            self.act_h.copy_(self.act_d, non_blocking=True)
+            self.ev.record()
+            self.ev.synchronize()
+            self._env_step()
+            self.stage_d.copy_(self.stage_h, non_blocking=True)
+        # reward/done of the last step -> slot T-1; final obs -> last_obs (bootstrap)
+        _lib.check(fn(dref, P, N, params, ctypes.byref(self._ios[T]), 0, 1, pop.act_seed, 0, s),
+                   "agx_ppo_rollout_step")
+        self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)  # last_done = term (:196)
+        self.env_steps += P * N * T
+
+    @torch.no_grad()
+    def _collect_torch(self) -> None:
+        pop, env = self.pop, self.env
         P, N, T = pop.P, pop.N, pop.T
         if not self.started:
             env.reset(out_obs=self.obs_h.numpy())
-            self._h2d(self.last_obs, self.obs_h)
+            self.last_obs.copy_(self.obs_h.view(P, N, -1), non_blocking=True)
             self.started = True
         pop.obs[:, 0].copy_(self.last_obs)
         for t in range(T):
@@ -53,22 +173,18 @@ class PopulationRunner:
             self.act_h.copy_(self.act_d, non_blocking=True)
             self.ev.record()
             self.ev.synchronize()
-            _, _, term, trunc, _ = env.step(self.act_h.numpy(), out_obs=self.obs_h.numpy(),
-                                            out_rew=self.rew_h.numpy(), out_done=self.done_h.numpy())
-            if trunc is not None and trunc.any():  # done = term | trunc (on_policy.py:121-126)
-                self.done_h.numpy()[:] |= trunc
-            self.term_h.numpy()[:] = term
-            self._h2d(pop.rewards[:, t], self.rew_h)
-            self._h2d(pop.dones[:, t], self.done_h.view(torch.uint8))
+            self._env_step()
+            pop.rewards[:, t].copy_(self.rew_h.view(P, N), non_blocking=True)
+            pop.dones[:, t].copy_(self.done_h.view(torch.uint8).view(P, N), non_blocking=True)
             nxt = pop.obs[:, t + 1] if t + 1 < T else self.last_obs
-            self._h2d(nxt, self.obs_h)
-            # running episode scores for fitness (on_policy.py:147-172)
-            self.scores += pop.rewards[:, t]
-            d = pop.dones[:, t].bool()
-            self.episode_return_sum += torch.where(d, self.scores, 0.0).sum(1).double()
-            self.episodes += d.sum(1)
+            nxt.copy_(self.obs_h.view(P, N, -1), non_blocking=True)
+            r = pop.rewards[:, t].reshape(-1)
+            d = pop.dones[:, t].reshape(-1).bool()
+            self.scores += r
+            self.ret_sum_env += torch.where(d, self.scores, 0.0).double()
+            self.episodes_env += d.long()
             self.scores.masked_fill_(d, 0.0)
-        self._h2d(self.last_done, self.term_h.view(torch.uint8))  # last_done = term only (:196)
+        self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)
         self.env_steps += P * N * T
 
     def iteration(self) -> torch.Tensor:

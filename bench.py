@@ -102,13 +102,15 @@ def population_leg(args, world, rank):
             sync.generation()
 
     for i in range(args.warmup):
-        step(i)
+        runner.iteration()
+    if sync is not None:  # first generation outside the timed region (loads its kernels)
+        sync.generation()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        step(i)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()

@@ -137,6 +137,37 @@ int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const float *param
                 uint64_t counter, int64_t *actions, float *log_probs, float *values,
                 float *entropy, int64_t out_agent_stride, int64_t *actions_flat,
                 void *workspace, void *stream);
+/* One vector step of rollout collection for all P agents x N envs
+ * (rollouts/on_policy.py:23-203 loop body + RolloutBuffer.add,
+ * rollout_buffer.py:235-411), fused into ONE launch:
+ *  - stage_obs [P][N][obs_dim] (the packed H2D staging of the env's new
+ *    observations) is copied to obs_slot (agent stride obs_agent_stride);
+ *  - if stage_rew: reward/done of the PREVIOUS step go to rewards_prev /
+ *    dones_prev (slot t-1) and, if scores, the per-env episode accounting
+ *    (score += r; on done: return_sum += score, episodes += 1, score = 0;
+ *    on_policy.py:147-172) is updated;
+ *  - if act: the policy step of agx_ppo_act on stage_obs writes actions /
+ *    log_probs / values (slot t, agent stride slot_agent_stride) and the
+ *    contiguous actions_flat [P*N] for the D2H. */
+typedef struct agx_rollout_io {
+    const float *stage_obs;
+    const float *stage_rew;           /* [P*N] or NULL */
+    const uint8_t *stage_done;        /* [P*N] */
+    float *obs_slot;                  /* or NULL */
+    int64_t obs_agent_stride;
+    float *rewards_prev;
+    uint8_t *dones_prev;
+    int64_t *actions;
+    float *log_probs, *values;
+    int64_t slot_agent_stride;
+    int64_t *actions_flat;
+    float *scores;                    /* [P*N] or NULL */
+    double *return_sum;               /* [P*N] */
+    int64_t *episodes;                /* [P*N] */
+} agx_rollout_io;
+int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
+                         const agx_rollout_io *io, int act, int sample, uint64_t seed,
+                         uint64_t counter, void *stream);
 
 /* ---- prioritized replay segment trees -----------------------------------
  * Replaces SumSegmentTree / MinSegmentTree (agilerl/components/

@@ -208,3 +208,84 @@ def test_fused_learner_partner_split_consistent(split, monkeypatch):
     m_f = pop.opt.exp_avg
     np.testing.assert_allclose(m_f.cpu().numpy(), m_t.cpu().numpy(), rtol=2e-3, atol=1e-5 * m_t.abs().max().item())
     np.testing.assert_allclose(loss_f.cpu().numpy(), loss_t.cpu().numpy(), rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_collect_fills_rollout_like_the_reference_loop(fused):
+    """One collect() against a replayed copy of the (action-independent)
+    synthetic env: obs / reward / done land in the right slots (done of step
+    t at slot t, on_policy.py:137-142; last_done = term), stored log-probs /
+    values equal the torch forward of the stored obs and actions, and the
+    episode accounting matches a recomputation from the stored rewards."""
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.population.nets import ActorCriticSpec, categorical
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+    from agilerl_amd.population.runner import PopulationRunner
+
+    P, N = 3, 40
+    spec = ActorCriticSpec(obs_dim=8, n_actions=4)
+    pop = PPOPopulation(spec, P, N, learn_step=8 * N, batch_size=64, device=DEV, fused=fused)
+    env = SyntheticVecEnv(P * N, seed=5, p_done=0.2)
+    ref = SyntheticVecEnv(P * N, seed=5, p_done=0.2)
+    runner = PopulationRunner(pop, env)
+    T = pop.T
+    for rep in range(2):
+        runner.collect()
+        torch.cuda.synchronize()
+        if rep == 0:
+            o, _ = ref.reset()
+            exp_obs = [o.copy()]
+        else:
+            exp_obs = [exp_last]
+        exp_r, exp_d = [], []
+        for t in range(T):
+            o, r, term, trunc, _ = ref.step(np.zeros(P * N, dtype=np.int64))
+            exp_obs.append(o.copy())
+            exp_r.append(r.copy())
+            exp_d.append(term | trunc)
+        exp_last = exp_obs[-1]
+        got_obs = pop.obs.cpu().numpy()  # [P, T, N, D]
+        for t in range(T):
+            np.testing.assert_array_equal(got_obs[:, t].reshape(P * N, 8), exp_obs[t])
+            np.testing.assert_array_equal(pop.rewards[:, t].cpu().numpy().reshape(-1), exp_r[t])
+            np.testing.assert_array_equal(pop.dones[:, t].cpu().numpy().reshape(-1).astype(bool), exp_d[t])
+        np.testing.assert_array_equal(runner.last_obs.cpu().numpy().reshape(P * N, 8), exp_obs[T])
+        np.testing.assert_array_equal(runner.last_done.cpu().numpy().reshape(-1).astype(bool), term)
+    # stored log-probs / values follow the stored (obs, action) pairs
+    logits, value = spec.forward(pop.params.data, pop.obs.view(P, -1, 8))
+    logp_all, _ = categorical(logits)
+    lp = logp_all.gather(-1, pop.actions.view(P, -1, 1)).squeeze(-1)
+    torch.testing.assert_close(pop.log_probs.view(P, -1), lp, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(pop.values.view(P, -1), value, rtol=1e-4, atol=1e-5)
+    assert int(pop.actions.min()) >= 0 and int(pop.actions.max()) < 4
+
+
+def test_collect_episode_accounting():
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+    from agilerl_amd.population.runner import PopulationRunner
+
+    P, N = 2, 33
+    spec = ActorCriticSpec(obs_dim=8, n_actions=4)
+    pop = PPOPopulation(spec, P, N, learn_step=6 * N, batch_size=64, device=DEV)
+    runner = PopulationRunner(pop, SyntheticVecEnv(P * N, seed=9, p_done=0.25))
+    R, D = [], []
+    for _ in range(3):
+        runner.collect()
+        torch.cuda.synchronize()
+        R.append(pop.rewards.cpu().numpy())
+        D.append(pop.dones.cpu().numpy().astype(bool))
+    r = np.concatenate(R, axis=1).reshape(P, -1, N)  # [P, 3T, N]
+    d = np.concatenate(D, axis=1).reshape(P, -1, N)
+    score = np.zeros((P, N), np.float32)
+    ret = np.zeros((P, N))
+    eps = np.zeros((P, N), np.int64)
+    for t in range(r.shape[1]):
+        score = score + r[:, t]
+        ret += np.where(d[:, t], score, 0.0)
+        eps += d[:, t]
+        score = np.where(d[:, t], 0.0, score).astype(np.float32)
+    np.testing.assert_array_equal(runner.episodes.cpu().numpy(), eps.sum(1))
+    np.testing.assert_allclose(runner.episode_return_sum.cpu().numpy(), ret.sum(1), rtol=1e-6)
+    np.testing.assert_allclose(runner.scores.view(P, N).cpu().numpy(), score, rtol=1e-6, atol=1e-6)
