@@ -55,6 +55,7 @@ constexpr int kNT = 512;
 constexpr int kNW = kNT / kWave;  // 8 waves
 constexpr int kSB = 32;           // rows per sub-batch
 constexpr int kMaxSlot = 10;      // dW tiles per wave
+constexpr int kMaxK = 4;          // partner workgroups per agent (hand-off unrolled for <= 4)
 constexpr int kMaxPT = 30;        // LDS parameter slots per thread
 constexpr int kMaxA = 16;
 constexpr int kMaxBlk = 28;
@@ -574,7 +575,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     (void)nmb_dummy;
     const int nmb = (int)((S + g.B - 1) / g.B);
     float loss_total = 0.f;
-    long long step = g.step0;
+    double pb1 = pow((double)g.b1, (double)g.step0), pb2 = pow((double)g.b2, (double)g.step0);
+    const float lr_p = g.lr[p];
     float *rowf = sm + pl.l_row;  // [4][SB]: old_logp, adv, ret, old_v
     float *stat = sm + pl.l_stat;
     int *acts = reinterpret_cast<int *>(sm + pl.l_row + 4 * kSB);
@@ -957,6 +959,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __hip_atomic_fetch_add(g.cnt + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    AGX_STAMP(64 + 11);
                     const unsigned target = (unsigned)(g.K * (upd + 1));
                     unsigned spins = 0;
                     int ok = 1;
@@ -971,15 +974,45 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     stat[3 * kNW] = ok ? 1.f : 0.f;
+                    AGX_STAMP(64 + 12);
                 }
                 __syncthreads();
                 if (stat[3 * kNW] == 0.f) return;  // partner never arrived: timeout word set, whole block exits
                 // fixed-order sum over partners: every workgroup of the agent computes
                 // bit-identical totals, hence bit-identical parameters after Adam
-                for (int i = tid; i < pl.param_end / 4; i += kNT) {
-                    f4 t = reinterpret_cast<const f4 *>(base)[i];
-                    for (int q = 1; q < g.K; ++q) t += reinterpret_cast<const f4 *>(base + (size_t)q * pl.slab)[i];
-                    reinterpret_cast<f4 *>(G)[i] = t;
+                // (own slab read back from LDS: same bits as the stored copy).  Chunks
+                // of 2 float4 per thread with all partner loads issued before the adds.
+                {
+                    constexpr int n4 = pl.param_end / 4;
+                    constexpr int NI = (n4 + kNT - 1) / kNT;
+                    const f4 *G4 = reinterpret_cast<const f4 *>(G);
+#pragma unroll
+                    for (int j0 = 0; j0 < NI; j0 += 2) {
+                        f4 t[2], v[3][2];
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const int i = tid + (j0 + j) * kNT;
+                            t[j] = f4{0.f, 0.f, 0.f, 0.f};
+                            if (j0 + j < NI && i < n4) {
+                                t[j] = kk == 0 ? G4[i] : reinterpret_cast<const f4 *>(base)[i];
+#pragma unroll
+                                for (int q = 1; q < 4; ++q)
+                                    if (q < g.K)
+                                        v[q - 1][j] = q == kk ? G4[i]
+                                                              : reinterpret_cast<const f4 *>(base + (size_t)q * pl.slab)[i];
+                            }
+                        }
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const int i = tid + (j0 + j) * kNT;
+                            if (j0 + j < NI && i < n4) {
+#pragma unroll
+                                for (int q = 1; q < 4; ++q)
+                                    if (q < g.K) t[j] += v[q - 1][j];
+                                reinterpret_cast<f4 *>(G)[i] = t[j];
+                            }
+                        }
+                    }
                 }
                 // (loss words via vector atomics: a uniform plain load would take the
                 // scalar-cache path, which the acquire does not invalidate)
@@ -989,6 +1022,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                             __HIP_MEMORY_SCOPE_AGENT);
                 lmb = lt;
                 __syncthreads();
+                AGX_STAMP(64 + 13);
             }
 
             // ---- P10: two-group norm, Adam from registers -------------------------
@@ -1003,15 +1037,34 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 }
             }
             AGX_IDS;
-            const float t0 = block_sum(n0, stat, 0, lane, wave);
-            const float t1 = block_sum(n1, stat, 1, lane, wave);
+            // both group norms in one reduction round (fixed order)
+            {
+                const float r0 = row_sum(n0), r1 = row_sum(n1);
+                const float w0 = readlane_f(r0, 0) + readlane_f(r0, 16) + readlane_f(r0, 32) + readlane_f(r0, 48);
+                const float w1 = readlane_f(r1, 0) + readlane_f(r1, 16) + readlane_f(r1, 32) + readlane_f(r1, 48);
+                if (lane == 0) {
+                    stat[wave] = w0;
+                    stat[kNW + wave] = w1;
+                }
+            }
+            __syncthreads();
+            float t0 = 0.f, t1 = 0.f;
+            for (int i = 0; i < kNW; ++i) {
+                t0 += stat[i];
+                t1 += stat[kNW + i];
+            }
             if (tid == 0) loss_total += lmb;
             const float c0 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t0) + 1e-6f), 1.f) : 1.f;
             const float c1 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t1) + 1e-6f), 1.f) : 1.f;
-            ++step;
-            const float bc1 = (float)(1.0 - pow((double)g.b1, (double)step));
-            const float bc2s = (float)sqrt(1.0 - pow((double)g.b2, (double)step));
-            const float step_size = g.lr[p] / bc1;
+            // bias corrections 1 - beta^step from running f64 products (the
+            // host/torch form is pow(); products agree to an ulp of f64, i.e.
+            // to the f32 results used here)
+            pb1 *= (double)g.b1;
+            pb2 *= (double)g.b2;
+            const float bc1 = (float)(1.0 - pb1);
+            const float bc2s = (float)sqrt(1.0 - pb2);
+            const float step_size = lr_p / bc1;
+            const float inv_bc2s = 1.f / bc2s;
 #pragma unroll
             for (int i = 0; i < kMaxPT; ++i) {
                 const int l = tid + kNT * i;
@@ -1019,8 +1072,11 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     const float gr = G[l] * (((gbits >> i) & 1u) ? c1 : c0);
                     am[i] = am[i] + (1.f - g.b1) * (gr - am[i]);
                     av[i] = av[i] * g.b2 + (1.f - g.b2) * gr * gr;
-                    const float denom = sqrtf(av[i]) / bc2s + g.eps;
-                    sm[l] = sm[l] - step_size * (am[i] / denom);
+                    // hardware sqrt / reciprocal (1 ulp) instead of the IEEE
+                    // expansions: the update m/(sqrt(v)+eps) is compared within
+                    // tolerance, never bit-exactly (summation order already differs)
+                    const float denom = __builtin_amdgcn_sqrtf(av[i]) * inv_bc2s + g.eps;
+                    sm[l] = sm[l] - step_size * (am[i] * __builtin_amdgcn_rcpf(denom));
                 }
             }
             __syncthreads();
@@ -1288,7 +1344,7 @@ static int max_partners(int64_t P) {
     int k = 4;
     if (const char *e = getenv("AGX_LEARN_SPLIT")) k = atoi(e);
     if (k < 1) k = 1;
-    if (k > 8) k = 8;
+    if (k > kMaxK) k = kMaxK;
     const int64_t fit = cu_count() / (P > 0 ? P : 1);  // all partners co-resident, 1 block per CU
     if (fit < k) k = fit < 1 ? 1 : (int)fit;
     return k;

@@ -40,5 +40,7 @@ for sb in range(4):
     row = st[sb * 16: sb * 16 + 8]
     seg = [row[i + 1] - row[i] for i in range(7)]
     print(f"sb{sb}: " + "  ".join(f"{n}={c}" for n, c in zip(names, seg)) + f"  total={row[7] - row[0]}")
-print("dump", st[64 + 9] - st[3 * 16 + 7], "norm+adam", st[64 + 10] - st[64 + 9],
-      "minibatch total cycles", st[64 + 10] - st[0])
+last = max(v for v in st[:64] if v)
+print("dump", st[64 + 9] - last, "| exchange: publish", st[64 + 11] - st[64 + 9], "wait+acquire",
+      st[64 + 12] - st[64 + 11], "sum", st[64 + 13] - st[64 + 12], "| norm+adam", st[64 + 10] - st[64 + 13],
+      "| minibatch total cycles", st[64 + 10] - st[0])
