@@ -52,6 +52,7 @@ SIGNATURES = {
     "agx_polyak": (_INT, [_P, _P, _I, _F, _P]),
     "agx_debug_pow": (_INT, [_P, _P, _P, _I, _P]),
     "agx_debug_learn_stamps": (_INT, [_P]),
+    "agx_debug_stream": (_INT, [_P, _P, _I, _INT, _I, _P]),
 }
 
 _lib = None

@@ -1503,7 +1503,7 @@ extern "C" int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N
                                     const agx_rollout_io *io, int act, int sample, uint64_t seed,
                                     uint64_t counter, void *stream) {
     AGX_REQUIRE(net && io && io->stage_obs && P > 0 && N > 0 && P <= 65535, "agx_ppo_rollout_step: bad arguments");
-    AGX_REQUIRE(!act || (params && io->actions_flat), "agx_ppo_rollout_step: act needs params and actions_flat");
+    AGX_REQUIRE(!act || params, "agx_ppo_rollout_step: act needs params");
     AGX_REQUIRE(!io->stage_rew || (io->stage_done && io->rewards_prev && io->dones_prev),
                 "agx_ppo_rollout_step: previous-step scatter needs rewards/dones slots");
     AGX_REQUIRE(!io->scores || (io->stage_rew && io->return_sum && io->episodes),
@@ -1535,7 +1535,7 @@ extern "C" int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N
     a.st_done = io->stage_done;
     a.rew_prev = io->rewards_prev;
     a.done_prev = io->dones_prev;
-    a.prev_pstride = io->slot_agent_stride;
+    a.prev_pstride = io->prev_agent_stride;
     a.scores = io->scores;
     a.ret_sum = io->return_sum;
     a.episodes = reinterpret_cast<long long *>(io->episodes);

@@ -38,3 +38,54 @@ extern "C" int agx_device_info(int *out3) {
     out3[2] = prop.warpSize;
     return AGX_OK;
 }
+
+// STREAM-style kernels used by bench.py to measure the box's achievable HBM
+// bandwidth (the roofline's "measured peak"): 16 B per lane, each block moves
+// one contiguous 16 KiB tile per pass (4 loads in flight per lane).
+//   mode 0: copy (read + write), nontemporal stores
+//   mode 1: read-only (sum into one float per block, written once)
+namespace agx {
+typedef float v4f __attribute__((ext_vector_type(4)));
+template <int MODE>
+__global__ __launch_bounds__(256) void stream_kernel(const v4f *__restrict__ src, v4f *__restrict__ dst, int64_t n4) {
+    constexpr int U = 4;
+    const int64_t tile = (int64_t)blockDim.x * U;
+    v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int64_t base = (int64_t)blockIdx.x * tile; base < n4; base += (int64_t)gridDim.x * tile) {
+        v4f v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + u * blockDim.x + threadIdx.x;
+            v[u] = i < n4 ? src[i] : v4f{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + u * blockDim.x + threadIdx.x;
+            if (MODE == 0) {
+                if (i < n4) __builtin_nontemporal_store(v[u], dst + i);
+            } else {
+                acc += v[u];
+            }
+        }
+    }
+    if (MODE == 1) {
+        const float t = acc.x + acc.y + acc.z + acc.w;
+        if (t == 12345.678f) dst[blockIdx.x] = acc;  // keeps the loads live; practically never stores
+    }
+}
+}  // namespace agx
+
+extern "C" int agx_debug_stream(const void *src, void *dst, int64_t bytes, int mode, int64_t grid, void *stream) {
+    AGX_REQUIRE(src && dst && bytes > 0 && bytes % 16 == 0 && (mode == 0 || mode == 1) && grid >= 0,
+                "agx_debug_stream: bad arguments");
+    const int64_t n4 = bytes / 16;
+    const int64_t tiles = agx::ceil_div(n4, 1024);
+    const unsigned g = (unsigned)(grid > 0 && grid < tiles ? grid : tiles);
+    if (mode == 0)
+        agx::stream_kernel<0><<<g, 256, 0, agx::as_stream(stream)>>>(static_cast<const agx::v4f *>(src),
+                                                                    static_cast<agx::v4f *>(dst), n4);
+    else
+        agx::stream_kernel<1><<<g, 256, 0, agx::as_stream(stream)>>>(static_cast<const agx::v4f *>(src),
+                                                                    static_cast<agx::v4f *>(dst), n4);
+    return agx::check_launch("agx_debug_stream");
+}

@@ -159,9 +159,12 @@ class PPOPopulation:
         self.log_probs[:, t].copy_(logp, non_blocking=True)
 
     @torch.no_grad()
-    def finish_rollout(self, last_obs: torch.Tensor, last_done: torch.Tensor):
-        """Bootstrap value + GAE (+ per-agent advantage statistics)."""
-        _, last_value = self.spec.forward(self.params.data, last_obs)
+    def finish_rollout(self, last_obs: torch.Tensor, last_done: torch.Tensor,
+                       last_value: torch.Tensor | None = None):
+        """Bootstrap value + GAE (+ per-agent advantage statistics).  The fused
+        runner computes last_value in its final rollout-step launch."""
+        if last_value is None:
+            _, last_value = self.spec.forward(self.params.data, last_obs)
         K.gae(self.rewards, self.dones, self.values, last_value.contiguous(), last_done.contiguous(),
               self.gamma, self.gae_lambda, True, advantages=self.advantages, returns=self.returns,
               with_stats=True, workspace=self.gae_ws, stats_out=self.adv_stats)

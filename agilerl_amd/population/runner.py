@@ -34,7 +34,7 @@ class AgxRolloutIO(ctypes.Structure):
     _fields_ = [
         ("stage_obs", ctypes.c_void_p), ("stage_rew", ctypes.c_void_p), ("stage_done", ctypes.c_void_p),
         ("obs_slot", ctypes.c_void_p), ("obs_agent_stride", ctypes.c_int64),
-        ("rewards_prev", ctypes.c_void_p), ("dones_prev", ctypes.c_void_p),
+        ("rewards_prev", ctypes.c_void_p), ("dones_prev", ctypes.c_void_p), ("prev_agent_stride", ctypes.c_int64),
         ("actions", ctypes.c_void_p), ("log_probs", ctypes.c_void_p), ("values", ctypes.c_void_p),
         ("slot_agent_stride", ctypes.c_int64), ("actions_flat", ctypes.c_void_p),
         ("scores", ctypes.c_void_p), ("return_sum", ctypes.c_void_p), ("episodes", ctypes.c_void_p),
@@ -66,6 +66,8 @@ class PopulationRunner:
         self.act_d = torch.zeros(P * N, dtype=torch.int64, device=dev)
         self.last_obs = torch.zeros(P, N, D, dtype=torch.float32, device=dev)
         self.last_done = torch.zeros(P, N, dtype=torch.uint8, device=dev)
+        self.last_value = torch.zeros(P, N, dtype=torch.float32, device=dev)
+        self.last_value_valid = False
         self.ev = torch.cuda.Event()
         self.started = False
         self.env_steps = 0
@@ -112,10 +114,13 @@ class PopulationRunner:
                 io.log_probs = pop.log_probs[:, t].data_ptr()
                 io.values = pop.values[:, t].data_ptr()
                 io.actions_flat = self.act_d.data_ptr()
-            else:
+                io.slot_agent_stride = T * N
+            else:  # final obs -> last_obs + bootstrap value
                 io.obs_slot = self.last_obs.data_ptr()
                 io.obs_agent_stride = N * D
-            io.slot_agent_stride = T * N
+                io.values = self.last_value.data_ptr()
+                io.slot_agent_stride = N
+            io.prev_agent_stride = T * N
             ios.append(io)
         self._ios = ios
 
@@ -153,9 +158,10 @@ class PopulationRunner:
             self.ev.synchronize()
             self._env_step()
             self.stage_d.copy_(self.stage_h, non_blocking=True)
-        # reward/done of the last step -> slot T-1; final obs -> last_obs (bootstrap)
-        _lib.check(fn(dref, P, N, params, ctypes.byref(self._ios[T]), 0, 1, pop.act_seed, 0, s),
+        # reward/done of the last step -> slot T-1; final obs -> last_obs + bootstrap value
+        _lib.check(fn(dref, P, N, params, ctypes.byref(self._ios[T]), 1, 0, pop.act_seed, 0, s),
                    "agx_ppo_rollout_step")
+        self.last_value_valid = True
         self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)  # last_done = term (:196)
         self.env_steps += P * N * T
 
@@ -167,6 +173,7 @@ class PopulationRunner:
             env.reset(out_obs=self.obs_h.numpy())
             self.last_obs.copy_(self.obs_h.view(P, N, -1), non_blocking=True)
             self.started = True
+        self.last_value_valid = False
         pop.obs[:, 0].copy_(self.last_obs)
         for t in range(T):
             pop.act_into(t, self.act_d)
@@ -190,5 +197,6 @@ class PopulationRunner:
     def iteration(self) -> torch.Tensor:
         """collect -> bootstrap + GAE -> learn; returns per-agent mean loss (device)."""
         self.collect()
-        self.pop.finish_rollout(self.last_obs, self.last_done)
+        self.pop.finish_rollout(self.last_obs, self.last_done,
+                                self.last_value if self.last_value_valid else None)
         return self.pop.learn()

@@ -122,31 +122,48 @@ def population_leg(args, world, rank):
 
 
 # --------------------------------------------------------------------------- #
-def measure_copy_peak():
-    n = 512 * 1024 * 1024 // 4  # 512 MiB per side
-    a = torch.empty(n, dtype=torch.float32, device="cuda").uniform_()
+def measure_hbm_peak():
+    """STREAM-style probes (agx_debug_stream, 16 B/lane, one 16 KiB tile per
+    block) over 1 GiB buffers — 4x the 256 MiB Infinity Cache — timed with HIP
+    events on the launch stream: (copy GB/s counting read + write, read GB/s)."""
+    from agilerl_amd import _lib
+
+    nbytes = 1 << 30
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda").uniform_()
     b = torch.empty_like(a)
-    for _ in range(3):
-        b.copy_(a)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    reps = 10
-    for _ in range(reps):
-        b.copy_(a)
-    e.record()
-    e.synchronize()
-    ms = s.elapsed_time(e) / reps
+    lib = _lib.load()
+    out = []
+    for mode in (0, 1):
+        def run():
+            _lib.check(lib.agx_debug_stream(a.data_ptr(), b.data_ptr(), nbytes, mode, 0, _lib.stream()),
+                       "agx_debug_stream")
+
+        for _ in range(3):
+            run()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 10
+        s.record()
+        for _ in range(reps):
+            run()
+        e.record()
+        e.synchronize()
+        ms = s.elapsed_time(e) / reps
+        out.append((2 if mode == 0 else 1) * nbytes / (ms * 1e-3) / 1e9)
     del a, b
-    return 2 * n * 4 / (ms * 1e-3) / 1e9
+    torch.cuda.empty_cache()
+    return out[0], out[1]
 
 
-def roofline_leg(args):
-    """GAE (P=8, T=1024, N=8192) + E=4 passes of the loss fwd+bwd over the same
-    67.1 M samples (b = 128), timed per kernel with HIP events on the launch
-    stream (torch's current stream: libagx launches there)."""
+ROOF_P, ROOF_T, ROOF_N, ROOF_E, ROOF_B = 8, 1024, 8192, 4, 128
+
+
+def roofline_workload():
+    """Inputs of SURVEY §8d (GAE P=8 T=1024 N=8192; loss over the same 67.1 M
+    samples, b = 128) -> (run_gae, run_loss, S).  Shared with
+    tools/pmc_roofline.py (the rocprofv3 --pmc pass)."""
     from agilerl_amd import kernels as K
 
-    P, T, N, E, b = 8, 1024, 8192, 4, 128
+    P, T, N, b = ROOF_P, ROOF_T, ROOF_N, ROOF_B
     S = P * T * N
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
@@ -175,6 +192,24 @@ def roofline_leg(args):
         K.ppo_loss_fwd_bwd(logp, old_logp, adv.view(-1), ret.view(-1), v.view(-1), newv, H, b, 0.2, 0.5,
                            0.01, out=out, stats=lstats)
 
+    return run_gae, run_loss, S
+
+
+def load_pmc_traffic():
+    """Per-launch HBM bytes of the roofline kernels from the committed
+    rocprofv3 --pmc summary (tools/pmc_roofline.py), or None."""
+    path = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def roofline_leg(args):
+    """GAE + E=4 passes of the loss fwd+bwd, timed per kernel with HIP events
+    on the launch stream (torch's current stream: libagx launches there)."""
+    E = ROOF_E
+    run_gae, run_loss, S = roofline_workload()
     for _ in range(2):
         run_gae()
         run_loss()
@@ -197,7 +232,8 @@ def roofline_leg(args):
         t_loss += [x.elapsed_time(y) * 1e-3 for x, y in evs]
     tg = float(np.mean(t_gae))
     tl = float(np.mean(t_loss))
-    peak_meas = measure_copy_peak()
+    peak_copy, peak_read = measure_hbm_peak()
+    peak_meas = max(peak_copy, peak_read)
     fused_bytes = (GAE_BYTES + E * LOSS_BYTES) * S
     fused_t = tg + E * tl
     ach = fused_bytes / fused_t / 1e9
@@ -208,9 +244,15 @@ def roofline_leg(args):
         units="transitions P=8 T=1024 N=8192 (67.1M), 177 B each (17 GAE + 4x40 loss)",
         gae_ms=round(tg * 1e3, 3), loss_ms=round(tl * 1e3, 3),
         gae_gbs=round(GAE_BYTES * S / tg / 1e9, 1), loss_gbs=round(LOSS_BYTES * S / tl / 1e9, 1),
-        peak_measured_copy=round(peak_meas, 1), frac_of_measured=round(ach / peak_meas, 4),
+        peak_measured_copy=round(peak_copy, 1), peak_measured_read=round(peak_read, 1),
+        peak_measured=round(peak_meas, 1), frac_of_measured=round(ach / peak_meas, 4),
     )
-    del r, v, d, adv, ret, old_logp, logp, newv, H, out
+    pmc = load_pmc_traffic()
+    if pmc is not None:  # FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, per launch set (1 GAE + E loss)
+        res["traffic"] = pmc["gae_bytes"] + E * pmc["loss_bytes"]
+        res["traffic_source"] = "profiles/r1_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
+        res["algorithmic_bytes"] = fused_bytes
+    del run_gae, run_loss
     torch.cuda.empty_cache()
     return res
 

@@ -148,16 +148,19 @@ int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const float *param
  *    on_policy.py:147-172) is updated;
  *  - if act: the policy step of agx_ppo_act on stage_obs writes actions /
  *    log_probs / values (slot t, agent stride slot_agent_stride) and the
- *    contiguous actions_flat [P*N] for the D2H. */
+ *    contiguous actions_flat [P*N] (may be NULL) for the D2H.  The call after
+ *    the last step uses act=1 with only `values` set for the bootstrap value
+ *    (on_policy.py:184-196). */
 typedef struct agx_rollout_io {
     const float *stage_obs;
     const float *stage_rew;           /* [P*N] or NULL */
     const uint8_t *stage_done;        /* [P*N] */
     float *obs_slot;                  /* or NULL */
     int64_t obs_agent_stride;
-    float *rewards_prev;
+    float *rewards_prev;              /* slot t-1, agent stride prev_agent_stride */
     uint8_t *dones_prev;
-    int64_t *actions;
+    int64_t prev_agent_stride;
+    int64_t *actions;                 /* each may be NULL; agent stride slot_agent_stride */
     float *log_probs, *values;
     int64_t slot_agent_stride;
     int64_t *actions_flat;
@@ -253,6 +256,11 @@ int agx_debug_pow(const double *x, const double *y, double *out, int64_t n, void
  * [sub_batch*16 + phase], phases 0-8 per sub-batch, 9-11 at slot 64+);
  * buf = NULL disables. */
 int agx_debug_learn_stamps(int64_t *buf);
+/* STREAM-style bandwidth probes for bench.py's measured HBM peak: mode 0
+ * copies `bytes` (read + write, nontemporal stores), mode 1 reads them
+ * (dst receives at most one float4 per block).  grid = 0: one block per
+ * 16 KiB tile, else a grid-stride loop over `grid` blocks.  bytes % 16 == 0. */
+int agx_debug_stream(const void *src, void *dst, int64_t bytes, int mode, int64_t grid, void *stream);
 
 #ifdef __cplusplus
 }

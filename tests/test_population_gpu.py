@@ -258,6 +258,9 @@ def test_collect_fills_rollout_like_the_reference_loop(fused):
     torch.testing.assert_close(pop.log_probs.view(P, -1), lp, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(pop.values.view(P, -1), value, rtol=1e-4, atol=1e-5)
     assert int(pop.actions.min()) >= 0 and int(pop.actions.max()) < 4
+    if fused:  # bootstrap value computed by the final rollout-step launch
+        _, lv = spec.forward(pop.params.data, runner.last_obs)
+        torch.testing.assert_close(runner.last_value, lv, rtol=1e-4, atol=1e-5)
 
 
 def test_collect_episode_accounting():
