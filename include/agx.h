@@ -207,6 +207,26 @@ int agx_per_sample(const double *sum_tree, const double *min_tree, int64_t capac
  * nodes (used for sum()/min() and leaf reads without a host round trip). */
 int agx_per_gather(const double *tree, const int64_t *nodes, int64_t n, double *out, void *stream);
 
+/* ---- single segment trees ------------------------------------------------
+ * SegmentTree / SumSegmentTree / MinSegmentTree used on their own
+ * (agilerl/components/segment_tree.py): op 0 = sum (init 0.0), 1 = min
+ * (init +inf); tree = 2*capacity doubles, capacity a power of two.
+ * set: SegmentTree.__setitem__ (:81-95) for n (index, value) pairs in order
+ *   (last duplicate wins); workspace (agx_segtree_workspace_bytes) is needed
+ *   only for n > 1024.
+ * operate: SegmentTree.operate(start, end) (:61-79), the reference recursion
+ *   and operand order; end <= 0 counts from capacity; result to *out (device).
+ * retrieve: SumSegmentTree.retrieve (:136-156) for n f64 upper bounds; err
+ *   (device int32, may be NULL) counts failed `0 <= ub <= sum + 1e-5`. */
+size_t agx_segtree_workspace_bytes(int64_t capacity);
+int agx_segtree_init(double *tree, int64_t capacity, int op, void *stream);
+int agx_segtree_set(double *tree, int64_t capacity, int op, const int64_t *indices, const double *values,
+                    int64_t n, void *workspace, void *stream);
+int agx_segtree_operate(const double *tree, int64_t capacity, int op, int64_t start, int64_t end,
+                        double *out, void *stream);
+int agx_segtree_retrieve(const double *tree, int64_t capacity, const double *upperbounds, int64_t n,
+                         int64_t *indices, int32_t *err, void *stream);
+
 /* ---- DQN TD target -------------------------------------------------------
  * Replaces DQN.update's target + loss (agilerl/algorithms/dqn.py:296-314):
  * y = r + gamma*q_t*(1-d), q_t = max_a Qtgt(s') or Qtgt(s')[argmax Q(s')]
