@@ -24,49 +24,65 @@
 
 namespace agx {
 
-__global__ void td_target_kernel(const float *__restrict__ qno, const float *__restrict__ qnt,
-                                 const float *__restrict__ qc, const int64_t *__restrict__ act,
-                                 const float *__restrict__ r, const float *__restrict__ d, int64_t B,
-                                 int A, float g, int dbl, float *__restrict__ y,
-                                 float *__restrict__ g_q) {
+constexpr int kTdBlock = 256;
+
+// one row per lane; the squared TD errors are reduced per block (f64, fixed
+// order) into partials[blockIdx] and summed by td_loss_finalize
+__global__ __launch_bounds__(kTdBlock) void td_target_kernel(
+    const float *__restrict__ qno, const float *__restrict__ qnt, const float *__restrict__ qc,
+    const int64_t *__restrict__ act, const float *__restrict__ r, const float *__restrict__ d, int64_t B, int A,
+    float g, int dbl, float *__restrict__ y, float *__restrict__ g_q, double *__restrict__ partials) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= B) return;
-    const float *tn = qnt + i * A;
-    float qt;
-    if (dbl) {
-        const float *on = qno + i * A;
-        int best = 0;
-        float bv = on[0];
-        for (int a = 1; a < A; ++a)
-            if (on[a] > bv) {
-                bv = on[a];
-                best = a;
+    double sq = 0.0;
+    if (i < B) {
+        const float *tn = qnt + i * A;
+        float qt;
+        if (dbl) {
+            const float *on = qno + i * A;
+            int best = 0;
+            float bv = on[0];
+            for (int a = 1; a < A; ++a)
+                if (on[a] > bv) {
+                    bv = on[a];
+                    best = a;
+                }
+            qt = tn[best];
+        } else {
+            qt = tn[0];
+            for (int a = 1; a < A; ++a) qt = fmaxf(qt, tn[a]);
+        }
+        const float yi = r[i] + (g * qt) * (1.0f - d[i]);
+        y[i] = yi;
+        if (qc) {
+            const int64_t ai = act[i];
+            const float qa = qc[i * A + ai];
+            if (g_q) {
+                const float diff = qa - yi;
+                const float scale = 2.0f / (float)B;
+                for (int a = 0; a < A; ++a) g_q[i * A + a] = (a == ai) ? diff * scale : 0.0f;
             }
-        qt = tn[best];
-    } else {
-        qt = tn[0];
-        for (int a = 1; a < A; ++a) qt = fmaxf(qt, tn[a]);
+            const double dd = (double)qa - (double)yi;
+            sq = dd * dd;
+        }
     }
-    const float yi = r[i] + (g * qt) * (1.0f - d[i]);
-    y[i] = yi;
-    if (g_q) {
-        const int64_t ai = act[i];
-        const float diff = qc[i * A + ai] - yi;
-        const float scale = 2.0f / (float)B;
-        for (int a = 0; a < A; ++a) g_q[i * A + a] = (a == ai) ? diff * scale : 0.0f;
+    if (partials) {
+        __shared__ double red[kTdBlock / kWave];
+        sq = wave_sum(sq);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x / 64] = sq;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0.0;
+            for (int w = 0; w < kTdBlock / kWave; ++w) t += red[w];
+            partials[blockIdx.x] = t;
+        }
     }
 }
 
-__global__ __launch_bounds__(1024) void td_loss_kernel(const float *__restrict__ qc,
-                                                       const int64_t *__restrict__ act,
-                                                       const float *__restrict__ y, int64_t B,
-                                                       int A, float *__restrict__ loss) {
+__global__ __launch_bounds__(1024) void td_loss_finalize(const double *__restrict__ partials, int64_t nblk,
+                                                         int64_t B, float *__restrict__ loss) {
     __shared__ double red[1024 / kWave];
     double s = 0.0;
-    for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
-        const double diff = (double)qc[i * A + act[i]] - (double)y[i];
-        s += diff * diff;
-    }
+    for (int64_t i = threadIdx.x; i < nblk; i += blockDim.x) s += partials[i];
     s = wave_sum(s);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x / 64] = s;
     __syncthreads();
@@ -173,22 +189,28 @@ __global__ __launch_bounds__(kC51Waves * 64) void c51_kernel(
 
 using namespace agx;
 
+extern "C" size_t agx_td_workspace_bytes(int64_t B) {
+    return B > 0 ? (size_t)ceil_div(B, kTdBlock) * sizeof(double) : 0;
+}
+
 extern "C" int agx_td_target(const float *q_next_online, const float *q_next_target,
                              const float *q_cur, const int64_t *actions, const float *rewards,
                              const float *dones, int64_t B, int64_t A, double gamma, int double_q,
-                             float *y, float *g_q, float *loss, void *stream) {
+                             float *y, float *g_q, float *loss, void *workspace, void *stream) {
     AGX_REQUIRE(q_next_target && rewards && dones && y && B >= 0 && A > 0 && A < 65536,
                 "agx_td_target: bad arguments");
     AGX_REQUIRE(!double_q || q_next_online, "agx_td_target: double_q needs q_next_online");
     AGX_REQUIRE(!(g_q || loss) || (q_cur && actions), "agx_td_target: loss needs q_cur/actions");
+    AGX_REQUIRE(!loss || workspace, "agx_td_target: loss needs the workspace (agx_td_workspace_bytes)");
     if (B == 0) return AGX_OK;
     hipStream_t s = as_stream(stream);
-    td_target_kernel<<<(unsigned)ceil_div(B, 256), 256, 0, s>>>(
-        q_next_online, q_next_target, q_cur, actions, rewards, dones, B, (int)A, (float)gamma,
-        double_q, y, g_q);
+    const int64_t nblk = ceil_div(B, kTdBlock);
+    double *part = loss ? static_cast<double *>(workspace) : nullptr;
+    td_target_kernel<<<(unsigned)nblk, kTdBlock, 0, s>>>(q_next_online, q_next_target, q_cur, actions, rewards,
+                                                         dones, B, (int)A, (float)gamma, double_q, y, g_q, part);
     int rc = check_launch("agx_td_target");
     if (rc || !loss) return rc;
-    td_loss_kernel<<<1, 1024, 0, s>>>(q_cur, actions, y, B, (int)A, loss);
+    td_loss_finalize<<<1, 1024, 0, s>>>(part, nblk, B, loss);
     return check_launch("agx_td_target loss");
 }
 

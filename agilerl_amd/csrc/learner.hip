@@ -61,6 +61,7 @@ constexpr int kMaxA = 16;
 constexpr int kMaxBlk = 28;
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 struct NetDims {
     int D, A, ne, eo[3], ha, hc;
@@ -950,14 +951,22 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 const int upd = e * nmb + mb;
                 float *base = g.slabs + ((size_t)p * 2 + (upd & 1)) * g.K * pl.slab;
                 float *mine = base + (size_t)kk * pl.slab;
-                for (int i = tid; i < pl.param_end / 4; i += kNT)
-                    reinterpret_cast<f4 *>(mine)[i] = reinterpret_cast<const f4 *>(G)[i];
-                if (tid == 0) mine[pl.param_end] = lmb;
+                // write-through (sc1) slab stores: drained by every storing wave before
+                // the barrier, so no release fence (cdna_hip_programming.md §6 G16 R1)
+                {
+                    const int nbytes = __builtin_amdgcn_readfirstlane(pl.slab * 4);
+                    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(mine, 0, nbytes, 0x00020000);
+                    for (int i = tid; i < pl.param_end / 4; i += kNT) {
+                        const f4 v = reinterpret_cast<const f4 *>(G)[i];
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rsrc, i * 16, 0, 16);
+                    }
+                    if (tid == 0)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, lmb), rsrc,
+                                                              pl.param_end * 4, 0, 16);
+                }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 if (tid == 0) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __hip_atomic_fetch_add(g.cnt + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     AGX_STAMP(64 + 11);
                     const unsigned target = (unsigned)(g.K * (upd + 1));
@@ -971,6 +980,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                             break;
                         }
                     }
+                    // ONE agent-scope acquire, then plain loads (measured: sc1 loads of the
+                    // slabs instead of the acquire cost more than the fence saves)
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     stat[3 * kNW] = ok ? 1.f : 0.f;
@@ -981,29 +992,30 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 // fixed-order sum over partners: every workgroup of the agent computes
                 // bit-identical totals, hence bit-identical parameters after Adam
                 // (own slab read back from LDS: same bits as the stored copy).  Chunks
-                // of 2 float4 per thread with all partner loads issued before the adds.
+                // of 4 float4 per thread with all partner loads issued before the adds.
                 {
                     constexpr int n4 = pl.param_end / 4;
                     constexpr int NI = (n4 + kNT - 1) / kNT;
                     const f4 *G4 = reinterpret_cast<const f4 *>(G);
+                    auto slab_ld = [&](int q, int i) {
+                        return reinterpret_cast<const f4 *>(base + (size_t)q * pl.slab)[i];
+                    };
 #pragma unroll
-                    for (int j0 = 0; j0 < NI; j0 += 2) {
-                        f4 t[2], v[3][2];
+                    for (int j0 = 0; j0 < NI; j0 += 4) {
+                        f4 t[4], v[3][4];
 #pragma unroll
-                        for (int j = 0; j < 2; ++j) {
+                        for (int j = 0; j < 4; ++j) {
                             const int i = tid + (j0 + j) * kNT;
                             t[j] = f4{0.f, 0.f, 0.f, 0.f};
                             if (j0 + j < NI && i < n4) {
-                                t[j] = kk == 0 ? G4[i] : reinterpret_cast<const f4 *>(base)[i];
+                                t[j] = kk == 0 ? G4[i] : slab_ld(0, i);
 #pragma unroll
                                 for (int q = 1; q < 4; ++q)
-                                    if (q < g.K)
-                                        v[q - 1][j] = q == kk ? G4[i]
-                                                              : reinterpret_cast<const f4 *>(base + (size_t)q * pl.slab)[i];
+                                    if (q < g.K) v[q - 1][j] = q == kk ? G4[i] : slab_ld(q, i);
                             }
                         }
 #pragma unroll
-                        for (int j = 0; j < 2; ++j) {
+                        for (int j = 0; j < 4; ++j) {
                             const int i = tid + (j0 + j) * kNT;
                             if (j0 + j < NI && i < n4) {
 #pragma unroll
@@ -1026,15 +1038,23 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             }
 
             // ---- P10: two-group norm, Adam from registers -------------------------
+            // Branch-free over the owned slots: slots entirely inside the parameter
+            // region need no bounds test (padding slots carry g = m = v = 0, so
+            // Adam writes their value back unchanged); per-slot branches cost
+            // exec-mask traffic and SGPR spills.
+            constexpr int kFull = pl.param_end / kNT;                  // slots < param_end for every thread
+            constexpr int kUsed = (pl.param_end + kNT - 1) / kNT;      // slots that exist at all
             float n0 = 0.f, n1 = 0.f;
+            float gr[kMaxPT];  // gradients stay in registers for the Adam pass
 #pragma unroll
-            for (int i = 0; i < kMaxPT; ++i) {
+            for (int i = 0; i < kUsed; ++i) {
                 const int l = tid + kNT * i;
-                if ((vbits >> i) & 1u) {
-                    const float x = G[l];
-                    if ((gbits >> i) & 1u) n1 += x * x;
-                    else n0 += x * x;
-                }
+                const float x = (i < kFull || l < pl.param_end) ? G[l] : 0.f;
+                const bool valid = (vbits >> i) & 1u, crit = (gbits >> i) & 1u;
+                gr[i] = valid ? x : 0.f;
+                const float x2 = gr[i] * gr[i];
+                n1 += crit ? x2 : 0.f;
+                n0 += crit ? 0.f : x2;
             }
             AGX_IDS;
             // both group norms in one reduction round (fixed order)
@@ -1054,6 +1074,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 t1 += stat[kNW + i];
             }
             if (tid == 0) loss_total += lmb;
+            AGX_STAMP(64 + 14);
             const float c0 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t0) + 1e-6f), 1.f) : 1.f;
             const float c1 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t1) + 1e-6f), 1.f) : 1.f;
             // bias corrections 1 - beta^step from running f64 products (the
@@ -1065,18 +1086,25 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             const float bc2s = (float)sqrt(1.0 - pb2);
             const float step_size = lr_p / bc1;
             const float inv_bc2s = 1.f / bc2s;
+            float pv[kMaxPT];  // all parameter reads issued before any write
 #pragma unroll
-            for (int i = 0; i < kMaxPT; ++i) {
+            for (int i = 0; i < kUsed; ++i) {
                 const int l = tid + kNT * i;
-                if ((vbits >> i) & 1u) {  // G (activation alias) and the parameters are disjoint
-                    const float gr = G[l] * (((gbits >> i) & 1u) ? c1 : c0);
-                    am[i] = am[i] + (1.f - g.b1) * (gr - am[i]);
-                    av[i] = av[i] * g.b2 + (1.f - g.b2) * gr * gr;
+                pv[i] = (i < kFull || l < pl.param_end) ? sm[l] : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < kUsed; ++i) {
+                const int l = tid + kNT * i;
+                {
+                    const float gr_c = gr[i] * (((gbits >> i) & 1u) ? c1 : c0);
+                    am[i] = am[i] + (1.f - g.b1) * (gr_c - am[i]);
+                    av[i] = av[i] * g.b2 + (1.f - g.b2) * gr_c * gr_c;
                     // hardware sqrt / reciprocal (1 ulp) instead of the IEEE
                     // expansions: the update m/(sqrt(v)+eps) is compared within
                     // tolerance, never bit-exactly (summation order already differs)
                     const float denom = __builtin_amdgcn_sqrtf(av[i]) * inv_bc2s + g.eps;
-                    sm[l] = sm[l] - step_size * (am[i] * __builtin_amdgcn_rcpf(denom));
+                    const float nv = pv[i] - step_size * (am[i] * __builtin_amdgcn_rcpf(denom));
+                    if (i < kFull || l < pl.param_end) sm[l] = nv;
                 }
             }
             __syncthreads();

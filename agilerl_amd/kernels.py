@@ -204,9 +204,10 @@ def td_target(q_next_target, rewards, dones, gamma, q_next_online=None, double=F
         loss = torch.empty(1, dtype=_f32, device=r.device)
     else:
         a = None
+    ws = _ws(_lib.load().agx_td_workspace_bytes(B), r.device) if with_loss else None
     _lib.call("agx_td_target", _lib.ptr(q_next_online), q_next_target.data_ptr(), _lib.ptr(q_cur),
               _lib.ptr(a), r.data_ptr(), d.data_ptr(), B, A, float(gamma), int(bool(double)),
-              y.data_ptr(), _lib.ptr(g_q), _lib.ptr(loss), _lib.stream())
+              y.data_ptr(), _lib.ptr(g_q), _lib.ptr(loss), _lib.ptr(ws), _lib.stream())
     return y, g_q, loss
 
 

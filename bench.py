@@ -258,6 +258,81 @@ def roofline_leg(args):
 
 
 # --------------------------------------------------------------------------- #
+def _time(fn, reps=5):
+    """Mean HIP-event time (s) of fn on the current (launch) stream."""
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e-3 / reps
+
+
+def kernels_leg(peak_meas):
+    """Config-3 kernels at the SURVEY §8d synthetic shapes, algorithmic
+    bytes / HIP-event time: PER retrieve (+ IS weights) over a 2^20-leaf tree
+    with 2^20 uniforms, PER priority update of 2^16 indices (duplicates),
+    C51 projection + loss over 2^20 rows (A=6, Z=51), DQN TD target + loss
+    gradient over 2^20 rows (A=6)."""
+    from agilerl_amd import kernels as K
+
+    dev = "cuda"
+    out = {}
+    g = torch.Generator(device=dev).manual_seed(2)
+    cap, max_size = 1 << 20, 1_000_000
+    st = torch.empty(2 * cap, dtype=torch.float64, device=dev)
+    mt = torch.empty_like(st)
+    K.per_init(st, mt, cap)
+    maxp = torch.ones(1, dtype=torch.float64, device=dev)
+    ws = K.per_workspace(cap, dev)
+    K.per_add(st, mt, cap, max_size, 0, max_size, 0.6, maxp, workspace=ws)
+    allidx = torch.arange(max_size, device=dev)
+    pri = torch.randn(max_size, device=dev, generator=g).abs() + 1e-5
+    K.per_update(st, mt, cap, max_size, allidx, pri, 0.6, maxp, workspace=ws)
+    u = torch.rand(1 << 20, device=dev, generator=g)
+    t = _time(lambda: K.per_sample(st, mt, cap, u, size=max_size, beta=0.4, weights=True))
+    nb = (8 * 20 + 4 + 8 + 8 + 4) * u.numel()  # walk + uniform + index + leaf + weight
+    out["per_sample"] = dict(unit_bytes=nb // u.numel(), units=u.numel(), ms=round(t * 1e3, 4),
+                             gbs=round(nb / t / 1e9, 1), frac_of_measured=round(nb / t / 1e9 / peak_meas, 4),
+                             bound="latency (dependent 20-level walk)")
+    idx = torch.randint(0, max_size, (1 << 16,), device=dev, generator=g)
+    p2 = torch.rand(1 << 16, device=dev, generator=g)
+    t = _time(lambda: K.per_update(st, mt, cap, max_size, idx, p2, 0.6, maxp, workspace=ws))
+    nb = 976 * idx.numel()
+    out["per_update"] = dict(unit_bytes=976, units=idx.numel(), ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
+                             frac_of_measured=round(nb / t / 1e9 / peak_meas, 4),
+                             bound="latency (level-synchronous rebuild)")
+    del st, mt, ws, allidx, pri
+    B, A, Z = 1 << 20, 6, 51
+    g3 = torch.Generator(device=dev).manual_seed(3)
+    qn = torch.randn(B, A, device=dev, generator=g3)
+    td = torch.softmax(torch.randn(B, A, Z, device=dev, generator=g3), -1).clamp_(min=1e-3)
+    lp = torch.log_softmax(torch.randn(B, A, Z, device=dev, generator=g3), -1)
+    act = torch.randint(0, A, (B,), device=dev, generator=g3)
+    r = torch.randn(B, device=dev, generator=g3)
+    d = (torch.rand(B, device=dev, generator=g3) < 0.05).float()
+    sup = torch.linspace(-200, 200, Z, device=dev)
+    t = _time(lambda: K.c51_project_loss(qn, td, lp, act, r, d, sup, -200.0, 200.0, 0.99 ** 4))
+    nb = 444 * B
+    out["c51_project_loss"] = dict(unit_bytes=444, units=B, ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
+                                   frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
+    del td, lp
+    qt = torch.randn(B, A, device=dev, generator=g3)
+    qc = torch.randn(B, A, device=dev, generator=g3)
+    t = _time(lambda: K.td_target(qt, r, d, 0.99, q_next_online=qn, double=True, q_cur=qc, actions=act))
+    ub = 3 * 4 * A + 8 + 4 + 4 + 4 + 4 * A  # Q(s'), Qt(s'), Q(s) rows, a, r, d in; y, dL/dQ out
+    nb = ub * B
+    out["td_target"] = dict(unit_bytes=ub, units=B, ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
+                            frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
+    torch.cuda.empty_cache()
+    return out
+
+
+# --------------------------------------------------------------------------- #
 def cpu_baseline_leg(args, S_per_agent):
     """The reference-style CPU PPO iteration (oracle/ppo_cpu.py), one agent at a
     time like train_on_policy.py:210, on a bounded sample: whole agent
@@ -297,9 +372,10 @@ def main():
 
     _lib.load()
     res = population_leg(args, world, rank)
-    roof = None
+    roof = kern = None
     if not args.no_roofline:
         roof = roofline_leg(args)
+        kern = kernels_leg(roof["peak_measured"])
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline_leg(args, res["S"])
@@ -329,6 +405,7 @@ def main():
             "learner_updates_per_s": round(res["updates"] / res["dt"], 1),
             "generations": res["generations"],
             "roofline": roof,
+            "kernels": kern,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

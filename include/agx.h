@@ -231,10 +231,11 @@ int agx_segtree_retrieve(const double *tree, int64_t capacity, const double *upp
  * Replaces DQN.update's target + loss (agilerl/algorithms/dqn.py:296-314):
  * y = r + gamma*q_t*(1-d), q_t = max_a Qtgt(s') or Qtgt(s')[argmax Q(s')]
  * (double_q); loss = mean((Q(s)[a] - y)^2); g_q = d loss / d Q(s) (B,A). */
+size_t agx_td_workspace_bytes(int64_t B);
 int agx_td_target(const float *q_next_online, const float *q_next_target, const float *q_cur,
                   const int64_t *actions, const float *rewards, const float *dones, int64_t B,
                   int64_t A, double gamma, int double_q, float *y, float *g_q, float *loss,
-                  void *stream);
+                  void *workspace, void *stream);
 
 /* ---- Rainbow C51 projection + cross entropy ------------------------------
  * Replaces RainbowDQN._dqn_loss (agilerl/algorithms/dqn_rainbow.py:313-367).

@@ -42,5 +42,5 @@ for sb in range(4):
     print(f"sb{sb}: " + "  ".join(f"{n}={c}" for n, c in zip(names, seg)) + f"  total={row[7] - row[0]}")
 last = max(v for v in st[:64] if v)
 print("dump", st[64 + 9] - last, "| exchange: publish", st[64 + 11] - st[64 + 9], "wait+acquire",
-      st[64 + 12] - st[64 + 11], "sum", st[64 + 13] - st[64 + 12], "| norm+adam", st[64 + 10] - st[64 + 13],
+      st[64 + 12] - st[64 + 11], "sum", st[64 + 13] - st[64 + 12], "| norm", st[64 + 14] - st[64 + 13], "adam", st[64 + 10] - st[64 + 14],
       "| minibatch total cycles", st[64 + 10] - st[0])
