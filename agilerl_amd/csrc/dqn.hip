@@ -185,6 +185,174 @@ __global__ __launch_bounds__(kC51Waves * 64) void c51_kernel(
     if (lane == 0 && live) loss[i] = -part;
 }
 
+// Z <= 64 (Rainbow: Z = 51): R rows per wave, processed in lock-step so the
+// dependent load levels (Q(s') row -> a* -> target row; a -> log_p row)
+// overlap.  The serial index_add_ order is kept without a search: L (and U)
+// is monotone in z, so the atoms feeding bin b form one run [s_b, e_b);
+// the atom that starts (ends) a run writes s_b (e_b) into per-wave LDS, and
+// bin lane b then folds its run left to right, reading the run's masses from
+// the atom lanes with ds_bpermute — the same additions, in the same order,
+// as the reference's two index_add_ calls.  Rows whose L/U are not monotone
+// take the ordered scan of c51_kernel.
+constexpr int kC51RowWaves = 4;
+
+__device__ __forceinline__ float bperm_f(int src_lane, float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_lane << 2, __builtin_bit_cast(int, v)));
+}
+template <int C>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), C, 0xf, 0xf, true));
+}
+// wave-wide sum (DPP within rows of 16, then the 4 row results)
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v += dpp_f<0xb1>(v);
+    v += dpp_f<0x4e>(v);
+    v += dpp_f<0x141>(v);
+    v += dpp_f<0x140>(v);
+    const int vi = __builtin_bit_cast(int, v);
+    return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(vi, 0)) +
+            __builtin_bit_cast(float, __builtin_amdgcn_readlane(vi, 16))) +
+           (__builtin_bit_cast(float, __builtin_amdgcn_readlane(vi, 32)) +
+            __builtin_bit_cast(float, __builtin_amdgcn_readlane(vi, 48)));
+}
+
+template <int R>
+__global__ __launch_bounds__(kC51RowWaves * 64) void c51_rows_kernel(
+    const float *__restrict__ qno, const float *__restrict__ tdist, const float *__restrict__ logp,
+    const int64_t *__restrict__ act, const float *__restrict__ rew, const float *__restrict__ dn,
+    const float *__restrict__ support, int64_t B, int A, int Z, float vmin, float vmax, float dz, float g,
+    float *__restrict__ loss, float *__restrict__ proj) {
+    // per row: monotone -> L-run start, L-run end, U-run start, U-run end per bin;
+    // otherwise (ordered-scan fallback) L, U, lower mass, upper mass per atom
+    __shared__ int sRun[kC51RowWaves][R][4][64];
+    const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
+    const int64_t row0 = ((int64_t)blockIdx.x * kC51RowWaves + __builtin_amdgcn_readfirstlane(w)) * R;
+    int64_t ri[R];
+    int astar[R];
+    float rr[R], kk[R];
+    int64_t ai[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        ri[r] = row0 + r < B ? row0 + r : B - 1;  // dead rows shadow the last row, store nothing
+        ai[r] = act[ri[r]];
+        rr[r] = rew[ri[r]];
+        kk[r] = (1.0f - dn[ri[r]]) * g;
+        // a* = argmax_a Q_online(s'), first maximum; the row is wave-uniform
+        const float *qr = qno + ri[r] * A;
+        float bv = qr[0];
+        int ba = 0;
+        if (A <= 8) {  // all (scalar) loads issued together
+            float qv[8];
+#pragma unroll
+            for (int a = 1; a < 8; ++a) qv[a] = a < A ? qr[a] : -__builtin_inff();
+#pragma unroll
+            for (int a = 1; a < 8; ++a)
+                if (qv[a] > bv) {
+                    bv = qv[a];
+                    ba = a;
+                }
+        } else {
+            for (int a = 1; a < A; ++a) {
+                const float qa = qr[a];
+                if (qa > bv) {
+                    bv = qa;
+                    ba = a;
+                }
+            }
+        }
+        astar[r] = ba;
+    }
+    const float sup = lane < Z ? support[lane] : 0.f;
+    float p[R], lp[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        p[r] = lane < Z ? tdist[((size_t)ri[r] * A + astar[r]) * Z + lane] : 0.f;
+        lp[r] = lane < Z ? logp[((size_t)ri[r] * A + ai[r]) * Z + lane] : 0.f;
+    }
+    int Lr[R], Ur[R];
+    float mlr[R], mur[R];
+    bool mono[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int L = 0x7fffffff, U = 0x7fffffff;  // lanes >= Z: beyond every bin
+        float ml = 0.f, mu = 0.f;
+        if (lane < Z) {
+            float tz = rr[r] + kk[r] * sup;
+            tz = fminf(fmaxf(tz, vmin), vmax);
+            const float b = (tz - vmin) / dz;
+            L = (int)floorf(b);
+            U = (int)ceilf(b);
+            if (U > 0 && U == L) L -= 1;
+            if (Z - 1 > L && U == L) U += 1;
+            L = L < 0 ? 0 : (L > Z - 1 ? Z - 1 : L);
+            U = U < 0 ? 0 : (U > Z - 1 ? Z - 1 : U);
+            ml = p[r] * ((float)U - b);
+            mu = p[r] * (b - (float)L);
+        }
+        Lr[r] = L;
+        Ur[r] = U;
+        mlr[r] = ml;
+        mur[r] = mu;
+        const int Lp = __shfl_up(L, 1, 64), Up = __shfl_up(U, 1, 64);
+        const int Ln = __shfl_down(L, 1, 64), Un = __shfl_down(U, 1, 64);
+        mono[r] = __all(!(lane + 1 < Z) || (Ln >= L && Un >= U));
+        // empty runs by default; run starts / ends written by their atoms
+        sRun[w][r][0][lane] = 0;
+        sRun[w][r][1][lane] = 0;
+        sRun[w][r][2][lane] = 0;
+        sRun[w][r][3][lane] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (mono[r] && lane < Z) {
+            if (lane == 0 || Lp != L) sRun[w][r][0][L] = lane;
+            if (lane + 1 == Z || Ln != L) sRun[w][r][1][L] = lane + 1;
+            if (lane == 0 || Up != U) sRun[w][r][2][U] = lane;
+            if (lane + 1 == Z || Un != U) sRun[w][r][3][U] = lane + 1;
+        }
+        if (!mono[r]) {
+            sRun[w][r][0][lane] = L;
+            sRun[w][r][1][lane] = U;
+            sRun[w][r][2][lane] = __builtin_bit_cast(int, ml);
+            sRun[w][r][3][lane] = __builtin_bit_cast(int, mu);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int bin = lane;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        float acc = 0.f;
+        if (mono[r]) {
+            const int l0 = sRun[w][r][0][bin], l1 = sRun[w][r][1][bin];
+            const int u0 = sRun[w][r][2][bin], u1 = sRun[w][r][3][bin];
+            // wave-uniform trip counts; masses come from the atom lanes
+            int nl = l1 - l0, nu = u1 - u0;
+            for (int o = 32; o > 0; o >>= 1) {
+                nl = max(nl, __shfl_xor(nl, o, 64));
+                nu = max(nu, __shfl_xor(nu, o, 64));
+            }
+            for (int t = 0; t < nl; ++t) {
+                const float m = bperm_f(l0 + t, mlr[r]);
+                if (l0 + t < l1) acc += m;
+            }
+            for (int t = 0; t < nu; ++t) {
+                const float m = bperm_f(u0 + t, mur[r]);
+                if (u0 + t < u1) acc += m;
+            }
+        } else if (bin < Z) {
+            for (int z = 0; z < Z; ++z)
+                if (sRun[w][r][0][z] == bin) acc += __builtin_bit_cast(float, sRun[w][r][2][z]);
+            for (int z = 0; z < Z; ++z)
+                if (sRun[w][r][1][z] == bin) acc += __builtin_bit_cast(float, sRun[w][r][3][z]);
+        }
+        const bool live = row0 + r < B;
+        if (proj && live && bin < Z) proj[(size_t)ri[r] * Z + bin] = acc;
+        const float part = wave_sum_dpp(bin < Z ? acc * lp[r] : 0.f);
+        if (lane == 0 && live) loss[ri[r]] = -part;
+    }
+}
+
 }  // namespace agx
 
 using namespace agx;
@@ -226,6 +394,14 @@ extern "C" int agx_c51_project_loss(const float *q_next_online, const float *tar
                 kC51MaxZ);
     if (B == 0) return AGX_OK;
     const float dz = (float)((v_max - v_min) / (double)(Z - 1));  // python float -> f32 operand
+    if (Z <= 64 && A <= 64) {
+        constexpr int R = 4;
+        const int64_t rows_per_block = (int64_t)kC51RowWaves * R;
+        c51_rows_kernel<R><<<(unsigned)ceil_div(B, rows_per_block), kC51RowWaves * 64, 0, as_stream(stream)>>>(
+            q_next_online, target_dist, logp_cur, actions, rewards, dones, support, B, (int)A, (int)Z,
+            (float)v_min, (float)v_max, dz, (float)gamma, loss, proj);
+        return check_launch("agx_c51_project_loss");
+    }
     c51_kernel<<<(unsigned)ceil_div(B, kC51Waves), kC51Waves * 64, 0, as_stream(stream)>>>(
         q_next_online, target_dist, logp_cur, actions, rewards, dones, support, B, (int)A, (int)Z,
         (float)v_min, (float)v_max, dz, (float)gamma, loss, proj);
