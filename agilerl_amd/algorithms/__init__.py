@@ -1,0 +1,6 @@
+"""Drop-in algorithm classes (agilerl.algorithms) on the agx hot path."""
+
+from .dqn import DQN, RainbowDQN
+from .ppo import PPO
+
+__all__ = ["PPO", "DQN", "RainbowDQN"]

@@ -1,0 +1,186 @@
+"""Drop-in ``PPO`` (agilerl/algorithms/ppo.py:108-1290) for discrete-action
+MLP actor-critics, backed by the HBM population engine.
+
+A ``PPO`` object is a *view* of one row of a :class:`PPOPopulation` (its
+parameters, Adam state and rollout SoA live in HBM, stacked with the other
+agents of the population).  ``create_population`` (agilerl_amd.utils) builds
+one population and P views, so ``train_on_policy`` can run the whole
+population with one launch per kernel; a standalone ``PPO(...)`` owns a
+population of one.
+
+Supported: Discrete action spaces, Box observations, ``net_config`` with
+``encoder_config`` / ``head_config`` MLP ``hidden_size`` lists and
+``latent_dim`` (the reference's defaults: encoder [64] -> latent 64, actor
+head [64], critic head [16] unless ``head_config`` is given, ppo.py:286-300),
+LayerNorm on, shared encoder.  ``get_action`` / ``learn`` / ``test`` keep the
+reference's signatures and return types; action masks, recurrent policies,
+continuous actions and custom ``actor_network`` objects raise
+NotImplementedError (outside the hot path).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Any
+
+import numpy as np
+import torch
+
+from .. import _lib
+from ..population.nets import ActorCriticSpec
+from ..population.ppo_pop import PPOPopulation
+
+
+def _hidden(cfg: dict | None, default: list[int]) -> list[int]:
+    if cfg is None:
+        return list(default)
+    if hasattr(cfg, "hidden_size"):
+        return list(cfg.hidden_size)
+    return list(cfg.get("hidden_size", default))
+
+
+def spec_from_net_config(observation_space, action_space, net_config: dict | None) -> ActorCriticSpec:
+    if not hasattr(action_space, "n"):
+        raise NotImplementedError("agx PPO supports Discrete action spaces")
+    net_config = dict(net_config or {})
+    enc = _hidden(net_config.get("encoder_config"), [64])
+    head = net_config.get("head_config")
+    actor_hidden = _hidden(head, [64])
+    critic_hidden = _hidden(head, [16])  # ppo.py:292-300 default critic head
+    latent = int(net_config.get("latent_dim", 64))
+    obs_dim = int(np.prod(observation_space.shape))
+    return ActorCriticSpec(obs_dim=obs_dim, n_actions=int(action_space.n), encoder_hidden=enc, latent_dim=latent,
+                           actor_hidden=actor_hidden, critic_hidden=critic_hidden)
+
+
+class PPO:
+    algo = "PPO"
+
+    def __init__(self, observation_space, action_space, index: int = 0, hp_config=None,
+                 net_config: dict[str, Any] | None = None, batch_size: int = 64, lr: float = 1e-4,
+                 learn_step: int = 2048, gamma: float = 0.99, gae_lambda: float = 0.95, mut=None,
+                 action_std_init: float = 0.0, clip_coef: float = 0.2, ent_coef: float = 0.01,
+                 vf_coef: float = 0.5, max_grad_norm: float = 0.5, target_kl: float | None = None,
+                 normalize_images: bool = True, update_epochs: int = 4, actor_network=None, critic_network=None,
+                 share_encoders: bool = True, num_envs: int = 1, use_rollout_buffer: bool = True,
+                 rollout_buffer_config=None, recurrent: bool = False, device="cuda", accelerator=None,
+                 wrap: bool = True, bptt_sequence_type=None, max_seq_len=None, *, _population=None,
+                 _row: int | None = None) -> None:
+        if recurrent:
+            raise NotImplementedError("recurrent PPO is outside the agx hot path")
+        if actor_network is not None or critic_network is not None:
+            raise NotImplementedError("custom actor/critic modules: use net_config (MLP) networks")
+        if not share_encoders:
+            raise NotImplementedError("agx PPO uses the shared-encoder actor-critic (the reference default)")
+        assert isinstance(batch_size, int) and batch_size >= 1, "Batch size must be an integer greater than or equal to one."
+        assert lr > 0, "Learning rate must be greater than zero."
+        assert isinstance(learn_step, int) and learn_step >= 1, "Learn step rate must be an integer greater than or equal to one."
+        self.observation_space, self.action_space = observation_space, action_space
+        self.index = index
+        self.net_config = net_config
+        self.batch_size, self.lr, self.learn_step = batch_size, lr, learn_step
+        self.gamma, self.gae_lambda, self.mut = gamma, gae_lambda, mut
+        self.clip_coef, self.ent_coef, self.vf_coef = clip_coef, ent_coef, vf_coef
+        self.max_grad_norm, self.target_kl, self.update_epochs = max_grad_norm, target_kl, update_epochs
+        self.num_envs = num_envs
+        self.device = torch.device(device)
+        self.scores: list[float] = []
+        self.fitness: list[float] = []
+        self.steps: list[int] = [0]
+        if _population is None:
+            spec = spec_from_net_config(observation_space, action_space, net_config)
+            _population = PPOPopulation(spec, 1, num_envs, learn_step=learn_step, batch_size=batch_size, lr=lr,
+                                        gamma=gamma, gae_lambda=gae_lambda, clip_coef=clip_coef, ent_coef=ent_coef,
+                                        vf_coef=vf_coef, max_grad_norm=max_grad_norm, update_epochs=update_epochs,
+                                        target_kl=target_kl, seeds=[index], device=self.device)
+            _row = 0
+        self.population, self.row = _population, int(_row)
+        self._counter = 0
+
+    # ------------------------------------------------------------------ #
+    @property
+    def spec(self) -> ActorCriticSpec:
+        return self.population.spec
+
+    def state_dict(self) -> dict[str, torch.Tensor]:
+        """Reference-compatible parameter names (actor.encoder / head_net /
+        critic.head_net ...) -> tensors (views of the HBM row)."""
+        flat = self.population.params.data[self.row]
+        return {k: flat[off:off + int(np.prod(shape))].view(shape)
+                for k, (off, shape) in self.spec.state_dict_keys().items()}
+
+    @torch.no_grad()
+    def get_action(self, obs, action_mask=None, hidden_state=None, *args, **kwargs):
+        """-> (action, log_prob, entropy, value) numpy arrays (ppo.py:567-633);
+        sampling is a Gumbel-max draw from a counter-based Philox stream."""
+        if action_mask is not None:
+            raise NotImplementedError("action masks are not supported by the agx policy step")
+        pop = self.population
+        o = torch.as_tensor(np.asarray(obs), dtype=torch.float32, device=self.device)
+        o = o.reshape(-1, pop.spec.obs_dim).contiguous()
+        n = o.shape[0]
+        out = dict(actions=torch.empty(n, dtype=torch.int64, device=self.device),
+                   log_probs=torch.empty(n, device=self.device), values=torch.empty(n, device=self.device),
+                   entropy=torch.empty(n, device=self.device))
+        desc = pop.fused_descriptor()
+        if desc is None:
+            logits, value = pop.spec.forward(pop.params.data[self.row:self.row + 1], o.unsqueeze(0))
+            from ..population.nets import categorical
+
+            logp_all, ent = categorical(logits)
+            u = torch.rand(logits.shape, device=self.device).clamp_(min=1e-20)
+            a = torch.argmax(logits - torch.log(-torch.log(u)), dim=-1)
+            out["actions"], out["values"], out["entropy"] = a.view(-1), value.view(-1), ent.view(-1)
+            out["log_probs"] = logp_all.gather(-1, a.unsqueeze(-1)).view(-1)
+        else:
+            self._counter += 1
+            params = pop.params.data[self.row]
+            _lib.call("agx_ppo_act", ctypes.byref(desc), 1, n, params.data_ptr(), o.data_ptr(), 0, 1,
+                      pop.act_seed + 7919 * self.row, (1 << 40) + self._counter, out["actions"].data_ptr(),
+                      out["log_probs"].data_ptr(), out["values"].data_ptr(), out["entropy"].data_ptr(), 0, None,
+                      None, _lib.stream())
+        return tuple(out[k].cpu().numpy() for k in ("actions", "log_probs", "entropy", "values"))
+
+    def learn(self, experiences=None) -> float:
+        """One PPO update of this agent from the HBM rollout (ppo.py:635-921);
+        returns the reference's mean loss (sum / (num_samples * epochs))."""
+        if experiences is not None:
+            raise NotImplementedError("agx PPO learns from its HBM rollout buffer (use_rollout_buffer=True path)")
+        # Views of one population learn together: the first view to call learn()
+        # after a rollout runs the fused learner for every agent (each agent is
+        # updated exactly once per rollout, as in the reference's per-agent loop).
+        pop = self.population
+        if getattr(pop, "_learned_rollout", None) != pop.rollout_id:
+            pop._last_losses = pop.learn().cpu().numpy()
+            pop._learned_rollout = pop.rollout_id
+        return float(pop._last_losses[self.row])
+
+    @torch.no_grad()
+    def test(self, env, swap_channels: bool = False, max_steps: int | None = None, loop: int = 3,
+             vectorized: bool = True, callback=None) -> float:
+        """Mean score over ``loop`` passes in which every env finishes one
+        episode (ppo.py:1113-1289); appends to ``self.fitness``."""
+        rewards = []
+        num_envs = env.num_envs if hasattr(env, "num_envs") and vectorized else 1
+        for _ in range(loop):
+            obs, _info = env.reset()
+            scores = np.zeros(num_envs)
+            completed = np.zeros(num_envs)
+            finished = np.zeros(num_envs, dtype=bool)
+            step = 0
+            while not np.all(finished):
+                action, _, _, _ = self.get_action(obs)
+                obs, reward, term, trunc, _info = env.step(action)
+                step += 1
+                scores += np.asarray(reward).reshape(num_envs)
+                done = np.logical_or(term, trunc).reshape(num_envs)
+                if max_steps is not None and step == max_steps:
+                    done = np.ones(num_envs, dtype=bool)
+                for i in range(num_envs):
+                    if done[i] and not finished[i]:
+                        completed[i] = scores[i]
+                        finished[i] = True
+            rewards.append(float(np.mean(completed)))
+        mean_fit = float(np.mean(rewards))
+        self.fitness.append(mean_fit)
+        return mean_fit

@@ -257,7 +257,9 @@ constexpr LearnPlan make_plan(NetDims d) {
 #define AGX_PPO_SHAPES(X)                 \
     X(8, 4, 2, 64, 64, 0, 64, 64)  /* LunarLander config 2 (ppo.yaml) */ \
     X(4, 2, 2, 64, 64, 0, 64, 64)  /* CartPole */                        \
-    X(6, 3, 2, 64, 64, 0, 64, 64)  /* Acrobot */
+    X(6, 3, 2, 64, 64, 0, 64, 64)  /* Acrobot */                         \
+    X(8, 4, 2, 64, 64, 0, 64, 16)  /* reference PPO default critic head [16] */ \
+    X(4, 2, 2, 64, 64, 0, 64, 16)
 
 template <int D_, int A_, int NE_, int E0, int E1, int E2, int HA, int HC>
 struct Shape {

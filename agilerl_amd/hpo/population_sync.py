@@ -26,12 +26,20 @@ class PopulationSync:
                  elitism: bool = True, eval_loop: int = 1):
         self.pop, self.runner = pop, runner
         self.world, self.rank = world, rank
-        self.rng_state = np.random.RandomState(seed)
+        # seed=None: draw from the GLOBAL numpy RNG, exactly as the reference's
+        # TournamentSelection does (tournament.py:41-51); else a private stream
+        self.rng_state = None if seed is None else np.random.RandomState(seed)
+        self.fitness_override = None  # host fitness for the next generation (else from the episode stats)
         self.tournament_size, self.elitism, self.eval_loop = tournament_size, elitism, eval_loop
         self.history: list[np.ndarray] = []
         self.last_parents: list[int] = []
 
     def _fitness(self) -> torch.Tensor:
+        if self.fitness_override is not None:
+            f = torch.as_tensor(np.asarray(self.fitness_override, dtype=np.float64), device=self.pop.device)
+            self.fitness_override = None
+            self.runner.reset_episode_stats()
+            return f
         r = self.runner
         f = torch.where(r.episodes > 0, r.episode_return_sum / r.episodes.clamp(min=1).double(),
                         torch.full_like(r.episode_return_sum, -1e9))
@@ -51,11 +59,14 @@ class PopulationSync:
         fit = self._all_gather(self._fitness()).cpu().numpy()  # the only host sync of the step
         self.history.append(fit)
         fits = [np.stack([h[i] for h in self.history[-self.eval_loop:]]) for i in range(len(fit))]
-        state = np.random.get_state()
-        np.random.set_state(self.rng_state.get_state())
-        _, parents = select_parents(fits, self.tournament_size, self.elitism, self.eval_loop)
-        self.rng_state.set_state(np.random.get_state())
-        np.random.set_state(state)
+        if self.rng_state is None:
+            _, parents = select_parents(fits, self.tournament_size, self.elitism, self.eval_loop)
+        else:
+            state = np.random.get_state()
+            np.random.set_state(self.rng_state.get_state())
+            _, parents = select_parents(fits, self.tournament_size, self.elitism, self.eval_loop)
+            self.rng_state.set_state(np.random.get_state())
+            np.random.set_state(state)
         P = pop.P
         mine = torch.as_tensor(parents[self.rank * P:(self.rank + 1) * P], device=pop.device)
         for buf in (pop.params.data, pop.opt.exp_avg, pop.opt.exp_avg_sq):

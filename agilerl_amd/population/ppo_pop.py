@@ -88,6 +88,7 @@ class PPOPopulation:
         self._desc = None
         self._alloc_rollout()
         self.learn_steps = 0
+        self.rollout_id = 0
 
     # ------------------------------------------------------------------ #
     def _alloc_rollout(self):
@@ -163,6 +164,7 @@ class PPOPopulation:
                        last_value: torch.Tensor | None = None):
         """Bootstrap value + GAE (+ per-agent advantage statistics).  The fused
         runner computes last_value in its final rollout-step launch."""
+        self.rollout_id += 1
         if last_value is None:
             _, last_value = self.spec.forward(self.params.data, last_obs)
         K.gae(self.rewards, self.dones, self.values, last_value.contiguous(), last_done.contiguous(),

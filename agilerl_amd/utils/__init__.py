@@ -1,0 +1,50 @@
+"""create_population (agilerl/utils/utils.py:347-): P agents of one algorithm.
+
+For PPO the agents are views of ONE HBM-resident PPOPopulation (stacked
+parameters / Adam state / rollout SoA), so a whole population is trained with
+one launch per kernel; the INIT_HP keys and defaults follow the reference
+(utils.py:502-537)."""
+
+from __future__ import annotations
+
+from typing import Any
+
+import torch
+
+
+def create_population(algo: str, net_config: dict[str, Any] | None, INIT_HP: dict[str, Any], observation_space=None,
+                      action_space=None, hp_config=None, actor_network=None, critic_network=None,
+                      agent_wrapper=None, wrapper_kwargs=None, population_size: int = 1, num_envs: int = 1,
+                      device="cuda", accelerator=None, torch_compiler=None, algo_kwargs=None, **_unused):
+    algo_kwargs = dict(algo_kwargs or {})
+    if algo == "PPO":
+        from ..algorithms.ppo import PPO, spec_from_net_config
+        from ..population.ppo_pop import PPOPopulation
+
+        if actor_network is not None or critic_network is not None:
+            raise NotImplementedError("custom actor/critic modules: use net_config (MLP) networks")
+        hp = dict(batch_size=INIT_HP.get("BATCH_SIZE", 64), lr=INIT_HP.get("LR", 0.0001),
+                  learn_step=INIT_HP.get("LEARN_STEP", 2048), gamma=INIT_HP.get("GAMMA", 0.99),
+                  gae_lambda=INIT_HP.get("GAE_LAMBDA", 0.95), clip_coef=INIT_HP.get("CLIP_COEF", 0.2),
+                  ent_coef=INIT_HP.get("ENT_COEF", 0.01), vf_coef=INIT_HP.get("VF_COEF", 0.5),
+                  max_grad_norm=INIT_HP.get("MAX_GRAD_NORM", 0.5), target_kl=INIT_HP.get("TARGET_KL"),
+                  update_epochs=INIT_HP.get("UPDATE_EPOCHS", 4))
+        if INIT_HP.get("RECURRENT", False):
+            raise NotImplementedError("recurrent PPO is outside the agx hot path")
+        spec = spec_from_net_config(observation_space, action_space, net_config)
+        pop = PPOPopulation(spec, population_size, num_envs, seeds=list(range(population_size)),
+                            device=torch.device(device), **hp)
+        return [PPO(observation_space, action_space, index=i, hp_config=hp_config, net_config=net_config,
+                    num_envs=num_envs, device=device, _population=pop, _row=i, **hp, **algo_kwargs)
+                for i in range(population_size)]
+    if algo in ("DQN", "Rainbow DQN", "RainbowDQN"):
+        from ..algorithms.dqn import DQN, RainbowDQN
+
+        cls = DQN if algo == "DQN" else RainbowDQN
+        return [cls.from_init_hp(observation_space, action_space, net_config, INIT_HP, index=i, device=device,
+                                 **algo_kwargs)
+                for i in range(population_size)]
+    raise NotImplementedError(f"algorithm {algo!r} is outside the agx hot path (PPO, DQN, Rainbow DQN)")
+
+
+__all__ = ["create_population"]
