@@ -341,20 +341,24 @@ __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
 // C[16x16] += A[16 x K] B[K x 16], K % 16 == 0 (operands batched 4 k-steps
 // at a time so LDS latency overlaps the MFMA chain)
+#ifndef AGX_MFMA_KB
+#define AGX_MFMA_KB 16
+#endif
 template <int K, class FA, class FB>
 __device__ __forceinline__ f4 mfma_tile(f4 acc, FA a, FB b) {
     const int lane = vlane();
     const int r = lane & 15, q = lane >> 4;
+    constexpr int KB = K < AGX_MFMA_KB ? K : AGX_MFMA_KB;  // k values whose operands are loaded per batch
 #pragma unroll
-    for (int k0 = 0; k0 < K; k0 += 16) {
-        float av[4], bv[4];
+    for (int k0 = 0; k0 < K; k0 += KB) {
+        float av[KB / 4], bv[KB / 4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < KB / 4; ++j) {
             av[j] = a(r, k0 + 4 * j + q);
             bv[j] = b(k0 + 4 * j + q, r);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
+        for (int j = 0; j < KB / 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
     }
     return acc;
 }
@@ -502,11 +506,23 @@ struct Fwd {
     }
 };
 
-template <class C>
-__device__ void load_params(float *sm, const float *gp, int tid) {
+template <class C, int B>
+__device__ __forceinline__ void blk_copy(float *sm, const float *gp, int tid) {
     constexpr LearnPlan pl = C::plan;
-#pragma unroll 8
-    for (int f = tid; f < pl.n; f += kNT) sm[flat_to_lds<C>(f)] = gp[f];
+    if constexpr (B < pl.nblk) {
+        constexpr Blk k = pl.blk[B];
+#pragma unroll 4
+        for (int i = tid; i < k.len; i += kNT) sm[k.l0 + (i / k.rowlen) * k.ldst + i % k.rowlen] = gp[k.f0 + i];
+        blk_copy<C, B + 1>(sm, gp, tid);
+    }
+}
+
+template <class C>
+__device__ __forceinline__ void load_params(float *sm, const float *gp, int tid) {
+    // block by block (compile-time table): one division by a constant row
+    // length per element instead of a search over all blocks
+    constexpr LearnPlan pl = C::plan;
+    blk_copy<C, 0>(sm, gp, tid);
 }
 
 struct LearnArgs {
@@ -1448,10 +1464,8 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, f
     int K = max_partners(P);
     if (K > nsb) K = (int)nsb;
     AGX_REQUIRE(P * K <= 65535, "agx_ppo_learn: too many workgroups");
-    if (K > 1) {
-        // counters + timeout word: one 16-byte-multiple block at the workspace start
-        if (hipMemsetAsync(ws, 0, w.gobs, s) != hipSuccess) return check_launch("agx_ppo_learn memset");
-    }
+    // counters + timeout word: one 16-byte-multiple block at the workspace start
+    if (hipMemsetAsync(ws, 0, w.gobs, s) != hipSuccess) return check_launch("agx_ppo_learn memset");
     dim3 ggrid((unsigned)ceil_div(S, 256), (unsigned)(epochs * P));
     ppo_gather_kernel<<<ggrid, 256, 0, s>>>(obs, reinterpret_cast<const long long *>(actions), old_logp, adv, ret,
                                             old_value, adv_stats, reinterpret_cast<const long long *>(perms), S,

@@ -85,6 +85,13 @@ class FusedLearner:
         opt.step_count += pop.update_epochs * pop.n_minibatches()
         return self.loss
 
+    def timed_out(self, pop) -> bool:
+        """True if a partner workgroup of the last learn() gave up waiting for
+        another (the kernel's bounded spin; the timeout word follows the P
+        arrival counters at the start of the workspace).  Synchronises."""
+        word = self.ws[4 * pop.P: 4 * pop.P + 4].view(torch.int32)
+        return bool(int(word.item()) != 0)
+
 
 def fused_learn(pop, perms=None) -> torch.Tensor:
     if getattr(pop, "_fused", None) is None:

@@ -205,6 +205,7 @@ def test_fused_learner_partner_split_consistent(split, monkeypatch):
     _restore(pop, st)
     loss_f = fused_learn(pop, perms).clone()
     torch.cuda.synchronize()
+    assert not pop._fused.timed_out(pop)
     m_f = pop.opt.exp_avg
     np.testing.assert_allclose(m_f.cpu().numpy(), m_t.cpu().numpy(), rtol=2e-3, atol=1e-5 * m_t.abs().max().item())
     np.testing.assert_allclose(loss_f.cpu().numpy(), loss_t.cpu().numpy(), rtol=1e-4, atol=1e-7)
