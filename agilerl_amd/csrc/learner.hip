@@ -320,10 +320,13 @@ __device__ __forceinline__ int swave() {
     asm volatile("" : "+s"(w));
     return w;
 }
+// Row passes: wave w owns rows w, w+8, w+16, w+24 (16 lanes per row), so the
+// two rows of a 32-lane LDS group are 8 rows apart: 8 * ld = 16 (mod 32) for
+// every padded stride here -> conflict-free ds_read_b32 (rows 1 apart were 2-way).
 #define AGX_IDS                                             \
     const int lane = vlane(), wave = swave();               \
     const int lr16 = lane & 15, lq = lane >> 4;             \
-    const int rrow = wave * 4 + lq, sub = lr16;             \
+    const int rrow = wave + kNW * lq, sub = lr16;           \
     (void)lr16, (void)lq, (void)rrow, (void)sub, (void)lane
 
 // workgroup-uniform sum (fixed order); uses stat[slot*kNW .. +kNW)
@@ -1261,7 +1264,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_act_kernel(ActArgs g) {
     Fwd<C> fw{sm};
     fw.run();
     // categorical over 16 lanes per row
-    const int r = wave * 4 + (lane >> 4), a = lane & 15;
+    const int r = wave + kNW * (lane >> 4), a = lane & 15;
     const bool live = r < nrow;
     const float lg = a < pl.A ? sm[pl.l_lg + r * kMaxA + a] : -3.0e38f;
     const float mx = row_max(lg);
