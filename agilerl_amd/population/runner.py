@@ -7,12 +7,14 @@ EVERY agent is, on the fused path (agx_ppo_rollout_step):
   1. ONE launch: scatter the staged obs into rollout slot t, the staged
      reward/done of step t-1 into slot t-1 (+ episode accounting), and the
      policy step (MFMA forward, Gumbel-max sample) writing action / log-prob /
-     value into slot t and a contiguous action copy;
-  2. ONE D2H of the P*N actions into pinned memory + an event wait (the only
-     synchronisation);
+     value into slot t and the P*N actions;
+  2. an event wait (the only synchronisation);
   3. the host env step, writing obs / reward / done straight into ONE packed
-     pinned staging buffer;
-  4. ONE async H2D of that staging buffer.
+     pinned staging buffer.
+The staging buffer and the action buffer are pinned host memory that the
+kernel reads / writes directly (zero-copy over the host link: 40 KB in and
+8 KB out per step at config 2), so a step is one launch and one wait; with
+AGX_ZERO_COPY=0 the staging goes through one H2D and one D2H copy instead.
 
 Architectures outside the fused kernels use the plain-PyTorch policy step
 with per-field copies (``_collect_torch``).
@@ -21,6 +23,7 @@ with per-field copies (``_collect_torch``).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -76,6 +79,7 @@ class PopulationRunner:
         self.ret_sum_env = torch.zeros(P * N, dtype=torch.float64, device=dev)
         self.episodes_env = torch.zeros(P * N, dtype=torch.int64, device=dev)
         self._ios = None
+        self.zero_copy = os.environ.get("AGX_ZERO_COPY", "1") != "0"
 
     # ------------------------------------------------------------------ #
     @property
@@ -98,10 +102,12 @@ class PopulationRunner:
         ios = []
         for t in range(T + 1):
             io = AgxRolloutIO()
-            io.stage_obs = self.obs_d.data_ptr()
+            src_obs, src_rew, src_done = ((self.obs_h, self.rew_h, self.done_h) if self.zero_copy
+                                          else (self.obs_d, self.rew_d, self.done_d))
+            io.stage_obs = src_obs.data_ptr()
             if t > 0:
-                io.stage_rew = self.rew_d.data_ptr()
-                io.stage_done = self.done_d.data_ptr()
+                io.stage_rew = src_rew.data_ptr()
+                io.stage_done = src_done.data_ptr()
                 io.rewards_prev = pop.rewards[:, t - 1].data_ptr()
                 io.dones_prev = pop.dones[:, t - 1].data_ptr()
                 io.scores = self.scores.data_ptr()
@@ -113,7 +119,7 @@ class PopulationRunner:
                 io.actions = pop.actions[:, t].data_ptr()
                 io.log_probs = pop.log_probs[:, t].data_ptr()
                 io.values = pop.values[:, t].data_ptr()
-                io.actions_flat = self.act_d.data_ptr()
+                io.actions_flat = (self.act_h if self.zero_copy else self.act_d).data_ptr()
                 io.slot_agent_stride = T * N
             else:  # final obs -> last_obs + bootstrap value
                 io.obs_slot = self.last_obs.data_ptr()
@@ -142,7 +148,8 @@ class PopulationRunner:
             self._build_ios()
         if not self.started:
             env.reset(out_obs=self.obs_h.numpy())
-            self.stage_d.copy_(self.stage_h, non_blocking=True)
+            if not self.zero_copy:
+                self.stage_d.copy_(self.stage_h, non_blocking=True)
             self.started = True
         lib = _lib.load()
         fn = lib.agx_ppo_rollout_step
@@ -153,11 +160,13 @@ class PopulationRunner:
             pop.act_counter += 1
             _lib.check(fn(dref, P, N, params, ctypes.byref(self._ios[t]), 1, 1, pop.act_seed, pop.act_counter, s),
                        "agx_ppo_rollout_step")
-            self.act_h.copy_(self.act_d, non_blocking=True)
+            if not self.zero_copy:
+                self.act_h.copy_(self.act_d, non_blocking=True)
             self.ev.record()
             self.ev.synchronize()
             self._env_step()
-            self.stage_d.copy_(self.stage_h, non_blocking=True)
+            if not self.zero_copy:
+                self.stage_d.copy_(self.stage_h, non_blocking=True)
         # reward/done of the last step -> slot T-1; final obs -> last_obs + bootstrap value
         _lib.check(fn(dref, P, N, params, ctypes.byref(self._ios[T]), 1, 0, pop.act_seed, 0, s),
                    "agx_ppo_rollout_step")

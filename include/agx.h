@@ -148,7 +148,10 @@ int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const float *param
  *    on_policy.py:147-172) is updated;
  *  - if act: the policy step of agx_ppo_act on stage_obs writes actions /
  *    log_probs / values (slot t, agent stride slot_agent_stride) and the
- *    contiguous actions_flat [P*N] (may be NULL) for the D2H.  The call after
+ *    contiguous actions_flat [P*N] (may be NULL) for the D2H.  stage_* and
+ *    actions_flat may be pinned host memory (device-accessible, zero-copy:
+ *    the kernel reads the env's staging and writes the actions over the host
+ *    link, so a vector step is one launch and one wait).  The call after
  *    the last step uses act=1 with only `values` set for the bootstrap value
  *    (on_policy.py:184-196). */
 typedef struct agx_rollout_io {
