@@ -183,12 +183,231 @@ class DQN:
         return f
 
 
+class NoisyLinear(nn.Module):
+    """Factorised-Gaussian noisy linear layer (modules/custom_components.py:38-131)."""
+
+    def __init__(self, in_features: int, out_features: int, std_init: float = 0.5, device="cuda"):
+        super().__init__()
+        self.in_features, self.out_features, self.std_init = in_features, out_features, std_init
+        self.weight_mu = nn.Parameter(torch.empty(out_features, in_features, device=device))
+        self.weight_sigma = nn.Parameter(torch.empty(out_features, in_features, device=device))
+        self.register_buffer("weight_epsilon", torch.empty(out_features, in_features, device=device))
+        self.bias_mu = nn.Parameter(torch.empty(out_features, device=device))
+        self.bias_sigma = nn.Parameter(torch.empty(out_features, device=device))
+        self.register_buffer("bias_epsilon", torch.empty(out_features, device=device))
+        mu_range = 1 / math.sqrt(in_features)
+        with torch.no_grad():
+            self.weight_mu.uniform_(-mu_range, mu_range)
+            self.weight_sigma.fill_(std_init / math.sqrt(in_features))
+            self.bias_mu.uniform_(-mu_range, mu_range)
+            self.bias_sigma.fill_(std_init / math.sqrt(out_features))
+        self.reset_noise()
+
+    def _scale_noise(self, size: int) -> torch.Tensor:
+        x = torch.randn(size, device=self.weight_mu.device)
+        return x.sign().mul_(x.abs().sqrt_())
+
+    @torch.no_grad()
+    def reset_noise(self) -> None:
+        eps_in, eps_out = self._scale_noise(self.in_features), self._scale_noise(self.out_features)
+        self.weight_epsilon.copy_(eps_out.ger(eps_in))
+        self.bias_epsilon.copy_(eps_out)
+
+    def forward(self, x):
+        if self.training:
+            return nn.functional.linear(x, self.weight_mu + self.weight_sigma * self.weight_epsilon,
+                                        self.bias_mu + self.bias_sigma * self.bias_epsilon)
+        return nn.functional.linear(x, self.weight_mu, self.bias_mu)
+
+
+def _noisy_mlp(n_in, n_out, hidden, noise_std, device, vanish=True):
+    """create_mlp(noisy=True, layer_norm=True, init_layers=False, output
+    activation None) (utils/evolvable_networks.py:527-644)."""
+    layers: list[nn.Module] = []
+    dims = [n_in, *hidden]
+    for i in range(1, len(dims)):
+        layers += [NoisyLinear(dims[i - 1], dims[i], noise_std, device), nn.LayerNorm(dims[i], device=device),
+                   nn.ReLU()]
+    out = NoisyLinear(dims[-1], n_out, noise_std, device)
+    if vanish:
+        with torch.no_grad():
+            for t in (out.weight_mu, out.bias_mu, out.weight_sigma, out.bias_sigma):
+                t.mul_(0.1)
+    layers.append(out)
+    return nn.Sequential(*layers)
+
+
+class RainbowQNetwork(nn.Module):
+    """Encoder MLP (LayerNorm, plain output LayerNorm + ReLU, default init) ->
+    DuelingDistributionalMLP (noisy value / advantage streams,
+    networks/custom_modules.py:127-162; networks/q_networks.py:170-290)."""
+
+    def __init__(self, obs_dim, n_actions, num_atoms, support, net_config=None, noise_std=0.5, device="cuda"):
+        super().__init__()
+        net_config = dict(net_config or {})
+        hidden = _hidden(net_config.get("encoder_config"), [64])
+        latent = int(net_config.get("latent_dim", 32))
+        head = _hidden(net_config.get("head_config"), [16])
+        dims = [obs_dim, *hidden]
+        enc: list[nn.Module] = []
+        for i in range(1, len(dims)):
+            enc += [nn.Linear(dims[i - 1], dims[i], device=device), nn.LayerNorm(dims[i], device=device), nn.ReLU()]
+        enc += [nn.Linear(dims[-1], latent, device=device), nn.LayerNorm(latent, elementwise_affine=False,
+                                                                          device=device), nn.ReLU()]
+        self.encoder = nn.Sequential(*enc)
+        self.value_net = _noisy_mlp(latent, num_atoms, head, noise_std, device)
+        self.advantage_net = _noisy_mlp(latent, n_actions * num_atoms, head, noise_std, device)
+        self.num_actions, self.num_atoms = n_actions, num_atoms
+        self.register_buffer("support", support)
+
+    def reset_noise(self):
+        for m in self.modules():
+            if isinstance(m, NoisyLinear):
+                m.reset_noise()
+
+    def forward(self, x, q: bool = True, log: bool = False):
+        z = self.encoder(x)
+        value = self.value_net(z).view(-1, 1, self.num_atoms)
+        adv = self.advantage_net(z).view(-1, self.num_actions, self.num_atoms)
+        x = value + adv - adv.mean(1, keepdim=True)
+        if log:
+            return nn.functional.log_softmax(x.view(-1, self.num_atoms), dim=-1).view(-1, self.num_actions,
+                                                                                     self.num_atoms)
+        x = nn.functional.softmax(x.view(-1, self.num_atoms), dim=-1)
+        x = x.view(-1, self.num_actions, self.num_atoms).clamp(min=1e-3)
+        return torch.sum(x * self.support, dim=2) if q else x
+
+
+class _C51Loss(torch.autograd.Function):
+    """Elementwise C51 cross entropy with the projection in agx_c51_project_loss
+    (bit-exact to the serial index_add_, dqn_rainbow.py:313-367); the gradient
+    w.r.t. log_p[i, a_i, :] is -proj[i, :]."""
+
+    @staticmethod
+    def forward(ctx, logp_cur, q_next_online, target_dist, actions, rewards, dones, support, v_min, v_max, gamma):
+        loss, proj = K.c51_project_loss(q_next_online.contiguous(), target_dist.contiguous(), logp_cur.contiguous(),
+                                        actions, rewards, dones, support, v_min, v_max, gamma, with_proj=True)
+        ctx.save_for_backward(proj, actions)
+        ctx.shape = logp_cur.shape
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        proj, actions = ctx.saved_tensors
+        grad = torch.zeros(ctx.shape, dtype=proj.dtype, device=proj.device)
+        grad[torch.arange(proj.shape[0], device=proj.device), actions] = -proj * g.unsqueeze(1)
+        return (grad,) + (None,) * 9
+
+
 class RainbowDQN:
-    """Placeholder kept for create_population's dispatch: the Rainbow
-    projection + loss is available as ``agilerl_amd.kernels.c51_project_loss``
-    (agx_c51_project_loss, bit-exact to dqn_rainbow.py:284-367); the noisy
-    dueling distributional network around it is outside this round's scope."""
+    """Drop-in RainbowDQN (agilerl/algorithms/dqn_rainbow.py:77-501) with the
+    C51 projection + loss in agx_c51_project_loss and Polyak in agx_polyak."""
+
+    algo = "Rainbow DQN"
+
+    def __init__(self, observation_space, action_space, index: int = 0, hp_config=None, net_config=None,
+                 batch_size: int = 64, lr: float = 1e-4, learn_step: int = 5, gamma: float = 0.99, tau: float = 1e-3,
+                 beta: float = 0.4, prior_eps: float = 1e-6, num_atoms: int = 51, v_min: float = 0,
+                 v_max: float = 200, noise_std: float = 0.5, n_step: int = 3, mut=None,
+                 normalize_images: bool = True, combined_reward: bool = False, actor_network=None, device="cuda",
+                 accelerator=None, wrap: bool = True):
+        if not hasattr(action_space, "n"):
+            raise NotImplementedError("agx RainbowDQN supports Discrete action spaces")
+        if actor_network is not None:
+            raise NotImplementedError("custom actor modules: use net_config (MLP) networks")
+        assert isinstance(batch_size, int) and batch_size >= 1, "Batch size must be an integer greater than or equal to one."
+        assert lr > 0, "Learning rate must be greater than zero."
+        self.observation_space, self.action_space = observation_space, action_space
+        self.index, self.net_config, self.mut = index, net_config, mut
+        self.batch_size, self.lr, self.learn_step = batch_size, lr, learn_step
+        self.gamma, self.tau, self.beta, self.prior_eps = gamma, tau, beta, prior_eps
+        self.num_atoms, self.v_min, self.v_max, self.noise_std = num_atoms, v_min, v_max, noise_std
+        self.n_step, self.combined_reward = n_step, combined_reward
+        self.device = torch.device(device)
+        self.action_dim = int(action_space.n)
+        self.obs_dim = int(np.prod(observation_space.shape))
+        self.support = torch.linspace(v_min, v_max, num_atoms, device=self.device)
+        self.delta_z = (v_max - v_min) / (num_atoms - 1)
+        self.actor = RainbowQNetwork(self.obs_dim, self.action_dim, num_atoms, self.support, net_config, noise_std,
+                                     self.device)
+        self.actor_target = RainbowQNetwork(self.obs_dim, self.action_dim, num_atoms, self.support, net_config,
+                                            noise_std, self.device)
+        self.actor_target.load_state_dict(self.actor.state_dict())
+        self.optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr)
+        self.scores: list[float] = []
+        self.fitness: list[float] = []
+        self.steps: list[int] = [0]
 
     @classmethod
-    def from_init_hp(cls, *a, **k):
-        raise NotImplementedError("RainbowDQN agent: use agilerl_amd.kernels.c51_project_loss for the loss")
+    def from_init_hp(cls, observation_space, action_space, net_config, INIT_HP, index=0, device="cuda", **kw):
+        return cls(observation_space, action_space, index=index, net_config=net_config,
+                   batch_size=INIT_HP.get("BATCH_SIZE", 64), lr=INIT_HP.get("LR", 1e-4),
+                   learn_step=INIT_HP.get("LEARN_STEP", 5), gamma=INIT_HP.get("GAMMA", 0.99),
+                   tau=INIT_HP.get("TAU", 1e-3), beta=INIT_HP.get("BETA", 0.4),
+                   prior_eps=INIT_HP.get("PRIOR_EPS", 1e-5), num_atoms=INIT_HP.get("NUM_ATOMS", 51),
+                   v_min=INIT_HP.get("V_MIN", -100), v_max=INIT_HP.get("V_MAX", 100),  # utils.py:454-457
+                   n_step=INIT_HP.get("N_STEP", 3), device=device, **kw)
+
+    def _obs(self, obs) -> torch.Tensor:
+        return torch.as_tensor(np.asarray(obs) if not isinstance(obs, torch.Tensor) else obs,
+                               dtype=torch.float32).to(self.device).reshape(-1, self.obs_dim)
+
+    @torch.no_grad()
+    def get_action(self, obs, action_mask=None, training: bool = True, *args, **kwargs) -> np.ndarray:
+        self.actor.train(mode=training)
+        q = self.actor(self._obs(obs)).cpu().numpy()
+        self.actor.train()
+        if action_mask is None:
+            return np.argmax(q, axis=-1)
+        return np.argmax(np.ma.array(q, mask=1 - np.asarray(action_mask)), axis=-1)
+
+    def _dqn_loss(self, obs, actions, rewards, next_obs, dones, gamma) -> torch.Tensor:
+        with torch.no_grad():
+            q_next = self.actor(next_obs)                   # a* = argmax online Q(s')
+            target_dist = self.actor_target(next_obs, q=False)
+        logp = self.actor(obs, q=False, log=True)
+        return _C51Loss.apply(logp, q_next, target_dist, actions.reshape(-1).long().contiguous(),
+                              rewards.reshape(-1).float().contiguous(), dones.reshape(-1).float().contiguous(),
+                              self.support, float(self.v_min), float(self.v_max), float(gamma))
+
+    def learn(self, experiences, n_experiences=None, per: bool = False):
+        """-> (loss, idxs, new_priorities) (dqn_rainbow.py:369-490)."""
+        to = lambda x: torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x).to(self.device)
+        get = lambda e, k: e[k]
+        n_step = n_experiences is not None
+        ex = [self._obs(get(experiences, "obs")), to(get(experiences, "action")), to(get(experiences, "reward")),
+              self._obs(get(experiences, "next_obs")), to(get(experiences, "done"))]
+        el = None
+        if self.combined_reward or not n_step:
+            el = self._dqn_loss(*ex, self.gamma)
+        if n_step:
+            nx = [self._obs(get(n_experiences, "obs")), to(get(n_experiences, "action")),
+                  to(get(n_experiences, "reward")), self._obs(get(n_experiences, "next_obs")),
+                  to(get(n_experiences, "done"))]
+            nl = self._dqn_loss(*nx, self.gamma ** self.n_step)
+            el = el + nl if self.combined_reward else nl
+        idxs = new_priorities = None
+        if per:
+            weights = to(get(experiences, "weights"))
+            idxs = get(experiences, "idxs")
+            # (B,) * (B,1) broadcasts to (B,B) in the reference: mean = mean(loss) * mean(w)
+            loss = torch.mean(el * weights)
+        else:
+            if n_step:
+                idxs = get(experiences, "idxs")
+            loss = torch.mean(el)
+        self.optimizer.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.actor.parameters(), 10.0)
+        self.optimizer.step()
+        self.soft_update()
+        self.actor.reset_noise()
+        self.actor_target.reset_noise()
+        if per:
+            new_priorities = el.detach().cpu().numpy() + self.prior_eps
+        return loss.item(), idxs, new_priorities
+
+    @torch.no_grad()
+    def soft_update(self) -> None:
+        for t, o in zip(self.actor_target.parameters(), self.actor.parameters()):
+            K.polyak_(t.data.view(-1), o.data.reshape(-1), float(self.tau))

@@ -1,9 +1,9 @@
 """Drop-in replacements for agilerl.components (segment trees, replay and
 rollout buffers) with their storage in HBM and their hot loops in libagx."""
 
-from .replay_buffer import PrioritizedReplayBuffer, ReplayBuffer
+from .replay_buffer import MultiStepReplayBuffer, PrioritizedReplayBuffer, ReplayBuffer
 from .rollout_buffer import RolloutBuffer
 from .segment_tree import MinSegmentTree, SegmentTree, SumSegmentTree
 
-__all__ = ["ReplayBuffer", "PrioritizedReplayBuffer", "RolloutBuffer", "SegmentTree", "SumSegmentTree",
+__all__ = ["ReplayBuffer", "MultiStepReplayBuffer", "PrioritizedReplayBuffer", "RolloutBuffer", "SegmentTree", "SumSegmentTree",
            "MinSegmentTree"]

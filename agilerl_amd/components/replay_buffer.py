@@ -20,6 +20,8 @@ same stream as the reference's B calls of ``torch.rand(1)``
 
 from __future__ import annotations
 
+from collections import deque
+
 import numpy as np
 import torch
 
@@ -114,6 +116,57 @@ class ReplayBuffer:
         self._cursor = 0
         self._storage = None
         self.initialized = False
+
+
+class MultiStepReplayBuffer(ReplayBuffer):
+    """n-step returns (replay_buffer.py:141-258): transitions pass through a
+    deque of n batched steps held in HBM; once full, the folded transition
+    r0 + sum_i r_{i+1} gamma**(i+1) (f32, the reference's weak-scalar
+    multiply), with next_obs / done of the last folded step, is stored.  The
+    fold stops after the first later step in which ANY env is done — the
+    reference's ``done.bool().any()`` — and does not look at the first
+    step's own done; both quirks are kept."""
+
+    def __init__(self, max_size: int, n_step: int = 3, gamma: float = 0.99, device="cuda",
+                 dtype: torch.dtype = torch.float32) -> None:
+        super().__init__(max_size, device, dtype)
+        self.n_step = int(n_step)
+        self.gamma = float(gamma)
+        self.n_step_buffer: deque = deque(maxlen=self.n_step)
+        self.reward_key = "reward"
+        self.done_key = None
+        self.ns_key = "next_obs"
+
+    def add(self, data: DataType):
+        items = {k: _to_tensor(v, self.device) for k, v in data.items()}
+        self.n_step_buffer.append(items)
+        if len(self.n_step_buffer) < self.n_step:
+            return None
+        super().add(self._get_n_step_info())
+        return self.n_step_buffer[0]
+
+    def _get_n_step_info(self) -> dict[str, torch.Tensor]:
+        first = {k: v.clone() for k, v in self.n_step_buffer[0].items()}
+        if self.done_key is None:
+            assert self.reward_key in first, f"Reward key not found in transition. Expected key: {self.reward_key}"
+            assert self.ns_key in first, f"Next observation key not found in transition. Expected key: {self.ns_key}"
+            for key in ("done", "termination", "terminated"):
+                if key in first:
+                    self.done_key = key
+                    break
+            assert self.done_key is not None, "No done/termination key found in transition."
+        reward = first[self.reward_key].clone()
+        for i, tr in enumerate(list(self.n_step_buffer)[1:]):
+            reward += tr[self.reward_key] * (self.gamma ** (i + 1))
+            first[self.ns_key] = tr[self.ns_key].clone()
+            first[self.done_key] = tr[self.done_key].clone()
+            if tr[self.done_key].bool().any():
+                break
+        first[self.reward_key] = reward
+        return first
+
+    def sample_from_indices(self, idxs) -> dict[str, torch.Tensor]:
+        return self._gather(torch.as_tensor(idxs).reshape(-1).to(torch.int64))
 
 
 class PrioritizedReplayBuffer(ReplayBuffer):

@@ -84,3 +84,23 @@ def c51_loss(q_next, target_dist, logp_cur, actions, r, d, support, vmin, vmax, 
     a = np.asarray(actions).reshape(-1)
     log_p = lp[np.arange(B), a].astype(np.float64)
     return -(proj.astype(np.float64) * log_p).sum(1), proj
+
+
+def nstep_fold(transitions, gamma: float):
+    """MultiStepReplayBuffer._get_n_step_info (replay_buffer.py:196-258) on a
+    list of n batched transitions (dicts of numpy arrays): reward folded as
+    r0 + sum_i r_{i+1} * gamma**(i+1) in f32, next_obs / done taken from each
+    later transition in turn, stopping after the first transition in which
+    ANY env is done (the reference's ``done.bool().any()``)."""
+    import numpy as _np
+
+    first = {k: _np.array(v, copy=True) for k, v in transitions[0].items()}
+    r = first["reward"].astype(_np.float32).copy()
+    for i, tr in enumerate(transitions[1:]):
+        r = (r + tr["reward"].astype(_np.float32) * _np.float32(gamma ** (i + 1))).astype(_np.float32)
+        first["next_obs"] = _np.array(tr["next_obs"], copy=True)
+        first["done"] = _np.array(tr["done"], copy=True)
+        if _np.asarray(tr["done"]).astype(bool).any():
+            break
+    first["reward"] = r
+    return first

@@ -190,3 +190,28 @@ def test_rollout_buffer_gae_bit_exact(use_gae):
         buf.add(np.zeros((N, 5)), np.zeros(N), r[0], d[0], v[0], r[0])
     with pytest.raises(ValueError):
         buf.add(np.zeros((N, 5)), np.zeros(N), r[0], d[0], v[0], r[0])
+
+
+def test_multistep_replay_buffer_matches_oracle():
+    from agilerl_amd.components.replay_buffer import MultiStepReplayBuffer
+    from oracle import dqn as odqn
+
+    rng = np.random.default_rng(4)
+    n, N = 3, 5
+    buf = MultiStepReplayBuffer(50, n_step=n, gamma=0.9)
+    hist = []
+    for t in range(12):
+        tr = {"obs": rng.standard_normal((N, 2)).astype(np.float32),
+              "action": rng.integers(0, 3, (N, 1)),
+              "reward": rng.standard_normal((N, 1)).astype(np.float32),
+              "next_obs": rng.standard_normal((N, 2)).astype(np.float32),
+              "done": (rng.random((N, 1)) < 0.15).astype(np.float32)}
+        hist.append(tr)
+        out = buf.add(tr)
+        assert (out is None) == (t < n - 1)
+    assert len(buf) == (12 - n + 1) * N
+    for k in range(12 - n + 1):
+        want = odqn.nstep_fold(hist[k:k + n], 0.9)
+        for key in ("obs", "reward", "next_obs", "done"):
+            got = buf.storage[key][k * N:(k + 1) * N].cpu().numpy()
+            np.testing.assert_array_equal(got, want[key].reshape(got.shape))
