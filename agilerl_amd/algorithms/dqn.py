@@ -149,6 +149,15 @@ class DQN:
         self.soft_update()
         return float(loss.item())
 
+    def clone(self, index: int | None = None, wrap: bool = True):
+        """Deep copy with a new index (EvolvableAlgorithm.clone, core/base.py)."""
+        import copy
+
+        c = copy.deepcopy(self)
+        if index is not None:
+            c.index = index
+        return c
+
     @torch.no_grad()
     def soft_update(self) -> None:
         """target <- tau * online + (1 - tau) * target (dqn.py:349-358), one
@@ -158,29 +167,35 @@ class DQN:
 
     @torch.no_grad()
     def test(self, env, swap_channels: bool = False, max_steps: int | None = None, loop: int = 3) -> float:
-        rewards = []
-        num_envs = env.num_envs if hasattr(env, "num_envs") else 1
-        for _ in range(loop):
-            obs, _ = env.reset()
-            scores = np.zeros(num_envs)
-            completed = np.zeros(num_envs)
-            finished = np.zeros(num_envs, dtype=bool)
-            step = 0
-            while not np.all(finished):
-                obs, r, term, trunc, _ = env.step(self.get_action(obs, epsilon=0.0))
-                step += 1
-                scores += np.asarray(r).reshape(num_envs)
-                done = np.logical_or(term, trunc).reshape(num_envs)
-                if max_steps is not None and step == max_steps:
-                    done[:] = True
-                for i in range(num_envs):
-                    if done[i] and not finished[i]:
-                        completed[i] = scores[i]
-                        finished[i] = True
-            rewards.append(float(np.mean(completed)))
-        f = float(np.mean(rewards))
-        self.fitness.append(f)
-        return f
+        return _evaluate(self, env, lambda o: self.get_action(o, epsilon=0.0), max_steps, loop)
+
+
+def _evaluate(agent, env, act, max_steps, loop) -> float:
+    """Mean over ``loop`` passes of the score of every env's first finished
+    episode (the reference algorithms' ``test``); appended to agent.fitness."""
+    rewards = []
+    num_envs = env.num_envs if hasattr(env, "num_envs") else 1
+    for _ in range(loop):
+        obs, _ = env.reset()
+        scores = np.zeros(num_envs)
+        completed = np.zeros(num_envs)
+        finished = np.zeros(num_envs, dtype=bool)
+        step = 0
+        while not np.all(finished):
+            obs, r, term, trunc, _ = env.step(act(obs))
+            step += 1
+            scores += np.asarray(r).reshape(num_envs)
+            done = np.logical_or(term, trunc).reshape(num_envs)
+            if max_steps is not None and step == max_steps:
+                done[:] = True
+            for i in range(num_envs):
+                if done[i] and not finished[i]:
+                    completed[i] = scores[i]
+                    finished[i] = True
+        rewards.append(float(np.mean(completed)))
+    f = float(np.mean(rewards))
+    agent.fitness.append(f)
+    return f
 
 
 class NoisyLinear(nn.Module):
@@ -370,6 +385,10 @@ class RainbowDQN:
                               rewards.reshape(-1).float().contiguous(), dones.reshape(-1).float().contiguous(),
                               self.support, float(self.v_min), float(self.v_max), float(gamma))
 
+    @torch.no_grad()
+    def test(self, env, swap_channels: bool = False, max_steps: int | None = None, loop: int = 3) -> float:
+        return _evaluate(self, env, lambda o: self.get_action(o, training=False), max_steps, loop)
+
     def learn(self, experiences, n_experiences=None, per: bool = False):
         """-> (loss, idxs, new_priorities) (dqn_rainbow.py:369-490)."""
         to = lambda x: torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x).to(self.device)
@@ -406,6 +425,15 @@ class RainbowDQN:
         if per:
             new_priorities = el.detach().cpu().numpy() + self.prior_eps
         return loss.item(), idxs, new_priorities
+
+    def clone(self, index: int | None = None, wrap: bool = True):
+        """Deep copy with a new index (EvolvableAlgorithm.clone, core/base.py)."""
+        import copy
+
+        c = copy.deepcopy(self)
+        if index is not None:
+            c.index = index
+        return c
 
     @torch.no_grad()
     def soft_update(self) -> None:

@@ -3,7 +3,8 @@ rollout buffers) with their storage in HBM and their hot loops in libagx."""
 
 from .replay_buffer import MultiStepReplayBuffer, PrioritizedReplayBuffer, ReplayBuffer
 from .rollout_buffer import RolloutBuffer
+from .sampler import Sampler
 from .segment_tree import MinSegmentTree, SegmentTree, SumSegmentTree
 
 __all__ = ["ReplayBuffer", "MultiStepReplayBuffer", "PrioritizedReplayBuffer", "RolloutBuffer", "SegmentTree", "SumSegmentTree",
-           "MinSegmentTree"]
+           "MinSegmentTree", "Sampler"]

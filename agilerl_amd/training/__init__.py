@@ -1,3 +1,4 @@
+from .train_off_policy import train_off_policy
 from .train_on_policy import train_on_policy
 
-__all__ = ["train_on_policy"]
+__all__ = ["train_on_policy", "train_off_policy"]

@@ -1,0 +1,114 @@
+"""Drop-in ``train_off_policy`` (agilerl/training/train_off_policy.py:41-616)
+for DQN / RainbowDQN populations on the agx HBM replay buffers.
+
+The loop mirrors the reference: agents in turn collect ``evo_steps`` from the
+shared env with epsilon-greedy (DQN, epsilon decayed per step) or noisy-net
+(Rainbow) actions into the SHARED memory (one replay for the population,
+train_off_policy.py:249, 340-345), learn every ``learn_step`` env steps once
+``len(memory) >= batch_size`` and ``memory.size > learning_delay`` (PER:
+sample with the agent's annealed beta, update priorities; n-step: the
+n-step memory sampled at the same indices), then every agent is evaluated
+with ``agent.test`` and a tournament (``TournamentSelection.select``, global
+numpy RNG) replaces the population.  The replay trees, TD / C51 losses and
+Polyak updates run in libagx.  Mutations are outside the hot path (ignored
+with a warning).  Returns (pop, pop_fitnesses)."""
+
+from __future__ import annotations
+
+import warnings
+
+import numpy as np
+
+from ..algorithms.dqn import DQN, RainbowDQN
+from ..components.sampler import Sampler
+
+
+def train_off_policy(env, env_name: str, algo: str, pop, memory, INIT_HP=None, MUT_P=None,
+                     swap_channels: bool = False, max_steps: int = 1_000_000, evo_steps: int = 10_000,
+                     eval_steps=None, eval_loop: int = 1, learning_delay: int = 0, eps_start: float = 1.0,
+                     eps_end: float = 0.1, eps_decay: float = 0.995, target: float | None = None, n_step: bool = False,
+                     per: bool = False, n_step_memory=None, tournament=None, mutation=None, checkpoint=None,
+                     checkpoint_path=None, overwrite_checkpoints: bool = False, save_elite: bool = False,
+                     elite_path=None, wb: bool = False, verbose: bool = True, accelerator=None, wandb_api_key=None,
+                     wandb_kwargs=None):
+    if mutation is not None:
+        warnings.warn("agx train_off_policy: mutations are outside the hot path and are not applied", stacklevel=2)
+    num_envs = env.num_envs if hasattr(env, "num_envs") else 1
+    sampler = Sampler(memory=memory)
+    n_step_sampler = Sampler(memory=n_step_memory) if n_step_memory is not None else None
+    pop_fitnesses: list[list[float]] = []
+
+    def learn_once(agent):
+        if per:
+            experiences = sampler.sample(agent.batch_size, agent.beta)
+            n_exp = n_step_sampler.sample(experiences["idxs"]) if n_step_sampler is not None else None
+            loss, idxs, priorities = agent.learn(experiences, n_experiences=n_exp, per=per)
+            memory.update_priorities(idxs, priorities)
+            return loss
+        experiences = sampler.sample(agent.batch_size, return_idx=n_step_memory is not None)
+        if n_step_memory is not None:
+            loss, *_ = agent.learn(experiences, n_experiences=n_step_sampler.sample(experiences["idxs"]))
+            return loss
+        out = agent.learn(experiences)
+        return out[0] if isinstance(out, tuple) else out
+
+    while np.less([agent.steps[-1] for agent in pop], max_steps).all():
+        for agent in pop:
+            obs, info = env.reset()
+            scores = np.zeros(num_envs)
+            if isinstance(agent, DQN):
+                epsilon = eps_start
+            for idx_step in range(evo_steps // num_envs):
+                if isinstance(agent, DQN):
+                    action = agent.get_action(obs, epsilon)
+                    epsilon = max(eps_end, epsilon * eps_decay)
+                elif isinstance(agent, RainbowDQN):
+                    action = agent.get_action(obs)
+                else:
+                    raise NotImplementedError(f"{type(agent).__name__} is outside the agx off-policy path")
+                next_obs, reward, done, trunc, info = env.step(action)
+                scores += np.asarray(reward)
+                for i, (d, t) in enumerate(zip(np.atleast_1d(done), np.atleast_1d(trunc))):
+                    if d or t:
+                        agent.scores.append(scores[i])
+                        scores[i] = 0
+                transition = {"obs": obs, "action": np.asarray(action).reshape(num_envs, 1),
+                              "reward": np.asarray(reward, dtype=np.float32).reshape(num_envs, 1),
+                              "next_obs": next_obs,
+                              "done": np.asarray(done, dtype=np.float32).reshape(num_envs, 1)}
+                if n_step_memory is not None:
+                    one_step = n_step_memory.add(transition)
+                    if one_step is not None:
+                        memory.add(one_step)
+                else:
+                    memory.add(transition)
+                if per:
+                    fraction = min((agent.steps[-1] + idx_step + 1) * num_envs / max_steps, 1.0)
+                    agent.beta += fraction * (1.0 - agent.beta)
+                ready = len(memory) >= agent.batch_size and memory.size > learning_delay
+                if agent.learn_step > num_envs:
+                    if idx_step % (agent.learn_step // num_envs) == 0 and ready:
+                        learn_once(agent)
+                elif ready:
+                    for _ in range(num_envs // agent.learn_step):
+                        learn_once(agent)
+                obs = next_obs
+            agent.steps[-1] += (evo_steps // num_envs) * num_envs
+        if isinstance(pop[-1], DQN):
+            eps_start = epsilon  # train_off_policy.py:456-458: the next generation starts where this one ended
+        fitnesses = [agent.test(env, swap_channels=swap_channels, max_steps=eval_steps, loop=eval_loop)
+                     for agent in pop]
+        pop_fitnesses.append(fitnesses)
+        if verbose:
+            print(f"--- {env_name} {algo}: steps {[a.steps[-1] for a in pop]}, fitness "
+                  f"{[round(f, 2) for f in fitnesses]}")
+        for agent in pop:
+            agent.steps.append(agent.steps[-1])
+        if target is not None and np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target)) \
+                and len(pop[0].steps) >= 100:
+            return pop, pop_fitnesses
+        if tournament is not None:
+            # the reference selects inside tournament_selection_and_mutation; selection runs here
+            # even without a mutation object (mutations are not applied)
+            _, pop = tournament.select(pop)
+    return pop, pop_fitnesses

@@ -182,3 +182,41 @@ def test_rainbow_learn_matches_torch_reference(per):
         assert new_pri is None
     acts = agent.get_action(exp["obs"], training=False)
     assert acts.shape == (B,) and ((acts >= 0) & (acts < 4)).all()
+
+
+@pytest.mark.parametrize("algo,per,n_step", [("DQN", False, False), ("Rainbow DQN", True, True),
+                                             ("Rainbow DQN", False, True)])
+def test_train_off_policy(algo, per, n_step):
+    """train_off_policy (train_off_policy.py:41-616): shared HBM replay, PER
+    beta annealing + priority updates, n-step memory sampled at the same
+    indices, fitness via agent.test, tournament selection of clones."""
+    from agilerl_amd.components import MultiStepReplayBuffer, PrioritizedReplayBuffer, ReplayBuffer
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.tournament import TournamentSelection
+    from agilerl_amd.training import train_off_policy
+    from agilerl_amd.utils import create_population
+
+    obs_space, act_space = _spaces()
+    INIT_HP = {"BATCH_SIZE": 32, "LR": 1e-3, "LEARN_STEP": 4, "GAMMA": 0.99, "TAU": 1e-2, "N_STEP": 3}
+    net_config = {"encoder_config": {"hidden_size": [32]}, "head_config": {"hidden_size": [32]}}
+    torch.manual_seed(0)
+    np.random.seed(0)
+    pop = create_population(algo, net_config, INIT_HP, obs_space, act_space, population_size=3)
+    memory = PrioritizedReplayBuffer(2000, alpha=0.6) if per else ReplayBuffer(2000)
+    n_mem = MultiStepReplayBuffer(2000, n_step=3, gamma=0.99) if n_step else None
+    env = SyntheticVecEnv(8, seed=4, p_done=0.1)
+    p0 = [p.detach().clone() for p in pop[0].actor.parameters()]
+    beta0 = getattr(pop[0], "beta", None)
+    pop, fits = train_off_policy(env, "Synthetic", algo, pop, memory, INIT_HP=INIT_HP, max_steps=256, evo_steps=128,
+                                 eval_steps=20, eval_loop=1, per=per, n_step=n_step, n_step_memory=n_mem,
+                                 tournament=TournamentSelection(2, True, 3, 1), verbose=False)
+    assert len(fits) == 2 and all(len(f) == 3 and all(np.isfinite(f)) for f in fits)
+    assert all(a.steps[-1] == 256 for a in pop) and len(memory) > 0
+    assert len({id(a) for a in pop}) == 3 and max(a.index for a in pop) > 2  # tournament clones, new ids
+    if per:
+        assert all(a.beta > beta0 for a in pop)
+        leaves = memory.sum_tree.tree[memory.tree_capacity:memory.tree_capacity + len(memory)]
+        assert not torch.all(leaves == leaves[0])  # priorities were updated from the TD errors
+    if n_step:
+        assert len(n_mem) == len(memory)
+    assert any(not torch.equal(a, b) for a, b in zip(p0, pop[0].actor.parameters()))
