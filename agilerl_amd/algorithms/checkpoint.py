@@ -1,0 +1,99 @@
+"""Checkpoints in the layout of ``get_checkpoint_dict`` (agilerl/algorithms/
+core/base.py:168-224, 939-1072): hyper-parameter attributes at the top level
+plus ``network_info = {network_names, modules: {<net>_state_dict},
+optimizer_names, optimizers: {<opt>_state_dict}}``, with the reference's
+state-dict key names.
+
+Differences of form: classes and spaces are not pickled (the file holds only
+tensors, numbers, strings, lists and dicts), so it is written by
+``torch.save`` and read back with ``torch.load(weights_only=True)`` — nothing
+in a checkpoint is executed on load.  Spaces are stored as
+``{"obs_shape", "n_actions"}`` for ``load``.
+"""
+
+from __future__ import annotations
+
+from typing import Any
+
+import torch
+
+HP_NAMES = ("index", "batch_size", "lr", "learn_step", "gamma", "tau", "double", "beta", "prior_eps", "num_atoms",
+            "v_min", "v_max", "noise_std", "n_step", "combined_reward", "gae_lambda", "clip_coef", "ent_coef",
+            "vf_coef", "max_grad_norm", "target_kl", "update_epochs", "num_envs", "net_config", "scores", "fitness",
+            "steps", "mut")
+
+
+def _plain(v: Any) -> Any:
+    if isinstance(v, torch.Tensor):
+        return v.detach().cpu().clone()
+    if isinstance(v, dict):
+        return {k: _plain(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_plain(x) for x in v]
+    if hasattr(v, "item") and callable(v.item) and not isinstance(v, (str, bytes)):
+        return v.item()
+    return v
+
+
+def checkpoint_dict(agent, modules: dict[str, dict[str, torch.Tensor]], optimizers: dict[str, Any]) -> dict:
+    out = {k: _plain(getattr(agent, k)) for k in HP_NAMES if hasattr(agent, k)}
+    out["algo"] = agent.algo
+    out["agilerl_version"] = "agx"
+    out["spaces"] = {"obs_shape": list(agent.observation_space.shape), "n_actions": int(agent.action_space.n)}
+    out["network_info"] = {
+        "network_names": list(modules),
+        "modules": {f"{k}_state_dict": _plain(v) for k, v in modules.items()},
+        "optimizer_names": list(optimizers),
+        "optimizers": {f"{k}_state_dict": _plain(v) for k, v in optimizers.items()},
+    }
+    return out
+
+
+def read(path: str, algo: str) -> dict:
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    if ckpt.get("algo") != algo:
+        raise ValueError("Loaded registry does not match the algorithm's registry. Please make sure you are "
+                         "loading the checkpoint with the correct algorithm.")
+    return ckpt
+
+
+def restore_attributes(agent, ckpt: dict) -> None:
+    for k in HP_NAMES:
+        if k in ckpt:
+            setattr(agent, k, ckpt[k])
+
+
+def spaces(ckpt: dict):
+    from ..envs import Box, Discrete
+
+    s = ckpt["spaces"]
+    return Box(-float("inf"), float("inf"), tuple(s["obs_shape"])), Discrete(s["n_actions"])
+
+
+class TorchCheckpointMixin:
+    """save_checkpoint / load_checkpoint / load for algorithms whose networks
+    are torch modules ``actor`` / ``actor_target`` with one ``optimizer``."""
+
+    def save_checkpoint(self, path: str) -> None:
+        torch.save(checkpoint_dict(self, {"actor": self.actor.state_dict(),
+                                          "actor_target": self.actor_target.state_dict()},
+                                   {"optimizer": self.optimizer.state_dict()}), path)
+
+    @torch.no_grad()
+    def load_checkpoint(self, path: str) -> None:
+        ck = read(path, self.algo)
+        info = ck["network_info"]
+        self.actor.load_state_dict(info["modules"]["actor_state_dict"])
+        self.actor_target.load_state_dict(info["modules"]["actor_target_state_dict"])
+        self.optimizer.load_state_dict(info["optimizers"]["optimizer_state_dict"])
+        restore_attributes(self, ck)
+
+    @classmethod
+    def load(cls, path: str, device="cuda", accelerator=None):
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        obs_space, act_space = spaces(ck)
+        code = cls.__init__.__code__
+        names = set(code.co_varnames[1:code.co_argcount])
+        agent = cls(obs_space, act_space, device=device, **{k: ck[k] for k in names if k in ck})
+        agent.load_checkpoint(path)
+        return agent

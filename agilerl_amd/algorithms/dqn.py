@@ -2,10 +2,9 @@
 MSE loss and its gradient in one HIP kernel (agx_td_target) and the soft
 target update in agx_polyak.
 
-The Q network is the reference's MLP (create_mlp, utils/evolvable_networks.py:
-527-644: [Linear -> LayerNorm -> ReLU] x L -> Linear, orthogonal init gain
-sqrt(2), output layer x0.1), as plain PyTorch modules on the GPU; ``learn``
-takes the reference's experience mapping (obs, action, reward, next_obs,
+The Q networks are the reference's ``QNetwork`` / ``RainbowQNetwork``
+(agilerl_amd.networks: EvolvableMLP encoder + head with the reference's
+defaults, initialisation and state-dict keys) on the GPU; ``learn`` takes the reference's experience mapping (obs, action, reward, next_obs,
 done) and returns the loss as a float.  Supported: Box observations,
 Discrete actions, ``net_config`` ``encoder_config`` / ``head_config``
 ``hidden_size`` lists.
@@ -13,42 +12,19 @@ Discrete actions, ``net_config`` ``encoder_config`` / ``head_config``
 
 from __future__ import annotations
 
-import math
 from typing import Any
 
 import numpy as np
 import torch
-from torch import nn
 
 from .. import kernels as K
+from . import checkpoint as C
+from ..networks import QNetwork, RainbowQNetwork
+from ..networks.base import mlp_net_config
 
 
-def _hidden(cfg, default):
-    if cfg is None:
-        return list(default)
-    return list(getattr(cfg, "hidden_size", None) or cfg.get("hidden_size", default))
-
-
-def build_q_mlp(obs_dim: int, n_actions: int, net_config: dict | None, seed: int | None = None) -> nn.Sequential:
-    net_config = dict(net_config or {})
-    hidden = _hidden(net_config.get("encoder_config"), [64])
-    latent = int(net_config.get("latent_dim", 64))
-    head = _hidden(net_config.get("head_config"), [64])
-    dims = [obs_dim, *hidden, latent, *head]
-    gen = torch.Generator().manual_seed(seed) if seed is not None else None
-    layers: list[nn.Module] = []
-    for i in range(len(dims) - 1):
-        lin = nn.Linear(dims[i], dims[i + 1])
-        nn.init.orthogonal_(lin.weight, math.sqrt(2), generator=gen)
-        nn.init.zeros_(lin.bias)
-        layers += [lin, nn.LayerNorm(dims[i + 1]), nn.ReLU()]
-    out = nn.Linear(dims[-1], n_actions)
-    nn.init.orthogonal_(out.weight, math.sqrt(2), generator=gen)
-    nn.init.zeros_(out.bias)
-    with torch.no_grad():
-        out.weight.mul_(0.1)  # output_vanish (evolvable_networks.py:621-629)
-    layers.append(out)
-    return nn.Sequential(*layers)
+def _net_kwargs(net_config) -> dict:
+    return {k: (dict(v) if isinstance(v, dict) else v) for k, v in dict(net_config or {}).items()}
 
 
 class _TDLoss(torch.autograd.Function):
@@ -69,7 +45,7 @@ class _TDLoss(torch.autograd.Function):
         return (g_q * gl,) + (None,) * 7
 
 
-class DQN:
+class DQN(C.TorchCheckpointMixin):
     algo = "DQN"
 
     def __init__(self, observation_space, action_space, index: int = 0, hp_config=None, net_config=None,
@@ -89,8 +65,9 @@ class DQN:
         self.device = torch.device(device)
         self.action_dim = int(action_space.n)
         self.obs_dim = int(np.prod(observation_space.shape))
-        self.actor = build_q_mlp(self.obs_dim, self.action_dim, net_config, seed=index).to(self.device)
-        self.actor_target = build_q_mlp(self.obs_dim, self.action_dim, net_config).to(self.device)
+        # QNetwork with the reference's defaults and state-dict keys (dqn.py:133-146)
+        self.actor = QNetwork(observation_space, action_space, device=self.device, **_net_kwargs(net_config))
+        self.actor_target = QNetwork(observation_space, action_space, device=self.device, **_net_kwargs(net_config))
         self.actor_target.load_state_dict(self.actor.state_dict())
         self.optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr)
         self.scores: list[float] = []
@@ -198,101 +175,6 @@ def _evaluate(agent, env, act, max_steps, loop) -> float:
     return f
 
 
-class NoisyLinear(nn.Module):
-    """Factorised-Gaussian noisy linear layer (modules/custom_components.py:38-131)."""
-
-    def __init__(self, in_features: int, out_features: int, std_init: float = 0.5, device="cuda"):
-        super().__init__()
-        self.in_features, self.out_features, self.std_init = in_features, out_features, std_init
-        self.weight_mu = nn.Parameter(torch.empty(out_features, in_features, device=device))
-        self.weight_sigma = nn.Parameter(torch.empty(out_features, in_features, device=device))
-        self.register_buffer("weight_epsilon", torch.empty(out_features, in_features, device=device))
-        self.bias_mu = nn.Parameter(torch.empty(out_features, device=device))
-        self.bias_sigma = nn.Parameter(torch.empty(out_features, device=device))
-        self.register_buffer("bias_epsilon", torch.empty(out_features, device=device))
-        mu_range = 1 / math.sqrt(in_features)
-        with torch.no_grad():
-            self.weight_mu.uniform_(-mu_range, mu_range)
-            self.weight_sigma.fill_(std_init / math.sqrt(in_features))
-            self.bias_mu.uniform_(-mu_range, mu_range)
-            self.bias_sigma.fill_(std_init / math.sqrt(out_features))
-        self.reset_noise()
-
-    def _scale_noise(self, size: int) -> torch.Tensor:
-        x = torch.randn(size, device=self.weight_mu.device)
-        return x.sign().mul_(x.abs().sqrt_())
-
-    @torch.no_grad()
-    def reset_noise(self) -> None:
-        eps_in, eps_out = self._scale_noise(self.in_features), self._scale_noise(self.out_features)
-        self.weight_epsilon.copy_(eps_out.ger(eps_in))
-        self.bias_epsilon.copy_(eps_out)
-
-    def forward(self, x):
-        if self.training:
-            return nn.functional.linear(x, self.weight_mu + self.weight_sigma * self.weight_epsilon,
-                                        self.bias_mu + self.bias_sigma * self.bias_epsilon)
-        return nn.functional.linear(x, self.weight_mu, self.bias_mu)
-
-
-def _noisy_mlp(n_in, n_out, hidden, noise_std, device, vanish=True):
-    """create_mlp(noisy=True, layer_norm=True, init_layers=False, output
-    activation None) (utils/evolvable_networks.py:527-644)."""
-    layers: list[nn.Module] = []
-    dims = [n_in, *hidden]
-    for i in range(1, len(dims)):
-        layers += [NoisyLinear(dims[i - 1], dims[i], noise_std, device), nn.LayerNorm(dims[i], device=device),
-                   nn.ReLU()]
-    out = NoisyLinear(dims[-1], n_out, noise_std, device)
-    if vanish:
-        with torch.no_grad():
-            for t in (out.weight_mu, out.bias_mu, out.weight_sigma, out.bias_sigma):
-                t.mul_(0.1)
-    layers.append(out)
-    return nn.Sequential(*layers)
-
-
-class RainbowQNetwork(nn.Module):
-    """Encoder MLP (LayerNorm, plain output LayerNorm + ReLU, default init) ->
-    DuelingDistributionalMLP (noisy value / advantage streams,
-    networks/custom_modules.py:127-162; networks/q_networks.py:170-290)."""
-
-    def __init__(self, obs_dim, n_actions, num_atoms, support, net_config=None, noise_std=0.5, device="cuda"):
-        super().__init__()
-        net_config = dict(net_config or {})
-        hidden = _hidden(net_config.get("encoder_config"), [64])
-        latent = int(net_config.get("latent_dim", 32))
-        head = _hidden(net_config.get("head_config"), [16])
-        dims = [obs_dim, *hidden]
-        enc: list[nn.Module] = []
-        for i in range(1, len(dims)):
-            enc += [nn.Linear(dims[i - 1], dims[i], device=device), nn.LayerNorm(dims[i], device=device), nn.ReLU()]
-        enc += [nn.Linear(dims[-1], latent, device=device), nn.LayerNorm(latent, elementwise_affine=False,
-                                                                          device=device), nn.ReLU()]
-        self.encoder = nn.Sequential(*enc)
-        self.value_net = _noisy_mlp(latent, num_atoms, head, noise_std, device)
-        self.advantage_net = _noisy_mlp(latent, n_actions * num_atoms, head, noise_std, device)
-        self.num_actions, self.num_atoms = n_actions, num_atoms
-        self.register_buffer("support", support)
-
-    def reset_noise(self):
-        for m in self.modules():
-            if isinstance(m, NoisyLinear):
-                m.reset_noise()
-
-    def forward(self, x, q: bool = True, log: bool = False):
-        z = self.encoder(x)
-        value = self.value_net(z).view(-1, 1, self.num_atoms)
-        adv = self.advantage_net(z).view(-1, self.num_actions, self.num_atoms)
-        x = value + adv - adv.mean(1, keepdim=True)
-        if log:
-            return nn.functional.log_softmax(x.view(-1, self.num_atoms), dim=-1).view(-1, self.num_actions,
-                                                                                     self.num_atoms)
-        x = nn.functional.softmax(x.view(-1, self.num_atoms), dim=-1)
-        x = x.view(-1, self.num_actions, self.num_atoms).clamp(min=1e-3)
-        return torch.sum(x * self.support, dim=2) if q else x
-
-
 class _C51Loss(torch.autograd.Function):
     """Elementwise C51 cross entropy with the projection in agx_c51_project_loss
     (bit-exact to the serial index_add_, dqn_rainbow.py:313-367); the gradient
@@ -314,7 +196,7 @@ class _C51Loss(torch.autograd.Function):
         return (grad,) + (None,) * 9
 
 
-class RainbowDQN:
+class RainbowDQN(C.TorchCheckpointMixin):
     """Drop-in RainbowDQN (agilerl/algorithms/dqn_rainbow.py:77-501) with the
     C51 projection + loss in agx_c51_project_loss and Polyak in agx_polyak."""
 
@@ -343,15 +225,25 @@ class RainbowDQN:
         self.obs_dim = int(np.prod(observation_space.shape))
         self.support = torch.linspace(v_min, v_max, num_atoms, device=self.device)
         self.delta_z = (v_max - v_min) / (num_atoms - 1)
-        self.actor = RainbowQNetwork(self.obs_dim, self.action_dim, num_atoms, self.support, net_config, noise_std,
-                                     self.device)
-        self.actor_target = RainbowQNetwork(self.obs_dim, self.action_dim, num_atoms, self.support, net_config,
-                                            noise_std, self.device)
+        # dqn_rainbow.py:190-215: head defaults hidden [64], noisy, output activation ReLU -> None
+        self.actor = RainbowQNetwork(observation_space, action_space, support=self.support, num_atoms=num_atoms,
+                                     noise_std=noise_std, device=self.device, **self._net_kwargs(net_config))
+        self.actor_target = RainbowQNetwork(observation_space, action_space, support=self.support,
+                                            num_atoms=num_atoms, noise_std=noise_std, device=self.device,
+                                            **self._net_kwargs(net_config))
         self.actor_target.load_state_dict(self.actor.state_dict())
         self.optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr)
         self.scores: list[float] = []
         self.fitness: list[float] = []
         self.steps: list[int] = [0]
+
+    def _net_kwargs(self, net_config) -> dict:
+        kw = _net_kwargs(net_config)
+        head = dict(kw.get("head_config") or {})
+        kw["head_config"] = mlp_net_config(head.get("hidden_size", [64]), noise_std=self.noise_std,
+                                           output_activation="ReLU", min_mlp_nodes=head.get("min_mlp_nodes", 16),
+                                           max_mlp_nodes=head.get("max_mlp_nodes", 500))
+        return kw
 
     @classmethod
     def from_init_hp(cls, observation_space, action_space, net_config, INIT_HP, index=0, device="cuda", **kw):

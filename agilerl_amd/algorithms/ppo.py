@@ -110,6 +110,74 @@ class PPO:
                 for k, (off, shape) in self.spec.state_dict_keys().items()}
 
     @torch.no_grad()
+    def load_state_dict(self, state_dict: dict[str, torch.Tensor], strict: bool = True) -> None:
+        """Copy reference-named tensors into this agent's HBM row."""
+        keys = self.spec.state_dict_keys()
+        if strict:
+            missing, unexpected = set(keys) - set(state_dict), set(state_dict) - set(keys)
+            if missing or unexpected:
+                raise KeyError(f"state_dict mismatch: missing {sorted(missing)}, unexpected {sorted(unexpected)}")
+        flat = self.population.params.data[self.row]
+        for k, (off, shape) in keys.items():
+            if k in state_dict and not k.startswith("critic.encoder."):
+                t = torch.as_tensor(state_dict[k])
+                if tuple(t.shape) != tuple(shape):
+                    raise ValueError(f"{k}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+                flat[off:off + t.numel()] = t.reshape(-1).to(flat)
+
+    def _opt_rows(self):
+        opt = self.population.opt
+        return opt.exp_avg[self.row], opt.exp_avg_sq[self.row]
+
+    def save_checkpoint(self, path: str) -> None:
+        """core/base.py:939-949 layout (see algorithms/checkpoint.py)."""
+        from . import checkpoint as C
+
+        sd = self.state_dict()
+        keys = self.spec.state_dict_keys()
+        m, v = self._opt_rows()
+        opt = {"exp_avg": {k: m[o:o + int(np.prod(sh))].view(sh) for k, (o, sh) in keys.items()
+                           if not k.startswith("critic.encoder.")},
+               "exp_avg_sq": {k: v[o:o + int(np.prod(sh))].view(sh) for k, (o, sh) in keys.items()
+                              if not k.startswith("critic.encoder.")},
+               "step": int(self.population.opt.step_count)}
+        mods = {net: {k[len(net) + 1:]: t for k, t in sd.items() if k.startswith(net + ".")}
+                for net in ("actor", "critic")}
+        torch.save(C.checkpoint_dict(self, mods, {"optimizer": opt}), path)
+
+    @torch.no_grad()
+    def load_checkpoint(self, path: str) -> None:
+        """core/base.py:951-1072 for the agx layout; torch.load(weights_only=True)."""
+        from . import checkpoint as C
+
+        ck = C.read(path, self.algo)
+        info = ck["network_info"]
+        sd = {f"{net}.{k}": t for net in info["network_names"] for k, t in info["modules"][f"{net}_state_dict"].items()}
+        self.load_state_dict(sd)
+        opt = info["optimizers"]["optimizer_state_dict"]
+        keys = self.spec.state_dict_keys()
+        m, v = self._opt_rows()
+        for k, t in opt["exp_avg"].items():
+            o, sh = keys[k]
+            m[o:o + t.numel()] = t.reshape(-1).to(m)
+            v[o:o + t.numel()] = opt["exp_avg_sq"][k].reshape(-1).to(v)
+        self.population.opt.step_count = int(opt["step"])
+        C.restore_attributes(self, ck)
+
+    @classmethod
+    def load(cls, path: str, device="cuda", accelerator=None) -> "PPO":
+        from . import checkpoint as C
+
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        obs_space, act_space = C.spaces(ck)
+        kw = {k: ck[k] for k in ("batch_size", "lr", "learn_step", "gamma", "gae_lambda", "clip_coef", "ent_coef",
+                                 "vf_coef", "max_grad_norm", "target_kl", "update_epochs", "num_envs",
+                                 "net_config", "index") if k in ck}
+        agent = cls(obs_space, act_space, device=device, **kw)
+        agent.load_checkpoint(path)
+        return agent
+
+    @torch.no_grad()
     def get_action(self, obs, action_mask=None, hidden_state=None, *args, **kwargs):
         """-> (action, log_prob, entropy, value) numpy arrays (ppo.py:567-633);
         sampling is a Gumbel-max draw from a counter-based Philox stream."""

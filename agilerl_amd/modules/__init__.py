@@ -1,0 +1,5 @@
+from .custom_components import GumbelSoftmax, NoisyLinear
+from .mlp import EvolvableMLP, create_mlp, get_activation, layer_init, preserve_parameters
+
+__all__ = ["EvolvableMLP", "create_mlp", "get_activation", "layer_init", "preserve_parameters", "NoisyLinear",
+           "GumbelSoftmax"]

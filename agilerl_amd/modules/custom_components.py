@@ -1,0 +1,64 @@
+"""NoisyLinear and GumbelSoftmax (agilerl/modules/custom_components.py:10-131)."""
+
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+
+class GumbelSoftmax(nn.Module):
+    """softmax(logits + Gumbel noise) over the last dim (custom_components.py:10-35)."""
+
+    @staticmethod
+    def gumbel_softmax(logits: torch.Tensor, tau: float = 1.0, eps: float = 1e-20) -> torch.Tensor:
+        u = torch.rand_like(logits)
+        return F.softmax((logits - torch.log(-torch.log(u + eps) + eps)) / tau, dim=-1)
+
+    def forward(self, input: torch.Tensor) -> torch.Tensor:
+        return self.gumbel_softmax(input)
+
+
+class NoisyLinear(nn.Module):
+    """Factorised-Gaussian noisy linear layer (custom_components.py:38-131):
+    mu ~ U(+-1/sqrt(in)), sigma = std_init/sqrt(in) (weights) and
+    std_init/sqrt(out) (bias); eps = sign(x) sqrt(|x|), x ~ N(0,1); train mode
+    uses mu + sigma * eps, eval mode mu."""
+
+    def __init__(self, in_features: int, out_features: int, std_init: float = 0.5, device="cpu"):
+        super().__init__()
+        self.in_features, self.out_features, self.std_init = in_features, out_features, std_init
+        self.weight_mu = nn.Parameter(torch.empty(out_features, in_features, device=device))
+        self.weight_sigma = nn.Parameter(torch.empty(out_features, in_features, device=device))
+        self.register_buffer("weight_epsilon", torch.empty(out_features, in_features, device=device))
+        self.bias_mu = nn.Parameter(torch.empty(out_features, device=device))
+        self.bias_sigma = nn.Parameter(torch.empty(out_features, device=device))
+        self.register_buffer("bias_epsilon", torch.empty(out_features, device=device))
+        self.reset_parameters()
+        self.reset_noise()
+
+    @torch.no_grad()
+    def reset_parameters(self) -> None:
+        mu_range = 1 / math.sqrt(self.in_features)
+        self.weight_mu.uniform_(-mu_range, mu_range)
+        self.weight_sigma.fill_(self.std_init / math.sqrt(self.in_features))
+        self.bias_mu.uniform_(-mu_range, mu_range)
+        self.bias_sigma.fill_(self.std_init / math.sqrt(self.out_features))
+
+    def _scale_noise(self, size: int) -> torch.Tensor:
+        x = torch.randn(size, device=self.weight_mu.device)
+        return x.sign().mul_(x.abs().sqrt_())
+
+    @torch.no_grad()
+    def reset_noise(self) -> None:
+        eps_in, eps_out = self._scale_noise(self.in_features), self._scale_noise(self.out_features)
+        self.weight_epsilon.copy_(eps_out.ger(eps_in))
+        self.bias_epsilon.copy_(eps_out)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.training:
+            return F.linear(x, self.weight_mu + self.weight_sigma * self.weight_epsilon,
+                            self.bias_mu + self.bias_sigma * self.bias_epsilon)
+        return F.linear(x, self.weight_mu, self.bias_mu)

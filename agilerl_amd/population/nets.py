@@ -63,7 +63,7 @@ class ActorCriticSpec:
         self.encoder.append(Layer("encoder_linear_layer_output", enc[-1], self.latent_dim,
                                   "plain" if self.layer_norm else None, True))
         self.actor = self._head("actor", self.actor_hidden, self.n_actions, ln)
-        self.critic = self._head("critic", self.critic_hidden, 1, ln)
+        self.critic = self._head("value", self.critic_hidden, 1, ln)  # ValueNetwork head name (value_networks.py:96)
         off = 0
         for lay in self.encoder + self.actor + self.critic:
             lay.w = off
@@ -136,8 +136,10 @@ class ActorCriticSpec:
     def state_dict_keys(self) -> dict[str, tuple[int, tuple[int, ...]]]:
         """Reference-compatible parameter names -> (offset, shape)."""
         out = {}
+        # critic.encoder is the reference's detached copy of the shared actor encoder
+        # (share_encoders, algo_utils.py:164-187): same offsets as actor.encoder
         for net, layers in (("actor.encoder.model", self.encoder), ("actor.head_net.model", self.actor),
-                            ("critic.head_net.model", self.critic)):
+                            ("critic.encoder.model", self.encoder), ("critic.head_net.model", self.critic)):
             for lay in layers:
                 out[f"{net}.{lay.name}.weight"] = (lay.w, (lay.fout, lay.fin))
                 out[f"{net}.{lay.name}.bias"] = (lay.b, (lay.fout,))

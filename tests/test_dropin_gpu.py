@@ -171,10 +171,13 @@ def test_rainbow_learn_matches_torch_reference(per):
     ref_opt.step()
     loss, idxs, new_pri = agent.learn(exp, per=per)
     assert abs(loss - loss_ref.item()) <= 1e-5 * abs(loss_ref.item())
-    # Adam's first step is ~lr * sign(g) where |g| >> eps and ill-conditioned
-    # where |g| ~ eps: compare within 1 % of lr
+    # the gradients are the kernel's output: compared tightly.  Adam's first step
+    # is ~lr * sign(g) where |g| >> eps and ill-conditioned where |g| ~ eps, so
+    # parameters are compared within 5 % of lr
     for p1, p2 in zip(agent.actor.parameters(), ref_actor.parameters()):
-        torch.testing.assert_close(p1, p2, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(p1.grad, p2.grad, rtol=1e-4, atol=1e-6)
+    for p1, p2 in zip(agent.actor.parameters(), ref_actor.parameters()):
+        torch.testing.assert_close(p1, p2, rtol=1e-4, atol=5e-5)
     if per:
         np.testing.assert_allclose(new_pri, el_ref.detach().cpu().numpy() + agent.prior_eps, rtol=1e-5)
         assert idxs is exp["idxs"]
@@ -220,3 +223,34 @@ def test_train_off_policy(algo, per, n_step):
     if n_step:
         assert len(n_mem) == len(memory)
     assert any(not torch.equal(a, b) for a, b in zip(p0, pop[0].actor.parameters()))
+
+
+def test_ppo_checkpoint_round_trip(tmp_path):
+    """PPO.save_checkpoint / load: reference state-dict names (actor.*,
+    critic.head_net.model.value_*, critic.encoder = the shared encoder), Adam
+    moments and step, attributes; the loaded agent acts identically."""
+    from agilerl_amd.algorithms import PPO
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.rollouts import collect_rollouts
+
+    obs_space, act_space = _spaces()
+    agent = PPO(obs_space, act_space, num_envs=16, learn_step=64, batch_size=32, lr=2e-3)
+    collect_rollouts(agent, SyntheticVecEnv(16, seed=5))
+    agent.learn()
+    agent.fitness = [0.5]
+    sd = agent.state_dict()
+    assert "critic.head_net.model.value_linear_layer_1.weight" in sd
+    assert torch.equal(sd["critic.encoder.model.encoder_linear_layer_1.weight"],
+                       sd["actor.encoder.model.encoder_linear_layer_1.weight"])
+    path = str(tmp_path / "ppo.pt")
+    agent.save_checkpoint(path)
+    other = PPO.load(path)
+    assert other.lr == 2e-3 and other.fitness == [0.5] and other.batch_size == 32
+    assert torch.equal(other.population.params.data[0], agent.population.params.data[0])
+    assert torch.equal(other.population.opt.exp_avg[0], agent.population.opt.exp_avg[0])
+    assert other.population.opt.step_count == agent.population.opt.step_count
+    obs = np.random.default_rng(0).standard_normal((16, 8)).astype(np.float32)
+    _, lp0, ent0, v0 = agent.get_action(obs)
+    _, lp1, ent1, v1 = other.get_action(obs)
+    np.testing.assert_array_equal(v0, v1)
+    np.testing.assert_array_equal(ent0, ent1)
