@@ -52,6 +52,7 @@ SIGNATURES = {
     "agx_segtree_retrieve": (_INT, [_P, _I, _P, _I, _P, _P, _P]),
     "agx_td_workspace_bytes": (_SZ, [_I]),
     "agx_td_target": (_INT, [_P] * 6 + [_I, _I, _D, _INT, _P, _P, _P, _P, _P]),
+    "agx_maddpg_critic_target": (_INT, [_P] * 4 + [_I, _D, _P, _P, _P, _P, _P]),
     "agx_c51_project_loss": (_INT, [_P] * 7 + [_I, _I, _I, _D, _D, _D, _P, _P, _P]),
     "agx_adam_workspace_bytes": (_SZ, [_I, _I]),
     "agx_clip_adam": (_INT, [_P, _P, _P, _P, _I, _I, _P, _INT, _F, _P, _F, _F, _F, _I, _P, _P]),

@@ -35,11 +35,13 @@ def _plain(v: Any) -> Any:
     return v
 
 
-def checkpoint_dict(agent, modules: dict[str, dict[str, torch.Tensor]], optimizers: dict[str, Any]) -> dict:
+def checkpoint_dict(agent, modules: dict[str, dict[str, torch.Tensor]], optimizers: dict[str, Any],
+                    spaces: bool = True) -> dict:
     out = {k: _plain(getattr(agent, k)) for k in HP_NAMES if hasattr(agent, k)}
     out["algo"] = agent.algo
     out["agilerl_version"] = "agx"
-    out["spaces"] = {"obs_shape": list(agent.observation_space.shape), "n_actions": int(agent.action_space.n)}
+    if spaces:
+        out["spaces"] = {"obs_shape": list(agent.observation_space.shape), "n_actions": int(agent.action_space.n)}
     out["network_info"] = {
         "network_names": list(modules),
         "modules": {f"{k}_state_dict": _plain(v) for k, v in modules.items()},

@@ -78,6 +78,40 @@ __global__ __launch_bounds__(kTdBlock) void td_target_kernel(
     }
 }
 
+// MADDPG critic target (agilerl/algorithms/maddpg.py:764-781): NaN rewards ->
+// 0, NaN dones -> 1, dones cast to uint8 (truncation), then
+//   y = r + ((1 - d) * gamma) * q'        ((1 - d) in uint8 arithmetic)
+//   loss = MSE(q, y);  dloss/dq = 2 (q - y) / B
+// One row per lane, squared errors reduced like td_target_kernel.
+__global__ __launch_bounds__(kTdBlock) void maddpg_critic_kernel(
+    const float *__restrict__ q, const float *__restrict__ qn, const float *__restrict__ r,
+    const float *__restrict__ d, int64_t B, float g, float *__restrict__ y, float *__restrict__ g_q,
+    double *__restrict__ partials) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double sq = 0.0;
+    if (i < B) {
+        const float ri = __builtin_isnan(r[i]) ? 0.0f : r[i];
+        const float di = __builtin_isnan(d[i]) ? 1.0f : d[i];
+        const unsigned char du = (unsigned char)(int)di;           // .to(torch.uint8)
+        const float nd = (float)(unsigned char)(1u - du);           // 1 - uint8 tensor (wraps)
+        const float yi = ri + (nd * g) * qn[i];
+        if (y) y[i] = yi;
+        const float diff = q[i] - yi;
+        if (g_q) g_q[i] = diff * (2.0f / (float)B);
+        const double dd = (double)q[i] - (double)yi;
+        sq = dd * dd;
+    }
+    __shared__ double red[kTdBlock / kWave];
+    sq = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x / 64] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < kTdBlock / kWave; ++w) t += red[w];
+        partials[blockIdx.x] = t;
+    }
+}
+
 __global__ __launch_bounds__(1024) void td_loss_finalize(const double *__restrict__ partials, int64_t nblk,
                                                          int64_t B, float *__restrict__ loss) {
     __shared__ double red[1024 / kWave];
@@ -380,6 +414,23 @@ extern "C" int agx_td_target(const float *q_next_online, const float *q_next_tar
     if (rc || !loss) return rc;
     td_loss_finalize<<<1, 1024, 0, s>>>(part, nblk, B, loss);
     return check_launch("agx_td_target loss");
+}
+
+extern "C" int agx_maddpg_critic_target(const float *q, const float *q_next, const float *rewards,
+                                        const float *dones, int64_t B, double gamma, float *y, float *g_q,
+                                        float *loss, void *workspace, void *stream) {
+    AGX_REQUIRE(q && q_next && rewards && dones && loss && workspace && B >= 0,
+                "agx_maddpg_critic_target: bad arguments");
+    if (B == 0) return AGX_OK;
+    hipStream_t s = as_stream(stream);
+    const int64_t nblk = ceil_div(B, kTdBlock);
+    double *part = static_cast<double *>(workspace);
+    maddpg_critic_kernel<<<(unsigned)nblk, kTdBlock, 0, s>>>(q, q_next, rewards, dones, B, (float)gamma, y, g_q,
+                                                            part);
+    int rc = check_launch("agx_maddpg_critic_target");
+    if (rc) return rc;
+    td_loss_finalize<<<1, 1024, 0, s>>>(part, nblk, B, loss);
+    return check_launch("agx_maddpg_critic_target loss");
 }
 
 extern "C" int agx_c51_project_loss(const float *q_next_online, const float *target_dist,

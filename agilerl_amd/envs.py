@@ -37,6 +37,34 @@ class Box:
         return np.random.uniform(self.low, self.high).astype(self.dtype)
 
 
+class Dict:
+    """Mapping of named spaces; a plain dict is key-sorted like gymnasium's
+    ``spaces.Dict``."""
+
+    def __init__(self, spaces: dict):
+        from collections import OrderedDict
+
+        self.spaces = spaces if isinstance(spaces, OrderedDict) else dict(sorted(spaces.items()))
+
+    def keys(self):
+        return self.spaces.keys()
+
+    def items(self):
+        return self.spaces.items()
+
+    def values(self):
+        return self.spaces.values()
+
+    def __getitem__(self, k):
+        return self.spaces[k]
+
+    def __iter__(self):
+        return iter(self.spaces)
+
+    def __len__(self):
+        return len(self.spaces)
+
+
 class SyntheticVecEnv:
     """``num_envs`` independent synthetic episodes; data drawn from a ring of
     pre-generated batches (``ring`` steps) so a step is a memcpy."""
@@ -78,6 +106,58 @@ class SyntheticVecEnv:
         if out_done is not None:
             np.copyto(out_done.reshape(term.shape), term)
         return obs, rew, term, self._trunc, {}
+
+    def close(self):
+        pass
+
+
+class SyntheticMultiAgentVecEnv:
+    """PettingZoo-parallel-style vectorised multi-agent stand-in shaped like
+    MPE simple_speaker_listener (speaker: obs 3, 3 actions; listener: obs 11,
+    5 actions): ``reset() -> (obs, infos)``, ``step(actions) -> (obs,
+    rewards, terminations, truncations, infos)``, each a dict agent_id ->
+    array with a leading ``num_envs`` dim.  Rewards ~ N(0,1) shared, episodes
+    truncate after ``max_cycles`` steps (simple_speaker_listener has no
+    terminations)."""
+
+    def __init__(self, num_envs: int, agent_dims: dict | None = None, max_cycles: int = 25, seed: int = 0,
+                 ring: int = 61):
+        agent_dims = agent_dims or {"speaker_0": (3, 3), "listener_0": (11, 5)}
+        self.num_envs = int(num_envs)
+        self.agents = list(agent_dims)
+        self.possible_agents = list(agent_dims)
+        self.observation_spaces = {a: Box(-np.inf, np.inf, (o,)) for a, (o, _) in agent_dims.items()}
+        self.action_spaces = {a: Discrete(n) for a, (_, n) in agent_dims.items()}
+        rng = np.random.default_rng(seed)
+        self._obs = {a: rng.standard_normal((ring, num_envs, o), dtype=np.float32) for a, (o, _) in agent_dims.items()}
+        self._rew = rng.standard_normal((ring, num_envs), dtype=np.float32)
+        self._ring, self._k, self._t = ring, 0, 0
+        self.max_cycles = max_cycles
+
+    def single_observation_space(self, agent):
+        return self.observation_spaces[agent]
+
+    def single_action_space(self, agent):
+        return self.action_spaces[agent]
+
+    def observation_space(self, agent):
+        return self.observation_spaces[agent]
+
+    def action_space(self, agent):
+        return self.action_spaces[agent]
+
+    def reset(self, seed=None, options=None):
+        self._k, self._t = 0, 0
+        return {a: self._obs[a][0].copy() for a in self.agents}, {a: {} for a in self.agents}
+
+    def step(self, actions):
+        self._k = (self._k + 1) % self._ring
+        self._t += 1
+        trunc = np.full(self.num_envs, self._t % self.max_cycles == 0)
+        obs = {a: self._obs[a][self._k].copy() for a in self.agents}
+        rew = {a: self._rew[self._k].copy() for a in self.agents}
+        term = {a: np.zeros(self.num_envs, dtype=bool) for a in self.agents}
+        return obs, rew, term, {a: trunc.copy() for a in self.agents}, {a: {} for a in self.agents}
 
     def close(self):
         pass

@@ -211,6 +211,22 @@ def td_target(q_next_target, rewards, dones, gamma, q_next_online=None, double=F
     return y, g_q, loss
 
 
+def maddpg_critic_target(q, q_next, rewards, dones, gamma):
+    """-> (y (B,1), dloss/dq (B,1), loss (1,)) of MADDPG._learn_individual's
+    critic step (maddpg.py:764-790) in one launch (+ the fixed-order loss sum)."""
+    B = q.shape[0]
+    qf, qn, r, d = (t.reshape(-1) for t in (q, q_next, rewards, dones))
+    for t, name in ((qf, "q"), (qn, "q_next"), (r, "rewards"), (d, "dones")):
+        _need(t, name, _f32, (B,))
+    y = torch.empty(B, 1, dtype=_f32, device=r.device)
+    g_q = torch.empty(B, 1, dtype=_f32, device=r.device)
+    loss = torch.empty(1, dtype=_f32, device=r.device)
+    ws = _ws(_lib.load().agx_td_workspace_bytes(B), r.device)
+    _lib.call("agx_maddpg_critic_target", qf.data_ptr(), qn.data_ptr(), r.data_ptr(), d.data_ptr(), B,
+              float(gamma), y.data_ptr(), g_q.data_ptr(), loss.data_ptr(), _lib.ptr(ws), _lib.stream())
+    return y, g_q, loss
+
+
 def c51_project_loss(q_next_online, target_dist, logp_cur, actions, rewards, dones, support, v_min,
                      v_max, gamma, with_proj=False):
     B, A, Z = target_dist.shape

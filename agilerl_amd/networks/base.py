@@ -48,8 +48,9 @@ class EvolvableNetwork(nn.Module):
         super().__init__()
         if encoder_cls is not None or simba or recurrent:
             raise NotImplementedError("agx networks build EvolvableMLP encoders (Box observations)")
-        if not hasattr(observation_space, "shape") or hasattr(observation_space, "n"):
-            raise NotImplementedError("agx networks take Box observation spaces")
+        multi = hasattr(observation_space, "spaces")
+        if not multi and (not hasattr(observation_space, "shape") or hasattr(observation_space, "n")):
+            raise NotImplementedError("agx networks take Box or Dict-of-Box observation spaces")
         assert latent_dim <= max_latent_dim, "Latent dimension must be less than or equal to max latent dimension."
         assert latent_dim >= min_latent_dim, "Latent dimension must be greater than or equal to min latent dimension."
         self.observation_space, self.action_space = observation_space, action_space
@@ -57,9 +58,19 @@ class EvolvableNetwork(nn.Module):
         self.device, self.random_seed, self.encoder_name = device, random_seed, encoder_name
         encoder_config = as_config(encoder_config)
         if encoder_config is None:  # get_default_encoder_config (utils/evolvable_networks.py:168-216)
-            encoder_config = mlp_net_config([64, 64], output_activation="ReLU", output_vanish=False)
+            encoder_config = {"output_activation": "ReLU"} if multi else \
+                mlp_net_config([64, 64], output_activation="ReLU", output_vanish=False)
         if encoder_config.get("output_activation") is None:  # base.py:226-230
             encoder_config["output_activation"] = encoder_config.get("activation", "ReLU")
+        self.flatten_obs = False
+        if multi:  # EvolvableMultiInput encoder (base.py:500-520)
+            from ..modules.multi_input import EvolvableMultiInput
+
+            encoder_config.pop("num_outputs", None)
+            self.encoder_config = encoder_config
+            self.encoder = EvolvableMultiInput(observation_space, num_outputs=latent_dim, device=device,
+                                               name=encoder_name, **encoder_config)
+            return
         # MLP encoders: output LayerNorm follows layer_norm, no output vanish (base.py:547-554)
         encoder_config["output_layernorm"] = encoder_config.get("layer_norm", True)
         encoder_config["output_vanish"] = False

@@ -7,6 +7,7 @@ weight_mu``, ``head_net.advantage_net.advantage_linear_layer_1.weight_mu`` ...).
 
 from __future__ import annotations
 
+import warnings
 from typing import Any
 
 import torch
@@ -123,3 +124,46 @@ class RainbowQNetwork(EvolvableNetwork):
 
     def forward(self, obs: torch.Tensor, q: bool = True, log: bool = False) -> torch.Tensor:
         return self.head_net(self.extract_features(obs), q=q, log=log)
+
+
+class ContinuousQNetwork(EvolvableNetwork):
+    """Q(s, a) (q_networks.py:302-430): encoder without LayerNorm (actions are
+    concatenated to the latent unscaled), head "value" on [latent, a] -> 1."""
+
+    def __init__(self, observation_space, action_space, encoder_cls=None, encoder_config=None, head_config=None,
+                 min_latent_dim: int = 8, max_latent_dim: int = 128, latent_dim: int = 32, simba: bool = False,
+                 recurrent: bool = False, device="cpu", random_seed: int | None = None) -> None:
+        encoder_config = as_config(encoder_config)
+        if not hasattr(observation_space, "spaces"):
+            if encoder_config is None:
+                encoder_config = mlp_net_config([64, 64], output_activation="ReLU", output_vanish=False,
+                                                layer_norm=False)
+            elif "hidden_size" in encoder_config:
+                if encoder_config.get("layer_norm", False):
+                    warnings.warn("Layer normalization is not supported for the encoder of DDPG networks. "
+                                  "Disabling it.", stacklevel=2)
+                encoder_config["layer_norm"] = False
+        super().__init__(observation_space, encoder_cls=encoder_cls, encoder_config=encoder_config,
+                         action_space=action_space, min_latent_dim=min_latent_dim, max_latent_dim=max_latent_dim,
+                         latent_dim=latent_dim, simba=simba, recurrent=recurrent, device=device,
+                         random_seed=random_seed)
+        head_config = as_config(head_config)
+        if head_config is None:
+            head_config = mlp_net_config([32], output_activation=None)
+        else:
+            head_config["output_activation"] = None
+        self.num_actions = action_space_flatdim(action_space)
+        self.head_net = self.create_mlp(self.latent_dim + self.num_actions, 1, "value", head_config)
+
+    def forward(self, obs, actions) -> torch.Tensor:
+        if not isinstance(actions, torch.Tensor):
+            actions = torch.as_tensor(actions, dtype=torch.float32)
+        if actions.dim() == 1:
+            actions = actions.unsqueeze(0)
+        return self.head_net(torch.cat([self.extract_features(obs), actions], dim=-1))
+
+
+def action_space_flatdim(space) -> int:
+    if isinstance(space, (list, tuple)):
+        return sum(action_space_flatdim(s) for s in space)
+    return flatdim(space)

@@ -44,7 +44,19 @@ def create_population(algo: str, net_config: dict[str, Any] | None, INIT_HP: dic
         return [cls.from_init_hp(observation_space, action_space, net_config, INIT_HP, index=i, device=device,
                                  **algo_kwargs)
                 for i in range(population_size)]
-    raise NotImplementedError(f"algorithm {algo!r} is outside the agx hot path (PPO, DQN, Rainbow DQN)")
+    if algo == "MADDPG":  # utils/utils.py:590-618
+        from ..algorithms.maddpg import MADDPG
+
+        hp = dict(batch_size=INIT_HP.get("BATCH_SIZE", 64), lr_actor=INIT_HP.get("LR_ACTOR", 0.0001),
+                  lr_critic=INIT_HP.get("LR_CRITIC", 0.001), learn_step=INIT_HP.get("LEARN_STEP", 5),
+                  gamma=INIT_HP.get("GAMMA", 0.95), tau=INIT_HP.get("TAU", 0.01),
+                  O_U_noise=INIT_HP.get("O_U_NOISE", True), expl_noise=INIT_HP.get("EXPL_NOISE", 0.1),
+                  vect_noise_dim=num_envs, mean_noise=INIT_HP.get("MEAN_NOISE", 0.0),
+                  theta=INIT_HP.get("THETA", 0.15), dt=INIT_HP.get("DT", 0.01))
+        return [MADDPG(observation_space, action_space, agent_ids=INIT_HP["AGENT_IDS"], index=i,
+                       net_config=net_config, device=device, **hp, **algo_kwargs)
+                for i in range(population_size)]
+    raise NotImplementedError(f"algorithm {algo!r} is outside the agx hot path (PPO, DQN, Rainbow DQN, MADDPG)")
 
 
 __all__ = ["create_population"]

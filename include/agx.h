@@ -240,6 +240,16 @@ int agx_td_target(const float *q_next_online, const float *q_next_target, const 
                   int64_t A, double gamma, int double_q, float *y, float *g_q, float *loss,
                   void *workspace, void *stream);
 
+/* ---- MADDPG critic target + MSE ------------------------------------------
+ * Replaces the critic half of MADDPG._learn_individual
+ * (agilerl/algorithms/maddpg.py:764-790): NaN rewards -> 0, NaN dones -> 1,
+ * dones cast to uint8; y = r + ((1 - d) * gamma) * q_next; loss =
+ * mean((q - y)^2) and dloss/dq = 2 (q - y) / B.  q, q_next, rewards, dones,
+ * y, g_q: (B) f32 (y, g_q may be NULL).  workspace: agx_td_workspace_bytes(B). */
+int agx_maddpg_critic_target(const float *q, const float *q_next, const float *rewards,
+                             const float *dones, int64_t B, double gamma, float *y, float *g_q,
+                             float *loss, void *workspace, void *stream);
+
 /* ---- Rainbow C51 projection + cross entropy ------------------------------
  * Replaces RainbowDQN._dqn_loss (agilerl/algorithms/dqn_rainbow.py:313-367).
  * q_next_online (B,A) picks a*; target_dist (B,A,Z) are the clamped target

@@ -1,0 +1,136 @@
+"""MADDPG hot path on the GPU: the HBM MultiAgentReplayBuffer against the
+deque restatement, agx_maddpg_critic_target against oracle/maddpg.py
+(maddpg.py:764-790, NaN rules included), MADDPG.learn against a plain-PyTorch
+_learn_individual on copies of the same networks, and the drop-in trainer."""
+
+import copy
+import random
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_replay_in_hbm_matches_deque():
+    from tests.test_multi_agent_replay import check_against_oracle
+
+    buf = check_against_oracle("cuda", memory_size=64, steps=40, n_envs=8, batch=32)
+    assert buf.storage.is_cuda
+
+
+@pytest.mark.parametrize("B", [1, 77, 4096])
+def test_critic_target_kernel(B):
+    from agilerl_amd import kernels as K
+    from oracle.maddpg import critic_target
+
+    rng = np.random.default_rng(B)
+    q, qn, r = (rng.standard_normal(B).astype(np.float32) for _ in range(3))
+    d = (rng.random(B) < 0.3).astype(np.float32)
+    r[rng.random(B) < 0.1] = np.nan
+    d[rng.random(B) < 0.1] = np.nan
+    y, g, loss = K.maddpg_critic_target(*(torch.from_numpy(x).cuda() for x in (q, qn, r, d)), 0.95)
+    ye, ge, le = critic_target(q, qn, r, d, 0.95)
+    np.testing.assert_array_equal(y.cpu().numpy().reshape(-1), ye)
+    np.testing.assert_array_equal(g.cpu().numpy().reshape(-1), ge)
+    assert abs(float(loss) - float(le)) <= 1e-6 * max(1.0, abs(float(le)))
+
+
+def _ma_spaces():
+    from agilerl_amd.envs import SyntheticMultiAgentVecEnv
+
+    env = SyntheticMultiAgentVecEnv(8, seed=2)
+    return env, [env.observation_spaces[a] for a in env.agents], [env.action_spaces[a] for a in env.agents]
+
+
+def _reference_learn(agent, actors, critics, actor_targets, critic_targets, opt_a, opt_c, experiences):
+    """maddpg.py:629-836 in plain PyTorch (criterion nn.MSELoss)."""
+    states, actions, rewards, next_states, dones = experiences
+    ids = agent.agent_ids
+    with torch.no_grad():
+        next_actions = [actor_targets[a](next_states[a]) for a in ids]
+    stacked = torch.cat([actions[a] for a in ids], dim=1)
+    stacked_next = torch.cat(next_actions, dim=1)
+    for a in ids:
+        q = critics[a](states, stacked)
+        with torch.no_grad():
+            qn = critic_targets[a](next_states, stacked_next)
+        r = torch.where(torch.isnan(rewards[a]), torch.zeros_like(rewards[a]), rewards[a]).float()
+        d = torch.where(torch.isnan(dones[a]), torch.ones_like(dones[a]), dones[a]).to(torch.uint8)
+        y = r + (1 - d) * agent.gamma * qn
+        loss = torch.nn.functional.mse_loss(q, y)
+        opt_c[a].zero_grad()
+        loss.backward()
+        opt_c[a].step()
+        act = actors[a](states[a])
+        det = {k: (act if k == a else actions[k]) for k in ids}
+        al = -critics[a](states, torch.cat([det[k] for k in ids], dim=1)).mean()
+        opt_a[a].zero_grad()
+        al.backward()
+        opt_a[a].step()
+    with torch.no_grad():
+        for a in ids:
+            for net, tgt in ((actors[a], actor_targets[a]), (critics[a], critic_targets[a])):
+                for e, t in zip(net.parameters(), tgt.parameters()):
+                    t.copy_(agent.tau * e + (1.0 - agent.tau) * t)
+
+
+def test_maddpg_learn_matches_torch():
+    from agilerl_amd.algorithms import MADDPG
+    from agilerl_amd.components import MultiAgentReplayBuffer
+
+    env, obs_spaces, act_spaces = _ma_spaces()
+    torch.manual_seed(0)
+    agent = MADDPG(obs_spaces, act_spaces, agent_ids=env.agents, batch_size=32, vect_noise_dim=8)
+    nets = copy.deepcopy((agent.actors, agent.critics, agent.actor_targets, agent.critic_targets))
+    opt_a = {a: torch.optim.Adam(nets[0][a].parameters(), lr=agent.lr_actor) for a in env.agents}
+    opt_c = {a: torch.optim.Adam(nets[1][a].parameters(), lr=agent.lr_critic) for a in env.agents}
+    mem = MultiAgentReplayBuffer(256, ["obs", "action", "reward", "next_obs", "done"], env.agents)
+    obs, info = env.reset()
+    for t in range(20):
+        action, raw = agent.get_action(obs, infos=info)
+        nxt, rew, term, trunc, info = env.step(action)
+        if t == 5:
+            rew["listener_0"][0] = np.nan
+        mem.save_to_memory(obs, raw, rew, nxt, term, is_vectorised=True)
+        obs = nxt
+    for it in range(3):
+        random.seed(it)
+        exp = mem.sample(32)
+        torch.manual_seed(10 + it)  # same Gumbel draws in both target-actor forwards
+        losses = agent.learn(exp)
+        torch.manual_seed(10 + it)
+        _reference_learn(agent, *nets, opt_a, opt_c, exp)
+        assert set(losses) == set(env.agents) and all(np.isfinite(v).all() for v in losses.values())
+    for mine, ref in ((agent.actors, nets[0]), (agent.critics, nets[1]), (agent.actor_targets, nets[2]),
+                      (agent.critic_targets, nets[3])):
+        for a in env.agents:
+            for p1, p2 in zip(mine[a].parameters(), ref[a].parameters()):
+                torch.testing.assert_close(p1, p2, rtol=1e-4, atol=2e-5)
+
+
+def test_train_multi_agent_off_policy_and_checkpoint(tmp_path):
+    from agilerl_amd.components import MultiAgentReplayBuffer
+    from agilerl_amd.hpo.tournament import TournamentSelection
+    from agilerl_amd.training import train_multi_agent_off_policy
+    from agilerl_amd.utils import create_population
+
+    env, obs_spaces, act_spaces = _ma_spaces()
+    INIT_HP = {"AGENT_IDS": env.agents, "BATCH_SIZE": 32, "LEARN_STEP": 8}
+    np.random.seed(0)
+    pop = create_population("MADDPG", None, INIT_HP, obs_spaces, act_spaces, population_size=2, num_envs=8)
+    mem = MultiAgentReplayBuffer(1000, ["obs", "action", "reward", "next_obs", "done"], env.agents)
+    pop, fits = train_multi_agent_off_policy(env, "synthetic_speaker_listener", "MADDPG", pop, mem,
+                                             INIT_HP=INIT_HP, max_steps=400, evo_steps=200, eval_loop=1,
+                                             tournament=TournamentSelection(2, True, 2, 1), verbose=False)
+    assert len(fits) == 2 and all(np.isfinite(f).all() for f in fits)
+    assert all(a.steps[-1] >= 400 for a in pop) and len(mem) == 800
+    path = str(tmp_path / "maddpg.pt")
+    pop[0].save_checkpoint(path)
+    other = create_population("MADDPG", None, INIT_HP, obs_spaces, act_spaces, population_size=1, num_envs=8)[0]
+    other.load_checkpoint(path)
+    for a in env.agents:
+        for p1, p2 in zip(pop[0].actors[a].parameters(), other.actors[a].parameters()):
+            assert torch.equal(p1, p2)
+    assert other.fitness == pop[0].fitness
