@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must load torch's HIP runtime before libagx binds to it)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libagx.so")
+LIB_PATH = os.environ.get("AGX_LIB") or os.path.join(_HERE, "lib", "libagx.so")  # AGX_LIB: A/B builds
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int64

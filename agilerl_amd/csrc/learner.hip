@@ -56,7 +56,7 @@ constexpr int kNW = kNT / kWave;  // 8 waves
 constexpr int kSB = 32;           // rows per sub-batch
 constexpr int kMaxSlot = 10;      // dW tiles per wave
 constexpr int kMaxK = 4;          // partner workgroups per agent (hand-off unrolled for <= 4)
-constexpr int kMaxPT = 30;        // LDS parameter slots per thread
+constexpr int kMaxPT = 32;        // LDS parameter slots per thread: 8 float4 chunks
 constexpr int kMaxA = 16;
 constexpr int kMaxBlk = 28;
 
@@ -97,6 +97,9 @@ struct LearnPlan {
 };
 
 constexpr int rup(int x, int m) { return (x + m - 1) / m * m; }
+// Adam / norm ownership: thread t owns the float4 chunks t, t + kNT, ... of the
+// LDS parameter image; slot s is float (s & 3) of chunk (s >> 2)
+__host__ __device__ constexpr int slot_l(int t, int s) { return 4 * (t + kNT * (s >> 2)) + (s & 3); }
 
 constexpr LearnPlan make_plan(NetDims d) {
     LearnPlan pl{};
@@ -546,6 +549,9 @@ struct LearnArgs {
     unsigned *cnt;        // [P] arrival counters, [P] = timeout word (zeroed per call)
 };
 
+#define IC(x) std::integral_constant<int, (x)>()
+#define BC(x) std::integral_constant<bool, (x)>()
+
 constexpr unsigned kSpinMax = 1u << 22;  // ~ seconds of s_sleep polling: a missing partner is a bug
 
 #define AGX_STAMP(slot)                                                          \
@@ -580,7 +586,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     unsigned gbits = 0, vbits = 0;
 #pragma unroll
     for (int i = 0; i < kMaxPT; ++i) {
-        const int l = tid + kNT * i;
+        const int l = slot_l(tid, i);
         int grp = 0;
         const int f = l < pl.param_end ? lds_to_flat<C>(l, grp) : -1;
         am[i] = f >= 0 ? gm[f] : 0.f;
@@ -617,8 +623,56 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             for (int s = 0; s < kMaxSlot; ++s) acc[s] = f4{0.f, 0.f, 0.f, 0.f};
             for (int i = tid; i < pl.l_stat - pl.l_red; i += kNT) sm[pl.l_red + i] = 0.f;
             float lsum = 0.f;
+            // this update's gradient slabs (double-buffered by update parity)
+            const int upd = e * nmb + mb;
+            float *base = g.K > 1 ? g.slabs + ((size_t)p * 2 + (upd & 1)) * g.K * pl.slab : nullptr;
+            const auto slab_rsrc = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)kk * pl.slab, 0,
+                                                                     __builtin_amdgcn_readfirstlane(pl.slab * 4),
+                                                                     0x00020000);
+            // dW tiles of group gg -> fn(LDS-image offset, value) (padding columns skipped)
+            auto emit_tiles = [&](auto gc, auto fn) {
+                constexpr int gg = decltype(gc)::value;
+                AGX_IDS;
+#pragma unroll
+                for (int j = 0; j < pl.nslot[gg]; ++j) {
+                    const int t = wave + kNW * j;
+                    if (t < pl.nt[gg]) {
+                        const int o0 = (t / pl.ncol[gg]) * 16, i0 = (t % pl.ncol[gg]) * 16;
+                        const int col = i0 + lr16;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int o = o0 + lq * 4 + i;
+                            const float x = acc[pl.slot0[gg] + j][i];
+                            if constexpr (gg < pl.ne) {
+                                if (col < pl.ein[gg]) fn(pl.l_ew[gg] + o * pl.l_eld[gg] + col, x);
+                            } else if constexpr (gg == pl.ne) {
+                                fn(pl.l_hw + o * pl.l_hld + col, x);
+                            } else if constexpr (gg == pl.ne + 1) {
+                                if (o < pl.A) {
+                                    if (col < pl.ha) fn(pl.l_aow + o * pl.l_aold + col, x);
+                                    else if (col == pl.ha) fn(pl.l_aob + o, x);
+                                }
+                            } else {
+                                if (o == 0) {
+                                    if (col < pl.hc) fn(pl.l_cow + col, x);
+                                    else if (col == pl.hc) fn(pl.l_cob, x);
+                                }
+                            }
+                        }
+                    }
+                }
+            };
+            // write-through (sc1) store of one gradient word into this workgroup's slab
+            auto slab_put = [&](int l, float x) {
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), slab_rsrc, l * 4, 0, 16);
+            };
+            // partners publish each group's dW straight from registers as soon as the
+            // group is final (last sub-batch), overlapping the stores with the rest of
+            // the backward pass
+            const bool direct = g.K > 1;
 
             for (int sb = kk * kSB; sb < bsz; sb += g.K * kSB) {
+                const bool last_sb = sb + g.K * kSB >= bsz;
                 const int nrow = bsz - sb < kSB ? bsz - sb : kSB;
                 const int jsb = (sb / kSB) / g.K;
                 const int stb = jsb < 4 ? jsb * 16 : 80;
@@ -723,6 +777,10 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                 });
                         }
                     }
+                    if (direct && last_sb) {
+                        emit_tiles(IC(pl.ne + 1), slab_put);
+                        emit_tiles(IC(pl.ne + 2), slab_put);
+                    }
                     constexpr int nt = (kSB / 16) * (pl.H / 16);
                     for (int t = wave; t < nt; t += kNW) {
                         const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
@@ -799,9 +857,6 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         }
                     }
                 };
-#define IC(x) std::integral_constant<int, (x)>()
-#define BC(x) std::integral_constant<bool, (x)>()
-
                 // ---- P6: head LN backward (dY_h in S2 -> dZ_h in S2) ----------
                 ln_bwd(IC(pl.H), IC(pl.ha), IC(pl.l_xh), IC(pl.ld_xh), IC(pl.l_rh), IC(pl.l_hg), IC(pl.l_hbe),
                        IC(pl.red_h), BC(true));
@@ -822,6 +877,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                 [&](int k, int n) { return relu(sm[pl.l_xe[Le] + k * pl.ld_xe[Le] + i0 + n]); });
                         }
                     }
+                    if (direct && last_sb) emit_tiles(IC(gh), slab_put);
                     constexpr int nt = (kSB / 16) * (pl.lat / 16);
                     for (int t = wave; t < nt; t += kNW) {
                         const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
@@ -874,6 +930,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                 });
                         }
                     }
+                    if (direct && last_sb) emit_tiles(IC(L), slab_put);
                     if constexpr (L > 0) {
                         constexpr int nt = (kSB / 16) * (fin / 16);
                         for (int t = wave; t < nt; t += kNW) {
@@ -893,46 +950,24 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 AGX_STAMP(stb + 7);
             }  // sub-batches
 
-            // ---- P9: dump gradients into the LDS image of the parameter region --
+            // ---- P9: gradients -> the LDS image (K == 1) or the slab (partners) --
             float *G = sm + pl.l_grad;
-            auto dump = [&](auto gc) {
-                constexpr int gg = decltype(gc)::value;
-                AGX_IDS;
-#pragma unroll
-                for (int j = 0; j < pl.nslot[gg]; ++j) {
-                    const int t = wave + kNW * j;
-                    if (t < pl.nt[gg]) {
-                        const int o0 = (t / pl.ncol[gg]) * 16, i0 = (t % pl.ncol[gg]) * 16;
-                        const int col = i0 + lr16;
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const int o = o0 + lq * 4 + i;
-                            const float x = acc[pl.slot0[gg] + j][i];
-                            if constexpr (gg < pl.ne) {
-                                if (col < pl.ein[gg]) G[pl.l_ew[gg] + o * pl.l_eld[gg] + col] = x;
-                            } else if constexpr (gg == pl.ne) {
-                                G[pl.l_hw + o * pl.l_hld + col] = x;
-                            } else if constexpr (gg == pl.ne + 1) {
-                                if (o < pl.A) {
-                                    if (col < pl.ha) G[pl.l_aow + o * pl.l_aold + col] = x;
-                                    else if (col == pl.ha) G[pl.l_aob + o] = x;
-                                }
-                            } else {
-                                if (o == 0) {
-                                    if (col < pl.hc) G[pl.l_cow + col] = x;
-                                    else if (col == pl.hc) G[pl.l_cob] = x;
-                                }
-                            }
-                        }
-                    }
-                }
-            };
-            dump(IC(0));
-            dump(IC(1));
-            if constexpr (pl.ne == 3) dump(IC(2));
-            dump(IC(pl.ne));
-            dump(IC(pl.ne + 1));
-            dump(IC(pl.ne + 2));
+            auto gput = [&](int l, float x) { G[l] = x; };
+            if (!direct) {
+                emit_tiles(IC(0), gput);
+                emit_tiles(IC(1), gput);
+                if constexpr (pl.ne == 3) emit_tiles(IC(2), gput);
+                emit_tiles(IC(pl.ne), gput);
+                emit_tiles(IC(pl.ne + 1), gput);
+                emit_tiles(IC(pl.ne + 2), gput);
+            } else if (kk * kSB >= bsz) {  // no sub-batch this update: publish zeros
+                emit_tiles(IC(0), slab_put);
+                emit_tiles(IC(1), slab_put);
+                if constexpr (pl.ne == 3) emit_tiles(IC(2), slab_put);
+                emit_tiles(IC(pl.ne), slab_put);
+                emit_tiles(IC(pl.ne + 1), slab_put);
+                emit_tiles(IC(pl.ne + 2), slab_put);
+            }
             // LN / bias vectors: fixed-order sums of the per-wave partials
             auto vdump = [&](auto Lc) {
                 constexpr int L = decltype(Lc)::value;
@@ -951,7 +986,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     } else {
                         l = (k == 0 ? pl.l_hb : (k == 1 ? pl.l_hg : pl.l_hbe)) + j;
                     }
-                    G[l] = x;
+                    if (direct) slab_put(l, x);
+                    else G[l] = x;
                 }
             };
             vdump(IC(0));
@@ -967,24 +1003,13 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             }
             if (g.K > 1) {
                 // ---- P9b: exchange partial gradients with the agent's partners --------
-                // (MI355X_MICROARCH visibility rules: plain stores -> vmcnt drain ->
-                // barrier -> agent release -> ticket; relaxed poll -> ONE agent acquire)
-                const int upd = e * nmb + mb;
-                float *base = g.slabs + ((size_t)p * 2 + (upd & 1)) * g.K * pl.slab;
-                float *mine = base + (size_t)kk * pl.slab;
-                // write-through (sc1) slab stores: drained by every storing wave before
-                // the barrier, so no release fence (cdna_hip_programming.md §6 G16 R1)
-                {
-                    const int nbytes = __builtin_amdgcn_readfirstlane(pl.slab * 4);
-                    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(mine, 0, nbytes, 0x00020000);
-                    for (int i = tid; i < pl.param_end / 4; i += kNT) {
-                        const f4 v = reinterpret_cast<const f4 *>(G)[i];
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rsrc, i * 16, 0, 16);
-                    }
-                    if (tid == 0)
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, lmb), rsrc,
-                                                              pl.param_end * 4, 0, 16);
-                }
+                // (MI355X_MICROARCH visibility rules: sc1 stores -> vmcnt drain ->
+                // barrier -> relaxed agent ticket; relaxed poll -> barrier -> sc1 loads)
+                // every gradient word went out as a write-through (sc1) store from the
+                // backward pass / vdump; the loss word follows.  Drained by every storing
+                // wave before the barrier, so no release fence (cdna_hip_programming.md
+                // §6 G16 R1)
+                if (tid == 0) slab_put(pl.param_end, lmb);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 if (tid == 0) {
@@ -1001,60 +1026,26 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                             break;
                         }
                     }
-                    // ONE agent-scope acquire, then plain loads (measured: sc1 loads of the
-                    // slabs instead of the acquire cost more than the fence saves)
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    // no acquire: the slabs are read with sc1 loads below
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     stat[3 * kNW] = ok ? 1.f : 0.f;
                     AGX_STAMP(64 + 12);
                 }
                 __syncthreads();
                 if (stat[3 * kNW] == 0.f) return;  // partner never arrived: timeout word set, whole block exits
-                // fixed-order sum over partners: every workgroup of the agent computes
-                // bit-identical totals, hence bit-identical parameters after Adam
-                // (own slab read back from LDS: same bits as the stored copy).  Chunks
-                // of 4 float4 per thread with all partner loads issued before the adds.
-                {
-                    constexpr int n4 = pl.param_end / 4;
-                    constexpr int NI = (n4 + kNT - 1) / kNT;
-                    const f4 *G4 = reinterpret_cast<const f4 *>(G);
-                    auto slab_ld = [&](int q, int i) {
-                        return reinterpret_cast<const f4 *>(base + (size_t)q * pl.slab)[i];
-                    };
-#pragma unroll
-                    for (int j0 = 0; j0 < NI; j0 += 4) {
-                        f4 t[4], v[3][4];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int i = tid + (j0 + j) * kNT;
-                            t[j] = f4{0.f, 0.f, 0.f, 0.f};
-                            if (j0 + j < NI && i < n4) {
-                                t[j] = kk == 0 ? G4[i] : slab_ld(0, i);
-#pragma unroll
-                                for (int q = 1; q < 4; ++q)
-                                    if (q < g.K) v[q - 1][j] = q == kk ? G4[i] : slab_ld(q, i);
-                            }
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int i = tid + (j0 + j) * kNT;
-                            if (j0 + j < NI && i < n4) {
-#pragma unroll
-                                for (int q = 1; q < 4; ++q)
-                                    if (q < g.K) t[j] += v[q - 1][j];
-                                reinterpret_cast<f4 *>(G)[i] = t[j];
-                            }
-                        }
-                    }
-                }
                 // (loss words via vector atomics: a uniform plain load would take the
-                // scalar-cache path, which the acquire does not invalidate)
-                float lt = __hip_atomic_load(base + pl.param_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (int q = 1; q < g.K; ++q)
-                    lt += __hip_atomic_load(base + (size_t)q * pl.slab + pl.param_end, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-                lmb = lt;
-                __syncthreads();
+                // scalar-cache path, which never sees the partners' stores)
+                // (one vector load: lane q reads partner q's loss word; summed in
+                // partner order)
+                {
+                    const int ln = vlane();
+                    const float w = ln < g.K ? __hip_atomic_load(base + (size_t)ln * pl.slab + pl.param_end,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                             : 0.f;
+                    float lt = readlane_f(w, 0);
+                    for (int q = 1; q < g.K; ++q) lt += readlane_f(w, q);
+                    lmb = lt;
+                }
                 AGX_STAMP(64 + 13);
             }
 
@@ -1063,14 +1054,62 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             // region need no bounds test (padding slots carry g = m = v = 0, so
             // Adam writes their value back unchanged); per-slot branches cost
             // exec-mask traffic and SGPR spills.
-            constexpr int kFull = pl.param_end / kNT;                  // slots < param_end for every thread
-            constexpr int kUsed = (pl.param_end + kNT - 1) / kNT;      // slots that exist at all
+            constexpr int n4 = pl.param_end / 4;
+            constexpr int kFull4 = n4 / kNT;               // chunks < param_end for every thread
+            constexpr int kUsed4 = (n4 + kNT - 1) / kNT;   // chunks that exist at all
             float n0 = 0.f, n1 = 0.f;
             float gr[kMaxPT];  // gradients stay in registers for the Adam pass
+            {
+                auto chunk_in = [&](int j) { return j < kFull4 || tid + kNT * j < n4; };
+                auto put = [&](int j, f4 x) {
 #pragma unroll
-            for (int i = 0; i < kUsed; ++i) {
-                const int l = tid + kNT * i;
-                const float x = (i < kFull || l < pl.param_end) ? G[l] : 0.f;
+                    for (int c = 0; c < 4; ++c) gr[4 * j + c] = x[c];
+                };
+                if (direct) {
+                    // fixed-order sum over the K partner slabs, straight from L2 into the
+                    // owned chunks: every workgroup of the agent adds the same words in the
+                    // same order -> bit-identical totals, hence bit-identical parameters
+                    // partners 0 and 1 in flight together, then 2, then 3 (K <= 4)
+                    // sc1 buffer loads (L1 bypassed): with every slab store sc1 and drained
+                    // before the ticket, no acquire fence is needed (MI355X_MICROARCH.md,
+                    // inter-workgroup visibility, valid forms: sc1 stores + sc1 loads)
+                    auto ld = [&](int q, int j) {
+                        const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                            base + (size_t)q * pl.slab, 0, __builtin_amdgcn_readfirstlane(pl.slab * 4), 0x00020000);
+                        return chunk_in(j) ? __builtin_bit_cast(
+                                                 f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + kNT * j) * 16, 0, 16))
+                                           : f4{0.f, 0.f, 0.f, 0.f};
+                    };
+                    {
+                        f4 b[kUsed4];
+#pragma unroll
+                        for (int j = 0; j < kUsed4; ++j) {
+                            put(j, ld(0, j));
+                            b[j] = ld(1, j);  // K >= 2 here
+                        }
+#pragma unroll
+                        for (int j = 0; j < kUsed4; ++j)
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) gr[4 * j + c] += b[j][c];
+                    }
+                    for (int q = 2; q < g.K; ++q) {
+#pragma unroll
+                        for (int j = 0; j < kUsed4; ++j) {
+                            const f4 x = ld(q, j);
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) gr[4 * j + c] += x[c];
+                        }
+                    }
+                } else {
+                    const f4 *G4 = reinterpret_cast<const f4 *>(G);
+#pragma unroll
+                    for (int j = 0; j < kUsed4; ++j)
+                        put(j, chunk_in(j) ? G4[tid + kNT * j] : f4{0.f, 0.f, 0.f, 0.f});
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4 * kUsed4; ++i) {
+                const float x = gr[i];
                 const bool valid = (vbits >> i) & 1u, crit = (gbits >> i) & 1u;
                 gr[i] = valid ? x : 0.f;
                 const float x2 = gr[i] * gr[i];
@@ -1107,26 +1146,43 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             const float bc2s = (float)sqrt(1.0 - pb2);
             const float step_size = lr_p / bc1;
             const float inv_bc2s = 1.f / bc2s;
-            float pv[kMaxPT];  // all parameter reads issued before any write
+            // Adam on float4 chunks: LDS b128 reads/writes; the elementwise math on
+            // 4-vectors lowers to packed-f32 VALU ops (v_pk_mul/add_f32, 2 lanes/op)
+            f4 pv[kMaxPT / 4];  // all parameter reads issued before any write
+            f4 *sm4 = reinterpret_cast<f4 *>(sm);
 #pragma unroll
-            for (int i = 0; i < kUsed; ++i) {
-                const int l = tid + kNT * i;
-                pv[i] = (i < kFull || l < pl.param_end) ? sm[l] : 0.f;
-            }
+            for (int j = 0; j < kUsed4; ++j)
+                pv[j] = (j < kFull4 || tid + kNT * j < n4) ? sm4[tid + kNT * j] : f4{0.f, 0.f, 0.f, 0.f};
+            const float ob1 = 1.f - g.b1, ob2 = 1.f - g.b2;
 #pragma unroll
-            for (int i = 0; i < kUsed; ++i) {
-                const int l = tid + kNT * i;
-                {
-                    const float gr_c = gr[i] * (((gbits >> i) & 1u) ? c1 : c0);
-                    am[i] = am[i] + (1.f - g.b1) * (gr_c - am[i]);
-                    av[i] = av[i] * g.b2 + (1.f - g.b2) * gr_c * gr_c;
-                    // hardware sqrt / reciprocal (1 ulp) instead of the IEEE
-                    // expansions: the update m/(sqrt(v)+eps) is compared within
-                    // tolerance, never bit-exactly (summation order already differs)
-                    const float denom = __builtin_amdgcn_sqrtf(av[i]) * inv_bc2s + g.eps;
-                    const float nv = pv[i] - step_size * (am[i] * __builtin_amdgcn_rcpf(denom));
-                    if (i < kFull || l < pl.param_end) sm[l] = nv;
+            for (int j = 0; j < kUsed4; ++j) {
+                f4 gc, m, v;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int i = 4 * j + c;
+                    gc[c] = ((gbits >> i) & 1u) ? c1 : c0;
+                    m[c] = am[i];
+                    v[c] = av[i];
                 }
+                gc = f4{gr[4 * j], gr[4 * j + 1], gr[4 * j + 2], gr[4 * j + 3]} * gc;
+                m = m + ob1 * (gc - m);
+                v = v * g.b2 + ob2 * gc * gc;
+                // hardware sqrt / reciprocal (1 ulp) instead of the IEEE expansions:
+                // the update m/(sqrt(v)+eps) is compared within tolerance, never
+                // bit-exactly (summation order already differs)
+                f4 r;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) r[c] = __builtin_amdgcn_sqrtf(v[c]);
+                r = r * inv_bc2s + g.eps;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) r[c] = __builtin_amdgcn_rcpf(r[c]);
+                const f4 nv = pv[j] - step_size * (m * r);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    am[4 * j + c] = m[c];
+                    av[4 * j + c] = v[c];
+                }
+                if (j < kFull4 || tid + kNT * j < n4) sm4[tid + kNT * j] = nv;
             }
             __syncthreads();
             AGX_STAMP(64 + 10);
@@ -1137,7 +1193,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     if (kk != 0) return;
 #pragma unroll
     for (int i = 0; i < kMaxPT; ++i) {
-        const int l = tid + kNT * i;
+        const int l = slot_l(tid, i);
         if ((vbits >> i) & 1u) {
             int grp;
             const int f = lds_to_flat<C>(l, grp);

@@ -362,6 +362,118 @@ def cpu_baseline_leg(args, S_per_agent):
                        f"so population env-steps/s = per-agent rate")
 
 
+def _cpu_threads() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_population_all_cores(args, seconds):
+    """The same CPU PPO port with torch intra-op threads on every allowed core
+    (OMP_NUM_THREADS / affinity; 16 on a 1-GPU box)."""
+    from agilerl_amd.envs import SyntheticVecEnv
+    from oracle.ppo_cpu import CpuPPOAgent
+
+    threads = torch.get_num_threads()
+    n_thr = int(os.environ.get("OMP_NUM_THREADS", _cpu_threads()))
+    torch.set_num_threads(n_thr)
+    agent = CpuPPOAgent(num_envs=args.num_envs, learn_step=args.learn_step, batch_size=args.batch_size,
+                        update_epochs=args.epochs)
+    env = SyntheticVecEnv(args.num_envs, seed=7)
+    t0, steps = time.perf_counter(), 0
+    while True:
+        steps += agent.iteration(env)
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    torch.set_num_threads(threads)
+    return dict(value=round(steps / dt, 1), unit="env-steps/s", cores=n_thr, kind="port")
+
+
+def _ppo_loss_torch_batched(logp, old_logp, adv, ret, old_v, v, H, b, clip, vf, ent):
+    """ppo.py:868-896 forward + its gradients (d/dlogp, d/dv, d/dH) as torch
+    CPU ops over all minibatches at once ([S/b, b] views)."""
+    t = [torch.from_numpy(np.ascontiguousarray(x)).view(-1, b) for x in (logp, old_logp, adv, ret, old_v, v, H)]
+    logp, old_logp, adv, ret, old_v, v, H = t
+    ratio = torch.exp(logp - old_logp)
+    rc = ratio.clamp(1 - clip, 1 + clip)
+    p1, p2 = -adv * ratio, -adv * rc
+    pg = torch.maximum(p1, p2).mean(1)
+    dv = v - old_v
+    vcl = old_v + dv.clamp(-clip, clip)
+    lu, lc = (v - ret) ** 2, (vcl - ret) ** 2
+    vl = 0.5 * torch.maximum(lu, lc).mean(1)
+    loss = pg + vf * vl - ent * H.mean(1)
+    g1 = (p1 > p2).float() + 0.5 * (p1 == p2).float()
+    g2 = (p2 > p1).float() + 0.5 * (p1 == p2).float()
+    inr = ((ratio >= 1 - clip) & (ratio <= 1 + clip)).float()
+    g_logp = (g1 * -adv + g2 * -adv * inr) / b * ratio
+    gu = (lu > lc).float() + 0.5 * (lu == lc).float()
+    gc = (lc > lu).float() + 0.5 * (lu == lc).float()
+    inv = ((dv >= -clip) & (dv <= clip)).float()
+    g_v = vf * 0.5 / b * (gu * 2 * (v - ret) + gc * 2 * (vcl - ret) * inv)
+    g_H = torch.full_like(H, -ent / b)
+    return loss, g_logp, g_v, g_H
+
+
+def cpu_kernels_leg(seconds):
+    """SURVEY §8d CPU lines for the roofline workload (GAE + 4 x loss, 177 B
+    per transition): the numpy T-loop GAE + the torch-op loss on 1 thread, and
+    the OpenMP C restatement (oracle/c/oracle.c) on every allowed core, each on
+    a bounded slice of the §8d inputs (whole agents of T=1024 x N=8192)."""
+    from oracle import cref
+    from oracle import gae as ogae
+
+    T, N, b = ROOF_T, ROOF_N, ROOF_B
+    rng = np.random.default_rng(0)
+    r = rng.standard_normal((T, N), dtype=np.float32)
+    v = rng.standard_normal((T, N), dtype=np.float32)
+    d = (rng.random((T, N)) < 0.01).astype(np.uint8)
+    lv = rng.standard_normal(N, dtype=np.float32)
+    ld = (rng.random(N) < 0.01).astype(np.uint8)
+    S = T * N
+    old_logp = (rng.random(S, dtype=np.float32) * -2.95 - 0.05).astype(np.float32)
+    logp = (old_logp + 0.05 * rng.standard_normal(S, dtype=np.float32)).astype(np.float32)
+    newv = (v.reshape(-1) + 0.1 * rng.standard_normal(S, dtype=np.float32)).astype(np.float32)
+    H = (rng.random(S, dtype=np.float32) * np.float32(np.log(4))).astype(np.float32)
+    out = {}
+    # numpy / torch-op path, 1 thread: GAE once + loss x4 per agent slice
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    t0, n = time.perf_counter(), 0
+    while True:
+        adv, ret = ogae.gae(r, v, d.astype(bool), lv, ld.astype(bool))
+        for _ in range(4):
+            _ppo_loss_torch_batched(logp, old_logp, adv.reshape(-1), ret.reshape(-1), v.reshape(-1), newv, H,
+                                    b, 0.2, 0.5, 0.01)
+        n += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    torch.set_num_threads(threads)
+    rate = n * S / dt
+    out["numpy_torch_1t"] = dict(value=round(rate, 1), unit="transitions/s", gbs=round(rate * 177 / 1e9, 3),
+                                 cores=1, kind="port",
+                                 sample=f"{n} x (T={T}, N={N}) GAE numpy T-loop + 4 torch-op loss passes")
+    n_thr = int(os.environ.get("OMP_NUM_THREADS", _cpu_threads()))
+    t0, n = time.perf_counter(), 0
+    while True:
+        adv, ret = cref.gae(r, v, d, lv, ld, 0.99, 0.95, nthreads=n_thr)
+        for _ in range(4):
+            cref.ppo_loss(logp, old_logp, adv.reshape(-1), ret.reshape(-1), v.reshape(-1), newv, H, b, 0.2, 0.5,
+                          0.01, nthreads=n_thr)
+        n += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    rate = n * S / dt
+    out["c_openmp"] = dict(value=round(rate, 1), unit="transitions/s", gbs=round(rate * 177 / 1e9, 3),
+                           cores=n_thr, kind="port",
+                           sample=f"{n} x (T={T}, N={N}) oracle_gae + 4 oracle_ppo_loss (gcc -O2 -fopenmp)")
+    return out
+
+
 # --------------------------------------------------------------------------- #
 def main():
     args = parse()
@@ -379,6 +491,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline_leg(args, res["S"])
+        cpu["all_cores"] = cpu_population_all_cores(args, min(args.cpu_seconds, 10.0))
+        cpu["roofline_workload"] = cpu_kernels_leg(min(args.cpu_seconds, 8.0))
     if rank == 0:
         value = res["env_steps"] / res["dt"]
         line = {
