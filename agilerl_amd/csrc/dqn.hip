@@ -20,6 +20,8 @@
 // scan.  One wave per row, lane z <-> atom z (Z <= 64 per pass, Z <= 256).
 // Algorithmic bytes per row: 4A (q row) + 4Z (target row a*) + 4Z (log_p row
 // a_i) + 8 (r, d) + 4 (loss) = 444 B at A = 6, Z = 51.
+#include <cmath>
+
 #include "agx_common.h"
 
 namespace agx {
@@ -233,6 +235,25 @@ constexpr int kC51RowWaves = 4;
 __device__ __forceinline__ float bperm_f(int src_lane, float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_lane << 2, __builtin_bit_cast(int, v)));
 }
+// acc += mass[s], mass[s+1], ..., mass[e-1] in that order (mass[z] lives in
+// lane z); nmax = wave max of e - s.  The usual run is 1-2 atoms; a d = 1 row
+// sends all Z atoms to one bin, so long runs keep 8 permutes in flight.
+__device__ __forceinline__ float fold_run(float acc, int s, int e, int nmax, float mass) {
+    if (nmax <= 2) {
+        const float m0 = bperm_f(s & 63, mass), m1 = bperm_f((s + 1) & 63, mass);
+        acc = s < e ? acc + m0 : acc;
+        return s + 1 < e ? acc + m1 : acc;
+    }
+    for (int t = 0; t < nmax; t += 8) {
+        float m[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = bperm_f((s + t + j) & 63, mass);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc = s + t + j < e ? acc + m[j] : acc;
+    }
+    return acc;
+}
+
 template <int C>
 __device__ __forceinline__ float dpp_f(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), C, 0xf, 0xf, true));
@@ -366,14 +387,8 @@ __global__ __launch_bounds__(kC51RowWaves * 64) void c51_rows_kernel(
                 nl = max(nl, __shfl_xor(nl, o, 64));
                 nu = max(nu, __shfl_xor(nu, o, 64));
             }
-            for (int t = 0; t < nl; ++t) {
-                const float m = bperm_f(l0 + t, mlr[r]);
-                if (l0 + t < l1) acc += m;
-            }
-            for (int t = 0; t < nu; ++t) {
-                const float m = bperm_f(u0 + t, mur[r]);
-                if (u0 + t < u1) acc += m;
-            }
+            acc = fold_run(acc, l0, l1, nl, mlr[r]);
+            acc = fold_run(acc, u0, u1, nu, mur[r]);
         } else if (bin < Z) {
             for (int z = 0; z < Z; ++z)
                 if (sRun[w][r][0][z] == bin) acc += __builtin_bit_cast(float, sRun[w][r][2][z]);
@@ -384,6 +399,182 @@ __global__ __launch_bounds__(kC51RowWaves * 64) void c51_rows_kernel(
         if (proj && live && bin < Z) proj[(size_t)ri[r] * Z + bin] = acc;
         const float part = wave_sum_dpp(bin < Z ? acc * lp[r] : 0.f);
         if (lane == 0 && live) loss[ri[r]] = -part;
+    }
+}
+
+
+// Z <= 64, A <= 64 (Rainbow: Z = 51, A = 6): one wave per 64 rows, one lane
+// per row.  The per-row serial order of the reference's two index_add_ calls
+// is then simply the lane's own loop over z:
+//   1. lane k finds a*_k = argmax Q_online(s'_k) from its own Q row;
+//   2. the wave gathers the 64 selected target rows with coalesced loads
+//      (flattened (row, atom) order, a* of the row fetched from its lane) into
+//      LDS transposed as sP[z][row] (pitch 65: conflict-free both ways);
+//   3. pass L: lane k walks z = 0..Z-1 and adds m_l to bin L_z; pass U adds
+//      m_u to bin U_z, on its own column sProj[bin][k] (pitch 64: a lane's
+//      bin never conflicts with another lane's).  L and U are monotone in z
+//      for a valid support, so pass L keeps the running bin sum in a register
+//      (each step stores the partial; the last store of a run is the sum) and
+//      pass U reads a bin's pass-L value only when a new run starts — those
+//      reads are issued 8 atoms ahead, which is exact because a new U bin has
+//      not yet been written by pass U.  A lane whose row turns out not to be
+//      monotone redoes both passes as plain read-modify-writes;
+//   4. the wave gathers log_p rows the same way, lane k folds its loss.
+// HBM reads are whole contiguous 4Z-byte row segments; every other access is
+// LDS.  One wave = one workgroup, 2·65·Z·4 ≈ 26 KB of LDS (6 per CU).
+constexpr int kC51LaneRows = 64;
+
+// Z atoms at compile time (the gather's (row, atom) split is a multiply-shift,
+// the atom loops unroll into independent chains).  POW2: Δz is a power of two
+// (±200 or ±100 over 51 atoms: 8 or 4), so (tz − v_min)/Δz is the exact
+// product with 1/Δz and the f32 division sequence is skipped.
+template <int Z, bool POW2>
+__global__ __launch_bounds__(64) void c51_lane_kernel(
+    const float *__restrict__ qno, const float *__restrict__ tdist, const float *__restrict__ logp,
+    const int64_t *__restrict__ act, const float *__restrict__ rew, const float *__restrict__ dn,
+    const float *__restrict__ support, int64_t B, int A, float vmin, float vmax, float dz, float inv_dz,
+    float g, float *__restrict__ loss, float *__restrict__ proj) {
+    static_assert(Z >= 2 && Z <= 64, "one lane per atom of the support");
+    __shared__ float sP[Z * 65];     // target probabilities, later log_p, [z][row]
+    __shared__ float sProj[Z * 64];  // projection [bin][row]
+    const int lane = threadIdx.x;
+    const int64_t row0 = (int64_t)blockIdx.x * kC51LaneRows;
+    const int nrows = (int)(B - row0 < kC51LaneRows ? B - row0 : kC51LaneRows);
+    const bool live = lane < nrows;
+    const int64_t i = row0 + (live ? lane : nrows - 1);  // dead lanes shadow the last row
+    const int a_cur = (int)act[i];
+    const float r = rew[i];
+    const float kk = (1.0f - dn[i]) * g;
+    const float *qr = qno + i * A;
+    float bv = qr[0];
+    int astar = 0;
+    for (int a = 1; a < A; ++a) {  // first maximum
+        const float q = qr[a];
+        if (q > bv) {
+            bv = q;
+            astar = a;
+        }
+    }
+    const float supv = lane < Z ? support[lane] : 0.f;
+    float4 *p4 = reinterpret_cast<float4 *>(sProj);
+#pragma unroll
+    for (int e = lane; e < Z * 16; e += 64) p4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // Gather the 64 selected rows (row index per lane: sel) of a [B][A][Z]
+    // array: buffer loads on a descriptor over this wave's 64·A·Z block (rows
+    // past B read as 0), all Z loads of both gathers in flight together.
+    // Element lane + 64 j is atom z of row rk, in flattened (row, atom) order.
+    const uint32_t blk = (uint32_t)(A * Z * 4);
+    auto gather = [&](const float *__restrict__ src, int sel, float (&v)[Z]) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(src) + row0 * A * Z, 0,
+                                                          (int)(blk * (uint32_t)nrows), 0x00020000);
+#pragma unroll
+        for (int j = 0; j < Z; ++j) {
+            const int e = lane + 64 * j, rk = e / Z, z = e - rk * Z;
+            const int srow = __shfl(sel, rk & 63, 64);
+            const uint32_t off = (uint32_t)rk * blk + (uint32_t)((srow * Z + z) * 4);
+            v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+    };
+    auto to_lds = [&](const float (&v)[Z]) {
+#pragma unroll
+        for (int j = 0; j < Z; ++j) {
+            const int e = lane + 64 * j, rk = e / Z, z = e - rk * Z;
+            sP[z * 65 + rk] = v[j];
+        }
+    };
+    float vl[Z];
+    {
+        float vt[Z];
+        gather(tdist, astar, vt);
+        to_lds(vt);
+    }
+    gather(logp, a_cur, vl);  // in flight during the two passes
+    __syncthreads();
+    auto atom = [&](int z, int &L, int &U, float &b) {
+        const float sup = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, supv), z));
+        float tz = r + kk * sup;
+        tz = fminf(fmaxf(tz, vmin), vmax);  // clamp(min=vmin, max=vmax)
+        b = POW2 ? (tz - vmin) * inv_dz : (tz - vmin) / dz;
+        L = (int)floorf(b);
+        U = (int)ceilf(b);
+        if (U > 0 && U == L) L -= 1;
+        if (Z - 1 > L && U == L) U += 1;
+        L = L < 0 ? 0 : (L > Z - 1 ? Z - 1 : L);  // guard (never taken for valid inputs)
+        U = U < 0 ? 0 : (U > Z - 1 ? Z - 1 : U);
+    };
+    // pass L: runs of equal L are consecutive; store every partial.  The
+    // upper masses and bins stay in registers for pass U.
+    bool mono = true;
+    float mu[Z];
+    uint32_t ub4[(Z + 3) / 4] = {};  // U bins, 8 bits each
+    {
+        int prev = -1;
+        float acc = 0.f;
+#pragma unroll
+        for (int z = 0; z < Z; ++z) {
+            int L, U;
+            float b;
+            atom(z, L, U, b);
+            ub4[z / 4] |= (uint32_t)U << (8 * (z % 4));
+            const float p = sP[z * 65 + lane];
+            const float ml = p * ((float)U - b);
+            mu[z] = p * (b - (float)L);
+            mono = mono && L >= prev;
+            acc = (L == prev ? acc : 0.f) + ml;
+            sProj[L * 64 + lane] = acc;
+            prev = L;
+        }
+    }
+    // pass U: a run's first atom starts from the bin's pass-L value (read 8
+    // atoms ahead: a new U bin has not been written by pass U yet)
+    {
+        int prev = -1;
+        float acc = 0.f;
+#pragma unroll
+        for (int z0 = 0; z0 < Z; z0 += 8) {
+            float base[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (z0 + j < Z) base[j] = sProj[(int)((ub4[(z0 + j) / 4] >> (8 * ((z0 + j) % 4))) & 255u) * 64 + lane];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (z0 + j < Z) {
+                    const int U = (int)((ub4[(z0 + j) / 4] >> (8 * ((z0 + j) % 4))) & 255u);
+                    mono = mono && U >= prev;
+                    acc = (U == prev ? acc : base[j]) + mu[z0 + j];
+                    sProj[U * 64 + lane] = acc;
+                    prev = U;
+                }
+            }
+        }
+    }
+    if (!mono) {  // never for a sorted support and gamma >= 0: plain ordered read-modify-writes
+        for (int bin = 0; bin < Z; ++bin) sProj[bin * 64 + lane] = 0.f;
+        for (int z = 0; z < Z; ++z) {
+            int L, U;
+            float b;
+            atom(z, L, U, b);
+            sProj[L * 64 + lane] += sP[z * 65 + lane] * ((float)U - b);
+        }
+        for (int z = 0; z < Z; ++z) {
+            int L, U;
+            float b;
+            atom(z, L, U, b);
+            sProj[U * 64 + lane] += sP[z * 65 + lane] * (b - (float)L);
+        }
+    }
+    __syncthreads();
+    to_lds(vl);
+    __syncthreads();
+    float part = 0.f;
+#pragma unroll
+    for (int bin = 0; bin < Z; ++bin) part += sProj[bin * 64 + lane] * sP[bin * 65 + lane];
+    if (live) loss[i] = -part;
+    if (proj) {  // optional projection output, coalesced over (row, bin)
+        for (int e = lane; e < nrows * Z; e += 64) {
+            const int rk = e / Z, z = e - rk * Z;
+            proj[(size_t)row0 * Z + e] = sProj[z * 64 + rk];
+        }
     }
 }
 
@@ -445,6 +636,17 @@ extern "C" int agx_c51_project_loss(const float *q_next_online, const float *tar
                 kC51MaxZ);
     if (B == 0) return AGX_OK;
     const float dz = (float)((v_max - v_min) / (double)(Z - 1));  // python float -> f32 operand
+    if (Z == 51 && A <= 64) {  // Rainbow's 51 atoms
+        int e2 = 0;
+        const double m = std::frexp((v_max - v_min) / (double)(Z - 1), &e2);
+        const bool pow2 = m == 0.5 && (double)dz == std::ldexp(1.0, e2 - 1) && e2 > -60 && e2 < 60;
+        const float inv = pow2 ? (float)std::ldexp(1.0, 1 - e2) : 0.f;
+        auto kern = pow2 ? c51_lane_kernel<51, true> : c51_lane_kernel<51, false>;
+        kern<<<(unsigned)ceil_div(B, kC51LaneRows), 64, 0, as_stream(stream)>>>(
+            q_next_online, target_dist, logp_cur, actions, rewards, dones, support, B, (int)A, (float)v_min,
+            (float)v_max, dz, inv, (float)gamma, loss, proj);
+        return check_launch("agx_c51_project_loss");
+    }
     if (Z <= 64 && A <= 64) {
         constexpr int R = 4;
         const int64_t rows_per_block = (int64_t)kC51RowWaves * R;

@@ -274,6 +274,26 @@ def test_c51_large_vs_c_oracle():
     np.testing.assert_allclose(loss.cpu().numpy(), eloss, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("vmin,vmax,gamma,Z", [(-10.0, 10.0, 0.99 ** 3, 51),   # Δz = 0.4: division path
+                                                 (-200.0, 200.0, -0.9, 51),       # L/U decreasing: RMW fallback
+                                                 (-100.0, 100.0, 0.99, 41)])      # other Z: row-wave kernel
+def test_c51_paths_vs_c_oracle(vmin, vmax, gamma, Z):
+    rng = np.random.default_rng(11)
+    B, A = 700, 5
+    support = torch.linspace(vmin, vmax, Z).numpy()
+    q = rng.standard_normal((B, A)).astype(np.float32)
+    td = torch.softmax(torch.randn(B, A, Z), -1).clamp(min=1e-3).numpy()
+    lp = torch.log_softmax(torch.randn(B, A, Z), -1).numpy()
+    a = rng.integers(0, A, B).astype(np.int64)
+    r = (rng.standard_normal(B) * (vmax - vmin) / 6).astype(np.float32)
+    d = (rng.random(B) < 0.1).astype(np.float32)
+    loss, proj = K().c51_project_loss(T(q), T(td), T(lp), T(a), T(r), T(d), T(support), vmin, vmax, gamma,
+                                      with_proj=True)
+    eloss, eproj = cref.c51(q, td, lp, a, r, d, support, vmin, vmax, gamma)
+    assert np.array_equal(proj.cpu().numpy(), eproj)
+    np.testing.assert_allclose(loss.cpu().numpy(), eloss, rtol=1e-5, atol=1e-5)
+
+
 # --------------------------------------------------------------------------- #
 # optimiser                                                                   #
 # --------------------------------------------------------------------------- #
