@@ -39,6 +39,15 @@ SIGNATURES = {
     "agx_ppo_act": (_INT, [_P, _I, _I, _P, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P, _I,
                            _P, _P, _P]),
     "agx_ppo_rollout_step": (_INT, [_P, _I, _I, _P, _P, _INT, _INT, ctypes.c_uint64, ctypes.c_uint64, _P]),
+    "agx_rollout_workgroups": (_I, [_I, _I]),
+    "agx_rollout_ctl_bytes": (_SZ, [_I, _I]),
+    "agx_rollout_args_bytes": (_SZ, [_I]),
+    "agx_ppo_rollout_persistent": (_INT, [_P, _I, _I, _P, _P, _I, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                          _P, _P, _D, _P]),
+    "agx_host_alloc": (_P, [_SZ]),
+    "agx_host_free": (_INT, [_P]),
+    "agx_host_signal": (_INT, [_P, ctypes.c_uint32]),
+    "agx_host_wait": (_INT, [_P, _I, ctypes.c_uint32, _D]),
     "agx_per_workspace_bytes": (_SZ, [_I, _I]),
     "agx_per_init": (_INT, [_P, _P, _I, _P]),
     "agx_per_add": (_INT, [_P, _P, _I, _I, _I, _I, _D, _P, _P, _P]),

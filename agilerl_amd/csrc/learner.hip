@@ -1279,18 +1279,47 @@ struct ActArgs {
     long long *episodes;  // [P*N] finished-episode count
 };
 
+// The env staging may be host memory that the host rewrites between the
+// steps of one persistent launch: read it with system-scope loads, which
+// bypass the vector L1 and the L2 (both may hold the previous step's lines).
+__device__ __forceinline__ float ld_sys(const float *p) {
+    return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned char ld_sys_u8(const unsigned char *p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const unsigned w = __hip_atomic_load(reinterpret_cast<unsigned *>(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+    return (unsigned char)(w >> (8 * (a & 3)));
+}
+
+// One policy step of workgroup (p, n0).  resident: the parameters (and the
+// zeroed padding of the parameter region) are already in LDS from an earlier
+// step of the same persistent launch; only the activations are re-zeroed.
 template <class C>
-__global__ __launch_bounds__(kNT, 1) void ppo_act_kernel(ActArgs g) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
+__device__ __forceinline__ void act_body(const ActArgs &g, float *sm, bool resident) {
     constexpr LearnPlan pl = C::plan;
     const int p = blockIdx.y, n0 = blockIdx.x * kSB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nrow = g.N - n0 < kSB ? g.N - n0 : kSB;
-    if (g.st_rew && tid < nrow) {  // reward/done of the previous step -> slot t-1, episode accounting
+    // every host read of the step is issued up front (one round trip)
+    const float *ob = g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * pl.D;
+    constexpr int kObsIt = (kSB * pl.D + kNT - 1) / kNT;
+    float obv[kObsIt];
+#pragma unroll
+    for (int k = 0; k < kObsIt; ++k) {
+        const int i = tid + k * kNT;
+        obv[k] = i < nrow * pl.D ? ld_sys(ob + i) : 0.f;
+    }
+    const bool prev = g.st_rew && tid < nrow;
+    const size_t idx = (size_t)p * g.N + n0 + tid;
+    float rw = 0.f;
+    unsigned char dn = 0;
+    if (prev) {
+        rw = ld_sys(g.st_rew + idx);
+        dn = ld_sys_u8(g.st_done + idx);
+    }
+    if (prev) {  // reward/done of the previous step -> slot t-1, episode accounting
         const int env = n0 + tid;
-        const size_t idx = (size_t)p * g.N + env;
-        const float rw = g.st_rew[idx];
-        const unsigned char dn = g.st_done[idx];
         g.rew_prev[(size_t)p * g.prev_pstride + env] = rw;
         g.done_prev[(size_t)p * g.prev_pstride + env] = dn;
         if (g.scores) {
@@ -1303,18 +1332,20 @@ __global__ __launch_bounds__(kNT, 1) void ppo_act_kernel(ActArgs g) {
             g.scores[idx] = sc;
         }
     }
-    const float *ob = g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * pl.D;
     if (g.obs_copy) {
         float *oc = g.obs_copy + (size_t)p * g.obs_copy_pstride + (size_t)n0 * pl.D;
-        for (int i = tid; i < nrow * pl.D; i += kNT) oc[i] = ob[i];
+#pragma unroll
+        for (int k = 0; k < kObsIt; ++k)
+            if (tid + k * kNT < nrow * pl.D) oc[tid + k * kNT] = obv[k];
     }
     if (!g.act) return;
-    for (int i = tid; i < pl.act_floats; i += kNT) sm[i] = 0.f;
+    for (int i = resident ? pl.param_end + tid : tid; i < pl.act_floats; i += kNT) sm[i] = 0.f;
     __syncthreads();
-    load_params<C>(sm, g.params + (size_t)p * pl.n, tid);
-    for (int i = tid; i < kSB * pl.D; i += kNT) {
-        const int r = i / pl.D, d = i % pl.D;
-        sm[pl.l_x0 + r * pl.ld_x0 + d] = r < nrow ? ob[i] : 0.f;
+    if (!resident) load_params<C>(sm, g.params + (size_t)p * pl.n, tid);
+#pragma unroll
+    for (int k = 0; k < kObsIt; ++k) {
+        const int i = tid + k * kNT;
+        if (i < kSB * pl.D) sm[pl.l_x0 + (i / pl.D) * pl.ld_x0 + i % pl.D] = obv[k];
     }
     __syncthreads();
     Fwd<C> fw{sm};
@@ -1348,7 +1379,75 @@ __global__ __launch_bounds__(kNT, 1) void ppo_act_kernel(ActArgs g) {
         if (g.logp_out) g.logp_out[o] = lgc - lse;
         if (g.ent_out) g.ent_out[o] = H;
         if (g.value_out) g.value_out[o] = sm[pl.l_val + r];
-        if (g.act_flat) g.act_flat[(size_t)p * g.N + n0 + r] = choice;
+        if (g.act_flat)  // host memory: system-scope (write-through) store
+            __hip_atomic_store(g.act_flat + (size_t)p * g.N + n0 + r, (long long)choice, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+template <class C>
+__global__ __launch_bounds__(kNT, 1) void ppo_act_kernel(ActArgs g) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    act_body<C>(g, sm, false);
+}
+
+// Persistent rollout: ONE launch runs all nsteps policy steps of a rollout
+// (agx_ppo_rollout_persistent).  Step t's arguments are read from
+// steps[t] (host memory) while the workgroup waits for the host to publish
+// sequence number base+t+1 in ctl->seq (the env step has written the staging);
+// after the step every thread's host stores are released at system scope and
+// thread 0 writes done[block] = base+t+1 (sequence numbers are offset by the
+// rollout's base so the control block is never reset).  Parameters are loaded into LDS once.
+// The wait is bounded: after timeout_ticks of s_memrealtime (100 MHz) or on
+// ctl->seq == kSeqAbort the workgroup sets ctl->timeout and exits.
+template <class C>
+__global__ __launch_bounds__(kNT, 1) void ppo_rollout_persistent_kernel(const ActArgs *steps, int nsteps,
+                                                                        agx_rollout_ctl *ctl,
+                                                                        unsigned long long timeout_ticks,
+                                                                        unsigned base) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    constexpr LearnPlan pl = C::plan;
+    __shared__ ActArgs s_args;
+    __shared__ int s_go;
+    const int tid = threadIdx.x;
+    const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+    constexpr int kArgWords = (int)(sizeof(ActArgs) / 4);
+    for (int t = 0; t < nsteps; ++t) {
+        if (tid < kArgWords)
+            reinterpret_cast<unsigned *>(&s_args)[tid] = reinterpret_cast<const unsigned *>(steps + t)[tid];
+        if (tid == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            int go = 1;
+            for (;;) {
+                // relaxed: an acquire at system scope would invalidate the
+                // caches on every poll; one invalidate follows the wait
+                const unsigned v = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (v == AGX_ROLLOUT_ABORT) {
+                    go = 0;
+                    break;
+                }
+                if (v >= base + (unsigned)(t + 1)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+                    go = 0;
+                    __hip_atomic_store(&ctl->timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+            s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) return;
+        const ActArgs g = s_args;
+        act_body<C>(g, sm, t > 0 && pl.param_end > 0);
+        // the host-memory stores (actions) are system-scope write-through;
+        // wait for their acknowledgements (no L2 write-back: a release fence
+        // would flush every dirty L2 line per wave)
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_store(reinterpret_cast<unsigned *>(ctl + 1) + blk, base + (unsigned)(t + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1379,6 +1478,8 @@ struct Launcher {
     const LearnPlan *plan;
     void (*learn)(const LearnArgs &, int nblocks, size_t lds, hipStream_t);
     void (*act)(const ActArgs &, dim3 grid, size_t lds, hipStream_t);
+    void (*persist)(const ActArgs *, int, agx_rollout_ctl *, unsigned long long, unsigned, dim3 grid, size_t lds,
+                    hipStream_t);
 };
 
 template <class C>
@@ -1400,6 +1501,18 @@ static void launch_act(const ActArgs &a, dim3 grid, size_t lds, hipStream_t s) {
     ppo_act_kernel<C><<<grid, kNT, lds, s>>>(a);
 }
 
+template <class C>
+static void launch_persist(const ActArgs *steps, int nsteps, agx_rollout_ctl *ctl, unsigned long long ticks,
+                           unsigned base, dim3 grid, size_t lds, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)ppo_rollout_persistent_kernel<C>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+        attr = true;
+    }
+    ppo_rollout_persistent_kernel<C><<<grid, kNT, lds, s>>>(steps, nsteps, ctl, ticks, base);
+}
+
 static bool find_launcher(const agx_ppo_net *net, Launcher &out) {
     if (!net) return false;
 #define AGX_TRY(D_, A_, NE_, E0, E1, E2, HA, HC)                                                      \
@@ -1407,7 +1520,7 @@ static bool find_launcher(const agx_ppo_net *net, Launcher &out) {
         using C = Shape<D_, A_, NE_, E0, E1, E2, HA, HC>;                                             \
         static_assert(C::plan.ok, "instantiated PPO shape must have a valid plan");                   \
         if (dims_match(net, C::dims) && same_layout(net, C::plan)) {                                  \
-            out = Launcher{&C::plan, &launch_learn<C>, &launch_act<C>};                               \
+            out = Launcher{&C::plan, &launch_learn<C>, &launch_act<C>, &launch_persist<C>};                               \
             return true;                                                                              \
         }                                                                                             \
     }
@@ -1602,24 +1715,11 @@ extern "C" int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const f
     return check_launch("agx_ppo_act");
 }
 
-extern "C" int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
-                                    const agx_rollout_io *io, int act, int sample, uint64_t seed,
-                                    uint64_t counter, void *stream) {
-    AGX_REQUIRE(net && io && io->stage_obs && P > 0 && N > 0 && P <= 65535, "agx_ppo_rollout_step: bad arguments");
-    AGX_REQUIRE(!act || params, "agx_ppo_rollout_step: act needs params");
-    AGX_REQUIRE(!io->stage_rew || (io->stage_done && io->rewards_prev && io->dones_prev),
-                "agx_ppo_rollout_step: previous-step scatter needs rewards/dones slots");
-    AGX_REQUIRE(!io->scores || (io->stage_rew && io->return_sum && io->episodes),
-                "agx_ppo_rollout_step: episode accounting needs return_sum, episodes and stage rewards");
-    Launcher L;
-    if (!find_launcher(net, L)) {
-        set_error("agx_ppo_rollout_step: network shape not instantiated");
-        return AGX_EUNSUPPORTED;
-    }
-    ActArgs a;
+static void fill_rollout_args(ActArgs &a, const LearnPlan &pl, int64_t P, int64_t N, const float *params,
+                              const agx_rollout_io *io, int act, int sample, uint64_t seed, uint64_t counter) {
     a.params = params;
     a.obs = io->stage_obs;
-    a.obs_pstride = N * (int64_t)L.plan->D;
+    a.obs_pstride = N * (int64_t)pl.D;
     a.N = (int)N;
     a.P = (int)P;
     a.sample = sample;
@@ -1642,7 +1742,64 @@ extern "C" int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N
     a.scores = io->scores;
     a.ret_sum = io->return_sum;
     a.episodes = reinterpret_cast<long long *>(io->episodes);
+}
+
+static int check_rollout_io(const agx_rollout_io *io, int act, const float *params, const char *who) {
+    AGX_REQUIRE(io && io->stage_obs, "%s: null io / stage_obs", who);
+    AGX_REQUIRE(!act || params, "%s: act needs params", who);
+    AGX_REQUIRE(!io->stage_rew || (io->stage_done && io->rewards_prev && io->dones_prev),
+                "%s: previous-step scatter needs rewards/dones slots", who);
+    AGX_REQUIRE(!io->scores || (io->stage_rew && io->return_sum && io->episodes),
+                "%s: episode accounting needs return_sum, episodes and stage rewards", who);
+    return AGX_OK;
+}
+
+extern "C" int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
+                                    const agx_rollout_io *io, int act, int sample, uint64_t seed,
+                                    uint64_t counter, void *stream) {
+    AGX_REQUIRE(net && io && P > 0 && N > 0 && P <= 65535, "agx_ppo_rollout_step: bad arguments");
+    if (int rc = check_rollout_io(io, act, params, "agx_ppo_rollout_step")) return rc;
+    Launcher L;
+    if (!find_launcher(net, L)) {
+        set_error("agx_ppo_rollout_step: network shape not instantiated");
+        return AGX_EUNSUPPORTED;
+    }
+    ActArgs a;
+    fill_rollout_args(a, *L.plan, P, N, params, io, act, sample, seed, counter);
     dim3 grid((unsigned)ceil_div(N, kSB), (unsigned)P);
     L.act(a, grid, (size_t)L.plan->act_floats * sizeof(float), as_stream(stream));
     return check_launch("agx_ppo_rollout_step");
+}
+
+extern "C" int64_t agx_rollout_workgroups(int64_t P, int64_t N) { return P * ceil_div(N, kSB); }
+extern "C" size_t agx_rollout_ctl_bytes(int64_t P, int64_t N) {
+    return sizeof(agx_rollout_ctl) + (size_t)agx_rollout_workgroups(P, N) * sizeof(uint32_t);
+}
+extern "C" size_t agx_rollout_args_bytes(int64_t nsteps) { return (size_t)nsteps * sizeof(ActArgs); }
+
+extern "C" int agx_ppo_rollout_persistent(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
+                                          const agx_rollout_io *ios, int64_t nsteps, uint32_t base, uint64_t seed,
+                                          uint64_t counter0, void *args_host, agx_rollout_ctl *ctl,
+                                          double timeout_s, void *stream) {
+    AGX_REQUIRE(net && ios && params && args_host && ctl && P > 0 && N > 0 && P <= 65535 && nsteps >= 1,
+                "agx_ppo_rollout_persistent: bad arguments");
+    AGX_REQUIRE((uint64_t)base + (uint64_t)nsteps < AGX_ROLLOUT_ABORT, "agx_ppo_rollout_persistent: base wraps");
+    AGX_REQUIRE(timeout_s > 0 && timeout_s < 3600, "agx_ppo_rollout_persistent: timeout_s out of range");
+    Launcher L;
+    if (!find_launcher(net, L)) {
+        set_error("agx_ppo_rollout_persistent: network shape not instantiated");
+        return AGX_EUNSUPPORTED;
+    }
+    ActArgs *steps = static_cast<ActArgs *>(args_host);
+    for (int64_t t = 0; t < nsteps; ++t) {
+        const bool last = t + 1 == nsteps;
+        if (int rc = check_rollout_io(ios + t, 1, params, "agx_ppo_rollout_persistent")) return rc;
+        fill_rollout_args(steps[t], *L.plan, P, N, params, ios + t, 1, last ? 0 : 1, seed,
+                          last ? 0 : counter0 + 1 + (uint64_t)t);
+    }
+    const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    dim3 grid((unsigned)ceil_div(N, kSB), (unsigned)P);
+    L.persist(steps, (int)nsteps, ctl, ticks, base, grid, (size_t)L.plan->act_floats * sizeof(float),
+              as_stream(stream));
+    return check_launch("agx_ppo_rollout_persistent");
 }

@@ -1,4 +1,5 @@
 // Library-level entry points: error reporting, version, device info.
+#include <chrono>
 #include <cstring>
 
 #include "agx_common.h"
@@ -88,4 +89,55 @@ extern "C" int agx_debug_stream(const void *src, void *dst, int64_t bytes, int m
         agx::stream_kernel<1><<<g, 256, 0, agx::as_stream(stream)>>>(static_cast<const agx::v4f *>(src),
                                                                     static_cast<agx::v4f *>(dst), n4);
     return agx::check_launch("agx_debug_stream");
+}
+
+// ---- coherent host memory and the persistent-rollout handshake (host side) ----
+extern "C" void *agx_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    if (hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        agx::set_error("agx_host_alloc: hipHostMalloc(%zu, coherent) failed", bytes);
+        return nullptr;
+    }
+    std::memset(p, 0, bytes);
+    return p;
+}
+
+extern "C" int agx_host_free(void *ptr) {
+    if (!ptr) return AGX_OK;
+    if (hipHostFree(ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        agx::set_error("agx_host_free: hipHostFree failed");
+        return AGX_EHIP;
+    }
+    return AGX_OK;
+}
+
+extern "C" int agx_host_signal(agx_rollout_ctl *ctl, uint32_t seq) {
+    AGX_REQUIRE(ctl, "agx_host_signal: null ctl");
+    __atomic_store_n(&ctl->seq, seq, __ATOMIC_RELEASE);
+    return AGX_OK;
+}
+
+extern "C" int agx_host_wait(const agx_rollout_ctl *ctl, int64_t nwg, uint32_t target, double timeout_s) {
+    AGX_REQUIRE(ctl && nwg > 0, "agx_host_wait: bad arguments");
+    const uint32_t *done = reinterpret_cast<const uint32_t *>(ctl + 1);
+    const auto t0 = std::chrono::steady_clock::now();
+    int64_t i = 0;
+    for (unsigned spin = 0;; ++spin) {
+        while (i < nwg && __atomic_load_n(done + i, __ATOMIC_ACQUIRE) >= target) ++i;
+        if (i == nwg) return AGX_OK;
+        if (__atomic_load_n(&ctl->timeout, __ATOMIC_RELAXED)) {
+            agx::set_error("agx_host_wait: a rollout workgroup timed out waiting for the host");
+            return AGX_EHIP;
+        }
+        if ((spin & 1023) == 1023 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+            agx::set_error("agx_host_wait: %lld of %lld workgroups not done after %.1f s", (long long)(nwg - i),
+                           (long long)nwg, timeout_s);
+            return AGX_EHIP;
+        }
+        __builtin_ia32_pause();
+    }
 }

@@ -16,6 +16,15 @@ kernel reads / writes directly (zero-copy over the host link: 40 KB in and
 8 KB out per step at config 2), so a step is one launch and one wait; with
 AGX_ZERO_COPY=0 the staging goes through one H2D and one D2H copy instead.
 
+Persistent mode (default; AGX_PERSISTENT_ROLLOUT=0 turns it off): the whole
+rollout is ONE launch (agx_ppo_rollout_persistent) whose workgroups keep the
+parameters in LDS and are paced step by step through a control block in
+coherent host memory — the host releases step t after the env step
+(agx_host_signal) and spins on the workgroups' done words (agx_host_wait),
+so a vector step costs no launch and no event wait.  Staging, actions and
+the control block then live in coherent (fine-grained) host memory, which
+the device re-reads within one launch.
+
 Architectures outside the fused kernels use the plain-PyTorch policy step
 with per-field copies (``_collect_torch``).
 """
@@ -24,7 +33,9 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
+import numpy as np
 import torch
 
 from .. import _lib
@@ -44,11 +55,22 @@ class AgxRolloutIO(ctypes.Structure):
     ]
 
 
-def _packed(P: int, N: int, D: int, **kw):
+def _coherent(owner, nbytes: int) -> torch.Tensor:
+    """uint8 CPU tensor over agx_host_alloc memory (coherent, device-accessible
+    at the same address), freed with its owner."""
+    lib = _lib.load()
+    p = lib.agx_host_alloc(nbytes)
+    if not p:
+        raise _lib.AgxError(lib.agx_last_error().decode(errors="replace"))
+    weakref.finalize(owner, lib.agx_host_free, p)
+    return torch.from_numpy(np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)))
+
+
+def _packed(P: int, N: int, D: int, owner=None, **kw):
     """One byte buffer [obs f32 P*N*D | reward f32 P*N | done u8 P*N] + views."""
     n_obs, n_rew = P * N * D * 4, P * N * 4
     nbytes = (n_obs + n_rew + P * N + 15) // 16 * 16
-    buf = torch.zeros(nbytes, dtype=torch.uint8, **kw)
+    buf = _coherent(owner, nbytes) if owner is not None else torch.zeros(nbytes, dtype=torch.uint8, **kw)
     obs = buf[:n_obs].view(torch.float32).view(P * N, D)
     rew = buf[n_obs:n_obs + n_rew].view(torch.float32)
     done = buf[n_obs + n_rew:n_obs + n_rew + P * N].view(torch.bool)
@@ -62,10 +84,23 @@ class PopulationRunner:
         self.pop, self.env = pop, env
         P, N, D = pop.P, pop.N, pop.spec.obs_dim
         dev = pop.device
-        self.stage_h, self.obs_h, self.rew_h, self.done_h = _packed(P, N, D, pin_memory=True)
+        self.zero_copy = os.environ.get("AGX_ZERO_COPY", "1") != "0"
+        self.persistent = (self.zero_copy and os.environ.get("AGX_PERSISTENT_ROLLOUT", "1") != "0"
+                           and pop.fused_descriptor() is not None)
+        if self.persistent:
+            self.stage_h, self.obs_h, self.rew_h, self.done_h = _packed(P, N, D, owner=self)
+            self.act_h = _coherent(self, P * N * 8).view(torch.int64)
+            lib = _lib.load()
+            self.n_wg = int(lib.agx_rollout_workgroups(P, N))
+            self.ctl_h = _coherent(self, int(lib.agx_rollout_ctl_bytes(P, N)))
+            self.args_h = _coherent(self, int(lib.agx_rollout_args_bytes(pop.T + 1)))
+            self.seq_base = 0
+            self.timeout_s = float(os.environ.get("AGX_ROLLOUT_TIMEOUT", "20"))
+        else:
+            self.stage_h, self.obs_h, self.rew_h, self.done_h = _packed(P, N, D, pin_memory=True)
+            self.act_h = torch.zeros(P * N, dtype=torch.int64, pin_memory=True)
         self.stage_d, self.obs_d, self.rew_d, self.done_d = _packed(P, N, D, device=dev)
         self.term_h = torch.zeros(P * N, dtype=torch.bool, pin_memory=True)
-        self.act_h = torch.zeros(P * N, dtype=torch.int64, pin_memory=True)
         self.act_d = torch.zeros(P * N, dtype=torch.int64, device=dev)
         self.last_obs = torch.zeros(P, N, D, dtype=torch.float32, device=dev)
         self.last_done = torch.zeros(P, N, dtype=torch.uint8, device=dev)
@@ -79,7 +114,6 @@ class PopulationRunner:
         self.ret_sum_env = torch.zeros(P * N, dtype=torch.float64, device=dev)
         self.episodes_env = torch.zeros(P * N, dtype=torch.int64, device=dev)
         self._ios = None
-        self.zero_copy = os.environ.get("AGX_ZERO_COPY", "1") != "0"
 
     # ------------------------------------------------------------------ #
     @property
@@ -99,7 +133,7 @@ class PopulationRunner:
         """agx_rollout_io for every step t = 0..T (t = T: final scatter only)."""
         pop = self.pop
         T, N, D = pop.T, pop.N, pop.spec.obs_dim
-        ios = []
+        ios = (AgxRolloutIO * (T + 1))()
         for t in range(T + 1):
             io = AgxRolloutIO()
             src_obs, src_rew, src_done = ((self.obs_h, self.rew_h, self.done_h) if self.zero_copy
@@ -127,7 +161,7 @@ class PopulationRunner:
                 io.values = self.last_value.data_ptr()
                 io.slot_agent_stride = N
             io.prev_agent_stride = T * N
-            ios.append(io)
+            ios[t] = io
         self._ios = ios
 
     def _env_step(self) -> None:
@@ -151,6 +185,8 @@ class PopulationRunner:
             if not self.zero_copy:
                 self.stage_d.copy_(self.stage_h, non_blocking=True)
             self.started = True
+        if self.persistent:
+            return self._collect_persistent(desc)
         lib = _lib.load()
         fn = lib.agx_ppo_rollout_step
         dref = ctypes.byref(desc)
@@ -170,6 +206,39 @@ class PopulationRunner:
         # reward/done of the last step -> slot T-1; final obs -> last_obs + bootstrap value
         _lib.check(fn(dref, P, N, params, ctypes.byref(self._ios[T]), 1, 0, pop.act_seed, 0, s),
                    "agx_ppo_rollout_step")
+        self.last_value_valid = True
+        self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)  # last_done = term (:196)
+        self.env_steps += P * N * T
+
+    def _collect_persistent(self, desc) -> None:
+        """One launch for the whole rollout; the host paces it step by step."""
+        pop = self.pop
+        P, N, T = pop.P, pop.N, pop.T
+        lib = _lib.load()
+        ctl = self.ctl_h.data_ptr()
+        base = self.seq_base
+        if base + T + 1 >= 0xFFFFFFF0:  # never in practice: 2^32 / (T + 1) rollouts
+            torch.cuda.current_stream().synchronize()
+            self.ctl_h.zero_()
+            base = 0
+        _lib.check(lib.agx_ppo_rollout_persistent(ctypes.byref(desc), P, N, pop.params.data.data_ptr(), self._ios,
+                                                  T + 1, base, pop.act_seed, pop.act_counter,
+                                                  self.args_h.data_ptr(), ctl, self.timeout_s, _lib.stream()),
+                   "agx_ppo_rollout_persistent")
+        self.seq_base = base + T + 1
+        try:
+            for t in range(T):
+                lib.agx_host_signal(ctl, base + t + 1)
+                _lib.check(lib.agx_host_wait(ctl, self.n_wg, base + t + 1, self.timeout_s), "agx_host_wait")
+                self._env_step()
+            lib.agx_host_signal(ctl, base + T + 1)  # reward/done of step T-1, final obs, bootstrap value
+        except BaseException:
+            lib.agx_host_signal(ctl, 0xFFFFFFFF)  # release the workgroups, then reset the block
+            torch.cuda.current_stream().synchronize()
+            self.ctl_h.zero_()
+            self.seq_base = 0
+            raise
+        pop.act_counter += T
         self.last_value_valid = True
         self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)  # last_done = term (:196)
         self.env_steps += P * N * T

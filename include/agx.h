@@ -175,6 +175,46 @@ int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N, const flo
                          const agx_rollout_io *io, int act, int sample, uint64_t seed,
                          uint64_t counter, void *stream);
 
+/* Persistent rollout: ONE launch runs a whole rollout of nsteps = T + 1
+ * agx_ppo_rollout_step calls (ios[0..T]; steps 0..T-1 sample with Philox
+ * counters counter0 + 1 + t, step T is the bootstrap step: act, no sample),
+ * paced by the host through a control block in coherent host memory
+ * (agx_host_alloc):
+ *   host:   env step writes the staging  ->  agx_host_signal(ctl, base + t + 1)
+ *           -> agx_host_wait(ctl, nwg, base + t + 1) -> actions_flat is ready;
+ *   device: each workgroup waits for ctl->seq >= base + t + 1, runs step t
+ *           with the parameters resident in LDS, releases its host stores and
+ *           sets its done word (uint32 after the header) to base + t + 1.
+ * `base` grows by nsteps per rollout, so the block is never reset.  Replaces
+ * the per-step launch + event wait of rollouts/on_policy.py:23-203's loop.
+ * args_host: agx_rollout_args_bytes(nsteps) of agx_host_alloc memory (the
+ * per-step arguments, read by the device as the host releases each step).
+ * A workgroup gives up after timeout_s or on seq == AGX_ROLLOUT_ABORT and
+ * sets ctl->timeout. */
+#define AGX_ROLLOUT_ABORT 0xffffffffu
+typedef struct agx_rollout_ctl {
+    uint32_t seq;     /* host -> device: last released step (base + t + 1) */
+    uint32_t timeout; /* device -> host: a workgroup stopped waiting       */
+    uint32_t reserved[2];
+    /* followed by agx_rollout_workgroups(P, N) uint32 done words */
+} agx_rollout_ctl;
+int64_t agx_rollout_workgroups(int64_t P, int64_t N);
+size_t agx_rollout_ctl_bytes(int64_t P, int64_t N);
+size_t agx_rollout_args_bytes(int64_t nsteps);
+int agx_ppo_rollout_persistent(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
+                               const agx_rollout_io *ios, int64_t nsteps, uint32_t base, uint64_t seed,
+                               uint64_t counter0, void *args_host, agx_rollout_ctl *ctl, double timeout_s,
+                               void *stream);
+/* Coherent (fine-grained) pinned host memory, device-accessible at the same
+ * address; NULL on failure. */
+void *agx_host_alloc(size_t bytes);
+int agx_host_free(void *ptr);
+/* release-store ctl->seq = seq */
+int agx_host_signal(agx_rollout_ctl *ctl, uint32_t seq);
+/* spin until every done word >= target; AGX_EHIP on ctl->timeout or after
+ * timeout_s */
+int agx_host_wait(const agx_rollout_ctl *ctl, int64_t nwg, uint32_t target, double timeout_s);
+
 /* ---- prioritized replay segment trees -----------------------------------
  * Replaces SumSegmentTree / MinSegmentTree (agilerl/components/
  * segment_tree.py) and the priority half of PrioritizedReplayBuffer

@@ -293,3 +293,64 @@ def test_collect_episode_accounting():
     np.testing.assert_array_equal(runner.episodes.cpu().numpy(), eps.sum(1))
     np.testing.assert_allclose(runner.episode_return_sum.cpu().numpy(), ret.sum(1), rtol=1e-6)
     np.testing.assert_allclose(runner.scores.view(P, N).cpu().numpy(), score, rtol=1e-6, atol=1e-6)
+
+
+def _runner_pair(monkeypatch, persistent, P=3, N=40, seed=5):
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+    from agilerl_amd.population.runner import PopulationRunner
+
+    monkeypatch.setenv("AGX_PERSISTENT_ROLLOUT", "1" if persistent else "0")
+    spec = ActorCriticSpec(obs_dim=8, n_actions=4)
+    pop = PPOPopulation(spec, P, N, learn_step=8 * N, batch_size=64, update_epochs=2, device=DEV,
+                        seeds=list(range(P)), fused=True)
+    runner = PopulationRunner(pop, SyntheticVecEnv(P * N, seed=seed, p_done=0.2))
+    assert runner.persistent == persistent
+    return pop, runner
+
+
+def test_persistent_rollout_matches_per_step_launches(monkeypatch):
+    """ONE persistent launch per rollout (host-paced through the coherent
+    control block) produces bit-identical rollouts, bootstrap values, episode
+    statistics and — after learn() — parameters to one launch per step."""
+    a_pop, a_run = _runner_pair(monkeypatch, True)
+    b_pop, b_run = _runner_pair(monkeypatch, False)
+    for _ in range(3):
+        for run in (a_run, b_run):
+            run.iteration()
+        torch.cuda.synchronize()
+        for name in ("obs", "actions", "log_probs", "values", "rewards", "dones", "advantages", "returns"):
+            assert torch.equal(getattr(a_pop, name), getattr(b_pop, name)), name
+        assert torch.equal(a_run.last_value, b_run.last_value)
+        assert torch.equal(a_run.last_done, b_run.last_done)
+        assert torch.equal(a_run.episodes, b_run.episodes)
+        assert torch.equal(a_run.episode_return_sum, b_run.episode_return_sum)
+        assert torch.equal(a_pop.params.data, b_pop.params.data)
+    assert a_pop.act_counter == b_pop.act_counter
+    assert int(a_run.ctl_h.view(torch.int32)[1]) == 0  # no workgroup timed out
+
+
+def test_persistent_rollout_abort_releases_kernel(monkeypatch):
+    """An env that raises mid-rollout: the runner releases the waiting
+    workgroups (abort sequence), re-arms the control block, and the next
+    collect() runs normally."""
+    pop, run = _runner_pair(monkeypatch, True)
+    run.collect()
+    real = run._env_step
+    calls = {"n": 0}
+
+    def flaky():
+        calls["n"] += 1
+        if calls["n"] == 3:
+            raise RuntimeError("env worker died")
+        real()
+
+    run._env_step = flaky
+    with pytest.raises(RuntimeError, match="env worker died"):
+        run.collect()
+    run._env_step = real
+    run.collect()
+    torch.cuda.synchronize()
+    assert run.seq_base == pop.T + 1
+    assert int(pop.actions.min()) >= 0 and int(pop.actions.max()) < 4
