@@ -11,6 +11,16 @@
 
 namespace agx {
 
+// persistent-rollout control block (agx.h agx_rollout_ctl): header, nwg done
+// words, then one 64-byte release line per workgroup
+__host__ __device__ inline unsigned *rollout_done_words(void *ctl) { return static_cast<unsigned *>(ctl) + 4; }
+__host__ __device__ inline unsigned rollout_release_offset(unsigned nwg, unsigned w) {  // in words
+    return ((4 + nwg + 15) / 16 + w) * 16;
+}
+__host__ __device__ inline unsigned *rollout_release_word(void *ctl, unsigned nwg, unsigned w) {
+    return static_cast<unsigned *>(ctl) + rollout_release_offset(nwg, w);
+}
+
 // thread-local last error (agx_last_error)
 void set_error(const char *fmt, ...);
 

@@ -1295,8 +1295,10 @@ __device__ __forceinline__ unsigned char ld_sys_u8(const unsigned char *p) {
 // One policy step of workgroup (p, n0).  resident: the parameters (and the
 // zeroed padding of the parameter region) are already in LDS from an earlier
 // step of the same persistent launch; only the activations are re-zeroed.
+// st (diagnostic, may be null): s_memrealtime after the host reads landed,
+// after the forward, after the outputs were issued (thread 0 only)
 template <class C>
-__device__ __forceinline__ void act_body(const ActArgs &g, float *sm, bool resident) {
+__device__ __forceinline__ void act_body(const ActArgs &g, float *sm, bool resident, long long *st = nullptr) {
     constexpr LearnPlan pl = C::plan;
     const int p = blockIdx.y, n0 = blockIdx.x * kSB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1317,6 +1319,10 @@ __device__ __forceinline__ void act_body(const ActArgs &g, float *sm, bool resid
     if (prev) {
         rw = ld_sys(g.st_rew + idx);
         dn = ld_sys_u8(g.st_done + idx);
+    }
+    if (st && tid == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        st[0] = (long long)__builtin_amdgcn_s_memrealtime() + (long long)(obv[0] != obv[0]);
     }
     if (prev) {  // reward/done of the previous step -> slot t-1, episode accounting
         const int env = n0 + tid;
@@ -1350,6 +1356,7 @@ __device__ __forceinline__ void act_body(const ActArgs &g, float *sm, bool resid
     __syncthreads();
     Fwd<C> fw{sm};
     fw.run();
+    if (st && tid == 0) st[1] = (long long)__builtin_amdgcn_s_memrealtime();
     // categorical over 16 lanes per row
     const int r = wave + kNW * (lane >> 4), a = lane & 15;
     const bool live = r < nrow;
@@ -1383,6 +1390,7 @@ __device__ __forceinline__ void act_body(const ActArgs &g, float *sm, bool resid
             __hip_atomic_store(g.act_flat + (size_t)p * g.N + n0 + r, (long long)choice, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (st && tid == 0) st[2] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 template <class C>
@@ -1404,15 +1412,18 @@ template <class C>
 __global__ __launch_bounds__(kNT, 1) void ppo_rollout_persistent_kernel(const ActArgs *steps, int nsteps,
                                                                         agx_rollout_ctl *ctl,
                                                                         unsigned long long timeout_ticks,
-                                                                        unsigned base) {
+                                                                        unsigned base, long long *stamps) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     constexpr LearnPlan pl = C::plan;
     __shared__ ActArgs s_args;
     __shared__ int s_go;
     const int tid = threadIdx.x;
     const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+    unsigned *rel = rollout_release_word(ctl, gridDim.x * gridDim.y, blk);  // this workgroup's own line
     constexpr int kArgWords = (int)(sizeof(ActArgs) / 4);
     for (int t = 0; t < nsteps; ++t) {
+        long long *st = stamps && blk == 0 && t < 32 ? stamps + 8 * t : nullptr;
+        if (st && tid == 0) st[0] = (long long)__builtin_amdgcn_s_memrealtime();
         if (tid < kArgWords)
             reinterpret_cast<unsigned *>(&s_args)[tid] = reinterpret_cast<const unsigned *>(steps + t)[tid];
         if (tid == 0) {
@@ -1421,7 +1432,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_rollout_persistent_kernel(const Ac
             for (;;) {
                 // relaxed: an acquire at system scope would invalidate the
                 // caches on every poll; one invalidate follows the wait
-                const unsigned v = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const unsigned v = __hip_atomic_load(rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (v == AGX_ROLLOUT_ABORT) {
                     go = 0;
                     break;
@@ -1432,21 +1443,25 @@ __global__ __launch_bounds__(kNT, 1) void ppo_rollout_persistent_kernel(const Ac
                     __hip_atomic_store(&ctl->timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(8);
+                __builtin_amdgcn_s_sleep(2);
             }
             s_go = go;
+            if (st) st[1] = (long long)__builtin_amdgcn_s_memrealtime();
+            if (stamps && t == 5 && blk < 64) stamps[256 + blk] = (long long)__builtin_amdgcn_s_memrealtime();
         }
         __syncthreads();
         if (!s_go) return;
         const ActArgs g = s_args;
-        act_body<C>(g, sm, t > 0 && pl.param_end > 0);
+        act_body<C>(g, sm, t > 0 && pl.param_end > 0, st ? st + 2 : nullptr);
         // the host-memory stores (actions) are system-scope write-through;
         // wait for their acknowledgements (no L2 write-back: a release fence
         // would flush every dirty L2 line per wave)
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
+        if (st && tid == 0) st[5] = (long long)__builtin_amdgcn_s_memrealtime();
+        if (stamps && tid == 0 && t == 5 && blk < 64) stamps[320 + blk] = (long long)__builtin_amdgcn_s_memrealtime();
         if (tid == 0)
-            __hip_atomic_store(reinterpret_cast<unsigned *>(ctl + 1) + blk, base + (unsigned)(t + 1), __ATOMIC_RELAXED,
+            __hip_atomic_store(rollout_done_words(ctl) + blk, base + (unsigned)(t + 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -1478,8 +1493,8 @@ struct Launcher {
     const LearnPlan *plan;
     void (*learn)(const LearnArgs &, int nblocks, size_t lds, hipStream_t);
     void (*act)(const ActArgs &, dim3 grid, size_t lds, hipStream_t);
-    void (*persist)(const ActArgs *, int, agx_rollout_ctl *, unsigned long long, unsigned, dim3 grid, size_t lds,
-                    hipStream_t);
+    void (*persist)(const ActArgs *, int, agx_rollout_ctl *, unsigned long long, unsigned, long long *, dim3 grid,
+                    size_t lds, hipStream_t);
 };
 
 template <class C>
@@ -1503,14 +1518,14 @@ static void launch_act(const ActArgs &a, dim3 grid, size_t lds, hipStream_t s) {
 
 template <class C>
 static void launch_persist(const ActArgs *steps, int nsteps, agx_rollout_ctl *ctl, unsigned long long ticks,
-                           unsigned base, dim3 grid, size_t lds, hipStream_t s) {
+                           unsigned base, long long *stamps, dim3 grid, size_t lds, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)ppo_rollout_persistent_kernel<C>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         attr = true;
     }
-    ppo_rollout_persistent_kernel<C><<<grid, kNT, lds, s>>>(steps, nsteps, ctl, ticks, base);
+    ppo_rollout_persistent_kernel<C><<<grid, kNT, lds, s>>>(steps, nsteps, ctl, ticks, base, stamps);
 }
 
 static bool find_launcher(const agx_ppo_net *net, Launcher &out) {
@@ -1773,7 +1788,8 @@ extern "C" int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N
 
 extern "C" int64_t agx_rollout_workgroups(int64_t P, int64_t N) { return P * ceil_div(N, kSB); }
 extern "C" size_t agx_rollout_ctl_bytes(int64_t P, int64_t N) {
-    return sizeof(agx_rollout_ctl) + (size_t)agx_rollout_workgroups(P, N) * sizeof(uint32_t);
+    const unsigned nwg = (unsigned)agx_rollout_workgroups(P, N);
+    return (size_t)rollout_release_offset(nwg, nwg) * sizeof(unsigned);
 }
 extern "C" size_t agx_rollout_args_bytes(int64_t nsteps) { return (size_t)nsteps * sizeof(ActArgs); }
 
@@ -1798,8 +1814,9 @@ extern "C" int agx_ppo_rollout_persistent(const agx_ppo_net *net, int64_t P, int
                           last ? 0 : counter0 + 1 + (uint64_t)t);
     }
     const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    ctl->nwg = (uint32_t)agx_rollout_workgroups(P, N);
     dim3 grid((unsigned)ceil_div(N, kSB), (unsigned)P);
-    L.persist(steps, (int)nsteps, ctl, ticks, base, grid, (size_t)L.plan->act_floats * sizeof(float),
+    L.persist(steps, (int)nsteps, ctl, ticks, base, g_stamps_ptr(), grid, (size_t)L.plan->act_floats * sizeof(float),
               as_stream(stream));
     return check_launch("agx_ppo_rollout_persistent");
 }

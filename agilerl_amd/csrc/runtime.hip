@@ -116,13 +116,15 @@ extern "C" int agx_host_free(void *ptr) {
 
 extern "C" int agx_host_signal(agx_rollout_ctl *ctl, uint32_t seq) {
     AGX_REQUIRE(ctl, "agx_host_signal: null ctl");
+    const unsigned nwg = __atomic_load_n(&ctl->nwg, __ATOMIC_RELAXED);
+    for (unsigned w = 0; w < nwg; ++w) __atomic_store_n(agx::rollout_release_word(ctl, nwg, w), seq, __ATOMIC_RELEASE);
     __atomic_store_n(&ctl->seq, seq, __ATOMIC_RELEASE);
     return AGX_OK;
 }
 
 extern "C" int agx_host_wait(const agx_rollout_ctl *ctl, int64_t nwg, uint32_t target, double timeout_s) {
     AGX_REQUIRE(ctl && nwg > 0, "agx_host_wait: bad arguments");
-    const uint32_t *done = reinterpret_cast<const uint32_t *>(ctl + 1);
+    const uint32_t *done = agx::rollout_done_words(const_cast<agx_rollout_ctl *>(ctl));
     const auto t0 = std::chrono::steady_clock::now();
     int64_t i = 0;
     for (unsigned spin = 0;; ++spin) {

@@ -195,8 +195,10 @@ int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N, const flo
 typedef struct agx_rollout_ctl {
     uint32_t seq;     /* host -> device: last released step (base + t + 1) */
     uint32_t timeout; /* device -> host: a workgroup stopped waiting       */
-    uint32_t reserved[2];
-    /* followed by agx_rollout_workgroups(P, N) uint32 done words */
+    uint32_t nwg;     /* workgroups (set by agx_ppo_rollout_persistent)    */
+    uint32_t reserved;
+    /* followed by nwg uint32 done words, then (64-byte aligned) one 64-byte
+     * release line per workgroup: each workgroup polls its own copy of seq */
 } agx_rollout_ctl;
 int64_t agx_rollout_workgroups(int64_t P, int64_t N);
 size_t agx_rollout_ctl_bytes(int64_t P, int64_t N);
@@ -209,7 +211,7 @@ int agx_ppo_rollout_persistent(const agx_ppo_net *net, int64_t P, int64_t N, con
  * address; NULL on failure. */
 void *agx_host_alloc(size_t bytes);
 int agx_host_free(void *ptr);
-/* release-store ctl->seq = seq */
+/* release-store seq into ctl->seq and every workgroup's release line */
 int agx_host_signal(agx_rollout_ctl *ctl, uint32_t seq);
 /* spin until every done word >= target; AGX_EHIP on ctl->timeout or after
  * timeout_s */

@@ -6,6 +6,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from agilerl_amd import _lib  # noqa: E402
@@ -66,3 +67,24 @@ print(f"device step (signal -> all done): median {1e6 * dev_t[len(dev_t) // 2]:.
       f"first step incl. kernel start {1e6 * sum(dev_t[:1]):.1f}")
 print(f"env step {1e6 * sum(env_t) / len(env_t):.1f} us; collect {1e3 * sum(launch_t) / len(launch_t):.3f} ms "
       f"({1e6 * sum(launch_t) / len(launch_t) / T:.1f} us/step)")
+
+# in-kernel phases of workgroup 0 (s_memrealtime, 100 MHz)
+buf = torch.zeros(384, dtype=torch.int64, device="cuda")
+lib.agx_debug_learn_stamps(ctypes.c_void_p(buf.data_ptr()))
+run.collect()
+lib.agx_debug_learn_stamps(None)
+pop.finish_rollout(run.last_obs, run.last_done, run.last_value)
+torch.cuda.synchronize()
+st = buf[:256].view(32, 8).cpu().numpy()[:T + 1].astype(float) * 10.0  # ns
+names = ["wait for host", "host reads", "scatter+zero+forward", "sample+stores", "store acks"]
+ph = [st[1:T, k + 1] - st[1:T, k] for k in range(5)]
+print("in-kernel phases (us, median over steps 1..T-1): " +
+      ", ".join(f"{n} {float(sorted(x)[len(x) // 2]) / 1e3:.2f}" for n, x in zip(names, ph)))
+gap = st[2:T, 1] - st[1:T - 1, 5]
+print(f"done -> next release seen: {float(sorted(gap)[len(gap) // 2]) / 1e3:.2f} us (host detect + env step + signal)")
+nwg = run.n_wg
+b = buf.cpu().numpy().astype(float) * 10.0
+go, dn = b[256:256 + nwg], b[320:320 + nwg]
+print(f"step 5 across {nwg} workgroups: release seen spread {(go.max() - go.min()) / 1e3:.2f} us, "
+      f"done spread {(dn.max() - dn.min()) / 1e3:.2f} us, per-workgroup step median {np.median(dn - go) / 1e3:.2f} "
+      f"max {(dn - go).max() / 1e3:.2f} us")
