@@ -17,6 +17,7 @@ import warnings
 import numpy as np
 
 from ..components.sampler import Sampler
+from ..hpo.sharded import select_population
 
 
 def train_multi_agent_off_policy(env, env_name: str, algo: str, pop, memory, INIT_HP=None, MUT_P=None,
@@ -88,5 +89,5 @@ def train_multi_agent_off_policy(env, env_name: str, algo: str, pop, memory, INI
                 and len(pop[0].steps) >= 100:
             return pop, pop_fitnesses
         if tournament is not None:
-            _, pop = tournament.select(pop)
+            _, pop = select_population(tournament, pop)
     return pop, pop_fitnesses

@@ -21,6 +21,7 @@ import numpy as np
 
 from ..algorithms.dqn import DQN, RainbowDQN
 from ..components.sampler import Sampler
+from ..hpo.sharded import select_population
 
 
 def train_off_policy(env, env_name: str, algo: str, pop, memory, INIT_HP=None, MUT_P=None,
@@ -109,6 +110,7 @@ def train_off_policy(env, env_name: str, algo: str, pop, memory, INIT_HP=None, M
             return pop, pop_fitnesses
         if tournament is not None:
             # the reference selects inside tournament_selection_and_mutation; selection runs here
-            # even without a mutation object (mutations are not applied)
-            _, pop = tournament.select(pop)
+            # even without a mutation object (mutations are not applied); under an
+            # initialised process group each rank holds a shard of the population
+            _, pop = select_population(tournament, pop)
     return pop, pop_fitnesses

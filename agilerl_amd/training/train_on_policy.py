@@ -24,6 +24,7 @@ import time
 import warnings
 
 import numpy as np
+import torch.distributed as dist
 
 from ..hpo.population_sync import PopulationSync
 from ..population.runner import PopulationRunner
@@ -49,7 +50,8 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
     runner = PopulationRunner(population, env)
     sync = None
     if tournament is not None:
-        sync = PopulationSync(population, runner, seed=None, tournament_size=tournament.tournament_size,
+        world, rank = (dist.get_world_size(), dist.get_rank()) if dist.is_initialized() else (1, 0)
+        sync = PopulationSync(population, runner, world, rank, seed=None, tournament_size=tournament.tournament_size,
                               elitism=tournament.elitism, eval_loop=tournament.eval_loop)
     iters_per_gen = max(1, -(-evo_steps // (T * N)))
     pop_fitnesses: list[list[float]] = []
