@@ -13,6 +13,8 @@
 // Two launches: (1) per-(agent, chunk) partial sums of squares per group into
 // the workspace, (2) every block re-reduces its agent's partials in a fixed
 // order (deterministic), derives the clip coefficients and updates its chunk.
+// Rows of more than 16 chunks add a per-agent pre-reduction (1b) so the
+// re-reduction does not grow with the square of the row length.
 // Traffic: 4 arrays read + 3 written = 28 B per parameter (+4 B norm pass).
 #include "agx_common.h"
 
@@ -22,6 +24,7 @@ constexpr int kOptBlock = 256;
 constexpr int kOptPer = 4;  // params per thread per block
 constexpr int kOptChunk = kOptBlock * kOptPer;
 constexpr int kMaxGroups = 8;
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 struct Groups {
     int64_t off[kMaxGroups + 1];
@@ -34,6 +37,9 @@ __device__ __forceinline__ int group_of(const Groups &g, int64_t j) {
     return k;
 }
 
+// (1) per-(agent, chunk) partial sums of squares per group.  V4: one float4
+// per thread (n % 4 == 0, 16-byte aligned rows), else kOptPer strided floats.
+template <bool V4>
 __global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const float *__restrict__ grads, int64_t n,
                                                           Groups gr, double *__restrict__ part) {
     const int p = blockIdx.y;
@@ -42,14 +48,24 @@ __global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const float *__restric
 #pragma unroll
     for (int k = 0; k < kMaxGroups; ++k) acc[k] = 0.0;
     const int64_t j0 = (int64_t)blockIdx.x * kOptChunk;
-    for (int r = 0; r < kOptPer; ++r) {
-        const int64_t j = j0 + r * kOptBlock + threadIdx.x;
-        if (j < n) {
-            const double x = (double)g[j];
-            const int k = group_of(gr, j);
+    auto add = [&](int64_t j, float xf) {
+        const double x = (double)xf;
+        const int k = group_of(gr, j);
 #pragma unroll
-            for (int q = 0; q < kMaxGroups; ++q)
-                if (q == k) acc[q] += x * x;
+        for (int q = 0; q < kMaxGroups; ++q)
+            if (q == k) acc[q] += x * x;
+    };
+    if constexpr (V4) {
+        const int64_t j = j0 + 4 * threadIdx.x;
+        if (j < n) {
+            const f4 x = *reinterpret_cast<const f4 *>(g + j);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) add(j + e, x[e]);
+        }
+    } else {
+        for (int r = 0; r < kOptPer; ++r) {
+            const int64_t j = j0 + r * kOptBlock + threadIdx.x;
+            if (j < n) add(j, g[j]);
         }
     }
     __shared__ double red[kMaxGroups][kOptBlock / kWave];
@@ -66,11 +82,42 @@ __global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const float *__restric
     }
 }
 
+__device__ __forceinline__ float clip_coef(double sumsq, float max_norm) {
+    const float norm = (float)sqrt(sumsq);
+    const float cc = max_norm / (norm + 1e-6f);
+    return cc < 1.0f ? cc : 1.0f;
+}
+
+// (1b) many chunks: one block per agent reduces its partials in a fixed order
+// (strided per-thread sums, then a fixed LDS tree) -> coef[p][group]
+__global__ __launch_bounds__(kOptBlock) void clip_coef_kernel(const double *__restrict__ part, int nblk, int G,
+                                                              float max_norm, float *__restrict__ coef) {
+    const int p = blockIdx.x;
+    __shared__ double red[kOptBlock];
+    for (int k = 0; k < G; ++k) {
+        double s = 0.0;
+        for (int b = threadIdx.x; b < nblk; b += kOptBlock) s += part[((size_t)p * nblk + b) * kMaxGroups + k];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (int h = kOptBlock / 2; h > 0; h >>= 1) {
+            if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) coef[(size_t)p * kMaxGroups + k] = clip_coef(red[0], max_norm);
+        __syncthreads();
+    }
+}
+
+// (2) clip + Adam over one chunk.  Clip coefficients: from coef_dev when the
+// partials were pre-reduced (many chunks), else every block re-reduces its
+// agent's few partials in a fixed order.
+template <bool V4>
 __global__ __launch_bounds__(kOptBlock) void adam_kernel(float *__restrict__ params,
                                                          float *__restrict__ grads,
                                                          float *__restrict__ m, float *__restrict__ v,
                                                          int64_t n, Groups gr, float max_norm,
                                                          const double *__restrict__ part,
+                                                         const float *__restrict__ coef_dev,
                                                          const float *__restrict__ lr_dev,
                                                          float b1, float b2, float eps, float bc1,
                                                          float bc2_sqrt, int clip) {
@@ -79,11 +126,14 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float *__restrict__ par
     if (threadIdx.x < kMaxGroups) {
         float c = 1.0f;
         if (clip && (int)threadIdx.x < gr.G) {
-            double s = 0.0;
-            for (int b = 0; b < (int)gridDim.x; ++b) s += part[((size_t)p * gridDim.x + b) * kMaxGroups + threadIdx.x];
-            const float norm = (float)sqrt(s);
-            const float cc = max_norm / (norm + 1e-6f);
-            c = cc < 1.0f ? cc : 1.0f;
+            if (coef_dev) {
+                c = coef_dev[(size_t)p * kMaxGroups + threadIdx.x];
+            } else {
+                double s = 0.0;
+                for (int b = 0; b < (int)gridDim.x; ++b)
+                    s += part[((size_t)p * gridDim.x + b) * kMaxGroups + threadIdx.x];
+                c = clip_coef(s, max_norm);
+            }
         }
         coef[threadIdx.x] = c;
     }
@@ -92,22 +142,44 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float *__restrict__ par
     const float step_size = lr / bc1;
     const size_t base = (size_t)p * n;
     const int64_t j0 = (int64_t)blockIdx.x * kOptChunk;
-    for (int r = 0; r < kOptPer; ++r) {
-        const int64_t j = j0 + r * kOptBlock + threadIdx.x;
-        if (j >= n) break;
-        float g = grads[base + j];
-        if (clip) {
-            g = g * coef[group_of(gr, j)];
-            grads[base + j] = g;
-        }
-        float mm = m[base + j];
+    auto upd = [&](int64_t j, float g, float &pp, float &mm, float &vv) {
+        if (clip) g = g * coef[group_of(gr, j)];
         mm = mm + (1.0f - b1) * (g - mm);  // lerp_(g, 1-b1)
-        float vv = v[base + j];
         vv = vv * b2 + (1.0f - b2) * g * g;
-        m[base + j] = mm;
-        v[base + j] = vv;
         const float denom = sqrtf(vv) / bc2_sqrt + eps;
-        params[base + j] = params[base + j] - step_size * (mm / denom);
+        pp = pp - step_size * (mm / denom);
+        return g;
+    };
+    if constexpr (V4) {
+        const int64_t j = j0 + 4 * threadIdx.x;
+        if (j >= n) return;
+        f4 g = *reinterpret_cast<const f4 *>(grads + base + j);
+        f4 pp = *reinterpret_cast<const f4 *>(params + base + j);
+        f4 mm = *reinterpret_cast<const f4 *>(m + base + j);
+        f4 vv = *reinterpret_cast<const f4 *>(v + base + j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float pe = pp[e], me = mm[e], ve = vv[e];
+            g[e] = upd(j + e, g[e], pe, me, ve);
+            pp[e] = pe;
+            mm[e] = me;
+            vv[e] = ve;
+        }
+        if (clip) *reinterpret_cast<f4 *>(grads + base + j) = g;
+        *reinterpret_cast<f4 *>(m + base + j) = mm;
+        *reinterpret_cast<f4 *>(v + base + j) = vv;
+        *reinterpret_cast<f4 *>(params + base + j) = pp;
+    } else {
+        for (int r = 0; r < kOptPer; ++r) {
+            const int64_t j = j0 + r * kOptBlock + threadIdx.x;
+            if (j >= n) break;
+            float pe = params[base + j], me = m[base + j], ve = v[base + j];
+            const float g = upd(j, grads[base + j], pe, me, ve);
+            if (clip) grads[base + j] = g;
+            m[base + j] = me;
+            v[base + j] = ve;
+            params[base + j] = pe;
+        }
     }
 }
 
@@ -122,7 +194,9 @@ __global__ void polyak_kernel(float *__restrict__ t, const float *__restrict__ o
 using namespace agx;
 
 extern "C" size_t agx_adam_workspace_bytes(int64_t P, int64_t n) {
-    return (size_t)P * (size_t)ceil_div(n, kOptChunk) * kMaxGroups * sizeof(double);
+    // partials [P][nblk][8] f64, then clip coefficients [P][8] f32
+    return (size_t)P * (size_t)ceil_div(n, kOptChunk) * kMaxGroups * sizeof(double) +
+           (size_t)P * kMaxGroups * sizeof(float);
 }
 
 extern "C" int agx_clip_adam(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t P,
@@ -141,11 +215,26 @@ extern "C" int agx_clip_adam(float *params, float *grads, float *exp_avg, float 
     double *part = static_cast<double *>(workspace);
     dim3 grid((unsigned)nblk, (unsigned)P);
     const int clip = max_norm > 0.0f;
-    if (clip) sumsq_kernel<<<grid, kOptBlock, 0, s>>>(grads, n, gr, part);
+    const bool v4 = n % 4 == 0 && ((uintptr_t)params | (uintptr_t)grads | (uintptr_t)exp_avg |
+                                   (uintptr_t)exp_avg_sq) % 16 == 0;
+    float *coef = nullptr;
+    if (clip) {
+        if (v4) sumsq_kernel<true><<<grid, kOptBlock, 0, s>>>(grads, n, gr, part);
+        else sumsq_kernel<false><<<grid, kOptBlock, 0, s>>>(grads, n, gr, part);
+        if (nblk > 16) {  // pre-reduce once per agent instead of once per block
+            coef = reinterpret_cast<float *>(part + (size_t)P * nblk * kMaxGroups);
+            clip_coef_kernel<<<(unsigned)P, kOptBlock, 0, s>>>(part, (int)nblk, G, max_norm, coef);
+        }
+    }
     const double bc1 = 1.0 - pow((double)beta1, (double)step);
     const double bc2 = 1.0 - pow((double)beta2, (double)step);
-    adam_kernel<<<grid, kOptBlock, 0, s>>>(params, grads, exp_avg, exp_avg_sq, n, gr, max_norm, part, lr,
-                                           beta1, beta2, eps, (float)bc1, (float)sqrt(bc2), clip);
+    if (v4)
+        adam_kernel<true><<<grid, kOptBlock, 0, s>>>(params, grads, exp_avg, exp_avg_sq, n, gr, max_norm, part, coef,
+                                                     lr, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2), clip);
+    else
+        adam_kernel<false><<<grid, kOptBlock, 0, s>>>(params, grads, exp_avg, exp_avg_sq, n, gr, max_norm, part,
+                                                      coef, lr, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2),
+                                                      clip);
     return check_launch("agx_clip_adam");
 }
 

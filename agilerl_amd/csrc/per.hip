@@ -180,11 +180,71 @@ __global__ void per_level(double *__restrict__ sum_tree, double *__restrict__ mi
 }
 
 // recompute every node of the top `levels` levels (nodes 1 .. 2^levels - 1)
+// from the 2^levels nodes below them, staged once in LDS (one HBM round trip
+// instead of one per level)
 __global__ __launch_bounds__(1024) void per_top(double *__restrict__ sum_tree,
                                                 double *__restrict__ min_tree, int levels) {
+    __shared__ double s_sum[1 << kTopLevels], s_min[1 << kTopLevels];
+    const int tid = threadIdx.x;
+    const int nin = 1 << levels;
+    for (int j = tid; j < nin; j += 1024) {
+        s_sum[j] = ld_agent(sum_tree + nin + j);
+        s_min[j] = ld_agent(min_tree + nin + j);
+    }
+    __syncthreads();
     for (int l = levels - 1; l >= 0; --l) {
-        const int64_t lo = (int64_t)1 << l, hi = (int64_t)1 << (l + 1);
-        for (int64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) recompute(sum_tree, min_tree, k);
+        const int m = 1 << l;
+        const bool act = tid < m;
+        double a = 0.0, c = 0.0;
+        if (act) {
+            a = s_sum[2 * tid] + s_sum[2 * tid + 1];
+            const double c0 = s_min[2 * tid], d0 = s_min[2 * tid + 1];
+            c = (d0 < c0) ? d0 : c0;  // Python min(c, d)
+            sum_tree[m + tid] = a;
+            min_tree[m + tid] = c;
+        }
+        __syncthreads();
+        if (act) {
+            s_sum[tid] = a;
+            s_min[tid] = c;
+        }
+        __syncthreads();
+    }
+}
+
+// recompute EVERY node of levels [r, r + k) from the (final) nodes of level
+// r + k: workgroup w owns the subtree rooted at node 2^r + w, stages its 2^k
+// inputs of both trees in LDS and writes each level back with coalesced
+// stores.  The tree is a pure function of the leaves, so a whole-band rebuild
+// gives the same bits as the dirty-path walk (same operands, same order).
+constexpr int kBandLevels = 9;  // 512 inputs per subtree: 8 KiB of LDS for both trees
+__global__ __launch_bounds__(256) void per_band(double *__restrict__ sum_tree, double *__restrict__ min_tree,
+                                               int r, int k) {
+    static_assert((1 << kBandLevels) <= 2 * 256, "one node per thread on the first level");
+    __shared__ double s_sum[1 << kBandLevels], s_min[1 << kBandLevels];
+    const int w = blockIdx.x, tid = threadIdx.x;
+    const int64_t root = ((int64_t)1 << r) + w;
+    const int64_t in0 = root << k;  // first input node (level r + k)
+    for (int j = tid; j < (1 << k); j += 256) {
+        s_sum[j] = sum_tree[in0 + j];
+        s_min[j] = min_tree[in0 + j];
+    }
+    __syncthreads();
+    for (int l = k - 1; l >= 0; --l) {  // level r + l: 2^l <= 256 nodes of this subtree
+        const bool act = tid < (1 << l);
+        double a = 0.0, c = 0.0;
+        if (act) {
+            a = s_sum[2 * tid] + s_sum[2 * tid + 1];
+            const double c0 = s_min[2 * tid], d0 = s_min[2 * tid + 1];
+            c = (d0 < c0) ? d0 : c0;  // Python min(c, d): c unless d < c
+            sum_tree[(root << l) + tid] = a;
+            min_tree[(root << l) + tid] = c;
+        }
+        __syncthreads();
+        if (act) {
+            s_sum[tid] = a;
+            s_min[tid] = c;
+        }
         __syncthreads();
     }
 }
@@ -259,6 +319,17 @@ static int rebuild_large(double *sum_tree, double *min_tree, int64_t cap, const 
     const int levels = log2_exact(cap);
     const int top = levels < kTopLevels ? levels : kTopLevels;
     const unsigned blocks = (unsigned)ceil_div(n, 256);
+    if (n * 32 >= cap && levels > top) {
+        // dense batch: nearly every subtree is dirty; rebuild whole bands of
+        // kBandLevels levels bottom-up (one launch per band, no per-level launches)
+        for (int lo = levels; lo > top;) {
+            const int k = lo - top < kBandLevels ? lo - top : kBandLevels;
+            per_band<<<(unsigned)((int64_t)1 << (lo - k)), 256, 0, s>>>(sum_tree, min_tree, lo - k, k);
+            lo -= k;
+        }
+        per_top<<<1, 1024, 0, s>>>(sum_tree, min_tree, top);
+        return check_launch("agx_per rebuild");
+    }
     // levels whose nodes lie below the top block: shift 1 .. levels - top
     for (int shift = 1; shift <= levels - top; ++shift)
         per_level<<<blocks, 256, 0, s>>>(sum_tree, min_tree, cap, indices, max_size, start, n, shift);

@@ -305,7 +305,7 @@ def kernels_leg(peak_meas):
     nb = 976 * idx.numel()
     out["per_update"] = dict(unit_bytes=976, units=idx.numel(), ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
                              frac_of_measured=round(nb / t / 1e9 / peak_meas, 4),
-                             bound="latency (level-synchronous rebuild)")
+                             bound="launch latency (leaf claim + band rebuild)")
     del st, mt, ws, allidx, pri
     B, A, Z = 1 << 20, 6, 51
     g3 = torch.Generator(device=dev).manual_seed(3)
@@ -328,6 +328,31 @@ def kernels_leg(peak_meas):
     nb = ub * B
     out["td_target"] = dict(unit_bytes=ub, units=B, ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
                             frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
+    # MADDPG critic target (a22): q, q', r, d in; y, dL/dq out
+    q1, qn1 = qc[:, 0].contiguous(), qt[:, 0].contiguous()
+    t = _time(lambda: K.maddpg_critic_target(q1, qn1, r, d, 0.95))
+    nb = 24 * B
+    out["maddpg_critic_target"] = dict(unit_bytes=24, units=B, ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
+                                       frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
+    del qn, qt, qc, q1, qn1
+    # Polyak (a10) and clip + Adam (a8) over a population of flat parameter
+    # rows: 8 agents x 2^22 parameters (large enough to leave the launch floor)
+    n8 = 8 << 22
+    tgt = torch.randn(n8, device=dev, generator=g3)
+    onl = torch.randn(n8, device=dev, generator=g3)
+    t = _time(lambda: K.polyak_(tgt, onl, 0.005))
+    nb = 12 * n8  # read target, online; write target
+    out["polyak"] = dict(unit_bytes=12, units=n8, ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
+                         frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
+    del tgt, onl
+    prm = torch.randn(8, 1 << 22, device=dev, generator=g3)
+    opt = K.ClipAdam(prm, [0, 1 << 21, 1 << 22], lr=1e-3, max_norm=0.5,
+                     grads=torch.randn(8, 1 << 22, device=dev, generator=g3))
+    t = _time(opt.step)
+    nb = 32 * prm.numel()  # norm pass reads g; Adam reads p, g, m, v, writes p, m, v
+    out["clip_adam"] = dict(unit_bytes=32, units=prm.numel(), ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
+                            frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
+    del prm, opt
     torch.cuda.empty_cache()
     return out
 

@@ -208,6 +208,35 @@ def test_per_large_batches_vs_c_oracle():
         np.testing.assert_allclose(w.cpu().numpy(), c.weights(eidx, beta), rtol=2e-7)
 
 
+def test_per_dense_batch_band_rebuild_is_pure_function_of_leaves():
+    """Dense batches (n * 32 >= capacity) rebuild whole bands of levels; at the
+    §8d shape (cap 2^20, 2^16 updates with duplicates) every internal node
+    must equal op(left, right) of its children bit for bit, as the reference's
+    per-write ancestor walk leaves them (segment_tree.py:81-95)."""
+    rng = np.random.default_rng(8)
+    ms, cap = 1_000_000, 1 << 20
+    st, mt = _trees(cap)
+    mp = torch.ones(1, dtype=torch.float64, device=DEV)
+    k = K()
+    k.per_add(st, mt, cap, ms, 0, ms, 0.6, mp)
+    idx = rng.integers(0, ms, 1 << 16)
+    pri = np.abs(rng.standard_normal(1 << 16)).astype(np.float32)
+    k.per_update(st, mt, cap, ms, T(idx.astype(np.int64)), T(pri), 0.6, mp)
+    s, m = st.cpu().numpy(), mt.cpu().numpy()
+    es, em = s.copy(), m.copy()
+    for lvl in range(19, -1, -1):
+        lo, hi = 1 << lvl, 1 << (lvl + 1)
+        es[lo:hi] = es[2 * lo:2 * hi:2] + es[2 * lo + 1:2 * hi:2]
+        c, d = em[2 * lo:2 * hi:2], em[2 * lo + 1:2 * hi:2]
+        em[lo:hi] = np.where(d < c, d, c)
+    assert np.array_equal(s[1:], es[1:]) and np.array_equal(m[1:], em[1:])
+    # last duplicate wins on the leaves
+    last = {int(i): j for j, i in enumerate(idx)}
+    j = np.array(list(last.values()))
+    leaves = s[cap + idx[j]]
+    np.testing.assert_allclose(leaves, np.maximum(pri[j].astype(np.float64), 1e-5) ** 0.6, rtol=4e-16)
+
+
 def test_per_ring_add_wraps():
     ms, cap = 1000, 1024
     st, mt = _trees(cap)
@@ -297,12 +326,13 @@ def test_c51_paths_vs_c_oracle(vmin, vmax, gamma, Z):
 # --------------------------------------------------------------------------- #
 # optimiser                                                                   #
 # --------------------------------------------------------------------------- #
-def test_clip_adam_matches_torch():
+@pytest.mark.parametrize("P,n,split", [(3, 5000, 3100), (3, 5001, 3101), (2, 40_000, 24_002)],
+                         ids=["float4", "scalar", "pre-reduced-norm"])
+def test_clip_adam_matches_torch(P, n, split):
     torch.manual_seed(0)
-    P, n, split = 3, 5000, 3100
     p0 = torch.randn(P, n)
     grads = [torch.randn(P, n) * (5.0 if s == 0 else 0.01) for s in range(4)]
-    lr = [1e-3, 5e-4, 2e-3]
+    lr = [1e-3, 5e-4, 2e-3][:P]
     ref = [torch.nn.Parameter(p0[i, :split].clone()) for i in range(P)]
     ref2 = [torch.nn.Parameter(p0[i, split:].clone()) for i in range(P)]
     opts = [torch.optim.Adam([ref[i], ref2[i]], lr=lr[i]) for i in range(P)]
