@@ -67,10 +67,12 @@ class Dict:
 
 class SyntheticVecEnv:
     """``num_envs`` independent synthetic episodes; data drawn from a ring of
-    pre-generated batches (``ring`` steps) so a step is a memcpy."""
+    pre-generated batches (``ring`` steps) so a step is a memcpy.
+    ``max_episode_steps`` truncates episodes like gymnasium's TimeLimit
+    (LunarLander: 1000); None never truncates (the bench's default)."""
 
     def __init__(self, num_envs: int, obs_dim: int = 8, n_actions: int = 4, p_done: float = 1 / 200,
-                 seed: int = 0, ring: int = 97):
+                 seed: int = 0, ring: int = 97, max_episode_steps: int | None = None):
         self.num_envs = int(num_envs)
         self.single_observation_space = Box(-np.inf, np.inf, (obs_dim,))
         self.single_action_space = Discrete(n_actions)
@@ -81,12 +83,15 @@ class SyntheticVecEnv:
         self._rew = rng.standard_normal((ring, num_envs), dtype=np.float32)
         self._term = rng.random((ring, num_envs)) < p_done
         self._trunc = np.zeros(num_envs, dtype=bool)
+        self.max_episode_steps = max_episode_steps
+        self._len = np.zeros(num_envs, dtype=np.int64)
         self._k = 0
         self._ring = ring
         self.steps = 0
 
     def reset(self, seed=None, options=None, out_obs: np.ndarray | None = None):
         self._k = 0
+        self._len[:] = 0
         obs = self._obs[0]
         if out_obs is not None:
             np.copyto(out_obs.reshape(obs.shape), obs)
@@ -105,7 +110,12 @@ class SyntheticVecEnv:
             rew = out_rew
         if out_done is not None:
             np.copyto(out_done.reshape(term.shape), term)
-        return obs, rew, term, self._trunc, {}
+        trunc = self._trunc
+        if self.max_episode_steps is not None:
+            self._len += 1
+            trunc = (self._len >= self.max_episode_steps) & ~term
+            self._len[term | trunc] = 0
+        return obs, rew, term, trunc, {}
 
     def close(self):
         pass

@@ -272,6 +272,59 @@ class PopulationRunner:
         self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)
         self.env_steps += P * N * T
 
+    @torch.no_grad()
+    def evaluate(self, loop: int = 1, max_steps: int | None = None) -> np.ndarray:
+        """Fitness of every agent at once: PPO.test (ppo.py:1113-1289) run for
+        the whole population on its env slices — agent p acts on envs
+        [p*N, (p+1)*N) with the sampled policy step (one agx_ppo_act launch per
+        vector step for all P agents); each env's first finished episode score
+        counts, ``max_steps`` ends the pass; mean over envs, then over ``loop``
+        passes.  The env is reset per pass (as test() does), so the next
+        rollout starts from a fresh reset like the reference's next
+        collect_rollouts (on_policy.py:50-56).  -> float64 [P]."""
+        pop, env = self.pop, self.env
+        P, N, D = pop.P, pop.N, pop.spec.obs_dim
+        desc = pop.fused_descriptor()
+        act_d = torch.empty(P * N, dtype=torch.int64, device=pop.device)
+        act_h = torch.empty(P * N, dtype=torch.int64, pin_memory=True)
+        obs_h = torch.empty(P * N * D, dtype=torch.float32, pin_memory=True)
+        obs_d = torch.empty(P, N, D, dtype=torch.float32, device=pop.device)
+        out = np.zeros((loop, P))
+        for k in range(loop):
+            obs, _ = env.reset()
+            scores = np.zeros(P * N)
+            completed = np.zeros(P * N)
+            finished = np.zeros(P * N, dtype=bool)
+            step = 0
+            while not finished.all():
+                obs_h.numpy()[:] = np.asarray(obs, dtype=np.float32).reshape(-1)
+                obs_d.view(-1).copy_(obs_h, non_blocking=True)
+                if desc is not None:
+                    from .learner import policy_step
+
+                    pop.act_counter += 1
+                    policy_step(pop, desc, obs_d, N * D, sample=True, counter=pop.act_counter,
+                                out_agent_stride=N, actions_flat=act_d)
+                else:
+                    act_d.copy_(pop.act(obs_d)[0].view(-1))
+                act_h.copy_(act_d, non_blocking=True)
+                self.ev.record()
+                self.ev.synchronize()
+                obs, reward, term, trunc, _ = env.step(act_h.numpy().copy())
+                step += 1
+                scores += np.asarray(reward, dtype=np.float64).reshape(-1)
+                done = np.logical_or(term, trunc if trunc is not None else False).reshape(-1)
+                if max_steps is not None and step == max_steps:
+                    done = np.ones(P * N, dtype=bool)
+                new = done & ~finished
+                completed[new] = scores[new]
+                finished |= done
+            out[k] = completed.reshape(P, N).mean(1)
+        self.started = False  # the next collect() starts from env.reset()
+        self.last_value_valid = False
+        self.scores.zero_()
+        return out.mean(0)
+
     def iteration(self) -> torch.Tensor:
         """collect -> bootstrap + GAE -> learn; returns per-agent mean loss (device)."""
         self.collect()

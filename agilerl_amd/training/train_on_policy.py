@@ -9,10 +9,14 @@ bootstrap + GAE + the fused learner for all agents at once.  A generation is
 ``ceil(evo_steps / learn_step)`` iterations per agent (:248-262), followed by
 fitness and tournament selection on the device (hpo.population_sync).
 
-Fitness is the mean return of the episodes each agent finished during the
-generation (the rollout's own episode accounting, on_policy.py:147-172)
-rather than a separate ``agent.test`` pass over the env; with ``eval_steps``
-not None, ``agent.test`` is not run either (the env is the population's).
+Fitness is ``agent.test`` of every agent (train_on_policy.py:363-373: one
+finished episode per env, ``eval_steps`` caps a pass, mean over
+``eval_loop`` passes), run for the whole population at once by
+``PopulationRunner.evaluate``: agent p acts on its own env slice with the
+fused policy step; the env is reset per pass, so the next generation's
+rollout starts from a reset like the reference's next collect_rollouts.
+Training-episode means go to ``agent.scores``.  Selection runs whenever a
+tournament is given (the reference also needs a mutation object).
 Mutations (architecture / hyper-parameter) are outside the hot path: a
 ``mutation`` object is ignored with a warning.  Returns (pop, pop_fitnesses)
 like the reference.
@@ -62,22 +66,27 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
             losses.append(runner.iteration().cpu().numpy())
             for agent in pop:
                 agent.steps[-1] += T * N
+        # training-episode scores (on_policy.py:147-172 -> agent.scores) ...
         r_sum = runner.episode_return_sum.cpu().numpy()
         r_cnt = runner.episodes.cpu().numpy()
-        fitness = [float(r_sum[i] / r_cnt[i]) if r_cnt[i] > 0 else float("nan") for i in range(P)]
+        runner.reset_episode_stats()
+        # ... then the population's fitness: agent.test for every agent
+        # (train_on_policy.py:363-373), batched on device over the env slices
+        fitness = [float(f) for f in runner.evaluate(loop=eval_loop, max_steps=eval_steps)]
         for i, agent in enumerate(pop):
+            if r_cnt[i] > 0:
+                agent.scores.append(float(r_sum[i] / r_cnt[i]))
             agent.fitness.append(fitness[i])
-            agent.scores.append(fitness[i])
+            agent.steps.append(agent.steps[-1])
         pop_fitnesses.append(fitness)
         if verbose:
             fps = sum(a.steps[-1] for a in pop) / max(time.time() - t0, 1e-9)
             print(f"--- {env_name} {algo}: steps {[a.steps[-1] for a in pop]}, fitness "
                   f"{[round(f, 2) for f in fitness]}, mean loss {np.mean(losses):.4f}, {fps:.0f} env-steps/s")
-        if target is not None and np.nanmean(fitness) >= target:
+        if target is not None and np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target)) \
+                and len(pop[0].steps) >= 100:
             break
-        if sync is not None:  # fitness already reduced on the host: hand it over (resets the stats)
-            sync.fitness_override = np.nan_to_num(np.asarray(fitness), nan=-1e9)
+        if sync is not None:  # fitness reduced on the host already: hand it over
+            sync.fitness_override = np.asarray(fitness)
             sync.generation()
-        else:
-            runner.reset_episode_stats()
     return pop, pop_fitnesses

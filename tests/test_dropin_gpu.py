@@ -51,7 +51,7 @@ def test_create_population_train_on_policy():
     pop = create_population("PPO", net_config, INIT_HP, obs_space, act_space, population_size=4, num_envs=16)
     assert len(pop) == 4 and all(a.population is pop[0].population for a in pop)
     assert pop[0].population.fused_descriptor() is not None
-    env = SyntheticVecEnv(4 * 16, seed=3, p_done=0.05)
+    env = SyntheticVecEnv(4 * 16, seed=3, p_done=0.05, max_episode_steps=60)
     tour = TournamentSelection(2, True, 4, 1)
     np.random.seed(0)
     pop, fits = train_on_policy(env, "Synthetic", "PPO", pop, INIT_HP=INIT_HP, max_steps=1024, evo_steps=256,

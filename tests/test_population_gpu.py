@@ -354,3 +354,49 @@ def test_persistent_rollout_abort_releases_kernel(monkeypatch):
     torch.cuda.synchronize()
     assert run.seq_base == pop.T + 1
     assert int(pop.actions.min()) >= 0 and int(pop.actions.max()) < 4
+
+
+class _FixedEpisodeEnv:
+    """Env e pays c[e] per step and terminates every L[e] steps, whatever
+    the actions: PPO.test's fitness (ppo.py:1113-1289) is then known exactly."""
+
+    def __init__(self, P, N, seed=0):
+        rng = np.random.default_rng(seed)
+        self.num_envs = P * N
+        self.L = rng.integers(1, 12, P * N)
+        self.c = rng.normal(size=P * N)
+        self.obs = rng.standard_normal((P * N, 8)).astype(np.float32)
+        self.t = np.zeros(P * N, dtype=np.int64)
+        self.seen = []
+
+    def reset(self, **kw):
+        self.t[:] = 0
+        return self.obs.copy(), {}
+
+    def step(self, actions):
+        a = np.asarray(actions)
+        assert a.shape == (self.num_envs,) and a.min() >= 0 and a.max() < 4
+        self.seen.append(a.copy())
+        self.t += 1
+        term = self.t % self.L == 0
+        return self.obs.copy(), self.c.astype(np.float32), term, np.zeros_like(term), {}
+
+
+@pytest.mark.parametrize("max_steps", [None, 5])
+def test_population_evaluate_matches_test_semantics(max_steps):
+    """PopulationRunner.evaluate = agent.test for every agent at once: each
+    env's first finished episode (or the max_steps cut) counts, mean over the
+    agent's envs, then over the loop passes; the runner resumes from a reset."""
+    from agilerl_amd.population.runner import PopulationRunner
+
+    P, N = 3, 16
+    pop = _pop(P=P, N=N)
+    env = _FixedEpisodeEnv(P, N)
+    runner = PopulationRunner(pop, env)
+    fit = runner.evaluate(loop=2, max_steps=max_steps)
+    steps = env.L if max_steps is None else np.minimum(env.L, max_steps)
+    exp = (env.c.astype(np.float32).astype(np.float64) * steps).reshape(P, N).mean(1)
+    np.testing.assert_allclose(fit, exp, rtol=1e-12)
+    assert len(env.seen) == 2 * int(steps.max())
+    # actions are the policy's: not constant across envs
+    assert len(np.unique(np.concatenate(env.seen))) > 1

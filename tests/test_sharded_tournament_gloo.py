@@ -80,13 +80,14 @@ def _worker(rank, port, kind, out_dir):
     from agilerl_amd.hpo.tournament import TournamentSelection
 
     pop = [_make_agent(kind, rank * P + j) for j in range(P)]
+    gen0 = _summary(pop)
     t = TournamentSelection(2, True, P * WORLD, 2)
     np.random.seed(11)
     sel = ShardedTournamentSelection(t)
     elite, new_pop = sel.select(pop)
     np.random.seed(12)
     _, newer = select_population(t, new_pop)  # second generation through the entry-point helper
-    torch.save({"gen1": _summary(new_pop), "gen2": _summary(newer), "parents": sel.last_parents,
+    torch.save({"gen0": gen0, "gen1": _summary(new_pop), "gen2": _summary(newer), "parents": sel.last_parents,
                 "elite": None if elite is None else _summary([elite])},
                os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
@@ -103,7 +104,13 @@ def test_sharded_tournament_matches_single_process(tmp_path, kind):
     mp.start_processes(_worker, args=(port, kind, str(tmp_path)), nprocs=WORLD, join=True, start_method="spawn")
     got = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
 
+    from agilerl_amd.hpo.sharded import unpack_agent
+
+    # the same agents in one process, carrying the ranks' exact initial bytes
+    # (network init may differ in the last bits across processes' thread counts)
     full = [_make_agent(kind, g) for g in range(P * WORLD)]
+    for g, a in enumerate(full):
+        unpack_agent(a, got[g // P]["gen0"][g % P]["state"])
     t = TournamentSelection(2, True, P * WORLD, 2)
     np.random.seed(11)
     elite, gen1 = t.select(full)
