@@ -407,21 +407,27 @@ __global__ __launch_bounds__(kC51RowWaves * 64) void c51_rows_kernel(
 // per row.  The per-row serial order of the reference's two index_add_ calls
 // is then simply the lane's own loop over z:
 //   1. lane k finds a*_k = argmax Q_online(s'_k) from its own Q row;
-//   2. the wave gathers the 64 selected target rows with coalesced loads
-//      (flattened (row, atom) order, a* of the row fetched from its lane) into
-//      LDS transposed as sP[z][row] (pitch 65: conflict-free both ways);
-//   3. pass L: lane k walks z = 0..Z-1 and adds m_l to bin L_z; pass U adds
-//      m_u to bin U_z, on its own column sProj[bin][k] (pitch 64: a lane's
-//      bin never conflicts with another lane's).  L and U are monotone in z
-//      for a valid support, so pass L keeps the running bin sum in a register
-//      (each step stores the partial; the last store of a run is the sum) and
-//      pass U reads a bin's pass-L value only when a new run starts — those
-//      reads are issued 8 atoms ahead, which is exact because a new U bin has
-//      not yet been written by pass U.  A lane whose row turns out not to be
-//      monotone redoes both passes as plain read-modify-writes;
-//   4. the wave gathers log_p rows the same way, lane k folds its loss.
-// HBM reads are whole contiguous 4Z-byte row segments; every other access is
-// LDS.  One wave = one workgroup, 2·65·Z·4 ≈ 26 KB of LDS (6 per CU).
+//   2. the wave gathers the 64 selected target rows by LDS-DMA
+//      (buffer_load ... lds, flattened (row, atom) order, a* of the row taken
+//      from its lane): they land in LDS as [row][z] without passing through
+//      VGPRs, and lane k reads its own row at pitch Z (odd: conflict-free);
+//   3. the same LDS region becomes the projection [bin][row] (pitch 64: a
+//      lane's bin never conflicts with another lane's).  Pass L: lane k walks
+//      z = 0..Z-1 and adds m_l to bin L_z; pass U adds m_u to bin U_z.  L and U
+//      are monotone in z for a valid support, so pass L keeps the running bin
+//      sum in a register (each step stores the partial; the last store of a
+//      run is the sum) and pass U reads a bin's pass-L value only when a new
+//      run starts — those reads are issued 8 atoms ahead, which is exact
+//      because a new U bin has not yet been written by pass U.  A lane whose
+//      row turns out not to be monotone redoes both passes as plain
+//      read-modify-writes;
+//   4. the projection goes to registers, the region receives the log_p rows
+//      (LDS-DMA again), lane k folds its loss.
+// One Z x 64 region (13 KB) for all three lives and ~150 VGPRs: 3 waves per
+// SIMD hide the dependent q -> a* -> gather chain (the register-staged
+// version, 26 KB and 341 registers, ran 1 wave per SIMD: 258 -> 151 us at
+// 2^20 rows).  Opaque copies of the lane id / bin words per group of 8
+// atoms keep the scheduler from hoisting all Z address computations.
 constexpr int kC51LaneRows = 64;
 
 // Z atoms at compile time (the gather's (row, atom) split is a multiply-shift,
@@ -429,14 +435,13 @@ constexpr int kC51LaneRows = 64;
 // (±200 or ±100 over 51 atoms: 8 or 4), so (tz − v_min)/Δz is the exact
 // product with 1/Δz and the f32 division sequence is skipped.
 template <int Z, bool POW2>
-__global__ __launch_bounds__(64) void c51_lane_kernel(
+__global__ __launch_bounds__(64) void c51_dma_kernel(
     const float *__restrict__ qno, const float *__restrict__ tdist, const float *__restrict__ logp,
     const int64_t *__restrict__ act, const float *__restrict__ rew, const float *__restrict__ dn,
     const float *__restrict__ support, int64_t B, int A, float vmin, float vmax, float dz, float inv_dz,
     float g, float *__restrict__ loss, float *__restrict__ proj) {
     static_assert(Z >= 2 && Z <= 64, "one lane per atom of the support");
-    __shared__ float sP[Z * 65];     // target probabilities, later log_p, [z][row]
-    __shared__ float sProj[Z * 64];  // projection [bin][row]
+    __shared__ float sA[Z * 64];
     const int lane = threadIdx.x;
     const int64_t row0 = (int64_t)blockIdx.x * kC51LaneRows;
     const int nrows = (int)(B - row0 < kC51LaneRows ? B - row0 : kC51LaneRows);
@@ -456,43 +461,37 @@ __global__ __launch_bounds__(64) void c51_lane_kernel(
         }
     }
     const float supv = lane < Z ? support[lane] : 0.f;
-    float4 *p4 = reinterpret_cast<float4 *>(sProj);
-#pragma unroll
-    for (int e = lane; e < Z * 16; e += 64) p4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-    // Gather the 64 selected rows (row index per lane: sel) of a [B][A][Z]
-    // array: buffer loads on a descriptor over this wave's 64·A·Z block (rows
-    // past B read as 0), all Z loads of both gathers in flight together.
-    // Element lane + 64 j is atom z of row rk, in flattened (row, atom) order.
     const uint32_t blk = (uint32_t)(A * Z * 4);
-    auto gather = [&](const float *__restrict__ src, int sel, float (&v)[Z]) {
+    // rows (row0 + rk, sel of lane rk) of a [B][A][Z] array -> sA[rk * Z + z];
+    // rows past B read as 0 (buffer range = this wave's nrows rows)
+    auto dma_rows = [&](const float *__restrict__ src, int sel) {
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(src) + row0 * A * Z, 0,
                                                           (int)(blk * (uint32_t)nrows), 0x00020000);
+        // opaque lane id: keeps the Z offset computations here instead of
+        // hoisted (and held in registers) across the passes
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
 #pragma unroll
         for (int j = 0; j < Z; ++j) {
-            const int e = lane + 64 * j, rk = e / Z, z = e - rk * Z;
+            const int e = ln + 64 * j, rk = e / Z, z = e - rk * Z;
             const int srow = __shfl(sel, rk & 63, 64);
             const uint32_t off = (uint32_t)rk * blk + (uint32_t)((srow * Z + z) * 4);
-            v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void *)(sA + 64 * j), 4, off, 0, 0, 0);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
     };
-    auto to_lds = [&](const float (&v)[Z]) {
-#pragma unroll
-        for (int j = 0; j < Z; ++j) {
-            const int e = lane + 64 * j, rk = e / Z, z = e - rk * Z;
-            sP[z * 65 + rk] = v[j];
-        }
+    // rv / kv: copies of r / kk re-made opaque every 8 atoms, so the
+    // scheduler cannot hoist all Z atom computations (3 Z live values) ahead
+    float rv = r, kv = kk;
+    int lf = lane;
+    auto fence = [&](int z) {
+        if (z % 8 == 0) asm volatile("" : "+v"(rv), "+v"(kv), "+v"(lf));
     };
-    float vl[Z];
-    {
-        float vt[Z];
-        gather(tdist, astar, vt);
-        to_lds(vt);
-    }
-    gather(logp, a_cur, vl);  // in flight during the two passes
-    __syncthreads();
     auto atom = [&](int z, int &L, int &U, float &b) {
         const float sup = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, supv), z));
-        float tz = r + kk * sup;
+        float tz = rv + kv * sup;
         tz = fminf(fmaxf(tz, vmin), vmax);  // clamp(min=vmin, max=vmax)
         b = POW2 ? (tz - vmin) * inv_dz : (tz - vmin) / dz;
         L = (int)floorf(b);
@@ -502,11 +501,17 @@ __global__ __launch_bounds__(64) void c51_lane_kernel(
         L = L < 0 ? 0 : (L > Z - 1 ? Z - 1 : L);  // guard (never taken for valid inputs)
         U = U < 0 ? 0 : (U > Z - 1 ? Z - 1 : U);
     };
-    // pass L: runs of equal L are consecutive; store every partial.  The
-    // upper masses and bins stay in registers for pass U.
+    dma_rows(tdist, astar);
+    float pm[Z];  // p_z, then the upper mass mu_z
+#pragma unroll
+    for (int z = 0; z < Z; ++z) pm[z] = sA[lane * Z + z];
+    __syncthreads();  // every row read before sA becomes the projection
+#pragma unroll
+    for (int bin = 0; bin < Z; ++bin) sA[bin * 64 + lane] = 0.f;
+    // pass L (runs of equal L are consecutive; every partial stored, the last
+    // store of a run is its sum), then pass U from the pass-L bin values
     bool mono = true;
-    float mu[Z];
-    uint32_t ub4[(Z + 3) / 4] = {};  // U bins, 8 bits each
+    uint32_t ub4[(Z + 3) / 4] = {};
     {
         int prev = -1;
         float acc = 0.f;
@@ -514,68 +519,77 @@ __global__ __launch_bounds__(64) void c51_lane_kernel(
         for (int z = 0; z < Z; ++z) {
             int L, U;
             float b;
+            fence(z);
             atom(z, L, U, b);
             ub4[z / 4] |= (uint32_t)U << (8 * (z % 4));
-            const float p = sP[z * 65 + lane];
+            const float p = pm[z];
             const float ml = p * ((float)U - b);
-            mu[z] = p * (b - (float)L);
+            pm[z] = p * (b - (float)L);
             mono = mono && L >= prev;
             acc = (L == prev ? acc : 0.f) + ml;
-            sProj[L * 64 + lane] = acc;
+            sA[L * 64 + lf] = acc;
             prev = L;
         }
     }
-    // pass U: a run's first atom starts from the bin's pass-L value (read 8
-    // atoms ahead: a new U bin has not been written by pass U yet)
     {
         int prev = -1;
         float acc = 0.f;
 #pragma unroll
         for (int z0 = 0; z0 < Z; z0 += 8) {
+            // opaque per group: the bin decode and addresses of one group of 8
+            // atoms at a time (hoisted for all Z they cost ~140 VGPRs)
+            int lu = lane;
+            uint32_t w0 = ub4[z0 / 4], w1 = z0 / 4 + 1 < (Z + 3) / 4 ? ub4[z0 / 4 + 1] : 0u;
+            asm volatile("" : "+v"(lu), "+v"(w0), "+v"(w1));
+            auto ubin = [&](int j) { return (int)(((j < 4 ? w0 : w1) >> (8 * (j % 4))) & 255u); };
             float base[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                if (z0 + j < Z) base[j] = sProj[(int)((ub4[(z0 + j) / 4] >> (8 * ((z0 + j) % 4))) & 255u) * 64 + lane];
+                if (z0 + j < Z) base[j] = sA[ubin(j) * 64 + lu];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if (z0 + j < Z) {
-                    const int U = (int)((ub4[(z0 + j) / 4] >> (8 * ((z0 + j) % 4))) & 255u);
+                    const int U = ubin(j);
                     mono = mono && U >= prev;
-                    acc = (U == prev ? acc : base[j]) + mu[z0 + j];
-                    sProj[U * 64 + lane] = acc;
+                    acc = (U == prev ? acc : base[j]) + pm[z0 + j];
+                    sA[U * 64 + lu] = acc;
                     prev = U;
                 }
             }
         }
     }
-    if (!mono) {  // never for a sorted support and gamma >= 0: plain ordered read-modify-writes
-        for (int bin = 0; bin < Z; ++bin) sProj[bin * 64 + lane] = 0.f;
+    if (!mono) {  // never for a sorted support and gamma >= 0: ordered read-modify-writes, p re-read
+        const float *trow = tdist + ((size_t)i * A + astar) * Z;
+        for (int bin = 0; bin < Z; ++bin) sA[bin * 64 + lane] = 0.f;
         for (int z = 0; z < Z; ++z) {
             int L, U;
             float b;
             atom(z, L, U, b);
-            sProj[L * 64 + lane] += sP[z * 65 + lane] * ((float)U - b);
+            sA[L * 64 + lane] += trow[z] * ((float)U - b);
         }
         for (int z = 0; z < Z; ++z) {
             int L, U;
             float b;
             atom(z, L, U, b);
-            sProj[U * 64 + lane] += sP[z * 65 + lane] * (b - (float)L);
+            sA[U * 64 + lane] += trow[z] * (b - (float)L);
         }
     }
     __syncthreads();
-    to_lds(vl);
-    __syncthreads();
-    float part = 0.f;
+    float pr[Z];
 #pragma unroll
-    for (int bin = 0; bin < Z; ++bin) part += sProj[bin * 64 + lane] * sP[bin * 65 + lane];
-    if (live) loss[i] = -part;
+    for (int bin = 0; bin < Z; ++bin) pr[bin] = sA[bin * 64 + lane];
     if (proj) {  // optional projection output, coalesced over (row, bin)
         for (int e = lane; e < nrows * Z; e += 64) {
             const int rk = e / Z, z = e - rk * Z;
-            proj[(size_t)row0 * Z + e] = sProj[z * 64 + rk];
+            proj[(size_t)row0 * Z + e] = sA[z * 64 + rk];
         }
     }
+    __syncthreads();  // projection read out before the log_p rows land
+    dma_rows(logp, a_cur);
+    float part = 0.f;
+#pragma unroll
+    for (int bin = 0; bin < Z; ++bin) part += pr[bin] * sA[lane * Z + bin];
+    if (live) loss[i] = -part;
 }
 
 }  // namespace agx
@@ -641,7 +655,7 @@ extern "C" int agx_c51_project_loss(const float *q_next_online, const float *tar
         const double m = std::frexp((v_max - v_min) / (double)(Z - 1), &e2);
         const bool pow2 = m == 0.5 && (double)dz == std::ldexp(1.0, e2 - 1) && e2 > -60 && e2 < 60;
         const float inv = pow2 ? (float)std::ldexp(1.0, 1 - e2) : 0.f;
-        auto kern = pow2 ? c51_lane_kernel<51, true> : c51_lane_kernel<51, false>;
+        auto kern = pow2 ? c51_dma_kernel<51, true> : c51_dma_kernel<51, false>;
         kern<<<(unsigned)ceil_div(B, kC51LaneRows), 64, 0, as_stream(stream)>>>(
             q_next_online, target_dist, logp_cur, actions, rewards, dones, support, B, (int)A, (float)v_min,
             (float)v_max, dz, inv, (float)gamma, loss, proj);
