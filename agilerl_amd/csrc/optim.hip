@@ -10,11 +10,12 @@
 // clip: coef = max_norm / (||g||_2 + 1e-6), g *= min(coef, 1).
 // Polyak: agilerl/algorithms/dqn.py:349-358 — t = tau*o + (1-tau)*t.
 //
-// Two launches: (1) per-(agent, chunk) partial sums of squares per group into
-// the workspace, (2) every block re-reduces its agent's partials in a fixed
-// order (deterministic), derives the clip coefficients and updates its chunk.
-// Rows of more than 16 chunks add a per-agent pre-reduction (1b) so the
-// re-reduction does not grow with the square of the row length.
+// Two launches: (1) per-(agent, 8192-element chunk) partial sums of squares
+// per group into the workspace, (2) every 1024-element block re-reduces its
+// agent's partials in a fixed order (deterministic), derives the clip
+// coefficients and updates its chunk.  Rows of more than 16 partials add a
+// per-agent pre-reduction (1b) so the re-reduction does not grow with the
+// square of the row length.
 // Traffic: 4 arrays read + 3 written = 28 B per parameter (+4 B norm pass).
 #include "agx_common.h"
 
@@ -23,6 +24,7 @@ namespace agx {
 constexpr int kOptBlock = 256;
 constexpr int kOptPer = 4;  // params per thread per block
 constexpr int kOptChunk = kOptBlock * kOptPer;
+constexpr int kSumChunk = kOptBlock * 4 * 8;  // sum-of-squares block: 8 float4 per thread
 constexpr int kMaxGroups = 8;
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -47,7 +49,7 @@ __global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const float *__restric
     double acc[kMaxGroups];
 #pragma unroll
     for (int k = 0; k < kMaxGroups; ++k) acc[k] = 0.0;
-    const int64_t j0 = (int64_t)blockIdx.x * kOptChunk;
+    const int64_t j0 = (int64_t)blockIdx.x * kSumChunk;
     auto add = [&](int64_t j, float xf) {
         const double x = (double)xf;
         const int k = group_of(gr, j);
@@ -56,14 +58,22 @@ __global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const float *__restric
             if (q == k) acc[q] += x * x;
     };
     if constexpr (V4) {
-        const int64_t j = j0 + 4 * threadIdx.x;
-        if (j < n) {
-            const f4 x = *reinterpret_cast<const f4 *>(g + j);
+        f4 x[8];  // all loads in flight before the f64 accumulation
 #pragma unroll
-            for (int e = 0; e < 4; ++e) add(j + e, x[e]);
+        for (int r = 0; r < 8; ++r) {
+            const int64_t j = j0 + 4 * (r * kOptBlock + threadIdx.x);
+            x[r] = j < n ? *reinterpret_cast<const f4 *>(g + j) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int64_t j = j0 + 4 * (r * kOptBlock + threadIdx.x);
+            if (j < n) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) add(j + e, x[r][e]);
+            }
         }
     } else {
-        for (int r = 0; r < kOptPer; ++r) {
+        for (int r = 0; r < kSumChunk / kOptBlock; ++r) {
             const int64_t j = j0 + r * kOptBlock + threadIdx.x;
             if (j < n) add(j, g[j]);
         }
@@ -116,7 +126,7 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float *__restrict__ par
                                                          float *__restrict__ grads,
                                                          float *__restrict__ m, float *__restrict__ v,
                                                          int64_t n, Groups gr, float max_norm,
-                                                         const double *__restrict__ part,
+                                                         const double *__restrict__ part, int nsum,
                                                          const float *__restrict__ coef_dev,
                                                          const float *__restrict__ lr_dev,
                                                          float b1, float b2, float eps, float bc1,
@@ -130,8 +140,7 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float *__restrict__ par
                 c = coef_dev[(size_t)p * kMaxGroups + threadIdx.x];
             } else {
                 double s = 0.0;
-                for (int b = 0; b < (int)gridDim.x; ++b)
-                    s += part[((size_t)p * gridDim.x + b) * kMaxGroups + threadIdx.x];
+                for (int b = 0; b < nsum; ++b) s += part[((size_t)p * nsum + b) * kMaxGroups + threadIdx.x];
                 c = clip_coef(s, max_norm);
             }
         }
@@ -195,7 +204,7 @@ using namespace agx;
 
 extern "C" size_t agx_adam_workspace_bytes(int64_t P, int64_t n) {
     // partials [P][nblk][8] f64, then clip coefficients [P][8] f32
-    return (size_t)P * (size_t)ceil_div(n, kOptChunk) * kMaxGroups * sizeof(double) +
+    return (size_t)P * (size_t)ceil_div(n, kSumChunk) * kMaxGroups * sizeof(double) +
            (size_t)P * kMaxGroups * sizeof(float);
 }
 
@@ -211,7 +220,7 @@ extern "C" int agx_clip_adam(float *params, float *grads, float *exp_avg, float 
     for (int k = 0; k <= kMaxGroups; ++k) gr.off[k] = k <= G ? group_offsets[k] : n;
     AGX_REQUIRE(gr.off[0] == 0 && gr.off[G] == n, "agx_clip_adam: group offsets must span [0, n)");
     hipStream_t s = as_stream(stream);
-    const int64_t nblk = ceil_div(n, kOptChunk);
+    const int64_t nblk = ceil_div(n, kOptChunk), nsum = ceil_div(n, kSumChunk);
     double *part = static_cast<double *>(workspace);
     dim3 grid((unsigned)nblk, (unsigned)P);
     const int clip = max_norm > 0.0f;
@@ -219,21 +228,23 @@ extern "C" int agx_clip_adam(float *params, float *grads, float *exp_avg, float 
                                    (uintptr_t)exp_avg_sq) % 16 == 0;
     float *coef = nullptr;
     if (clip) {
-        if (v4) sumsq_kernel<true><<<grid, kOptBlock, 0, s>>>(grads, n, gr, part);
-        else sumsq_kernel<false><<<grid, kOptBlock, 0, s>>>(grads, n, gr, part);
-        if (nblk > 16) {  // pre-reduce once per agent instead of once per block
-            coef = reinterpret_cast<float *>(part + (size_t)P * nblk * kMaxGroups);
-            clip_coef_kernel<<<(unsigned)P, kOptBlock, 0, s>>>(part, (int)nblk, G, max_norm, coef);
+        const dim3 sgrid((unsigned)nsum, (unsigned)P);
+        if (v4) sumsq_kernel<true><<<sgrid, kOptBlock, 0, s>>>(grads, n, gr, part);
+        else sumsq_kernel<false><<<sgrid, kOptBlock, 0, s>>>(grads, n, gr, part);
+        if (nsum > 16) {  // pre-reduce once per agent instead of once per block
+            coef = reinterpret_cast<float *>(part + (size_t)P * nsum * kMaxGroups);
+            clip_coef_kernel<<<(unsigned)P, kOptBlock, 0, s>>>(part, (int)nsum, G, max_norm, coef);
         }
     }
     const double bc1 = 1.0 - pow((double)beta1, (double)step);
     const double bc2 = 1.0 - pow((double)beta2, (double)step);
     if (v4)
-        adam_kernel<true><<<grid, kOptBlock, 0, s>>>(params, grads, exp_avg, exp_avg_sq, n, gr, max_norm, part, coef,
-                                                     lr, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2), clip);
+        adam_kernel<true><<<grid, kOptBlock, 0, s>>>(params, grads, exp_avg, exp_avg_sq, n, gr, max_norm, part,
+                                                     (int)nsum, coef, lr, beta1, beta2, eps, (float)bc1,
+                                                     (float)sqrt(bc2), clip);
     else
         adam_kernel<false><<<grid, kOptBlock, 0, s>>>(params, grads, exp_avg, exp_avg_sq, n, gr, max_norm, part,
-                                                      coef, lr, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2),
+                                                      (int)nsum, coef, lr, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2),
                                                       clip);
     return check_launch("agx_clip_adam");
 }
