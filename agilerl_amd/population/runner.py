@@ -114,6 +114,7 @@ class PopulationRunner:
         self.ret_sum_env = torch.zeros(P * N, dtype=torch.float64, device=dev)
         self.episodes_env = torch.zeros(P * N, dtype=torch.int64, device=dev)
         self._ios = None
+        self._np = None
 
     # ------------------------------------------------------------------ #
     @property
@@ -165,11 +166,15 @@ class PopulationRunner:
         self._ios = ios
 
     def _env_step(self) -> None:
-        _, _, term, trunc, _ = self.env.step(self.act_h.numpy(), out_obs=self.obs_h.numpy(),
-                                             out_rew=self.rew_h.numpy(), out_done=self.done_h.numpy())
-        if trunc is not None and trunc.any():  # done = term | trunc (on_policy.py:121-126)
-            self.done_h.numpy()[:] |= trunc
-        self.term_h.numpy()[:] = term
+        # numpy views of the staging made once (Tensor.numpy() costs ~1-3 us a call)
+        if self._np is None:
+            self._np = (self.act_h.numpy(), self.obs_h.numpy(), self.rew_h.numpy(), self.done_h.numpy(),
+                        self.term_h.numpy())
+        act, obs, rew, done, term_np = self._np
+        _, _, term, trunc, _ = self.env.step(act, out_obs=obs, out_rew=rew, out_done=done)
+        if trunc is not None and np.count_nonzero(trunc):  # done = term | trunc (on_policy.py:121-126)
+            done |= trunc
+        np.copyto(term_np, term)
 
     @torch.no_grad()
     def collect(self) -> None:
