@@ -72,6 +72,31 @@ def gae(rewards, dones, values, last_value, last_done, gamma=0.99, gae_lambda=0.
     return (adv, ret, stats) if with_stats else (adv, ret)
 
 
+def gae_launcher(rewards, dones, values, last_value, last_done, gamma, gae_lambda, use_gae, advantages,
+                 returns, stats_out, workspace):
+    """Validate once, then return ``launch(stream)``: agx_gae on these fixed
+    tensors (the population's persistent rollout buffers) with no per-call
+    checks — the per-iteration call costs one ctypes call, not ~10 tensor
+    validations (host time that sat between the rollout and the learner)."""
+    adv, ret, _ = gae(rewards, dones, values, last_value, last_done, gamma, gae_lambda, use_gae,
+                      advantages=advantages, returns=returns, with_stats=True, workspace=workspace,
+                      stats_out=stats_out)  # validates (and runs once)
+    P, T, N = adv.shape
+    d = dones.view(torch.uint8) if dones.dtype == torch.bool else dones
+    ld = last_done.view(torch.uint8) if last_done.dtype == torch.bool else last_done
+    fn = _lib.load().agx_gae
+    args = (rewards.data_ptr(), d.data_ptr(), values.data_ptr(), last_value.data_ptr(), ld.data_ptr(), P, T, N,
+            float(gamma), float(gae_lambda), int(bool(use_gae)), adv.data_ptr(), ret.data_ptr(),
+            stats_out.data_ptr(), workspace.data_ptr())
+
+    def launch(stream: int) -> None:
+        rc = fn(*args, stream)
+        if rc != 0:
+            _lib.check(rc, "agx_gae")
+
+    return launch
+
+
 def adv_normalize_(adv: torch.Tensor, stats: torch.Tensor) -> torch.Tensor:
     P = stats.shape[0]
     _need(adv, "adv", _f32)

@@ -66,6 +66,7 @@ class FusedLearner:
         _lib.check(lib.agx_ppo_learn_prepare(ctypes.byref(self.desc), self.ws.data_ptr(), _lib.stream()),
                    "agx_ppo_learn_prepare")
         self.loss = torch.zeros(pop.P, dtype=torch.float32, device=pop.device)
+        self.args = None
 
     def learn(self, pop, perms: torch.Tensor | None = None) -> torch.Tensor:
         """All epochs x minibatches of every agent in two launches (gather +
@@ -75,13 +76,26 @@ class FusedLearner:
             perms = pop.permutations()
         opt = pop.opt
         b1, b2 = opt.betas
-        _lib.call("agx_ppo_learn", ctypes.byref(self.desc), pop.P, pop.params.data.data_ptr(),
-                  opt.exp_avg.data_ptr(), opt.exp_avg_sq.data_ptr(), opt.lr.data_ptr(), float(b1), float(b2),
-                  float(opt.eps), opt.step_count, pop.obs.data_ptr(), pop.actions.data_ptr(),
-                  pop.log_probs.data_ptr(), pop.advantages.data_ptr(), pop.adv_stats.data_ptr(),
-                  pop.returns.data_ptr(), pop.values.data_ptr(), pop.S, perms.data_ptr(), pop.update_epochs,
-                  pop.batch_size, float(pop.clip_coef), float(pop.vf_coef), float(pop.ent_coef),
-                  float(pop.max_grad_norm), self.loss.data_ptr(), self.ws.data_ptr(), _lib.stream())
+        # the argument list is built once per set of buffers; per call only the
+        # Adam step, the permutations and the stream change (host time between
+        # the rollout and the learner is on the critical path)
+        key = (pop.params.data.data_ptr(), opt.exp_avg.data_ptr(), opt.exp_avg_sq.data_ptr(), opt.lr.data_ptr(),
+               pop.obs.data_ptr(), pop.advantages.data_ptr(), pop.returns.data_ptr(), pop.values.data_ptr(),
+               pop.log_probs.data_ptr(), pop.actions.data_ptr(), pop.adv_stats.data_ptr(), float(b1), float(b2),
+               float(opt.eps), pop.batch_size, pop.update_epochs, float(pop.clip_coef), float(pop.vf_coef),
+               float(pop.ent_coef), float(pop.max_grad_norm))
+        if self.args is None or self.args[0] != key:
+            a = [ctypes.byref(self.desc), pop.P, key[0], key[1], key[2], key[3], key[11], key[12], key[13], 0,
+                 key[4], key[9], key[8], key[5], key[10], key[6], key[7], pop.S, 0, pop.update_epochs,
+                 pop.batch_size, key[16], key[17], key[18], key[19], self.loss.data_ptr(), self.ws.data_ptr(), 0]
+            self.args = (key, a, _lib.load().agx_ppo_learn)
+        a, fn = self.args[1], self.args[2]
+        a[9] = opt.step_count
+        a[18] = perms.data_ptr()
+        a[27] = torch.cuda.current_stream(pop.device).cuda_stream
+        rc = fn(*a)
+        if rc != 0:
+            _lib.check(rc, "agx_ppo_learn")
         opt.step_count += pop.update_epochs * pop.n_minibatches()
         return self.loss
 

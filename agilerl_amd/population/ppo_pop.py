@@ -30,6 +30,7 @@ Two learner back ends share this state:
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -89,6 +90,10 @@ class PPOPopulation:
         self._alloc_rollout()
         self.learn_steps = 0
         self.rollout_id = 0
+        self.prefetch_perms = os.environ.get("AGX_PREFETCH_PERMS", "1") != "0"
+        self._perm_next = None
+        self._perm_stream = None
+        self._gae_launch = None
 
     # ------------------------------------------------------------------ #
     def _alloc_rollout(self):
@@ -167,9 +172,17 @@ class PPOPopulation:
         self.rollout_id += 1
         if last_value is None:
             _, last_value = self.spec.forward(self.params.data, last_obs)
-        K.gae(self.rewards, self.dones, self.values, last_value.contiguous(), last_done.contiguous(),
-              self.gamma, self.gae_lambda, True, advantages=self.advantages, returns=self.returns,
-              with_stats=True, workspace=self.gae_ws, stats_out=self.adv_stats)
+        last_value, last_done = last_value.contiguous(), last_done.contiguous()
+        key = (last_value.data_ptr(), last_done.data_ptr(), last_value.shape, last_done.dtype,
+               *(t.data_ptr() for t in (self.rewards, self.dones, self.values, self.advantages, self.returns,
+                                        self.adv_stats, self.gae_ws)))
+        if self._gae_launch is not None and self._gae_launch[0] == key:
+            self._gae_launch[1](torch.cuda.current_stream(self.device).cuda_stream)
+            return
+        launch = K.gae_launcher(self.rewards, self.dones, self.values, last_value, last_done, self.gamma,
+                                self.gae_lambda, True, self.advantages, self.returns, self.adv_stats, self.gae_ws)
+        # keep a launcher only for the runner's persistent last_value / last_done
+        self._gae_launch = (key, launch, last_value, last_done)
 
     # ------------------------------------------------------------------ #
     def learn(self) -> torch.Tensor:
@@ -179,7 +192,10 @@ class PPOPopulation:
         if self.target_kl is None and self.fused_descriptor() is not None:
             from .learner import fused_learn
 
-            return fused_learn(self)
+            loss = fused_learn(self)
+            if self.prefetch_perms:
+                self.prefetch_permutations()
+            return loss
         return self._learn_torch()
 
     def minibatch_plan(self):
@@ -188,9 +204,37 @@ class PPOPopulation:
 
     def permutations(self) -> torch.Tensor:
         """[E, P, S] int64 per-agent shuffles (the reference's np.random.shuffle
-        per epoch, ppo.py:842), drawn on the device."""
+        per epoch, ppo.py:842), drawn on the device.  Returns the draw made
+        ahead by prefetch_permutations() if there is one (the same draw, in
+        the same order, as drawing here)."""
+        if self._perm_next is not None:
+            perms, ev = self._perm_next
+            self._perm_next = None
+            main = torch.cuda.current_stream(self.device)
+            main.wait_event(ev)
+            perms.record_stream(main)
+            return perms
         keys = torch.rand(self.update_epochs, self.P, self.S, generator=self.gen, device=self.device)
         return torch.argsort(keys, dim=-1)
+
+    def prefetch_permutations(self) -> None:
+        """Draw the next permutations on a side stream now (rand + a radix
+        sort, ~35 us of small launches), so they run beside the learner and
+        the next rollout instead of between them.  Only the fused path calls
+        it: there the generator draws nothing else, so the sequence of draws
+        is unchanged."""
+        if self._perm_next is not None or self.device.type != "cuda":
+            return
+        if self._perm_stream is None:
+            self._perm_stream = torch.cuda.Stream(device=self.device)
+        side = self._perm_stream
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            keys = torch.rand(self.update_epochs, self.P, self.S, generator=self.gen, device=self.device)
+            perms = torch.argsort(keys, dim=-1)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        self._perm_next = (perms, ev)
 
     def _learn_torch(self, perms: torch.Tensor | None = None) -> torch.Tensor:
         P, S, D = self.P, self.S, self.spec.obs_dim

@@ -217,6 +217,11 @@ class PopulationRunner:
 
     def _collect_persistent(self, desc) -> None:
         """One launch for the whole rollout; the host paces it step by step."""
+        lib, ctl, base = self._launch_persistent(desc)
+        self._pace_persistent(lib, ctl, base)
+        self._finish_persistent()
+
+    def _launch_persistent(self, desc):
         pop = self.pop
         P, N, T = pop.P, pop.N, pop.T
         lib = _lib.load()
@@ -231,6 +236,10 @@ class PopulationRunner:
                                                   self.args_h.data_ptr(), ctl, self.timeout_s, _lib.stream()),
                    "agx_ppo_rollout_persistent")
         self.seq_base = base + T + 1
+        return lib, ctl, base
+
+    def _pace_persistent(self, lib, ctl, base) -> None:
+        T = self.pop.T
         try:
             for t in range(T):
                 lib.agx_host_signal(ctl, base + t + 1)
@@ -243,10 +252,14 @@ class PopulationRunner:
             self.ctl_h.zero_()
             self.seq_base = 0
             raise
-        pop.act_counter += T
+        self.pop.act_counter += T
+        self.env_steps += self.pop.P * self.pop.N * T
+
+    def _finish_persistent(self) -> None:
+        # stream-ordered after the rollout kernel, which ends only after the
+        # host's final release — by then the last env step has written term_h
         self.last_value_valid = True
         self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)  # last_done = term (:196)
-        self.env_steps += P * N * T
 
     @torch.no_grad()
     def _collect_torch(self) -> None:
@@ -332,7 +345,32 @@ class PopulationRunner:
 
     def iteration(self) -> torch.Tensor:
         """collect -> bootstrap + GAE -> learn; returns per-agent mean loss (device)."""
+        desc = self.pop.fused_descriptor()
+        if self.persistent and desc is not None and self.pop.target_kl is None:
+            return self._iteration_pipelined(desc)
         self.collect()
         self.pop.finish_rollout(self.last_obs, self.last_done,
                                 self.last_value if self.last_value_valid else None)
         return self.pop.learn()
+
+    @torch.no_grad()
+    def _iteration_pipelined(self, desc) -> torch.Tensor:
+        """The persistent rollout, the last_done copy, GAE and the learner are
+        all enqueued on the stream BEFORE the host paces the rollout: the GPU
+        runs rollout -> GAE -> learner back to back with no host launch gap
+        (the host-side launch work overlaps the rollout instead of sitting
+        between it and the learner).  Same launches, same order, same data as
+        collect() + finish_rollout() + learn().  If the host loop raises, the
+        workgroups are released and the queued GAE / learner run on the
+        partial rollout before the exception propagates."""
+        if self._ios is None:
+            self._build_ios()
+        if not self.started:
+            self.env.reset(out_obs=self.obs_h.numpy())
+            self.started = True
+        lib, ctl, base = self._launch_persistent(desc)
+        self._finish_persistent()
+        self.pop.finish_rollout(self.last_obs, self.last_done, self.last_value)
+        loss = self.pop.learn()
+        self._pace_persistent(lib, ctl, base)
+        return loss

@@ -400,3 +400,23 @@ def test_population_evaluate_matches_test_semantics(max_steps):
     assert len(env.seen) == 2 * int(steps.max())
     # actions are the policy's: not constant across envs
     assert len(np.unique(np.concatenate(env.seen))) > 1
+
+
+def test_permutation_prefetch_keeps_the_draw_sequence(monkeypatch):
+    """learn() draws the next permutations on a side stream; the results are
+    bit-identical to drawing them at the start of every learn()."""
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.population.runner import PopulationRunner
+
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("AGX_PREFETCH_PERMS", flag)
+        pop = _pop(P=3, N=32, learn_step=256, batch=64, epochs=2)
+        runner = PopulationRunner(pop, SyntheticVecEnv(3 * 32, seed=4, p_done=0.1))
+        for _ in range(3):
+            runner.iteration()
+        explicit = pop.permutations()  # an explicit draw takes the prefetched one
+        torch.cuda.synchronize()
+        out.append((pop.params.data.clone(), pop.opt.exp_avg.clone(), explicit.clone()))
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
