@@ -1215,10 +1215,14 @@ __global__ void ppo_gather_kernel(const float *__restrict__ obs, const long long
                                   const float *__restrict__ ret, const float *__restrict__ old_v,
                                   const double *__restrict__ adv_stats, const long long *__restrict__ perms,
                                   long long S, int D, int P, float *__restrict__ gobs, int *__restrict__ gact,
-                                  float *__restrict__ grow) {
+                                  float *__restrict__ grow, unsigned *__restrict__ counters, int ncounters) {
     const int ep = blockIdx.y;  // e * P + p
     const int p = ep % P;
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    // the learner's arrival counters + timeout word (stream-ordered before it;
+    // replaces a separate memset launch)
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (int i = threadIdx.x; i < ncounters; i += blockDim.x) counters[i] = 0u;
     if (j >= S) return;
     const long long src = perms[(size_t)ep * S + j];
     const size_t sp = (size_t)p * S + src;
@@ -1651,12 +1655,12 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, f
     int K = max_partners(P);
     if (K > nsb) K = (int)nsb;
     AGX_REQUIRE(P * K <= 65535, "agx_ppo_learn: too many workgroups");
-    // counters + timeout word: one 16-byte-multiple block at the workspace start
-    if (hipMemsetAsync(ws, 0, w.gobs, s) != hipSuccess) return check_launch("agx_ppo_learn memset");
+    // counters + timeout word: one 16-byte-multiple block at the workspace start, zeroed by the gather
     dim3 ggrid((unsigned)ceil_div(S, 256), (unsigned)(epochs * P));
     ppo_gather_kernel<<<ggrid, 256, 0, s>>>(obs, reinterpret_cast<const long long *>(actions), old_logp, adv, ret,
                                             old_value, adv_stats, reinterpret_cast<const long long *>(perms), S,
-                                            pl.D, (int)P, gobs, gact, grow);
+                                            pl.D, (int)P, gobs, gact, grow, reinterpret_cast<unsigned *>(ws),
+                                            (int)(w.gobs / sizeof(unsigned)));
     const int rc2 = check_launch("agx_ppo_learn gather");
     if (rc2) return rc2;
     LearnArgs a;
