@@ -303,6 +303,35 @@ def test_c51_large_vs_c_oracle():
     np.testing.assert_allclose(loss.cpu().numpy(), eloss, rtol=1e-5, atol=1e-5)
 
 
+def test_c51_full_size_properties():
+    """SURVEY §8d shape (2^20 rows, A=6, Z=51, ±200, γ_n = 0.99^4), where the
+    CPU oracle is too slow for every row: (1) mass conservation — U = L + 1 for
+    every atom, so each projected row sums to its target row's (clamped) mass;
+    (2) loss >= 0 (log-probs <= 0); (3) 4096 rows spread over the batch are
+    bit-exact against the C oracle."""
+    B, A, Z = 1 << 20, 6, 51
+    g = torch.Generator(device=DEV).manual_seed(3)
+    qn = torch.randn(B, A, device=DEV, generator=g)
+    td = torch.softmax(torch.randn(B, A, Z, device=DEV, generator=g), -1).clamp_(min=1e-3)
+    lp = torch.log_softmax(torch.randn(B, A, Z, device=DEV, generator=g), -1)
+    act = torch.randint(0, A, (B,), device=DEV, generator=g)
+    r = torch.randn(B, device=DEV, generator=g) * 50
+    d = (torch.rand(B, device=DEV, generator=g) < 0.05).float()
+    sup = torch.linspace(-200, 200, Z, device=DEV)
+    loss, proj = K().c51_project_loss(qn, td, lp, act, r, d, sup, -200.0, 200.0, 0.99 ** 4, with_proj=True)
+    astar = qn.argmax(1)
+    mass = td[torch.arange(B, device=DEV), astar].double().sum(1)
+    err = (proj.double().sum(1) - mass).abs().max().item()
+    assert err < 1e-5, err
+    assert loss.min().item() >= 0.0
+    rows = torch.linspace(0, B - 1, 4096, device=DEV).long()
+    sel = lambda x: x[rows].cpu().numpy()  # noqa: E731
+    eloss, eproj = cref.c51(sel(qn), sel(td), sel(lp), sel(act), sel(r), sel(d), sup.cpu().numpy(), -200.0,
+                            200.0, 0.99 ** 4)
+    assert np.array_equal(proj[rows].cpu().numpy(), eproj)
+    np.testing.assert_allclose(loss[rows].cpu().numpy(), eloss, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("vmin,vmax,gamma,Z", [(-10.0, 10.0, 0.99 ** 3, 51),   # Δz = 0.4: division path
                                                  (-200.0, 200.0, -0.9, 51),       # L/U decreasing: RMW fallback
                                                  (-100.0, 100.0, 0.99, 41)])      # other Z: row-wave kernel
