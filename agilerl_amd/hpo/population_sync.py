@@ -36,18 +36,48 @@ class PopulationSync:
         self.tournament_size, self.elitism, self.eval_loop = tournament_size, elitism, eval_loop
         self.history: list[np.ndarray] = []
         self.last_parents: list[int] = []
+        self._side = None      # stream for the fitness read (behind the rollout only)
+        self._fit_h = None     # pinned landing buffer of the gathered fitness
+        self._idx_h = None     # pinned parent indices -> device, non-blocking
+        self._idx_d = None
+        self._idx_ev = None
 
-    def _fitness(self) -> torch.Tensor:
+    def _fitness_host(self) -> np.ndarray:
+        """Every rank's fitness on the host.  The episode statistics are final
+        once the rollout is (runner.stats_event); they are reduced, gathered
+        (RCCL) and copied out on a side stream that waits only for that event,
+        so the host does not wait for the learner queued behind the rollout."""
         if self.fitness_override is not None:
-            f = torch.as_tensor(np.asarray(self.fitness_override, dtype=np.float64), device=self.pop.device)
+            f = np.asarray(self.fitness_override, dtype=np.float64)
             self.fitness_override = None
             self.runner.reset_episode_stats()
-            return f
+            if self.world == 1:
+                return f
+            t = torch.as_tensor(f, device=self.pop.device)
+            return self._all_gather(t).cpu().numpy()
         r = self.runner
-        f = torch.where(r.episodes > 0, r.episode_return_sum / r.episodes.clamp(min=1).double(),
-                        torch.full_like(r.episode_return_sum, -1e9))
-        r.reset_episode_stats()
-        return f
+        ev = getattr(r, "stats_event", None)
+        if self.pop.device.type != "cuda" or ev is None:
+            f = torch.where(r.episodes > 0, r.episode_return_sum / r.episodes.clamp(min=1).double(),
+                            torch.full_like(r.episode_return_sum, -1e9))
+            r.reset_episode_stats()
+            return self._all_gather(f).cpu().numpy()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.pop.device)
+            self._fit_h = torch.empty(self.world * self.pop.P, dtype=torch.float64, pin_memory=True)
+        side = self._side
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            eps = r.episodes
+            f = torch.where(eps > 0, r.episode_return_sum / eps.clamp(min=1).double(),
+                            torch.full_like(r.episode_return_sum, -1e9))
+            g = self._all_gather(f)
+            self._fit_h.copy_(g, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(side)
+        done.synchronize()
+        r.reset_episode_stats()  # on the main stream: after the queued learner, before the next rollout
+        return self._fit_h.numpy().copy()
 
     def _all_gather(self, x: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
@@ -56,13 +86,40 @@ class PopulationSync:
         dist.all_gather_into_tensor(out, x.contiguous())
         return out
 
+    def _dev_index(self, rows: list[int]) -> torch.Tensor:
+        """A small index list on the device without a blocking copy: pinned
+        staging (re-used only after its previous copy has landed)."""
+        n = len(rows)
+        if self._idx_h is None or self._idx_h.numel() < n:
+            m = max(n, self.pop.P)
+            self._idx_h = torch.empty(m, dtype=torch.int64, pin_memory=True)
+            self._idx_d = torch.empty(m, dtype=torch.int64, device=self.pop.device)
+            self._idx_ev = None
+        if self._idx_ev is not None:
+            self._idx_ev.synchronize()
+        self._idx_h.numpy()[:n] = rows
+        out = self._idx_d[:n]
+        out.copy_(self._idx_h[:n], non_blocking=True)
+        self._idx_ev = torch.cuda.Event()
+        self._idx_ev.record()
+        return out
+
     @torch.no_grad()
     def _clone_rows(self, parents: list[int]) -> None:
         """Row j of this rank becomes global row parents[rank*P + j] (params and
-        both Adam moments)."""
+        both Adam moments).  Everything is enqueued on the current stream, in
+        order after the learner; the host does not wait."""
         pop, P, me = self.pop, self.pop.P, self.rank
         bufs = (pop.params.data, pop.opt.exp_avg, pop.opt.exp_avg_sq)
         n = bufs[0].shape[1]
+        mine = parents[me * P:(me + 1) * P]
+        if self.world == 1:  # a permutation-with-repeats of the rows: one gather per buffer
+            if mine == list(range(P)):
+                return
+            idx = self._dev_index(mine) if pop.device.type == "cuda" else torch.as_tensor(mine)
+            for b in bufs:
+                b.copy_(b.index_select(0, idx))
+            return
         # rows each rank needs from each other rank (sorted, unique): the same
         # plan on every rank, derived from the shared parent list
         need = [[sorted({q % P for q in parents[r * P:(r + 1) * P] if q // P == src}) if src != r else []
@@ -81,7 +138,6 @@ class PopulationSync:
             if rows:
                 recv[src] = torch.empty(len(rows), 3 * n, dtype=bufs[0].dtype, device=pop.device)
                 ops.append(dist.P2POp(dist.irecv, recv[src], src))
-        mine = parents[me * P:(me + 1) * P]
         local = [j for j in range(P) if mine[j] // P == me]
         snap = None
         if local:
@@ -105,18 +161,10 @@ class PopulationSync:
 
     @torch.no_grad()
     def generation(self) -> list[int]:
-        pop = self.pop
-        fit = self._all_gather(self._fitness()).cpu().numpy()  # the only host sync of the step
+        fit = self._fitness_host()
         self.history.append(fit)
         fits = [np.stack([h[i] for h in self.history[-self.eval_loop:]]) for i in range(len(fit))]
-        if self.rng_state is None:
-            _, parents = select_parents(fits, self.tournament_size, self.elitism, self.eval_loop)
-        else:
-            state = np.random.get_state()
-            np.random.set_state(self.rng_state.get_state())
-            _, parents = select_parents(fits, self.tournament_size, self.elitism, self.eval_loop)
-            self.rng_state.set_state(np.random.get_state())
-            np.random.set_state(state)
+        _, parents = select_parents(fits, self.tournament_size, self.elitism, self.eval_loop, rng=self.rng_state)
         self._clone_rows(parents)
         self.last_parents = parents
         return parents

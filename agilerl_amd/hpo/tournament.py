@@ -14,14 +14,17 @@ from __future__ import annotations
 import numpy as np
 
 
-def select_parents(fitnesses, tournament_size: int, elitism: bool, eval_loop: int):
-    """-> (elite position, list of parent positions for the new population)."""
+def select_parents(fitnesses, tournament_size: int, elitism: bool, eval_loop: int, rng=None):
+    """-> (elite position, list of parent positions for the new population).
+    rng: a numpy RandomState to draw from instead of the global one (the same
+    legacy MT19937 randint stream)."""
+    draw = np.random.randint if rng is None else rng.randint
     last = [np.mean(np.asarray(f)[-eval_loop:]) for f in fitnesses]
     rank = np.argsort(last).argsort()
     elite = int(np.argsort(rank)[-1])
     parents = [elite] if elitism else []
     for _ in range(len(fitnesses) - (1 if elitism else 0)):
-        sel = np.random.randint(0, len(rank), size=tournament_size)
+        sel = draw(0, len(rank), size=tournament_size)
         parents.append(int(sel[np.argmax([rank[i] for i in sel])]))
     return elite, parents
 

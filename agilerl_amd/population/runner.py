@@ -115,6 +115,7 @@ class PopulationRunner:
         self.episodes_env = torch.zeros(P * N, dtype=torch.int64, device=dev)
         self._ios = None
         self._np = None
+        self.stats_event = None
 
     # ------------------------------------------------------------------ #
     @property
@@ -211,6 +212,7 @@ class PopulationRunner:
         # reward/done of the last step -> slot T-1; final obs -> last_obs + bootstrap value
         _lib.check(fn(dref, P, N, params, ctypes.byref(self._ios[T]), 1, 0, pop.act_seed, 0, s),
                    "agx_ppo_rollout_step")
+        self._mark_stats()
         self.last_value_valid = True
         self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)  # last_done = term (:196)
         self.env_steps += P * N * T
@@ -236,7 +238,16 @@ class PopulationRunner:
                                                   self.args_h.data_ptr(), ctl, self.timeout_s, _lib.stream()),
                    "agx_ppo_rollout_persistent")
         self.seq_base = base + T + 1
+        self._mark_stats()
         return lib, ctl, base
+
+    def _mark_stats(self) -> None:
+        """Event after the rollout's last episode-accounting write: the
+        generation step reads the episode statistics behind it (on a side
+        stream) instead of behind everything queued after the rollout."""
+        if self.stats_event is None:
+            self.stats_event = torch.cuda.Event()
+        self.stats_event.record()
 
     def _pace_persistent(self, lib, ctl, base) -> None:
         T = self.pop.T
@@ -287,6 +298,7 @@ class PopulationRunner:
             self.ret_sum_env += torch.where(d, self.scores, 0.0).double()
             self.episodes_env += d.long()
             self.scores.masked_fill_(d, 0.0)
+        self._mark_stats()
         self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)
         self.env_steps += P * N * T
 

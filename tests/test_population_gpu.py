@@ -117,8 +117,50 @@ def test_runner_iteration_end_to_end():
     sync = PopulationSync(pop, runner, seed=1)
     parents = sync.generation()
     assert len(parents) == 4 and all(0 <= p < 4 for p in parents)
-    for i, par in enumerate(parents):
-        assert torch.equal(pop.params.data[i], pop.params.data[i]) and par >= 0
+
+
+def test_generation_behind_queued_learner_matches_synchronous():
+    """PopulationSync.generation straight after iteration() (the learner still
+    queued): fitness read behind the rollout only, parent rows cloned in stream
+    order after the learner.  Must equal the synchronous computation: the
+    same parents from the same fitness, new row j = learned row parents[j]."""
+    import numpy as np
+
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.population_sync import PopulationSync
+    from agilerl_amd.hpo.tournament import select_parents
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+    from agilerl_amd.population.runner import PopulationRunner
+
+    def make():
+        spec = ActorCriticSpec(obs_dim=8, n_actions=4)
+        pop = PPOPopulation(spec, 6, 32, learn_step=256, batch_size=64, update_epochs=2, device=DEV,
+                            seeds=list(range(6)))
+        return pop, PopulationRunner(pop, SyntheticVecEnv(6 * 32, seed=7, p_done=0.2))
+
+    a_pop, a_run = make()
+    b_pop, b_run = make()
+    sync = PopulationSync(a_pop, a_run, seed=3)
+    for g in range(3):
+        a_run.iteration()
+        parents = sync.generation()  # no host sync before it
+        b_run.iteration()
+        torch.cuda.synchronize()
+        r = b_run
+        fit = torch.where(r.episodes > 0, r.episode_return_sum / r.episodes.clamp(min=1).double(),
+                          torch.full_like(r.episode_return_sum, -1e9)).cpu().numpy()
+        b_run.reset_episode_stats()
+        if g == 0:
+            rng = np.random.RandomState(3)
+        _, exp = select_parents([np.asarray([f]) for f in fit], 2, True, 1, rng=rng)
+        assert parents == exp
+        idx = torch.as_tensor(exp, device=DEV)
+        for buf in (b_pop.params.data, b_pop.opt.exp_avg, b_pop.opt.exp_avg_sq):
+            buf.copy_(buf.index_select(0, idx))
+        torch.cuda.synchronize()
+        assert torch.equal(a_pop.params.data, b_pop.params.data)
+        assert torch.equal(a_pop.opt.exp_avg_sq, b_pop.opt.exp_avg_sq)
 
 
 @pytest.mark.parametrize("P,N", [(3, 16), (2, 45), (8, 1)])
