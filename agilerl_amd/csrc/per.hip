@@ -267,31 +267,52 @@ __global__ __launch_bounds__(256) void per_sample_kernel(
     double max_w = 0.0;
     if (weights) max_w = cr_pow(min_tree[1] / total * size, -beta);
     int32_t bad = 0;
+    // kPer independent walks per lane advance level by level in lock step: each
+    // level issues kPer independent loads, so a lane's latency chain is one
+    // walk deep instead of kPer walks (identical arithmetic per walk)
     constexpr int kPer = 4;
+    int64_t i[kPer], k[kPer];
+    double ub[kPer];
+#pragma unroll
     for (int r = 0; r < kPer; ++r) {
-        const int64_t i = ((int64_t)blockIdx.x * kPer + r) * blockDim.x + threadIdx.x;
-        if (i >= B) break;
-        const double a = segment * (double)i;
-        const double b = segment * (double)(i + 1);
-        double ub = (double)u[i] * (b - a) + a;
-        if (!(ub >= 0.0 && ub <= total + 1e-5)) ++bad;
-        int64_t k = 1;
-        // children of node k live at 2k, 2k+1; the LDS copy holds nodes < 2^s
-        while (k < cap) {
-            const int64_t l = 2 * k;
-            const double left = (kStage && l < ((int64_t)1 << stage_levels)) ? top[l] : sum_tree[l];
-            if (left > ub) {
-                k = l;
+        i[r] = ((int64_t)blockIdx.x * kPer + r) * blockDim.x + threadIdx.x;
+        k[r] = 1;
+        ub[r] = 0.0;
+        if (i[r] < B) {
+            const double a = segment * (double)i[r];
+            const double b = segment * (double)(i[r] + 1);
+            ub[r] = (double)u[i[r]] * (b - a) + a;
+            if (!(ub[r] >= 0.0 && ub[r] <= total + 1e-5)) ++bad;
+        }
+    }
+    // children of node k live at 2k, 2k+1; the LDS copy holds nodes < 2^s;
+    // every walk takes exactly `levels` steps (cap = 2^levels)
+    for (int lev = 0; lev < levels; ++lev) {
+        double left[kPer];
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) {
+            const int64_t l = 2 * k[r];
+            // l = 2k lies at depth lev + 1: in the LDS copy iff it is < 2^s
+            left[r] = (kStage && lev + 1 < stage_levels) ? top[l] : sum_tree[l];
+        }
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) {
+            const int64_t l = 2 * k[r];
+            if (left[r] > ub[r]) {
+                k[r] = l;
             } else {
-                ub -= left;
-                k = l + 1;
+                ub[r] -= left[r];
+                k[r] = l + 1;
             }
         }
-        const int64_t idx = k - cap;
-        out_idx[i] = idx;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+        if (i[r] >= B) continue;
+        out_idx[i[r]] = k[r] - cap;
         if (weights) {
-            const double ps = sum_tree[k] / total;
-            weights[i] = (float)(cr_pow(ps * size, -beta) / max_w);
+            const double ps = sum_tree[k[r]] / total;
+            weights[i[r]] = (float)(cr_pow(ps * size, -beta) / max_w);
         }
     }
     if (err && bad) atomicAdd(err, bad);
