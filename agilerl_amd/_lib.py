@@ -34,12 +34,12 @@ SIGNATURES = {
     "agx_ppo_learn_lds_bytes": (_SZ, [_P]),
     "agx_ppo_learn_workspace_bytes": (_SZ, [_P, _I, _I, _I]),
     "agx_ppo_learn_prepare": (_INT, [_P, _P, _P]),
-    "agx_ppo_learn": (_INT, [_P, _I, _P, _P, _P, _P, _F, _F, _F, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I,
-                             _I, _F, _F, _F, _F, _P, _P, _P]),
-    "agx_ppo_act": (_INT, [_P, _I, _I, _P, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P, _I,
-                           _P, _P, _P]),
+    "agx_ppo_learn": (_INT, [_P, _P, _P, _P]),
+    "agx_ppo_act": (_INT, [_P, _I, _I, _P, _P, _I, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P,
+                           _I, _P, _P, _P]),
     "agx_ppo_rollout_step": (_INT, [_P, _I, _I, _P, _P, _INT, _INT, ctypes.c_uint64, ctypes.c_uint64, _P]),
     "agx_rollout_workgroups": (_I, [_I, _I]),
+    "agx_rollout_max_workgroups": (_I, [_P]),
     "agx_rollout_ctl_bytes": (_SZ, [_I, _I]),
     "agx_rollout_args_bytes": (_SZ, [_I]),
     "agx_ppo_rollout_persistent": (_INT, [_P, _I, _I, _P, _P, _I, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
@@ -64,10 +64,12 @@ SIGNATURES = {
     "agx_maddpg_critic_target": (_INT, [_P] * 4 + [_I, _D, _P, _P, _P, _P, _P]),
     "agx_c51_project_loss": (_INT, [_P] * 7 + [_I, _I, _I, _D, _D, _D, _P, _P, _P]),
     "agx_adam_workspace_bytes": (_SZ, [_I, _I]),
-    "agx_clip_adam": (_INT, [_P, _P, _P, _P, _I, _I, _P, _INT, _F, _P, _F, _F, _F, _I, _P, _P]),
+    "agx_clip_adam": (_INT, [_P, _P, _P, _P, _I, _I, _P, _INT, _F, _P, _F, _F, _F, _P, _P, _P, _P]),
     "agx_polyak": (_INT, [_P, _P, _I, _F, _P]),
     "agx_debug_pow": (_INT, [_P, _P, _P, _I, _P]),
     "agx_debug_learn_stamps": (_INT, [_P]),
+    "agx_debug_learn_stall": (_INT, [_INT]),
+    "agx_host_shuffle_perms": (_INT, [_P, _P, _I, _I, _I, _P]),
     "agx_debug_stream": (_INT, [_P, _P, _I, _INT, _I, _P]),
 }
 

@@ -13,9 +13,12 @@ Supported: Discrete action spaces, Box observations, ``net_config`` with
 ``latent_dim`` (the reference's defaults: encoder [64] -> latent 64, actor
 head [64], critic head [16] unless ``head_config`` is given, ppo.py:286-300),
 LayerNorm on, shared encoder.  ``get_action`` / ``learn`` / ``test`` keep the
-reference's signatures and return types; action masks, recurrent policies,
+reference's signatures and return types; recurrent policies,
 continuous actions and custom ``actor_network`` objects raise
-NotImplementedError (outside the hot path).
+NotImplementedError (outside the hot path).  ``get_action(obs, action_mask)``
+applies the reference's legal-action masks (logits of illegal actions ->
+-1e8, ppo.py:529-565); ``target_kl`` stops an agent's epochs early exactly
+as ppo.py:917-918 does, inside the fused learner.
 """
 
 from __future__ import annotations
@@ -140,7 +143,7 @@ class PPO:
                            if not k.startswith("critic.encoder.")},
                "exp_avg_sq": {k: v[o:o + int(np.prod(sh))].view(sh) for k, (o, sh) in keys.items()
                               if not k.startswith("critic.encoder.")},
-               "step": int(self.population.opt.step_count)}
+               "step": int(self.population.opt.steps[self.row])}
         mods = {net: {k[len(net) + 1:]: t for k, t in sd.items() if k.startswith(net + ".")}
                 for net in ("actor", "critic")}
         torch.save(C.checkpoint_dict(self, mods, {"optimizer": opt}), path)
@@ -161,7 +164,7 @@ class PPO:
             o, sh = keys[k]
             m[o:o + t.numel()] = t.reshape(-1).to(m)
             v[o:o + t.numel()] = opt["exp_avg_sq"][k].reshape(-1).to(v)
-        self.population.opt.step_count = int(opt["step"])
+        self.population.opt.steps[self.row] = int(opt["step"])
         C.restore_attributes(self, ck)
 
     @classmethod
@@ -181,12 +184,14 @@ class PPO:
     def get_action(self, obs, action_mask=None, hidden_state=None, *args, **kwargs):
         """-> (action, log_prob, entropy, value) numpy arrays (ppo.py:567-633);
         sampling is a Gumbel-max draw from a counter-based Philox stream."""
-        if action_mask is not None:
-            raise NotImplementedError("action masks are not supported by the agx policy step")
         pop = self.population
         o = torch.as_tensor(np.asarray(obs), dtype=torch.float32, device=self.device)
         o = o.reshape(-1, pop.spec.obs_dim).contiguous()
         n = o.shape[0]
+        mask = None
+        if action_mask is not None:
+            mask = torch.as_tensor(np.asarray(action_mask), device=self.device).reshape(n, pop.spec.n_actions)
+            mask = (mask != 0).to(torch.uint8).contiguous()
         out = dict(actions=torch.empty(n, dtype=torch.int64, device=self.device),
                    log_probs=torch.empty(n, device=self.device), values=torch.empty(n, device=self.device),
                    entropy=torch.empty(n, device=self.device))
@@ -195,6 +200,8 @@ class PPO:
             logits, value = pop.spec.forward(pop.params.data[self.row:self.row + 1], o.unsqueeze(0))
             from ..population.nets import categorical
 
+            if mask is not None:
+                logits = torch.where(mask.bool().unsqueeze(0), logits, torch.full_like(logits, -1e8))
             logp_all, ent = categorical(logits)
             u = torch.rand(logits.shape, device=self.device).clamp_(min=1e-20)
             a = torch.argmax(logits - torch.log(-torch.log(u)), dim=-1)
@@ -203,8 +210,8 @@ class PPO:
         else:
             self._counter += 1
             params = pop.params.data[self.row]
-            _lib.call("agx_ppo_act", ctypes.byref(desc), 1, n, params.data_ptr(), o.data_ptr(), 0, 1,
-                      pop.act_seed + 7919 * self.row, (1 << 40) + self._counter, out["actions"].data_ptr(),
+            _lib.call("agx_ppo_act", ctypes.byref(desc), 1, n, params.data_ptr(), o.data_ptr(), 0, _lib.ptr(mask), 0,
+                      1, pop.act_seed + 7919 * self.row, (1 << 40) + self._counter, out["actions"].data_ptr(),
                       out["log_probs"].data_ptr(), out["values"].data_ptr(), out["entropy"].data_ptr(), 0, None,
                       None, _lib.stream())
         return tuple(out[k].cpu().numpy() for k in ("actions", "log_probs", "entropy", "values"))
@@ -220,6 +227,7 @@ class PPO:
         pop = self.population
         if getattr(pop, "_learned_rollout", None) != pop.rollout_id:
             pop._last_losses = pop.learn().cpu().numpy()
+            pop.check_errors()  # a partner timeout would leave the update incomplete: raise, never return it
             pop._learned_rollout = pop.rollout_id
         return float(pop._last_losses[self.row])
 

@@ -192,7 +192,7 @@ constexpr LearnPlan make_plan(NetDims d) {
     pl.act_floats = off;  // the policy-step kernel needs only this much
     pl.l_dlg = off; off += kSB * kMaxA;
     pl.l_dvb = off; off += kSB * kMaxA;
-    pl.l_row = off; off += 5 * kSB;
+    pl.l_row = off; off += 6 * kSB;  // old_logp, adv, ret, old_v, action, legal-action mask
     pl.l_grad = pl.l_x0;
     if (off - pl.l_x0 < pl.param_end) off = pl.l_x0 + pl.param_end;  // room for the gradient image
     int red = 0;
@@ -203,10 +203,10 @@ constexpr LearnPlan make_plan(NetDims d) {
     pl.red_h = red;
     red += 3 * kNW * pl.H;
     pl.l_red = off; off += red;
-    pl.l_stat = off; off += 4 * kNW;
+    pl.l_stat = off; off += 5 * kNW;
     pl.lds_floats = off;
     if (pl.lds_floats * 4 > 160 * 1024) return pl;
-    pl.slab = rup(pl.param_end + 1, 64);
+    pl.slab = rup(pl.param_end + 2, 64);  // + loss and approx_kl words
     // ---- dW tile groups
     int slot = 0;
     for (int g = 0; g < pl.ne + 3; ++g) {
@@ -332,15 +332,24 @@ __device__ __forceinline__ int swave() {
     const int rrow = wave + kNW * lq, sub = lr16;           \
     (void)lr16, (void)lq, (void)rrow, (void)sub, (void)lane
 
-// workgroup-uniform sum (fixed order); uses stat[slot*kNW .. +kNW)
-__device__ __forceinline__ float block_sum(float v, float *stat, int slot, int lane, int wave) {
-    v = row_sum(v);
-    const float w = readlane_f(v, 0) + readlane_f(v, 16) + readlane_f(v, 32) + readlane_f(v, 48);
-    if (lane == 0) stat[slot * kNW + wave] = w;
+// workgroup-uniform sums of two values (fixed order); uses stat[slot*kNW .. +2*kNW)
+__device__ __forceinline__ void block_sum2(float &a, float &b, float *stat, int slot, int lane, int wave) {
+    a = row_sum(a);
+    b = row_sum(b);
+    const float wa = readlane_f(a, 0) + readlane_f(a, 16) + readlane_f(a, 32) + readlane_f(a, 48);
+    const float wb = readlane_f(b, 0) + readlane_f(b, 16) + readlane_f(b, 32) + readlane_f(b, 48);
+    if (lane == 0) {
+        stat[slot * kNW + wave] = wa;
+        stat[(slot + 1) * kNW + wave] = wb;
+    }
     __syncthreads();
-    float t = 0.f;
-    for (int i = 0; i < kNW; ++i) t += stat[slot * kNW + i];
-    return t;
+    float ta = 0.f, tb = 0.f;
+    for (int i = 0; i < kNW; ++i) {
+        ta += stat[slot * kNW + i];
+        tb += stat[(slot + 1) * kNW + i];
+    }
+    a = ta;
+    b = tb;
 }
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
@@ -535,18 +544,23 @@ struct LearnArgs {
     float *params, *m, *v;
     const float *lr;
     float b1, b2, eps;
-    long long step0;
-    const float *gobs;  // [E][P][S][D] minibatch-ordered
-    const int *gact;    // [E][P][S]
-    const float *grow;  // [E][P][4][S]: old_logp, adv_norm, ret, old_v
+    long long *step;       // [P] Adam steps taken (in/out)
+    const float *gobs;     // [E][P][S][D] minibatch-ordered
+    const int *gact;       // [E][P][S]
+    const unsigned *gmask; // [E][P][S] legal-action bitmask, or null (no masks)
+    const float *grow;     // [E][P][4][S]: old_logp, adv_norm, ret, old_v
     long long S;
     int E, B, P;
     float clip, vf, ent, max_norm;
-    float *loss_out;
+    double target_kl;      // <= 0: no early stop
+    float *loss_out, *kl_out;
+    int *epochs_out;
+    unsigned *err;         // sticky error word (partner timeout)
     long long *stamps;
-    int K;                // workgroups per agent (data-parallel over sub-batches)
-    float *slabs;         // [P][2][K][slab] gradient hand-off (double-buffered)
-    unsigned *cnt;        // [P] arrival counters, [P] = timeout word (zeroed per call)
+    int K;                 // workgroups per agent (data-parallel over sub-batches)
+    float *slabs;          // [P][2][K][slab] gradient hand-off (double-buffered)
+    unsigned *cnt;         // [P] arrival counters, [P] = timeout word (zeroed per call)
+    int debug_stall;       // test hook: partner 1 of agent 0 never arrives
 };
 
 #define IC(x) std::integral_constant<int, (x)>()
@@ -603,15 +617,21 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     (void)nmb_dummy;
     const int nmb = (int)((S + g.B - 1) / g.B);
     float loss_total = 0.f;
-    double pb1 = pow((double)g.b1, (double)g.step0), pb2 = pow((double)g.b2, (double)g.step0);
+    double kl_total = 0.0;  // sum of per-minibatch approx_kl (np.mean over all minibatches so far, ppo.py:917)
+    int n_done = 0, epochs_done = 0;
+    const long long step0 = g.step[p];
+    double pb1 = pow((double)g.b1, (double)step0), pb2 = pow((double)g.b2, (double)step0);
     const float lr_p = g.lr[p];
     float *rowf = sm + pl.l_row;  // [4][SB]: old_logp, adv, ret, old_v
     float *stat = sm + pl.l_stat;
     int *acts = reinterpret_cast<int *>(sm + pl.l_row + 4 * kSB);
+    unsigned *legal = reinterpret_cast<unsigned *>(sm + pl.l_row + 5 * kSB);
+    if (g.debug_stall && p == 0 && kk == 1) return;  // test hook: a partner that never arrives
 
     for (int e = 0; e < g.E; ++e) {
         const float *eobs = g.gobs + ((size_t)e * g.P + p) * S * pl.D;
         const int *eact = g.gact + ((size_t)e * g.P + p) * S;
+        const unsigned *emask = g.gmask ? g.gmask + ((size_t)e * g.P + p) * S : nullptr;
         const float *erow = g.grow + ((size_t)e * g.P + p) * 4 * S;
         for (int mb = 0; mb < nmb; ++mb) {
             const long long s0 = (long long)mb * g.B;
@@ -622,7 +642,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
 #pragma unroll
             for (int s = 0; s < kMaxSlot; ++s) acc[s] = f4{0.f, 0.f, 0.f, 0.f};
             for (int i = tid; i < pl.l_stat - pl.l_red; i += kNT) sm[pl.l_red + i] = 0.f;
-            float lsum = 0.f;
+            float lsum = 0.f, klsum = 0.f;
             // this update's gradient slabs (double-buffered by update parity)
             const int upd = e * nmb + mb;
             float *base = g.K > 1 ? g.slabs + ((size_t)p * 2 + (upd & 1)) * g.K * pl.slab : nullptr;
@@ -690,6 +710,9 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 } else if (tid < 5 * kSB) {
                     const int r = tid - 4 * kSB;
                     acts[r] = r < nrow ? eact[s0 + sb + r] : 0;
+                } else if (tid < 6 * kSB) {
+                    const int r = tid - 5 * kSB;
+                    legal[r] = (emask && r < nrow) ? emask[s0 + sb + r] : 0xffffffffu;
                 }
                 __syncthreads();
                 AGX_STAMP(stb + 1);
@@ -703,7 +726,9 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     AGX_IDS;
                     const int r = rrow, a = sub;
                     const bool live = r < nrow;
-                    const float lg = a < pl.A ? sm[pl.l_lg + r * kMaxA + a] : -3.0e38f;
+                    // illegal actions: logits -> -1e8 (apply_action_mask_discrete, distributions.py:16-28)
+                    const bool ok_a = (legal[r] >> a) & 1u;
+                    const float lg = a < pl.A ? (ok_a ? sm[pl.l_lg + r * kMaxA + a] : -1.0e8f) : -3.0e38f;
                     const float mx = row_max(lg);
                     const float ex = a < pl.A ? expf(lg - mx) : 0.f;
                     const float lse = mx + logf(row_sum(ex));
@@ -737,11 +762,14 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     const float inv = (dv >= -g.clip && dv <= g.clip) ? 1.f : 0.f;
                     const float g_H = -g.ent * inv_b;
                     const float dl = g_logp * ((a == a_t ? 1.f : 0.f) - pa) + g_H * pa * (gh - pg_dot);
-                    if (a < pl.A) sm[pl.l_dlg + r * kMaxA + a] = live ? dl : 0.f;
+                    if (a < pl.A) sm[pl.l_dlg + r * kMaxA + a] = (live && ok_a) ? dl : 0.f;
                     if (a == 0) {
                         sm[pl.l_dvb + r * kMaxA] =
                             live ? g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv) : 0.f;
-                        if (live) lsum += (fmaxf(p1, p2) + g.vf * 0.5f * fmaxf(lu, lc) - g.ent * Hs) * inv_b;
+                        if (live) {
+                            lsum += (fmaxf(p1, p2) + g.vf * 0.5f * fmaxf(lu, lc) - g.ent * Hs) * inv_b;
+                            klsum += ((ratio - 1.f) - lrt) * inv_b;  // approx_kl (ppo.py:899-902)
+                        }
                     }
                 }
                 __syncthreads();
@@ -996,10 +1024,10 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             vdump(IC(pl.ne));
             AGX_STAMP(64 + 9);
             __syncthreads();
-            float lmb;
+            float lmb = lsum, klmb = klsum;
             {
                 AGX_IDS;
-                lmb = block_sum(lsum, stat, 2, lane, wave);
+                block_sum2(lmb, klmb, stat, 2, lane, wave);
             }
             if (g.K > 1) {
                 // ---- P9b: exchange partial gradients with the agent's partners --------
@@ -1009,7 +1037,10 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 // backward pass / vdump; the loss word follows.  Drained by every storing
                 // wave before the barrier, so no release fence (cdna_hip_programming.md
                 // §6 G16 R1)
-                if (tid == 0) slab_put(pl.param_end, lmb);
+                if (tid == 0) {
+                    slab_put(pl.param_end, lmb);
+                    slab_put(pl.param_end + 1, klmb);
+                }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 if (tid == 0) {
@@ -1022,17 +1053,18 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         __builtin_amdgcn_s_sleep(2);
                         if (++spins > kSpinMax) {
                             __hip_atomic_store(g.cnt + g.P, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (g.err) __hip_atomic_fetch_or(g.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             ok = 0;
                             break;
                         }
                     }
                     // no acquire: the slabs are read with sc1 loads below
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    stat[3 * kNW] = ok ? 1.f : 0.f;
+                    stat[4 * kNW] = ok ? 1.f : 0.f;
                     AGX_STAMP(64 + 12);
                 }
                 __syncthreads();
-                if (stat[3 * kNW] == 0.f) return;  // partner never arrived: timeout word set, whole block exits
+                if (stat[4 * kNW] == 0.f) return;  // partner never arrived: timeout word set, whole block exits
                 // (loss words via vector atomics: a uniform plain load would take the
                 // scalar-cache path, which never sees the partners' stores)
                 // (one vector load: lane q reads partner q's loss word; summed in
@@ -1042,9 +1074,16 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     const float w = ln < g.K ? __hip_atomic_load(base + (size_t)ln * pl.slab + pl.param_end,
                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                              : 0.f;
-                    float lt = readlane_f(w, 0);
-                    for (int q = 1; q < g.K; ++q) lt += readlane_f(w, q);
+                    const float wk = ln < g.K ? __hip_atomic_load(base + (size_t)ln * pl.slab + pl.param_end + 1,
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                              : 0.f;
+                    float lt = readlane_f(w, 0), kt = readlane_f(wk, 0);
+                    for (int q = 1; q < g.K; ++q) {
+                        lt += readlane_f(w, q);
+                        kt += readlane_f(wk, q);
+                    }
                     lmb = lt;
+                    klmb = kt;
                 }
                 AGX_STAMP(64 + 13);
             }
@@ -1134,6 +1173,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 t1 += stat[kNW + i];
             }
             if (tid == 0) loss_total += lmb;
+            kl_total += (double)klmb;
+            ++n_done;
             AGX_STAMP(64 + 14);
             const float c0 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t0) + 1e-6f), 1.f) : 1.f;
             const float c1 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t1) + 1e-6f), 1.f) : 1.f;
@@ -1187,7 +1228,11 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             __syncthreads();
             AGX_STAMP(64 + 10);
         }  // minibatches
-    }      // epochs
+        ++epochs_done;
+        // target-KL early stop after the epoch (ppo.py:917-918); every partner
+        // holds the same fixed-order kl words, so all take the same branch
+        if (g.target_kl > 0.0 && kl_total / (double)n_done > g.target_kl) break;
+    }  // epochs
 
     // ---- write parameters and moments back (partners hold identical copies) ------
     if (kk != 0) return;
@@ -1202,7 +1247,12 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             gv[f] = av[i];
         }
     }
-    if (tid == 0 && g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)g.E);
+    if (tid == 0) {
+        if (g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)g.E);
+        if (g.kl_out) g.kl_out[p] = n_done ? (float)(kl_total / (double)n_done) : 0.f;
+        if (g.epochs_out) g.epochs_out[p] = epochs_done;
+        g.step[p] = step0 + n_done;
+    }
 #undef IC
 #undef BC
 }
@@ -1214,8 +1264,10 @@ __global__ void ppo_gather_kernel(const float *__restrict__ obs, const long long
                                   const float *__restrict__ old_logp, const float *__restrict__ adv,
                                   const float *__restrict__ ret, const float *__restrict__ old_v,
                                   const double *__restrict__ adv_stats, const long long *__restrict__ perms,
+                                  const unsigned char *__restrict__ masks, int A,
                                   long long S, int D, int P, float *__restrict__ gobs, int *__restrict__ gact,
-                                  float *__restrict__ grow, unsigned *__restrict__ counters, int ncounters) {
+                                  unsigned *__restrict__ gmask, float *__restrict__ grow,
+                                  unsigned *__restrict__ counters, int ncounters) {
     const int ep = blockIdx.y;  // e * P + p
     const int p = ep % P;
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1228,6 +1280,11 @@ __global__ void ppo_gather_kernel(const float *__restrict__ obs, const long long
     const size_t sp = (size_t)p * S + src;
     for (int d = 0; d < D; ++d) gobs[((size_t)ep * S + j) * D + d] = obs[sp * D + d];
     gact[(size_t)ep * S + j] = (int)act[sp];
+    if (masks) {  // [P][S][A] u8 -> one bit per action
+        unsigned bits = 0;
+        for (int a = 0; a < A; ++a) bits |= (masks[sp * A + a] != 0 ? 1u : 0u) << a;
+        gmask[(size_t)ep * S + j] = bits;
+    }
     float *gr = grow + (size_t)ep * 4 * S;
     double a = adv[sp];
     if (adv_stats) a = (a - adv_stats[2 * p]) * (1.0 / (adv_stats[2 * p + 1] + 1e-8));  // == adv_normalize_kernel
@@ -1281,6 +1338,12 @@ struct ActArgs {
     float *scores;        // [P*N] running episode score (on_policy.py:147-172), or null
     double *ret_sum;      // [P*N] sum of finished-episode returns
     long long *episodes;  // [P*N] finished-episode count
+    // legal-action masks (1 = legal): agent p, env n at mask + p*mask_pstride + n*A, or null;
+    // copied to mask_copy (rollout slot t, agent stride mask_copy_pstride) when set
+    const unsigned char *mask;
+    long long mask_pstride;
+    unsigned char *mask_copy;
+    long long mask_copy_pstride;
 };
 
 // The env staging may be host memory that the host rewrites between the
@@ -1364,7 +1427,13 @@ __device__ __forceinline__ void act_body(const ActArgs &g, float *sm, bool resid
     // categorical over 16 lanes per row
     const int r = wave + kNW * (lane >> 4), a = lane & 15;
     const bool live = r < nrow;
-    const float lg = a < pl.A ? sm[pl.l_lg + r * kMaxA + a] : -3.0e38f;
+    float lg = a < pl.A ? sm[pl.l_lg + r * kMaxA + a] : -3.0e38f;
+    if (g.mask && a < pl.A && live) {  // illegal -> -1e8 (apply_action_mask_discrete, distributions.py:16-28)
+        const size_t mo = (size_t)p * g.mask_pstride + (size_t)(n0 + r) * pl.A + a;
+        const unsigned char ok = ld_sys_u8(g.mask + mo);
+        if (g.mask_copy) g.mask_copy[(size_t)p * g.mask_copy_pstride + (size_t)(n0 + r) * pl.A + a] = ok;
+        if (!ok) lg = -1.0e8f;
+    }
     const float mx = row_max(lg);
     const float lse = mx + logf(row_sum(a < pl.A ? expf(lg - mx) : 0.f));
     const float pa = a < pl.A ? expf(lg - lse) : 0.f;
@@ -1499,6 +1568,7 @@ struct Launcher {
     void (*act)(const ActArgs &, dim3 grid, size_t lds, hipStream_t);
     void (*persist)(const ActArgs *, int, agx_rollout_ctl *, unsigned long long, unsigned, long long *, dim3 grid,
                     size_t lds, hipStream_t);
+    int (*persist_occupancy)(size_t lds);  // co-resident persistent workgroups per CU
 };
 
 template <class C>
@@ -1521,6 +1591,16 @@ static void launch_act(const ActArgs &a, dim3 grid, size_t lds, hipStream_t s) {
 }
 
 template <class C>
+static int persist_occupancy(size_t lds) {
+    (void)hipFuncSetAttribute((const void *)ppo_rollout_persistent_kernel<C>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ppo_rollout_persistent_kernel<C>, kNT, lds) != hipSuccess)
+        return 0;
+    return n;
+}
+
+template <class C>
 static void launch_persist(const ActArgs *steps, int nsteps, agx_rollout_ctl *ctl, unsigned long long ticks,
                            unsigned base, long long *stamps, dim3 grid, size_t lds, hipStream_t s) {
     static bool attr = false;
@@ -1539,7 +1619,7 @@ static bool find_launcher(const agx_ppo_net *net, Launcher &out) {
         using C = Shape<D_, A_, NE_, E0, E1, E2, HA, HC>;                                             \
         static_assert(C::plan.ok, "instantiated PPO shape must have a valid plan");                   \
         if (dims_match(net, C::dims) && same_layout(net, C::plan)) {                                  \
-            out = Launcher{&C::plan, &launch_learn<C>, &launch_act<C>, &launch_persist<C>};                               \
+            out = Launcher{&C::plan, &launch_learn<C>, &launch_act<C>, &launch_persist<C>, &persist_occupancy<C>};                               \
             return true;                                                                              \
         }                                                                                             \
     }
@@ -1587,7 +1667,7 @@ static int max_partners(int64_t P) {
     return k;
 }
 struct LearnWs {
-    size_t cnt, gobs, gact, grow, slabs, total;
+    size_t cnt, gobs, gact, gmask, grow, slabs, total;
 };
 static LearnWs learn_ws(const LearnPlan &pl, int64_t P, int64_t S, int64_t epochs) {
     LearnWs w;
@@ -1596,7 +1676,8 @@ static LearnWs learn_ws(const LearnPlan &pl, int64_t P, int64_t S, int64_t epoch
     w.cnt = 0;
     w.gobs = up(((size_t)P + 1) * 4);
     w.gact = w.gobs + up(per * pl.D * 4);
-    w.grow = w.gact + up(per * 4);
+    w.gmask = w.gact + up(per * 4);
+    w.grow = w.gmask + up(per * 4);
     w.slabs = w.grow + up(per * 4 * 4);
     const int K = max_partners(P);
     w.total = w.slabs + (K > 1 ? (size_t)P * 2 * K * pl.slab * 4 : 0);
@@ -1627,18 +1708,24 @@ extern "C" int agx_ppo_learn_prepare(const agx_ppo_net *net, void *workspace, vo
     return AGX_OK;
 }
 
-extern "C" int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, float *exp_avg,
-                             float *exp_avg_sq, const float *lr, float beta1, float beta2, float eps,
-                             int64_t adam_step0, const float *obs, const int64_t *actions,
-                             const float *old_logp, const float *adv, const double *adv_stats,
-                             const float *ret, const float *old_value, int64_t S, const int64_t *perms,
-                             int64_t epochs, int64_t batch, float clip_coef, float vf_coef, float ent_coef,
-                             float max_grad_norm, float *loss_out, void *workspace, void *stream) {
-    AGX_REQUIRE(net && params && exp_avg && exp_avg_sq && lr && obs && actions && old_logp && adv && ret &&
-                    old_value && perms && workspace,
+static int &g_debug_stall() {
+    static int v = 0;
+    return v;
+}
+extern "C" int agx_debug_learn_stall(int on) {
+    g_debug_stall() = on;
+    return AGX_OK;
+}
+
+extern "C" int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *x, void *workspace, void *stream) {
+    AGX_REQUIRE(net && x && workspace, "agx_ppo_learn: null net / args / workspace");
+    AGX_REQUIRE(x->params && x->exp_avg && x->exp_avg_sq && x->adam_step && x->lr && x->obs && x->actions &&
+                    x->old_logp && x->adv && x->ret && x->old_value && x->perms,
                 "agx_ppo_learn: null pointer");
-    AGX_REQUIRE(P > 0 && P <= 65535 && S > 0 && epochs > 0 && batch > 0 && epochs * P <= 65535,
-                "agx_ppo_learn: bad sizes");
+    const int64_t P = x->P, S = x->S, epochs = x->epochs, batch = x->batch;
+    AGX_REQUIRE(P > 0 && P <= 65535 && S > 0 && S < (1ll << 31) && epochs > 0 && batch > 0 && epochs * P <= 65535,
+                "agx_ppo_learn: bad sizes P=%lld S=%lld epochs=%lld batch=%lld", (long long)P, (long long)S,
+                (long long)epochs, (long long)batch);
     Launcher L;
     if (!find_launcher(net, L)) {
         set_error("agx_ppo_learn: network shape not instantiated for the fused learner");
@@ -1650,6 +1737,7 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, f
     char *ws = static_cast<char *>(workspace);
     float *gobs = reinterpret_cast<float *>(ws + w.gobs);
     int *gact = reinterpret_cast<int *>(ws + w.gact);
+    unsigned *gmask = x->action_masks ? reinterpret_cast<unsigned *>(ws + w.gmask) : nullptr;
     float *grow = reinterpret_cast<float *>(ws + w.grow);
     const int64_t nsb = (batch + kSB - 1) / kSB;
     int K = max_partners(P);
@@ -1657,43 +1745,51 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, f
     AGX_REQUIRE(P * K <= 65535, "agx_ppo_learn: too many workgroups");
     // counters + timeout word: one 16-byte-multiple block at the workspace start, zeroed by the gather
     dim3 ggrid((unsigned)ceil_div(S, 256), (unsigned)(epochs * P));
-    ppo_gather_kernel<<<ggrid, 256, 0, s>>>(obs, reinterpret_cast<const long long *>(actions), old_logp, adv, ret,
-                                            old_value, adv_stats, reinterpret_cast<const long long *>(perms), S,
-                                            pl.D, (int)P, gobs, gact, grow, reinterpret_cast<unsigned *>(ws),
+    ppo_gather_kernel<<<ggrid, 256, 0, s>>>(x->obs, reinterpret_cast<const long long *>(x->actions), x->old_logp,
+                                            x->adv, x->ret, x->old_value, x->adv_stats,
+                                            reinterpret_cast<const long long *>(x->perms), x->action_masks, pl.A, S,
+                                            pl.D, (int)P, gobs, gact, gmask, grow, reinterpret_cast<unsigned *>(ws),
                                             (int)(w.gobs / sizeof(unsigned)));
     const int rc2 = check_launch("agx_ppo_learn gather");
     if (rc2) return rc2;
     LearnArgs a;
-    a.params = params;
-    a.m = exp_avg;
-    a.v = exp_avg_sq;
-    a.lr = lr;
-    a.b1 = beta1;
-    a.b2 = beta2;
-    a.eps = eps;
-    a.step0 = adam_step0;
+    a.params = x->params;
+    a.m = x->exp_avg;
+    a.v = x->exp_avg_sq;
+    a.lr = x->lr;
+    a.b1 = x->beta1;
+    a.b2 = x->beta2;
+    a.eps = x->eps;
+    a.step = reinterpret_cast<long long *>(x->adam_step);
     a.gobs = gobs;
     a.gact = gact;
+    a.gmask = gmask;
     a.grow = grow;
     a.S = S;
     a.E = (int)epochs;
     a.B = (int)batch;
     a.P = (int)P;
-    a.clip = clip_coef;
-    a.vf = vf_coef;
-    a.ent = ent_coef;
-    a.max_norm = max_grad_norm;
-    a.loss_out = loss_out;
+    a.clip = x->clip_coef;
+    a.vf = x->vf_coef;
+    a.ent = x->ent_coef;
+    a.max_norm = x->max_grad_norm;
+    a.target_kl = x->target_kl;
+    a.loss_out = x->loss_out;
+    a.kl_out = x->kl_out;
+    a.epochs_out = x->epochs_out;
+    a.err = x->error_word;
     a.stamps = g_stamps_ptr();
     a.K = K;
     a.slabs = reinterpret_cast<float *>(ws + w.slabs);
     a.cnt = reinterpret_cast<unsigned *>(ws);
+    a.debug_stall = K > 1 ? g_debug_stall() : 0;
     L.learn(a, (int)(P * K), (size_t)pl.lds_floats * sizeof(float), s);
     return check_launch("agx_ppo_learn");
 }
 
 extern "C" int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const float *params, const float *obs,
-                           int64_t obs_agent_stride, int sample, uint64_t seed, uint64_t counter,
+                           int64_t obs_agent_stride, const uint8_t *action_mask, int64_t mask_agent_stride,
+                           int sample, uint64_t seed, uint64_t counter,
                            int64_t *actions, float *log_probs, float *values, float *entropy,
                            int64_t out_agent_stride, int64_t *actions_flat, void *workspace, void *stream) {
     (void)workspace;
@@ -1729,6 +1825,10 @@ extern "C" int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const f
     a.scores = nullptr;
     a.ret_sum = nullptr;
     a.episodes = nullptr;
+    a.mask = action_mask;
+    a.mask_pstride = mask_agent_stride;
+    a.mask_copy = nullptr;
+    a.mask_copy_pstride = 0;
     dim3 grid((unsigned)ceil_div(N, kSB), (unsigned)P);
     L.act(a, grid, (size_t)L.plan->act_floats * sizeof(float), as_stream(stream));
     return check_launch("agx_ppo_act");
@@ -1761,6 +1861,10 @@ static void fill_rollout_args(ActArgs &a, const LearnPlan &pl, int64_t P, int64_
     a.scores = io->scores;
     a.ret_sum = io->return_sum;
     a.episodes = reinterpret_cast<long long *>(io->episodes);
+    a.mask = io->stage_mask;
+    a.mask_pstride = N * (int64_t)pl.A;
+    a.mask_copy = io->mask_slot;
+    a.mask_copy_pstride = io->mask_agent_stride;
 }
 
 static int check_rollout_io(const agx_rollout_io *io, int act, const float *params, const char *who) {
@@ -1791,6 +1895,16 @@ extern "C" int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N
 }
 
 extern "C" int64_t agx_rollout_workgroups(int64_t P, int64_t N) { return P * ceil_div(N, kSB); }
+
+// Every workgroup of a persistent rollout must be resident at once: the host
+// releases step t only after EVERY workgroup has finished step t-1, while the
+// resident ones spin on the release word — a grid larger than the GPU holds
+// would deadlock until the timeout.
+extern "C" int64_t agx_rollout_max_workgroups(const agx_ppo_net *net) {
+    Launcher L;
+    if (!find_launcher(net, L)) return 0;
+    return (int64_t)L.persist_occupancy((size_t)L.plan->act_floats * sizeof(float)) * cu_count();
+}
 extern "C" size_t agx_rollout_ctl_bytes(int64_t P, int64_t N) {
     const unsigned nwg = (unsigned)agx_rollout_workgroups(P, N);
     return (size_t)rollout_release_offset(nwg, nwg) * sizeof(unsigned);
@@ -1809,6 +1923,16 @@ extern "C" int agx_ppo_rollout_persistent(const agx_ppo_net *net, int64_t P, int
     if (!find_launcher(net, L)) {
         set_error("agx_ppo_rollout_persistent: network shape not instantiated");
         return AGX_EUNSUPPORTED;
+    }
+    {
+        const int64_t nwg = agx_rollout_workgroups(P, N);
+        const int64_t cap = (int64_t)L.persist_occupancy((size_t)L.plan->act_floats * sizeof(float)) * cu_count();
+        if (nwg > cap) {
+            set_error("agx_ppo_rollout_persistent: %lld workgroups cannot all be resident (the GPU holds %lld of "
+                      "this kernel at once); use per-step launches (agx_ppo_rollout_step)",
+                      (long long)nwg, (long long)cap);
+            return AGX_EUNSUPPORTED;
+        }
     }
     ActArgs *steps = static_cast<ActArgs *>(args_host);
     for (int64_t t = 0; t < nsteps; ++t) {

@@ -121,6 +121,21 @@ __global__ __launch_bounds__(kOptBlock) void clip_coef_kernel(const double *__re
 // (2) clip + Adam over one chunk.  Clip coefficients: from coef_dev when the
 // partials were pre-reduced (many chunks), else every block re-reduces its
 // agent's few partials in a fixed order.
+// Per-agent Adam bias corrections for this update (torch.optim.Adam,
+// single-tensor path: step_size = lr / (1 - b1^t), denom = sqrt(v) /
+// sqrt(1 - b2^t) + eps) from each agent's own step count; active agents'
+// counts advance by one.
+__global__ void adam_prep_kernel(long long *__restrict__ steps, const unsigned char *__restrict__ active, int P,
+                                 float b1, float b2, float *__restrict__ bc) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const bool on = !active || active[p];
+    const long long t = steps[p] + 1;
+    bc[2 * p] = (float)(1.0 - pow((double)b1, (double)t));
+    bc[2 * p + 1] = (float)sqrt(1.0 - pow((double)b2, (double)t));
+    if (on) steps[p] = t;
+}
+
 template <bool V4>
 __global__ __launch_bounds__(kOptBlock) void adam_kernel(float *__restrict__ params,
                                                          float *__restrict__ grads,
@@ -129,9 +144,12 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float *__restrict__ par
                                                          const double *__restrict__ part, int nsum,
                                                          const float *__restrict__ coef_dev,
                                                          const float *__restrict__ lr_dev,
-                                                         float b1, float b2, float eps, float bc1,
-                                                         float bc2_sqrt, int clip) {
+                                                         float b1, float b2, float eps,
+                                                         const float *__restrict__ bc,
+                                                         const unsigned char *__restrict__ active, int clip) {
     const int p = blockIdx.y;
+    if (active && !active[p]) return;  // this agent stopped (target_kl): untouched
+    const float bc1 = bc[2 * p], bc2_sqrt = bc[2 * p + 1];
     __shared__ float coef[kMaxGroups];
     if (threadIdx.x < kMaxGroups) {
         float c = 1.0f;
@@ -203,17 +221,18 @@ __global__ void polyak_kernel(float *__restrict__ t, const float *__restrict__ o
 using namespace agx;
 
 extern "C" size_t agx_adam_workspace_bytes(int64_t P, int64_t n) {
-    // partials [P][nblk][8] f64, then clip coefficients [P][8] f32
+    // partials [P][nblk][8] f64, then clip coefficients [P][8] f32, then bias corrections [P][2] f32
     return (size_t)P * (size_t)ceil_div(n, kSumChunk) * kMaxGroups * sizeof(double) +
-           (size_t)P * kMaxGroups * sizeof(float);
+           (size_t)P * kMaxGroups * sizeof(float) + (size_t)P * 2 * sizeof(float);
 }
 
 extern "C" int agx_clip_adam(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t P,
                              int64_t n, const int64_t *group_offsets, int G, float max_norm,
-                             const float *lr, float beta1, float beta2, float eps, int64_t step,
-                             void *workspace, void *stream) {
-    AGX_REQUIRE(params && grads && exp_avg && exp_avg_sq && lr && workspace, "agx_clip_adam: null pointer");
-    AGX_REQUIRE(P > 0 && P <= 65535 && n > 0 && G >= 1 && G <= kMaxGroups && step >= 1,
+                             const float *lr, float beta1, float beta2, float eps, int64_t *steps,
+                             const uint8_t *active, void *workspace, void *stream) {
+    AGX_REQUIRE(params && grads && exp_avg && exp_avg_sq && lr && steps && workspace,
+                "agx_clip_adam: null pointer");
+    AGX_REQUIRE(P > 0 && P <= 65535 && n > 0 && G >= 1 && G <= kMaxGroups,
                 "agx_clip_adam: bad shape P=%lld n=%lld G=%d", (long long)P, (long long)n, G);
     Groups gr;
     gr.G = G;
@@ -227,6 +246,11 @@ extern "C" int agx_clip_adam(float *params, float *grads, float *exp_avg, float 
     const bool v4 = n % 4 == 0 && ((uintptr_t)params | (uintptr_t)grads | (uintptr_t)exp_avg |
                                    (uintptr_t)exp_avg_sq) % 16 == 0;
     float *coef = nullptr;
+    float *bc = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) +
+                                          (size_t)P * nsum * kMaxGroups * sizeof(double) +
+                                          (size_t)P * kMaxGroups * sizeof(float));
+    adam_prep_kernel<<<(unsigned)ceil_div(P, 256), 256, 0, s>>>(reinterpret_cast<long long *>(steps), active, (int)P,
+                                                               beta1, beta2, bc);
     if (clip) {
         const dim3 sgrid((unsigned)nsum, (unsigned)P);
         if (v4) sumsq_kernel<true><<<sgrid, kOptBlock, 0, s>>>(grads, n, gr, part);
@@ -236,16 +260,12 @@ extern "C" int agx_clip_adam(float *params, float *grads, float *exp_avg, float 
             clip_coef_kernel<<<(unsigned)P, kOptBlock, 0, s>>>(part, (int)nsum, G, max_norm, coef);
         }
     }
-    const double bc1 = 1.0 - pow((double)beta1, (double)step);
-    const double bc2 = 1.0 - pow((double)beta2, (double)step);
     if (v4)
         adam_kernel<true><<<grid, kOptBlock, 0, s>>>(params, grads, exp_avg, exp_avg_sq, n, gr, max_norm, part,
-                                                     (int)nsum, coef, lr, beta1, beta2, eps, (float)bc1,
-                                                     (float)sqrt(bc2), clip);
+                                                     (int)nsum, coef, lr, beta1, beta2, eps, bc, active, clip);
     else
         adam_kernel<false><<<grid, kOptBlock, 0, s>>>(params, grads, exp_avg, exp_avg_sq, n, gr, max_norm, part,
-                                                      (int)nsum, coef, lr, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2),
-                                                      clip);
+                                                      (int)nsum, coef, lr, beta1, beta2, eps, bc, active, clip);
     return check_launch("agx_clip_adam");
 }
 

@@ -104,14 +104,30 @@ class PopulationSync:
         self._idx_ev.record()
         return out
 
+    def _row_buffers(self) -> list[torch.Tensor]:
+        """Every per-agent tensor a clone copies (agent.clone() deep-copies the
+        networks, the optimizer state and the hyperparameters): params, both
+        Adam moments, the learning rate and the Adam step count (int64 rows
+        viewed as two f32 words: moved bit for bit, never computed on)."""
+        pop, P = self.pop, self.pop.P
+        bufs = [pop.params.data, pop.opt.exp_avg, pop.opt.exp_avg_sq]
+        lr = getattr(pop.opt, "lr", None)
+        if isinstance(lr, torch.Tensor) and lr.shape == (P,):
+            bufs.append(lr.view(P, 1))
+        steps = getattr(pop.opt, "steps", None)
+        if isinstance(steps, torch.Tensor) and steps.shape == (P,) and steps.dtype == torch.int64:
+            bufs.append(steps.view(torch.float32).view(P, 2))
+        return bufs
+
     @torch.no_grad()
     def _clone_rows(self, parents: list[int]) -> None:
-        """Row j of this rank becomes global row parents[rank*P + j] (params and
-        both Adam moments).  Everything is enqueued on the current stream, in
-        order after the learner; the host does not wait."""
+        """Row j of this rank becomes global row parents[rank*P + j] (params,
+        both Adam moments, lr, Adam step).  Everything is enqueued on the
+        current stream, in order after the learner; the host does not wait."""
         pop, P, me = self.pop, self.pop.P, self.rank
-        bufs = (pop.params.data, pop.opt.exp_avg, pop.opt.exp_avg_sq)
-        n = bufs[0].shape[1]
+        bufs = self._row_buffers()
+        widths = [b.shape[1] for b in bufs]
+        offs = np.concatenate([[0], np.cumsum(widths)]).tolist()
         mine = parents[me * P:(me + 1) * P]
         if self.world == 1:  # a permutation-with-repeats of the rows: one gather per buffer
             if mine == list(range(P)):
@@ -136,7 +152,7 @@ class PopulationSync:
         for src in range(self.world):
             rows = need[me][src]
             if rows:
-                recv[src] = torch.empty(len(rows), 3 * n, dtype=bufs[0].dtype, device=pop.device)
+                recv[src] = torch.empty(len(rows), offs[-1], dtype=bufs[0].dtype, device=pop.device)
                 ops.append(dist.P2POp(dist.irecv, recv[src], src))
         local = [j for j in range(P) if mine[j] // P == me]
         snap = None
@@ -157,10 +173,14 @@ class PopulationSync:
             dst_idx = torch.as_tensor(js, device=pop.device)
             rows = msg.index_select(0, sel)
             for k, b in enumerate(bufs):
-                b.index_copy_(0, dst_idx, rows[:, k * n:(k + 1) * n])
+                b.index_copy_(0, dst_idx, rows[:, offs[k]:offs[k + 1]])
 
     @torch.no_grad()
     def generation(self) -> list[int]:
+        if self.rng_state is None and hasattr(self.pop, "discard_prefetch"):
+            # the tournament draws from the global numpy stream: put back any
+            # minibatch shuffles drawn ahead, so the draws keep the reference's order
+            self.pop.discard_prefetch()
         fit = self._fitness_host()
         self.history.append(fit)
         fits = [np.stack([h[i] for h in self.history[-self.eval_loop:]]) for i in range(len(fit))]

@@ -278,7 +278,8 @@ def c51_project_loss(q_next_online, target_dist, logp_cur, actions, rewards, don
 # optimiser                                                                   #
 # --------------------------------------------------------------------------- #
 class ClipAdam:
-    """Fused per-agent grad-norm clip + Adam over flat [P, n] buffers."""
+    """Fused per-agent grad-norm clip + Adam over flat [P, n] buffers, with a
+    per-agent Adam step count on the device (``steps``, int64 [P])."""
 
     def __init__(self, params: torch.Tensor, group_offsets, lr, betas=(0.9, 0.999), eps=1e-8,
                  max_norm=0.5, grads: torch.Tensor | None = None):
@@ -291,23 +292,24 @@ class ClipAdam:
         _need(self.grads, "grads", _f32, tuple(params.shape))
         self.exp_avg = torch.zeros_like(params)
         self.exp_avg_sq = torch.zeros_like(params)
+        self.steps = torch.zeros(P, dtype=torch.int64, device=params.device)
         self.offsets = (torch.tensor(list(group_offsets), dtype=torch.int64)).contiguous()
         if int(self.offsets[0]) != 0 or int(self.offsets[-1]) != n:
             raise ValueError("group offsets must span [0, n)")
         lr_t = torch.as_tensor(lr, dtype=_f32).reshape(-1)
         self.lr = (lr_t.expand(P) if lr_t.numel() == 1 else lr_t).to(params.device).contiguous()
         self.betas, self.eps, self.max_norm = betas, eps, max_norm
-        self.step_count = 0
         self.workspace = _ws(_lib.load().agx_adam_workspace_bytes(P, n), params.device)
 
-    def step(self):
-        self.step_count += 1
+    def step(self, active: torch.Tensor | None = None):
+        """One clip + Adam update of every agent (or of the agents whose
+        ``active`` u8 flag is set; the others are untouched)."""
         P, n = self.params.shape
         _lib.call("agx_clip_adam", self.params.data_ptr(), self.grads.data_ptr(),
                   self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), P, n,
                   self.offsets.data_ptr(), len(self.offsets) - 1, float(self.max_norm),
                   self.lr.data_ptr(), float(self.betas[0]), float(self.betas[1]), float(self.eps),
-                  self.step_count, self.workspace.data_ptr(), _lib.stream())
+                  self.steps.data_ptr(), _lib.ptr(active), self.workspace.data_ptr(), _lib.stream())
 
 
 def polyak_(target: torch.Tensor, online: torch.Tensor, tau: float) -> None:

@@ -55,6 +55,25 @@ def net_descriptor(spec: ActorCriticSpec) -> AgxPPONet | None:
     return d
 
 
+class AgxPPOLearnArgs(ctypes.Structure):
+    """Mirror of ``agx_ppo_learn_args`` (include/agx.h)."""
+
+    _fields_ = [
+        ("P", ctypes.c_int64), ("S", ctypes.c_int64), ("epochs", ctypes.c_int64), ("batch", ctypes.c_int64),
+        ("params", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
+        ("adam_step", ctypes.c_void_p), ("lr", ctypes.c_void_p),
+        ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
+        ("max_grad_norm", ctypes.c_float),
+        ("obs", ctypes.c_void_p), ("actions", ctypes.c_void_p), ("old_logp", ctypes.c_void_p),
+        ("adv", ctypes.c_void_p), ("ret", ctypes.c_void_p), ("old_value", ctypes.c_void_p),
+        ("adv_stats", ctypes.c_void_p), ("action_masks", ctypes.c_void_p), ("perms", ctypes.c_void_p),
+        ("clip_coef", ctypes.c_float), ("vf_coef", ctypes.c_float), ("ent_coef", ctypes.c_float),
+        ("target_kl", ctypes.c_double),
+        ("loss_out", ctypes.c_void_p), ("kl_out", ctypes.c_void_p), ("epochs_out", ctypes.c_void_p),
+        ("error_word", ctypes.c_void_p),
+    ]
+
+
 class FusedLearner:
     def __init__(self, pop):
         self.desc = net_descriptor(pop.spec)
@@ -66,7 +85,11 @@ class FusedLearner:
         _lib.check(lib.agx_ppo_learn_prepare(ctypes.byref(self.desc), self.ws.data_ptr(), _lib.stream()),
                    "agx_ppo_learn_prepare")
         self.loss = torch.zeros(pop.P, dtype=torch.float32, device=pop.device)
-        self.args = None
+        self.kl = torch.zeros(pop.P, dtype=torch.float32, device=pop.device)
+        self.epochs_run = torch.zeros(pop.P, dtype=torch.int32, device=pop.device)
+        self.args = AgxPPOLearnArgs()
+        self.key = None
+        self.fn = lib.agx_ppo_learn
 
     def learn(self, pop, perms: torch.Tensor | None = None) -> torch.Tensor:
         """All epochs x minibatches of every agent in two launches (gather +
@@ -76,27 +99,35 @@ class FusedLearner:
             perms = pop.permutations()
         opt = pop.opt
         b1, b2 = opt.betas
-        # the argument list is built once per set of buffers; per call only the
-        # Adam step, the permutations and the stream change (host time between
-        # the rollout and the learner is on the critical path)
+        masks = pop.action_masks
+        # the argument block is rebuilt only when a buffer or hyperparameter
+        # changes; per call only the permutations and the stream change (host
+        # time between the rollout and the learner is on the critical path)
         key = (pop.params.data.data_ptr(), opt.exp_avg.data_ptr(), opt.exp_avg_sq.data_ptr(), opt.lr.data_ptr(),
-               pop.obs.data_ptr(), pop.advantages.data_ptr(), pop.returns.data_ptr(), pop.values.data_ptr(),
-               pop.log_probs.data_ptr(), pop.actions.data_ptr(), pop.adv_stats.data_ptr(), float(b1), float(b2),
-               float(opt.eps), pop.batch_size, pop.update_epochs, float(pop.clip_coef), float(pop.vf_coef),
-               float(pop.ent_coef), float(pop.max_grad_norm))
-        if self.args is None or self.args[0] != key:
-            a = [ctypes.byref(self.desc), pop.P, key[0], key[1], key[2], key[3], key[11], key[12], key[13], 0,
-                 key[4], key[9], key[8], key[5], key[10], key[6], key[7], pop.S, 0, pop.update_epochs,
-                 pop.batch_size, key[16], key[17], key[18], key[19], self.loss.data_ptr(), self.ws.data_ptr(), 0]
-            self.args = (key, a, _lib.load().agx_ppo_learn)
-        a, fn = self.args[1], self.args[2]
-        a[9] = opt.step_count
-        a[18] = perms.data_ptr()
-        a[27] = torch.cuda.current_stream(pop.device).cuda_stream
-        rc = fn(*a)
+               opt.steps.data_ptr(), pop.obs.data_ptr(), pop.advantages.data_ptr(), pop.returns.data_ptr(),
+               pop.values.data_ptr(), pop.log_probs.data_ptr(), pop.actions.data_ptr(), pop.adv_stats.data_ptr(),
+               None if masks is None else masks.data_ptr(), float(b1), float(b2), float(opt.eps), pop.batch_size,
+               pop.update_epochs, float(pop.clip_coef), float(pop.vf_coef), float(pop.ent_coef),
+               float(pop.max_grad_norm), float(pop.target_kl or 0.0), pop.err_word.data_ptr())
+        if self.key != key:
+            a = self.args
+            a.P, a.S, a.epochs, a.batch = pop.P, pop.S, pop.update_epochs, pop.batch_size
+            a.params, a.exp_avg, a.exp_avg_sq = key[0], key[1], key[2]
+            a.lr, a.adam_step = key[3], key[4]
+            a.beta1, a.beta2, a.eps, a.max_grad_norm = key[13], key[14], key[15], key[21]
+            a.obs, a.actions, a.old_logp = key[5], key[10], key[9]
+            a.adv, a.ret, a.old_value, a.adv_stats = key[6], key[7], key[8], key[11]
+            a.action_masks = key[12]
+            a.clip_coef, a.vf_coef, a.ent_coef, a.target_kl = key[18], key[19], key[20], key[22]
+            a.loss_out, a.kl_out = self.loss.data_ptr(), self.kl.data_ptr()
+            a.epochs_out, a.error_word = self.epochs_run.data_ptr(), key[23]
+            self.key = key
+            self.aref = ctypes.byref(self.args)
+            self.dref = ctypes.byref(self.desc)
+        self.args.perms = perms.data_ptr()
+        rc = self.fn(self.dref, self.aref, self.ws.data_ptr(), torch.cuda.current_stream(pop.device).cuda_stream)
         if rc != 0:
             _lib.check(rc, "agx_ppo_learn")
-        opt.step_count += pop.update_epochs * pop.n_minibatches()
         return self.loss
 
     def timed_out(self, pop) -> bool:
@@ -115,8 +146,9 @@ def fused_learn(pop, perms=None) -> torch.Tensor:
 
 def policy_step(pop, desc: AgxPPONet, obs: torch.Tensor, obs_agent_stride: int, *, sample: bool, counter: int,
                 actions=None, log_probs=None, values=None, entropy=None, out_agent_stride: int = 0,
-                actions_flat=None) -> None:
+                actions_flat=None, action_mask=None, mask_agent_stride: int = 0) -> None:
     """agx_ppo_act over all P agents x N envs (PPO.get_action, ppo.py:567-633)."""
     _lib.call("agx_ppo_act", ctypes.byref(desc), pop.P, pop.N, pop.params.data.data_ptr(), obs.data_ptr(),
-              obs_agent_stride, 1 if sample else 0, pop.act_seed, counter, _lib.ptr(actions), _lib.ptr(log_probs),
-              _lib.ptr(values), _lib.ptr(entropy), out_agent_stride, _lib.ptr(actions_flat), None, _lib.stream())
+              obs_agent_stride, _lib.ptr(action_mask), mask_agent_stride, 1 if sample else 0, pop.act_seed, counter,
+              _lib.ptr(actions), _lib.ptr(log_probs), _lib.ptr(values), _lib.ptr(entropy), out_agent_stride,
+              _lib.ptr(actions_flat), None, _lib.stream())

@@ -15,7 +15,12 @@ Reference behaviour mirrored per agent:
 The population axis replaces the reference's sequential agent loop
 (train_on_policy.py:210): every kernel processes all P agents at once.
 Sampling uses an on-device Gumbel-max draw (the reference's torch.multinomial
-stream cannot be reproduced on a GPU generator anyway).
+stream cannot be reproduced on a GPU generator anyway).  Minibatch order is
+the reference's: by default the permutations come from numpy's global
+legacy MT19937 exactly as PPO.learn's ``np.random.shuffle`` draws them
+(``perm_source="numpy"``, agilerl_amd/rng.py); ``perm_source="device"``
+draws them on the GPU instead (no host work, not reproducible against the
+reference).
 
 Two learner back ends share this state:
   * ``fused=True``  one persistent HIP workgroup per agent runs all E x M
@@ -32,9 +37,12 @@ from __future__ import annotations
 import math
 import os
 
+import numpy as np
 import torch
 
+from .. import _lib
 from .. import kernels as K
+from ..rng import numpy_shuffle_perms
 from .nets import ActorCriticSpec, categorical
 
 
@@ -62,7 +70,7 @@ class PPOPopulation:
     def __init__(self, spec: ActorCriticSpec, pop_size: int, num_envs: int, *, learn_step=2048,
                  batch_size=128, lr=1e-3, gamma=0.99, gae_lambda=0.95, clip_coef=0.2, ent_coef=0.01,
                  vf_coef=0.5, max_grad_norm=0.5, update_epochs=4, target_kl=None, seeds=None,
-                 device="cuda", fused=True):
+                 device="cuda", fused=True, perm_source="numpy", action_masks=False):
         self.spec = spec
         self.P, self.N = int(pop_size), int(num_envs)
         self.T = -(learn_step // -self.N)  # capacity = ceil(learn_step / num_envs), ppo.py:363
@@ -83,6 +91,13 @@ class PPOPopulation:
                               grads=self.params.grad)
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(int(seeds[0]) * 7919 + 17)
+        if perm_source not in ("numpy", "device"):
+            raise ValueError("perm_source must be 'numpy' or 'device'")
+        self.perm_source = perm_source
+        self.use_action_masks = bool(action_masks)
+        # sticky device error word of the fused learner (partner timeout); checked at host sync points
+        self.err_word = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.last_kl = None
         self.fused = fused
         self.act_seed = (int(seeds[0]) * 0x9E3779B97F4A7C15 + 0x5851F42D) & 0xFFFFFFFFFFFFFFFF
         self.act_counter = 0
@@ -93,6 +108,8 @@ class PPOPopulation:
         self.prefetch_perms = os.environ.get("AGX_PREFETCH_PERMS", "1") != "0"
         self._perm_next = None
         self._perm_stream = None
+        self._perm_host = None
+        self._perm_k = 0
         self._gae_launch = None
 
     # ------------------------------------------------------------------ #
@@ -108,6 +125,9 @@ class PPOPopulation:
         self.advantages = torch.zeros(P, T, N, **f32)
         self.returns = torch.zeros(P, T, N, **f32)
         self.adv_stats = torch.zeros(P, 2, dtype=torch.float64, device=dev)
+        # legal-action masks (1 = legal) stored with the rollout when the env provides them
+        self.action_masks = (torch.ones(P, T, N, self.spec.n_actions, dtype=torch.uint8, device=dev)
+                             if self.use_action_masks else None)
         self.gae_ws = torch.empty(max(16, K._lib.load().agx_gae_workspace_bytes(P, T, N)), dtype=torch.uint8,
                                   device=dev)
 
@@ -185,62 +205,124 @@ class PPOPopulation:
         self._gae_launch = (key, launch, last_value, last_done)
 
     # ------------------------------------------------------------------ #
-    def learn(self) -> torch.Tensor:
+    def learn(self, prefetch: bool = True) -> torch.Tensor:
         """One PPO update of every agent; returns the reference's mean_loss per
-        agent (device tensor [P], no host sync)."""
+        agent (device tensor [P], no host sync).  ``prefetch``: draw the next
+        learn's permutations right away (the pipelined runner passes False and
+        prefetches after pacing the rollout instead)."""
         self.learn_steps += 1
-        if self.target_kl is None and self.fused_descriptor() is not None:
+        if self.fused_descriptor() is not None:
             from .learner import fused_learn
 
             loss = fused_learn(self)
-            if self.prefetch_perms:
+            self.last_kl = self._fused.kl
+            if prefetch and self.prefetch_perms:
                 self.prefetch_permutations()
             return loss
         return self._learn_torch()
+
+    def check_errors(self) -> None:
+        """Raise AgxError if a fused learn() since the last check left an agent's
+        update incomplete (a partner workgroup timed out); resets the word.
+        Synchronises with the device."""
+        if int(self.err_word.item()) != 0:
+            self.err_word.zero_()
+            raise _lib.AgxError("agx_ppo_learn: a partner workgroup timed out; the population's parameters are "
+                                "incomplete for this learn()")
 
     def minibatch_plan(self):
         b = self.batch_size
         return [(s, min(s + b, self.S)) for s in range(0, self.S, b)]
 
     def permutations(self) -> torch.Tensor:
-        """[E, P, S] int64 per-agent shuffles (the reference's np.random.shuffle
-        per epoch, ppo.py:842), drawn on the device.  Returns the draw made
-        ahead by prefetch_permutations() if there is one (the same draw, in
-        the same order, as drawing here)."""
+        """[E, P, S] int64 per-agent minibatch orders for the next learn():
+        numpy's global np.random.shuffle stream (default, ppo.py:836-842) or a
+        device draw.  Returns the draw made ahead by prefetch_permutations()
+        if there is one (the same draw, in the same order, as drawing here)."""
         if self._perm_next is not None:
-            perms, ev = self._perm_next
+            perms, ev, _ = self._perm_next
             self._perm_next = None
             main = torch.cuda.current_stream(self.device)
             main.wait_event(ev)
             perms.record_stream(main)
             return perms
+        if self.perm_source == "numpy":
+            host = self._host_perm_buffer()
+            numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=host.numpy())
+            perms = host.to(self.device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._perm_host[self._perm_k ^ 1][1] = ev
+            return perms
         keys = torch.rand(self.update_epochs, self.P, self.S, generator=self.gen, device=self.device)
         return torch.argsort(keys, dim=-1)
 
+    def _host_perm_buffer(self) -> torch.Tensor:
+        """One of two pinned [E, P, S] int64 host buffers, alternating (the H2D
+        copy that last read a buffer finished long before it is reused: it
+        precedes a whole learn() on the stream; checked by its event)."""
+        if self._perm_host is None:
+            shape = (self.update_epochs, self.P, self.S)
+            self._perm_host = [[torch.empty(shape, dtype=torch.int64, pin_memory=True), None] for _ in range(2)]
+        slot = self._perm_host[self._perm_k]
+        self._perm_k ^= 1
+        if slot[1] is not None:
+            slot[1].synchronize()
+        return slot[0]
+
     def prefetch_permutations(self) -> None:
-        """Draw the next permutations on a side stream now (rand + a radix
-        sort, ~35 us of small launches), so they run beside the learner and
-        the next rollout instead of between them.  Only the fused path calls
-        it: there the generator draws nothing else, so the sequence of draws
-        is unchanged."""
+        """Draw the next learn's permutations now, off the critical path:
+        device mode enqueues rand + a radix sort on a side stream (beside the
+        learner and the next rollout); numpy mode runs the native host shuffle
+        (~0.5 ms of host time while the GPU learns) and an async H2D copy.
+        Anything else that draws from the global numpy generator in between
+        (tournament selection, mutations) must call discard_prefetch() first,
+        so the draws stay in the reference's order."""
         if self._perm_next is not None or self.device.type != "cuda":
             return
         if self._perm_stream is None:
             self._perm_stream = torch.cuda.Stream(device=self.device)
         side = self._perm_stream
-        side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(side):
-            keys = torch.rand(self.update_epochs, self.P, self.S, generator=self.gen, device=self.device)
-            perms = torch.argsort(keys, dim=-1)
-            ev = torch.cuda.Event()
-            ev.record(side)
-        self._perm_next = (perms, ev)
+        state = None
+        if self.perm_source == "numpy":
+            state = np.random.get_state(legacy=True)
+            host = self._host_perm_buffer()
+            numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=host.numpy())
+            with torch.cuda.stream(side):
+                perms = host.to(self.device, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            self._perm_host[self._perm_k ^ 1][1] = ev
+        else:
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                keys = torch.rand(self.update_epochs, self.P, self.S, generator=self.gen, device=self.device)
+                perms = torch.argsort(keys, dim=-1)
+                ev = torch.cuda.Event()
+                ev.record(side)
+        self._perm_next = (perms, ev, state)
+
+    def discard_prefetch(self) -> None:
+        """Undo a prefetched numpy draw: the global numpy state goes back to
+        before it, so the next consumer of the stream draws what it would have
+        drawn without the prefetch (the permutations are re-drawn later)."""
+        if self._perm_next is None or self._perm_next[2] is None:
+            return  # nothing drawn ahead from numpy (device draws use the pop's own generator)
+        perms, ev, state = self._perm_next
+        self._perm_next = None
+        np.random.set_state(state)
 
     def _learn_torch(self, perms: torch.Tensor | None = None) -> torch.Tensor:
+        """Plain-PyTorch fp32 autograd learner over the stacked networks (HIP
+        loss and clip + Adam kernels): the numerics cross-check of the fused
+        kernel and the path for architectures it does not cover.  Same
+        semantics, including target-KL early stop per agent (stopped agents'
+        rows are left untouched) and action masks."""
         P, S, D = self.P, self.S, self.spec.obs_dim
         K.adv_normalize_(self.advantages, self.adv_stats)
         obs = self.obs.view(P, S, D)
         act = self.actions.view(P, S)
+        masks = None if self.action_masks is None else self.action_masks.view(P, S, -1)
         old_logp = self.log_probs.view(-1)
         adv = self.advantages.view(-1)
         ret = self.returns.view(-1)
@@ -249,12 +331,18 @@ class PPOPopulation:
         if perms is None:
             perms = self.permutations()
         total = torch.zeros(P, dtype=torch.float32, device=self.device)
+        kl_sum = torch.zeros(P, dtype=torch.float64, device=self.device)
+        n_mb = 0
+        active = None  # all agents until one stops (u8 [P])
         for e in range(self.update_epochs):
             for s0, s1 in self.minibatch_plan():
                 idx = perms[e][:, s0:s1]  # [P, b]
                 ob = torch.gather(obs, 1, idx.unsqueeze(-1).expand(-1, -1, D))
                 ac = torch.gather(act, 1, idx)
                 logits, value = self.spec.forward(self.params, ob)
+                if masks is not None:
+                    mk = torch.gather(masks, 1, idx.unsqueeze(-1).expand(-1, -1, masks.shape[-1]))
+                    logits = torch.where(mk.bool(), logits, torch.full_like(logits, -1e8))
                 logp_all, ent = categorical(logits)
                 logp = logp_all.gather(-1, ac.unsqueeze(-1)).squeeze(-1)
                 gidx = (idx + base).reshape(-1).contiguous()
@@ -262,8 +350,21 @@ class PPOPopulation:
                                                s1 - s0, self.clip_coef, self.vf_coef, self.ent_coef)
                 self.params.grad.zero_()
                 loss.backward()
-                self.opt.step()
-                total += stats[:, 0]
+                self.opt.step(active)
+                on = 1.0 if active is None else active.float()
+                total += stats[:, 0] * on
+                kl_sum += stats[:, 4].double() * (1.0 if active is None else active.double())
+                n_mb += 1
+            if self.target_kl is not None:
+                # np.mean(approx_kl_divs) over every minibatch so far (ppo.py:917-918)
+                stop = (kl_sum / n_mb > float(self.target_kl)).to(torch.uint8)
+                now = (1 - stop) if active is None else active * (1 - stop)
+                if int(now.sum()) == P and active is None:
+                    continue
+                active = now.contiguous()
+                if int(active.sum()) == 0:
+                    break
+        self.last_kl = (kl_sum / n_mb).float()
         return total / (S * self.update_epochs)
 
     # ------------------------------------------------------------------ #

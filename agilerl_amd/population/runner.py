@@ -52,6 +52,7 @@ class AgxRolloutIO(ctypes.Structure):
         ("actions", ctypes.c_void_p), ("log_probs", ctypes.c_void_p), ("values", ctypes.c_void_p),
         ("slot_agent_stride", ctypes.c_int64), ("actions_flat", ctypes.c_void_p),
         ("scores", ctypes.c_void_p), ("return_sum", ctypes.c_void_p), ("episodes", ctypes.c_void_p),
+        ("stage_mask", ctypes.c_void_p), ("mask_slot", ctypes.c_void_p), ("mask_agent_stride", ctypes.c_int64),
     ]
 
 
@@ -85,8 +86,15 @@ class PopulationRunner:
         P, N, D = pop.P, pop.N, pop.spec.obs_dim
         dev = pop.device
         self.zero_copy = os.environ.get("AGX_ZERO_COPY", "1") != "0"
+        desc = pop.fused_descriptor()
         self.persistent = (self.zero_copy and os.environ.get("AGX_PERSISTENT_ROLLOUT", "1") != "0"
-                           and pop.fused_descriptor() is not None)
+                           and desc is not None)
+        if self.persistent:
+            # every workgroup of the persistent launch must be co-resident (the
+            # host paces them in lock step); larger grids take per-step launches
+            lib = _lib.load()
+            if lib.agx_rollout_workgroups(P, N) > lib.agx_rollout_max_workgroups(ctypes.byref(desc)):
+                self.persistent = False
         if self.persistent:
             self.stage_h, self.obs_h, self.rew_h, self.done_h = _packed(P, N, D, owner=self)
             self.act_h = _coherent(self, P * N * 8).view(torch.int64)
@@ -358,7 +366,7 @@ class PopulationRunner:
     def iteration(self) -> torch.Tensor:
         """collect -> bootstrap + GAE -> learn; returns per-agent mean loss (device)."""
         desc = self.pop.fused_descriptor()
-        if self.persistent and desc is not None and self.pop.target_kl is None:
+        if self.persistent and desc is not None:
             return self._iteration_pipelined(desc)
         self.collect()
         self.pop.finish_rollout(self.last_obs, self.last_done,
@@ -383,6 +391,8 @@ class PopulationRunner:
         lib, ctl, base = self._launch_persistent(desc)
         self._finish_persistent()
         self.pop.finish_rollout(self.last_obs, self.last_done, self.last_value)
-        loss = self.pop.learn()
+        loss = self.pop.learn(prefetch=False)
         self._pace_persistent(lib, ctl, base)
+        if self.pop.prefetch_perms:  # next learn's minibatch orders: host work while the GPU learns
+            self.pop.prefetch_permutations()
         return loss

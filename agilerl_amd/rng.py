@@ -1,0 +1,45 @@
+"""The reference's host RNG streams, reproduced draw for draw.
+
+* PPO minibatch order: ``np.random.shuffle`` on numpy's GLOBAL legacy
+  RandomState (agilerl/algorithms/ppo.py:836-842), cumulative over the epochs
+  of one learn(), agents learning one after another
+  (train_on_policy.py:210).  ``numpy_shuffle_perms`` draws all of a
+  population's permutations natively (agx_host_shuffle_perms) from the global
+  generator's state and advances that state exactly as the reference's
+  shuffles would, so a seeded run reproduces the reference's minibatches.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+def numpy_shuffle_perms(P: int, epochs: int, S: int, out: np.ndarray | None = None) -> np.ndarray:
+    """[epochs, P, S] int64: for agent p = 0..P-1 in turn, arange(S) shuffled
+    ``epochs`` times in place by the global ``np.random`` generator, row e =
+    the order after the (e+1)-th shuffle.  Equivalent to (and as fast as a
+    memcpy of) the Python loop::
+
+        for p in range(P):
+            idx = np.arange(S)
+            for e in range(epochs):
+                np.random.shuffle(idx); out[e, p] = idx
+    """
+    if out is None:
+        out = np.empty((epochs, P, S), dtype=np.int64)
+    if out.shape != (epochs, P, S) or out.dtype != np.int64 or not out.flags.c_contiguous:
+        raise ValueError("out must be a C-contiguous int64 array of shape (epochs, P, S)")
+    name, key, pos, has_gauss, gauss = np.random.get_state(legacy=True)
+    if name != "MT19937":
+        raise RuntimeError(f"global numpy generator is {name}, expected MT19937")
+    key = np.array(key, dtype=np.uint32)  # own, writable copy
+    pos_c = ctypes.c_int32(int(pos))
+    lib = _lib.load(require_gpu=False)  # host code: no device work
+    _lib.check(lib.agx_host_shuffle_perms(key.ctypes.data, ctypes.byref(pos_c), int(P), int(epochs), int(S),
+                                          out.ctypes.data), "agx_host_shuffle_perms")
+    np.random.set_state(("MT19937", key, int(pos_c.value), has_gauss, gauss))
+    return out

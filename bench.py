@@ -50,17 +50,46 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--roof-reps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="no GPU: gloo ranks run a trivial CPU step through the same launch, barrier and "
+                         "max-over-ranks timing (tests/test_bench_launch.py)")
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """``--gpus N`` (N > 1) without a torch.distributed launcher around us:
+    start N ranks as ONE child ``torch.distributed.run`` before this process
+    touches the GPU (no exec from a GPU-initialised process), relay its output
+    (rank 0 prints the JSON line) and return its exit code."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 # --------------------------------------------------------------------------- #
-def setup_dist():
+def setup_dist(gpu: bool = True):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if gpu:
+        torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gpu:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     return world, rank, local
 
 
@@ -72,9 +101,27 @@ def barrier(world):
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def dist_selftest(args, world, rank):
+    """The launch / barrier / max-over-ranks skeleton of main() on CPU ranks."""
+    x = torch.randn(256, 256)
+    for _ in range(args.warmup):
+        x = torch.tanh(x @ x.T * 1e-3)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x = torch.tanh(x @ x.T * 1e-3)
+    barrier(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    if rank == 0:
+        print(json.dumps({"metric": "dist selftest steps/s", "value": round(world * args.steps / dt, 1),
+                          "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(dt / args.steps * 1e3, 3), "selftest": True}))
 
 
 # --------------------------------------------------------------------------- #
@@ -502,9 +549,16 @@ def cpu_kernels_leg(seconds):
 # --------------------------------------------------------------------------- #
 def main():
     args = parse()
-    world, rank, local = setup_dist()
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    world, rank, local = setup_dist(gpu=not args.dist_selftest)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.dist_selftest:
+        dist_selftest(args, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     from agilerl_amd import _lib
 
     _lib.load()

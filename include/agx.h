@@ -110,30 +110,64 @@ size_t agx_ppo_learn_workspace_bytes(const agx_ppo_net *net, int64_t P, int64_t 
 /* Validates that `net` is one of the instantiated shapes (the kernel plan is
  * compile-time); no device work.  AGX_EUNSUPPORTED otherwise. */
 int agx_ppo_learn_prepare(const agx_ppo_net *net, void *workspace, void *stream);
-/* params / exp_avg / exp_avg_sq: [P][n_params] (updated in place);
- * lr: device f32 [P]; Adam steps adam_step0+1 ... are used for the
- * epochs*ceil(S/batch) updates; obs [P][S][obs_dim], actions int64 [P][S],
- * old_logp / adv / ret / old_value f32 [P][S]; adv_stats f64 [P][2]
- * (mean, unbiased std from agx_gae) normalises adv on the fly, or NULL when
- * adv is already normalised; perms int64 [epochs][P][S] (each row a
- * permutation of 0..S-1); loss_out f32 [P] = sum of minibatch losses /
- * (S * epochs) (ppo.py:920). */
-int agx_ppo_learn(const agx_ppo_net *net, int64_t P, float *params, float *exp_avg,
-                  float *exp_avg_sq, const float *lr, float beta1, float beta2, float eps,
-                  int64_t adam_step0, const float *obs, const int64_t *actions,
-                  const float *old_logp, const float *adv, const double *adv_stats,
-                  const float *ret, const float *old_value, int64_t S, const int64_t *perms,
-                  int64_t epochs, int64_t batch, float clip_coef, float vf_coef, float ent_coef,
-                  float max_grad_norm, float *loss_out, void *workspace, void *stream);
+/* Arguments of one agx_ppo_learn call (all device pointers, caller-owned).
+ *   params / exp_avg / exp_avg_sq  [P][n_params] f32, updated in place;
+ *   adam_step   [P] int64, in/out: Adam steps each agent has taken (the
+ *               1-based step of the next update is adam_step[p] + 1; an agent
+ *               that stops early on target_kl takes fewer);
+ *   lr          [P] f32 per-agent learning rate (HPO-mutable);
+ *   obs [P][S][obs_dim] f32, actions [P][S] int64, old_logp / adv / ret /
+ *   old_value [P][S] f32 — the rollout SoA flattened as get_tensor_batch
+ *   does (rollout_buffer.py:525-577), row t*N + n;
+ *   adv_stats   [P][2] f64 (mean, unbiased std; agx_gae) normalises adv on
+ *               the fly as ppo.py:829-834, or NULL when adv is normalised;
+ *   action_masks [P][S][n_actions] u8 (1 = legal) or NULL: illegal logits
+ *               become -1e8 before the log-softmax (distributions.py:16-28);
+ *   perms       [epochs][P][S] int64: epoch e, agent p visits rows
+ *               perms[e][p][0..S) in order (the reference's cumulative
+ *               np.random.shuffle stream, ppo.py:838-842);
+ *   target_kl   <= 0: off; else after every epoch an agent stops when the
+ *               mean approx_kl over all its minibatches so far exceeds it
+ *               (ppo.py:899-902, 917-918);
+ *   loss_out    [P] f32 = sum of minibatch losses / (S * epochs) (ppo.py:920);
+ *   kl_out      [P] f32 mean approx_kl over the minibatches run, or NULL;
+ *   epochs_out  [P] int32 epochs run, or NULL;
+ *   error_word  one uint32, sticky: the kernel ORs in 1 when a partner
+ *               workgroup gave up waiting (the agent's update is then
+ *               incomplete); never cleared by the library — the caller
+ *               checks and resets it (PPOPopulation raises AgxError). */
+typedef struct agx_ppo_learn_args {
+    int64_t P, S, epochs, batch;
+    float *params, *exp_avg, *exp_avg_sq;
+    int64_t *adam_step;
+    const float *lr;
+    float beta1, beta2, eps, max_grad_norm;
+    const float *obs;
+    const int64_t *actions;
+    const float *old_logp, *adv, *ret, *old_value;
+    const double *adv_stats;
+    const uint8_t *action_masks;
+    const int64_t *perms;
+    float clip_coef, vf_coef, ent_coef;
+    double target_kl;
+    float *loss_out, *kl_out;
+    int32_t *epochs_out;
+    uint32_t *error_word;
+} agx_ppo_learn_args;
+int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *args, void *workspace, void *stream);
 /* Rollout policy step (PPO.get_action / _get_action_and_values, ppo.py:
  * 400-633) for all P agents x N envs: obs of agent p, env n at
  * obs + p*obs_agent_stride + n*obs_dim; writes (each output may be NULL)
  * actions int64, log_probs, values, entropy at + p*out_agent_stride + n and
  * actions_flat[p*N + n].  sample=1: Gumbel-max draw from Philox4x32-10
  * keyed by seed, counter = (env index, step counter); sample=0: argmax.
+ * action_mask: NULL, or legal-action flags of agent p, env n at
+ * action_mask + p*mask_agent_stride + n*n_actions (u8, 1 = legal): illegal
+ * logits become -1e8 first (ppo.py:529-565, distributions.py:16-28).
  * `workspace` is unused (may be NULL). */
 int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
-                const float *obs, int64_t obs_agent_stride, int sample, uint64_t seed,
+                const float *obs, int64_t obs_agent_stride, const uint8_t *action_mask,
+                int64_t mask_agent_stride, int sample, uint64_t seed,
                 uint64_t counter, int64_t *actions, float *log_probs, float *values,
                 float *entropy, int64_t out_agent_stride, int64_t *actions_flat,
                 void *workspace, void *stream);
@@ -170,6 +204,13 @@ typedef struct agx_rollout_io {
     float *scores;                    /* [P*N] or NULL */
     double *return_sum;               /* [P*N] */
     int64_t *episodes;                /* [P*N] */
+    /* legal-action masks of this step ([P*N][n_actions] u8, 1 = legal, the
+     * env's info["action_mask"], on_policy.py:82-110) or NULL; illegal
+     * logits become -1e8 before sampling; copied to mask_slot (rollout
+     * slot t, agent stride mask_agent_stride) when that is set */
+    const uint8_t *stage_mask;
+    uint8_t *mask_slot;
+    int64_t mask_agent_stride;
 } agx_rollout_io;
 int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
                          const agx_rollout_io *io, int act, int sample, uint64_t seed,
@@ -201,12 +242,30 @@ typedef struct agx_rollout_ctl {
      * release line per workgroup: each workgroup polls its own copy of seq */
 } agx_rollout_ctl;
 int64_t agx_rollout_workgroups(int64_t P, int64_t N);
+/* Workgroups of the persistent rollout kernel for `net` the GPU holds at once
+ * (occupancy x CUs; 0: shape not instantiated).  Every workgroup of a
+ * persistent rollout must be resident together (the host paces them in lock
+ * step), so agx_ppo_rollout_persistent returns AGX_EUNSUPPORTED when
+ * agx_rollout_workgroups(P, N) exceeds this; callers then use per-step
+ * launches (agx_ppo_rollout_step). */
+int64_t agx_rollout_max_workgroups(const agx_ppo_net *net);
 size_t agx_rollout_ctl_bytes(int64_t P, int64_t N);
 size_t agx_rollout_args_bytes(int64_t nsteps);
 int agx_ppo_rollout_persistent(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
                                const agx_rollout_io *ios, int64_t nsteps, uint32_t base, uint64_t seed,
                                uint64_t counter0, void *args_host, agx_rollout_ctl *ctl, double timeout_s,
                                void *stream);
+/* ---- reference RNG streams (host) ----------------------------------------
+ * The minibatch permutations PPO._learn_from_rollout_buffer_flat draws from
+ * numpy's global legacy MT19937 (ppo.py:836-842: indices = arange(S) once
+ * per learn, np.random.shuffle(indices) per epoch), for P agents learning
+ * one after another as train_on_policy's agent loop does
+ * (train_on_policy.py:210): perms [epochs][P][S] in HOST memory.  mt_key
+ * [624] / mt_pos are numpy's state (np.random.get_state()[1:3]), advanced in
+ * place (the caller writes them back with np.random.set_state).  Host code,
+ * no device work. */
+int agx_host_shuffle_perms(uint32_t *mt_key, int32_t *mt_pos, int64_t P, int64_t epochs, int64_t S,
+                           int64_t *perms);
 /* Coherent (fine-grained) pinned host memory, device-accessible at the same
  * address; NULL on failure. */
 void *agx_host_alloc(size_t bytes);
@@ -312,13 +371,16 @@ int agx_c51_project_loss(const float *q_next_online, const float *target_dist,
  * params/grads/exp_avg/exp_avg_sq: [P][n]; the n parameters are split into
  * G clip groups by group_offsets[0..G] (host array, G <= 8); with
  * max_norm <= 0 nothing is clipped.  lr: device f32 [P] (per-agent learning
- * rates, mutable by HPO without recompiling a graph); step is the 1-based
- * Adam step count shared by the population. */
+ * rates, mutable by HPO without recompiling a graph); steps: device int64
+ * [P], in/out — each agent's Adam step count (this update uses steps[p]+1
+ * for the bias corrections and advances the counts of the agents it
+ * updates); active: device u8 [P] or NULL (all) — inactive agents' rows
+ * and counts are left untouched (agents stopped early by target_kl). */
 size_t agx_adam_workspace_bytes(int64_t P, int64_t n);
 int agx_clip_adam(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t P,
                   int64_t n, const int64_t *group_offsets, int G, float max_norm,
-                  const float *lr, float beta1, float beta2, float eps, int64_t step,
-                  void *workspace, void *stream);
+                  const float *lr, float beta1, float beta2, float eps, int64_t *steps,
+                  const uint8_t *active, void *workspace, void *stream);
 /* Polyak soft update target <- tau*online + (1-tau)*target
  * (dqn.py:349-358, dqn_rainbow.py:492-501). */
 int agx_polyak(float *target, const float *online, int64_t n, float tau, void *stream);
@@ -332,6 +394,11 @@ int agx_debug_pow(const double *x, const double *y, double *out, int64_t n, void
  * [sub_batch*16 + phase], phases 0-8 per sub-batch, 9-11 at slot 64+);
  * buf = NULL disables. */
 int agx_debug_learn_stamps(int64_t *buf);
+/* Test hook: on != 0 makes partner workgroup 1 of agent 0 skip every
+ * hand-off of subsequent agx_ppo_learn calls (when the call splits agents
+ * over partners), so the bounded partner wait times out and sets
+ * args->error_word — the failure path tests/test_population_gpu.py checks. */
+int agx_debug_learn_stall(int on);
 /* STREAM-style bandwidth probes for bench.py's measured HBM peak: mode 0
  * copies `bytes` (read + write, nontemporal stores), mode 1 reads them
  * (dst receives at most one float4 per block).  grid = 0: one block per

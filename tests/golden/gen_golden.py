@@ -15,7 +15,13 @@ Reference functions exercised (paths relative to /root/reference):
   * agilerl/components/replay_buffer.py:261-428   PrioritizedReplayBuffer (_update_priority,
                                                   _sample_proportional, _calculate_weights,
                                                   update_priorities)
-  * agilerl/algorithms/ppo.py:814-921             PPO._learn_from_rollout_buffer_flat (loss math)
+  * agilerl/algorithms/ppo.py:814-921             PPO._learn_from_rollout_buffer_flat (loss math;
+                                                  and end to end on a real actor-critic built by
+                                                  create_mlp, agilerl/utils/evolvable_networks.py:
+                                                  527-644, with log_prob_discrete / entropy_discrete,
+                                                  agilerl/utils/torch_utils.py:142-199, and
+                                                  apply_action_mask_discrete,
+                                                  agilerl/networks/distributions.py:16-28)
   * agilerl/algorithms/dqn.py:274-324             DQN.update (TD target)
   * agilerl/algorithms/dqn_rainbow.py:284-367     RainbowDQN._dqn_loss (C51 projection)
   * agilerl/hpo/tournament.py:41-119              TournamentSelection
@@ -50,6 +56,9 @@ class _StubMeta(type):
         if name.startswith("__"):
             raise AttributeError(name)
         return f"<stub {cls.__name__}.{name}>"
+
+    def __getitem__(cls, item):  # generic annotations (ModuleDict[EvolvableModule])
+        return cls
 
 
 class _StubModule(types.ModuleType):
@@ -89,6 +98,7 @@ def _install_stubs() -> None:
         "agilerl.modules",
         "agilerl.modules.base",
         "agilerl.modules.configs",
+        "agilerl.modules.custom_components",
         "agilerl.networks",
         "agilerl.networks.value_networks",
         "agilerl.networks.q_networks",
@@ -473,9 +483,167 @@ def gen_tournament(tour_mod, out: dict) -> None:
 
 
 # --------------------------------------------------------------------------- #
+# PPO learn() end to end                                                      #
+# --------------------------------------------------------------------------- #
+def _flat_names(mods: dict) -> dict:
+    """reference state-dict names -> tensors for the shared-encoder PPO:
+    actor.encoder.model.*, actor.head_net.model.*, critic.head_net.model.*"""
+    out = {}
+    for pre, m in mods.items():
+        for k, t in m.state_dict().items():
+            out[pre + k] = t.detach().clone().numpy()
+    return out
+
+
+def gen_ppo_learn(ppo_mod, en_mod, tu_mod, dist_mod, spaces_mod, out: dict) -> None:
+    """The reference's _learn_from_rollout_buffer_flat on a real network: the
+    encoder / heads are the reference's create_mlp modules (encoder:
+    output_layernorm, ReLU output; heads: output_vanish), evaluate_actions is
+    the shared-encoder forward of ppo.py:487-491 with log_prob_discrete /
+    entropy_discrete and apply_action_mask_discrete, and the optimizer is
+    torch.optim.Adam over actor + critic parameters (what OptimizerWrapper
+    builds).  Everything after evaluate_actions is the reference's own loop."""
+    PPO = ppo_mod.PPO
+    create_mlp = en_mod.create_mlp
+    cases = [
+        # (name, T, N, obs, A, enc, latent, actor, critic, batch, epochs, target_kl, masks, lr, seed)
+        ("learn0", 16, 128, 8, 4, [64], 64, [64], [64], 128, 4, None, False, 1e-3, 71),  # config 2
+        ("learn1", 15, 20, 4, 2, [64], 64, [64], [16], 64, 3, 0.004, True, 3e-3, 72),    # KL stop + masks
+        ("learn2", 16, 128, 8, 4, [64], 64, [64], [64], 128, 4, None, False, 1e-3, 73),  # Adam step > 0
+    ]
+    carry = None
+    for (name, T, N, D, A, enc, lat, ah, ch, bs, E, tkl, use_masks, lr, seed) in cases:
+        torch.manual_seed(seed)
+        encoder = create_mlp(D, lat, enc, output_vanish=False, output_activation="ReLU", layer_norm=True,
+                             output_layernorm=True, name="encoder")
+        actor_head = create_mlp(lat, A, ah, output_vanish=True, output_activation=None, layer_norm=True,
+                                name="actor")
+        critic_head = create_mlp(lat, 1, ch, output_vanish=True, output_activation=None, layer_norm=True,
+                                 name="value")
+        mods = {"actor.encoder.model.": encoder, "actor.head_net.model.": actor_head,
+                "critic.head_net.model.": critic_head}
+        if name == "learn2":  # continue learn0's agent (parameters + Adam state)
+            with torch.no_grad():
+                for pre, m in mods.items():
+                    for k, t in m.state_dict().items():
+                        t.copy_(torch.as_tensor(carry["state"][pre + k]))
+        params = [p for m in mods.values() for p in m.parameters()]
+        opt = torch.optim.Adam(params, lr=lr)
+        if name == "learn2":
+            names = [pre + k for pre, m in mods.items() for k, _ in m.named_parameters()]
+            for n_, p_ in zip(names, params):
+                opt.state[p_] = {"step": torch.tensor(float(carry["step"])),
+                                 "exp_avg": torch.as_tensor(carry["exp_avg"][n_]).clone(),
+                                 "exp_avg_sq": torch.as_tensor(carry["exp_avg_sq"][n_]).clone()}
+        init = _flat_names(mods)
+        rng = np.random.default_rng(seed)
+        S = T * N
+        obs = rng.standard_normal((S, D)).astype(np.float32)
+        masks = None
+        if use_masks:
+            masks = rng.random((S, A)) < 0.7
+            masks[np.arange(S), rng.integers(0, A, S)] = True  # at least one legal action
+        with torch.no_grad():
+            lat_t = encoder(torch.tensor(obs))
+            logits = actor_head(lat_t)
+            if masks is not None:
+                logits = dist_mod.apply_action_mask_discrete(logits, torch.tensor(masks))
+            probs = torch.softmax(logits, -1).numpy().astype(np.float64)
+            probs /= probs.sum(1, keepdims=True)
+            act = np.array([rng.choice(A, p=p) for p in probs], dtype=np.int64)
+            old_logp = tu_mod.log_prob_discrete(logits, torch.tensor(act)).numpy()
+            old_v = critic_head(lat_t).squeeze(-1).numpy()
+        old_logp = (old_logp + rng.normal(0, 0.02, S)).astype(np.float32)
+        old_v = (old_v + rng.normal(0, 0.1, S)).astype(np.float32)
+        adv = (rng.standard_normal(S) * 1.5 + 0.2).astype(np.float32)
+        ret = (old_v + rng.standard_normal(S)).astype(np.float32)
+
+        class _Net:
+            def __init__(self, ms):
+                self.ms = ms
+
+            def parameters(self):
+                return [p for m in self.ms for p in m.parameters()]
+
+        class _RB:
+            def size(self):
+                return S
+
+        fake = object.__new__(PPO)
+        fake.batch_size, fake.update_epochs = bs, E
+        fake.clip_coef, fake.vf_coef, fake.ent_coef = 0.2, 0.5, 0.01
+        fake.target_kl, fake.accelerator, fake.max_grad_norm = tkl, None, 0.5
+        fake.action_space = spaces_mod.Discrete()
+        fake.optimizer = opt
+        fake.actor, fake.critic = _Net([encoder, actor_head]), _Net([critic_head])
+        fake.rollout_buffer = _RB()
+        kls_seen: list = []
+
+        def _eval(obs, actions, hidden_state=None, action_mask=None):
+            lat_ = encoder(obs)
+            lg = actor_head(lat_)
+            if action_mask is not None:
+                lg = dist_mod.apply_action_mask_discrete(lg, action_mask)
+            lp = tu_mod.log_prob_discrete(lg, actions)
+            ent = tu_mod.entropy_discrete(lg)
+            return lp, ent, critic_head(lat_).squeeze(-1)
+
+        fake.evaluate_actions = _eval
+        td = dict(observations=torch.tensor(obs), actions=torch.tensor(act).view(S, 1).float(),
+                  log_probs=torch.tensor(old_logp), advantages=torch.tensor(adv), returns=torch.tensor(ret),
+                  values=torch.tensor(old_v))
+        if masks is not None:
+            td["action_masks"] = torch.tensor(masks)
+        td = _FakeTD(td)
+        np.random.seed(seed)
+        perm_state = np.random.get_state()
+        mean_loss = PPO._learn_from_rollout_buffer_flat(fake, buffer_td_external=td)
+        # replay the permutation stream the learner consumed (all E epochs drawn;
+        # an early stop uses a prefix)
+        np.random.set_state(perm_state)
+        perms = []
+        idx = np.arange(S)
+        for _ in range(E):
+            np.random.shuffle(idx)
+            perms.append(idx.copy())
+        final = _flat_names(mods)
+        names = [pre + k for pre, m in mods.items() for k, _ in m.named_parameters()]
+        m_out = {n_: opt.state[p_]["exp_avg"].numpy().copy() for n_, p_ in zip(names, params)}
+        v_out = {n_: opt.state[p_]["exp_avg_sq"].numpy().copy() for n_, p_ in zip(names, params)}
+        step = int(opt.state[params[0]]["step"])
+        n_mb = -(-S // bs)
+        rec = dict(T=np.int64(T), N=np.int64(N), obs_dim=np.int64(D), n_actions=np.int64(A),
+                   enc=np.array(enc, np.int64), latent=np.int64(lat), actor_hidden=np.array(ah, np.int64),
+                   critic_hidden=np.array(ch, np.int64), batch=np.int64(bs), epochs=np.int64(E),
+                   target_kl=np.float64(-1.0 if tkl is None else tkl), lr=np.float64(lr), seed=np.int64(seed),
+                   clip=np.float64(0.2), vf=np.float64(0.5), ent=np.float64(0.01), max_norm=np.float64(0.5),
+                   obs=obs, actions=act, old_logp=old_logp, old_v=old_v, adv=adv, ret=ret,
+                   perms=np.stack(perms).astype(np.int64), mean_loss=np.float64(mean_loss),
+                   step_in=np.int64(0 if carry is None or name != "learn2" else carry["step"]),
+                   step_out=np.int64(step), epochs_run=np.int64(step - (0 if name != "learn2" else carry["step"]))
+                   // n_mb)
+        if masks is not None:
+            rec["masks"] = masks.astype(np.uint8)
+        for n_, a_ in init.items():
+            rec["init." + n_] = a_
+            if name == "learn2":
+                rec["init_m." + n_] = carry["exp_avg"].get(n_, np.zeros_like(a_))
+                rec["init_v." + n_] = carry["exp_avg_sq"].get(n_, np.zeros_like(a_))
+        for n_, a_ in final.items():
+            rec["final." + n_] = a_
+        for n_ in names:
+            rec["m." + n_] = m_out[n_]
+            rec["v." + n_] = v_out[n_]
+        out[name] = rec
+        if name == "learn0":
+            carry = dict(state=final, exp_avg=m_out, exp_avg_sq=v_out, step=step)
+
+
+# --------------------------------------------------------------------------- #
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", nargs="*", default=None, help="write only these fixture groups")
     args = ap.parse_args()
     if not os.path.isdir(os.path.join(args.ref, "agilerl")):
         print("reference checkout not present; nothing generated")
@@ -490,6 +658,9 @@ def main() -> None:
     dqn = _load(ref, "agilerl.algorithms.dqn", "agilerl/algorithms/dqn.py")
     rainbow = _load(ref, "agilerl.algorithms.dqn_rainbow", "agilerl/algorithms/dqn_rainbow.py")
     tour = _load(ref, "agilerl.hpo.tournament", "agilerl/hpo/tournament.py")
+    tu = _load(ref, "agilerl.utils.torch_utils", "agilerl/utils/torch_utils.py")
+    en = _load(ref, "agilerl.utils.evolvable_networks", "agilerl/utils/evolvable_networks.py")
+    dist_mod = _load(ref, "agilerl.networks.distributions", "agilerl/networks/distributions.py")
 
     groups: dict[str, dict] = {}
     gen_gae(rb, groups)
@@ -499,14 +670,21 @@ def main() -> None:
     gen_dqn(dqn, groups)
     gen_c51(rainbow, groups)
     gen_tournament(tour, groups)
+    gen_ppo_learn(ppo, en, tu, dist_mod, sys.modules["gymnasium.spaces"], groups)
 
+    if args.only:
+        groups = {k: v for k, v in groups.items() if k in set(args.only)}
+        old = json.load(open(os.path.join(HERE, "META.json")))
+        groups_all = sorted(set(old.get("groups", [])) | set(groups))
+    else:
+        groups_all = sorted(groups)
     meta = {
         "generator": "tests/golden/gen_golden.py",
         "torch": torch.__version__,
         "numpy": np.__version__,
         "python": sys.version.split()[0],
         "reference_pins": {"torch": "2.9.0 (pyproject.toml:34)", "numpy": ">=2 (pyproject.toml:22)"},
-        "groups": sorted(groups),
+        "groups": groups_all,
     }
     for name, rec in groups.items():
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)

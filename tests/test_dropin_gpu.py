@@ -248,7 +248,7 @@ def test_ppo_checkpoint_round_trip(tmp_path):
     assert other.lr == 2e-3 and other.fitness == [0.5] and other.batch_size == 32
     assert torch.equal(other.population.params.data[0], agent.population.params.data[0])
     assert torch.equal(other.population.opt.exp_avg[0], agent.population.opt.exp_avg[0])
-    assert other.population.opt.step_count == agent.population.opt.step_count
+    assert torch.equal(other.population.opt.steps.cpu(), agent.population.opt.steps.cpu())
     obs = np.random.default_rng(0).standard_normal((16, 8)).astype(np.float32)
     _, lp0, ent0, v0 = agent.get_action(obs)
     _, lp1, ent1, v1 = other.get_action(obs)

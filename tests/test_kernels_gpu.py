@@ -62,6 +62,31 @@ def test_gae_population_bit_exact_vs_c_oracle(P, Tn, N, pd, use_gae):
             assert abs(st[p, 1] - s) <= 1e-9 * s
 
 
+def test_gae_full_size_section8d_bit_exact():
+    """The SURVEY §8d roofline shape itself (P=8, T=1024, N=8192: 67.1 M
+    transitions, done ~ Bernoulli(0.01)) against the C oracle: every advantage
+    and return bit for bit, plus the fused per-agent statistics."""
+    P, Tn, N = 8, 1024, 8192
+    rng = np.random.default_rng(0)
+    r = rng.standard_normal((P, Tn, N), dtype=np.float32)
+    v = rng.standard_normal((P, Tn, N), dtype=np.float32)
+    d = (rng.random((P, Tn, N), dtype=np.float32) < 0.01).astype(np.uint8)
+    lv = rng.standard_normal((P, N), dtype=np.float32)
+    ld = (rng.random((P, N)) < 0.01).astype(np.uint8)
+    adv, ret, stats = K().gae(T(r), T(d), T(v), T(lv), T(ld), 0.99, 0.95, True, with_stats=True)
+    ea, er = cref.gae(r, v, d, lv, ld, 0.99, 0.95, True, nthreads=16)
+    ga = adv.cpu().numpy()
+    assert np.array_equal(ga.view(np.uint32), ea.view(np.uint32))
+    del ga, adv
+    assert np.array_equal(ret.cpu().numpy().view(np.uint32), er.view(np.uint32))
+    st = stats.cpu().numpy()
+    for p in range(P):
+        a64 = ea[p].astype(np.float64)
+        m = a64.mean()
+        assert abs(st[p, 0] - m) <= 1e-9 * max(1.0, abs(m))
+        assert abs(st[p, 1] - a64.std(ddof=1)) <= 1e-9 * a64.std(ddof=1)
+
+
 def test_gae_bool_dones_and_normalize():
     rng = np.random.default_rng(7)
     r = rng.standard_normal((2, 40, 300)).astype(np.float32)

@@ -36,7 +36,7 @@ def _pop(P=3, N=16, learn_step=128, batch=64, epochs=1, seed=0, **kw):
 
 def _clone_state(pop):
     return (pop.params.data.clone(), pop.opt.exp_avg.clone(), pop.opt.exp_avg_sq.clone(),
-            pop.advantages.clone(), pop.opt.step_count)
+            pop.advantages.clone(), pop.opt.steps.clone())
 
 
 def _restore(pop, st):
@@ -44,7 +44,7 @@ def _restore(pop, st):
     pop.opt.exp_avg.copy_(st[1])
     pop.opt.exp_avg_sq.copy_(st[2])
     pop.advantages.copy_(st[3])
-    pop.opt.step_count = st[4]
+    pop.opt.steps.copy_(st[4])
 
 
 @pytest.mark.parametrize("N,learn_step,batch,epochs", [(16, 64, 64, 1), (16, 128, 64, 1), (8, 100, 32, 2),
@@ -135,8 +135,10 @@ def test_generation_behind_queued_learner_matches_synchronous():
 
     def make():
         spec = ActorCriticSpec(obs_dim=8, n_actions=4)
+        # two populations interleaved: each draws its minibatch orders from its
+        # own (identically seeded) device generator, not the shared numpy stream
         pop = PPOPopulation(spec, 6, 32, learn_step=256, batch_size=64, update_epochs=2, device=DEV,
-                            seeds=list(range(6)))
+                            seeds=list(range(6)), perm_source="device")
         return pop, PopulationRunner(pop, SyntheticVecEnv(6 * 32, seed=7, p_done=0.2))
 
     a_pop, a_run = make()
@@ -220,8 +222,8 @@ def test_policy_step_rejects_unsupported_shape():
     d = AgxPPONet()
     d.obs_dim, d.n_actions, d.n_enc = 7, 3, 2
     lib = _lib.load()
-    rc = lib.agx_ppo_act(ctypes_byref(d), 1, 1, None, None, 0, 0, 0, 0, None, None, None, None, 0, None, None,
-                         None)
+    rc = lib.agx_ppo_act(ctypes_byref(d), 1, 1, None, None, 0, None, 0, 0, 0, 0, None, None, None, None, 0, None,
+                         None, None)
     assert rc != 0
 
 
@@ -346,7 +348,7 @@ def _runner_pair(monkeypatch, persistent, P=3, N=40, seed=5):
     monkeypatch.setenv("AGX_PERSISTENT_ROLLOUT", "1" if persistent else "0")
     spec = ActorCriticSpec(obs_dim=8, n_actions=4)
     pop = PPOPopulation(spec, P, N, learn_step=8 * N, batch_size=64, update_epochs=2, device=DEV,
-                        seeds=list(range(P)), fused=True)
+                        seeds=list(range(P)), fused=True, perm_source="device")
     runner = PopulationRunner(pop, SyntheticVecEnv(P * N, seed=seed, p_done=0.2))
     assert runner.persistent == persistent
     return pop, runner
@@ -398,6 +400,46 @@ def test_persistent_rollout_abort_releases_kernel(monkeypatch):
     assert int(pop.actions.min()) >= 0 and int(pop.actions.max()) < 4
 
 
+def test_persistent_rollout_oversized_grid_falls_back():
+    """A grid the GPU cannot hold at once (every persistent workgroup must be
+    resident: the host paces them in lock step) is refused with
+    AGX_EUNSUPPORTED, and PopulationRunner takes the per-step launches
+    instead of deadlocking until the timeout."""
+    import ctypes
+
+    from agilerl_amd import _lib
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.population.runner import PopulationRunner
+
+    pop0 = _pop(P=2, N=32)
+    desc = pop0.fused_descriptor()
+    lib = _lib.load()
+    cap = int(lib.agx_rollout_max_workgroups(ctypes.byref(desc)))
+    assert cap >= 256  # at least one workgroup per CU
+    P = 2
+    N = 32 * (cap // P + 1)
+    assert lib.agx_rollout_workgroups(P, N) > cap
+    pop = _pop(P=P, N=N, learn_step=2 * N, batch=N)
+    run = PopulationRunner(pop, SyntheticVecEnv(P * N, seed=3))
+    assert not run.persistent
+    run.iteration()
+    torch.cuda.synchronize()
+    assert int(pop.actions.min()) >= 0 and int(pop.actions.max()) < 4
+    assert torch.isfinite(pop.params.data).all()
+    # and the ABI itself refuses the oversized persistent launch
+    from agilerl_amd.population.runner import AgxRolloutIO
+
+    ios = (AgxRolloutIO * 2)()
+    for t in range(2):
+        ios[t].stage_obs = pop.obs.data_ptr()
+    ctl = torch.zeros(4096, dtype=torch.uint8)
+    args = torch.zeros(4096, dtype=torch.uint8)
+    rc = lib.agx_ppo_rollout_persistent(ctypes.byref(desc), P, N, pop.params.data.data_ptr(), ios, 2, 0, 1, 0,
+                                        args.data_ptr(), ctl.data_ptr(), 1.0, _lib.stream())
+    assert rc == -3, rc  # AGX_EUNSUPPORTED, nothing launched
+    assert b"resident" in lib.agx_last_error()
+
+
 class _FixedEpisodeEnv:
     """Env e pays c[e] per step and terminates every L[e] steps, whatever
     the actions: PPO.test's fitness (ppo.py:1113-1289) is then known exactly."""
@@ -444,21 +486,31 @@ def test_population_evaluate_matches_test_semantics(max_steps):
     assert len(np.unique(np.concatenate(env.seen))) > 1
 
 
-def test_permutation_prefetch_keeps_the_draw_sequence(monkeypatch):
-    """learn() draws the next permutations on a side stream; the results are
-    bit-identical to drawing them at the start of every learn()."""
+@pytest.mark.parametrize("source", ["numpy", "device"])
+def test_permutation_prefetch_keeps_the_draw_sequence(monkeypatch, source):
+    """The runner draws the next learn's permutations ahead (numpy: host
+    shuffles after pacing the rollout; device: a side stream); the results
+    are bit-identical to drawing them at the start of every learn(), and the
+    global numpy stream ends where it would have."""
     from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.population_sync import PopulationSync
     from agilerl_amd.population.runner import PopulationRunner
 
     out = []
     for flag in ("1", "0"):
         monkeypatch.setenv("AGX_PREFETCH_PERMS", flag)
+        np.random.seed(11)
         pop = _pop(P=3, N=32, learn_step=256, batch=64, epochs=2)
+        pop.perm_source = source
         runner = PopulationRunner(pop, SyntheticVecEnv(3 * 32, seed=4, p_done=0.1))
-        for _ in range(3):
+        sync = PopulationSync(pop, runner, seed=None)  # tournament draws from the GLOBAL numpy stream
+        for i in range(4):
             runner.iteration()
+            if i == 1:
+                sync.generation()  # discards a prefetched numpy draw first
         explicit = pop.permutations()  # an explicit draw takes the prefetched one
         torch.cuda.synchronize()
-        out.append((pop.params.data.clone(), pop.opt.exp_avg.clone(), explicit.clone()))
+        out.append((pop.params.data.clone(), pop.opt.exp_avg.clone(), explicit.clone(),
+                    torch.as_tensor(np.random.random(4))))
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
