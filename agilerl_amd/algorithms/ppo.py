@@ -78,14 +78,18 @@ class PPO:
         assert isinstance(batch_size, int) and batch_size >= 1, "Batch size must be an integer greater than or equal to one."
         assert lr > 0, "Learning rate must be greater than zero."
         assert isinstance(learn_step, int) and learn_step >= 1, "Learn step rate must be an integer greater than or equal to one."
+        from ..hpo.registry import MutationRegistry
+
         self.observation_space, self.action_space = observation_space, action_space
         self.index = index
         self.net_config = net_config
-        self.batch_size, self.lr, self.learn_step = batch_size, lr, learn_step
+        self._learn_step = learn_step
         self.gamma, self.gae_lambda, self.mut = gamma, gae_lambda, mut
-        self.clip_coef, self.ent_coef, self.vf_coef = clip_coef, ent_coef, vf_coef
-        self.max_grad_norm, self.target_kl, self.update_epochs = max_grad_norm, target_kl, update_epochs
+        self.clip_coef, self.vf_coef = clip_coef, vf_coef
+        self.max_grad_norm, self.target_kl = max_grad_norm, target_kl
         self.num_envs = num_envs
+        # hyperparameters the HPO may mutate (core/base.py:301, registry.py:190-242)
+        self.registry = MutationRegistry(hp_config)
         self.device = torch.device(device)
         self.scores: list[float] = []
         self.fitness: list[float] = []
@@ -99,6 +103,77 @@ class PPO:
             _row = 0
         self.population, self.row = _population, int(_row)
         self._counter = 0
+        pop = self.population
+        if _population is not None and (batch_size, update_epochs, ent_coef) != (
+                pop.agent_batch[self.row], pop.agent_epochs[self.row], pop.agent_ent[self.row]):
+            self.batch_size, self.update_epochs, self.ent_coef = batch_size, update_epochs, ent_coef
+        if pop.agent_lr[self.row] != float(lr):
+            self.lr = lr
+
+    # ---- per-agent RL hyperparameters: rows of the population's tables ---- #
+    @property
+    def lr(self) -> float:
+        return self.population.agent_lr[self.row]
+
+    @lr.setter
+    def lr(self, value: float) -> None:
+        self.population.set_agent_hparam(self.row, "lr", value)
+
+    def reinit_optimizers(self, optimizer=None) -> None:
+        """core/base.py:760-775: a fresh Adam for this agent (zero moments and
+        step, current lr) — after an lr or a parameter mutation."""
+        self.population.reinit_agent_optimizer(self.row)
+
+    @property
+    def batch_size(self) -> int:
+        return int(self.population.agent_batch[self.row])
+
+    @batch_size.setter
+    def batch_size(self, value: int) -> None:
+        self.population.set_agent_hparam(self.row, "batch_size", int(value))
+
+    @property
+    def update_epochs(self) -> int:
+        return int(self.population.agent_epochs[self.row])
+
+    @update_epochs.setter
+    def update_epochs(self, value: int) -> None:
+        self.population.set_agent_hparam(self.row, "update_epochs", int(value))
+
+    @property
+    def ent_coef(self) -> float:
+        return float(self.population.agent_ent[self.row])
+
+    @ent_coef.setter
+    def ent_coef(self, value: float) -> None:
+        self.population.set_agent_hparam(self.row, "ent_coef", float(value))
+
+    @property
+    def learn_step(self) -> int:
+        return self._learn_step
+
+    @learn_step.setter
+    def learn_step(self, value: int) -> None:
+        if int(value) != self._learn_step:
+            self.population.set_agent_hparam(self.row, "learn_step", int(value))  # raises: shared rollout length
+
+    def get_lr_names(self) -> list[str]:
+        return ["lr"]
+
+    def policy_weights(self) -> dict[str, torch.Tensor]:
+        """The policy network's (actor: encoder + head) parameters by the
+        reference's actor state-dict names, as views of the HBM row (what
+        parameter mutations perturb, mutation.py:536-565; the critic's
+        encoder is the same memory, so the shared-encoder copy follows)."""
+        out = {}
+        for k, t in self.state_dict().items():
+            if k.startswith("actor."):
+                out[k[len("actor."):]] = t
+        return out
+
+    def mutation_hook(self) -> None:
+        """Shared-encoder hook (core/base.py): the critic encoder aliases the
+        actor encoder in the flat layout, so there is nothing to copy."""
 
     # ------------------------------------------------------------------ #
     @property

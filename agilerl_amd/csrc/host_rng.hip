@@ -80,16 +80,22 @@ struct MT {
 }  // namespace
 
 extern "C" int agx_host_shuffle_perms(uint32_t *mt_key, int32_t *mt_pos, int64_t P, int64_t epochs, int64_t S,
-                                      int64_t *perms) {
+                                      const int64_t *epochs_per_agent, int64_t *perms) {
     AGX_REQUIRE(mt_key && mt_pos && perms, "agx_host_shuffle_perms: null pointer");
     AGX_REQUIRE(P > 0 && epochs > 0 && S > 0 && *mt_pos >= 0 && *mt_pos <= kN,
                 "agx_host_shuffle_perms: bad arguments P=%lld epochs=%lld S=%lld pos=%d", (long long)P,
                 (long long)epochs, (long long)S, (int)*mt_pos);
+    if (epochs_per_agent)  // validate everything before the generator moves
+        for (int64_t p = 0; p < P; ++p)
+            AGX_REQUIRE(epochs_per_agent[p] >= 1 && epochs_per_agent[p] <= epochs,
+                        "agx_host_shuffle_perms: agent %lld epochs %lld outside [1, %lld]", (long long)p,
+                        (long long)epochs_per_agent[p], (long long)epochs);
     MT mt{mt_key, *mt_pos};
     for (int64_t p = 0; p < P; ++p) {
         int64_t *first = perms + (size_t)p * S;  // epoch 0 row of agent p
         for (int64_t i = 0; i < S; ++i) first[i] = i;
-        for (int64_t e = 0; e < epochs; ++e) {
+        const int64_t ep = epochs_per_agent ? epochs_per_agent[p] : epochs;
+        for (int64_t e = 0; e < ep; ++e) {
             int64_t *x = perms + ((size_t)e * P + p) * S;
             if (e > 0) std::memcpy(x, perms + ((size_t)(e - 1) * P + p) * S, (size_t)S * sizeof(int64_t));
             for (int64_t i = S - 1; i >= 1; --i) {

@@ -553,6 +553,9 @@ struct LearnArgs {
     int E, B, P;
     float clip, vf, ent, max_norm;
     double target_kl;      // <= 0: no early stop
+    const int *batch_p;    // [P] per-agent minibatch size, or null (B)
+    const int *epochs_p;   // [P] per-agent update epochs (<= E), or null (E)
+    const float *ent_p;    // [P] per-agent entropy coefficient, or null (ent)
     float *loss_out, *kl_out;
     int *epochs_out;
     unsigned *err;         // sticky error word (partner timeout)
@@ -615,7 +618,11 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
 
     constexpr int nmb_dummy = 0;
     (void)nmb_dummy;
-    const int nmb = (int)((S + g.B - 1) / g.B);
+    // per-agent hyperparameters (HPO mutations, mutation.py:413-453) or the population's
+    const int Bp = g.batch_p ? g.batch_p[p] : g.B;
+    const int Ep = g.epochs_p ? g.epochs_p[p] : g.E;
+    const float entp = g.ent_p ? g.ent_p[p] : g.ent;
+    const int nmb = (int)((S + Bp - 1) / Bp);
     float loss_total = 0.f;
     double kl_total = 0.0;  // sum of per-minibatch approx_kl (np.mean over all minibatches so far, ppo.py:917)
     int n_done = 0, epochs_done = 0;
@@ -628,14 +635,14 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     unsigned *legal = reinterpret_cast<unsigned *>(sm + pl.l_row + 5 * kSB);
     if (g.debug_stall && p == 0 && kk == 1) return;  // test hook: a partner that never arrives
 
-    for (int e = 0; e < g.E; ++e) {
+    for (int e = 0; e < Ep; ++e) {
         const float *eobs = g.gobs + ((size_t)e * g.P + p) * S * pl.D;
         const int *eact = g.gact + ((size_t)e * g.P + p) * S;
         const unsigned *emask = g.gmask ? g.gmask + ((size_t)e * g.P + p) * S : nullptr;
         const float *erow = g.grow + ((size_t)e * g.P + p) * 4 * S;
         for (int mb = 0; mb < nmb; ++mb) {
-            const long long s0 = (long long)mb * g.B;
-            const int bsz = (int)((s0 + g.B <= S) ? g.B : S - s0);
+            const long long s0 = (long long)mb * Bp;
+            const int bsz = (int)((s0 + Bp <= S) ? Bp : S - s0);
             const float inv_b = 1.f / (float)bsz;
             const int tid = vtid();
             f4 acc[kMaxSlot];
@@ -760,14 +767,14 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     const float gu = lu > lc ? 1.f : (lu == lc ? 0.5f : 0.f);
                     const float gc = lc > lu ? 1.f : (lu == lc ? 0.5f : 0.f);
                     const float inv = (dv >= -g.clip && dv <= g.clip) ? 1.f : 0.f;
-                    const float g_H = -g.ent * inv_b;
+                    const float g_H = -entp * inv_b;
                     const float dl = g_logp * ((a == a_t ? 1.f : 0.f) - pa) + g_H * pa * (gh - pg_dot);
                     if (a < pl.A) sm[pl.l_dlg + r * kMaxA + a] = (live && ok_a) ? dl : 0.f;
                     if (a == 0) {
                         sm[pl.l_dvb + r * kMaxA] =
                             live ? g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv) : 0.f;
                         if (live) {
-                            lsum += (fmaxf(p1, p2) + g.vf * 0.5f * fmaxf(lu, lc) - g.ent * Hs) * inv_b;
+                            lsum += (fmaxf(p1, p2) + g.vf * 0.5f * fmaxf(lu, lc) - entp * Hs) * inv_b;
                             klsum += ((ratio - 1.f) - lrt) * inv_b;  // approx_kl (ppo.py:899-902)
                         }
                     }
@@ -1248,7 +1255,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
         }
     }
     if (tid == 0) {
-        if (g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)g.E);
+        if (g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)Ep);
         if (g.kl_out) g.kl_out[p] = n_done ? (float)(kl_total / (double)n_done) : 0.f;
         if (g.epochs_out) g.epochs_out[p] = epochs_done;
         g.step[p] = step0 + n_done;
@@ -1774,6 +1781,9 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *x
     a.ent = x->ent_coef;
     a.max_norm = x->max_grad_norm;
     a.target_kl = x->target_kl;
+    a.batch_p = x->batch_per_agent;
+    a.epochs_p = x->epochs_per_agent;
+    a.ent_p = x->ent_coef_per_agent;
     a.loss_out = x->loss_out;
     a.kl_out = x->kl_out;
     a.epochs_out = x->epochs_out;

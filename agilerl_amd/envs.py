@@ -171,3 +171,78 @@ class SyntheticMultiAgentVecEnv:
 
     def close(self):
         pass
+
+
+class StackedVecEnv:
+    """P vector envs side by side as ONE vector env of sum(num_envs) envs, in
+    order (agent p of a population owns the p-th block).  Works with any
+    gymnasium-style vector env (``reset() -> (obs, info)``, ``step(a) ->
+    (obs, reward, terminated, truncated, info)``) and also offers the
+    ``out_*`` write-into-staging arguments PopulationRunner uses.  A per-step
+    ``info["action_mask"]`` is stacked the same way.
+
+    ``from_shared(env, copies)`` builds it from the reference's call-site env
+    (train_on_policy.py:210 shares ONE N-env between agents that take turns,
+    each turn starting from env.reset()): the population engine steps all
+    agents at once, so each agent gets its own deep copy of that env."""
+
+    def __init__(self, envs: list):
+        self.envs = list(envs)
+        self.sizes = [int(e.num_envs) for e in self.envs]
+        self.num_envs = int(sum(self.sizes))
+        e0 = self.envs[0]
+        for attr in ("single_observation_space", "single_action_space", "observation_space", "action_space"):
+            if hasattr(e0, attr):
+                setattr(self, attr, getattr(e0, attr))
+
+    @classmethod
+    def from_shared(cls, env, copies: int) -> "StackedVecEnv":
+        import copy
+
+        try:
+            return cls([env] + [copy.deepcopy(env) for _ in range(copies - 1)])
+        except Exception as err:  # noqa: BLE001 - e.g. subprocess-backed vector envs
+            raise TypeError(f"cannot clone {type(env).__name__} for {copies} agents ({err}); pass a vector env "
+                            f"of population_size x num_envs environments or a StackedVecEnv of one env per agent")
+
+    def _split(self, x):
+        out, s = [], 0
+        for n in self.sizes:
+            out.append(x[s:s + n])
+            s += n
+        return out
+
+    @staticmethod
+    def _cat(parts, out=None, dtype=None):
+        arr = np.concatenate([np.asarray(p, dtype=dtype) for p in parts], axis=0)
+        if out is not None:
+            np.copyto(out.reshape(arr.shape), arr)
+            return out
+        return arr
+
+    @staticmethod
+    def _infos(infos):
+        masks = [i.get("action_mask") if isinstance(i, dict) else None for i in infos]
+        if all(m is not None for m in masks):
+            return {"action_mask": np.concatenate([np.asarray(m) for m in masks], axis=0)}
+        return {}
+
+    def reset(self, seed=None, options=None, out_obs: np.ndarray | None = None):
+        res = [e.reset() if seed is None else e.reset(seed=seed + k) for k, e in enumerate(self.envs)]
+        obs = self._cat([r[0] for r in res], out_obs, np.float32)
+        return obs, self._infos([r[1] for r in res])
+
+    def step(self, actions, out_obs=None, out_rew=None, out_done=None):
+        res = [e.step(a) for e, a in zip(self.envs, self._split(np.asarray(actions)))]
+        obs = self._cat([r[0] for r in res], out_obs, np.float32)
+        rew = self._cat([r[1] for r in res], out_rew, np.float32)
+        term = np.concatenate([np.asarray(r[2], dtype=bool) for r in res])
+        trunc = np.concatenate([np.asarray(r[3], dtype=bool) for r in res])
+        if out_done is not None:
+            np.copyto(out_done.reshape(term.shape), term)
+        return obs, rew, term, trunc, self._infos([r[4] for r in res])
+
+    def close(self):
+        for e in self.envs:
+            if hasattr(e, "close"):
+                e.close()

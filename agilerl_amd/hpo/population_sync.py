@@ -117,6 +117,10 @@ class PopulationSync:
         steps = getattr(pop.opt, "steps", None)
         if isinstance(steps, torch.Tensor) and steps.shape == (P,) and steps.dtype == torch.int64:
             bufs.append(steps.view(torch.float32).view(P, 2))
+        for name in ("hp_batch_d", "hp_epochs_d", "hp_ent_d"):  # per-agent RL hyperparameters
+            t = getattr(pop, name, None)
+            if isinstance(t, torch.Tensor) and t.shape == (P,):
+                bufs.append(t.view(torch.float32).view(P, 1))
         return bufs
 
     @torch.no_grad()
@@ -185,6 +189,13 @@ class PopulationSync:
         self.history.append(fit)
         fits = [np.stack([h[i] for h in self.history[-self.eval_loop:]]) for i in range(len(fit))]
         _, parents = select_parents(fits, self.tournament_size, self.elitism, self.eval_loop, rng=self.rng_state)
+        # clones inherit their parent's fitness history (copy_attributes, core/base.py:444-503),
+        # which the next generation's eval_loop window reads
+        self.history = [np.asarray(h)[np.asarray(parents)] for h in self.history]
         self._clone_rows(parents)
+        if hasattr(self.pop, "after_clone"):
+            P = self.pop.P
+            mine = parents[self.rank * P:(self.rank + 1) * P]
+            self.pop.after_clone([q % P for q in mine] if self.world == 1 else None)
         self.last_parents = parents
         return parents

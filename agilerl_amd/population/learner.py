@@ -71,6 +71,8 @@ class AgxPPOLearnArgs(ctypes.Structure):
         ("target_kl", ctypes.c_double),
         ("loss_out", ctypes.c_void_p), ("kl_out", ctypes.c_void_p), ("epochs_out", ctypes.c_void_p),
         ("error_word", ctypes.c_void_p),
+        ("batch_per_agent", ctypes.c_void_p), ("epochs_per_agent", ctypes.c_void_p),
+        ("ent_coef_per_agent", ctypes.c_void_p),
     ]
 
 
@@ -84,6 +86,7 @@ class FusedLearner:
         self.ws = torch.empty(max(16, nbytes), dtype=torch.uint8, device=pop.device)
         _lib.check(lib.agx_ppo_learn_prepare(ctypes.byref(self.desc), self.ws.data_ptr(), _lib.stream()),
                    "agx_ppo_learn_prepare")
+        self.epochs_ws = pop.update_epochs
         self.loss = torch.zeros(pop.P, dtype=torch.float32, device=pop.device)
         self.kl = torch.zeros(pop.P, dtype=torch.float32, device=pop.device)
         self.epochs_run = torch.zeros(pop.P, dtype=torch.int32, device=pop.device)
@@ -108,7 +111,8 @@ class FusedLearner:
                pop.values.data_ptr(), pop.log_probs.data_ptr(), pop.actions.data_ptr(), pop.adv_stats.data_ptr(),
                None if masks is None else masks.data_ptr(), float(b1), float(b2), float(opt.eps), pop.batch_size,
                pop.update_epochs, float(pop.clip_coef), float(pop.vf_coef), float(pop.ent_coef),
-               float(pop.max_grad_norm), float(pop.target_kl or 0.0), pop.err_word.data_ptr())
+               float(pop.max_grad_norm), float(pop.target_kl or 0.0), pop.err_word.data_ptr(),
+               *((None, None, None) if pop._hp_dev is None else (t.data_ptr() for t in pop._hp_dev)))
         if self.key != key:
             a = self.args
             a.P, a.S, a.epochs, a.batch = pop.P, pop.S, pop.update_epochs, pop.batch_size
@@ -121,6 +125,7 @@ class FusedLearner:
             a.clip_coef, a.vf_coef, a.ent_coef, a.target_kl = key[18], key[19], key[20], key[22]
             a.loss_out, a.kl_out = self.loss.data_ptr(), self.kl.data_ptr()
             a.epochs_out, a.error_word = self.epochs_run.data_ptr(), key[23]
+            a.batch_per_agent, a.epochs_per_agent, a.ent_coef_per_agent = key[24], key[25], key[26]
             self.key = key
             self.aref = ctypes.byref(self.args)
             self.dref = ctypes.byref(self.desc)
@@ -139,7 +144,7 @@ class FusedLearner:
 
 
 def fused_learn(pop, perms=None) -> torch.Tensor:
-    if getattr(pop, "_fused", None) is None:
+    if getattr(pop, "_fused", None) is None or pop._fused.epochs_ws < pop.update_epochs:
         pop._fused = FusedLearner(pop)
     return pop._fused.learn(pop, perms)
 

@@ -98,6 +98,18 @@ class PPOPopulation:
         # sticky device error word of the fused learner (partner timeout); checked at host sync points
         self.err_word = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.last_kl = None
+        # per-agent RL hyperparameters (mutation.py:413-453 mutates them agent by
+        # agent); batch_size / update_epochs above are the population maxima
+        self.agent_batch = [self.batch_size] * self.P
+        self.agent_epochs = [self.update_epochs] * self.P
+        self.agent_ent = [self.ent_coef] * self.P
+        self.agent_lr = list(lr_list)  # exact host values (the device table is f32)
+        # device copies (the learner reads them once the population is heterogeneous;
+        # PopulationSync moves them with the parent rows)
+        self.hp_batch_d = torch.full((self.P,), self.batch_size, dtype=torch.int32, device=self.device)
+        self.hp_epochs_d = torch.full((self.P,), self.update_epochs, dtype=torch.int32, device=self.device)
+        self.hp_ent_d = torch.full((self.P,), self.ent_coef, dtype=torch.float32, device=self.device)
+        self._hetero = False
         self.fused = fused
         self.act_seed = (int(seeds[0]) * 0x9E3779B97F4A7C15 + 0x5851F42D) & 0xFFFFFFFFFFFFFFFF
         self.act_counter = 0
@@ -230,6 +242,82 @@ class PPOPopulation:
             raise _lib.AgxError("agx_ppo_learn: a partner workgroup timed out; the population's parameters are "
                                 "incomplete for this learn()")
 
+    # ------------------------------------------------------------------ #
+    @property
+    def heterogeneous(self) -> bool:
+        return self._hetero
+
+    @property
+    def _hp_dev(self):
+        """(batch i32 [P], epochs i32 [P], ent f32 [P]) for the learner, or None
+        while every agent shares the population's values."""
+        return (self.hp_batch_d, self.hp_epochs_d, self.hp_ent_d) if self._hetero else None
+
+    def set_agent_hparam(self, p: int, name: str, value) -> None:
+        """Set one agent's RL hyperparameter (the HPO mutation of
+        mutation.py:413-453 on agent p).  ``learn_step`` would change the
+        agent's rollout length, which the lock-step population engine shares
+        across agents: it raises NotImplementedError."""
+        p = int(p)
+        if name == "lr":
+            self.opt.lr[p] = float(value)
+            self.agent_lr[p] = float(value)
+            return
+        if name == "batch_size":
+            self.agent_batch[p] = int(value)
+            self.hp_batch_d[p] = int(value)
+        elif name == "update_epochs":
+            if int(value) < 1:
+                raise ValueError("update_epochs must be >= 1")
+            self.agent_epochs[p] = int(value)
+            self.hp_epochs_d[p] = int(value)
+        elif name == "ent_coef":
+            self.agent_ent[p] = float(value)
+            self.hp_ent_d[p] = float(value)
+        elif name == "learn_step":
+            raise NotImplementedError("learn_step is the rollout length every agent of the population engine shares")
+        else:
+            raise KeyError(f"no per-agent hyperparameter {name!r}")
+        self._rederive()
+
+    def reinit_agent_optimizer(self, p: int) -> None:
+        """reinit_optimizers for agent p (core/base.py:654-710): a fresh Adam,
+        zero moments and step count, the agent's current learning rate."""
+        self.opt.exp_avg[p].zero_()
+        self.opt.exp_avg_sq[p].zero_()
+        self.opt.steps[p] = 0
+
+    def _rederive(self) -> None:
+        """Population maxima (they size the learner's workspace and partner
+        split) and the heterogeneity flag, from the per-agent lists."""
+        self.batch_size = max(self.agent_batch)
+        if max(self.agent_epochs) != self.update_epochs:
+            self.update_epochs = max(self.agent_epochs)
+            self._fused = None      # workspace is sized by the epochs
+            self._perm_host = None  # pinned [E, P, S] staging
+            self.discard_prefetch()
+            self._perm_next = None
+        self._hetero = not (len(set(self.agent_batch)) == 1 and len(set(self.agent_epochs)) == 1
+                            and len(set(self.agent_ent)) == 1)
+
+    def after_clone(self, local_parents: list[int] | None) -> None:
+        """PopulationSync has copied every cloned row (params, Adam state, lr,
+        step, and the per-agent hyperparameter rows).  Single rank: the new
+        agent j took local row local_parents[j], mirrored on the host lists;
+        several ranks (parents may be remote): re-read the device rows."""
+        if local_parents is not None:
+            b, e, h, r = list(self.agent_batch), list(self.agent_epochs), list(self.agent_ent), list(self.agent_lr)
+            self.agent_batch = [b[q] for q in local_parents]
+            self.agent_epochs = [e[q] for q in local_parents]
+            self.agent_ent = [h[q] for q in local_parents]
+            self.agent_lr = [r[q] for q in local_parents]
+        else:
+            self.agent_batch = [int(x) for x in self.hp_batch_d.cpu()]
+            self.agent_epochs = [int(x) for x in self.hp_epochs_d.cpu()]
+            self.agent_ent = [float(x) for x in self.hp_ent_d.cpu()]
+            self.agent_lr = [float(x) for x in self.opt.lr.cpu()]
+        self._rederive()
+
     def minibatch_plan(self):
         b = self.batch_size
         return [(s, min(s + b, self.S)) for s in range(0, self.S, b)]
@@ -248,7 +336,8 @@ class PPOPopulation:
             return perms
         if self.perm_source == "numpy":
             host = self._host_perm_buffer()
-            numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=host.numpy())
+            numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=host.numpy(),
+                                epochs_per_agent=self.agent_epochs if self.heterogeneous else None)
             perms = host.to(self.device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
@@ -287,7 +376,8 @@ class PPOPopulation:
         if self.perm_source == "numpy":
             state = np.random.get_state(legacy=True)
             host = self._host_perm_buffer()
-            numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=host.numpy())
+            numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=host.numpy(),
+                                epochs_per_agent=self.agent_epochs if self.heterogeneous else None)
             with torch.cuda.stream(side):
                 perms = host.to(self.device, non_blocking=True)
                 ev = torch.cuda.Event()
@@ -319,6 +409,9 @@ class PPOPopulation:
         semantics, including target-KL early stop per agent (stopped agents'
         rows are left untouched) and action masks."""
         P, S, D = self.P, self.S, self.spec.obs_dim
+        if self.heterogeneous:
+            raise NotImplementedError("per-agent batch / epochs / entropy hyperparameters need the fused learner "
+                                      "(agx_ppo_learn); this architecture runs the PyTorch learner")
         K.adv_normalize_(self.advantages, self.adv_stats)
         obs = self.obs.view(P, S, D)
         act = self.actions.view(P, S)
@@ -376,3 +469,7 @@ class PPOPopulation:
 
     def n_minibatches(self) -> int:
         return math.ceil(self.S / self.batch_size)
+
+    def n_updates(self) -> int:
+        """Minibatch updates of one learn() over the whole population (no early stop)."""
+        return sum(e * math.ceil(self.S / b) for b, e in zip(self.agent_batch, self.agent_epochs))

@@ -18,7 +18,8 @@ import numpy as np
 from . import _lib
 
 
-def numpy_shuffle_perms(P: int, epochs: int, S: int, out: np.ndarray | None = None) -> np.ndarray:
+def numpy_shuffle_perms(P: int, epochs: int, S: int, out: np.ndarray | None = None,
+                        epochs_per_agent=None) -> np.ndarray:
     """[epochs, P, S] int64: for agent p = 0..P-1 in turn, arange(S) shuffled
     ``epochs`` times in place by the global ``np.random`` generator, row e =
     the order after the (e+1)-th shuffle.  Equivalent to (and as fast as a
@@ -28,6 +29,9 @@ def numpy_shuffle_perms(P: int, epochs: int, S: int, out: np.ndarray | None = No
             idx = np.arange(S)
             for e in range(epochs):
                 np.random.shuffle(idx); out[e, p] = idx
+
+    ``epochs_per_agent``: agent p draws only its own number of shuffles
+    (mutated update_epochs); rows beyond are left untouched.
     """
     if out is None:
         out = np.empty((epochs, P, S), dtype=np.int64)
@@ -39,7 +43,13 @@ def numpy_shuffle_perms(P: int, epochs: int, S: int, out: np.ndarray | None = No
     key = np.array(key, dtype=np.uint32)  # own, writable copy
     pos_c = ctypes.c_int32(int(pos))
     lib = _lib.load(require_gpu=False)  # host code: no device work
+    ep = None
+    if epochs_per_agent is not None:
+        ep = np.ascontiguousarray(epochs_per_agent, dtype=np.int64)
+        if ep.shape != (P,):
+            raise ValueError("epochs_per_agent must have one entry per agent")
     _lib.check(lib.agx_host_shuffle_perms(key.ctypes.data, ctypes.byref(pos_c), int(P), int(epochs), int(S),
-                                          out.ctypes.data), "agx_host_shuffle_perms")
+                                          None if ep is None else ep.ctypes.data, out.ctypes.data),
+               "agx_host_shuffle_perms")
     np.random.set_state(("MT19937", key, int(pos_c.value), has_gauss, gauss))
     return out

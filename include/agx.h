@@ -153,6 +153,13 @@ typedef struct agx_ppo_learn_args {
     float *loss_out, *kl_out;
     int32_t *epochs_out;
     uint32_t *error_word;
+    /* heterogeneous population (RL-hyperparameter mutations, mutation.py:
+     * 413-453), each NULL = the scalar above for every agent: per-agent
+     * minibatch size (<= batch, which sizes the partner split), update
+     * epochs (<= epochs; perms rows e >= epochs_per_agent[p] are not read)
+     * and entropy coefficient.  loss_out divides by S * epochs_per_agent[p]. */
+    const int32_t *batch_per_agent, *epochs_per_agent;
+    const float *ent_coef_per_agent;
 } agx_ppo_learn_args;
 int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *args, void *workspace, void *stream);
 /* Rollout policy step (PPO.get_action / _get_action_and_values, ppo.py:
@@ -262,10 +269,12 @@ int agx_ppo_rollout_persistent(const agx_ppo_net *net, int64_t P, int64_t N, con
  * one after another as train_on_policy's agent loop does
  * (train_on_policy.py:210): perms [epochs][P][S] in HOST memory.  mt_key
  * [624] / mt_pos are numpy's state (np.random.get_state()[1:3]), advanced in
- * place (the caller writes them back with np.random.set_state).  Host code,
- * no device work. */
+ * place (the caller writes them back with np.random.set_state).
+ * epochs_per_agent (host, [P]) or NULL: agent p draws only its own
+ * epochs_per_agent[p] <= epochs shuffles (rows beyond are left as they are).
+ * Host code, no device work. */
 int agx_host_shuffle_perms(uint32_t *mt_key, int32_t *mt_pos, int64_t P, int64_t epochs, int64_t S,
-                           int64_t *perms);
+                           const int64_t *epochs_per_agent, int64_t *perms);
 /* Coherent (fine-grained) pinned host memory, device-accessible at the same
  * address; NULL on failure. */
 void *agx_host_alloc(size_t bytes);

@@ -78,14 +78,19 @@ class CpuPPOAgent:
         done_buf = np.zeros((T, N), bool)
         val_buf = np.zeros((T, N), np.float32)
         lp_buf = np.zeros((T, N), np.float32)
-        obs, _ = env.reset()
-        obs = np.array(obs)
+        # the env is reset once, on the first collect (rollouts/on_policy.py:50-56);
+        # later rollouts continue from the last observation
+        if getattr(self, "_obs", None) is None:
+            obs, _ = env.reset()
+            self._obs = np.array(obs)
+        obs = self._obs
         term = np.zeros(N, bool)
         for t in range(T):
             a, lp, v = self.get_action(obs)
             nobs, r, term, trunc, _ = env.step(a)
             obs_buf[t], act_buf[t], rew_buf[t], done_buf[t], val_buf[t], lp_buf[t] = obs, a, r, term | trunc, v, lp
             obs = np.array(nobs)
+        self._obs = obs
         _, _, lv = self.get_action(obs)
         adv, ret = ogae.gae(rew_buf, val_buf, done_buf, lv, term)
         S = T * N

@@ -25,6 +25,9 @@ Reference functions exercised (paths relative to /root/reference):
   * agilerl/algorithms/dqn.py:274-324             DQN.update (TD target)
   * agilerl/algorithms/dqn_rainbow.py:284-367     RainbowDQN._dqn_loss (C51 projection)
   * agilerl/hpo/tournament.py:41-119              TournamentSelection
+  * agilerl/hpo/mutation.py:311-453, 515-827      Mutations.mutation / rl_hyperparam_mutation /
+                                                  parameter_mutation (+ RLParameter /
+                                                  HyperparameterConfig, algorithms/core/registry.py)
 
 Usage:  python tests/golden/gen_golden.py  [--ref /root/reference]
 """
@@ -105,6 +108,9 @@ def _install_stubs() -> None:
         "agilerl.wrappers",
         "agilerl.wrappers.make_evolvable",
         "agilerl.components",
+        "agilerl.algorithms.core.registry_stub",
+        "agilerl.wrappers.agent",
+        "fastrand",
     ]:
         _stub(name)
     sys.modules["gymnasium"].spaces = sys.modules["gymnasium.spaces"]
@@ -640,6 +646,97 @@ def gen_ppo_learn(ppo_mod, en_mod, tu_mod, dist_mod, spaces_mod, out: dict) -> N
 
 
 # --------------------------------------------------------------------------- #
+# HPO mutations                                                               #
+# --------------------------------------------------------------------------- #
+class _MutNet(torch.nn.Module):
+    """A policy with the reference's actor state-dict names (encoder.model.*,
+    head_net.model.*) whose 2-D weights parameter_mutation perturbs."""
+
+    def __init__(self, D, A, seed):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed)
+        enc = torch.nn.Sequential()
+        enc.add_module("encoder_linear_layer_1", torch.nn.Linear(D, 64))
+        enc.add_module("encoder_layer_norm_1", torch.nn.LayerNorm(64))
+        enc.add_module("encoder_linear_layer_output", torch.nn.Linear(64, 64))
+        head = torch.nn.Sequential()
+        head.add_module("actor_linear_layer_1", torch.nn.Linear(64, 64))
+        head.add_module("actor_layer_norm_1", torch.nn.LayerNorm(64))
+        head.add_module("actor_linear_layer_output", torch.nn.Linear(64, A))
+        self.encoder, self.head_net = torch.nn.Module(), torch.nn.Module()
+        self.encoder.model, self.head_net.model = enc, head
+        with torch.no_grad():
+            for p_ in self.parameters():
+                p_.copy_(torch.randn(p_.shape, generator=g) * 0.3)
+
+
+def gen_mutation(mut_mod, reg_mod, out: dict) -> None:
+    """Mutations.mutation over a small fake population for several
+    generations: the choices drawn, the RL-hyperparameter values (shared
+    HyperparameterConfig, torch-drawn sample / grow-or-shrink), and the
+    parameter-mutated policy weights."""
+    RLParameter, HPC = reg_mod.RLParameter, reg_mod.HyperparameterConfig
+    cases = [
+        # (P, no, arch, params, act, rl_hp, mutate_elite, seed, generations)
+        (4, 0.4, 0.0, 0.2, 0.0, 0.2, True, 42, 6),    # ppo.yaml-like (architecture / activation off)
+        (8, 0.0, 0.0, 0.5, 0.0, 0.5, False, 7, 5),    # no elite mutation
+    ]
+    for k, (P, no, arch, par, act, rlhp, mut_elite, seed, G) in enumerate(cases):
+        hp = HPC(lr=RLParameter(min=1e-4, max=1e-2), batch_size=RLParameter(min=8, max=1024, dtype=int),
+                 ent_coef=RLParameter(min=0.001, max=0.1), update_epochs=RLParameter(min=1, max=10, dtype=int))
+
+        class _OptCfg:
+            lr = "lr"
+
+        class _Registry:
+            def __init__(self):
+                self.hp_config = hp  # shared, as create_population hands it to every agent
+                self.optimizers = [_OptCfg()]
+                self.groups = []
+
+            def policy(self, return_group=False):
+                grp = types.SimpleNamespace(eval_network="actor", shared_networks=None)
+                return grp if return_group else "actor"
+
+        class _Agent:
+            def __init__(self, i):
+                self.index, self.lr, self.batch_size, self.ent_coef, self.update_epochs = i, 1e-3, 128, 0.01, 4
+                self.registry = _Registry()
+                self.actor = _MutNet(8, 4, 1000 * k + i)
+                self.mut, self.reinits = None, 0
+
+            def get_lr_names(self):
+                return ["lr"]
+
+            def reinit_optimizers(self, optimizer=None):
+                self.reinits += 1
+
+            def mutation_hook(self):
+                pass
+
+        pop = [_Agent(i) for i in range(P)]
+        init_w = {f"a{i}.{n}": t.detach().clone().numpy() for i, a in enumerate(pop)
+                  for n, t in a.actor.state_dict().items()}
+        m = mut_mod.Mutations(no_mutation=no, architecture=arch, new_layer_prob=0.2, parameters=par,
+                              activation=act, rl_hp=rlhp, mutation_sd=0.1, mutate_elite=mut_elite,
+                              rand_seed=seed, device="cpu")
+        muts, hps = [], []
+        for _ in range(G):
+            pop = m.mutation(pop)
+            muts.append([str(a.mut) for a in pop])
+            hps.append([[a.lr, a.batch_size, a.ent_coef, a.update_epochs, a.reinits] for a in pop])
+        rec = dict(P=np.int64(P), probs=np.array([no, arch, par, act, rlhp], np.float64),
+                   mutate_elite=np.int32(mut_elite), seed=np.int64(seed), generations=np.int64(G),
+                   muts=np.array(muts), hps=np.array(hps, np.float64))
+        for n, v in init_w.items():
+            rec["init." + n] = v
+        for i, a in enumerate(pop):
+            for n, t in a.actor.state_dict().items():
+                rec[f"final.a{i}.{n}"] = t.detach().numpy().copy()
+        out[f"mut{k}"] = rec
+
+
+# --------------------------------------------------------------------------- #
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -661,6 +758,8 @@ def main() -> None:
     tu = _load(ref, "agilerl.utils.torch_utils", "agilerl/utils/torch_utils.py")
     en = _load(ref, "agilerl.utils.evolvable_networks", "agilerl/utils/evolvable_networks.py")
     dist_mod = _load(ref, "agilerl.networks.distributions", "agilerl/networks/distributions.py")
+    reg = _load(ref, "agilerl.algorithms.core.registry", "agilerl/algorithms/core/registry.py")
+    mut = _load(ref, "agilerl.hpo.mutation", "agilerl/hpo/mutation.py")
 
     groups: dict[str, dict] = {}
     gen_gae(rb, groups)
@@ -671,6 +770,7 @@ def main() -> None:
     gen_c51(rainbow, groups)
     gen_tournament(tour, groups)
     gen_ppo_learn(ppo, en, tu, dist_mod, sys.modules["gymnasium.spaces"], groups)
+    gen_mutation(mut, reg, groups)
 
     if args.only:
         groups = {k: v for k, v in groups.items() if k in set(args.only)}

@@ -8,6 +8,7 @@ import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
 
 
 def _spaces(obs_dim=8, n=4):
@@ -59,6 +60,93 @@ def test_create_population_train_on_policy():
     assert len(fits) == 4 and all(len(f) == 4 for f in fits)
     assert all(a.steps[-1] >= 1024 for a in pop)
     assert all(len(a.fitness) == 4 for a in pop)
+
+
+def test_train_on_policy_reference_call_site(tmp_path):
+    """The reference's call site unchanged: ONE shared N-env (cloned per agent
+    here), a tournament AND a mutation object (RL-hyperparameter + parameter
+    mutations), population checkpoints and the elite saved."""
+    import glob
+    import os
+
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.mutation import Mutations
+    from agilerl_amd.hpo.registry import HyperparameterConfig, RLParameter
+    from agilerl_amd.hpo.tournament import TournamentSelection
+    from agilerl_amd.training import train_on_policy
+    from agilerl_amd.utils import create_population
+
+    obs_space, act_space = _spaces()
+    INIT_HP = {"BATCH_SIZE": 64, "LR": 1e-3, "LEARN_STEP": 128, "UPDATE_EPOCHS": 2}
+    net_config = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}}
+    hp = HyperparameterConfig(lr=RLParameter(min=1e-4, max=1e-2), batch_size=RLParameter(min=32, max=256, dtype=int),
+                              ent_coef=RLParameter(min=0.001, max=0.1),
+                              update_epochs=RLParameter(min=1, max=4, dtype=int))
+    pop = create_population("PPO", net_config, INIT_HP, obs_space, act_space, hp_config=hp, population_size=4,
+                            num_envs=16)
+    env = SyntheticVecEnv(16, seed=3, p_done=0.05, max_episode_steps=60)  # the reference's shared N-env
+    tour = TournamentSelection(2, True, 4, 1)
+    mut = Mutations(no_mutation=0.2, architecture=0, new_layer_prob=0.2, parameters=0.3, activation=0, rl_hp=0.5,
+                    rand_seed=1)
+    ck = os.path.join(tmp_path, "ck.pt")
+    elite = os.path.join(tmp_path, "elite.pt")
+    pop, fits = train_on_policy(env, "Synthetic", "PPO", pop, INIT_HP=INIT_HP, max_steps=1536, evo_steps=256,
+                                tournament=tour, mutation=mut, checkpoint=512, checkpoint_path=ck, save_elite=True,
+                                elite_path=elite, verbose=False)
+    assert len(fits) == 6 and all(len(f) == 4 for f in fits)
+    population = pop[0].population
+    population.check_errors()
+    muts = {a.mut for a in pop}
+    assert muts - {"None"}, muts  # something was mutated
+    # per-agent hyperparameters live in the population's tables
+    assert [a.batch_size for a in pop] == population.agent_batch
+    assert [a.update_epochs for a in pop] == population.agent_epochs
+    assert torch.isfinite(population.params.data).all()
+    assert os.path.exists(elite)
+    assert len(glob.glob(os.path.join(tmp_path, "ck_*_*.pt"))) >= 4
+    assert sorted(a.index for a in pop) == sorted(set(a.index for a in pop))  # clone indices are unique
+
+
+def test_heterogeneous_hyperparameters_match_separate_agents():
+    """Three agents with their own (batch, epochs, entropy coefficient) in ONE
+    fused learn() == each agent alone with those hyperparameters: bit for
+    bit (idle partner workgroups add exact zeros)."""
+    from agilerl_amd.population.learner import fused_learn
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+
+    spec = ActorCriticSpec(obs_dim=8, n_actions=4)
+    hps = [(64, 2, 0.01), (128, 3, 0.05), (32, 1, 0.0)]
+    big = PPOPopulation(spec, 3, 32, learn_step=256, batch_size=128, update_epochs=3, seeds=[0, 1, 2], device=DEV)
+    for p, (b, e, h) in enumerate(hps):
+        big.set_agent_hparam(p, "batch_size", b)
+        big.set_agent_hparam(p, "update_epochs", e)
+        big.set_agent_hparam(p, "ent_coef", h)
+    assert big.heterogeneous and big.batch_size == 128 and big.update_epochs == 3
+    g = torch.Generator(device=DEV).manual_seed(5)
+    for name in ("obs", "rewards", "values", "log_probs", "advantages", "returns"):
+        getattr(big, name).copy_(torch.randn(getattr(big, name).shape, device=DEV, generator=g))
+    big.actions.copy_(torch.randint(0, 4, big.actions.shape, device=DEV, generator=g))
+    big.adv_stats[:, 0] = 0.1
+    big.adv_stats[:, 1] = 1.3
+    np.random.seed(3)
+    perms = big.permutations()
+    singles = []
+    for p, (b, e, h) in enumerate(hps):
+        one = PPOPopulation(spec, 1, 32, learn_step=256, batch_size=b, update_epochs=e, ent_coef=h, seeds=[p],
+                            device=DEV)
+        one.params.data.copy_(big.params.data[p:p + 1])
+        for name in ("obs", "rewards", "values", "log_probs", "advantages", "returns", "actions", "adv_stats"):
+            getattr(one, name).copy_(getattr(big, name)[p:p + 1])
+        fused_learn(one, perms[:e, p:p + 1].contiguous())
+        singles.append(one)
+    loss = fused_learn(big, perms)
+    torch.cuda.synchronize()
+    for p, one in enumerate(singles):
+        assert torch.equal(big.params.data[p], one.params.data[0]), p
+        assert torch.equal(big.opt.exp_avg_sq[p], one.opt.exp_avg_sq[0]), p
+        assert int(big.opt.steps[p]) == int(one.opt.steps[0]) == hps[p][1] * (256 // hps[p][0])
+        assert torch.equal(loss[p], one._fused.loss[0]), p
 
 
 def test_ppo_default_critic_head_uses_fused_kernels():

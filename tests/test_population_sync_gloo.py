@@ -85,7 +85,8 @@ def test_generation_two_ranks(tmp_path, world, P):
     _, parents0 = oracle_select([[f] for f in fit], 2, True, 1)
     np.random.set_state(state)
     assert list(res[0]["parents"][0]) == list(parents0)
-    np.testing.assert_array_equal(res[0]["hist"][0].numpy(), fit)
+    # the fitness history follows the lineage: clones inherit their parent's record
+    np.testing.assert_array_equal(res[0]["hist"][0].numpy(), fit[list(parents0)][list(res[0]["parents"][1])])
     # each rank's agents after two generations are the rows selected by
     # generation 1 (params and Adam state of the parents), re-selected by
     # generation 2 (fitness of the reset stats is -1e9 everywhere: ties)

@@ -38,6 +38,8 @@ print(f"learn() wall {1e3 * (t1 - t0):.3f} ms  ({nmb} minibatch updates per agen
 names = ["gather", "fwd", "loss", "out bwd", "head LN bwd", "head dW+dX", "enc bwd"]
 for sb in range(4):
     row = st[sb * 16: sb * 16 + 8]
+    if not all(row):  # only workgroup 0 stamps: with K partners it runs 1 of every K sub-batches
+        continue
     seg = [row[i + 1] - row[i] for i in range(7)]
     print(f"sb{sb}: " + "  ".join(f"{n}={c}" for n, c in zip(names, seg)) + f"  total={row[7] - row[0]}")
 last = max(v for v in st[:64] if v)
