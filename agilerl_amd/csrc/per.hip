@@ -26,7 +26,7 @@
 // rest of the walk reads HBM/L2.  Algorithmic bytes:
 // 8 B x depth (left-child reads) + 4 B uniform + 8 B index per sample.
 #include "agx_common.h"
-#include "dd_pow.h"
+#include "libm_pow.h"
 
 namespace agx {
 
@@ -97,9 +97,9 @@ __global__ __launch_bounds__(kSmallBatch) void per_small(
     }
     double leaf = 0.0;
     if (kMode == 0) {
-        if (writer) leaf = cr_pow(p, alpha);
+        if (writer) leaf = libm_pow(p, alpha);
     } else {
-        leaf = cr_pow(*max_priority, alpha);
+        leaf = libm_pow(*max_priority, alpha);
     }
     if (writer) {
         sum_tree[cap + idx] = leaf;
@@ -149,7 +149,7 @@ __global__ void per_write_leaves(double *__restrict__ sum_tree, double *__restri
     if (win[idx] != (int32_t)i) return;
     double p = (double)pri[i];
     if (p < floor_) p = floor_;
-    const double leaf = cr_pow(p, alpha);
+    const double leaf = libm_pow(p, alpha);
     sum_tree[cap + idx] = leaf;
     min_tree[cap + idx] = leaf;
 }
@@ -159,7 +159,7 @@ __global__ void per_add_leaves(double *__restrict__ sum_tree, double *__restrict
                                double alpha, const double *__restrict__ max_priority) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const double leaf = cr_pow(*max_priority, alpha);
+    const double leaf = libm_pow(*max_priority, alpha);
     const int64_t idx = (start + i) % max_size;
     sum_tree[cap + idx] = leaf;
     min_tree[cap + idx] = leaf;
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void per_sample_kernel(
     const double total = sum_tree[1];
     const double segment = total / (double)B;
     double max_w = 0.0;
-    if (weights) max_w = cr_pow(min_tree[1] / total * size, -beta);
+    if (weights) max_w = libm_pow(min_tree[1] / total * size, -beta);
     int32_t bad = 0;
     // kPer independent walks per lane advance level by level in lock step: each
     // level issues kPer independent loads, so a lane's latency chain is one
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(256) void per_sample_kernel(
         out_idx[i[r]] = k[r] - cap;
         if (weights) {
             const double ps = sum_tree[k[r]] / total;
-            weights[i[r]] = (float)(cr_pow(ps * size, -beta) / max_w);
+            weights[i[r]] = (float)(libm_pow(ps * size, -beta) / max_w);
         }
     }
     if (err && bad) atomicAdd(err, bad);
@@ -326,7 +326,7 @@ __global__ void per_gather_kernel(const double *__restrict__ tree, const int64_t
 
 __global__ void pow_kernel(const double *x, const double *y, double *o, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) o[i] = cr_pow(x[i], y[i]);
+    if (i < n) o[i] = libm_pow(x[i], y[i]);
 }
 
 static inline int log2_exact(int64_t cap) {

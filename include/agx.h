@@ -292,9 +292,11 @@ int agx_host_wait(const agx_rollout_ctl *ctl, int64_t nwg, uint32_t target, doub
  * Trees are 1-indexed heaps of 2*capacity doubles (node k has children 2k,
  * 2k+1; leaf i at capacity+i), capacity a power of two >= max_size.
  * max_priority is a device f64 scalar (initialise to 1.0).
- * Leaves hold priority**alpha computed with a correctly rounded pow; the
- * tree is a pure function of the leaves, so batched updates are identical
- * to the reference's sequential path walks. */
+ * Leaves hold priority**alpha computed by glibc's own pow algorithm
+ * (csrc/libm_pow.h: the reference's Python float ** is glibc pow, which is
+ * not correctly rounded), bit for bit; the tree is a pure function of the
+ * leaves, so batched updates are identical to the reference's sequential
+ * path walks. */
 size_t agx_per_workspace_bytes(int64_t capacity, int64_t max_batch);
 int agx_per_init(double *sum_tree, double *min_tree, int64_t capacity, void *stream);
 /* PrioritizedReplayBuffer.add (replay_buffer.py:296-309): n leaves at ring
@@ -395,8 +397,8 @@ int agx_clip_adam(float *params, float *grads, float *exp_avg, float *exp_avg_sq
 int agx_polyak(float *target, const float *online, int64_t n, float tau, void *stream);
 
 /* ---- diagnostics ---------------------------------------------------------
- * out[i] = correctly rounded pow(x[i], y[i]) (the routine the PER leaves and
- * IS weights use); for parity tests against libm / high-precision values. */
+ * out[i] = pow(x[i], y[i]) by the routine the PER leaves and IS weights use
+ * (glibc's pow algorithm, bit-identical to the host libm); for parity tests. */
 int agx_debug_pow(const double *x, const double *y, double *out, int64_t n, void *stream);
 /* Fused-learner phase timing: subsequent agx_ppo_learn calls write shader
  * cycle stamps of agent 0's first minibatch into buf (device int64[80]:

@@ -208,3 +208,10 @@ void oracle_c51(const float *q_next, const float *tdist, const float *logp_cur, 
         loss[i] = (float)(-s);
     }
 }
+
+/* libm pow, element-wise: what the reference's Python ``float ** float``
+ * calls (replay_buffer.py:322 leaves, :399-406 IS weights).  The checker of
+ * the device restatement of glibc's pow (agilerl_amd/csrc/libm_pow.h). */
+void oracle_pow(const double *x, const double *y, double *out, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) out[i] = pow(x[i], y[i]);
+}

@@ -37,6 +37,7 @@ def lib():
         L.oracle_per_weights.argtypes = [_P, _P, _I, _P, _I, _I, _D, _P]
         L.oracle_ppo_loss.argtypes = [_P] * 7 + [_I, _I, _D, _D, _D, _P, _P, _P, _P, ctypes.c_int]
         L.oracle_c51.argtypes = [_P] * 7 + [_I, _I, _I, _D, _D, _D, _P, _P]
+        L.oracle_pow.argtypes = [_P, _P, _P, _I]
         _lib = L
     return _lib
 
@@ -126,3 +127,12 @@ def c51(q_next, tdist, logp_cur, act, r, d, support, vmin, vmax, gamma):
     loss = np.empty(B, np.float32)
     lib().oracle_c51(*[_p(a) for a in arrs], B, A, Z, vmin, vmax, gamma, _p(proj), _p(loss))
     return loss, proj
+
+
+def libm_pow(x, y):
+    """Element-wise libm pow (the reference's Python float ** float)."""
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(np.broadcast_to(np.asarray(y, np.float64), x.shape))
+    out = np.empty_like(x)
+    lib().oracle_pow(_p(x), _p(y), _p(out), x.size)
+    return out

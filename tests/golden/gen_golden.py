@@ -25,6 +25,11 @@ Reference functions exercised (paths relative to /root/reference):
   * agilerl/algorithms/dqn.py:274-324             DQN.update (TD target)
   * agilerl/algorithms/dqn_rainbow.py:284-367     RainbowDQN._dqn_loss (C51 projection)
   * agilerl/hpo/tournament.py:41-119              TournamentSelection
+  * agilerl/components/replay_buffer.py:206-258   MultiStepReplayBuffer._get_n_step_info
+  * agilerl/components/multi_agent_replay_buffer.py:155-167  MultiAgentReplayBuffer.sample
+                                                  (Python random.sample + _process_transition)
+  * agilerl/algorithms/maddpg.py:707-821          MADDPG._learn_individual (critic TD target, NaN
+                                                  rules, MSE loss and its gradient)
   * agilerl/hpo/mutation.py:311-453, 515-827      Mutations.mutation / rl_hyperparam_mutation /
                                                   parameter_mutation (+ RLParameter /
                                                   HyperparameterConfig, algorithms/core/registry.py)
@@ -646,6 +651,152 @@ def gen_ppo_learn(ppo_mod, en_mod, tu_mod, dist_mod, spaces_mod, out: dict) -> N
 
 
 # --------------------------------------------------------------------------- #
+# n-step fold, multi-agent replay sampling, MADDPG critic target              #
+# --------------------------------------------------------------------------- #
+class _CloneTD(dict):
+    def clone(self):
+        return _CloneTD({k: v.clone() for k, v in self.items()})
+
+
+def gen_nstep(rp_mod, out: dict) -> None:
+    """MultiStepReplayBuffer._get_n_step_info on batched transitions (the
+    reference's vectorised add: one TensorDict per env step)."""
+    import collections
+
+    MSB = rp_mod.MultiStepReplayBuffer
+    cases = [
+        # (n_step, num_envs, obs_dim, p_done, gamma, seed, done key)
+        (3, 4, 3, 0.0, 0.99, 81, "done"),
+        (4, 5, 2, 0.3, 0.99, 82, "done"),         # some env done -> early stop (any)
+        (4, 16, 4, 0.05, 0.9, 83, "terminated"),
+        (2, 1, 1, 0.5, 0.97, 84, "termination"),
+    ]
+    for k, (n, B, D, pd, gamma, seed, dkey) in enumerate(cases):
+        rng = np.random.default_rng(seed)
+        trs = []
+        for _ in range(n):
+            trs.append(_CloneTD(obs=torch.tensor(rng.standard_normal((B, D)), dtype=torch.float32),
+                                reward=torch.tensor(rng.standard_normal((B, 1)) * 3, dtype=torch.float32),
+                                next_obs=torch.tensor(rng.standard_normal((B, D)), dtype=torch.float32),
+                                **{dkey: torch.tensor(rng.random((B, 1)) < pd, dtype=torch.float32)}))
+        buf = object.__new__(MSB)
+        buf.n_step, buf.gamma = n, gamma
+        buf.n_step_buffer = collections.deque(trs, maxlen=n)
+        buf.reward_key, buf.ns_key, buf.done_key = "reward", "next_obs", None
+        buf.initialized = False
+        res = buf._get_n_step_info()
+        rec = dict(n_step=np.int64(n), gamma=np.float64(gamma), done_key=np.array(dkey))
+        for i, t in enumerate(trs):
+            for f, v in t.items():
+                rec[f"in{i}.{'done' if f == dkey else f}"] = v.numpy()
+        for f, v in res.items():
+            rec[f"out.{'done' if f == dkey else f}"] = v.numpy()
+        out[f"nstep{k}"] = rec
+
+
+def gen_ma_replay(mar_mod, out: dict) -> None:
+    """MultiAgentReplayBuffer: vectorised saves (ring wrap-around, binary
+    fields with and without NaN), then random.seed + sample.  obs_to_tensor
+    (agilerl/utils/algo_utils.py:746-773, an np.ndarray -> torch.as_tensor(
+    ...).float()) is the only helper the sample path calls."""
+    import random
+
+    mar_mod.obs_to_tensor = lambda obs, device: torch.as_tensor(obs, device=device).float()
+    MAR = mar_mod.MultiAgentReplayBuffer
+    fields = ["obs", "action", "reward", "next_obs", "done"]
+    agents = ["speaker_0", "listener_0"]
+    dims = {"speaker_0": (3, 3), "listener_0": (11, 5)}
+    for k, (mem, steps, n_envs, batch, seed) in enumerate([(50, 23, 4, 16, 3), (1000, 40, 8, 64, 4)]):
+        rng = np.random.default_rng(seed)
+        buf = MAR(mem, fields, agents, device="cpu")
+        rec = dict(memory_size=np.int64(mem), steps=np.int64(steps), n_envs=np.int64(n_envs),
+                   batch=np.int64(batch), seed=np.int64(seed))
+        for t in range(steps):
+            nan = t == steps - 1
+            obs = {a: rng.standard_normal((n_envs, dims[a][0])).astype(np.float32) for a in agents}
+            act = {a: rng.random((n_envs, dims[a][1])).astype(np.float32) for a in agents}
+            rew = {a: rng.standard_normal(n_envs).astype(np.float32) for a in agents}
+            nxt = {a: rng.standard_normal((n_envs, dims[a][0])).astype(np.float32) for a in agents}
+            done = {a: (rng.random(n_envs) < 0.3) for a in agents}
+            if nan:
+                rew["listener_0"][0] = np.nan
+                done["listener_0"] = done["listener_0"].astype(np.float32)
+                done["listener_0"][0] = np.nan
+            for f, d in zip(fields, (obs, act, rew, nxt, done)):
+                for a in agents:
+                    rec[f"save{t}.{f}.{a}"] = np.asarray(d[a])
+            buf.save_to_memory(obs, act, rew, nxt, done, is_vectorised=True)
+        for s in range(3):
+            random.seed(100 * seed + s)
+            sample = buf.sample(batch)
+            for f, per in zip(fields, sample):
+                for a in agents:
+                    rec[f"sample{s}.{f}.{a}"] = per[a].numpy()
+        out[f"marep{k}"] = rec
+
+
+def gen_maddpg(maddpg_mod, out: dict) -> None:
+    """MADDPG._learn_individual with stand-in critic / target / actor: the
+    critic TD target y = r + (1 - d) * gamma * Q'(s', a') after the NaN rules
+    (reward NaN -> 0, done NaN -> 1 then uint8), the MSE critic loss and its
+    gradient dL/dQ (captured at the critic optimizer step)."""
+    MADDPG = maddpg_mod.MADDPG
+    for k, (B, gamma, seed) in enumerate([(64, 0.95, 91), (33, 0.99, 92), (1024, 0.9, 93)]):
+        rng = np.random.default_rng(seed)
+        q = rng.standard_normal((B, 1)).astype(np.float32)
+        qn = rng.standard_normal((B, 1)).astype(np.float32)
+        r = rng.standard_normal((B, 1)).astype(np.float32)
+        d = (rng.random((B, 1)) < 0.2).astype(np.float32)
+        r[rng.random(B) < 0.05] = np.nan
+        d[rng.random(B) < 0.05] = np.nan
+        Q = torch.tensor(q, requires_grad=True)
+        rec: dict = {}
+
+        class _Critic:
+            def __call__(self, states, actions):
+                return Q
+
+        class _Target:
+            def __call__(self, states, actions):
+                return torch.tensor(qn)
+
+        class _Actor:
+            def __call__(self, x):
+                return torch.zeros(B, 2)
+
+        class _COpt:
+            def zero_grad(self):
+                Q.grad = None
+
+            def step(self):
+                rec["g_q"] = Q.grad.clone()
+
+        class _AOpt:
+            def zero_grad(self):
+                pass
+
+            def step(self):
+                pass
+
+        class _Crit:
+            def __call__(self, q_eval, y):
+                rec["y"] = y.detach().clone()
+                return torch.nn.functional.mse_loss(q_eval, y)
+
+        fake = object.__new__(MADDPG)
+        fake.gamma, fake.accelerator, fake.agent_ids = gamma, None, ["a0"]
+        fake.get_network_id = lambda agent_id: agent_id
+        fake.actors, fake.critics, fake.critic_targets = {"a0": _Actor()}, {"a0": _Critic()}, {"a0": _Target()}
+        fake.actor_optimizers, fake.critic_optimizers = {"a0": _AOpt()}, {"a0": _COpt()}
+        fake.criterion = _Crit()
+        _, closs = MADDPG._learn_individual(fake, "a0", torch.zeros(B, 2), torch.zeros(B, 2), {"a0": torch.zeros(B, 1)},
+                                            {"a0": torch.zeros(B, 1)}, {"a0": torch.zeros(B, 2)},
+                                            {"a0": torch.tensor(r)}, {"a0": torch.tensor(d)})
+        out[f"maddpg{k}"] = dict(gamma=np.float64(gamma), q=q, q_next=qn, r=r, d=d, y=rec["y"].numpy(),
+                                 critic_loss=np.float64(closs), g_q=rec["g_q"].numpy())
+
+
+# --------------------------------------------------------------------------- #
 # HPO mutations                                                               #
 # --------------------------------------------------------------------------- #
 class _MutNet(torch.nn.Module):
@@ -760,6 +911,9 @@ def main() -> None:
     dist_mod = _load(ref, "agilerl.networks.distributions", "agilerl/networks/distributions.py")
     reg = _load(ref, "agilerl.algorithms.core.registry", "agilerl/algorithms/core/registry.py")
     mut = _load(ref, "agilerl.hpo.mutation", "agilerl/hpo/mutation.py")
+    mar = _load(ref, "agilerl.components.multi_agent_replay_buffer",
+                "agilerl/components/multi_agent_replay_buffer.py")
+    maddpg = _load(ref, "agilerl.algorithms.maddpg", "agilerl/algorithms/maddpg.py")
 
     groups: dict[str, dict] = {}
     gen_gae(rb, groups)
@@ -771,6 +925,9 @@ def main() -> None:
     gen_tournament(tour, groups)
     gen_ppo_learn(ppo, en, tu, dist_mod, sys.modules["gymnasium.spaces"], groups)
     gen_mutation(mut, reg, groups)
+    gen_nstep(rp, groups)
+    gen_ma_replay(mar, groups)
+    gen_maddpg(maddpg, groups)
 
     if args.only:
         groups = {k: v for k, v in groups.items() if k in set(args.only)}

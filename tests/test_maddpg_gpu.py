@@ -134,3 +134,39 @@ def test_train_multi_agent_off_policy_and_checkpoint(tmp_path):
         for p1, p2 in zip(pop[0].actors[a].parameters(), other.actors[a].parameters()):
             assert torch.equal(p1, p2)
     assert other.fitness == pop[0].fitness
+
+
+@pytest.mark.parametrize("case", ["maddpg0", "maddpg1", "maddpg2"])
+def test_critic_target_kernel_matches_reference_golden(golden, case):
+    """agx_maddpg_critic_target against MADDPG._learn_individual run by the
+    reference (maddpg.py:764-790): y bit for bit, dL/dQ and the loss to f32
+    rounding of the mean."""
+    from agilerl_amd import kernels as K
+
+    g = golden(case)
+    q, qn, r, d = (torch.from_numpy(np.ascontiguousarray(g[k].reshape(-1))).cuda() for k in ("q", "q_next", "r", "d"))
+    y, grad, loss = K.maddpg_critic_target(q, qn, r, d, float(g["gamma"]))
+    np.testing.assert_array_equal(y.cpu().numpy().reshape(-1), g["y"].reshape(-1))
+    np.testing.assert_allclose(grad.cpu().numpy().reshape(-1), g["g_q"].reshape(-1), rtol=1e-6, atol=1e-9)
+    assert abs(float(loss) - float(g["critic_loss"])) <= 1e-6 * abs(float(g["critic_loss"]))
+
+
+@pytest.mark.parametrize("case", ["marep0", "marep1"])
+def test_hbm_replay_matches_reference_golden(golden, case):
+    """MultiAgentReplayBuffer in HBM: the reference's own samples under the
+    same Python random seeds (multi_agent_replay_buffer.py:155-167)."""
+    import random
+
+    from agilerl_amd.components import MultiAgentReplayBuffer
+
+    fields, agents = ["obs", "action", "reward", "next_obs", "done"], ["speaker_0", "listener_0"]
+    g = golden(case)
+    buf = MultiAgentReplayBuffer(int(g["memory_size"]), fields, agents, device="cuda")
+    for t in range(int(g["steps"])):
+        buf.save_to_memory(*[{a: g[f"save{t}.{f}.{a}"] for a in agents} for f in fields], is_vectorised=True)
+    for s in range(3):
+        random.seed(100 * int(g["seed"]) + s)
+        sample = buf.sample(int(g["batch"]))
+        for f, per in zip(fields, sample):
+            for a in agents:
+                assert np.array_equal(per[a].cpu().numpy(), g[f"sample{s}.{f}.{a}"], equal_nan=True), (s, f, a)
