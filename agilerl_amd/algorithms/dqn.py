@@ -5,7 +5,8 @@ target update in agx_polyak.
 The Q networks are the reference's ``QNetwork`` / ``RainbowQNetwork``
 (agilerl_amd.networks: EvolvableMLP encoder + head with the reference's
 defaults, initialisation and state-dict keys) on the GPU; ``learn`` takes the reference's experience mapping (obs, action, reward, next_obs,
-done) and returns the loss as a float.  Supported: Box observations,
+done) and returns the loss as a float.  Supported: Box observations (vectors, or
+image frames through EvolvableCNN encoders on the HIP conv kernels),
 Discrete actions, ``net_config`` ``encoder_config`` / ``head_config``
 ``hidden_size`` lists.
 """
@@ -20,7 +21,35 @@ import torch
 from .. import kernels as K
 from . import checkpoint as C
 from ..networks import QNetwork, RainbowQNetwork
-from ..networks.base import mlp_net_config
+from ..networks.base import image_norm_bounds, is_image_space, mlp_net_config
+
+
+def _setup_image_input(agent, normalize_images: bool) -> None:
+    """Image Box spaces: the networks get EvolvableCNN encoders; with
+    normalize_images and finite [low, high] != [0, 1] the frames stay uint8
+    up to the first convolution, which normalises them in its load
+    (preprocess_observation -> apply_image_normalization, algo_utils.py:
+    996-1022, 1134-1183)."""
+    agent.normalize_images = normalize_images
+    agent._image = is_image_space(agent.observation_space)
+    agent._img_norm = image_norm_bounds(agent.observation_space) if agent._image and normalize_images else None
+    for net in (agent.actor, agent.actor_target):
+        net.set_image_norm(agent._img_norm)
+
+
+def _obs_tensor(agent, obs) -> torch.Tensor:
+    x = obs if isinstance(obs, torch.Tensor) else torch.as_tensor(np.asarray(obs))
+    x = x.to(agent.device)
+    if not agent._image:
+        return x.to(torch.float32).reshape(-1, agent.obs_dim)
+    x = x.reshape(-1, *agent.observation_space.shape)
+    if x.dtype == torch.uint8 and agent._img_norm is not None:
+        return x  # normalised inside the first convolution
+    x = x.to(torch.float32)
+    if agent._img_norm is not None:  # float frames: the reference's (x - low) / (high - low) in f32
+        lo, hi = agent._img_norm
+        x = (x - lo) / float(np.float32(hi) - np.float32(lo))
+    return x
 
 
 def _net_kwargs(net_config) -> dict:
@@ -69,6 +98,7 @@ class DQN(C.TorchCheckpointMixin):
         self.actor = QNetwork(observation_space, action_space, device=self.device, **_net_kwargs(net_config))
         self.actor_target = QNetwork(observation_space, action_space, device=self.device, **_net_kwargs(net_config))
         self.actor_target.load_state_dict(self.actor.state_dict())
+        _setup_image_input(self, normalize_images)
         self.optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr)
         self.scores: list[float] = []
         self.fitness: list[float] = []
@@ -82,8 +112,7 @@ class DQN(C.TorchCheckpointMixin):
                    tau=INIT_HP.get("TAU", 1e-3), double=INIT_HP.get("DOUBLE", False), device=device, **kw)
 
     def _obs(self, obs) -> torch.Tensor:
-        return torch.as_tensor(np.asarray(obs) if not isinstance(obs, torch.Tensor) else obs,
-                               dtype=torch.float32).to(self.device).reshape(-1, self.obs_dim)
+        return _obs_tensor(self, obs)
 
     @torch.no_grad()
     def get_action(self, obs, epsilon: float = 0.0, action_mask=None, *args: Any, **kwargs: Any) -> np.ndarray:
@@ -232,6 +261,7 @@ class RainbowDQN(C.TorchCheckpointMixin):
                                             num_atoms=num_atoms, noise_std=noise_std, device=self.device,
                                             **self._net_kwargs(net_config))
         self.actor_target.load_state_dict(self.actor.state_dict())
+        _setup_image_input(self, normalize_images)
         self.optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr)
         self.scores: list[float] = []
         self.fitness: list[float] = []
@@ -256,8 +286,7 @@ class RainbowDQN(C.TorchCheckpointMixin):
                    n_step=INIT_HP.get("N_STEP", 3), device=device, **kw)
 
     def _obs(self, obs) -> torch.Tensor:
-        return torch.as_tensor(np.asarray(obs) if not isinstance(obs, torch.Tensor) else obs,
-                               dtype=torch.float32).to(self.device).reshape(-1, self.obs_dim)
+        return _obs_tensor(self, obs)
 
     @torch.no_grad()
     def get_action(self, obs, action_mask=None, training: bool = True, *args, **kwargs) -> np.ndarray:

@@ -121,6 +121,33 @@ class SyntheticVecEnv:
         pass
 
 
+class SyntheticAtariVecEnv(SyntheticVecEnv):
+    """Pong-shaped stand-in (ALE is not installed): uint8 frame stacks
+    ``(4, 84, 84)`` in [0, 255] (AtariPreprocessing + FrameStack, channels
+    first), 6 discrete actions, sparse rewards in {-1, 0, +1} (a point every
+    ~60 steps), termination ~ Bernoulli(1/800).  Frames come from a ring of
+    pre-generated batches, as SyntheticVecEnv."""
+
+    def __init__(self, num_envs: int, frame_shape=(4, 84, 84), n_actions: int = 6, p_done: float = 1 / 800,
+                 seed: int = 0, ring: int = 13, max_episode_steps: int | None = None):
+        self.num_envs = int(num_envs)
+        self.single_observation_space = Box(0, 255, tuple(frame_shape), dtype=np.uint8)
+        self.single_action_space = Discrete(n_actions)
+        self.observation_space = self.single_observation_space
+        self.action_space = self.single_action_space
+        rng = np.random.default_rng(seed)
+        self._obs = rng.integers(0, 256, (ring, num_envs, *frame_shape), dtype=np.uint8)
+        point = rng.random((ring, num_envs)) < 1 / 60
+        self._rew = np.where(point, np.where(rng.random((ring, num_envs)) < 0.5, -1.0, 1.0), 0.0).astype(np.float32)
+        self._term = rng.random((ring, num_envs)) < p_done
+        self._trunc = np.zeros(num_envs, dtype=bool)
+        self.max_episode_steps = max_episode_steps
+        self._len = np.zeros(num_envs, dtype=np.int64)
+        self._k = 0
+        self._ring = ring
+        self.steps = 0
+
+
 class SyntheticMultiAgentVecEnv:
     """PettingZoo-parallel-style vectorised multi-agent stand-in shaped like
     MPE simple_speaker_listener (speaker: obs 3, 3 actions; listener: obs 11,

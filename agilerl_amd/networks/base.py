@@ -1,7 +1,9 @@
-"""MLP-encoder part of ``EvolvableNetwork`` (agilerl/networks/base.py:150-560).
+"""Encoder part of ``EvolvableNetwork`` (agilerl/networks/base.py:150-560).
 
-The hot path covers Box observations with EvolvableMLP encoders; image / dict
-/ recurrent / SimBa encoders are outside it and raise NotImplementedError.
+Box observations get EvolvableMLP encoders, image Box spaces (3-D shape,
+utils/evolvable_networks.py:74-84) EvolvableCNN encoders on the HIP conv
+kernels (modules/cnn.py), Dict/Tuple spaces EvolvableMultiInput; recurrent
+and SimBa encoders are outside the hot path and raise NotImplementedError.
 """
 
 from __future__ import annotations
@@ -12,6 +14,7 @@ import numpy as np
 import torch
 from torch import nn
 
+from ..modules.cnn import EvolvableCNN
 from ..modules.mlp import EvolvableMLP, preserve_parameters
 
 
@@ -22,6 +25,39 @@ def mlp_net_config(hidden_size, **overrides) -> dict[str, Any]:
                output_layernorm=False, init_layers=True, noisy=False, noise_std=0.5)
     cfg.update(overrides)
     return cfg
+
+
+def cnn_net_config(**overrides) -> dict[str, Any]:
+    """``asdict(CnnNetConfig(channel_size=[32, 32], kernel_size=[3, 3],
+    stride_size=[1, 1], output_activation="ReLU"))`` — the default image
+    encoder (evolvable_networks.py:190-196, configs.py:114-127)."""
+    cfg = dict(channel_size=[32, 32], kernel_size=[3, 3], stride_size=[1, 1], sample_input=None, activation="ReLU",
+               output_activation="ReLU", block_type="Conv2d", min_hidden_layers=1, max_hidden_layers=6,
+               min_channel_size=16, max_channel_size=256, layer_norm=False, init_layers=True)
+    cfg.update(overrides)
+    return cfg
+
+
+def is_image_space(space) -> bool:
+    """evolvable_networks.py:74-84: a Box with a 3-D shape."""
+    return hasattr(space, "shape") and not hasattr(space, "n") and not hasattr(space, "spaces") \
+        and space.shape is not None and len(space.shape) == 3
+
+
+def image_norm_bounds(space) -> tuple[float, float] | None:
+    """(low, high) of apply_image_normalization (algo_utils.py:1134-1183) when
+    the kernel can fold it into its load: finite, uniform bounds other than
+    [0, 1].  None when the reference leaves the frames as they are (infinite
+    or [0, 1] bounds); ValueError for per-pixel bounds, which the agx path
+    does not normalise."""
+    low, high = np.asarray(space.low, dtype=np.float64), np.asarray(space.high, dtype=np.float64)
+    if np.isinf(high).any() or np.isinf(low).any():
+        return None
+    if np.all(high == 1) and np.all(low == 0):
+        return None
+    if low.min() != low.max() or high.min() != high.max():
+        raise ValueError("agx image inputs: per-pixel observation bounds are not supported (uniform low/high)")
+    return float(np.float32(low.flat[0])), float(np.float32(high.flat[0]))
 
 
 def as_config(cfg) -> dict[str, Any] | None:
@@ -57,8 +93,9 @@ class EvolvableNetwork(nn.Module):
         self.latent_dim, self.min_latent_dim, self.max_latent_dim = latent_dim, min_latent_dim, max_latent_dim
         self.device, self.random_seed, self.encoder_name = device, random_seed, encoder_name
         encoder_config = as_config(encoder_config)
+        image = not multi and is_image_space(observation_space)
         if encoder_config is None:  # get_default_encoder_config (utils/evolvable_networks.py:168-216)
-            encoder_config = {"output_activation": "ReLU"} if multi else \
+            encoder_config = {"output_activation": "ReLU"} if multi else cnn_net_config() if image else \
                 mlp_net_config([64, 64], output_activation="ReLU", output_vanish=False)
         if encoder_config.get("output_activation") is None:  # base.py:226-230
             encoder_config["output_activation"] = encoder_config.get("activation", "ReLU")
@@ -70,6 +107,12 @@ class EvolvableNetwork(nn.Module):
             self.encoder_config = encoder_config
             self.encoder = EvolvableMultiInput(observation_space, num_outputs=latent_dim, device=device,
                                                name=encoder_name, **encoder_config)
+            return
+        if image:  # EvolvableCNN encoder (base.py:521-530)
+            encoder_config.pop("num_outputs", None)
+            self.encoder_config = encoder_config
+            self.encoder = EvolvableCNN(input_shape=list(observation_space.shape), num_outputs=latent_dim,
+                                        device=device, name=encoder_name, **encoder_config)
             return
         # MLP encoders: output LayerNorm follows layer_norm, no output vanish (base.py:547-554)
         encoder_config["output_layernorm"] = encoder_config.get("layer_norm", True)
@@ -92,8 +135,19 @@ class EvolvableNetwork(nn.Module):
         return EvolvableMLP(num_inputs=num_inputs, num_outputs=num_outputs, device=self.device, name=name,
                             **net_config)
 
+    def set_image_norm(self, bounds: tuple[float, float] | None) -> None:
+        """uint8 frames are normalised inside the first convolution's load."""
+        if not isinstance(self.encoder, EvolvableCNN):
+            return
+        if bounds is None:
+            self.encoder.clear_image_norm()
+        else:
+            self.encoder.set_image_norm(*bounds)
+
     def recreate_encoder(self) -> None:
         cfg = dict(self.encoder.net_config)
+        if isinstance(self.encoder, EvolvableCNN):
+            raise NotImplementedError("CNN architecture mutations change the conv shapes (not applied)")
         new = EvolvableMLP(num_inputs=self.encoder.num_inputs, num_outputs=self.latent_dim, device=self.device,
                            name=self.encoder_name, **cfg)
         self.encoder = preserve_parameters(self.encoder, new)

@@ -14,7 +14,7 @@ import torch
 from torch.nn import functional as F
 
 from ..modules.mlp import EvolvableMLP, create_mlp
-from .base import EvolvableNetwork, as_config, flatdim, mlp_net_config
+from .base import EvolvableNetwork, as_config, flatdim, is_image_space, mlp_net_config
 
 
 class QNetwork(EvolvableNetwork):
@@ -94,14 +94,15 @@ class RainbowQNetwork(EvolvableNetwork):
                  max_latent_dim: int = 128, latent_dim: int = 32, device="cpu",
                  random_seed: int | None = None) -> None:
         encoder_config = as_config(encoder_config)
-        if encoder_config is None:
-            encoder_config = mlp_net_config([64, 64], output_activation="ReLU", output_vanish=False)
-        # q_networks.py:212-220: plain (non-noisy) encoder, default init, LayerNorm
-        encoder_config["noise_std"] = noise_std
-        encoder_config["output_activation"] = encoder_config.get("activation", "ReLU")
-        encoder_config["output_vanish"] = False
-        encoder_config["init_layers"] = False
-        encoder_config["layer_norm"] = True
+        if not is_image_space(observation_space):  # q_networks.py:189-206: MLP encoders only
+            if encoder_config is None:
+                encoder_config = mlp_net_config([64, 64], output_activation="ReLU", output_vanish=False)
+            # plain (non-noisy) encoder, default init, LayerNorm
+            encoder_config["noise_std"] = noise_std
+            encoder_config["output_activation"] = encoder_config.get("activation", "ReLU")
+            encoder_config["output_vanish"] = False
+            encoder_config["init_layers"] = False
+            encoder_config["layer_norm"] = True
         super().__init__(observation_space, encoder_config=encoder_config, action_space=action_space,
                          min_latent_dim=min_latent_dim, max_latent_dim=max_latent_dim, latent_dim=latent_dim,
                          device=device, random_seed=random_seed)

@@ -396,6 +396,31 @@ int agx_clip_adam(float *params, float *grads, float *exp_avg, float *exp_avg_sq
  * (dqn.py:349-358, dqn_rainbow.py:492-501). */
 int agx_polyak(float *target, const float *online, int64_t n, float tau, void *stream);
 
+/* ---- convolutional encoder (EvolvableCNN) -----------------------------------
+ * Conv2d layers of agilerl/modules/cnn.py:224-552 (create_cnn,
+ * utils/evolvable_networks.py:460-525) as implicit GEMMs on the f32 matrix
+ * cores; NCHW f32 tensors, weights [Cout][Cin][KH][KW], no padding, square
+ * stride (the Atari encoders: 8x8/4, 4x4/2, 3x3/1).  The first layer may
+ * read uint8 frames directly (x_is_u8): each pixel becomes
+ * (x - x_low) / (x_high - x_low) on load, the reference's image
+ * normalisation (utils/algo_utils.py:1134-1183), in f32 with an IEEE divide. */
+typedef struct agx_conv2d_shape {
+    int64_t batch;
+    int32_t in_channels, height, width, out_channels, kernel_h, kernel_w, stride;
+} agx_conv2d_shape;
+/* y = act(conv(x, w) + bias), act = ReLU when relu != 0 (bias may be NULL). */
+int agx_conv2d_forward(const agx_conv2d_shape *shape, const void *x, int x_is_u8, float x_low, float x_high,
+                       const float *w, const float *bias, int relu, float *y, void *stream);
+size_t agx_conv2d_wgrad_workspace_bytes(const agx_conv2d_shape *shape);
+/* Gradients of that layer from dy = dL/d(output): y_act (the forward's
+ * post-ReLU output, or NULL for no activation) masks dy; dw, db (db may be
+ * NULL) receive (or with accumulate += ) the weight / bias gradients — a
+ * split-K reduction summed in a fixed order; dx (NULL: skip; not available
+ * for u8 inputs) receives the input gradient. */
+int agx_conv2d_backward(const agx_conv2d_shape *shape, const void *x, int x_is_u8, float x_low, float x_high,
+                        const float *w, const float *y_act, const float *dy, float *dx, float *dw, float *db,
+                        int accumulate, void *workspace, void *stream);
+
 /* ---- diagnostics ---------------------------------------------------------
  * out[i] = pow(x[i], y[i]) by the routine the PER leaves and IS weights use
  * (glibc's pow algorithm, bit-identical to the host libm); for parity tests. */

@@ -112,3 +112,70 @@ def test_dqn_checkpoint_round_trip_cpu(algo, tmp_path):
     wrong = (dqn.RainbowDQN if algo == "DQN" else dqn.DQN)(Box(-np.inf, np.inf, (8,)), Discrete(4), device="cpu")
     with pytest.raises(ValueError):  # registry mismatch (core/base.py:1046-1052)
         wrong.load_checkpoint(path)
+
+
+def test_evolvable_cnn_layout_and_seeded_init():
+    """EvolvableCNN (modules/cnn.py:224-552): module names / state-dict keys of
+    create_cnn (utils/evolvable_networks.py:460-525) + flatten / linear output,
+    and the reference's draw order under one seed — each nn.Conv2d built then
+    layer_init'd (orthogonal gain sqrt(2), bias 0), then the final Linear with
+    torch's default init — so a seeded run starts from the reference's weights."""
+    from torch import nn
+
+    from agilerl_amd.modules import EvolvableCNN
+
+    cfg = dict(channel_size=[32, 64, 128], kernel_size=[8, 4, 3], stride_size=[4, 2, 1])
+    torch.manual_seed(3)
+    net = EvolvableCNN([4, 84, 84], 256, name="encoder", output_activation="ReLU", **cfg)
+    names = [n for n, _ in net.model.named_children()]
+    assert names == ["encoder_conv_layer_1", "encoder_activation_1", "encoder_conv_layer_2", "encoder_activation_2",
+                     "encoder_conv_layer_3", "encoder_activation_3", "encoder_flatten", "encoder_linear_output",
+                     "encoder_output_activation"]
+    assert tuple(net.cnn_output_size) == (1, 128, 7, 7)
+    # restated reference construction order
+    torch.manual_seed(3)
+    want, c = [], 4
+    for ch, k, s in zip(cfg["channel_size"], cfg["kernel_size"], cfg["stride_size"]):
+        conv = nn.Conv2d(c, ch, k, s)
+        nn.init.orthogonal_(conv.weight, np.sqrt(2))
+        nn.init.constant_(conv.bias, 0.0)
+        want += [conv.weight, conv.bias]
+        c = ch
+    lin = nn.Linear(128 * 7 * 7, 256)
+    want += [lin.weight, lin.bias]
+    got = list(net.state_dict().values())
+    assert len(got) == len(want) and all(torch.equal(a, b) for a, b in zip(got, want))
+    assert net.model.encoder_conv_layer_1.fuse_relu and net.model.encoder_conv_layer_1.image_norm is None
+    net.set_image_norm(0.0, 255.0)
+    assert net.model.encoder_conv_layer_1.image_norm == (0.0, 255.0)
+    assert net.model.encoder_conv_layer_2.image_norm is None
+    with pytest.raises(Exception):  # no CPU fallback for the convolutions
+        net(torch.zeros(1, 4, 84, 84))
+
+
+def test_image_space_networks_and_preprocessing():
+    """Image Box spaces (is_image_space, evolvable_networks.py:74-84) get the
+    default CNN encoder (32/32, 3/3, 1/1, evolvable_networks.py:190-196); the
+    agents keep uint8 frames for the kernel's in-load normalisation and
+    normalise f32 frames as apply_image_normalization (algo_utils.py:1134-1183)."""
+    from agilerl_amd.algorithms import DQN, RainbowDQN
+    from agilerl_amd.envs import Box, Discrete
+    from agilerl_amd.modules import EvolvableCNN
+    from agilerl_amd.networks.base import image_norm_bounds
+
+    obs, act = Box(0, 255, (4, 84, 84), dtype=np.uint8), Discrete(6)
+    d = DQN(obs, act, device="cpu")
+    assert isinstance(d.actor.encoder, EvolvableCNN)
+    assert d.actor.encoder.channel_size == [32, 32] and d.actor.encoder.kernel_size == [3, 3]
+    assert d.actor.encoder.output_activation == "ReLU"
+    r = RainbowDQN(obs, act, device="cpu", normalize_images=False)
+    assert r._img_norm is None and r.actor.encoder.model.encoder_conv_layer_1.image_norm is None
+    x = r._obs(np.full((2, 4, 84, 84), 255, np.uint8))
+    assert x.dtype == torch.float32 and float(x.max()) == 255.0  # no normalisation requested
+    u = d._obs(np.full((4, 84, 84), 51, np.uint8))
+    assert u.dtype == torch.uint8 and u.shape == (1, 4, 84, 84)
+    f = d._obs(np.full((1, 4, 84, 84), 51.0, np.float32))
+    assert f.dtype == torch.float32 and float(f[0, 0, 0, 0]) == np.float32(51.0) / np.float32(255.0)
+    assert image_norm_bounds(Box(0, 1, (3, 8, 8))) is None
+    assert image_norm_bounds(Box(-np.inf, np.inf, (3, 8, 8))) is None
+    assert image_norm_bounds(Box(-1, 7, (3, 8, 8))) == (-1.0, 7.0)
