@@ -71,6 +71,7 @@ SIGNATURES = {
     "agx_conv2d_backward": (_INT, [_P, _P, _INT, _F, _F, _P, _P, _P, _P, _P, _P, _INT, _P, _P]),
     "agx_debug_pow": (_INT, [_P, _P, _P, _I, _P]),
     "agx_debug_learn_stamps": (_INT, [_P]),
+    "agx_debug_rollout_stamps": (_INT, [_P]),
     "agx_debug_learn_stall": (_INT, [_INT]),
     "agx_host_shuffle_perms": (_INT, [_P, _P, _I, _I, _I, _P, _P]),
     "agx_debug_stream": (_INT, [_P, _P, _I, _INT, _I, _P]),

@@ -1635,7 +1635,11 @@ static bool find_launcher(const agx_ppo_net *net, Launcher &out) {
     return false;
 }
 
-static long long *&g_stamps_ptr() {
+static long long *&g_stamps_ptr() {  // learner phase stamps, int64[80]
+    static long long *p = nullptr;
+    return p;
+}
+static long long *&g_roll_stamps_ptr() {  // persistent-rollout stamps, int64[384]
     static long long *p = nullptr;
     return p;
 }
@@ -1700,6 +1704,11 @@ extern "C" size_t agx_ppo_learn_workspace_bytes(const agx_ppo_net *net, int64_t 
 extern "C" int agx_debug_learn_stamps(int64_t *buf) {
     static_assert(sizeof(long long) == sizeof(int64_t), "");
     g_stamps_ptr() = reinterpret_cast<long long *>(buf);
+    return AGX_OK;
+}
+
+extern "C" int agx_debug_rollout_stamps(int64_t *buf) {
+    g_roll_stamps_ptr() = reinterpret_cast<long long *>(buf);
     return AGX_OK;
 }
 
@@ -1954,7 +1963,7 @@ extern "C" int agx_ppo_rollout_persistent(const agx_ppo_net *net, int64_t P, int
     const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
     ctl->nwg = (uint32_t)agx_rollout_workgroups(P, N);
     dim3 grid((unsigned)ceil_div(N, kSB), (unsigned)P);
-    L.persist(steps, (int)nsteps, ctl, ticks, base, g_stamps_ptr(), grid, (size_t)L.plan->act_floats * sizeof(float),
+    L.persist(steps, (int)nsteps, ctl, ticks, base, g_roll_stamps_ptr(), grid, (size_t)L.plan->act_floats * sizeof(float),
               as_stream(stream));
     return check_launch("agx_ppo_rollout_persistent");
 }

@@ -430,6 +430,11 @@ int agx_debug_pow(const double *x, const double *y, double *out, int64_t n, void
  * [sub_batch*16 + phase], phases 0-8 per sub-batch, 9-11 at slot 64+);
  * buf = NULL disables. */
 int agx_debug_learn_stamps(int64_t *buf);
+/* Persistent-rollout phase timing: subsequent agx_ppo_rollout_persistent
+ * launches write s_memrealtime stamps into buf (device int64[384]: workgroup
+ * 0's phases [step*8 + k] for steps < 32, per-workgroup stamps of step 5 at
+ * 256 + wg and 320 + wg for wg < 64); buf = NULL disables. */
+int agx_debug_rollout_stamps(int64_t *buf);
 /* Test hook: on != 0 makes partner workgroup 1 of agent 0 skip every
  * hand-off of subsequent agx_ppo_learn calls (when the call splits agents
  * over partners), so the bounded partner wait times out and sets

@@ -70,9 +70,9 @@ print(f"env step {1e6 * sum(env_t) / len(env_t):.1f} us; collect {1e3 * sum(laun
 
 # in-kernel phases of workgroup 0 (s_memrealtime, 100 MHz)
 buf = torch.zeros(384, dtype=torch.int64, device="cuda")
-lib.agx_debug_learn_stamps(ctypes.c_void_p(buf.data_ptr()))
+lib.agx_debug_rollout_stamps(ctypes.c_void_p(buf.data_ptr()))
 run.collect()
-lib.agx_debug_learn_stamps(None)
+lib.agx_debug_rollout_stamps(None)
 pop.finish_rollout(run.last_obs, run.last_done, run.last_value)
 torch.cuda.synchronize()
 st = buf[:256].view(32, 8).cpu().numpy()[:T + 1].astype(float) * 10.0  # ns
