@@ -55,7 +55,7 @@ constexpr int kNT = 512;
 constexpr int kNW = kNT / kWave;  // 8 waves
 constexpr int kSB = 32;           // rows per sub-batch
 constexpr int kMaxSlot = 10;      // dW tiles per wave
-constexpr int kMaxK = 4;          // partner workgroups per agent (hand-off unrolled for <= 4)
+constexpr int kMaxK = 8;          // partner workgroups per agent
 constexpr int kMaxPT = 32;        // LDS parameter slots per thread: 8 float4 chunks
 constexpr int kMaxA = 16;
 constexpr int kMaxBlk = 28;
@@ -420,9 +420,10 @@ __device__ __forceinline__ int lds_to_flat(int l, int &group) {
 // ---------------------------------------------------------------------------
 // shared forward (X0 in LDS -> y_h in S1, logits in lg, value in val)
 // ---------------------------------------------------------------------------
-template <class C>
+template <class C, int SB = kSB>
 struct Fwd {
     static constexpr LearnPlan pl = C::plan;
+    static_assert(SB == 16 || SB == 32, "sub-batch rows");
     float *sm;
 
     // LayerNorm(+affine)+ReLU of Z (S2, width F; LN groups [0,split), [split,F))
@@ -433,6 +434,7 @@ struct Fwd {
         constexpr int F0 = split < F ? split : F, F1 = F - F0;
         AGX_IDS;
         const int r = rrow;
+        if (SB < kSB && r >= SB) return;  // whole 16-lane rows beyond the sub-batch idle
         float z[NC];
         float s0 = 0.f, s1 = 0.f;
 #pragma unroll
@@ -467,10 +469,10 @@ struct Fwd {
     // Z[SB x fout] = X W^T + b  -> S2
     template <int xb, int ldx, int K, int wb, int ldw, int bias, int fout>
     __device__ __forceinline__ void gemm_fwd() {
-        constexpr int nt = (kSB / 16) * (fout / 16);
+        constexpr int nt = (SB / 16) * (fout / 16);
         AGX_IDS;
         for (int t = wave; t < nt; t += kNW) {
-            const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
+            const int m0 = (t % (SB / 16)) * 16, n0 = (t / (SB / 16)) * 16;
             f4 c = f4{0.f, 0.f, 0.f, 0.f};
             c = mfma_tile<K>(c, [&](int m, int k) { return sm[xb + (m0 + m) * ldx + k]; },
                              [&](int k, int n) { return sm[wb + (n0 + n) * ldw + k]; });
@@ -498,9 +500,9 @@ struct Fwd {
         __syncthreads();
         ln_rows<pl.H, pl.ha, pl.l_xh, pl.ld_xh, pl.l_rh, pl.l_hg, pl.l_hbe>();
         __syncthreads();
-        // output layers: 2 row tiles x {actor logits, critic value}
+        // output layers: SB/16 row tiles x {actor logits (waves 0-1), critic value (waves 2-3)}
         AGX_IDS;
-        if (wave < 2) {
+        if (wave < SB / 16) {
             const int m0 = wave * 16;
             f4 c = f4{0.f, 0.f, 0.f, 0.f};
             c = mfma_tile<pl.ha>(c, [&](int m, int k) { return sm[pl.l_s1 + (m0 + m) * pl.ld_s + k]; },
@@ -508,7 +510,7 @@ struct Fwd {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 if (lr16 < pl.A) sm[pl.l_lg + (m0 + lq * 4 + i) * kMaxA + lr16] = c[i] + sm[pl.l_aob + lr16];
-        } else if (wave < 4) {
+        } else if (wave >= 2 && wave < 2 + SB / 16) {
             const int m0 = (wave - 2) * 16;
             f4 c = f4{0.f, 0.f, 0.f, 0.f};
             c = mfma_tile<pl.hc>(c, [&](int m, int k) { return sm[pl.l_s1 + (m0 + m) * pl.ld_s + pl.ha + k]; },
@@ -536,7 +538,6 @@ template <class C>
 __device__ __forceinline__ void load_params(float *sm, const float *gp, int tid) {
     // block by block (compile-time table): one division by a constant row
     // length per element instead of a search over all blocks
-    constexpr LearnPlan pl = C::plan;
     blk_copy<C, 0>(sm, gp, tid);
 }
 
@@ -562,14 +563,16 @@ struct LearnArgs {
     long long *stamps;
     int K;                 // workgroups per agent (data-parallel over sub-batches)
     float *slabs;          // [P][2][K][slab] gradient hand-off (double-buffered)
-    unsigned *cnt;         // [P] arrival counters, [P] = timeout word (zeroed per call)
+    float *sums;           // [P][2][slab] reduce-scattered gradient sums (double-buffered)
+    unsigned *cnt;         // [P] arrival counters, [P] timeout word, [P+1+p] second-barrier
+                           // counters (zeroed per call)
     int debug_stall;       // test hook: partner 1 of agent 0 never arrives
 };
 
 #define IC(x) std::integral_constant<int, (x)>()
 #define BC(x) std::integral_constant<bool, (x)>()
 
-constexpr unsigned kSpinMax = 1u << 22;  // ~ seconds of s_sleep polling: a missing partner is a bug
+constexpr unsigned kSpinMax = 1u << 23;  // ~ seconds of s_sleep polling: a missing partner is a bug
 
 #define AGX_STAMP(slot)                                                          \
     do {                                                                         \
@@ -580,7 +583,7 @@ constexpr unsigned kSpinMax = 1u << 22;  // ~ seconds of s_sleep polling: a miss
 // ---------------------------------------------------------------------------
 // learner
 // ---------------------------------------------------------------------------
-template <class C>
+template <class C, int SB>
 __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     constexpr LearnPlan pl = C::plan;
@@ -593,7 +596,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     float *gm = g.m + (size_t)p * pl.n;
     float *gv = g.v + (size_t)p * pl.n;
     const long long S = g.S;
-    Fwd<C> fw{sm};
+    Fwd<C, SB> fw{sm};
 
     for (int i = tid; i < pl.lds_floats; i += kNT) sm[i] = 0.f;
     __syncthreads();
@@ -635,11 +638,48 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     unsigned *legal = reinterpret_cast<unsigned *>(sm + pl.l_row + 5 * kSB);
     if (g.debug_stall && p == 0 && kk == 1) return;  // test hook: a partner that never arrives
 
+    // one thread's share of a sub-batch's inputs: obs words (LDS x0 image incl.
+    // padding) and one row word (old_logp/adv/ret/old_v, action or legal mask)
+    constexpr int kPreObs = (SB * pl.ld_x0 + kNT - 1) / kNT;
+    struct Pre {
+        int e, mb, sb;
+        float ob[kPreObs];
+        unsigned rv;
+    };
+    auto fetch = [&](int e_, int mb_, int sb_) {
+        Pre r;
+        r.e = e_;
+        r.mb = mb_;
+        r.sb = sb_;
+        const int tid = vtid();
+        const long long s0_ = (long long)mb_ * Bp;
+        const int bsz_ = (int)((s0_ + Bp <= S) ? Bp : S - s0_);
+        const int nrow_ = e_ >= Ep ? 0 : (bsz_ - sb_ < SB ? bsz_ - sb_ : SB);
+        const size_t ep = (size_t)(e_ < Ep ? e_ : 0) * g.P + p;
+        const float *eo = g.gobs + ep * S * pl.D;
+#pragma unroll
+        for (int k = 0; k < kPreObs; ++k) {
+            const int i = tid + k * kNT;
+            const int rr = i / pl.ld_x0, dd = i % pl.ld_x0;
+            r.ob[k] = (rr < nrow_ && dd < pl.D) ? eo[(s0_ + sb_ + rr) * pl.D + dd] : 0.f;
+        }
+        r.rv = 0u;
+        if (tid < 4 * kSB) {
+            const int k = tid / kSB, rr = tid % kSB;
+            r.rv = rr < nrow_ ? __builtin_bit_cast(unsigned, g.grow[ep * 4 * S + (size_t)k * S + s0_ + sb_ + rr]) : 0u;
+        } else if (tid < 5 * kSB) {
+            const int rr = tid - 4 * kSB;
+            r.rv = rr < nrow_ ? (unsigned)g.gact[ep * S + s0_ + sb_ + rr] : 0u;
+        } else if (tid < 6 * kSB) {
+            const int rr = tid - 5 * kSB;
+            r.rv = (g.gmask && rr < nrow_) ? g.gmask[ep * S + s0_ + sb_ + rr] : 0xffffffffu;
+        }
+        return r;
+    };
+    Pre pre{};
+    if constexpr (kPreObs == 1) pre = fetch(0, 0, kk * SB);
+
     for (int e = 0; e < Ep; ++e) {
-        const float *eobs = g.gobs + ((size_t)e * g.P + p) * S * pl.D;
-        const int *eact = g.gact + ((size_t)e * g.P + p) * S;
-        const unsigned *emask = g.gmask ? g.gmask + ((size_t)e * g.P + p) * S : nullptr;
-        const float *erow = g.grow + ((size_t)e * g.P + p) * 4 * S;
         for (int mb = 0; mb < nmb; ++mb) {
             const long long s0 = (long long)mb * Bp;
             const int bsz = (int)((s0 + Bp <= S) ? Bp : S - s0);
@@ -693,33 +733,82 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             auto slab_put = [&](int l, float x) {
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), slab_rsrc, l * 4, 0, 16);
             };
+            // this agent's summed-gradient slab (written by the reduce-scatter)
+            const auto sum_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                g.K > 1 ? g.sums + ((size_t)p * 2 + (upd & 1)) * pl.slab : nullptr, 0,
+                __builtin_amdgcn_readfirstlane(pl.slab * 4), 0x00020000);
+            // Partner barrier (MI355X_MICROARCH visibility rules): every wave drains its
+            // write-through (sc1) stores (vmcnt) -> workgroup barrier -> one relaxed
+            // agent-scope ticket; relaxed poll with s_sleep -> barrier -> readers use
+            // sc1 loads (no fences, cdna_hip_programming.md §6 G16 R1).  Bounded: on
+            // timeout the timeout word and the caller's error word are set and the
+            // caller's whole block exits.
+            auto partner_sync = [&](unsigned *ctr, unsigned target, int st0, int st1) -> bool {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                const int tid = vtid();
+                if (tid == 0) {
+                    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    AGX_STAMP(st0);
+                    unsigned spins = 0;
+                    int ok = 1;
+                    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > kSpinMax) {
+                            __hip_atomic_store(g.cnt + g.P, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (g.err) __hip_atomic_fetch_or(g.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            ok = 0;
+                            break;
+                        }
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    stat[4 * kNW] = ok ? 1.f : 0.f;
+                    AGX_STAMP(st1);
+                }
+                __syncthreads();
+                return stat[4 * kNW] != 0.f;
+            };
             // partners publish each group's dW straight from registers as soon as the
             // group is final (last sub-batch), overlapping the stores with the rest of
             // the backward pass
             const bool direct = g.K > 1;
 
-            for (int sb = kk * kSB; sb < bsz; sb += g.K * kSB) {
-                const bool last_sb = sb + g.K * kSB >= bsz;
-                const int nrow = bsz - sb < kSB ? bsz - sb : kSB;
-                const int jsb = (sb / kSB) / g.K;
+            for (int sb = kk * SB; sb < bsz; sb += g.K * SB) {
+                const bool last_sb = sb + g.K * SB >= bsz;
+                const int nrow = bsz - sb < SB ? bsz - sb : SB;
+                const int jsb = (sb / SB) / g.K;
                 const int stb = jsb < 4 ? jsb * 16 : 80;
                 const int tid = vtid();
                 AGX_STAMP(stb + 0);
-                // ---- P0: contiguous gather of the sub-batch -------------------
+                // ---- P0: the sub-batch -> LDS (prefetched into registers during the
+                // previous sub-batch; fetched here only when the prefetch guessed
+                // another one).  Then the next sub-batch in this partner's sequence is
+                // prefetched: its loads fly under this sub-batch's compute.
                 // (padding columns rewritten too: the gradient image aliases them)
-                for (int i = tid; i < kSB * pl.ld_x0; i += kNT) {
-                    const int r = i / pl.ld_x0, dd = i % pl.ld_x0;
-                    sm[pl.l_x0 + i] = (r < nrow && dd < pl.D) ? eobs[(s0 + sb + r) * pl.D + dd] : 0.f;
-                }
-                if (tid < 4 * kSB) {
-                    const int k = tid / kSB, r = tid % kSB;
-                    rowf[k * kSB + r] = r < nrow ? erow[(size_t)k * S + s0 + sb + r] : 0.f;
-                } else if (tid < 5 * kSB) {
-                    const int r = tid - 4 * kSB;
-                    acts[r] = r < nrow ? eact[s0 + sb + r] : 0;
-                } else if (tid < 6 * kSB) {
-                    const int r = tid - 5 * kSB;
-                    legal[r] = (emask && r < nrow) ? emask[s0 + sb + r] : 0xffffffffu;
+                {
+                    auto commit = [&](const Pre &x) {
+#pragma unroll
+                        for (int k = 0; k < kPreObs; ++k)
+                            if (tid + k * kNT < SB * pl.ld_x0) sm[pl.l_x0 + tid + k * kNT] = x.ob[k];
+                        if (tid < 4 * kSB) rowf[tid] = __builtin_bit_cast(float, x.rv);
+                        else if (tid < 5 * kSB) acts[tid - 4 * kSB] = (int)x.rv;
+                        else if (tid < 6 * kSB) legal[tid - 5 * kSB] = x.rv;
+                    };
+                    if constexpr (kPreObs > 1) {  // 32-row sub-batches: registers too tight to carry
+                        commit(fetch(e, mb, sb));
+                    } else {
+                        if (pre.e != e || pre.mb != mb || pre.sb != sb) pre = fetch(e, mb, sb);
+                        commit(pre);
+                        int ne = e, nm = mb, ns = sb + g.K * SB;
+                        if (ns >= bsz) {
+                            ns = kk * SB;
+                            if (++nm >= nmb) {
+                                nm = 0;
+                                ++ne;
+                            }
+                        }
+                        pre = fetch(ne, nm, ns);
+                    }
                 }
                 __syncthreads();
                 AGX_STAMP(stb + 1);
@@ -791,7 +880,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         const int t = wave + kNW * j;
                         if (t < pl.nt[ga]) {
                             const int i0 = (t % pl.ncol[ga]) * 16;
-                            acc[pl.slot0[ga] + j] = mfma_tile<kSB>(
+                            acc[pl.slot0[ga] + j] = mfma_tile<SB>(
                                 acc[pl.slot0[ga] + j], [&](int m, int k) { return sm[pl.l_dlg + k * kMaxA + m]; },
                                 [&](int k, int n) {
                                     const int c = i0 + n;
@@ -804,7 +893,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         const int t = wave + kNW * j;
                         if (t < pl.nt[gc]) {
                             const int i0 = (t % pl.ncol[gc]) * 16;
-                            acc[pl.slot0[gc] + j] = mfma_tile<kSB>(
+                            acc[pl.slot0[gc] + j] = mfma_tile<SB>(
                                 acc[pl.slot0[gc] + j], [&](int m, int k) { return sm[pl.l_dvb + k * kMaxA + m]; },
                                 [&](int k, int n) {
                                     const int c = i0 + n;
@@ -816,9 +905,9 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         emit_tiles(IC(pl.ne + 1), slab_put);
                         emit_tiles(IC(pl.ne + 2), slab_put);
                     }
-                    constexpr int nt = (kSB / 16) * (pl.H / 16);
+                    constexpr int nt = (SB / 16) * (pl.H / 16);
                     for (int t = wave; t < nt; t += kNW) {
-                        const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
+                        const int m0 = (t % (SB / 16)) * 16, n0 = (t / (SB / 16)) * 16;
                         f4 c = f4{0.f, 0.f, 0.f, 0.f};
                         if (n0 < pl.ha) {
                             c = mfma_tile<16>(c, [&](int m, int k) { return sm[pl.l_dlg + (m0 + m) * kMaxA + k]; },
@@ -850,14 +939,17 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     constexpr int F0 = split < F ? split : F, F1 = F - F0;
                     AGX_IDS;
                     const int r = rrow;
+                    // rows beyond the sub-batch (SB = 16: lanes 32-63) hold stale LDS
+                    // data: they contribute exact zeros to the column reductions
+                    const bool rl = SB == kSB || r < SB;
                     float xh[NC], dxh[NC], dyp[NC];
                     float a1 = 0.f, a2 = 0.f, c1 = 0.f, c2 = 0.f;
-                    const float rs0 = sm[rb + 2 * r], rs1 = sm[rb + 2 * r + 1];
+                    const float rs0 = rl ? sm[rb + 2 * r] : 0.f, rs1 = rl ? sm[rb + 2 * r + 1] : 0.f;
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
                         const int j = sub + 16 * i;
-                        const float dy = sm[pl.l_s2 + r * pl.ld_s + j];
-                        xh[i] = sm[xb + r * ldx + j];
+                        const float dy = rl ? sm[pl.l_s2 + r * pl.ld_s + j] : 0.f;
+                        xh[i] = rl ? sm[xb + r * ldx + j] : 0.f;
                         const float gam = aff ? sm[gb + j] : 1.f;
                         const float y = aff ? xh[i] * gam + sm[bb + j] : xh[i];
                         dyp[i] = y > 0.f ? dy : 0.f;
@@ -874,21 +966,46 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     const float mc1 = F1 > 0 ? row_sum(c1) * (1.f / (float)(F1 > 0 ? F1 : 1)) : 0.f;
                     const float mc2 = F1 > 0 ? row_sum(c2) * (1.f / (float)(F1 > 0 ? F1 : 1)) : 0.f;
                     float *rd = sm + pl.l_red + red;
+                    // dZ row pass; the column sums (bias, gamma, beta gradients) of the
+                    // wave's rows are batched: all cross-row reductions, then all LDS
+                    // loads of the per-wave accumulators, then all stores (one LDS
+                    // round trip instead of a read-modify-write chain per column)
+                    constexpr int NV = aff ? 3 : 1;
+                    float cs[NV][NC];
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
                         const int j = sub + 16 * i;
                         const bool g0 = 16 * i < split;
                         const float dz = (g0 ? rs0 : rs1) * (dxh[i] - (g0 ? ma1 : mc1) - xh[i] * (g0 ? ma2 : mc2));
-                        sm[pl.l_s2 + r * pl.ld_s + j] = dz;
-                        const float sdz = rowgroup_sum(dz);
-                        if (lane < 16) rd[(0 * kNW + wave) * F + j] += sdz;
-                        if (aff) {
-                            const float sg = rowgroup_sum(dyp[i] * xh[i]);
-                            const float sbt = rowgroup_sum(dyp[i]);
-                            if (lane < 16) {
-                                rd[(1 * kNW + wave) * F + j] += sg;
-                                rd[(2 * kNW + wave) * F + j] += sbt;
-                            }
+                        if (rl) sm[pl.l_s2 + r * pl.ld_s + j] = dz;
+                        cs[0][i] = rl ? dz : 0.f;
+                        if constexpr (aff) {
+                            cs[1][i] = dyp[i] * xh[i];
+                            cs[2][i] = dyp[i];
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < NV; ++k)
+#pragma unroll
+                        for (int i = 0; i < NC; ++i)
+                            cs[k][i] += __builtin_bit_cast(
+                                float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, cs[k][i]), 0x401f));  // lane ^ 16
+                    if constexpr (SB > 16) {  // rows in lanes 32-63 too
+#pragma unroll
+                        for (int k = 0; k < NV; ++k)
+#pragma unroll
+                            for (int i = 0; i < NC; ++i)
+                                cs[k][i] += __builtin_bit_cast(
+                                    float, __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, __builtin_bit_cast(int, cs[k][i])));
+                    }
+                    if (lane < 16) {
+#pragma unroll
+                        for (int k = 0; k < NV; ++k) {
+                            float o[NC];
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) o[i] = rd[(k * kNW + wave) * F + sub + 16 * i];
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) rd[(k * kNW + wave) * F + sub + 16 * i] = o[i] + cs[k][i];
                         }
                     }
                 };
@@ -907,15 +1024,15 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         const int t = wave + kNW * j;
                         if (t < pl.nt[gh]) {
                             const int o0 = (t / pl.ncol[gh]) * 16, i0 = (t % pl.ncol[gh]) * 16;
-                            acc[pl.slot0[gh] + j] = mfma_tile<kSB>(
+                            acc[pl.slot0[gh] + j] = mfma_tile<SB>(
                                 acc[pl.slot0[gh] + j], [&](int m, int k) { return sm[pl.l_s2 + k * pl.ld_s + o0 + m]; },
                                 [&](int k, int n) { return relu(sm[pl.l_xe[Le] + k * pl.ld_xe[Le] + i0 + n]); });
                         }
                     }
                     if (direct && last_sb) emit_tiles(IC(gh), slab_put);
-                    constexpr int nt = (kSB / 16) * (pl.lat / 16);
+                    constexpr int nt = (SB / 16) * (pl.lat / 16);
                     for (int t = wave; t < nt; t += kNW) {
-                        const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
+                        const int m0 = (t % (SB / 16)) * 16, n0 = (t / (SB / 16)) * 16;
                         f4 c = f4{0.f, 0.f, 0.f, 0.f};
                         c = mfma_tile<pl.H>(c, [&](int m, int k) { return sm[pl.l_s2 + (m0 + m) * pl.ld_s + k]; },
                                             [&](int k, int n) { return sm[pl.l_hw + k * pl.l_hld + n0 + n]; });
@@ -933,10 +1050,12 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     AGX_IDS;
                     {  // dY (S1) -> S2: the row pass works in place on S2
                         const int r = rrow;
+                        if (SB == kSB || r < SB) {
 #pragma unroll
-                        for (int i = 0; i < fout / 16; ++i) {
-                            const int j = sub + 16 * i;
-                            sm[pl.l_s2 + r * pl.ld_s + j] = sm[pl.l_s1 + r * pl.ld_s + j];
+                            for (int i = 0; i < fout / 16; ++i) {
+                                const int j = sub + 16 * i;
+                                sm[pl.l_s2 + r * pl.ld_s + j] = sm[pl.l_s1 + r * pl.ld_s + j];
+                            }
                         }
                     }
                     ln_bwd(IC(fout), IC(fout), IC(pl.l_xe[L]), IC(pl.ld_xe[L]), IC(pl.l_re[L]), IC(pl.l_eg[L]),
@@ -956,7 +1075,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                             const bool cv = col < fin;
                             const float gam = (in_aff && cv) ? sm[gbase + col] : 1.f;
                             const float bet = (in_aff && cv) ? sm[bbase + col] : 0.f;
-                            acc[pl.slot0[L] + j] = mfma_tile<kSB>(
+                            acc[pl.slot0[L] + j] = mfma_tile<SB>(
                                 acc[pl.slot0[L] + j], [&](int m, int k) { return sm[pl.l_s2 + k * pl.ld_s + o0 + m]; },
                                 [&](int k, int n) {
                                     const float x = sm[xb + k * ldx + i0 + n];
@@ -967,9 +1086,9 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     }
                     if (direct && last_sb) emit_tiles(IC(L), slab_put);
                     if constexpr (L > 0) {
-                        constexpr int nt = (kSB / 16) * (fin / 16);
+                        constexpr int nt = (SB / 16) * (fin / 16);
                         for (int t = wave; t < nt; t += kNW) {
-                            const int m0 = (t % (kSB / 16)) * 16, n0 = (t / (kSB / 16)) * 16;
+                            const int m0 = (t % (SB / 16)) * 16, n0 = (t / (SB / 16)) * 16;
                             f4 c = f4{0.f, 0.f, 0.f, 0.f};
                             c = mfma_tile<fout>(c, [&](int m, int k) { return sm[pl.l_s2 + (m0 + m) * pl.ld_s + k]; },
                                                 [&](int k, int n) { return sm[pl.l_ew[L] + k * pl.l_eld[L] + n0 + n]; });
@@ -995,7 +1114,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 emit_tiles(IC(pl.ne), gput);
                 emit_tiles(IC(pl.ne + 1), gput);
                 emit_tiles(IC(pl.ne + 2), gput);
-            } else if (kk * kSB >= bsz) {  // no sub-batch this update: publish zeros
+            } else if (kk * SB >= bsz) {  // no sub-batch this update: publish zeros
                 emit_tiles(IC(0), slab_put);
                 emit_tiles(IC(1), slab_put);
                 if constexpr (pl.ne == 3) emit_tiles(IC(2), slab_put);
@@ -1048,50 +1167,42 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     slab_put(pl.param_end, lmb);
                     slab_put(pl.param_end + 1, klmb);
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) {
-                    __hip_atomic_fetch_add(g.cnt + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    AGX_STAMP(64 + 11);
-                    const unsigned target = (unsigned)(g.K * (upd + 1));
-                    unsigned spins = 0;
-                    int ok = 1;
-                    while (__hip_atomic_load(g.cnt + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                        __builtin_amdgcn_s_sleep(2);
-                        if (++spins > kSpinMax) {
-                            __hip_atomic_store(g.cnt + g.P, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            if (g.err) __hip_atomic_fetch_or(g.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            ok = 0;
-                            break;
-                        }
-                    }
-                    // no acquire: the slabs are read with sc1 loads below
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    stat[4 * kNW] = ok ? 1.f : 0.f;
-                    AGX_STAMP(64 + 12);
-                }
-                __syncthreads();
-                if (stat[4 * kNW] == 0.f) return;  // partner never arrived: timeout word set, whole block exits
-                // (loss words via vector atomics: a uniform plain load would take the
-                // scalar-cache path, which never sees the partners' stores)
-                // (one vector load: lane q reads partner q's loss word; summed in
-                // partner order)
+                if (!partner_sync(g.cnt + p, (unsigned)(g.K * (upd + 1)), 64 + 11, 64 + 12)) return;
+                // ---- reduce-scatter: partner kk sums float4 chunks [c0, c1) of the
+                // parameter image (+ the chunk holding the loss / approx_kl words)
+                // over the K slabs in partner order and publishes them to the agent's
+                // sum slab (every partner then reads ONE slab: K x (1/K) + 1 slab
+                // reads per workgroup instead of K)
                 {
-                    const int ln = vlane();
-                    const float w = ln < g.K ? __hip_atomic_load(base + (size_t)ln * pl.slab + pl.param_end,
-                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                             : 0.f;
-                    const float wk = ln < g.K ? __hip_atomic_load(base + (size_t)ln * pl.slab + pl.param_end + 1,
-                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                              : 0.f;
-                    float lt = readlane_f(w, 0), kt = readlane_f(wk, 0);
-                    for (int q = 1; q < g.K; ++q) {
-                        lt += readlane_f(w, q);
-                        kt += readlane_f(wk, q);
+                    constexpr int n4s = pl.param_end / 4 + 1;
+                    static_assert(pl.param_end % 4 == 0 && pl.slab >= 4 * n4s, "loss words chunk");
+                    const int c0 = (int)((long long)n4s * kk / g.K), c1 = (int)((long long)n4s * (kk + 1) / g.K);
+                    const int tid = vtid();
+                    // one buffer descriptor over the K consecutive slabs; 4 loads in flight
+                    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                        base, 0, __builtin_amdgcn_readfirstlane(g.K * pl.slab * 4), 0x00020000);
+                    for (int c = c0 + tid; c < c1; c += kNT) {
+                        f4 x[kMaxK];  // all K loads in flight at once
+#pragma unroll
+                        for (int q = 0; q < kMaxK; ++q)
+                            x[q] = q < g.K ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                       rs, (q * pl.slab + 4 * c) * 4, 0, 16))
+                                           : f4{0.f, 0.f, 0.f, 0.f};
+                        f4 t = x[0];  // partner order
+#pragma unroll
+                        for (int q = 1; q < kMaxK; ++q)
+                            if (q < g.K) t += x[q];
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 16);
                     }
-                    lmb = lt;
-                    klmb = kt;
                 }
+                AGX_STAMP(64 + 13);
+                if (!partner_sync(g.cnt + g.P + 1 + p, (unsigned)(g.K * (upd + 1)), 64 + 8, 64 + 15)) return;
+                // the minibatch loss and approx_kl: partner-order sums of the K words
+                // (uniform: the early-stop branch depends on it)
+                lmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                                                    __builtin_amdgcn_raw_buffer_load_b32(sum_rsrc, pl.param_end * 4, 0, 16)));
+                klmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b32(
+                                                     sum_rsrc, (pl.param_end + 1) * 4, 0, 16)));
                 AGX_STAMP(64 + 13);
             }
 
@@ -1112,40 +1223,16 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     for (int c = 0; c < 4; ++c) gr[4 * j + c] = x[c];
                 };
                 if (direct) {
-                    // fixed-order sum over the K partner slabs, straight from L2 into the
-                    // owned chunks: every workgroup of the agent adds the same words in the
-                    // same order -> bit-identical totals, hence bit-identical parameters
-                    // partners 0 and 1 in flight together, then 2, then 3 (K <= 4)
-                    // sc1 buffer loads (L1 bypassed): with every slab store sc1 and drained
-                    // before the ticket, no acquire fence is needed (MI355X_MICROARCH.md,
-                    // inter-workgroup visibility, valid forms: sc1 stores + sc1 loads)
-                    auto ld = [&](int q, int j) {
-                        const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-                            base + (size_t)q * pl.slab, 0, __builtin_amdgcn_readfirstlane(pl.slab * 4), 0x00020000);
-                        return chunk_in(j) ? __builtin_bit_cast(
-                                                 f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + kNT * j) * 16, 0, 16))
-                                           : f4{0.f, 0.f, 0.f, 0.f};
-                    };
-                    {
-                        f4 b[kUsed4];
+                    // the summed gradient of the reduce-scatter, straight from L2 into the
+                    // owned chunks: every workgroup of the agent reads the same words ->
+                    // bit-identical parameters.  sc1 buffer loads (L1 bypassed): with every
+                    // store sc1 and drained before the ticket, no acquire fence is needed
+                    // (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores + sc1 loads)
 #pragma unroll
-                        for (int j = 0; j < kUsed4; ++j) {
-                            put(j, ld(0, j));
-                            b[j] = ld(1, j);  // K >= 2 here
-                        }
-#pragma unroll
-                        for (int j = 0; j < kUsed4; ++j)
-#pragma unroll
-                            for (int c = 0; c < 4; ++c) gr[4 * j + c] += b[j][c];
-                    }
-                    for (int q = 2; q < g.K; ++q) {
-#pragma unroll
-                        for (int j = 0; j < kUsed4; ++j) {
-                            const f4 x = ld(q, j);
-#pragma unroll
-                            for (int c = 0; c < 4; ++c) gr[4 * j + c] += x[c];
-                        }
-                    }
+                    for (int j = 0; j < kUsed4; ++j)
+                        put(j, chunk_in(j) ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                       sum_rsrc, (tid + kNT * j) * 16, 0, 16))
+                                           : f4{0.f, 0.f, 0.f, 0.f});
                 } else {
                     const f4 *G4 = reinterpret_cast<const f4 *>(G);
 #pragma unroll
@@ -1571,7 +1658,7 @@ static bool dims_match(const agx_ppo_net *net, const NetDims &d) {
 
 struct Launcher {
     const LearnPlan *plan;
-    void (*learn)(const LearnArgs &, int nblocks, size_t lds, hipStream_t);
+    void (*learn)(const LearnArgs &, int nblocks, size_t lds, hipStream_t, int sb);
     void (*act)(const ActArgs &, dim3 grid, size_t lds, hipStream_t);
     void (*persist)(const ActArgs *, int, agx_rollout_ctl *, unsigned long long, unsigned, long long *, dim3 grid,
                     size_t lds, hipStream_t);
@@ -1579,13 +1666,17 @@ struct Launcher {
 };
 
 template <class C>
-static void launch_learn(const LearnArgs &a, int nblocks, size_t lds, hipStream_t s) {
+static void launch_learn(const LearnArgs &a, int nblocks, size_t lds, hipStream_t s, int sb) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
         attr = true;
     }
-    ppo_learn_kernel<C><<<(unsigned)nblocks, kNT, lds, s>>>(a);
+    if (sb == 16) ppo_learn_kernel<C, 16><<<(unsigned)nblocks, kNT, lds, s>>>(a);
+    else ppo_learn_kernel<C, 32><<<(unsigned)nblocks, kNT, lds, s>>>(a);
 }
 template <class C>
 static void launch_act(const ActArgs &a, dim3 grid, size_t lds, hipStream_t s) {
@@ -1668,30 +1759,52 @@ static int cu_count() {
     }
     return n;
 }
+// Partner workgroups per agent: all partners must be co-resident (1 block per
+// CU), so K <= CUs / P; AGX_LEARN_SPLIT lowers the cap (tests, diagnostics).
 static int max_partners(int64_t P) {
-    int k = 4;
+    int k = kMaxK;
     if (const char *e = getenv("AGX_LEARN_SPLIT")) k = atoi(e);
     if (k < 1) k = 1;
     if (k > kMaxK) k = kMaxK;
-    const int64_t fit = cu_count() / (P > 0 ? P : 1);  // all partners co-resident, 1 block per CU
+    const int64_t fit = cu_count() / (P > 0 ? P : 1);
     if (fit < k) k = fit < 1 ? 1 : (int)fit;
     return k;
 }
+// Sub-batch rows and partner count of one learn: 16-row sub-batches over up to
+// 8 partners when the population leaves that many CUs per agent (shorter MFMA
+// chains per CU), else 32-row sub-batches over up to 4.  AGX_LEARN_SB = 16 / 32
+// forces the row count.
+static void pick_split(int64_t P, int64_t batch, int &K, int &SB) {
+    const int kmax = max_partners(P);
+    int sb = kmax >= 8 ? 16 : 32;
+    if (const char *e = getenv("AGX_LEARN_SB")) {
+        const int v = atoi(e);
+        if (v == 16 || v == 32) sb = v;
+    }
+    const int64_t nsb = (batch + sb - 1) / sb;
+    K = sb == 32 && kmax > 4 ? 4 : kmax;
+    if (K > nsb) K = (int)nsb;
+    if (K < 1) K = 1;
+    SB = sb;
+}
 struct LearnWs {
-    size_t cnt, gobs, gact, gmask, grow, slabs, total;
+    size_t cnt, gobs, gact, gmask, grow, slabs, sums, total;
 };
 static LearnWs learn_ws(const LearnPlan &pl, int64_t P, int64_t S, int64_t epochs) {
     LearnWs w;
     const size_t per = (size_t)epochs * P * S;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     w.cnt = 0;
-    w.gobs = up(((size_t)P + 1) * 4);
+    w.gobs = up(((size_t)2 * P + 1) * 4);  // arrival counters, timeout word, second-barrier counters
     w.gact = w.gobs + up(per * pl.D * 4);
     w.gmask = w.gact + up(per * 4);
     w.grow = w.gmask + up(per * 4);
     w.slabs = w.grow + up(per * 4 * 4);
-    const int K = max_partners(P);
-    w.total = w.slabs + (K > 1 ? (size_t)P * 2 * K * pl.slab * 4 : 0);
+    // partners of any split pick_split can choose (AGX_LEARN_SPLIT only lowers it)
+    const int64_t fit = cu_count() / (P > 0 ? P : 1);
+    const int K = fit < 1 ? 1 : (fit > kMaxK ? kMaxK : (int)fit);
+    w.sums = w.slabs + (K > 1 ? up((size_t)P * 2 * K * pl.slab * 4) : 0);
+    w.total = w.sums + (K > 1 ? (size_t)P * 2 * pl.slab * 4 : 0);
     return w;
 }
 
@@ -1755,9 +1868,8 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *x
     int *gact = reinterpret_cast<int *>(ws + w.gact);
     unsigned *gmask = x->action_masks ? reinterpret_cast<unsigned *>(ws + w.gmask) : nullptr;
     float *grow = reinterpret_cast<float *>(ws + w.grow);
-    const int64_t nsb = (batch + kSB - 1) / kSB;
-    int K = max_partners(P);
-    if (K > nsb) K = (int)nsb;
+    int K = 1, SB = kSB;
+    pick_split(P, batch, K, SB);
     AGX_REQUIRE(P * K <= 65535, "agx_ppo_learn: too many workgroups");
     // counters + timeout word: one 16-byte-multiple block at the workspace start, zeroed by the gather
     dim3 ggrid((unsigned)ceil_div(S, 256), (unsigned)(epochs * P));
@@ -1800,9 +1912,10 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *x
     a.stamps = g_stamps_ptr();
     a.K = K;
     a.slabs = reinterpret_cast<float *>(ws + w.slabs);
+    a.sums = reinterpret_cast<float *>(ws + w.sums);
     a.cnt = reinterpret_cast<unsigned *>(ws);
     a.debug_stall = K > 1 ? g_debug_stall() : 0;
-    L.learn(a, (int)(P * K), (size_t)pl.lds_floats * sizeof(float), s);
+    L.learn(a, (int)(P * K), (size_t)pl.lds_floats * sizeof(float), s, SB);
     return check_launch("agx_ppo_learn");
 }
 

@@ -2,7 +2,9 @@
 
 Slots (learner.hip AGX_STAMP): sub-batch k of agent 0's first minibatch at
 k*16 + {0 start, 1 gathered, 2 forward, 3 loss, 4 out-layer bwd, 5 head LN bwd,
-6 head dW/dX, 7 encoder bwd}; 64+9 gradients dumped, 64+10 Adam done."""
+6 head dW/dX, 7 encoder bwd}; 64+9 gradients dumped, 64+10 Adam done;
+partners: 64+11/12 first barrier ticket/passed, 64+13 reduce-scatter done,
+64+8/15 second barrier ticket/passed, 64+14 norm done."""
 import os
 import sys
 import time
@@ -43,6 +45,11 @@ for sb in range(4):
     seg = [row[i + 1] - row[i] for i in range(7)]
     print(f"sb{sb}: " + "  ".join(f"{n}={c}" for n, c in zip(names, seg)) + f"  total={row[7] - row[0]}")
 last = max(v for v in st[:64] if v)
-print("dump", st[64 + 9] - last, "| exchange: publish", st[64 + 11] - st[64 + 9], "wait+acquire",
-      st[64 + 12] - st[64 + 11], "sum", st[64 + 13] - st[64 + 12], "| norm", st[64 + 14] - st[64 + 13], "adam", st[64 + 10] - st[64 + 14],
-      "| minibatch total cycles", st[64 + 10] - st[0])
+if st[64 + 15]:  # partners: reduce-scatter exchange (two barriers)
+    print("dump", st[64 + 9] - last, "| publish", st[64 + 11] - st[64 + 9], "wait", st[64 + 12] - st[64 + 11],
+          "loss words + reduce-scatter", st[64 + 13] - st[64 + 12], "| barrier 2: drain", st[64 + 8] - st[64 + 13],
+          "wait", st[64 + 15] - st[64 + 8], "| sum read + norm", st[64 + 14] - st[64 + 15],
+          "adam", st[64 + 10] - st[64 + 14], "| minibatch total cycles", st[64 + 10] - st[0])
+else:
+    print("dump", st[64 + 9] - last, "| norm", st[64 + 14] - st[64 + 9], "adam", st[64 + 10] - st[64 + 14],
+          "| minibatch total cycles", st[64 + 10] - st[0])
