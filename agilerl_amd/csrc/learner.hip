@@ -206,7 +206,7 @@ constexpr LearnPlan make_plan(NetDims d) {
     pl.l_stat = off; off += 5 * kNW;
     pl.lds_floats = off;
     if (pl.lds_floats * 4 > 160 * 1024) return pl;
-    pl.slab = rup(pl.param_end + 2, 64);  // + loss and approx_kl words
+    pl.slab = rup(pl.param_end + 4, 64);  // + the loss / approx_kl chunk
     // ---- dW tile groups
     int slot = 0;
     for (int g = 0; g < pl.ne + 3; ++g) {
@@ -428,7 +428,11 @@ struct Fwd {
 
     // LayerNorm(+affine)+ReLU of Z (S2, width F; LN groups [0,split), [split,F))
     // -> xhat to xb (stride ldx), y to S1, rstd to rb[2r + group]
-    template <int F, int split, int xb, int ldx, int rb, int gb, int bb>
+    // OUT (the merged head layer): the output layers ride along as row dot
+    // products — logits[a] = y_actor . W_out[a] + b[a] and value = y_critic .
+    // w_v + b_v, each a per-lane partial over the lane's 16-strided columns
+    // then a DPP row sum — and land in lg / val: no separate output phase.
+    template <int F, int split, int xb, int ldx, int rb, int gb, int bb, bool OUT = false>
     __device__ __forceinline__ void ln_rows() {
         constexpr int NC = F / 16;
         constexpr int F0 = split < F ? split : F, F1 = F - F0;
@@ -457,12 +461,36 @@ struct Fwd {
             sm[rb + 2 * r] = r0;
             sm[rb + 2 * r + 1] = r1;
         }
+        constexpr int NA = OUT ? pl.A : 1;
+        float pa[NA], pv = 0.f;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) pa[a] = 0.f;
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
             const int j = sub + 16 * i;
             const float xh = 16 * i < split ? (z[i] - m0) * r0 : (z[i] - m1) * r1;
             sm[xb + r * ldx + j] = xh;
-            sm[pl.l_s1 + r * pl.ld_s + j] = gb >= 0 ? relu(xh * sm[gb + j] + sm[bb + j]) : relu(xh);
+            const float y = gb >= 0 ? relu(xh * sm[gb + j] + sm[bb + j]) : relu(xh);
+            sm[pl.l_s1 + r * pl.ld_s + j] = y;
+            if constexpr (OUT) {
+                if (16 * i < split) {
+#pragma unroll
+                    for (int a = 0; a < NA; ++a) pa[a] += y * sm[pl.l_aow + a * pl.l_aold + j];
+                } else {
+                    pv += y * sm[pl.l_cow + j - split];
+                }
+            }
+        }
+        if constexpr (OUT) {
+            float mine = 0.f;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                const float t = row_sum(pa[a]);
+                mine = sub == a ? t : mine;
+            }
+            pv = row_sum(pv);
+            if (sub < NA) sm[pl.l_lg + r * kMaxA + sub] = mine + sm[pl.l_aob + sub];
+            if (sub == 0) sm[pl.l_val + r] = pv + sm[pl.l_cob];
         }
     }
 
@@ -498,27 +526,7 @@ struct Fwd {
         enc_layer<0>();
         gemm_fwd<pl.l_s1, pl.ld_s, pl.lat, pl.l_hw, pl.l_hld, pl.l_hb, pl.H>();
         __syncthreads();
-        ln_rows<pl.H, pl.ha, pl.l_xh, pl.ld_xh, pl.l_rh, pl.l_hg, pl.l_hbe>();
-        __syncthreads();
-        // output layers: SB/16 row tiles x {actor logits (waves 0-1), critic value (waves 2-3)}
-        AGX_IDS;
-        if (wave < SB / 16) {
-            const int m0 = wave * 16;
-            f4 c = f4{0.f, 0.f, 0.f, 0.f};
-            c = mfma_tile<pl.ha>(c, [&](int m, int k) { return sm[pl.l_s1 + (m0 + m) * pl.ld_s + k]; },
-                                 [&](int k, int n) { return n < pl.A ? sm[pl.l_aow + n * pl.l_aold + k] : 0.f; });
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (lr16 < pl.A) sm[pl.l_lg + (m0 + lq * 4 + i) * kMaxA + lr16] = c[i] + sm[pl.l_aob + lr16];
-        } else if (wave >= 2 && wave < 2 + SB / 16) {
-            const int m0 = (wave - 2) * 16;
-            f4 c = f4{0.f, 0.f, 0.f, 0.f};
-            c = mfma_tile<pl.hc>(c, [&](int m, int k) { return sm[pl.l_s1 + (m0 + m) * pl.ld_s + pl.ha + k]; },
-                                 [&](int k, int n) { return n == 0 ? sm[pl.l_cow + k] : 0.f; });
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (lr16 == 0) sm[pl.l_val + m0 + lq * 4 + i] = c[i] + sm[pl.l_cob];
-        }
+        ln_rows<pl.H, pl.ha, pl.l_xh, pl.ld_xh, pl.l_rh, pl.l_hg, pl.l_hbe, true>();  // + output layers
         __syncthreads();
     }
 };
@@ -564,9 +572,11 @@ struct LearnArgs {
     int K;                 // workgroups per agent (data-parallel over sub-batches)
     float *slabs;          // [P][2][K][slab] gradient hand-off (double-buffered)
     float *sums;           // [P][2][slab] reduce-scattered gradient sums (double-buffered)
-    unsigned *cnt;         // [P] arrival counters, [P] timeout word, [P+1+p] second-barrier
-                           // counters (zeroed per call)
+    unsigned *cnt;         // [P] arrival counters, [P] timeout word, [P+1+p] second-barrier,
+                           // [2P+1+p] setup-barrier counters, [3P+1 + p*kMaxK + kk] XCC ids
+                           // (zeroed per call)
     int debug_stall;       // test hook: partner 1 of agent 0 never arrives
+    int write_through;     // 1: always sc1 stores (AGX_LEARN_WRITETHROUGH=1; tests the cross-XCD form)
 };
 
 #define IC(x) std::integral_constant<int, (x)>()
@@ -679,6 +689,44 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     Pre pre{};
     if constexpr (kPreObs == 1) pre = fetch(0, 0, kk * SB);
 
+    // Partners that share one XCD share its L2: plain stores (the line stays in
+    // that L2) + sc1 loads (L1 bypassed) hand data over without the write-through
+    // to memory that sc1 stores cost.  Placement is not guaranteed, so it is
+    // checked here: each workgroup publishes HW_REG_XCC_ID and, after one setup
+    // barrier, uses the L2-local form only if all K ids agree.
+    bool local = false;
+    if (g.K > 1) {
+        unsigned *xc = g.cnt + 3 * g.P + 1 + (size_t)p * kMaxK;
+        if (tid == 0) {
+            int x;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+            __hip_atomic_store(xc + kk, (unsigned)(x & 15) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            unsigned *ctr = g.cnt + 2 * g.P + 1 + p;
+            __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned spins = 0;
+            int ok = 1;
+            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)g.K) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kSpinMax) {
+                    __hip_atomic_store(g.cnt + g.P, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (g.err) __hip_atomic_fetch_or(g.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = 0;
+                    break;
+                }
+            }
+            stat[4 * kNW] = ok ? 1.f : 0.f;
+        }
+        __syncthreads();
+        if (stat[4 * kNW] == 0.f) return;
+        const int ln = vlane();
+        const unsigned v = ln < g.K ? __hip_atomic_load(xc + ln, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const unsigned v0 = __builtin_amdgcn_readlane(v, 0);
+        bool same = v0 != 0u;
+        for (int q = 1; q < g.K; ++q) same = same && __builtin_amdgcn_readlane(v, q) == v0;
+        local = same && !g.write_through;
+    }
+
     for (int e = 0; e < Ep; ++e) {
         for (int mb = 0; mb < nmb; ++mb) {
             const long long s0 = (long long)mb * Bp;
@@ -730,8 +778,10 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 }
             };
             // write-through (sc1) store of one gradient word into this workgroup's slab
+            // (plain store when the partners share this XCD's L2, else write-through)
             auto slab_put = [&](int l, float x) {
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), slab_rsrc, l * 4, 0, 16);
+                if (local) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), slab_rsrc, l * 4, 0, 0);
+                else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), slab_rsrc, l * 4, 0, 16);
             };
             // this agent's summed-gradient slab (written by the reduce-scatter)
             const auto sum_rsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -871,70 +921,19 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 __syncthreads();
                 AGX_STAMP(stb + 3);
 
-                // ---- P5: output-layer dW (bias = ones column); dY_h = dOut . W_out -> S2
-                {
-                    AGX_IDS;
-                    constexpr int ga = pl.ne + 1, gc = pl.ne + 2;
-#pragma unroll
-                    for (int j = 0; j < pl.nslot[ga]; ++j) {
-                        const int t = wave + kNW * j;
-                        if (t < pl.nt[ga]) {
-                            const int i0 = (t % pl.ncol[ga]) * 16;
-                            acc[pl.slot0[ga] + j] = mfma_tile<SB>(
-                                acc[pl.slot0[ga] + j], [&](int m, int k) { return sm[pl.l_dlg + k * kMaxA + m]; },
-                                [&](int k, int n) {
-                                    const int c = i0 + n;
-                                    return c < pl.ha ? sm[pl.l_s1 + k * pl.ld_s + c] : (c == pl.ha ? 1.f : 0.f);
-                                });
-                        }
-                    }
-#pragma unroll
-                    for (int j = 0; j < pl.nslot[gc]; ++j) {
-                        const int t = wave + kNW * j;
-                        if (t < pl.nt[gc]) {
-                            const int i0 = (t % pl.ncol[gc]) * 16;
-                            acc[pl.slot0[gc] + j] = mfma_tile<SB>(
-                                acc[pl.slot0[gc] + j], [&](int m, int k) { return sm[pl.l_dvb + k * kMaxA + m]; },
-                                [&](int k, int n) {
-                                    const int c = i0 + n;
-                                    return c < pl.hc ? sm[pl.l_s1 + k * pl.ld_s + pl.ha + c] : (c == pl.hc ? 1.f : 0.f);
-                                });
-                        }
-                    }
-                    if (direct && last_sb) {
-                        emit_tiles(IC(pl.ne + 1), slab_put);
-                        emit_tiles(IC(pl.ne + 2), slab_put);
-                    }
-                    constexpr int nt = (SB / 16) * (pl.H / 16);
-                    for (int t = wave; t < nt; t += kNW) {
-                        const int m0 = (t % (SB / 16)) * 16, n0 = (t / (SB / 16)) * 16;
-                        f4 c = f4{0.f, 0.f, 0.f, 0.f};
-                        if (n0 < pl.ha) {
-                            c = mfma_tile<16>(c, [&](int m, int k) { return sm[pl.l_dlg + (m0 + m) * kMaxA + k]; },
-                                              [&](int k, int n) {
-                                                  return k < pl.A ? sm[pl.l_aow + k * pl.l_aold + n0 + n] : 0.f;
-                                              });
-                        } else {
-                            c = mfma_tile<16>(c, [&](int m, int k) { return sm[pl.l_dvb + (m0 + m) * kMaxA + k]; },
-                                              [&](int k, int n) {
-                                                  return k == 0 ? sm[pl.l_cow + n0 - pl.ha + n] : 0.f;
-                                              });
-                        }
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) sm[pl.l_s2 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i];
-                    }
-                }
-                __syncthreads();
-                AGX_STAMP(stb + 4);
+                AGX_STAMP(stb + 4);  // (output-layer backward: folded into P6)
 
                 // backward row pass through LN(+affine)+ReLU: S2 (dY) -> S2 (dZ)
+                // HO (the merged head layer): dY comes straight from the output
+                // layers' d(logits) / d(value) rows, dY[j] = sum_a dlg[a] W_out[a][j]
+                // (actor columns) or dv w_v[j] (critic columns), instead of S2
                 auto ln_bwd = [&](auto Fc, auto splitc, auto xbc, auto ldxc, auto rbc, auto gbc, auto bbc, auto redc,
-                                  auto affc) {
+                                  auto affc, auto hoc) {
                     constexpr int F = decltype(Fc)::value, split = decltype(splitc)::value;
                     constexpr int xb = decltype(xbc)::value, ldx = decltype(ldxc)::value;
                     constexpr int rb = decltype(rbc)::value, gb = decltype(gbc)::value, bb = decltype(bbc)::value;
                     constexpr int red = decltype(redc)::value;
-                    constexpr bool aff = decltype(affc)::value;
+                    constexpr bool aff = decltype(affc)::value, HO = decltype(hoc)::value;
                     constexpr int NC = F / 16;
                     constexpr int F0 = split < F ? split : F, F1 = F - F0;
                     AGX_IDS;
@@ -945,10 +944,28 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     float xh[NC], dxh[NC], dyp[NC];
                     float a1 = 0.f, a2 = 0.f, c1 = 0.f, c2 = 0.f;
                     const float rs0 = rl ? sm[rb + 2 * r] : 0.f, rs1 = rl ? sm[rb + 2 * r + 1] : 0.f;
+                    constexpr int NA = HO ? pl.A : 1;
+                    float dl[NA], dvr = 0.f;
+                    if constexpr (HO) {
+#pragma unroll
+                        for (int a = 0; a < NA; ++a) dl[a] = rl ? sm[pl.l_dlg + r * kMaxA + a] : 0.f;
+                        dvr = rl ? sm[pl.l_dvb + r * kMaxA] : 0.f;
+                    }
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
                         const int j = sub + 16 * i;
-                        const float dy = rl ? sm[pl.l_s2 + r * pl.ld_s + j] : 0.f;
+                        float dy;
+                        if constexpr (HO) {
+                            if (16 * i < split) {
+                                dy = 0.f;
+#pragma unroll
+                                for (int a = 0; a < NA; ++a) dy += dl[a] * sm[pl.l_aow + a * pl.l_aold + j];
+                            } else {
+                                dy = dvr * sm[pl.l_cow + j - split];
+                            }
+                        } else {
+                            dy = rl ? sm[pl.l_s2 + r * pl.ld_s + j] : 0.f;
+                        }
                         xh[i] = rl ? sm[xb + r * ldx + j] : 0.f;
                         const float gam = aff ? sm[gb + j] : 1.f;
                         const float y = aff ? xh[i] * gam + sm[bb + j] : xh[i];
@@ -1010,8 +1027,44 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     }
                 };
                 // ---- P6: head LN backward (dY_h in S2 -> dZ_h in S2) ----------
+                // (+ the output layers' dW tiles, bias = ones column: they read
+                // d(logits) / d(value) and y_h, nothing this row pass writes)
                 ln_bwd(IC(pl.H), IC(pl.ha), IC(pl.l_xh), IC(pl.ld_xh), IC(pl.l_rh), IC(pl.l_hg), IC(pl.l_hbe),
-                       IC(pl.red_h), BC(true));
+                       IC(pl.red_h), BC(true), BC(true));
+                {
+                    AGX_IDS;
+                    constexpr int ga = pl.ne + 1, gc = pl.ne + 2;
+#pragma unroll
+                    for (int j = 0; j < pl.nslot[ga]; ++j) {
+                        const int t = wave + kNW * j;
+                        if (t < pl.nt[ga]) {
+                            const int i0 = (t % pl.ncol[ga]) * 16;
+                            acc[pl.slot0[ga] + j] = mfma_tile<SB>(
+                                acc[pl.slot0[ga] + j], [&](int m, int k) { return sm[pl.l_dlg + k * kMaxA + m]; },
+                                [&](int k, int n) {
+                                    const int c = i0 + n;
+                                    return c < pl.ha ? sm[pl.l_s1 + k * pl.ld_s + c] : (c == pl.ha ? 1.f : 0.f);
+                                });
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < pl.nslot[gc]; ++j) {
+                        const int t = wave + kNW * j;
+                        if (t < pl.nt[gc]) {
+                            const int i0 = (t % pl.ncol[gc]) * 16;
+                            acc[pl.slot0[gc] + j] = mfma_tile<SB>(
+                                acc[pl.slot0[gc] + j], [&](int m, int k) { return sm[pl.l_dvb + k * kMaxA + m]; },
+                                [&](int k, int n) {
+                                    const int c = i0 + n;
+                                    return c < pl.hc ? sm[pl.l_s1 + k * pl.ld_s + pl.ha + c] : (c == pl.hc ? 1.f : 0.f);
+                                });
+                        }
+                    }
+                    if (direct && last_sb) {
+                        emit_tiles(IC(pl.ne + 1), slab_put);
+                        emit_tiles(IC(pl.ne + 2), slab_put);
+                    }
+                }
                 __syncthreads();
                 AGX_STAMP(stb + 5);
 
@@ -1059,7 +1112,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         }
                     }
                     ln_bwd(IC(fout), IC(fout), IC(pl.l_xe[L]), IC(pl.ld_xe[L]), IC(pl.l_re[L]), IC(pl.l_eg[L]),
-                           IC(pl.l_ebe[L]), IC(pl.red_e[L]), BC(pl.eaff[L] != 0));
+                           IC(pl.l_ebe[L]), IC(pl.red_e[L]), BC(pl.eaff[L] != 0), BC(false));
                     __syncthreads();
                     constexpr bool in_aff = L > 0 && pl.eaff[L > 0 ? L - 1 : 0];
                     constexpr int xb = L == 0 ? pl.l_x0 : pl.l_xe[L > 0 ? L - 1 : 0];
@@ -1157,12 +1210,9 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             }
             if (g.K > 1) {
                 // ---- P9b: exchange partial gradients with the agent's partners --------
-                // (MI355X_MICROARCH visibility rules: sc1 stores -> vmcnt drain ->
-                // barrier -> relaxed agent ticket; relaxed poll -> barrier -> sc1 loads)
                 // every gradient word went out as a write-through (sc1) store from the
-                // backward pass / vdump; the loss word follows.  Drained by every storing
-                // wave before the barrier, so no release fence (cdna_hip_programming.md
-                // §6 G16 R1)
+                // backward pass / vdump; the loss words follow.  Drained by every storing
+                // wave before the barrier (partner_sync), so no release fence
                 if (tid == 0) {
                     slab_put(pl.param_end, lmb);
                     slab_put(pl.param_end + 1, klmb);
@@ -1178,7 +1228,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     static_assert(pl.param_end % 4 == 0 && pl.slab >= 4 * n4s, "loss words chunk");
                     const int c0 = (int)((long long)n4s * kk / g.K), c1 = (int)((long long)n4s * (kk + 1) / g.K);
                     const int tid = vtid();
-                    // one buffer descriptor over the K consecutive slabs; 4 loads in flight
+                    // one buffer descriptor over the K consecutive slabs
                     const auto rs = __builtin_amdgcn_make_buffer_rsrc(
                         base, 0, __builtin_amdgcn_readfirstlane(g.K * pl.slab * 4), 0x00020000);
                     for (int c = c0 + tid; c < c1; c += kNT) {
@@ -1192,7 +1242,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
 #pragma unroll
                         for (int q = 1; q < kMaxK; ++q)
                             if (q < g.K) t += x[q];
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 16);
+                        if (local) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 0);
+                        else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 16);
                     }
                 }
                 AGX_STAMP(64 + 13);
@@ -1203,7 +1254,6 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                                     __builtin_amdgcn_raw_buffer_load_b32(sum_rsrc, pl.param_end * 4, 0, 16)));
                 klmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b32(
                                                      sum_rsrc, (pl.param_end + 1) * 4, 0, 16)));
-                AGX_STAMP(64 + 13);
             }
 
             // ---- P10: two-group norm, Adam from registers -------------------------
@@ -1328,12 +1378,12 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
         if (g.target_kl > 0.0 && kl_total / (double)n_done > g.target_kl) break;
     }  // epochs
 
-    // ---- write parameters and moments back (partners hold identical copies) ------
-    if (kk != 0) return;
+    // ---- write parameters and moments back (partners hold identical copies; each
+    // writes the chunks j % K == kk) ------------------------------------------------
 #pragma unroll
     for (int i = 0; i < kMaxPT; ++i) {
         const int l = slot_l(tid, i);
-        if ((vbits >> i) & 1u) {
+        if (((vbits >> i) & 1u) && (g.K == 1 || (i >> 2) % g.K == kk)) {
             int grp;
             const int f = lds_to_flat<C>(l, grp);
             gp[f] = sm[l];
@@ -1341,7 +1391,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             gv[f] = av[i];
         }
     }
-    if (tid == 0) {
+    if (tid == 0 && kk == 0) {
         if (g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)Ep);
         if (g.kl_out) g.kl_out[p] = n_done ? (float)(kl_total / (double)n_done) : 0.f;
         if (g.epochs_out) g.epochs_out[p] = epochs_done;
@@ -1795,7 +1845,7 @@ static LearnWs learn_ws(const LearnPlan &pl, int64_t P, int64_t S, int64_t epoch
     const size_t per = (size_t)epochs * P * S;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     w.cnt = 0;
-    w.gobs = up(((size_t)2 * P + 1) * 4);  // arrival counters, timeout word, second-barrier counters
+    w.gobs = up(((size_t)(3 + kMaxK) * P + 1) * 4);  // barrier counters, timeout word, XCC ids
     w.gact = w.gobs + up(per * pl.D * 4);
     w.gmask = w.gact + up(per * 4);
     w.grow = w.gmask + up(per * 4);
@@ -1915,6 +1965,10 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *x
     a.sums = reinterpret_cast<float *>(ws + w.sums);
     a.cnt = reinterpret_cast<unsigned *>(ws);
     a.debug_stall = K > 1 ? g_debug_stall() : 0;
+    {
+        const char *wt = getenv("AGX_LEARN_WRITETHROUGH");
+        a.write_through = wt && atoi(wt) != 0;
+    }
     L.learn(a, (int)(P * K), (size_t)pl.lds_floats * sizeof(float), s, SB);
     return check_launch("agx_ppo_learn");
 }

@@ -233,7 +233,7 @@ def ctypes_byref(x):
     return ctypes.byref(x)
 
 
-@pytest.mark.parametrize("split", ["1", "2", "4", "8", "4x16", "1x16"])
+@pytest.mark.parametrize("split", ["1", "2", "4", "8", "8wt", "4x16", "1x16"])
 def test_fused_learner_partner_split_consistent(split, monkeypatch):
     """The learner spreads an agent's sub-batches (16 or 32 rows) over K
     partner workgroups that reduce-scatter partial gradients through HBM; K
@@ -245,6 +245,9 @@ def test_fused_learner_partner_split_consistent(split, monkeypatch):
     bound that drift against fp64); the bulk and the loss still agree."""
     from agilerl_amd.population.learner import fused_learn
 
+    if split.endswith("wt"):  # partners exchange through write-through stores (any XCD placement)
+        split = split[:-2]
+        monkeypatch.setenv("AGX_LEARN_WRITETHROUGH", "1")
     k, _, sb = split.partition("x")
     monkeypatch.setenv("AGX_LEARN_SPLIT", k)
     if sb:

@@ -47,7 +47,7 @@ for sb in range(4):
 last = max(v for v in st[:64] if v)
 if st[64 + 15]:  # partners: reduce-scatter exchange (two barriers)
     print("dump", st[64 + 9] - last, "| publish", st[64 + 11] - st[64 + 9], "wait", st[64 + 12] - st[64 + 11],
-          "loss words + reduce-scatter", st[64 + 13] - st[64 + 12], "| barrier 2: drain", st[64 + 8] - st[64 + 13],
+          "reduce-scatter", st[64 + 13] - st[64 + 12], "| barrier 2 drain + ticket", st[64 + 8] - st[64 + 13],
           "wait", st[64 + 15] - st[64 + 8], "| sum read + norm", st[64 + 14] - st[64 + 15],
           "adam", st[64 + 10] - st[64 + 14], "| minibatch total cycles", st[64 + 10] - st[0])
 else:
