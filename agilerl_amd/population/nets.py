@@ -54,13 +54,18 @@ class ActorCriticSpec:
     actor_hidden: list[int] = field(default_factory=lambda: [64])
     critic_hidden: list[int] = field(default_factory=lambda: [64])
     layer_norm: bool = True
+    # ppo.py:308: the actor's encoder is named "shared_encoder" when the critic
+    # shares it (the reference default), so its layers are
+    # shared_encoder_linear_layer_1, ... in the state dict
+    encoder_name: str = "shared_encoder"
 
     def __post_init__(self) -> None:
         ln = "affine" if self.layer_norm else None
         enc = [self.obs_dim, *self.encoder_hidden]
-        self.encoder = [Layer(f"encoder_linear_layer_{i}", enc[i - 1], enc[i], ln, True)
+        e = self.encoder_name
+        self.encoder = [Layer(f"{e}_linear_layer_{i}", enc[i - 1], enc[i], ln, True)
                         for i in range(1, len(enc))]
-        self.encoder.append(Layer("encoder_linear_layer_output", enc[-1], self.latent_dim,
+        self.encoder.append(Layer(f"{e}_linear_layer_output", enc[-1], self.latent_dim,
                                   "plain" if self.layer_norm else None, True))
         self.actor = self._head("actor", self.actor_hidden, self.n_actions, ln)
         self.critic = self._head("value", self.critic_hidden, 1, ln)  # ValueNetwork head name (value_networks.py:96)

@@ -245,11 +245,16 @@ def roofline_workload():
 def load_pmc_traffic():
     """Per-launch HBM bytes of the roofline kernels from the committed
     rocprofv3 --pmc summary (tools/pmc_roofline.py), or None."""
-    path = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
-    if not os.path.exists(path):
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")),
+                   key=lambda q: int(os.path.basename(q)[1:].split("_")[0]))
+    if not paths:
         return None
-    with open(path) as f:
-        return json.load(f)
+    with open(paths[-1]) as f:
+        out = json.load(f)
+    out["_source"] = "profiles/" + os.path.basename(paths[-1])
+    return out
 
 
 def roofline_leg(args):
@@ -297,7 +302,7 @@ def roofline_leg(args):
     pmc = load_pmc_traffic()
     if pmc is not None:  # FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, per launch set (1 GAE + E loss)
         res["traffic"] = pmc["gae_bytes"] + E * pmc["loss_bytes"]
-        res["traffic_source"] = "profiles/r1_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
+        res["traffic_source"] = pmc["_source"] + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
         res["algorithmic_bytes"] = fused_bytes
     del run_gae, run_loss
     torch.cuda.empty_cache()

@@ -35,7 +35,7 @@ def test_ppo_standalone_cycle():
     assert np.isfinite(loss) and not torch.equal(p0, agent.population.params.data)
     assert agent.steps[-1] == 128
     sd = agent.state_dict()
-    assert sd["actor.encoder.model.encoder_linear_layer_1.weight"].shape == (64, 8)
+    assert sd["actor.encoder.model.shared_encoder_linear_layer_1.weight"].shape == (64, 8)
     f = agent.test(SyntheticVecEnv(4, seed=2, p_done=0.2), loop=2)
     assert np.isfinite(f) and agent.fitness[-1] == f
 
@@ -328,8 +328,8 @@ def test_ppo_checkpoint_round_trip(tmp_path):
     agent.fitness = [0.5]
     sd = agent.state_dict()
     assert "critic.head_net.model.value_linear_layer_1.weight" in sd
-    assert torch.equal(sd["critic.encoder.model.encoder_linear_layer_1.weight"],
-                       sd["actor.encoder.model.encoder_linear_layer_1.weight"])
+    assert torch.equal(sd["critic.encoder.model.shared_encoder_linear_layer_1.weight"],
+                       sd["actor.encoder.model.shared_encoder_linear_layer_1.weight"])
     path = str(tmp_path / "ppo.pt")
     agent.save_checkpoint(path)
     other = PPO.load(path)

@@ -1,11 +1,19 @@
+# Round-end measurement sequence (run from the repo root on the GPU box):
+#   R=r2 bash tools/gpu_round_check.sh
+# GPU tests, the default bench line, a kernel trace of the bench, and the
+# separate FETCH_SIZE / WRITE_SIZE passes over the roofline workload and over
+# the C51 kernel.  Everything lands in gpurun_out/; copy summaries to profiles/.
 set -o pipefail
 export TMPDIR=/tmp
+R=${R:-r2}
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_full.log 2>&1 || { tail -20 gpurun_out/bench_full.log; exit 1; }
 tail -1 gpurun_out/bench_full.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r1 -o bench -- python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/prof_r1.log 2>&1 || { tail -20 gpurun_out/prof_r1.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o roof -- python tools/pmc_roofline.py > gpurun_out/pmc_fetch.log 2>&1 || { tail -20 gpurun_out/pmc_fetch.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o roof -- python tools/pmc_roofline.py > gpurun_out/pmc_write.log 2>&1 || { tail -20 gpurun_out/pmc_write.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$R -o bench -- python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/prof_$R.log 2>&1 || { tail -20 gpurun_out/prof_$R.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o roof -- python tools/pmc_roofline.py > gpurun_out/pmc_fetch.log 2>&1 || { tail -20 gpurun_out/pmc_fetch.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o roof -- python tools/pmc_roofline.py > gpurun_out/pmc_write.log 2>&1 || { tail -20 gpurun_out/pmc_write.log; exit 1; }
+timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/c51_fetch -o c51 -- python tools/c51_pmc.py > gpurun_out/c51_fetch.log 2>&1 || { tail -20 gpurun_out/c51_fetch.log; exit 1; }
+timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/c51_write -o c51 -- python tools/c51_pmc.py > gpurun_out/c51_write.log 2>&1 || { tail -20 gpurun_out/c51_write.log; exit 1; }
 echo ALLOK
