@@ -42,10 +42,41 @@ def _hidden(cfg: dict | None, default: list[int]) -> list[int]:
     return list(cfg.get("hidden_size", default))
 
 
-def spec_from_net_config(observation_space, action_space, net_config: dict | None) -> ActorCriticSpec:
+def _image_spec(observation_space, action_space, net_config: dict, normalize_images: bool):
+    """ImageActorCriticSpec for an image Box space (ppo.py:286-320 with
+    base.py:521-530): EvolvableCNN encoder from ``encoder_config``
+    (channel_size / kernel_size / stride_size; the reference default
+    CnnNetConfig [32, 32] 3x3 stride 1), MLP heads from ``head_config``
+    (layer_norm as configured; critic default [16])."""
+    from ..networks.base import as_config, cnn_net_config, image_norm_bounds
+    from ..population.image_nets import ImageActorCriticSpec
+
+    enc = cnn_net_config(**(as_config(net_config.get("encoder_config")) or {}))
+    if enc.get("block_type", "Conv2d") != "Conv2d" or enc.get("layer_norm"):
+        raise NotImplementedError("agx image PPO: Conv2d blocks without BatchNorm (the Atari encoders)")
+    if enc.get("activation", "ReLU") != "ReLU" or enc.get("output_activation", "ReLU") not in (None, "ReLU"):
+        raise NotImplementedError("agx image PPO: ReLU encoders")
+    head = as_config(net_config.get("head_config"))
+    actor_hidden = _hidden(head, [64])
+    critic_hidden = _hidden(head, [16])  # ppo.py:292-300 default critic head
+    head_ln = bool((head or {}).get("layer_norm", True))
+    dtype = torch.uint8 if np.dtype(observation_space.dtype) == np.uint8 else torch.float32
+    norm = image_norm_bounds(observation_space) if normalize_images else None
+    return ImageActorCriticSpec(obs_shape=tuple(observation_space.shape), n_actions=int(action_space.n),
+                                channel_size=list(enc["channel_size"]), kernel_size=list(enc["kernel_size"]),
+                                stride_size=list(enc["stride_size"]), latent_dim=int(net_config.get("latent_dim", 32)),
+                                actor_hidden=actor_hidden, critic_hidden=critic_hidden, head_layer_norm=head_ln,
+                                obs_dtype=dtype, image_norm=norm)
+
+
+def spec_from_net_config(observation_space, action_space, net_config: dict | None, normalize_images: bool = True):
     if not hasattr(action_space, "n"):
         raise NotImplementedError("agx PPO supports Discrete action spaces")
     net_config = dict(net_config or {})
+    from ..networks.base import is_image_space
+
+    if is_image_space(observation_space):
+        return _image_spec(observation_space, action_space, net_config, normalize_images)
     enc = _hidden(net_config.get("encoder_config"), [64])
     head = net_config.get("head_config")
     actor_hidden = _hidden(head, [64])
@@ -95,7 +126,7 @@ class PPO:
         self.fitness: list[float] = []
         self.steps: list[int] = [0]
         if _population is None:
-            spec = spec_from_net_config(observation_space, action_space, net_config)
+            spec = spec_from_net_config(observation_space, action_space, net_config, normalize_images)
             _population = PPOPopulation(spec, 1, num_envs, learn_step=learn_step, batch_size=batch_size, lr=lr,
                                         gamma=gamma, gae_lambda=gae_lambda, clip_coef=clip_coef, ent_coef=ent_coef,
                                         vf_coef=vf_coef, max_grad_norm=max_grad_norm, update_epochs=update_epochs,
@@ -260,7 +291,9 @@ class PPO:
         """-> (action, log_prob, entropy, value) numpy arrays (ppo.py:567-633);
         sampling is a Gumbel-max draw from a counter-based Philox stream."""
         pop = self.population
-        o = torch.as_tensor(np.asarray(obs), dtype=torch.float32, device=self.device)
+        o = np.asarray(obs)
+        keep_u8 = o.dtype == np.uint8 and pop.obs.dtype == torch.uint8  # frames normalised in the conv load
+        o = torch.as_tensor(o, dtype=torch.uint8 if keep_u8 else torch.float32, device=self.device)
         o = o.reshape(-1, pop.spec.obs_dim).contiguous()
         n = o.shape[0]
         mask = None

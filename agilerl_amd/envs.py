@@ -221,6 +221,9 @@ class StackedVecEnv:
         for attr in ("single_observation_space", "single_action_space", "observation_space", "action_space"):
             if hasattr(e0, attr):
                 setattr(self, attr, getattr(e0, attr))
+        space = getattr(e0, "single_observation_space", None)
+        # uint8 image frames stay uint8; everything else is stacked as f32
+        self._obs_dtype = np.uint8 if getattr(space, "dtype", None) == np.uint8 else np.float32
 
     @classmethod
     def from_shared(cls, env, copies: int) -> "StackedVecEnv":
@@ -256,12 +259,12 @@ class StackedVecEnv:
 
     def reset(self, seed=None, options=None, out_obs: np.ndarray | None = None):
         res = [e.reset() if seed is None else e.reset(seed=seed + k) for k, e in enumerate(self.envs)]
-        obs = self._cat([r[0] for r in res], out_obs, np.float32)
+        obs = self._cat([r[0] for r in res], out_obs, self._obs_dtype)
         return obs, self._infos([r[1] for r in res])
 
     def step(self, actions, out_obs=None, out_rew=None, out_done=None):
         res = [e.step(a) for e, a in zip(self.envs, self._split(np.asarray(actions)))]
-        obs = self._cat([r[0] for r in res], out_obs, np.float32)
+        obs = self._cat([r[0] for r in res], out_obs, self._obs_dtype)
         rew = self._cat([r[1] for r in res], out_rew, np.float32)
         term = np.concatenate([np.asarray(r[2], dtype=bool) for r in res])
         trunc = np.concatenate([np.asarray(r[3], dtype=bool) for r in res])

@@ -128,7 +128,8 @@ class PPOPopulation:
     def _alloc_rollout(self):
         P, T, N, D, dev = self.P, self.T, self.N, self.spec.obs_dim, self.device
         f32 = dict(dtype=torch.float32, device=dev)
-        self.obs = torch.zeros(P, T, N, D, **f32)
+        # image specs keep uint8 frames (normalised inside the first conv's load)
+        self.obs = torch.zeros(P, T, N, D, dtype=getattr(self.spec, "obs_dtype", torch.float32), device=dev)
         self.actions = torch.zeros(P, T, N, dtype=torch.int64, device=dev)
         self.rewards = torch.zeros(P, T, N, **f32)
         self.dones = torch.zeros(P, T, N, dtype=torch.uint8, device=dev)
@@ -157,8 +158,8 @@ class PPOPopulation:
     def fused_descriptor(self):
         """agx_ppo_net for this architecture, or None when the fused kernels do
         not cover it (then the plain-PyTorch forward / learner run)."""
-        if not self.fused:
-            return None
+        if not self.fused or not isinstance(self.spec, ActorCriticSpec):
+            return None  # the fused kernels take the MLP actor-critic shapes only
         if self._desc is None:
             from .learner import net_descriptor
 
@@ -408,11 +409,31 @@ class PPOPopulation:
         kernel and the path for architectures it does not cover.  Same
         semantics, including target-KL early stop per agent (stopped agents'
         rows are left untouched) and action masks."""
-        P, S, D = self.P, self.S, self.spec.obs_dim
-        if self.heterogeneous:
-            raise NotImplementedError("per-agent batch / epochs / entropy hyperparameters need the fused learner "
-                                      "(agx_ppo_learn); this architecture runs the PyTorch learner")
+        if perms is None:
+            perms = self.permutations()
         K.adv_normalize_(self.advantages, self.adv_stats)
+        if not self.heterogeneous:
+            return self._learn_torch_group(perms, None, self.batch_size, self.update_epochs, self.ent_coef)
+        # per-agent batch / epochs / entropy (HPO mutations): agents sharing all
+        # three learn together; the others' rows are left untouched (active mask)
+        groups: dict[tuple, list[int]] = {}
+        for p in range(self.P):
+            groups.setdefault((self.agent_batch[p], self.agent_epochs[p], self.agent_ent[p]), []).append(p)
+        out = torch.zeros(self.P, dtype=torch.float32, device=self.device)
+        kl = torch.zeros(self.P, dtype=torch.float32, device=self.device)
+        for (b, e, ent), rows in groups.items():
+            loss = self._learn_torch_group(perms, rows, b, e, ent)
+            idx = torch.tensor(rows, device=self.device)
+            out[idx] = loss[idx]
+            kl[idx] = self.last_kl[idx]
+        self.last_kl = kl
+        return out
+
+    def _learn_torch_group(self, perms, rows, batch_size, epochs, ent_coef) -> torch.Tensor:
+        """E epochs x minibatches of ``batch_size`` for the agents in ``rows``
+        (None: all agents); -> the reference's mean loss per agent [P]."""
+        P, S, D = self.P, self.S, self.spec.obs_dim
+        image = not isinstance(self.spec, ActorCriticSpec)
         obs = self.obs.view(P, S, D)
         act = self.actions.view(P, S)
         masks = None if self.action_masks is None else self.action_masks.view(P, S, -1)
@@ -421,18 +442,22 @@ class PPOPopulation:
         ret = self.returns.view(-1)
         old_v = self.values.view(-1)
         base = (torch.arange(P, device=self.device) * S).unsqueeze(1)
-        if perms is None:
-            perms = self.permutations()
         total = torch.zeros(P, dtype=torch.float32, device=self.device)
         kl_sum = torch.zeros(P, dtype=torch.float64, device=self.device)
         n_mb = 0
-        active = None  # all agents until one stops (u8 [P])
-        for e in range(self.update_epochs):
-            for s0, s1 in self.minibatch_plan():
+        member = None
+        if rows is not None:
+            member = torch.zeros(P, dtype=torch.uint8, device=self.device)
+            member[torch.tensor(rows, device=self.device)] = 1
+        active = member  # all (member) agents until one stops (u8 [P])
+        plan = [(s, min(s + batch_size, S)) for s in range(0, S, batch_size)]
+        for e in range(epochs):
+            for s0, s1 in plan:
                 idx = perms[e][:, s0:s1]  # [P, b]
                 ob = torch.gather(obs, 1, idx.unsqueeze(-1).expand(-1, -1, D))
                 ac = torch.gather(act, 1, idx)
-                logits, value = self.spec.forward(self.params, ob)
+                logits, value = (self.spec.forward(self.params, ob, rows=rows) if image
+                                 else self.spec.forward(self.params, ob))
                 if masks is not None:
                     mk = torch.gather(masks, 1, idx.unsqueeze(-1).expand(-1, -1, masks.shape[-1]))
                     logits = torch.where(mk.bool(), logits, torch.full_like(logits, -1e8))
@@ -440,7 +465,7 @@ class PPOPopulation:
                 logp = logp_all.gather(-1, ac.unsqueeze(-1)).squeeze(-1)
                 gidx = (idx + base).reshape(-1).contiguous()
                 loss, stats = _PPOLossFn.apply(logp, value, ent, old_logp, adv, ret, old_v, gidx,
-                                               s1 - s0, self.clip_coef, self.vf_coef, self.ent_coef)
+                                               s1 - s0, self.clip_coef, self.vf_coef, ent_coef)
                 self.params.grad.zero_()
                 loss.backward()
                 self.opt.step(active)
@@ -457,8 +482,8 @@ class PPOPopulation:
                 active = now.contiguous()
                 if int(active.sum()) == 0:
                     break
-        self.last_kl = (kl_sum / n_mb).float()
-        return total / (S * self.update_epochs)
+        self.last_kl = (kl_sum / max(n_mb, 1)).float()
+        return total / (S * epochs)
 
     # ------------------------------------------------------------------ #
     @torch.no_grad()

@@ -67,12 +67,14 @@ def _coherent(owner, nbytes: int) -> torch.Tensor:
     return torch.from_numpy(np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)))
 
 
-def _packed(P: int, N: int, D: int, owner=None, **kw):
-    """One byte buffer [obs f32 P*N*D | reward f32 P*N | done u8 P*N] + views."""
-    n_obs, n_rew = P * N * D * 4, P * N * 4
+def _packed(P: int, N: int, D: int, owner=None, obs_dtype=torch.float32, **kw):
+    """One byte buffer [obs P*N*D (f32, or uint8 frames) | reward f32 P*N |
+    done u8 P*N] + views (the reward stays 4-byte aligned)."""
+    isz = torch.empty(0, dtype=obs_dtype).element_size()
+    n_obs, n_rew = (P * N * D * isz + 15) // 16 * 16, P * N * 4
     nbytes = (n_obs + n_rew + P * N + 15) // 16 * 16
     buf = _coherent(owner, nbytes) if owner is not None else torch.zeros(nbytes, dtype=torch.uint8, **kw)
-    obs = buf[:n_obs].view(torch.float32).view(P * N, D)
+    obs = buf[:P * N * D * isz].view(obs_dtype).view(P * N, D)
     rew = buf[n_obs:n_obs + n_rew].view(torch.float32)
     done = buf[n_obs + n_rew:n_obs + n_rew + P * N].view(torch.bool)
     return buf, obs, rew, done
@@ -105,12 +107,13 @@ class PopulationRunner:
             self.seq_base = 0
             self.timeout_s = float(os.environ.get("AGX_ROLLOUT_TIMEOUT", "20"))
         else:
-            self.stage_h, self.obs_h, self.rew_h, self.done_h = _packed(P, N, D, pin_memory=True)
+            self.stage_h, self.obs_h, self.rew_h, self.done_h = _packed(P, N, D, obs_dtype=pop.obs.dtype,
+                                                                        pin_memory=True)
             self.act_h = torch.zeros(P * N, dtype=torch.int64, pin_memory=True)
-        self.stage_d, self.obs_d, self.rew_d, self.done_d = _packed(P, N, D, device=dev)
+        self.stage_d, self.obs_d, self.rew_d, self.done_d = _packed(P, N, D, obs_dtype=pop.obs.dtype, device=dev)
         self.term_h = torch.zeros(P * N, dtype=torch.bool, pin_memory=True)
         self.act_d = torch.zeros(P * N, dtype=torch.int64, device=dev)
-        self.last_obs = torch.zeros(P, N, D, dtype=torch.float32, device=dev)
+        self.last_obs = torch.zeros(P, N, D, dtype=pop.obs.dtype, device=dev)
         self.last_done = torch.zeros(P, N, dtype=torch.uint8, device=dev)
         self.last_value = torch.zeros(P, N, dtype=torch.float32, device=dev)
         self.last_value_valid = False
@@ -325,8 +328,8 @@ class PopulationRunner:
         desc = pop.fused_descriptor()
         act_d = torch.empty(P * N, dtype=torch.int64, device=pop.device)
         act_h = torch.empty(P * N, dtype=torch.int64, pin_memory=True)
-        obs_h = torch.empty(P * N * D, dtype=torch.float32, pin_memory=True)
-        obs_d = torch.empty(P, N, D, dtype=torch.float32, device=pop.device)
+        obs_h = torch.empty(P * N * D, dtype=pop.obs.dtype, pin_memory=True)
+        obs_d = torch.empty(P, N, D, dtype=pop.obs.dtype, device=pop.device)
         out = np.zeros((loop, P))
         for k in range(loop):
             obs, _ = env.reset()
@@ -335,7 +338,7 @@ class PopulationRunner:
             finished = np.zeros(P * N, dtype=bool)
             step = 0
             while not finished.all():
-                obs_h.numpy()[:] = np.asarray(obs, dtype=np.float32).reshape(-1)
+                obs_h.numpy()[:] = np.asarray(obs).reshape(-1)
                 obs_d.view(-1).copy_(obs_h, non_blocking=True)
                 if desc is not None:
                     from .learner import policy_step

@@ -99,6 +99,74 @@ class ActorCritic(nn.Module):
         return logp, ent, value
 
 
+class _Norm(nn.Module):
+    """preprocess_observation's image normalisation (algo_utils.py:1134-1183)."""
+
+    def __init__(self, bounds):
+        super().__init__()
+        self.bounds = bounds
+
+    def forward(self, x):
+        x = x.float()
+        if self.bounds is None:
+            return x
+        lo, hi = self.bounds
+        return (x - lo) / (hi - lo)
+
+
+class ImageActorCritic(ActorCritic):
+    """The shared-encoder actor-critic for image spaces (ppo.py:286-320,
+    base.py:521-530): EvolvableCNN encoder (cnn.py:224-552: Conv2d -> ReLU per
+    layer, flatten, Linear -> ReLU) and create_mlp heads (layer_norm as given,
+    output x0.1).  Plain nn.Conv2d modules with the reference's names
+    (``{encoder}_conv_layer_{i}``, ``{encoder}_linear_output``)."""
+
+    def __init__(self, obs_shape, n_actions: int, channels: list[int], kernels: list[int], strides: list[int],
+                 latent: int, actor_hidden: list[int], critic_hidden: list[int], head_ln: bool = False,
+                 norm=(0.0, 255.0), encoder_name: str = "shared_encoder"):
+        nn.Module.__init__(self)
+        c, h, w = obs_shape
+        d: "OrderedDict[str, nn.Module]" = OrderedDict()
+        for i, (co, k, st) in enumerate(zip(channels, kernels, strides), 1):
+            d[f"{encoder_name}_conv_layer_{i}"] = nn.Conv2d(c, co, k, stride=st)
+            d[f"{encoder_name}_activation_{i}"] = nn.ReLU()
+            c, h, w = co, (h - k) // st + 1, (w - k) // st + 1
+        d[f"{encoder_name}_flatten"] = nn.Flatten()
+        d[f"{encoder_name}_linear_output"] = nn.Linear(c * h * w, latent)
+        d[f"{encoder_name}_output_activation"] = nn.ReLU()
+        self.encoder = nn.Sequential(d)
+        self.norm = _Norm(norm)
+        self.obs_shape = tuple(obs_shape)
+        self.actor_head = _head_mlp("actor", latent, actor_hidden, n_actions, head_ln)
+        self.critic_head = _head_mlp("value", latent, critic_hidden, 1, head_ln)
+
+    def evaluate(self, obs, actions, mask=None):
+        x = self.norm(obs.reshape(-1, *self.obs_shape))
+        lat = self.encoder(x)
+        logits = self.actor_head(lat)
+        if mask is not None:
+            logits = torch.where(mask, logits, torch.full_like(logits, -1e8))
+        logp_all = torch.log_softmax(logits, dim=-1)
+        logp = logp_all.gather(-1, actions.long().unsqueeze(-1)).squeeze(-1)
+        p = torch.softmax(logits, dim=-1)
+        ent = -(p * torch.log(p + 1e-8)).sum(-1)
+        value = self.critic_head(lat).squeeze(-1)
+        return logp, ent, value
+
+
+def _head_mlp(name: str, fin: int, hidden: list[int], fout: int, ln: bool) -> nn.Sequential:
+    d: "OrderedDict[str, nn.Module]" = OrderedDict()
+    dims = [fin, *hidden]
+    for i in range(1, len(dims)):
+        d[f"{name}_linear_layer_{i}"] = nn.Linear(dims[i - 1], dims[i])
+        if ln:
+            d[f"{name}_layer_norm_{i}"] = nn.LayerNorm(dims[i])
+        d[f"{name}_activation_{i}"] = nn.ReLU()
+    d[f"{name}_linear_layer_output"] = nn.Linear(dims[-1], fout)
+    d[f"{name}_activation_output"] = nn.Identity()
+    return nn.Sequential(d)
+
+
 def reference_learn(net: ActorCritic, adam_state: dict | None, obs, actions, old_logp, adv, ret, old_v,
                     perms, *, batch_size: int, epochs: int, clip: float = 0.2, vf: float = 0.5, ent: float = 0.01,
                     max_norm: float = 0.5, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
@@ -125,7 +193,9 @@ def reference_learn(net: ActorCritic, adam_state: dict | None, obs, actions, old
     actor_params = list(net.encoder.parameters()) + list(net.actor_head.parameters())
     critic_params = list(net.critic_head.parameters())
     t = lambda a: torch.as_tensor(np.asarray(a))  # noqa: E731
-    obs, actions = t(obs).to(dtype), t(actions)
+    obs, actions = t(obs), t(actions)
+    if not isinstance(net, ImageActorCritic):  # image frames stay uint8 until the net normalises them
+        obs = obs.to(dtype)
     old_logp, ret, old_v, adv = (t(x).to(dtype) for x in (old_logp, ret, old_v, adv))
     mask_t = None if masks is None else t(masks).bool()
     adv = (adv - adv.mean()) / (adv.std() + 1e-8)

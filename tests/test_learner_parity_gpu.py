@@ -59,8 +59,10 @@ def _pop(P, N, T, D, A, enc, lat, ah, ch, batch, epochs, lr, target_kl=None, mas
     from agilerl_amd.population.nets import ActorCriticSpec
     from agilerl_amd.population.ppo_pop import PPOPopulation
 
+    # the golden networks are create_mlp(..., name="encoder") (gen_golden.py), so
+    # the spec takes that encoder name for the state-dict key map
     spec = ActorCriticSpec(obs_dim=D, n_actions=A, encoder_hidden=list(enc), latent_dim=lat,
-                           actor_hidden=list(ah), critic_hidden=list(ch))
+                           actor_hidden=list(ah), critic_hidden=list(ch), encoder_name="encoder")
     pop = PPOPopulation(spec, P, N, learn_step=T * N, batch_size=batch, lr=lr, update_epochs=epochs,
                         target_kl=target_kl, seeds=seeds, device=DEV, fused=True, action_masks=masks)
     assert pop.fused_descriptor() is not None

@@ -179,3 +179,40 @@ def test_image_space_networks_and_preprocessing():
     assert image_norm_bounds(Box(0, 1, (3, 8, 8))) is None
     assert image_norm_bounds(Box(-np.inf, np.inf, (3, 8, 8))) is None
     assert image_norm_bounds(Box(-1, 7, (3, 8, 8))) == (-1.0, 7.0)
+
+
+def test_image_actor_critic_spec_layout():
+    """ppo_image.yaml's network as the population's flat layout: reference
+    state-dict names (shared_encoder_conv_layer_i, linear_output, heads),
+    the clip groups and the uint8 frame storage (CPU: no forward)."""
+    import numpy as np
+
+    from agilerl_amd.algorithms.ppo import spec_from_net_config
+    from agilerl_amd.envs import Box, Discrete
+
+    space = Box(0, 255, (4, 84, 84), dtype=np.uint8)
+    net_config = {"latent_dim": 256,
+                  "encoder_config": {"channel_size": [32, 64, 128], "kernel_size": [8, 4, 3], "stride_size": [4, 2, 1]},
+                  "head_config": {"hidden_size": [256], "layer_norm": False}}
+    spec = spec_from_net_config(space, Discrete(4), net_config)
+    keys = spec.state_dict_keys()
+    assert keys["actor.encoder.model.shared_encoder_conv_layer_1.weight"][1] == (32, 4, 8, 8)
+    assert keys["actor.encoder.model.shared_encoder_conv_layer_3.weight"][1] == (128, 64, 3, 3)
+    assert keys["actor.encoder.model.shared_encoder_linear_output.weight"][1] == (256, 128 * 7 * 7)
+    assert keys["actor.head_net.model.actor_linear_layer_1.weight"][1] == (256, 256)
+    assert keys["critic.head_net.model.value_linear_layer_output.weight"][1] == (1, 256)
+    assert keys["critic.encoder.model.shared_encoder_conv_layer_2.bias"] == \
+        keys["actor.encoder.model.shared_encoder_conv_layer_2.bias"]
+    assert spec.group_offsets == [0, keys["critic.head_net.model.value_linear_layer_1.weight"][0], spec.n_params]
+    assert spec.obs_dtype == torch.uint8 and spec.image_norm == (0.0, 255.0) and spec.obs_dim == 4 * 84 * 84
+    # every parameter is covered exactly once by the state-dict map
+    cover = np.zeros(spec.n_params, np.int32)
+    for k, (o, sh) in keys.items():
+        if not k.startswith("critic.encoder."):
+            cover[o:o + int(np.prod(sh))] += 1
+    assert (cover == 1).all()
+    flat = spec.init_params(2, [0, 1])
+    w1 = flat[0, :32 * 4 * 64].view(32, 256)
+    torch.testing.assert_close(w1 @ w1.T, 2.0 * torch.eye(32), rtol=0, atol=1e-4)  # orthogonal, gain sqrt 2
+    o, sh = keys["actor.head_net.model.actor_linear_layer_output.weight"]
+    assert flat[0, o:o + 4 * 256].abs().max() < 0.2  # output_vanish x0.1
