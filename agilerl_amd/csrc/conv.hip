@@ -10,28 +10,52 @@
 //            algo_utils.py:1134-1183): 4x fewer bytes than a separate f32 copy.
 //   wgrad    dW[co,(ci,kh,kw)] = sum_p dZ[co,p] Xcol[(ci,kh,kw),p], dZ = dY * act'(Y);
 //            M = Cout, N = Cin*KH*KW + 1 (the extra ones-column gives db), K = B*OH*OW,
-//            split over workgroups (partials in a workspace, summed in a fixed order).
+//            split over enough workgroups to fill the chip (>= ~1024 tiles x splits;
+//            partials in a workspace, summed in a fixed order).
 //   dgrad    dX[b,ci,ih,iw] = sum_{co,kh,kw} W[co,ci,kh,kw] dZ[b,co,(ih-kh)/s,(iw-kw)/s]
 //            over the taps that land on the output grid; M = Cin, N = B*H*W, K = Cout*KH*KW.
 //
-// One kernel template serves the three: a 64x64 output tile per 256-thread
-// workgroup (4 waves, each 32x32 = 2x2 v_mfma_f32_16x16x4_f32 tiles), K in
-// steps of 16 staged through LDS (rows padded to 80 floats: the two 32-lane
-// halves of a ds_read_b32 land in disjoint banks), the next step's operands
-// gathered into registers while the current one multiplies.  The operand
-// gathers and the epilogue are the only per-mode code (functors below).
+// One kernel template serves the three: a BM x BN output tile per 256-thread
+// workgroup (4 waves, each 32x32 = 2x2 v_mfma_f32_16x16x4_f32 tiles; 64x64, or
+// 32x128 when M <= 32 so a 32-channel layer wastes no MFMA rows), K in steps of
+// 16 staged through LDS (rows padded by 16 floats), the next step's operands
+// gathered into registers while the current one multiplies.
+//
+// Gathers are table driven: im2col index arithmetic (the div / mod chains
+// that turn a GEMM index into a tensor offset) is done ONCE per workgroup into
+// LDS tables over the K range it walks (in chunks of kTab entries), and once
+// per thread for its fixed output column — every thread of a 256-thread tile
+// keeps the same GEMM column for the whole K loop (bn = tid % BN).  A gathered
+// element then costs one LDS table read and one global load; with the old
+// per-element decode the kernels were VALU-bound several times over the MFMA
+// time.
 #include "agx_common.h"
 
 namespace agx {
 
 namespace conv {
 
-constexpr int BM = 64, BN = 64, BK = 16, NT = 256, LDP = 80;
+constexpr int BK = 16, NT = 256, kTab = 1024, kTapMax = 16;
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 struct Shape {
     int B, Cin, H, W, Cout, KH, KW, S, OH, OW;
 };
+
+// per-workgroup LDS: operand double buffers + gather tables
+template <int BM, int BN>
+struct Smem {
+    static constexpr int LDA = BM + 16, LDB = BN + 16;
+    float As[2][BK][LDA];  // As[k][m]
+    float Bs[2][BK][LDB];  // Bs[k][n]
+    int tabA[kTab], tabB[kTab];
+    int col[BN][2 * kTapMax];  // dgrad: per output column, oh of tap kh / ow of tap kw (-1: no tap)
+};
+
+__device__ __forceinline__ float ld_x(const void *x, int o, bool u8, float lo, float rng) {
+    if (u8) return ((float)static_cast<const unsigned char *>(x)[o] - lo) / rng;  // IEEE division, as the reference
+    return static_cast<const float *>(x)[o];
+}
 
 // ---- forward -------------------------------------------------------------
 template <bool U8>
@@ -40,21 +64,51 @@ struct FwdOps {
     const void *x;       // [B][Cin][H][W], f32 or u8
     const float *bias;   // [Cout] or null
     float *y;            // [B][Cout][OH][OW]
-    float lo, rng;  // u8 normalisation: (x - lo) / rng
+    float lo, rng;       // u8 normalisation: (x - lo) / rng
     int relu;
     Shape s;
     int M, N, K;
-    __device__ float a(int m, int k) const { return (m < M && k < K) ? w[(size_t)m * K + k] : 0.f; }
-    __device__ float b(int k, int n) const {
-        if (k >= K || n >= N) return 0.f;
-        const int kw = k % s.KW, t = k / s.KW, kh = t % s.KH, ci = t / s.KH;
-        const int ow = n % s.OW, t2 = n / s.OW, oh = t2 % s.OH, bb = t2 / s.OH;
-        const size_t o = (((size_t)bb * s.Cin + ci) * s.H + (oh * s.S + kh)) * s.W + (ow * s.S + kw);
-        if constexpr (U8) {
-            const float v = (float)static_cast<const unsigned char *>(x)[o];
-            return (v - lo) / rng;  // IEEE division, as the reference's tensor op
+    long long gx, gw, gb, gy;  // per-group element strides (population-batched launch)
+    __device__ FwdOps at(int g) const {
+        FwdOps o = *this;
+        o.x = static_cast<const char *>(x) + (size_t)g * gx * (U8 ? 1 : 4);
+        o.w = w + (size_t)g * gw;
+        o.bias = bias ? bias + (size_t)g * gb : nullptr;
+        o.y = y + (size_t)g * gy;
+        return o;
+    }
+    struct Ctx {
+        int xbase;  // input offset of this thread's output pixel, -1 past N
+    };
+    template <class SM>
+    __device__ void setup(Ctx &c, SM &, int, int n, int) const {
+        if (n < N) {
+            const int ow = n % s.OW, t = n / s.OW, oh = t % s.OH, bb = t / s.OH;
+            c.xbase = ((bb * s.Cin) * s.H + oh * s.S) * s.W + ow * s.S;
         } else {
-            return static_cast<const float *>(x)[o];
+            c.xbase = -1;
+        }
+    }
+    template <class SM>
+    __device__ void build(SM &sm, int kc, int kce, int tid) const {  // tabB[k - kc] = im2col offset of k
+        for (int k = kc + tid; k < kce; k += NT) {
+            const int kw = k % s.KW, t = k / s.KW, kh = t % s.KH, ci = t / s.KH;
+            sm.tabB[k - kc] = (ci * s.H + kh) * s.W + kw;
+        }
+    }
+    template <int NA, int NB, int BN, class SM>
+    __device__ void gather(const Ctx &c, const SM &sm, int m_blk, int kc, int kb, int k1, int tid, float *ra,
+                           float *rb) const {
+        const int k = kb + tid % BK;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int m = m_blk + tid / BK + i * (NT / BK);
+            ra[i] = (m < M && k < k1) ? w[(size_t)m * K + k] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const int kk = kb + tid / BN + i * (NT / BN);
+            rb[i] = (c.xbase >= 0 && kk < k1) ? ld_x(x, c.xbase + sm.tabB[kk - kc], U8, lo, rng) : 0.f;
         }
     }
     __device__ void store(int m, int n, float v, int) const {
@@ -73,24 +127,63 @@ struct WgradOps {
     const float *yact;   // post-activation output (ReLU mask), or null
     const void *x;       // layer input
     float lo, rng;
-    float *part;         // [splits][Cout][K+1]
+    float *part;         // [groups][splits][Cout][K+1]
     Shape s;
     int M, N, K;         // M = Cout, N = Cin*KH*KW + 1, K = B*OH*OW (split over blockIdx.z)
-    __device__ float a(int m, int p) const {
-        if (m >= M || p >= K) return 0.f;
-        const int ow = p % s.OW, t = p / s.OW, oh = t % s.OH, bb = t / s.OH;
-        const size_t o = (((size_t)bb * s.Cout + m) * s.OH + oh) * s.OW + ow;
-        const float g = dy[o];
-        return (yact && !(yact[o] > 0.f)) ? 0.f : g;
+    long long gx, gy, gp;
+    __device__ WgradOps at(int g) const {
+        WgradOps o = *this;
+        o.x = static_cast<const char *>(x) + (size_t)g * gx * (U8 ? 1 : 4);
+        o.dy = dy + (size_t)g * gy;
+        o.yact = yact ? yact + (size_t)g * gy : nullptr;
+        o.part = part + (size_t)g * gp;
+        return o;
     }
-    __device__ float b(int p, int n) const {
-        if (p >= K || n >= N) return 0.f;
-        if (n == N - 1) return 1.f;  // ones column -> bias gradient
-        const int kw = n % s.KW, t = n / s.KW, kh = t % s.KH, ci = t / s.KH;
-        const int ow = p % s.OW, t2 = p / s.OW, oh = t2 % s.OH, bb = t2 / s.OH;
-        const size_t o = (((size_t)bb * s.Cin + ci) * s.H + (oh * s.S + kh)) * s.W + (ow * s.S + kw);
-        if constexpr (U8) return ((float)static_cast<const unsigned char *>(x)[o] - lo) / rng;
-        else return static_cast<const float *>(x)[o];
+    struct Ctx {
+        int koff;  // im2col offset of this thread's weight column; -2: the ones column, -1: past N
+    };
+    template <class SM>
+    __device__ void setup(Ctx &c, SM &, int, int n, int) const {
+        if (n < N - 1) {
+            const int kw = n % s.KW, t = n / s.KW, kh = t % s.KH, ci = t / s.KH;
+            c.koff = (ci * s.H + kh) * s.W + kw;
+        } else {
+            c.koff = n == N - 1 ? -2 : -1;
+        }
+    }
+    template <class SM>
+    __device__ void build(SM &sm, int kc, int kce, int tid) const {
+        const int ohw = s.OH * s.OW;
+        for (int p = kc + tid; p < kce; p += NT) {
+            const int r = p % ohw, bb = p / ohw, ow = r % s.OW, oh = r / s.OW;
+            sm.tabA[p - kc] = bb * s.Cout * ohw + r;                            // dy offset, channel 0
+            sm.tabB[p - kc] = ((bb * s.Cin) * s.H + oh * s.S) * s.W + ow * s.S;  // x offset, column 0
+        }
+    }
+    template <int NA, int NB, int BN, class SM>
+    __device__ void gather(const Ctx &c, const SM &sm, int m_blk, int kc, int kb, int k1, int tid, float *ra,
+                           float *rb) const {
+        const int ohw = s.OH * s.OW;
+        const int p = kb + tid % BK;
+        const int dbase = p < k1 ? sm.tabA[p - kc] : 0;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int m = m_blk + tid / BK + i * (NT / BK);
+            float g = 0.f;
+            if (m < M && p < k1) {
+                const int o = dbase + m * ohw;
+                g = dy[o];
+                if (yact && !(yact[o] > 0.f)) g = 0.f;
+            }
+            ra[i] = g;
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const int pp = kb + tid / BN + i * (NT / BN);
+            float v = 0.f;
+            if (pp < k1) v = c.koff >= 0 ? ld_x(x, sm.tabB[pp - kc] + c.koff, U8, lo, rng) : (c.koff == -2 ? 1.f : 0.f);
+            rb[i] = v;
+        }
     }
     __device__ void store(int m, int n, float v, int z) const {
         if (m < M && n < N) part[((size_t)z * M + m) * N + n] = v;
@@ -98,97 +191,154 @@ struct WgradOps {
 };
 
 // ---- data gradient -------------------------------------------------------
+// Sub-pixel form for stride s > 1: input pixels of one phase (ih mod s, iw mod s)
+// = (ph, pw) are reached only by the taps kh = ph + s*a, kw = pw + s*b, at
+// output (ih' - a, iw' - b) where ih = ih'*s + ph.  One GEMM per phase over just
+// those taps (K / s^2 of the full tap set: no MFMA work on structural zeros).
 struct DgradOps {
     const float *w;      // [Cout][Cin][KH][KW]
     const float *dy, *yact;
     float *dx;           // [B][Cin][H][W]
     Shape s;
-    int M, N, K;         // M = Cin, N = B*H*W, K = Cout*KH*KW
-    __device__ float a(int ci, int k) const {
-        if (ci >= M || k >= K) return 0.f;
-        const int kw = k % s.KW, t = k / s.KW, kh = t % s.KH, co = t / s.KH;
-        return w[(((size_t)co * s.Cin + ci) * s.KH + kh) * s.KW + kw];
+    int M, N, K;         // M = Cin, N = B*Hp*Wp (this phase's pixels), K = Cout*nA*nB (its taps)
+    int ph, pw, Hp, Wp, nA, nB;
+    long long gw, gy, gx;
+    __device__ DgradOps at(int g) const {
+        DgradOps o = *this;
+        o.w = w + (size_t)g * gw;
+        o.dy = dy + (size_t)g * gy;
+        o.yact = yact ? yact + (size_t)g * gy : nullptr;
+        o.dx = dx + (size_t)g * gx;
+        return o;
     }
-    __device__ float b(int k, int n) const {
-        if (k >= K || n >= N) return 0.f;
-        const int kw = k % s.KW, t = k / s.KW, kh = t % s.KH, co = t / s.KH;
-        const int iw = n % s.W, t2 = n / s.W, ih = t2 % s.H, bb = t2 / s.H;
-        const int ph = ih - kh, pw = iw - kw;
-        if (ph < 0 || pw < 0 || ph % s.S || pw % s.S) return 0.f;
-        const int oh = ph / s.S, ow = pw / s.S;
-        if (oh >= s.OH || ow >= s.OW) return 0.f;
-        const size_t o = (((size_t)bb * s.Cout + co) * s.OH + oh) * s.OW + ow;
-        const float g = dy[o];
-        return (yact && !(yact[o] > 0.f)) ? 0.f : g;
+    struct Ctx {
+        int dbase;  // dy offset of this thread's image (channel 0), -1 past N
+        int c;      // column within the tile
+    };
+    template <class SM>
+    __device__ void setup(Ctx &c, SM &sm, int n_local, int n, int tid) const {
+        c.c = n_local;
+        int ihp = 0, iwp = 0;
+        c.dbase = -1;
+        if (n < N) {
+            iwp = n % Wp;
+            const int t = n / Wp;
+            ihp = t % Hp;
+            c.dbase = (t / Hp) * s.Cout * s.OH * s.OW;
+        }
+        if (tid == n_local) {  // one thread per column fills its tap table
+            for (int a = 0; a < nA; ++a) {
+                const int oh = ihp - a;
+                sm.col[n_local][a] = (oh >= 0 && oh < s.OH) ? oh : -1;
+            }
+            for (int b = 0; b < nB; ++b) {
+                const int ow = iwp - b;
+                sm.col[n_local][kTapMax + b] = (ow >= 0 && ow < s.OW) ? ow : -1;
+            }
+        }
+    }
+    template <class SM>
+    __device__ void build(SM &sm, int kc, int kce, int tid) const {
+        const int khw = s.KH * s.KW, nab = nA * nB;
+        for (int k = kc + tid; k < kce; k += NT) {
+            const int r = k % nab, co = k / nab, a = r / nB, b = r % nB;
+            sm.tabA[k - kc] = co * s.Cin * khw + (ph + s.S * a) * s.KW + pw + s.S * b;  // weight offset, channel 0
+            sm.tabB[k - kc] = co | (a << 16) | (b << 24);
+        }
+    }
+    template <int NA, int NB, int BN, class SM>
+    __device__ void gather(const Ctx &c, const SM &sm, int m_blk, int kc, int kb, int k1, int tid, float *ra,
+                           float *rb) const {
+        const int khw = s.KH * s.KW, ohw = s.OH * s.OW;
+        const int k = kb + tid % BK;
+        const int wb = k < k1 ? sm.tabA[k - kc] : 0;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int ci = m_blk + tid / BK + i * (NT / BK);
+            ra[i] = (ci < M && k < k1) ? w[wb + ci * khw] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const int kk = kb + tid / BN + i * (NT / BN);
+            float g = 0.f;
+            if (kk < k1 && c.dbase >= 0) {
+                const int pk = sm.tabB[kk - kc];
+                const int oh = sm.col[c.c][(pk >> 16) & 255], ow = sm.col[c.c][kTapMax + (pk >> 24)];
+                if (oh >= 0 && ow >= 0) {
+                    const int o = c.dbase + (pk & 0xffff) * ohw + oh * s.OW + ow;
+                    g = dy[o];
+                    if (yact && !(yact[o] > 0.f)) g = 0.f;
+                }
+            }
+            rb[i] = g;
+        }
     }
     __device__ void store(int ci, int n, float v, int) const {
         if (ci >= M || n >= N) return;
-        const int iw = n % s.W, t2 = n / s.W, ih = t2 % s.H, bb = t2 / s.H;
-        dx[(((size_t)bb * s.Cin + ci) * s.H + ih) * s.W + iw] = v;
+        const int iwp = n % Wp, t2 = n / Wp, ihp = t2 % Hp, bb = t2 / Hp;
+        dx[(((size_t)bb * s.Cin + ci) * s.H + ihp * s.S + ph) * s.W + iwp * s.S + pw] = v;
     }
 };
 
 // K range [k0, k1); chunk > 0 splits it over blockIdx.z (split-K, partial tiles per z)
-template <class Ops>
-__global__ __launch_bounds__(NT) void igemm_kernel(Ops ops, int k0, int k1, int chunk) {
+// blockIdx.z = group * zsub + split: groups are the population's agents (each
+// its own weights and activations, one launch for all of them)
+template <int BM, int BN, class Ops>
+__global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, int chunk, int zsub) {
+    static_assert((BM / 32) * (BN / 32) == NT / 64 && NT % BN == 0, "4 waves of 32x32");
+    constexpr int NA = BM * BK / NT, NB = BK * BN / NT;
+    const int split = (int)blockIdx.z % zsub;
+    const Ops ops = ops_g.at((int)blockIdx.z / zsub);
     if (chunk > 0) {
-        k0 += (int)blockIdx.z * chunk;
+        k0 += split * chunk;
         k1 = k0 + chunk < k1 ? k0 + chunk : k1;
     }
     if (k0 >= k1) k1 = k0;  // empty split: stores zeros
-    __shared__ float As[2][BK][LDP];  // As[k][m]
-    __shared__ float Bs[2][BK][LDP];  // Bs[k][n]
+    __shared__ Smem<BM, BN> sm;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int m_blk = blockIdx.y * BM, n_blk = blockIdx.x * BN;
-    // staging: thread t gathers A(m = t / 4 ... ) and B for one K-step: 4 values each
-    float ra[4], rb[4];
-    auto gather = [&](int kb) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int e = tid + i * NT;       // 0 .. 1023
-            const int am = e / BK, ak = e % BK;  // A: 64 rows x 16 k
-            ra[i] = kb + ak < k1 ? ops.a(m_blk + am, kb + ak) : 0.f;  // never past this split's K range
-            const int bk = e / BN, bn = e % BN;  // B: 16 k x 64 cols (consecutive n: coalesced)
-            rb[i] = kb + bk < k1 ? ops.b(kb + bk, n_blk + bn) : 0.f;
-        }
-    };
+    typename Ops::Ctx ctx;
+    ops.setup(ctx, sm, tid % BN, n_blk + tid % BN, tid);
+    float ra[NA], rb[NB];
     auto stash = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int e = tid + i * NT;
-            As[buf][e % BK][e / BK] = ra[i];
-            Bs[buf][e / BN][e % BN] = rb[i];
-        }
+        for (int i = 0; i < NA; ++i) sm.As[buf][tid % BK][tid / BK + i * (NT / BK)] = ra[i];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) sm.Bs[buf][tid / BN + i * (NT / BN)][tid % BN] = rb[i];
     };
     f4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;  // this wave's 32x32 sub-tile
+    const int wm = (wave % (BM / 32)) * 32, wn = (wave / (BM / 32)) * 32;  // this wave's 32x32 sub-tile
     const int r = lane & 15, q = lane >> 4;
-    int buf = 0;
-    if (k0 < k1) {
-        gather(k0);
+    for (int kc = k0; kc < k1; kc += kTab) {
+        const int kce = kc + kTab < k1 ? kc + kTab : k1;
+        __syncthreads();  // previous chunk's tables and operands consumed
+        ops.build(sm, kc, kce, tid);
+        __syncthreads();
+        int buf = 0;
+        ops.template gather<NA, NB, BN>(ctx, sm, m_blk, kc, kc, kce, tid, ra, rb);
         stash(0);
-    }
-    __syncthreads();
-    for (int kb = k0; kb < k1; kb += BK) {
-        const bool more = kb + BK < k1;
-        if (more) gather(kb + BK);  // next step's operands in flight during the MFMAs
+        __syncthreads();
+        for (int kb = kc; kb < kce; kb += BK) {
+            const bool more = kb + BK < kce;
+            if (more) ops.template gather<NA, NB, BN>(ctx, sm, m_blk, kc, kb + BK, kce, tid, ra, rb);
 #pragma unroll
-        for (int kk = 0; kk < BK; kk += 4) {
-            const float a0 = As[buf][kk + q][wm + r], a1 = As[buf][kk + q][wm + 16 + r];
-            const float b0 = Bs[buf][kk + q][wn + r], b1 = Bs[buf][kk + q][wn + 16 + r];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
-        }
-        if (more) {
-            stash(buf ^ 1);
-            __syncthreads();
-            buf ^= 1;
+            for (int kk = 0; kk < BK; kk += 4) {
+                const float a0 = sm.As[buf][kk + q][wm + r], a1 = sm.As[buf][kk + q][wm + 16 + r];
+                const float b0 = sm.Bs[buf][kk + q][wn + r], b1 = sm.Bs[buf][kk + q][wn + 16 + r];
+                acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+            }
+            if (more) {
+                stash(buf ^ 1);
+                __syncthreads();
+                buf ^= 1;
+            }
         }
     }
     // C layout: lane holds rows 4q + i, column r of each 16x16 tile
@@ -198,16 +348,39 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops, int k0, int k1, int 
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                ops.store(m_blk + wm + 16 * i + 4 * q + e, n_blk + wn + 16 * j + r, acc[i][j][e], (int)blockIdx.z);
+                ops.store(m_blk + wm + 16 * i + 4 * q + e, n_blk + wn + 16 * j + r, acc[i][j][e], split);
 }
 
-// fixed-order sum of the wgrad split partials: dW (+)= sum_z part[z], db (+)= last column
-__global__ void wgrad_reduce_kernel(const float *__restrict__ part, int splits, int M, int N, float *__restrict__ dw,
-                                    float *__restrict__ db, int accumulate) {
+// fixed-order sum of the wgrad split partials, in two parallel stages (a
+// single pass had one thread walk every split of its element: a long chain of
+// dependent-latency loads over few threads):
+//   stage 1: group g of kRedG consecutive splits -> part[g * kRedG] (in place)
+//   stage 2: dW (+)= sum_g part[g * kRedG], db (+)= the last column
+constexpr int kRedG = 16;
+__global__ void wgrad_reduce1_kernel(float *__restrict__ part, int splits, int MN) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int z0 = (int)blockIdx.y * kRedG;
+    if (i >= MN) return;
+    part += (size_t)blockIdx.z * splits * MN;
+    const int nz = splits - z0 < kRedG ? splits - z0 : kRedG;
+    float v[kRedG];
+#pragma unroll
+    for (int z = 0; z < kRedG; ++z) v[z] = z < nz ? part[(size_t)(z0 + z) * MN + i] : 0.f;
+    float t = 0.f;
+#pragma unroll
+    for (int z = 0; z < kRedG; ++z) t += v[z];
+    part[(size_t)z0 * MN + i] = t;
+}
+__global__ void wgrad_reduce2_kernel(const float *__restrict__ part, int splits, int groups, int M, int N,
+                                     float *__restrict__ dw, float *__restrict__ db, int accumulate) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= M * N) return;
+    const size_t grp = blockIdx.y;  // population group
+    part += grp * splits * M * N;
+    dw += grp * M * (N - 1);
+    if (db) db += grp * M;
     float v = 0.f;
-    for (int z = 0; z < splits; ++z) v += part[(size_t)z * M * N + i];
+    for (int g = 0; g < groups; ++g) v += part[(size_t)g * kRedG * M * N + i];
     const int m = i / N, n = i % N;
     if (n < N - 1) {
         float *d = dw + (size_t)m * (N - 1) + n;
@@ -215,6 +388,31 @@ __global__ void wgrad_reduce_kernel(const float *__restrict__ part, int splits, 
     } else if (db) {
         db[m] = accumulate ? db[m] + v : v;
     }
+}
+
+// a 32 x 128 tile for GEMMs with at most 32 rows (32-channel layers), else 64 x 64
+template <class Ops>
+static void launch(const Ops &o, int M, int N, int k0, int k1, int chunk, int splits, int groups, hipStream_t st) {
+    const unsigned z = (unsigned)(splits * groups);
+    if (M <= 32) {
+        dim3 grid((unsigned)ceil_div(N, 128), (unsigned)ceil_div(M, 32), z);
+        igemm_kernel<32, 128><<<grid, NT, 0, st>>>(o, k0, k1, chunk, splits);
+    } else {
+        dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(M, 64), z);
+        igemm_kernel<64, 64><<<grid, NT, 0, st>>>(o, k0, k1, chunk, splits);
+    }
+}
+
+// wgrad split-K plan: enough (group, tile, split) workgroups to fill 256 CUs
+// several times over, each split a multiple of BK and at least 64 reduction
+// steps long
+static void wgrad_plan(const Shape &s, int groups, int &splits, int &chunk) {
+    const int M = s.Cout, N = s.Cin * s.KH * s.KW + 1, P = s.B * s.OH * s.OW;
+    const int tiles = (M <= 32 ? (int)ceil_div(N, 128) : (int)(ceil_div(N, 64) * ceil_div(M, 64))) * groups;
+    int want = (int)ceil_div(1024, tiles);
+    chunk = (int)(ceil_div(ceil_div(P, want), BK) * BK);
+    if (chunk < 64) chunk = 64;
+    splits = (int)ceil_div(P, chunk);
 }
 
 }  // namespace conv
@@ -237,6 +435,8 @@ static int check_shape(const agx_conv2d_shape *sh, Shape &s, const char *who) {
     AGX_REQUIRE(s.B > 0 && s.Cin > 0 && s.H > 0 && s.W > 0 && s.Cout > 0 && s.KH > 0 && s.KW > 0 && s.S > 0 &&
                     s.KH <= s.H && s.KW <= s.W,
                 "%s: bad shape", who);
+    AGX_REQUIRE(s.KH <= kTapMax && s.KW <= kTapMax && s.Cout < 65536, "%s: kernel taps > %d or > 65535 channels",
+                who, kTapMax);
     s.OH = (s.H - s.KH) / s.S + 1;
     s.OW = (s.W - s.KW) / s.S + 1;
     AGX_REQUIRE((int64_t)s.B * s.Cout * s.OH * s.OW < (1ll << 31) && (int64_t)s.B * s.Cin * s.H * s.W < (1ll << 31),
@@ -244,63 +444,95 @@ static int check_shape(const agx_conv2d_shape *sh, Shape &s, const char *who) {
     return AGX_OK;
 }
 
-extern "C" int agx_conv2d_forward(const agx_conv2d_shape *shape, const void *x, int x_is_u8, float x_low,
-                                  float x_high, const float *w, const float *bias, int relu, float *y, void *stream) {
+extern "C" int agx_conv2d_forward_grouped(const agx_conv2d_shape *shape, int64_t groups, const void *x,
+                                          int64_t x_gstride, int x_is_u8, float x_low, float x_high, const float *w,
+                                          int64_t w_gstride, const float *bias, int64_t b_gstride, int relu, float *y,
+                                          int64_t y_gstride, void *stream) {
     Shape s;
     if (int rc = check_shape(shape, s, "agx_conv2d_forward")) return rc;
-    AGX_REQUIRE(x && w && y, "agx_conv2d_forward: null pointer");
+    AGX_REQUIRE(x && w && y && groups >= 1 && groups < 65536, "agx_conv2d_forward: null pointer or bad groups");
     AGX_REQUIRE(!x_is_u8 || x_high > x_low, "agx_conv2d_forward: u8 input needs high > low");
     const int M = s.Cout, N = s.B * s.OH * s.OW, K = s.Cin * s.KH * s.KW;
-    dim3 grid((unsigned)ceil_div(N, BN), (unsigned)ceil_div(M, BM));
     hipStream_t st = as_stream(stream);
     if (x_is_u8) {
-        FwdOps<true> o{w, x, bias, y, x_low, x_high - x_low, relu, s, M, N, K};
-        igemm_kernel<<<grid, NT, 0, st>>>(o, 0, K, 0);
+        FwdOps<true> o{w, x, bias, y, x_low, x_high - x_low, relu, s, M, N, K, x_gstride, w_gstride, b_gstride,
+                       y_gstride};
+        launch(o, M, N, 0, K, 0, 1, (int)groups, st);
     } else {
-        FwdOps<false> o{w, x, bias, y, 0.f, 1.f, relu, s, M, N, K};
-        igemm_kernel<<<grid, NT, 0, st>>>(o, 0, K, 0);
+        FwdOps<false> o{w, x, bias, y, 0.f, 1.f, relu, s, M, N, K, x_gstride, w_gstride, b_gstride, y_gstride};
+        launch(o, M, N, 0, K, 0, 1, (int)groups, st);
     }
     return check_launch("agx_conv2d_forward");
 }
 
-extern "C" size_t agx_conv2d_wgrad_workspace_bytes(const agx_conv2d_shape *shape) {
+extern "C" int agx_conv2d_forward(const agx_conv2d_shape *shape, const void *x, int x_is_u8, float x_low,
+                                  float x_high, const float *w, const float *bias, int relu, float *y, void *stream) {
+    return agx_conv2d_forward_grouped(shape, 1, x, 0, x_is_u8, x_low, x_high, w, 0, bias, 0, relu, y, 0, stream);
+}
+
+extern "C" size_t agx_conv2d_wgrad_workspace_bytes_grouped(const agx_conv2d_shape *shape, int64_t groups) {
     Shape s;
-    if (check_shape(shape, s, "agx_conv2d_wgrad_workspace_bytes")) return 0;
-    const int64_t P = (int64_t)s.B * s.OH * s.OW;
-    const int64_t splits = P / 4096 + 1;
-    return (size_t)(splits < 128 ? splits : 128) * s.Cout * (s.Cin * s.KH * s.KW + 1) * sizeof(float);
+    if (check_shape(shape, s, "agx_conv2d_wgrad_workspace_bytes") || groups < 1) return 0;
+    int splits = 1, chunk = 0;
+    wgrad_plan(s, (int)groups, splits, chunk);
+    return (size_t)groups * splits * s.Cout * (s.Cin * s.KH * s.KW + 1) * sizeof(float);
+}
+
+extern "C" size_t agx_conv2d_wgrad_workspace_bytes(const agx_conv2d_shape *shape) {
+    return agx_conv2d_wgrad_workspace_bytes_grouped(shape, 1);
+}
+
+extern "C" int agx_conv2d_backward_grouped(const agx_conv2d_shape *shape, int64_t groups, const void *x,
+                                           int64_t x_gstride, int x_is_u8, float x_low, float x_high, const float *w,
+                                           int64_t w_gstride, const float *y_act, const float *dy, int64_t y_gstride,
+                                           float *dx, float *dw, float *db, int accumulate, void *workspace,
+                                           void *stream) {
+    Shape s;
+    if (int rc = check_shape(shape, s, "agx_conv2d_backward")) return rc;
+    AGX_REQUIRE(x && w && dy && dw && workspace && groups >= 1 && groups < 65536,
+                "agx_conv2d_backward: null pointer or bad groups");
+    hipStream_t st = as_stream(stream);
+    const int G = (int)groups;
+    const int K = s.Cin * s.KH * s.KW;
+    const int P = s.B * s.OH * s.OW;
+    int splits = 1, chunk = 0;
+    wgrad_plan(s, G, splits, chunk);
+    float *part = static_cast<float *>(workspace);
+    const int M = s.Cout, N = K + 1;
+    const long long gp = (long long)splits * M * N;
+    if (x_is_u8) {
+        WgradOps<true> o{dy, y_act, x, x_low, x_high - x_low, part, s, M, N, P, x_gstride, y_gstride, gp};
+        launch(o, M, N, 0, P, chunk, splits, G, st);
+    } else {
+        WgradOps<false> o{dy, y_act, x, 0.f, 1.f, part, s, M, N, P, x_gstride, y_gstride, gp};
+        launch(o, M, N, 0, P, chunk, splits, G, st);
+    }
+    // dW / db of group g land densely at dw + g*Cout*K, db + g*Cout
+    const int rgroups = (int)ceil_div(splits, kRedG);
+    wgrad_reduce1_kernel<<<dim3((unsigned)ceil_div(M * N, 256), (unsigned)rgroups, (unsigned)G), 256, 0, st>>>(
+        part, splits, M * N);
+    wgrad_reduce2_kernel<<<dim3((unsigned)ceil_div(M * N, 256), (unsigned)G), 256, 0, st>>>(part, splits, rgroups, M,
+                                                                                          N, dw, db, accumulate);
+    if (int rc = check_launch("agx_conv2d_backward wgrad")) return rc;
+    if (dx) {
+        AGX_REQUIRE(!x_is_u8, "agx_conv2d_backward: no data gradient for a u8 input layer");
+        for (int ph = 0; ph < s.S; ++ph)
+            for (int pw = 0; pw < s.S; ++pw) {
+                const int Hp = (int)ceil_div(s.H - ph, s.S), Wp = (int)ceil_div(s.W - pw, s.S);
+                const int nA = (int)ceil_div(s.KH - ph, s.S), nB = (int)ceil_div(s.KW - pw, s.S);
+                if (Hp <= 0 || Wp <= 0) continue;
+                DgradOps o{w, dy, y_act, dx, s, s.Cin, s.B * Hp * Wp, s.Cout * (nA > 0 ? nA : 0) * (nB > 0 ? nB : 0),
+                           ph, pw, Hp, Wp, nA, nB, w_gstride, y_gstride, x_gstride};
+                launch(o, o.M, o.N, 0, o.K, 0, 1, G, st);  // K = 0 (no tap reaches this phase): zeros
+            }
+        if (int rc = check_launch("agx_conv2d_backward dgrad")) return rc;
+    }
+    return AGX_OK;
 }
 
 extern "C" int agx_conv2d_backward(const agx_conv2d_shape *shape, const void *x, int x_is_u8, float x_low,
                                    float x_high, const float *w, const float *y_act, const float *dy, float *dx,
                                    float *dw, float *db, int accumulate, void *workspace, void *stream) {
-    Shape s;
-    if (int rc = check_shape(shape, s, "agx_conv2d_backward")) return rc;
-    AGX_REQUIRE(x && w && dy && dw && workspace, "agx_conv2d_backward: null pointer");
-    hipStream_t st = as_stream(stream);
-    const int K = s.Cin * s.KH * s.KW;
-    const int P = s.B * s.OH * s.OW;
-    int splits = P / 4096 + 1;
-    if (splits > 128) splits = 128;
-    const int chunk = (int)(ceil_div(ceil_div(P, splits), BK) * BK);
-    float *part = static_cast<float *>(workspace);
-    const int M = s.Cout, N = K + 1;
-    dim3 grid((unsigned)ceil_div(N, BN), (unsigned)ceil_div(M, BM), (unsigned)splits);
-    if (x_is_u8) {
-        WgradOps<true> o{dy, y_act, x, x_low, x_high - x_low, part, s, M, N, P};
-        igemm_kernel<<<grid, NT, 0, st>>>(o, 0, P, chunk);
-    } else {
-        WgradOps<false> o{dy, y_act, x, 0.f, 1.f, part, s, M, N, P};
-        igemm_kernel<<<grid, NT, 0, st>>>(o, 0, P, chunk);
-    }
-    wgrad_reduce_kernel<<<(unsigned)ceil_div(M * N, 256), 256, 0, st>>>(part, splits, M, N, dw, db, accumulate);
-    if (int rc = check_launch("agx_conv2d_backward wgrad")) return rc;
-    if (dx) {
-        AGX_REQUIRE(!x_is_u8, "agx_conv2d_backward: no data gradient for a u8 input layer");
-        DgradOps o{w, dy, y_act, dx, s, s.Cin, s.B * s.H * s.W, s.Cout * s.KH * s.KW};
-        dim3 g2((unsigned)ceil_div(o.N, BN), (unsigned)ceil_div(o.M, BM));
-        igemm_kernel<<<g2, NT, 0, st>>>(o, 0, o.K, 0);
-        if (int rc = check_launch("agx_conv2d_backward dgrad")) return rc;
-    }
-    return AGX_OK;
+    return agx_conv2d_backward_grouped(shape, 1, x, 0, x_is_u8, x_low, x_high, w, 0, y_act, dy, 0, dx, dw, db,
+                                       accumulate, workspace, stream);
 }

@@ -90,6 +90,57 @@ class Conv2dFn(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
+class Conv2dGroupedFn(torch.autograd.Function):
+    """G independent convolutions of one shape in one launch (the population's
+    agents): x [G, B, C, H, W] (f32, or uint8 with ``norm``), w [G, Cout, C, k,
+    k] and b [G, Cout] whose groups may sit at any stride (views of rows of a
+    flat [P, n] parameter buffer); -> y [G, B, Cout, OH, OW], relu fused.
+    agx_conv2d_forward_grouped / agx_conv2d_backward_grouped."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride: int, relu: bool, norm):
+        if x.device.type != "cuda":
+            raise _lib.AgxError("Conv2dGroupedFn runs on the GPU (agx_conv2d_forward_grouped); no CPU fallback")
+        u8 = x.dtype == torch.uint8
+        if u8 and norm is None:
+            raise ValueError("uint8 input needs image_norm = (low, high)")
+        if not u8 and x.dtype != torch.float32:
+            raise TypeError(f"conv input must be float32 or uint8, got {x.dtype}")
+        G = x.shape[0]
+        x = x.contiguous()
+        if w.shape[0] != G or b.shape[0] != G or not w[0].is_contiguous() or b.stride(1) != 1:
+            raise ValueError("grouped conv: w [G, Cout, C, k, k] / b [G, Cout] with contiguous groups")
+        sh = _shape(x[0], w[0], stride)
+        OH = (sh.height - sh.kernel_h) // stride + 1
+        OW = (sh.width - sh.kernel_w) // stride + 1
+        y = torch.empty(G, x.shape[1], w.shape[1], OH, OW, dtype=torch.float32, device=x.device)
+        lo, hi = (float(norm[0]), float(norm[1])) if u8 else (0.0, 1.0)
+        _lib.call("agx_conv2d_forward_grouped", ctypes.byref(sh), G, x.data_ptr(), x[0].numel(), int(u8), lo, hi,
+                  w.data_ptr(), w.stride(0), b.data_ptr(), b.stride(0), int(relu), y.data_ptr(), y[0].numel(),
+                  _lib.stream())
+        ctx.save_for_backward(x, w, y if relu else None)
+        ctx.meta = (stride, relu, u8, lo, hi)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        stride, relu, u8, lo, hi = ctx.meta
+        G = x.shape[0]
+        sh = _shape(x[0], w[0], stride)
+        dy = dy.contiguous()
+        dw = torch.empty((G, *w.shape[1:]), dtype=torch.float32, device=w.device)
+        db = torch.empty(G, w.shape[1], dtype=torch.float32, device=w.device)
+        need_dx = ctx.needs_input_grad[0] and not u8
+        dx = torch.empty_like(x) if need_dx else None
+        nws = _lib.load().agx_conv2d_wgrad_workspace_bytes_grouped(ctypes.byref(sh), G)
+        ws = torch.empty(max(16, nws), dtype=torch.uint8, device=w.device)
+        _lib.call("agx_conv2d_backward_grouped", ctypes.byref(sh), G, x.data_ptr(), x[0].numel(), int(u8), lo, hi,
+                  w.data_ptr(), w.stride(0), _lib.ptr(y), dy.data_ptr(), dy[0].numel(), _lib.ptr(dx),
+                  dw.data_ptr(), db.data_ptr(), 0, ws.data_ptr(), _lib.stream())
+        return dx, dw, db, None, None, None
+
+
 class AgxConv2d(nn.Conv2d):
     """nn.Conv2d (same parameters / state dict) whose forward is Conv2dFn;
     ``fuse_relu`` folds the following ReLU into the kernel epilogue."""

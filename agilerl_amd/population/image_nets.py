@@ -18,13 +18,14 @@ of ppo.py:910-911 are [0, actor_end) (shared encoder + actor head) and
 [actor_end, n) (critic head), as for the MLP spec.
 
 Forward: the convolutions run on the HIP implicit-GEMM kernels
-(modules/cnn.py ``Conv2dFn``: f32 MFMA, ReLU fused in the epilogue; uint8
+(modules/cnn.py ``Conv2dGroupedFn``: f32 MFMA, ReLU fused in the epilogue; uint8
 frames are normalised to (x - low) / (high - low) inside the first layer's
-load, so the uint8 rollout SoA is read as is).  The convolutions are per
-agent (each agent has its own filters); the linear_output layer and the heads
-are batched over the population (one bmm each).  The flat buffer is split
-into per-parameter chunks once per forward (``split`` / ``unbind``: their
-backward is one cat / stack, not a full-size scatter per view).
+load, so the uint8 rollout SoA is read as is).  Every layer is ONE
+population-batched launch (agx_conv2d_*_grouped: each agent its own
+filters, read in place from its row of the flat buffer); the linear_output
+layer and the heads are batched over the population too (one bmm each).  The
+flat buffer is split into per-parameter chunks once per forward (``split``:
+its backward is one cat, not a full-size scatter per view).
 """
 
 from __future__ import annotations
@@ -35,7 +36,7 @@ from dataclasses import dataclass, field
 import torch
 import torch.nn.functional as F
 
-from ..modules.cnn import Conv2dFn
+from ..modules.cnn import Conv2dGroupedFn
 from .nets import ActorCriticSpec, Layer
 
 
@@ -158,33 +159,29 @@ class ImageActorCriticSpec:
         return x
 
     def features(self, flat: torch.Tensor, obs: torch.Tensor, parts=None, rows=None) -> torch.Tensor:
-        """Conv stack of every agent (or of ``rows``; the others read zeros)
-        -> flattened features [P, B, feat_dim]."""
+        """Conv stack of every agent -> flattened features [P, B, feat_dim]:
+        one population-batched launch per layer and direction
+        (agx_conv2d_*_grouped, each agent its own filters).  ``rows`` (the
+        agents a heterogeneous learner group updates) does not narrow it: the
+        other agents' outputs are computed and left unused."""
         P, B = obs.shape[0], obs.shape[1]
         parts = self._split(flat) if parts is None else parts
         x = obs.reshape(P, B, *self.obs_shape)
         u8 = x.dtype == torch.uint8
-        if not u8:
+        if u8 and self.image_norm is None:
+            x = x.float()
+            u8 = False
+        elif not u8:
             x = x.float()
             if self.image_norm is not None:  # preprocess_observation (algo_utils.py:1134-1183)
                 lo, hi = self.image_norm
                 x = (x - lo) / (hi - lo)
-        per_agent = [parts[self._index[c[5]]].unbind(0) for c in self.convs]
-        bias_agent = [parts[self._index[c[6]]].unbind(0) for c in self.convs]
-        outs = []
-        for p in range(P):
-            if rows is not None and p not in rows:
-                outs.append(torch.zeros(B, self.feat_dim, device=obs.device))
-                continue
-            h = x[p]
-            for j, (_name, ci, co, k, s, _wo, _bo) in enumerate(self.convs):
-                w = per_agent[j][p].view(co, ci, k, k)
-                norm = self.image_norm if (j == 0 and u8) else None
-                if j == 0 and u8 and norm is None:
-                    h = h.float()
-                h = Conv2dFn.apply(h, w, bias_agent[j][p], s, True, norm)
-            outs.append(h.reshape(B, self.feat_dim))
-        return torch.stack(outs)
+        h = x
+        for j, (_name, ci, co, k, s, wo, bo) in enumerate(self.convs):
+            w = parts[self._index[wo]].view(P, co, ci, k, k)
+            b = parts[self._index[bo]]
+            h = Conv2dGroupedFn.apply(h, w, b, s, True, self.image_norm if (j == 0 and u8) else None)
+        return h.reshape(P, B, self.feat_dim)
 
     def forward(self, flat: torch.Tensor, obs: torch.Tensor, rows=None):
         """obs [P, B, obs_dim] (uint8 frames or f32) -> (logits [P, B, A], value [P, B])."""

@@ -421,6 +421,23 @@ int agx_conv2d_backward(const agx_conv2d_shape *shape, const void *x, int x_is_u
                         const float *w, const float *y_act, const float *dy, float *dx, float *dw, float *db,
                         int accumulate, void *workspace, void *stream);
 
+/* Population-batched forms (no reference counterpart: the reference runs one
+ * agent's nn.Conv2d at a time): `groups` independent convolutions of one shape
+ * in ONE launch — group g reads x + g*x_gstride, w + g*w_gstride,
+ * bias + g*b_gstride and writes y + g*y_gstride (element strides; dy / y_act
+ * share y_gstride, dx shares x_gstride).  The weight / bias gradients of group
+ * g land densely at dw + g*Cout*Cin*KH*KW and db + g*Cout.  groups = 1 is the
+ * single-agent call above. */
+int agx_conv2d_forward_grouped(const agx_conv2d_shape *shape, int64_t groups, const void *x, int64_t x_gstride,
+                               int x_is_u8, float x_low, float x_high, const float *w, int64_t w_gstride,
+                               const float *bias, int64_t b_gstride, int relu, float *y, int64_t y_gstride,
+                               void *stream);
+size_t agx_conv2d_wgrad_workspace_bytes_grouped(const agx_conv2d_shape *shape, int64_t groups);
+int agx_conv2d_backward_grouped(const agx_conv2d_shape *shape, int64_t groups, const void *x, int64_t x_gstride,
+                                int x_is_u8, float x_low, float x_high, const float *w, int64_t w_gstride,
+                                const float *y_act, const float *dy, int64_t y_gstride, float *dx, float *dw,
+                                float *db, int accumulate, void *workspace, void *stream);
+
 /* ---- diagnostics ---------------------------------------------------------
  * out[i] = pow(x[i], y[i]) by the routine the PER leaves and IS weights use
  * (glibc's pow algorithm, bit-identical to the host libm); for parity tests. */

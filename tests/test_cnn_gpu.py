@@ -36,6 +36,8 @@ SHAPES = [
     (4, 32, 82, 82, 32, 3, 1),
     (1, 3, 17, 13, 5, 5, 3),
     (3, 7, 11, 11, 9, 2, 2),
+    (2, 72, 12, 12, 40, 5, 1),  # K = 1800: gather tables rebuilt per 1024-entry chunk
+    (2, 3, 14, 14, 6, 2, 3),    # k < stride: input phases no tap reaches (zero data gradient)
 ]
 
 
@@ -234,3 +236,36 @@ def test_config3_pong_rainbow_generation():
     assert not torch.all(leaves == leaves[0])  # priorities updated from the C51 losses
     assert all(a.steps[-1] == 128 for a in pop)
     assert any(not torch.equal(a, b) for a, b in zip(p0, pop[0].actor.parameters()))
+
+
+@pytest.mark.parametrize("shape", [SHAPES[0], SHAPES[1], SHAPES[2], SHAPES[5], SHAPES[8]])
+def test_grouped_conv_matches_per_group_torch(shape):
+    """agx_conv2d_*_grouped: G agents' convolutions in one launch, each agent's
+    filters read in place from its row of a flat [G, n] buffer (row stride
+    n > the filter size) == G separate fp64 convolutions."""
+    from agilerl_amd.modules.cnn import Conv2dGroupedFn
+
+    B, C, H, W, OC, k, s = shape
+    G = 3
+    g = torch.Generator().manual_seed(40 + SHAPES.index(shape))
+    nw = OC * C * k * k
+    flat = torch.randn(G, nw + OC + 7, generator=g) / (C * k * k) ** 0.5
+    x = torch.randn(G, B, C, H, W, generator=g)
+    flat_d = flat.to(DEV).requires_grad_(True)
+    w = flat_d[:, :nw].view(G, OC, C, k, k)
+    b = flat_d[:, nw:nw + OC]
+    xd = x.to(DEV).requires_grad_(True)
+    y = Conv2dGroupedFn.apply(xd, w, b, s, True, None)
+    gy = torch.randn(y.shape, generator=g)
+    y.backward(gy.to(DEV))
+    for p in range(G):
+        xr = x[p].double().requires_grad_(True)
+        wr = flat[p, :nw].view(OC, C, k, k).double().requires_grad_(True)
+        br = flat[p, nw:nw + OC].double().requires_grad_(True)
+        yr = torch.relu(F.conv2d(xr, wr, br, stride=s))
+        yr.backward(gy[p].double())
+        _close(y[p], yr, 2e-5, f"y[{p}]")
+        _close(xd.grad[p], xr.grad, 2e-5, f"dx[{p}]")
+        _close(flat_d.grad[p, :nw].view(OC, C, k, k), wr.grad, 1e-5, f"dw[{p}]")
+        _close(flat_d.grad[p, nw:nw + OC], br.grad, 1e-5, f"db[{p}]")
+    assert float(flat_d.grad[:, nw + OC:].abs().max()) == 0.0  # the rest of each row untouched
