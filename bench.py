@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--learner", choices=["fused", "torch"], default="fused")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (Atari PPO) side measurement")
     ap.add_argument("--roof-reps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--dist-selftest", action="store_true",
@@ -247,8 +248,11 @@ def load_pmc_traffic():
     rocprofv3 --pmc summary (tools/pmc_roofline.py), or None."""
     import glob
 
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")),
-                   key=lambda q: int(os.path.basename(q)[1:].split("_")[0]))
+    import re
+
+    paths = [q for q in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json"))
+             if re.fullmatch(r"r\d+_pmc_traffic\.json", os.path.basename(q))]  # not r2_c51_pmc_traffic.json
+    paths.sort(key=lambda q: int(os.path.basename(q)[1:].split("_")[0]))
     if not paths:
         return None
     with open(paths[-1]) as f:
@@ -561,6 +565,44 @@ def cpu_kernels_leg(seconds):
 
 
 # --------------------------------------------------------------------------- #
+def config5_leg(iters: int = 5):
+    """Config 5's per-GPU shard (Atari Breakout PPO, ppo_image.yaml network:
+    conv 32/64/128 k8/4/3 s4/2/1 -> latent 256 -> heads [256]): 4 agents x 64
+    envs of uint8 4x84x84 frames (32 agents / 2048 envs over 8 GPUs), learn_step
+    256 (T = 4), batch 128, 4 epochs; the population-grouped HIP convolutions
+    and the autograd learner.  A side measurement, not the headline line."""
+    from agilerl_amd.envs import StackedVecEnv, SyntheticAtariVecEnv
+    from agilerl_amd.population.runner import PopulationRunner
+    from agilerl_amd.utils import create_population
+
+    P, N = 4, 64
+    hp = {"BATCH_SIZE": 128, "LR": 1e-3, "LEARN_STEP": 256, "UPDATE_EPOCHS": 4}
+    net = {"latent_dim": 256,
+           "encoder_config": {"channel_size": [32, 64, 128], "kernel_size": [8, 4, 3], "stride_size": [4, 2, 1]},
+           "head_config": {"hidden_size": [256], "layer_norm": False}}
+    env = SyntheticAtariVecEnv(N, n_actions=4, seed=1)
+    agents = create_population("PPO", net, hp, env.single_observation_space, env.single_action_space,
+                               population_size=P, num_envs=N)
+    pop = agents[0].population
+    runner = PopulationRunner(pop, StackedVecEnv.from_shared(env, P))
+    for _ in range(2):
+        runner.iteration()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        runner.iteration()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"workload": "config 5 shard: PPO pop=4 x 64 envs, uint8 4x84x84 frames, T=4, batch 128, 4 epochs, "
+                       "CNN 32/64/128 -> 256, heads [256]",
+           "iterations": iters, "ms_per_iteration": round(dt / iters * 1e3, 2),
+           "env_steps_per_s": round(P * N * pop.T * iters / dt, 1),
+           "learner_updates_per_s": round(pop.n_updates() * iters / dt, 1)}
+    del runner, agents, pop
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -581,6 +623,7 @@ def main():
     if not args.no_roofline:
         roof = roofline_leg(args)
         kern = kernels_leg(roof["peak_measured"])
+    c5 = config5_leg() if (world == 1 and not args.no_config5) else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline_leg(args, res["S"])
@@ -618,6 +661,7 @@ def main():
                                "natively on the host while the GPU learns",
             "roofline": roof,
             "kernels": kern,
+            "config5": c5,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

@@ -32,3 +32,12 @@ def test_bench_spawns_two_ranks():
 def test_bench_single_rank_default():
     line = _run()
     assert line["n_gpus"] == 1
+
+
+def test_bench_reads_the_roofline_pmc_summary():
+    """bench.py's roofline.traffic comes from the newest profiles/rN_pmc_traffic.json
+    (not another kernel's rN_*_pmc_traffic.json)."""
+    import bench
+
+    pmc = bench.load_pmc_traffic()
+    assert pmc is not None and "gae_bytes" in pmc and "loss_bytes" in pmc, pmc
