@@ -33,6 +33,8 @@ Reference functions exercised (paths relative to /root/reference):
   * agilerl/hpo/mutation.py:311-453, 515-827      Mutations.mutation / rl_hyperparam_mutation /
                                                   parameter_mutation (+ RLParameter /
                                                   HyperparameterConfig, algorithms/core/registry.py)
+  * agilerl/modules/custom_components.py:38-131   NoisyLinear (init / noise draw order, forwards)
+  * agilerl/networks/custom_modules.py:127-162    DuelingDistributionalMLP.forward (q / probs / log)
 
 Usage:  python tests/golden/gen_golden.py  [--ref /root/reference]
 """
@@ -888,6 +890,57 @@ def gen_mutation(mut_mod, reg_mod, out: dict) -> None:
 
 
 # --------------------------------------------------------------------------- #
+def gen_dueling(ref: str, en, out: dict) -> None:
+    """NoisyLinear (agilerl/modules/custom_components.py:38-131) and the
+    DuelingDistributionalMLP head forward (agilerl/networks/custom_modules.py:
+    127-162) on noisy create_mlp streams (utils/evolvable_networks.py:527-644),
+    run by the reference's own code: seeded construction (parameter / noise
+    draw order), train / eval forwards, a re-drawn noise sample, and the head's
+    q / probability / log-probability outputs."""
+    cc = _load(ref, "agilerl.modules.custom_components", "agilerl/modules/custom_components.py")
+    for name in ("NoisyLinear", "GumbelSoftmax", "NewGELU"):  # evolvable_networks bound the stubs at import
+        if hasattr(cc, name):
+            setattr(en, name, getattr(cc, name))
+    _stub("agilerl.modules.mlp")
+    cm = _load(ref, "agilerl.networks.custom_modules", "agilerl/networks/custom_modules.py")
+    # NoisyLinear alone
+    torch.manual_seed(5)
+    nl = cc.NoisyLinear(12, 7, std_init=0.4)
+    init = {k: v.detach().clone().numpy() for k, v in nl.state_dict().items()}
+    x = torch.randn(9, 12)
+    y_train = nl(x).detach().numpy()
+    nl.eval()
+    y_eval = nl(x).detach().numpy()
+    nl.train()
+    torch.manual_seed(9)
+    nl.reset_noise()
+    out["noisy0"] = dict(x=x.numpy(), y_train=y_train, y_eval=y_eval, w_eps2=nl.weight_epsilon.numpy().copy(),
+                         b_eps2=nl.bias_epsilon.numpy().copy(),
+                         **{f"init.{k}": v for k, v in init.items()})
+    # the dueling distributional head (Rainbow's q_networks.py:208-230 head: noisy, LayerNorm, vanish)
+    for k, (L, H, A, Z, vmin, vmax, seed) in enumerate([(32, [16], 6, 51, -10.0, 10.0, 21),
+                                                         (20, [24, 24], 3, 11, -200.0, 200.0, 22)]):
+        torch.manual_seed(seed)
+        kw = dict(input_size=L, hidden_size=list(H), output_vanish=True, output_activation=None, noisy=True,
+                  init_layers=False, layer_norm=True, activation="ReLU", noise_std=0.5)
+        value = en.create_mlp(output_size=Z, name="value", **kw)
+        adv = en.create_mlp(output_size=A * Z, name="advantage", **kw)
+        head = object.__new__(cm.DuelingDistributionalMLP)
+        head.model, head.advantage_net = value, adv
+        head.num_atoms, head.num_actions = Z, A
+        head.support = torch.linspace(vmin, vmax, Z)
+        x = torch.randn(13, L)
+        fwd = cm.DuelingDistributionalMLP.forward
+        rec = dict(x=x.numpy(), support=head.support.numpy(), dims=np.array([L, A, Z], np.int64),
+                   hidden=np.array(H, np.int64),
+                   q=fwd(head, x).detach().numpy(), probs=fwd(head, x, q=False).detach().numpy(),
+                   logp=fwd(head, x, log=True).detach().numpy())
+        for pre, m in (("model.", value), ("advantage_net.", adv)):
+            for kk, v in m.state_dict().items():
+                rec[f"sd.{pre}{kk}"] = v.detach().clone().numpy()
+        out[f"dueling{k}"] = rec
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -928,6 +981,7 @@ def main() -> None:
     gen_nstep(rp, groups)
     gen_ma_replay(mar, groups)
     gen_maddpg(maddpg, groups)
+    gen_dueling(ref, en, groups)
 
     if args.only:
         groups = {k: v for k, v in groups.items() if k in set(args.only)}
