@@ -97,9 +97,6 @@ struct LearnPlan {
 };
 
 constexpr int rup(int x, int m) { return (x + m - 1) / m * m; }
-// Adam / norm ownership: thread t owns the float4 chunks t, t + kNT, ... of the
-// LDS parameter image; slot s is float (s & 3) of chunk (s >> 2)
-__host__ __device__ constexpr int slot_l(int t, int s) { return 4 * (t + kNT * (s >> 2)) + (s & 3); }
 
 constexpr LearnPlan make_plan(NetDims d) {
     LearnPlan pl{};
@@ -206,7 +203,8 @@ constexpr LearnPlan make_plan(NetDims d) {
     pl.l_stat = off; off += 5 * kNW;
     pl.lds_floats = off;
     if (pl.lds_floats * 4 > 160 * 1024) return pl;
-    pl.slab = rup(pl.param_end + 4, 64);  // + the loss / approx_kl chunk
+    // + the loss / approx_kl chunk + the partners' per-wave partial gradient norms
+    pl.slab = rup(pl.param_end + 4 + 2 * kNW * kMaxK, 64);
     // ---- dW tile groups
     int slot = 0;
     for (int g = 0; g < pl.ne + 3; ++g) {
@@ -573,7 +571,8 @@ struct LearnArgs {
     float *slabs;          // [P][2][K][slab] gradient hand-off (double-buffered)
     float *sums;           // [P][2][slab] reduce-scattered gradient sums (double-buffered)
     unsigned *cnt;         // [P] arrival counters, [P] timeout word, [P+1+p] second-barrier,
-                           // [2P+1+p] setup-barrier counters, [3P+1 + p*kMaxK + kk] XCC ids
+                           // [2P+1+p] setup-barrier counters, [3P+1 + p*kMaxK + kk] XCC ids,
+                           // [3P+1 + P*kMaxK + p] third-barrier (parameter hand-off) counters
                            // (zeroed per call)
     int debug_stall;       // test hook: partner 1 of agent 0 never arrives
     int write_through;     // 1: always sc1 stores (AGX_LEARN_WRITETHROUGH=1; tests the cross-XCD form)
@@ -593,7 +592,10 @@ constexpr unsigned kSpinMax = 1u << 23;  // ~ seconds of s_sleep polling: a miss
 // ---------------------------------------------------------------------------
 // learner
 // ---------------------------------------------------------------------------
-template <class C, int SB>
+// JN > 0: every partner owns at most JN float4 chunk rounds (kNT chunks each) —
+// with 8 partners one round, and the per-slot Adam / norm code is instantiated
+// for that round only (a smaller kernel body); JN = 0: any split (K = 1 owns all)
+template <class C, int SB, int JN = 0>
 __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     constexpr LearnPlan pl = C::plan;
@@ -611,14 +613,33 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     for (int i = tid; i < pl.lds_floats; i += kNT) sm[i] = 0.f;
     __syncthreads();
     load_params<C>(sm, gp, tid);
+    // Parameter ownership (Adam is distributed over the partners): partner kk
+    // owns the float4 chunks [oc0, oc1) of the LDS parameter image + loss chunk
+    // (n4s chunks split K ways); thread tid owns chunks oc0 + tid + kNT*j of it,
+    // i.e. slot i is float (i & 3) of chunk oc0 + tid + kNT*(i >> 2).  K == 1:
+    // every chunk, thread t owning t, t + kNT, ...
+    constexpr int n4 = pl.param_end / 4, n4s = n4 + 1;
+    const int oc0 = (int)((long long)n4s * kk / g.K), oc1 = (int)((long long)n4s * (kk + 1) / g.K);
+    const int pc1 = oc1 < n4 ? oc1 : n4;  // own parameter chunks [oc0, pc1)
+    constexpr int kUsed4 = JN > 0 ? JN : (n4 + kNT - 1) / kNT;  // owned chunk rounds per thread, at most
+    static_assert(pl.param_end % 4 == 0 && pl.slab >= pl.param_end + 4 + 2 * kNW * kMaxK, "sum slab layout");
+    static_assert(4 * kUsed4 <= kMaxPT, "owned slots");
+    auto own_c = [&](int j) { return oc0 + vtid() + kNT * j; };
+    // owned chunk rounds: a block-uniform trip count (1 with 8 partners), so the
+    // unrolled per-slot loops below skip the rounds no thread owns
+    const int jn_own = __builtin_amdgcn_readfirstlane((oc1 - oc0 + kNT - 1) / kNT);
     // Adam moments of the owned LDS parameter slots -> registers; group bits
     float am[kMaxPT], av[kMaxPT];
     unsigned gbits = 0, vbits = 0;
 #pragma unroll
     for (int i = 0; i < kMaxPT; ++i) {
-        const int l = slot_l(tid, i);
+        if (i >= 4 * kUsed4) {
+            am[i] = av[i] = 0.f;
+            continue;
+        }
+        const int c = own_c(i >> 2), l = 4 * c + (i & 3);
         int grp = 0;
-        const int f = l < pl.param_end ? lds_to_flat<C>(l, grp) : -1;
+        const int f = c < pc1 ? lds_to_flat<C>(l, grp) : -1;
         am[i] = f >= 0 ? gm[f] : 0.f;
         av[i] = f >= 0 ? gv[f] : 0.f;
         if (f >= 0) vbits |= 1u << i;
@@ -1208,6 +1229,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 AGX_IDS;
                 block_sum2(lmb, klmb, stat, 2, lane, wave);
             }
+            float gr[kMaxPT];  // summed gradients of the owned slots
             if (g.K > 1) {
                 // ---- P9b: exchange partial gradients with the agent's partners --------
                 // every gradient word went out as a write-through (sc1) store from the
@@ -1218,32 +1240,65 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     slab_put(pl.param_end + 1, klmb);
                 }
                 if (!partner_sync(g.cnt + p, (unsigned)(g.K * (upd + 1)), 64 + 11, 64 + 12)) return;
-                // ---- reduce-scatter: partner kk sums float4 chunks [c0, c1) of the
-                // parameter image (+ the chunk holding the loss / approx_kl words)
-                // over the K slabs in partner order and publishes them to the agent's
-                // sum slab (every partner then reads ONE slab: K x (1/K) + 1 slab
-                // reads per workgroup instead of K)
+                // ---- reduce-scatter: partner kk sums its own float4 chunks [oc0, oc1)
+                // of the parameter image (+ the chunk holding the loss / approx_kl
+                // words) over the K slabs in partner order; the sums stay in its
+                // registers (it alone runs Adam on them), only the loss chunk and the
+                // per-wave partial gradient norms go to the agent's sum slab
                 {
-                    constexpr int n4s = pl.param_end / 4 + 1;
-                    static_assert(pl.param_end % 4 == 0 && pl.slab >= 4 * n4s, "loss words chunk");
-                    const int c0 = (int)((long long)n4s * kk / g.K), c1 = (int)((long long)n4s * (kk + 1) / g.K);
                     const int tid = vtid();
                     // one buffer descriptor over the K consecutive slabs
                     const auto rs = __builtin_amdgcn_make_buffer_rsrc(
                         base, 0, __builtin_amdgcn_readfirstlane(g.K * pl.slab * 4), 0x00020000);
-                    for (int c = c0 + tid; c < c1; c += kNT) {
-                        f4 x[kMaxK];  // all K loads in flight at once
 #pragma unroll
-                        for (int q = 0; q < kMaxK; ++q)
-                            x[q] = q < g.K ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                       rs, (q * pl.slab + 4 * c) * 4, 0, 16))
-                                           : f4{0.f, 0.f, 0.f, 0.f};
-                        f4 t = x[0];  // partner order
+                    for (int j = 0; j < kUsed4; ++j) {
+                        const int c = oc0 + tid + kNT * j;
+                        f4 t = f4{0.f, 0.f, 0.f, 0.f};
+                        if (j >= jn_own) {  // uniform: no thread owns round j
 #pragma unroll
-                        for (int q = 1; q < kMaxK; ++q)
-                            if (q < g.K) t += x[q];
-                        if (local) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 0);
-                        else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 16);
+                            for (int cc = 0; cc < 4; ++cc) gr[4 * j + cc] = 0.f;
+                            continue;
+                        }
+                        if (c < oc1) {
+                            f4 x[kMaxK];  // all K loads in flight at once
+#pragma unroll
+                            for (int q = 0; q < kMaxK; ++q)
+                                x[q] = q < g.K ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                           rs, (q * pl.slab + 4 * c) * 4, 0, 16))
+                                               : f4{0.f, 0.f, 0.f, 0.f};
+                            t = x[0];  // partner order
+#pragma unroll
+                            for (int q = 1; q < kMaxK; ++q)
+                                if (q < g.K) t += x[q];
+                            if (c == n4) {  // the loss / approx_kl chunk: every partner reads it
+                                if (local) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 0);
+                                else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 16);
+                            }
+                        }
+#pragma unroll
+                        for (int cc = 0; cc < 4; ++cc) gr[4 * j + cc] = c < pc1 ? t[cc] : 0.f;
+                    }
+                    AGX_STAMP(64 + 3);
+                    // partial two-group squared norms of the owned (valid) slots, per wave
+                    float n0 = 0.f, n1 = 0.f;
+#pragma unroll
+                    for (int i = 0; i < 4 * kUsed4; ++i) {
+                        if ((i >> 2) >= jn_own) break;
+                        const bool valid = (vbits >> i) & 1u, crit = (gbits >> i) & 1u;
+                        gr[i] = valid ? gr[i] : 0.f;
+                        const float x2 = gr[i] * gr[i];
+                        n1 += crit ? x2 : 0.f;
+                        n0 += crit ? 0.f : x2;
+                    }
+                    const int lane = vlane(), wave = swave();
+                    const float r0 = row_sum(n0), r1 = row_sum(n1);
+                    const float w0 = readlane_f(r0, 0) + readlane_f(r0, 16) + readlane_f(r0, 32) + readlane_f(r0, 48);
+                    const float w1 = readlane_f(r1, 0) + readlane_f(r1, 16) + readlane_f(r1, 32) + readlane_f(r1, 48);
+                    if (lane < 2) {
+                        const float w = lane ? w1 : w0;
+                        const int o = (pl.param_end + 4 + (kk * kNW + wave) * 2 + lane) * 4;
+                        if (local) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, w), sum_rsrc, o, 0, 0);
+                        else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, w), sum_rsrc, o, 0, 16);
                     }
                 }
                 AGX_STAMP(64 + 13);
@@ -1261,60 +1316,57 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             // region need no bounds test (padding slots carry g = m = v = 0, so
             // Adam writes their value back unchanged); per-slot branches cost
             // exec-mask traffic and SGPR spills.
-            constexpr int n4 = pl.param_end / 4;
-            constexpr int kFull4 = n4 / kNT;               // chunks < param_end for every thread
-            constexpr int kUsed4 = (n4 + kNT - 1) / kNT;   // chunks that exist at all
-            float n0 = 0.f, n1 = 0.f;
-            float gr[kMaxPT];  // gradients stay in registers for the Adam pass
-            {
-                auto chunk_in = [&](int j) { return j < kFull4 || tid + kNT * j < n4; };
-                auto put = [&](int j, f4 x) {
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) gr[4 * j + c] = x[c];
-                };
-                if (direct) {
-                    // the summed gradient of the reduce-scatter, straight from L2 into the
-                    // owned chunks: every workgroup of the agent reads the same words ->
-                    // bit-identical parameters.  sc1 buffer loads (L1 bypassed): with every
-                    // store sc1 and drained before the ticket, no acquire fence is needed
-                    // (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores + sc1 loads)
-#pragma unroll
-                    for (int j = 0; j < kUsed4; ++j)
-                        put(j, chunk_in(j) ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                       sum_rsrc, (tid + kNT * j) * 16, 0, 16))
-                                           : f4{0.f, 0.f, 0.f, 0.f});
-                } else {
-                    const f4 *G4 = reinterpret_cast<const f4 *>(G);
-#pragma unroll
-                    for (int j = 0; j < kUsed4; ++j)
-                        put(j, chunk_in(j) ? G4[tid + kNT * j] : f4{0.f, 0.f, 0.f, 0.f});
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4 * kUsed4; ++i) {
-                const float x = gr[i];
-                const bool valid = (vbits >> i) & 1u, crit = (gbits >> i) & 1u;
-                gr[i] = valid ? x : 0.f;
-                const float x2 = gr[i] * gr[i];
-                n1 += crit ? x2 : 0.f;
-                n0 += crit ? 0.f : x2;
-            }
-            AGX_IDS;
-            // both group norms in one reduction round (fixed order)
-            {
-                const float r0 = row_sum(n0), r1 = row_sum(n1);
-                const float w0 = readlane_f(r0, 0) + readlane_f(r0, 16) + readlane_f(r0, 32) + readlane_f(r0, 48);
-                const float w1 = readlane_f(r1, 0) + readlane_f(r1, 16) + readlane_f(r1, 32) + readlane_f(r1, 48);
-                if (lane == 0) {
-                    stat[wave] = w0;
-                    stat[kNW + wave] = w1;
-                }
-            }
-            __syncthreads();
             float t0 = 0.f, t1 = 0.f;
-            for (int i = 0; i < kNW; ++i) {
-                t0 += stat[i];
-                t1 += stat[kNW + i];
+            if (!direct) {
+                const f4 *G4 = reinterpret_cast<const f4 *>(G);
+#pragma unroll
+                for (int j = 0; j < kUsed4; ++j) {
+                    const int c = own_c(j);
+                    const f4 x = c < pc1 ? G4[c] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int cc = 0; cc < 4; ++cc) gr[4 * j + cc] = x[cc];
+                }
+                float n0 = 0.f, n1 = 0.f;
+#pragma unroll
+                for (int i = 0; i < 4 * kUsed4; ++i) {
+                    const bool valid = (vbits >> i) & 1u, crit = (gbits >> i) & 1u;
+                    gr[i] = valid ? gr[i] : 0.f;
+                    const float x2 = gr[i] * gr[i];
+                    n1 += crit ? x2 : 0.f;
+                    n0 += crit ? 0.f : x2;
+                }
+                AGX_IDS;
+                // both group norms in one reduction round (fixed order)
+                {
+                    const float r0 = row_sum(n0), r1 = row_sum(n1);
+                    const float w0 = readlane_f(r0, 0) + readlane_f(r0, 16) + readlane_f(r0, 32) + readlane_f(r0, 48);
+                    const float w1 = readlane_f(r1, 0) + readlane_f(r1, 16) + readlane_f(r1, 32) + readlane_f(r1, 48);
+                    if (lane == 0) {
+                        stat[wave] = w0;
+                        stat[kNW + wave] = w1;
+                    }
+                }
+                __syncthreads();
+                for (int i = 0; i < kNW; ++i) {
+                    t0 += stat[i];
+                    t1 += stat[kNW + i];
+                }
+            } else {
+                // the K x kNW per-wave partials of both groups from the sum slab
+                // ([partner][wave][group]: group = index parity), summed in one
+                // fixed order by every wave of every partner -> identical clip
+                const int lane = vlane();
+                const int np = 2 * kNW * g.K;  // <= 128
+                const float v0 = lane < np ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                           sum_rsrc, (pl.param_end + 4 + lane) * 4, 0, 16))
+                                           : 0.f;
+                const float v1 = lane + 64 < np ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                                sum_rsrc, (pl.param_end + 68 + lane) * 4, 0, 16))
+                                                : 0.f;
+                const float v = v0 + v1;
+                const float x0 = row_sum((lane & 1) ? 0.f : v), x1 = row_sum((lane & 1) ? v : 0.f);
+                t0 = readlane_f(x0, 0) + readlane_f(x0, 16) + readlane_f(x0, 32) + readlane_f(x0, 48);
+                t1 = readlane_f(x1, 0) + readlane_f(x1, 16) + readlane_f(x1, 32) + readlane_f(x1, 48);
             }
             if (tid == 0) loss_total += lmb;
             kl_total += (double)klmb;
@@ -1331,16 +1383,19 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             const float bc2s = (float)sqrt(1.0 - pb2);
             const float step_size = lr_p / bc1;
             const float inv_bc2s = 1.f / bc2s;
-            // Adam on float4 chunks: LDS b128 reads/writes; the elementwise math on
-            // 4-vectors lowers to packed-f32 VALU ops (v_pk_mul/add_f32, 2 lanes/op)
+            // Adam on the owned float4 chunks: LDS b128 reads/writes; the elementwise
+            // math on 4-vectors lowers to packed-f32 VALU ops (v_pk_mul/add_f32)
             f4 pv[kMaxPT / 4];  // all parameter reads issued before any write
             f4 *sm4 = reinterpret_cast<f4 *>(sm);
 #pragma unroll
-            for (int j = 0; j < kUsed4; ++j)
-                pv[j] = (j < kFull4 || tid + kNT * j < n4) ? sm4[tid + kNT * j] : f4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < kUsed4; ++j) {
+                const int c = own_c(j);
+                pv[j] = (j < jn_own && c < pc1) ? sm4[c] : f4{0.f, 0.f, 0.f, 0.f};
+            }
             const float ob1 = 1.f - g.b1, ob2 = 1.f - g.b2;
 #pragma unroll
             for (int j = 0; j < kUsed4; ++j) {
+                if (j >= jn_own) break;  // uniform
                 f4 gc, m, v;
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
@@ -1367,7 +1422,44 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     am[4 * j + c] = m[c];
                     av[4 * j + c] = v[c];
                 }
-                if (j < kFull4 || tid + kNT * j < n4) sm4[tid + kNT * j] = nv;
+                const int c = own_c(j);
+                if (c < pc1) {
+                    sm4[c] = nv;
+                    // partners: the updated chunk goes to this workgroup's slab (its
+                    // gradient words there were consumed before the second barrier)
+                    if (direct) {
+                        if (local) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, nv), slab_rsrc, c * 16, 0, 0);
+                        else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, nv), slab_rsrc, c * 16, 0, 16);
+                    }
+                }
+            }
+            if (direct) {
+                // ---- P11: every partner's updated chunks -> this LDS image --------
+                if (!partner_sync(g.cnt + 3 * g.P + 1 + (size_t)g.P * kMaxK + p, (unsigned)(g.K * (upd + 1)), 64 + 0,
+                                  64 + 1))
+                    return;
+                const int tid = vtid();
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                    base, 0, __builtin_amdgcn_readfirstlane(g.K * pl.slab * 4), 0x00020000);
+                // round r: chunk qc0 + tid + kNT*r of every other partner q, all loads in flight
+                const int span = (n4s + g.K - 1) / g.K + 1;
+                for (int r0 = 0; r0 < span; r0 += kNT) {
+                    f4 x[kMaxK];
+                    int cq[kMaxK];
+#pragma unroll
+                    for (int q = 0; q < kMaxK; ++q) {
+                        const int qc0 = (int)((long long)n4s * q / g.K), qc1 = (int)((long long)n4s * (q + 1) / g.K);
+                        const int c = qc0 + tid + r0;
+                        cq[q] = (q < g.K && q != kk && c < qc1 && c < n4) ? c : -1;
+                        x[q] = cq[q] >= 0 ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                        rs, (q * pl.slab + 4 * c) * 4, 0, 16))
+                                          : f4{0.f, 0.f, 0.f, 0.f};
+                    }
+#pragma unroll
+                    for (int q = 0; q < kMaxK; ++q)
+                        if (cq[q] >= 0) sm4[cq[q]] = x[q];
+                }
+                AGX_STAMP(64 + 2);
             }
             __syncthreads();
             AGX_STAMP(64 + 10);
@@ -1378,12 +1470,12 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
         if (g.target_kl > 0.0 && kl_total / (double)n_done > g.target_kl) break;
     }  // epochs
 
-    // ---- write parameters and moments back (partners hold identical copies; each
-    // writes the chunks j % K == kk) ------------------------------------------------
+    // ---- write parameters and moments back (partners hold identical parameter
+    // images; each writes its own chunks, whose moments it holds) -------------------
 #pragma unroll
-    for (int i = 0; i < kMaxPT; ++i) {
-        const int l = slot_l(tid, i);
-        if (((vbits >> i) & 1u) && (g.K == 1 || (i >> 2) % g.K == kk)) {
+    for (int i = 0; i < 4 * kUsed4; ++i) {
+        const int l = 4 * own_c(i >> 2) + (i & 3);
+        if ((vbits >> i) & 1u) {
             int grp;
             const int f = lds_to_flat<C>(l, grp);
             gp[f] = sm[l];
@@ -1719,13 +1811,19 @@ template <class C>
 static void launch_learn(const LearnArgs &a, int nblocks, size_t lds, hipStream_t s, int sb) {
     static bool attr = false;
     if (!attr) {
+        (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 16, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
         (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 32>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr = true;
     }
-    if (sb == 16) ppo_learn_kernel<C, 16><<<(unsigned)nblocks, kNT, lds, s>>>(a);
+    // one owned chunk round per thread when the K-way split leaves <= kNT chunks per partner
+    constexpr int n4s = C::plan.param_end / 4 + 1;
+    const bool one_round = (n4s + a.K - 1) / a.K + 1 <= kNT;
+    if (sb == 16 && one_round) ppo_learn_kernel<C, 16, 1><<<(unsigned)nblocks, kNT, lds, s>>>(a);
+    else if (sb == 16) ppo_learn_kernel<C, 16><<<(unsigned)nblocks, kNT, lds, s>>>(a);
     else ppo_learn_kernel<C, 32><<<(unsigned)nblocks, kNT, lds, s>>>(a);
 }
 template <class C>
@@ -1845,7 +1943,7 @@ static LearnWs learn_ws(const LearnPlan &pl, int64_t P, int64_t S, int64_t epoch
     const size_t per = (size_t)epochs * P * S;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     w.cnt = 0;
-    w.gobs = up(((size_t)(3 + kMaxK) * P + 1) * 4);  // barrier counters, timeout word, XCC ids
+    w.gobs = up(((size_t)(4 + kMaxK) * P + 1) * 4);  // barrier counters, timeout word, XCC ids
     w.gact = w.gobs + up(per * pl.D * 4);
     w.gmask = w.gact + up(per * 4);
     w.grow = w.gmask + up(per * 4);

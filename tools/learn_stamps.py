@@ -45,7 +45,14 @@ for sb in range(4):
     seg = [row[i + 1] - row[i] for i in range(7)]
     print(f"sb{sb}: " + "  ".join(f"{n}={c}" for n, c in zip(names, seg)) + f"  total={row[7] - row[0]}")
 last = max(v for v in st[:64] if v)
-if st[64 + 15]:  # partners: reduce-scatter exchange (two barriers)
+if st[64 + 1]:  # partners: reduce-scatter + distributed Adam (three barriers)
+    print("dump", st[64 + 9] - last, "| publish", st[64 + 11] - st[64 + 9], "wait", st[64 + 12] - st[64 + 11],
+          "| RS loads+sum", st[64 + 3] - st[64 + 12], "norm partials", st[64 + 13] - st[64 + 3],
+          "| B2 drain + ticket", st[64 + 8] - st[64 + 13], "wait", st[64 + 15] - st[64 + 8],
+          "| norm read", st[64 + 14] - st[64 + 15], "adam + publish + B3 drain/ticket", st[64 + 0] - st[64 + 14],
+          "B3 wait", st[64 + 1] - st[64 + 0], "param read", st[64 + 2] - st[64 + 1],
+          "sync", st[64 + 10] - st[64 + 2], "| minibatch total cycles", st[64 + 10] - st[0])
+elif st[64 + 15]:  # partners: reduce-scatter exchange (two barriers)
     print("dump", st[64 + 9] - last, "| publish", st[64 + 11] - st[64 + 9], "wait", st[64 + 12] - st[64 + 11],
           "reduce-scatter", st[64 + 13] - st[64 + 12], "| barrier 2 drain + ticket", st[64 + 8] - st[64 + 13],
           "wait", st[64 + 15] - st[64 + 8], "| sum read + norm", st[64 + 14] - st[64 + 15],
