@@ -352,9 +352,13 @@ def kernels_leg(peak_meas):
     u = torch.rand(1 << 20, device=dev, generator=g)
     t = _time(lambda: K.per_sample(st, mt, cap, u, size=max_size, beta=0.4, weights=True))
     nb = (8 * 20 + 4 + 8 + 8 + 4) * u.numel()  # walk + uniform + index + leaf + weight
+    # the 16 MiB sum tree is re-walked 2^20 times and stays cache resident (LDS
+    # top levels, L2 / Infinity Cache): the walk's algorithmic bytes are not HBM
+    # traffic, so no HBM fraction is claimed for it
     out["per_sample"] = dict(unit_bytes=nb // u.numel(), units=u.numel(), ms=round(t * 1e3, 4),
-                             gbs=round(nb / t / 1e9, 1), frac_of_measured=round(nb / t / 1e9 / peak_meas, 4),
-                             bound="latency (dependent 20-level walk)")
+                             samples_per_s=round(u.numel() / t, 1), walk_gbs=round(nb / t / 1e9, 1),
+                             frac_of_measured=None,
+                             bound="latency (dependent 20-level walk over a cache-resident 16 MiB tree)")
     idx = torch.randint(0, max_size, (1 << 16,), device=dev, generator=g)
     p2 = torch.rand(1 << 16, device=dev, generator=g)
     t = _time(lambda: K.per_update(st, mt, cap, max_size, idx, p2, 0.6, maxp, workspace=ws))
