@@ -39,6 +39,39 @@ class QNetwork(EvolvableNetwork):
         return self.head_net(self.extract_features(obs))
 
 
+class DuelingHeadFn(torch.autograd.Function):
+    """(value [B, Z], advantage [B, A*Z]) -> the head output of ``mode``
+    (0: q [B, A], 1: clamped probabilities [B, A, Z], 2: log-probabilities
+    [B, A, Z]) on agx_dueling_head_forward / _backward (csrc/heads.hip)."""
+
+    @staticmethod
+    def forward(ctx, value, adv, support, A: int, Z: int, mode: int):
+        from .. import _lib
+
+        value, adv = value.contiguous(), adv.contiguous()
+        B = value.shape[0]
+        sup = support.to(device=value.device, dtype=torch.float32).contiguous() if mode == 0 else None
+        shape = (B, A) if mode == 0 else (B, A, Z)
+        out = torch.empty(shape, dtype=torch.float32, device=value.device)
+        _lib.call("agx_dueling_head_forward", value.data_ptr(), adv.data_ptr(), _lib.ptr(sup), B, A, Z, mode,
+                  out.data_ptr(), _lib.stream())
+        ctx.save_for_backward(value, adv, sup if sup is not None else value.new_empty(0))
+        ctx.meta = (A, Z, mode)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _lib
+
+        value, adv, sup = ctx.saved_tensors
+        A, Z, mode = ctx.meta
+        g = g.contiguous()
+        dv, da = torch.empty_like(value), torch.empty_like(adv)
+        _lib.call("agx_dueling_head_backward", value.data_ptr(), adv.data_ptr(), _lib.ptr(sup if mode == 0 else None),
+                  g.data_ptr(), value.shape[0], A, Z, mode, dv.data_ptr(), da.data_ptr(), _lib.stream())
+        return dv, da, None, None, None, None
+
+
 class DuelingDistributionalMLP(EvolvableMLP):
     """value stream = self.model (name "value"), advantage stream =
     self.advantage_net (name "advantage"); x = V + A - mean_a A; log-softmax
@@ -73,6 +106,10 @@ class DuelingDistributionalMLP(EvolvableMLP):
     def forward(self, x: torch.Tensor, q: bool = True, log: bool = False) -> torch.Tensor:
         value = self.model(x)
         advantage = self.advantage_net(x)
+        if value.is_cuda and self.num_atoms <= 64 and value.dtype == torch.float32:
+            # the combine, softmax, clamp and support dot in one HIP launch (csrc/heads.hip)
+            mode = 2 if log else (0 if q else 1)
+            return DuelingHeadFn.apply(value, advantage, self.support, self.num_actions, self.num_atoms, mode)
         b = value.size(0)
         x = value.view(b, 1, self.num_atoms) + advantage.view(b, self.num_actions, self.num_atoms)
         x = x - advantage.view(b, self.num_actions, self.num_atoms).mean(1, keepdim=True)

@@ -438,6 +438,20 @@ int agx_conv2d_backward_grouped(const agx_conv2d_shape *shape, int64_t groups, c
                                 const float *y_act, const float *dy, int64_t y_gstride, float *dx, float *dw,
                                 float *db, int accumulate, void *workspace, void *stream);
 
+/* ---- Rainbow dueling distributional head ------------------------------------
+ * DuelingDistributionalMLP.forward (agilerl/networks/custom_modules.py:127-162)
+ * after its value [B][Z] and advantage [B][A][Z] streams:
+ * x = (v + adv) - mean_a adv; mode 2 (log=True) out = log_softmax_z(x)
+ * [B][A][Z]; mode 1 (q=False) out = clamp(softmax_z(x), min=1e-3) [B][A][Z];
+ * mode 0 (q=True) out[b][a] = sum_z clamp(softmax_z(x), 1e-3) * support[z].
+ * 1 <= Z <= 64.  The backward maps dL/d(out) of the same mode to
+ * dL/d(value) [B][Z] and dL/d(advantage) [B][A][Z]. */
+int agx_dueling_head_forward(const float *value, const float *advantage, const float *support, int64_t B, int64_t A,
+                             int64_t Z, int mode, float *out, void *stream);
+int agx_dueling_head_backward(const float *value, const float *advantage, const float *support,
+                              const float *grad_out, int64_t B, int64_t A, int64_t Z, int mode, float *grad_value,
+                              float *grad_advantage, void *stream);
+
 /* ---- diagnostics ---------------------------------------------------------
  * out[i] = pow(x[i], y[i]) by the routine the PER leaves and IS weights use
  * (glibc's pow algorithm, bit-identical to the host libm); for parity tests. */

@@ -2,7 +2,10 @@
 fixtures the reference's own code produced (tests/golden/gen_golden.py
 gen_dueling: agilerl/modules/custom_components.py:38-131,
 agilerl/networks/custom_modules.py:127-162 on create_mlp streams).  CPU, the
-same torch ops: bit-exact."""
+same torch ops: bit-exact in the build container; torch's CPU normal draws and
+GEMMs take ISA-specific vector paths (a host with other SIMD units can differ
+in the last bit), so draws-derived tensors and outputs are compared within
+1e-6 relative and the uniform / constant initialisations exactly."""
 
 import numpy as np
 import pytest
@@ -16,16 +19,26 @@ def test_noisy_linear_matches_reference(golden):
     torch.manual_seed(5)  # the reference's draw order: weight_mu, bias_mu uniforms, then eps_in, eps_out normals
     nl = NoisyLinear(12, 7, std_init=0.4)
     for k, v in nl.state_dict().items():
-        assert np.array_equal(v.numpy(), g[f"init.{k}"]), k
+        if "epsilon" in k:  # normal draws
+            _near(v.numpy(), g[f"init.{k}"], k)
+        else:
+            assert np.array_equal(v.numpy(), g[f"init.{k}"]), k
     x = torch.from_numpy(g["x"])
-    assert np.array_equal(nl(x).detach().numpy(), g["y_train"])
+    _near(nl(x).detach().numpy(), g["y_train"], "train forward")
     nl.eval()
-    assert np.array_equal(nl(x).detach().numpy(), g["y_eval"])
+    _near(nl(x).detach().numpy(), g["y_eval"], "eval forward")
     nl.train()
     torch.manual_seed(9)
     nl.reset_noise()
-    assert np.array_equal(nl.weight_epsilon.numpy(), g["w_eps2"])
-    assert np.array_equal(nl.bias_epsilon.numpy(), g["b_eps2"])
+    _near(nl.weight_epsilon.numpy(), g["w_eps2"], "weight_epsilon")
+    _near(nl.bias_epsilon.numpy(), g["b_eps2"], "bias_epsilon")
+
+
+def _near(a, b, what, rtol=1e-6, scale=None):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    err = float(np.abs(a - b).max())
+    scale = float(np.abs(b).max()) if scale is None else scale
+    assert err <= rtol * max(1e-6, scale), (what, err)
 
 
 @pytest.mark.parametrize("case", ["dueling0", "dueling1"])
@@ -43,8 +56,71 @@ def test_dueling_distributional_head_matches_reference(golden, case):
     head.load_state_dict(sd)
     x = torch.from_numpy(g["x"])
     with torch.no_grad():
-        assert np.array_equal(head(x).numpy(), g["q"])
-        assert np.array_equal(head(x, q=False).numpy(), g["probs"])
-        assert np.array_equal(head(x, log=True).numpy(), g["logp"])
+        # q = sum_z p_z z: rounding scales with the support (|z| up to 200), not with q
+        _near(head(x).numpy(), g["q"], "q", scale=float(np.abs(g["support"]).max()))
+        _near(head(x, q=False).numpy(), g["probs"], "probs")
+        _near(head(x, log=True).numpy(), g["logp"], "logp")
     # the clamp(min=1e-3) is applied after the softmax and not renormalised (custom_modules.py:158)
     assert g["probs"].min() >= 1e-3
+
+
+def _torch_head(value, adv, support, A, Z, mode):
+    """The reference's combine (custom_modules.py:145-162) in plain torch ops."""
+    b = value.size(0)
+    v = value.view(b, 1, Z)
+    a = adv.view(b, A, Z)
+    x = v + a - a.mean(1, keepdim=True)
+    if mode == 2:
+        return torch.log_softmax(x.view(-1, Z), dim=-1).view(-1, A, Z)
+    x = torch.softmax(x.view(-1, Z), dim=-1).view(-1, A, Z).clamp(min=1e-3)
+    return torch.sum(x * support, dim=2) if mode == 0 else x
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("A,Z,B", [(6, 51, 37), (18, 51, 256), (3, 11, 5), (4, 64, 9)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_dueling_head_kernel_matches_torch(A, Z, B, mode):
+    """agx_dueling_head_forward / _backward vs the reference's tensor ops
+    (fp32 within 2e-6 of scale; the exp / sum orders differ)."""
+    from agilerl_amd.networks.q_networks import DuelingHeadFn
+
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(A * 100 + Z + mode)
+    value = (torch.randn(B, Z, device=dev, generator=g) * 2).requires_grad_(True)
+    adv = (torch.randn(B, A * Z, device=dev, generator=g) * 2).requires_grad_(True)
+    support = torch.linspace(-10, 10, Z, device=dev)
+    out = DuelingHeadFn.apply(value, adv, support, A, Z, mode)
+    v2, a2 = value.detach().clone().requires_grad_(True), adv.detach().clone().requires_grad_(True)
+    ref = _torch_head(v2, a2, support, A, Z, mode)
+    assert out.shape == ref.shape
+    scale = float(ref.abs().max())
+    assert float((out - ref).abs().max()) <= 2e-6 * scale + 1e-7
+    w = torch.randn(ref.shape, device=dev, generator=g)
+    (out * w).sum().backward()
+    (ref * w).sum().backward()
+    for got, want in ((value.grad, v2.grad), (adv.grad, a2.grad)):
+        s = float(want.abs().max()) + 1e-12
+        assert float((got - want).abs().max()) <= 5e-6 * s, (float((got - want).abs().max()), s)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["dueling0", "dueling1"])
+def test_dueling_head_on_gpu_matches_reference_fixture(golden, case):
+    """The module on cuda (the HIP combine) against the reference-run outputs."""
+    from agilerl_amd.networks.q_networks import DuelingDistributionalMLP
+
+    g = golden(case)
+    L, A, Z = (int(v) for v in g["dims"])
+    dev = torch.device("cuda:0")
+    support = torch.from_numpy(g["support"]).to(dev)
+    head = DuelingDistributionalMLP(num_inputs=L, num_outputs=A, hidden_size=[int(h) for h in g["hidden"]],
+                                    num_atoms=Z, support=support, noisy=True, layer_norm=True, output_vanish=True,
+                                    init_layers=False, noise_std=0.5, device=dev)
+    head.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("sd.")})
+    x = torch.from_numpy(g["x"]).to(dev)
+    with torch.no_grad():
+        for out, key in ((head(x), "q"), (head(x, q=False), "probs"), (head(x, log=True), "logp")):
+            want = g[key]
+            err = float(np.abs(out.cpu().numpy() - want).max())
+            scale = float(np.abs(g["support"]).max()) if key == "q" else float(np.abs(want).max())
+            assert err <= 1e-5 * max(1.0, scale), (key, err)
