@@ -128,7 +128,9 @@ class Conv2dGroupedFn(torch.autograd.Function):
         stride, relu, u8, lo, hi = ctx.meta
         G = x.shape[0]
         sh = _shape(x[0], w[0], stride)
-        dy = dy.contiguous()
+        # dZ = dY * relu'(Y) once (one elementwise pass) instead of a second
+        # (mask) load per gathered element in both the wgrad and the dgrad GEMM
+        dy = (dy * (y > 0)).contiguous() if y is not None else dy.contiguous()
         dw = torch.empty((G, *w.shape[1:]), dtype=torch.float32, device=w.device)
         db = torch.empty(G, w.shape[1], dtype=torch.float32, device=w.device)
         need_dx = ctx.needs_input_grad[0] and not u8
@@ -136,7 +138,7 @@ class Conv2dGroupedFn(torch.autograd.Function):
         nws = _lib.load().agx_conv2d_wgrad_workspace_bytes_grouped(ctypes.byref(sh), G)
         ws = torch.empty(max(16, nws), dtype=torch.uint8, device=w.device)
         _lib.call("agx_conv2d_backward_grouped", ctypes.byref(sh), G, x.data_ptr(), x[0].numel(), int(u8), lo, hi,
-                  w.data_ptr(), w.stride(0), _lib.ptr(y), dy.data_ptr(), dy[0].numel(), _lib.ptr(dx),
+                  w.data_ptr(), w.stride(0), None, dy.data_ptr(), dy[0].numel(), _lib.ptr(dx),
                   dw.data_ptr(), db.data_ptr(), 0, ws.data_ptr(), _lib.stream())
         return dx, dw, db, None, None, None
 
