@@ -93,7 +93,7 @@ def test_dueling_head_kernel_matches_torch(A, Z, B, mode):
     v2, a2 = value.detach().clone().requires_grad_(True), adv.detach().clone().requires_grad_(True)
     ref = _torch_head(v2, a2, support, A, Z, mode)
     assert out.shape == ref.shape
-    scale = float(ref.abs().max())
+    scale = float(ref.detach().abs().max())
     assert float((out - ref).abs().max()) <= 2e-6 * scale + 1e-7
     w = torch.randn(ref.shape, device=dev, generator=g)
     (out * w).sum().backward()
