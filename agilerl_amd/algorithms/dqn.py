@@ -20,6 +20,7 @@ import torch
 
 from .. import kernels as K
 from . import checkpoint as C
+from .evolvable import EvolvableAgentMixin
 from ..networks import QNetwork, RainbowQNetwork
 from ..networks.base import image_norm_bounds, is_image_space, mlp_net_config
 
@@ -74,7 +75,7 @@ class _TDLoss(torch.autograd.Function):
         return (g_q * gl,) + (None,) * 7
 
 
-class DQN(C.TorchCheckpointMixin):
+class DQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
     algo = "DQN"
 
     def __init__(self, observation_space, action_space, index: int = 0, hp_config=None, net_config=None,
@@ -100,6 +101,7 @@ class DQN(C.TorchCheckpointMixin):
         self.actor_target.load_state_dict(self.actor.state_dict())
         _setup_image_input(self, normalize_images)
         self.optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr)
+        self._init_registry(hp_config)
         self.scores: list[float] = []
         self.fitness: list[float] = []
         self.steps: list[int] = [0]
@@ -154,6 +156,9 @@ class DQN(C.TorchCheckpointMixin):
         loss = self.update(obs, to(get("action")), to(get("reward")), next_obs, to(get("done")))
         self.soft_update()
         return float(loss.item())
+
+    def _fresh_optimizer(self, lr_name: str):
+        return torch.optim.Adam(self.actor.parameters(), lr=self.lr)
 
     def clone(self, index: int | None = None, wrap: bool = True):
         """Deep copy with a new index (EvolvableAlgorithm.clone, core/base.py)."""
@@ -225,7 +230,7 @@ class _C51Loss(torch.autograd.Function):
         return (grad,) + (None,) * 9
 
 
-class RainbowDQN(C.TorchCheckpointMixin):
+class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
     """Drop-in RainbowDQN (agilerl/algorithms/dqn_rainbow.py:77-501) with the
     C51 projection + loss in agx_c51_project_loss and Polyak in agx_polyak."""
 
@@ -263,6 +268,7 @@ class RainbowDQN(C.TorchCheckpointMixin):
         self.actor_target.load_state_dict(self.actor.state_dict())
         _setup_image_input(self, normalize_images)
         self.optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr)
+        self._init_registry(hp_config)
         self.scores: list[float] = []
         self.fitness: list[float] = []
         self.steps: list[int] = [0]
@@ -346,6 +352,9 @@ class RainbowDQN(C.TorchCheckpointMixin):
         if per:
             new_priorities = el.detach().cpu().numpy() + self.prior_eps
         return loss.item(), idxs, new_priorities
+
+    def _fresh_optimizer(self, lr_name: str):
+        return torch.optim.Adam(self.actor.parameters(), lr=self.lr)
 
     def clone(self, index: int | None = None, wrap: bool = True):
         """Deep copy with a new index (EvolvableAlgorithm.clone, core/base.py)."""

@@ -27,6 +27,7 @@ from ..envs import Dict as DictSpace
 from ..networks import ContinuousQNetwork, DeterministicActor
 from ..networks.base import as_config, mlp_net_config
 from . import checkpoint as C
+from .evolvable import EvolvableAgentMixin
 
 
 class _CriticLoss(torch.autograd.Function):
@@ -53,8 +54,12 @@ def _action_dim(space) -> int:
     return int(space.n) if hasattr(space, "n") else int(np.prod(space.shape))
 
 
-class MADDPG:
+class MADDPG(EvolvableAgentMixin):
     algo = "MADDPG"
+    # maddpg.py:424-444: the actors are the policy group (targets shared); one
+    # optimizer set per learning rate
+    _lr_optimizers = {"lr_actor": "actor_optimizers", "lr_critic": "critic_optimizers"}
+    _policy_group = ("actors", "actor_targets")
 
     def __init__(self, observation_spaces, action_spaces, agent_ids: list[str] | None = None,
                  O_U_noise: bool = True, expl_noise: float = 0.1, vect_noise_dim: int = 1, mean_noise: float = 0.0,
@@ -116,6 +121,11 @@ class MADDPG:
         self.actor_optimizers = {a: torch.optim.Adam(self.actors[a].parameters(), lr=lr_actor) for a in self.agent_ids}
         self.critic_optimizers = {a: torch.optim.Adam(self.critics[a].parameters(), lr=lr_critic)
                                   for a in self.agent_ids}
+        self._init_registry(hp_config)
+
+    def _fresh_optimizer(self, lr_name: str):
+        nets, lr = (self.actors, self.lr_actor) if lr_name == "lr_actor" else (self.critics, self.lr_critic)
+        return {a: torch.optim.Adam(nets[a].parameters(), lr=lr) for a in self.agent_ids}
 
     # ---- network construction (maddpg.py:296-380) ---------------------------
     def _agent_configs(self, net_config) -> dict[str, dict]:

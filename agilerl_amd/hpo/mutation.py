@@ -134,17 +134,37 @@ class Mutations:
             warnings.warn(f"agx Mutations: {attr} not applied ({err})", stacklevel=2)
             individual.mut = "None"
             return individual
-        if attr in individual.get_lr_names():  # a new lr: fresh optimizer (:440-450)
-            individual.reinit_optimizers()
+        if attr in individual.get_lr_names():  # a new lr: fresh optimizer for it (:440-450)
+            individual.reinit_optimizers(attr)
         individual.mut = attr
         return individual
 
     def parameter_mutation(self, individual):
-        """mutation.py:515-565 + _gaussian_parameter_mutation :733-827 on the
-        policy network's weight matrices (``individual.policy_weights()``:
-        reference state-dict name -> 2-D device view, in state-dict order)."""
-        weights = individual.policy_weights()
+        """mutation.py:515-570: _gaussian_parameter_mutation (:733-827) on the
+        policy's 2-D weight matrices — one network, or each agent's network of
+        a ModuleDict policy in turn (``policy_weight_groups``); then the policy
+        group's shared networks load the mutated policy and the optimizers are
+        re-initialised."""
+        groups = individual.policy_weight_groups() if hasattr(individual, "policy_weight_groups") \
+            else [individual.policy_weights()]
+        for weights in groups:
+            self._gaussian_parameter_mutation(weights)
+        if hasattr(individual, "sync_shared_networks"):
+            individual.sync_shared_networks()
+        individual.reinit_optimizers()  # :567
+        individual.mut = "param"
+        return individual
+
+    def _gaussian_parameter_mutation(self, weights: dict) -> None:
+        """mutation.py:733-827 on ``weights`` (reference state-dict name ->
+        device tensor, in state-dict order): the chosen keys, entries and the
+        normal / super / reset noise drawn exactly as the reference draws them
+        (self.rng, then torch.normal on the CPU generator); each chosen matrix
+        is updated on the host with the reference's CPU indexing semantics and
+        copied back in place."""
         potential = [k for k, w in weights.items() if w.dim() == 2 and "lstm" not in k and "norm" not in k]
+        if not potential:
+            return
         mut_strength, frac, super_strength, super_prob = self.mutation_sd, 0.1, 10, 0.05
         reset_prob, mag_limit = super_prob + 0.05, 1000000
         how_many = int(self.rng.integers(1, len(potential) + 1))
@@ -179,6 +199,3 @@ class Mutations:
                 new = new.clamp(min=-mag_limit, max=mag_limit)
                 W[r_t, c_t] = new
                 W_dev.copy_(W)
-        individual.reinit_optimizers()  # :567
-        individual.mut = "param"
-        return individual

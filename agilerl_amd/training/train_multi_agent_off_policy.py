@@ -7,12 +7,11 @@ Per generation each agent in turn: ``evo_steps // num_envs`` vector steps of
 memory, learning every ``learn_step`` env steps once ``len(memory) >=
 batch_size`` and ``memory.counter > learning_delay``; episode bookkeeping and
 OU-noise resets on finished envs; then ``agent.test`` fitness, and tournament
-selection of clones.  Mutations are outside the hot path (ignored with a
-warning).  Returns (pop, pop_fitnesses)."""
+selection of clones and mutations (RL hyperparameters, actor parameters with
+the targets synced) when both a tournament and a mutation object are given,
+as the reference.  Returns (pop, pop_fitnesses)."""
 
 from __future__ import annotations
-
-import warnings
 
 import numpy as np
 
@@ -28,9 +27,8 @@ def train_multi_agent_off_policy(env, env_name: str, algo: str, pop, memory, INI
                                  overwrite_checkpoints: bool = False, save_elite: bool = False, elite_path=None,
                                  wb: bool = False, verbose: bool = True, accelerator=None, wandb_api_key=None,
                                  wandb_kwargs=None):
-    if mutation is not None:
-        warnings.warn("agx train_multi_agent_off_policy: mutations are outside the hot path and are not applied",
-                      stacklevel=2)
+    if mutation is not None:  # pre-training mutation (the reference's :238-240 / :204-206)
+        pop = mutation.mutation(pop, pre_training_mut=True)
     vec = hasattr(env, "num_envs")
     num_envs = env.num_envs if vec else 1
     sampler = Sampler(memory=memory)
@@ -88,6 +86,7 @@ def train_multi_agent_off_policy(env, env_name: str, algo: str, pop, memory, INI
         if target is not None and np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target)) \
                 and len(pop[0].steps) >= 100:
             return pop, pop_fitnesses
-        if tournament is not None:
+        if tournament and mutation is not None:  # tournament_selection_and_mutation (:525-535)
             _, pop = select_population(tournament, pop)
+            pop = mutation.mutation(pop)
     return pop, pop_fitnesses

@@ -8,14 +8,14 @@ train_off_policy.py:249, 340-345), learn every ``learn_step`` env steps once
 ``len(memory) >= batch_size`` and ``memory.size > learning_delay`` (PER:
 sample with the agent's annealed beta, update priorities; n-step: the
 n-step memory sampled at the same indices), then every agent is evaluated
-with ``agent.test`` and a tournament (``TournamentSelection.select``, global
-numpy RNG) replaces the population.  The replay trees, TD / C51 losses and
-Polyak updates run in libagx.  Mutations are outside the hot path (ignored
-with a warning).  Returns (pop, pop_fitnesses)."""
+with ``agent.test``; with a tournament AND a mutation object (as the
+reference) the tournament (``TournamentSelection.select``, global numpy RNG)
+replaces the population and ``mutation.mutation`` mutates it (RL
+hyperparameters, Q-network parameters with the target synced).  The replay
+trees, TD / C51 losses and Polyak updates run in libagx.  Returns
+(pop, pop_fitnesses)."""
 
 from __future__ import annotations
-
-import warnings
 
 import numpy as np
 
@@ -32,8 +32,8 @@ def train_off_policy(env, env_name: str, algo: str, pop, memory, INIT_HP=None, M
                      checkpoint_path=None, overwrite_checkpoints: bool = False, save_elite: bool = False,
                      elite_path=None, wb: bool = False, verbose: bool = True, accelerator=None, wandb_api_key=None,
                      wandb_kwargs=None):
-    if mutation is not None:
-        warnings.warn("agx train_off_policy: mutations are outside the hot path and are not applied", stacklevel=2)
+    if mutation is not None:  # pre-training mutation (the reference's :238-240 / :204-206)
+        pop = mutation.mutation(pop, pre_training_mut=True)
     num_envs = env.num_envs if hasattr(env, "num_envs") else 1
     sampler = Sampler(memory=memory)
     n_step_sampler = Sampler(memory=n_step_memory) if n_step_memory is not None else None
@@ -108,9 +108,9 @@ def train_off_policy(env, env_name: str, algo: str, pop, memory, INIT_HP=None, M
         if target is not None and np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target)) \
                 and len(pop[0].steps) >= 100:
             return pop, pop_fitnesses
-        if tournament is not None:
-            # the reference selects inside tournament_selection_and_mutation; selection runs here
-            # even without a mutation object (mutations are not applied); under an
-            # initialised process group each rank holds a shard of the population
+        if tournament and mutation is not None:
+            # tournament_selection_and_mutation (utils.py:1137-1225, train_off_policy.py:557-565):
+            # under an initialised process group each rank holds a shard of the population
             _, pop = select_population(tournament, pop)
+            pop = mutation.mutation(pop)
     return pop, pop_fitnesses

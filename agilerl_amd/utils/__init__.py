@@ -42,7 +42,7 @@ def create_population(algo: str, net_config: dict[str, Any] | None, INIT_HP: dic
 
         cls = DQN if algo == "DQN" else RainbowDQN
         return [cls.from_init_hp(observation_space, action_space, net_config, INIT_HP, index=i, device=device,
-                                 **algo_kwargs)
+                                 hp_config=hp_config, **algo_kwargs)
                 for i in range(population_size)]
     if algo == "MADDPG":  # utils/utils.py:590-618
         from ..algorithms.maddpg import MADDPG
@@ -54,7 +54,7 @@ def create_population(algo: str, net_config: dict[str, Any] | None, INIT_HP: dic
                   vect_noise_dim=num_envs, mean_noise=INIT_HP.get("MEAN_NOISE", 0.0),
                   theta=INIT_HP.get("THETA", 0.15), dt=INIT_HP.get("DT", 0.01))
         return [MADDPG(observation_space, action_space, agent_ids=INIT_HP["AGENT_IDS"], index=i,
-                       net_config=net_config, device=device, **hp, **algo_kwargs)
+                       net_config=net_config, device=device, hp_config=hp_config, **hp, **algo_kwargs)
                 for i in range(population_size)]
     raise NotImplementedError(f"algorithm {algo!r} is outside the agx hot path (PPO, DQN, Rainbow DQN, MADDPG)")
 

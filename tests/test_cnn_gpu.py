@@ -217,6 +217,8 @@ def test_config3_pong_rainbow_generation():
                   "encoder_config": dict(ATARI_ENCODER), "head_config": {"hidden_size": [256]}}
     torch.manual_seed(0)
     np.random.seed(0)
+    from agilerl_amd.hpo.mutation import Mutations
+
     pop = create_population("Rainbow DQN", net_config, INIT_HP, obs_space, act_space, population_size=8)
     memory = PrioritizedReplayBuffer(1_000_000, alpha=0.6)
     n_mem = MultiStepReplayBuffer(1_000_000, n_step=3, gamma=0.99)
@@ -226,7 +228,8 @@ def test_config3_pong_rainbow_generation():
     pop, fits = train_off_policy(env, "PongSynthetic", "Rainbow DQN", pop, memory, INIT_HP=INIT_HP,
                                  max_steps=128, evo_steps=128, eval_steps=40, eval_loop=1, per=True, n_step=True,
                                  n_step_memory=n_mem, learning_delay=64,
-                                 tournament=TournamentSelection(2, True, 8, 1), verbose=False)
+                                 tournament=TournamentSelection(2, True, 8, 1),
+                                 mutation=Mutations(0.4, 0, 0.2, 0.3, 0, 0.3, rand_seed=3), verbose=False)
     assert len(fits) == 1 and len(fits[0]) == 8 and all(np.isfinite(fits[0]))
     st = memory.storage
     assert st["obs"].dtype == torch.uint8 and st["obs"].shape == (1_000_000, 4, 84, 84)

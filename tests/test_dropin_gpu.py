@@ -293,6 +293,11 @@ def test_train_off_policy(algo, per, n_step):
     torch.manual_seed(0)
     np.random.seed(0)
     pop = create_population(algo, net_config, INIT_HP, obs_space, act_space, population_size=3)
+    from agilerl_amd.hpo.mutation import Mutations
+
+    # the reference selects only with a tournament AND a mutation object
+    mut = Mutations(no_mutation=0.4, architecture=0, new_layer_prob=0.2, parameters=0.3, activation=0, rl_hp=0.3,
+                    rand_seed=2)
     memory = PrioritizedReplayBuffer(2000, alpha=0.6) if per else ReplayBuffer(2000)
     n_mem = MultiStepReplayBuffer(2000, n_step=3, gamma=0.99) if n_step else None
     env = SyntheticVecEnv(8, seed=4, p_done=0.1)
@@ -300,7 +305,7 @@ def test_train_off_policy(algo, per, n_step):
     beta0 = getattr(pop[0], "beta", None)
     pop, fits = train_off_policy(env, "Synthetic", algo, pop, memory, INIT_HP=INIT_HP, max_steps=256, evo_steps=128,
                                  eval_steps=20, eval_loop=1, per=per, n_step=n_step, n_step_memory=n_mem,
-                                 tournament=TournamentSelection(2, True, 3, 1), verbose=False)
+                                 tournament=TournamentSelection(2, True, 3, 1), mutation=mut, verbose=False)
     assert len(fits) == 2 and all(len(f) == 3 and all(np.isfinite(f)) for f in fits)
     assert all(a.steps[-1] == 256 for a in pop) and len(memory) > 0
     assert len({id(a) for a in pop}) == 3 and max(a.index for a in pop) > 2  # tournament clones, new ids

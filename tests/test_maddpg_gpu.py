@@ -112,6 +112,7 @@ def test_maddpg_learn_matches_torch():
 
 def test_train_multi_agent_off_policy_and_checkpoint(tmp_path):
     from agilerl_amd.components import MultiAgentReplayBuffer
+    from agilerl_amd.hpo.mutation import Mutations
     from agilerl_amd.hpo.tournament import TournamentSelection
     from agilerl_amd.training import train_multi_agent_off_policy
     from agilerl_amd.utils import create_population
@@ -123,7 +124,8 @@ def test_train_multi_agent_off_policy_and_checkpoint(tmp_path):
     mem = MultiAgentReplayBuffer(1000, ["obs", "action", "reward", "next_obs", "done"], env.agents)
     pop, fits = train_multi_agent_off_policy(env, "synthetic_speaker_listener", "MADDPG", pop, mem,
                                              INIT_HP=INIT_HP, max_steps=400, evo_steps=200, eval_loop=1,
-                                             tournament=TournamentSelection(2, True, 2, 1), verbose=False)
+                                             tournament=TournamentSelection(2, True, 2, 1),
+                                             mutation=Mutations(1.0, 0, 0.2, 0, 0, 0, rand_seed=1), verbose=False)
     assert len(fits) == 2 and all(np.isfinite(f).all() for f in fits)
     assert all(a.steps[-1] >= 400 for a in pop) and len(mem) == 800
     path = str(tmp_path / "maddpg.pt")
@@ -170,3 +172,32 @@ def test_hbm_replay_matches_reference_golden(golden, case):
         for f, per in zip(fields, sample):
             for a in agents:
                 assert np.array_equal(per[a].cpu().numpy(), g[f"sample{s}.{f}.{a}"], equal_nan=True), (s, f, a)
+
+
+def test_config4_maddpg_population_of_eight():
+    """Config 4's population (MADDPG pop 8 on speaker-listener-shaped envs; the
+    8-GPU run shards it one agent per rank through hpo/sharded.py, covered by
+    the gloo tests): all 8 agents on one GPU through the reference call site,
+    tournament + RL-hyperparameter mutations, two generations."""
+    from agilerl_amd.components import MultiAgentReplayBuffer
+    from agilerl_amd.hpo.mutation import Mutations
+    from agilerl_amd.hpo.tournament import TournamentSelection
+    from agilerl_amd.training import train_multi_agent_off_policy
+    from agilerl_amd.utils import create_population
+
+    env, obs_spaces, act_spaces = _ma_spaces()
+    INIT_HP = {"AGENT_IDS": env.agents, "BATCH_SIZE": 64, "LEARN_STEP": 8, "LR_ACTOR": 1e-3, "LR_CRITIC": 1e-3}
+    np.random.seed(1)
+    pop = create_population("MADDPG", None, INIT_HP, obs_spaces, act_spaces, population_size=8, num_envs=8)
+    mem = MultiAgentReplayBuffer(100_000, ["obs", "action", "reward", "next_obs", "done"], env.agents)
+    mut = Mutations(no_mutation=0.4, architecture=0, new_layer_prob=0.2, parameters=0.2, activation=0, rl_hp=0.2,
+                    rand_seed=1)
+    pop, fits = train_multi_agent_off_policy(env, "synthetic_speaker_listener", "MADDPG", pop, mem,
+                                             INIT_HP=INIT_HP, max_steps=256, evo_steps=128, eval_loop=1,
+                                             tournament=TournamentSelection(2, True, 8, 1), mutation=mut,
+                                             verbose=False)
+    assert len(fits) == 2 and all(len(f) == 8 and np.isfinite(f).all() for f in fits)
+    assert all(a.steps[-1] >= 256 for a in pop)
+    for agent in pop:
+        for a in env.agents:
+            assert all(torch.isfinite(p).all() for p in agent.actors[a].parameters())

@@ -75,3 +75,60 @@ def test_no_hp_config_is_no_mutation():
     a = types.SimpleNamespace(registry=MutationRegistry(None), mut=None)
     m = Mutations(0, 0, 0, 0, 0, 1, rand_seed=1)
     assert m.rl_hyperparam_mutation(a).mut == "None"
+
+
+def _dqn_cpu(algo, hp=None):
+    from agilerl_amd.algorithms.dqn import DQN, RainbowDQN
+    from agilerl_amd.envs import Box, Discrete
+
+    cls = DQN if algo == "DQN" else RainbowDQN
+    torch.manual_seed(0)
+    return cls(Box(-1, 1, (6,)), Discrete(3), hp_config=hp, device="cpu", batch_size=32, lr=1e-3)
+
+
+@pytest.mark.parametrize("algo", ["DQN", "Rainbow DQN"])
+def test_parameter_mutation_on_q_network_syncs_target(algo):
+    """mutation.py:515-570 on DQN / Rainbow: only 2-D non-norm entries of the
+    actor change (Rainbow: noisy mu / sigma / epsilon matrices included), the
+    target (the policy group's shared network) loads the mutated actor, and a
+    fresh optimizer is built."""
+    from agilerl_amd.hpo.mutation import Mutations
+
+    agent = _dqn_cpu(algo)
+    before = {k: v.clone() for k, v in agent.actor.state_dict().items()}
+    opt0 = agent.optimizer
+    mut = Mutations(0, 0, 0.2, 1.0, 0, 0, rand_seed=5)
+    mut.mutation([agent])
+    assert agent.mut == "param" and agent.optimizer is not opt0
+    after = agent.actor.state_dict()
+    changed = [k for k in before if not torch.equal(before[k], after[k])]
+    assert changed and all(after[k].dim() == 2 and "norm" not in k for k in changed)
+    for k, v in agent.actor_target.state_dict().items():
+        assert torch.equal(v, after[k]), k
+
+
+def test_rl_hyperparameter_mutation_reinits_only_the_mutated_optimizer():
+    """MADDPG (mutation.py:440-450): a mutated lr_actor re-creates the actor
+    optimizers only; batch_size / learn_step land on the agent."""
+    from agilerl_amd.algorithms.maddpg import MADDPG
+    from agilerl_amd.envs import Box, Discrete
+    from agilerl_amd.hpo.mutation import Mutations
+    from agilerl_amd.hpo.registry import HyperparameterConfig, RLParameter
+
+    hp = HyperparameterConfig(lr_actor=RLParameter(min=1e-4, max=1e-2))
+    ids = ["speaker_0", "listener_0"]
+    agent = MADDPG({"speaker_0": Box(-1, 1, (3,)), "listener_0": Box(-1, 1, (11,))},
+                   {"speaker_0": Discrete(3), "listener_0": Discrete(5)}, agent_ids=ids, hp_config=hp, device="cpu")
+    a0, c0 = agent.actor_optimizers, agent.critic_optimizers
+    lr0 = agent.lr_actor
+    Mutations(0, 0, 0.2, 0, 0, 1.0, rand_seed=3).mutation([agent])
+    assert agent.mut == "lr_actor" and agent.lr_actor != lr0
+    assert agent.actor_optimizers is not a0 and agent.critic_optimizers is c0
+    assert all(o.param_groups[0]["lr"] == agent.lr_actor for o in agent.actor_optimizers.values())
+    # parameter mutation: each agent's actor in turn, targets synced
+    before = {a: {k: v.clone() for k, v in agent.actors[a].state_dict().items()} for a in ids}
+    Mutations(0, 0, 0.2, 1.0, 0, 0, rand_seed=4).mutation([agent])
+    for a in ids:
+        assert any(not torch.equal(before[a][k], v) for k, v in agent.actors[a].state_dict().items()), a
+        for k, v in agent.actor_targets[a].state_dict().items():
+            assert torch.equal(v, agent.actors[a].state_dict()[k])
