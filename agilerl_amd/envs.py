@@ -242,13 +242,15 @@ class StackedVecEnv:
             s += n
         return out
 
-    @staticmethod
-    def _cat(parts, out=None, dtype=None):
-        arr = np.concatenate([np.asarray(p, dtype=dtype) for p in parts], axis=0)
-        if out is not None:
-            np.copyto(out.reshape(arr.shape), arr)
+    def _cat(self, parts, out=None, dtype=None):
+        if out is not None:  # each env's block straight into its slice of the staging (one copy)
+            flat = out.reshape(self.num_envs, -1)
+            s = 0
+            for n, p in zip(self.sizes, parts):
+                np.copyto(flat[s:s + n], np.asarray(p).reshape(n, -1), casting="unsafe")
+                s += n
             return out
-        return arr
+        return np.concatenate([np.asarray(p, dtype=dtype) for p in parts], axis=0)
 
     @staticmethod
     def _infos(infos):
