@@ -32,6 +32,7 @@ import torch.distributed as dist  # noqa: E402
 GAE_BYTES = 17          # per transition   
 LOSS_BYTES = 40         # per sample·epoch
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md, chip-level parameters (spec)
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak (spec)
 
 
 def parse():
@@ -163,9 +164,29 @@ def population_leg(args, world, rank):
     barrier(world)
     torch.cuda.synchronize()
     dt = max_over_ranks(time.perf_counter() - t0, world)
+    pop.check_errors()  # a partner timeout in any timed learn() fails the run loudly
     env_steps = world * P * pop.S * args.steps
     updates = world * P * args.epochs * pop.n_minibatches() * args.steps
-    return dict(dt=dt, env_steps=env_steps, updates=updates, S=pop.S, T=pop.T,
+    # the dominant kernel alone: learn() (gather prologue + fused learner) on the
+    # last rollout, HIP events on the launch stream
+    reps = 10
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        pop.learn(prefetch=False)
+    e1.record()
+    torch.cuda.synchronize()
+    pop.check_errors()
+    learn_s = e0.elapsed_time(e1) * 1e-3 / reps
+    flop = 79e3 * P * pop.S * args.epochs  # ~79 kFLOP per sample and update (fwd + bwd)
+    learner = dict(kernel="agx_ppo_learn (gather prologue + ppo_learn_kernel)", ms_per_learn=round(learn_s * 1e3, 3),
+                   updates_per_learn=P * args.epochs * pop.n_minibatches(),
+                   us_per_update=round(learn_s * 1e6 / (args.epochs * pop.n_minibatches()), 2),
+                   achieved_tflops=round(flop / learn_s / 1e12, 2), peak_tflops=F32_MFMA_PEAK_TFLOPS,
+                   frac=round(flop / learn_s / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
+                   bound="latency: 64 serial minibatch updates per agent, each a chain of barrier-separated "
+                         "small GEMM / row phases and a 3-barrier partner hand-off (DESIGN §5)")
+    return dict(dt=dt, env_steps=env_steps, updates=updates, S=pop.S, T=pop.T, learner=learner,
                 generations=(args.steps // args.evo_every) if args.evo_every else 0)
 
 
@@ -657,6 +678,7 @@ def main():
                 "parallelism": f"population-sharded x{world}",
             },
             "learner_updates_per_s": round(res["updates"] / res["dt"], 1),
+            "learner": res["learner"],
             "generations": res["generations"],
             "generation_fitness": "mean return of the training episodes finished since the previous generation "
                                   "(fitness all-gather + tournament + parent clone are timed; a separate "
