@@ -69,6 +69,8 @@ SIGNATURES = {
     "agx_conv2d_forward": (_INT, [_P, _P, _INT, _F, _F, _P, _P, _INT, _P, _P]),
     "agx_conv2d_wgrad_workspace_bytes": (_SZ, [_P]),
     "agx_conv2d_backward": (_INT, [_P, _P, _INT, _F, _F, _P, _P, _P, _P, _P, _P, _INT, _P, _P]),
+    "agx_rows_gather_workspace_bytes": (_SZ, [_P, _INT, _I]),
+    "agx_rows_gather": (_INT, [_P, _P, _INT, _I, _P, _P, _P]),
     "agx_dueling_head_forward": (_INT, [_P, _P, _P, _I, _I, _I, _INT, _P, _P]),
     "agx_dueling_head_backward": (_INT, [_P, _P, _P, _P, _I, _I, _I, _INT, _P, _P, _P]),
     "agx_conv2d_forward_grouped": (_INT, [_P, _I, _P, _I, _INT, _F, _F, _P, _I, _P, _I, _INT, _P, _I, _P]),

@@ -17,6 +17,8 @@ Single rank: step 2 is the identity and step 4 a local gather.
 
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -123,6 +125,20 @@ class PopulationSync:
                 bufs.append(t.view(torch.float32).view(P, 1))
         return bufs
 
+    def _rows_gather(self, bufs: list[torch.Tensor], idx: torch.Tensor) -> None:
+        """agx_rows_gather: row j of every buffer := its old row idx[j]."""
+        import ctypes
+
+        from .. import _lib
+
+        n, P = len(bufs), self.pop.P
+        widths = (ctypes.c_int64 * n)(*[int(b.shape[1]) for b in bufs])
+        ptrs = (ctypes.c_void_p * n)(*[b.data_ptr() for b in bufs])
+        nbytes = int(_lib.load().agx_rows_gather_workspace_bytes(widths, n, P))
+        if getattr(self, "_rows_ws", None) is None or self._rows_ws.numel() < nbytes:
+            self._rows_ws = torch.empty(nbytes, dtype=torch.uint8, device=self.pop.device)
+        _lib.call("agx_rows_gather", ptrs, widths, n, P, idx.data_ptr(), self._rows_ws.data_ptr(), _lib.stream())
+
     @torch.no_grad()
     def _clone_rows(self, parents: list[int]) -> None:
         """Row j of this rank becomes global row parents[rank*P + j] (params,
@@ -135,6 +151,10 @@ class PopulationSync:
         mine = parents[me * P:(me + 1) * P]
         if self.world == 1:  # a permutation-with-repeats of the rows: one gather per buffer
             if mine == list(range(P)):
+                return
+            if (pop.device.type == "cuda" and len(bufs) <= 8 and all(b.is_contiguous() for b in bufs)
+                    and os.environ.get("AGX_ROWS_GATHER", "1") != "0"):
+                self._rows_gather(bufs, self._dev_index(mine))  # every buffer in two launches
                 return
             idx = self._dev_index(mine) if pop.device.type == "cuda" else torch.as_tensor(mine)
             for b in bufs:

@@ -452,6 +452,17 @@ int agx_dueling_head_backward(const float *value, const float *advantage, const 
                               const float *grad_out, int64_t B, int64_t A, int64_t Z, int mode, float *grad_value,
                               float *grad_advantage, void *stream);
 
+/* ---- population row gather ---------------------------------------------------
+ * The single-rank generation step's clone (tournament.py:71-119 + clone,
+ * core/base.py): for each of nbuf buffers of P rows (widths[k] 4-byte words
+ * per row, row-major), row j becomes the old row idx[j] (device int64[P], may
+ * repeat).  All buffers in two launches through a caller-owned workspace of
+ * agx_rows_gather_workspace_bytes. */
+#define AGX_ROWS_MAX_BUFS 8
+size_t agx_rows_gather_workspace_bytes(const int64_t *widths, int nbuf, int64_t P);
+int agx_rows_gather(float *const *bufs, const int64_t *widths, int nbuf, int64_t P, const int64_t *idx,
+                    void *workspace, void *stream);
+
 /* ---- diagnostics ---------------------------------------------------------
  * out[i] = pow(x[i], y[i]) by the routine the PER leaves and IS weights use
  * (glibc's pow algorithm, bit-identical to the host libm); for parity tests. */

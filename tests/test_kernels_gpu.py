@@ -427,3 +427,28 @@ def test_polyak():
     td = t.to(DEV)
     K().polyak_(td, o.to(DEV), 1e-3)
     assert torch.equal(td.cpu(), exp)
+
+
+def test_rows_gather_matches_index_select():
+    """agx_rows_gather (the single-rank generation clone): every buffer's row j
+    becomes its old row idx[j], repeats included, bit for bit."""
+    import ctypes
+
+    from agilerl_amd import _lib
+
+    dev = torch.device("cuda:0")
+    P = 8
+    g = torch.Generator(device=dev).manual_seed(9)
+    bufs = [torch.randn(P, w, device=dev, generator=g) for w in (13829, 13829, 13829, 1, 2, 1, 1, 1)]
+    want = None
+    idx_l = [0, 0, 3, 7, 3, 1, 6, 6]
+    idx = torch.tensor(idx_l, device=dev)
+    want = [b[idx].clone() for b in bufs]
+    n = len(bufs)
+    widths = (ctypes.c_int64 * n)(*[b.shape[1] for b in bufs])
+    ptrs = (ctypes.c_void_p * n)(*[b.data_ptr() for b in bufs])
+    ws = torch.empty(int(_lib.load().agx_rows_gather_workspace_bytes(widths, n, P)), dtype=torch.uint8, device=dev)
+    _lib.call("agx_rows_gather", ptrs, widths, n, P, idx.data_ptr(), ws.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    for b, w in zip(bufs, want):
+        assert torch.equal(b, w)
