@@ -9,10 +9,16 @@ tensors, numbers, strings, lists and dicts), so it is written by
 ``torch.save`` and read back with ``torch.load(weights_only=True)`` — nothing
 in a checkpoint is executed on load.  Spaces are stored as
 ``{"obs_shape", "n_actions"}`` for ``load``.
+
+Checkpoints the reference itself wrote (dill-pickled agents, spaces and
+registries) are read by ``refckpt.read_reference`` — the same weights-only
+unpickler with inert stand-ins for the classes they name — and converted to
+this layout, so ``load_checkpoint`` / ``load`` accept either file.
 """
 
 from __future__ import annotations
 
+import pickle
 from typing import Any
 
 import torch
@@ -20,7 +26,7 @@ import torch
 HP_NAMES = ("index", "batch_size", "lr", "learn_step", "gamma", "tau", "double", "beta", "prior_eps", "num_atoms",
             "v_min", "v_max", "noise_std", "n_step", "combined_reward", "gae_lambda", "clip_coef", "ent_coef",
             "vf_coef", "max_grad_norm", "target_kl", "update_epochs", "num_envs", "net_config", "scores", "fitness",
-            "steps", "mut")
+            "steps", "mut", "normalize_images")
 
 
 def _plain(v: Any) -> Any:
@@ -51,8 +57,24 @@ def checkpoint_dict(agent, modules: dict[str, dict[str, torch.Tensor]], optimize
     return out
 
 
-def read(path: str, algo: str) -> dict:
-    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+def load_file(path: str, adam_networks: tuple[str, ...] | None = None) -> dict:
+    """An agx checkpoint as written, or a reference one converted to the agx
+    layout (refckpt.to_agx; ``adam_networks`` as there)."""
+    from . import refckpt
+
+    try:
+        ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    except pickle.UnpicklingError:
+        ckpt = refckpt.read_reference(path)
+    if isinstance(ckpt, dict) and ckpt.get("agilerl_version") == "agx":
+        return ckpt
+    if not refckpt.is_reference_checkpoint(ckpt):
+        raise ValueError(f"{path}: not an agent checkpoint of agilerl >= 2.0 (no network_info)")
+    return refckpt.to_agx(ckpt, adam_networks)
+
+
+def read(path: str, algo: str, adam_networks: tuple[str, ...] | None = None) -> dict:
+    ckpt = load_file(path, adam_networks)
     if ckpt.get("algo") != algo:
         raise ValueError("Loaded registry does not match the algorithm's registry. Please make sure you are "
                          "loading the checkpoint with the correct algorithm.")
@@ -85,14 +107,16 @@ class TorchCheckpointMixin:
     def load_checkpoint(self, path: str) -> None:
         ck = read(path, self.algo)
         info = ck["network_info"]
-        self.actor.load_state_dict(info["modules"]["actor_state_dict"])
-        self.actor_target.load_state_dict(info["modules"]["actor_target_state_dict"])
+        for name in ("actor", "actor_target"):
+            sd = info["modules"].get(f"{name}_state_dict")
+            if sd:  # an empty state dict is skipped, as the reference (core/base.py:1010)
+                getattr(self, name).load_state_dict(sd)
         self.optimizer.load_state_dict(info["optimizers"]["optimizer_state_dict"])
         restore_attributes(self, ck)
 
     @classmethod
     def load(cls, path: str, device="cuda", accelerator=None):
-        ck = torch.load(path, map_location="cpu", weights_only=True)
+        ck = load_file(path)
         obs_space, act_space = spaces(ck)
         code = cls.__init__.__code__
         names = set(code.co_varnames[1:code.co_argcount])

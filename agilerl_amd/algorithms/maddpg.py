@@ -319,7 +319,8 @@ class MADDPG(EvolvableAgentMixin):
         info = ck["network_info"]
         for n in ("actors", "actor_targets", "critics", "critic_targets"):
             for a, sd in info["modules"][f"{n}_state_dict"].items():
-                getattr(self, n)[a].load_state_dict(sd)
+                if sd:  # empty ones are skipped, as the reference (core/base.py:1006-1008)
+                    getattr(self, n)[a].load_state_dict(sd)
         for n in ("actor_optimizers", "critic_optimizers"):
             for a, sd in info["optimizers"][f"{n}_state_dict"].items():
                 getattr(self, n)[a].load_state_dict(sd)

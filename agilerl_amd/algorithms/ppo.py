@@ -259,7 +259,7 @@ class PPO:
         """core/base.py:951-1072 for the agx layout; torch.load(weights_only=True)."""
         from . import checkpoint as C
 
-        ck = C.read(path, self.algo)
+        ck = C.read(path, self.algo, adam_networks=("actor", "critic"))
         info = ck["network_info"]
         sd = {f"{net}.{k}": t for net in info["network_names"] for k, t in info["modules"][f"{net}_state_dict"].items()}
         self.load_state_dict(sd)
@@ -267,6 +267,8 @@ class PPO:
         keys = self.spec.state_dict_keys()
         m, v = self._opt_rows()
         for k, t in opt["exp_avg"].items():
+            if k.startswith("critic.encoder."):  # shares the actor encoder's row (a reference file holds both)
+                continue
             o, sh = keys[k]
             m[o:o + t.numel()] = t.reshape(-1).to(m)
             v[o:o + t.numel()] = opt["exp_avg_sq"][k].reshape(-1).to(v)
@@ -277,7 +279,7 @@ class PPO:
     def load(cls, path: str, device="cuda", accelerator=None) -> "PPO":
         from . import checkpoint as C
 
-        ck = torch.load(path, map_location="cpu", weights_only=True)
+        ck = C.load_file(path, adam_networks=("actor", "critic"))
         obs_space, act_space = C.spaces(ck)
         kw = {k: ck[k] for k in ("batch_size", "lr", "learn_step", "gamma", "gae_lambda", "clip_coef", "ent_coef",
                                  "vf_coef", "max_grad_norm", "target_kl", "update_epochs", "num_envs",
