@@ -125,9 +125,13 @@ __global__ void per_mark(int32_t *__restrict__ win, const int64_t *__restrict__ 
     if (i < n) win[indices[i]] = -1;
 }
 
-__global__ void per_claim(int32_t *__restrict__ win, const int64_t *__restrict__ indices,
-                          const float *__restrict__ pri, int64_t n, double floor_,
-                          double *__restrict__ max_priority) {
+// The running max priority is one address: an atomic per wave serialises
+// ~1k same-address atomics at L2 (14 us at 2^16 updates).  One per block, and
+// only when the block's max exceeds the value already there (max only grows).
+__global__ __launch_bounds__(256) void per_claim(int32_t *__restrict__ win, const int64_t *__restrict__ indices,
+                                                 const float *__restrict__ pri, int64_t n, double floor_,
+                                                 double *__restrict__ max_priority) {
+    __shared__ double red[256 / kWave];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double pm = 0.0;
     if (i < n) {
@@ -136,7 +140,13 @@ __global__ void per_claim(int32_t *__restrict__ win, const int64_t *__restrict__
         pm = p < floor_ ? floor_ : p;
     }
     for (int o = 32; o > 0; o >>= 1) pm = fmax(pm, __shfl_xor(pm, o, 64));
-    if ((threadIdx.x & 63) == 0 && pm > 0.0) atomic_max_pos_double(max_priority, pm);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 256 / kWave; ++w) pm = fmax(pm, red[w]);
+        if (pm > 0.0 && pm > __hip_atomic_load(max_priority, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomic_max_pos_double(max_priority, pm);
+    }
 }
 
 __global__ void per_write_leaves(double *__restrict__ sum_tree, double *__restrict__ min_tree,

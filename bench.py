@@ -349,12 +349,45 @@ def _time(fn, reps=5):
     return s.elapsed_time(e) * 1e-3 / reps
 
 
+def _time_graph(fn, reps=20):
+    """Mean time (s) of one fn call replayed from a HIP graph of ``reps``
+    captured calls: the kernels back to back on the stream, without the
+    Python / ctypes launch cost that dominates an eager loop of these
+    microsecond-scale entry points (torch.cuda.CUDAGraph is hipGraph here)."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(reps):
+            fn()
+    graph.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    graph.replay()
+    e.record()
+    e.synchronize()
+    del graph
+    return s.elapsed_time(e) * 1e-3 / reps
+
+
+def _both(fn):
+    """(graph-replayed time, eager time) of fn."""
+    return _time_graph(fn), _time(fn)
+
+
 def kernels_leg(peak_meas):
     """Config-3 kernels at the SURVEY §8d synthetic shapes, algorithmic
     bytes / HIP-event time: PER retrieve (+ IS weights) over a 2^20-leaf tree
     with 2^20 uniforms, PER priority update of 2^16 indices (duplicates),
     C51 projection + loss over 2^20 rows (A=6, Z=51), DQN TD target + loss
-    gradient over 2^20 rows (A=6)."""
+    gradient over 2^20 rows (A=6).  The microsecond-scale entry points are
+    timed replayed from a HIP graph (``ms``) and as an eager Python loop
+    (``ms_eager``, launch-cost inclusive); rates use ``ms``."""
     from agilerl_amd import kernels as K
 
     dev = "cuda"
@@ -371,20 +404,22 @@ def kernels_leg(peak_meas):
     pri = torch.randn(max_size, device=dev, generator=g).abs() + 1e-5
     K.per_update(st, mt, cap, max_size, allidx, pri, 0.6, maxp, workspace=ws)
     u = torch.rand(1 << 20, device=dev, generator=g)
-    t = _time(lambda: K.per_sample(st, mt, cap, u, size=max_size, beta=0.4, weights=True))
+    t, te = _both(lambda: K.per_sample(st, mt, cap, u, size=max_size, beta=0.4, weights=True))
     nb = (8 * 20 + 4 + 8 + 8 + 4) * u.numel()  # walk + uniform + index + leaf + weight
     # the 16 MiB sum tree is re-walked 2^20 times and stays cache resident (LDS
     # top levels, L2 / Infinity Cache): the walk's algorithmic bytes are not HBM
     # traffic, so no HBM fraction is claimed for it
     out["per_sample"] = dict(unit_bytes=nb // u.numel(), units=u.numel(), ms=round(t * 1e3, 4),
+                             ms_eager=round(te * 1e3, 4),
                              samples_per_s=round(u.numel() / t, 1), walk_gbs=round(nb / t / 1e9, 1),
                              frac_of_measured=None,
                              bound="latency (dependent 20-level walk over a cache-resident 16 MiB tree)")
     idx = torch.randint(0, max_size, (1 << 16,), device=dev, generator=g)
     p2 = torch.rand(1 << 16, device=dev, generator=g)
-    t = _time(lambda: K.per_update(st, mt, cap, max_size, idx, p2, 0.6, maxp, workspace=ws))
+    t, te = _both(lambda: K.per_update(st, mt, cap, max_size, idx, p2, 0.6, maxp, workspace=ws))
     nb = 976 * idx.numel()
-    out["per_update"] = dict(unit_bytes=976, units=idx.numel(), ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
+    out["per_update"] = dict(unit_bytes=976, units=idx.numel(), ms=round(t * 1e3, 4), ms_eager=round(te * 1e3, 4),
+                             gbs=round(nb / t / 1e9, 1),
                              frac_of_measured=round(nb / t / 1e9 / peak_meas, 4),
                              bound="launch latency (leaf claim + band rebuild)")
     del st, mt, ws, allidx, pri
@@ -397,23 +432,26 @@ def kernels_leg(peak_meas):
     r = torch.randn(B, device=dev, generator=g3)
     d = (torch.rand(B, device=dev, generator=g3) < 0.05).float()
     sup = torch.linspace(-200, 200, Z, device=dev)
-    t = _time(lambda: K.c51_project_loss(qn, td, lp, act, r, d, sup, -200.0, 200.0, 0.99 ** 4))
+    t, te = _both(lambda: K.c51_project_loss(qn, td, lp, act, r, d, sup, -200.0, 200.0, 0.99 ** 4))
     nb = 444 * B
-    out["c51_project_loss"] = dict(unit_bytes=444, units=B, ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
+    out["c51_project_loss"] = dict(unit_bytes=444, units=B, ms=round(t * 1e3, 4), ms_eager=round(te * 1e3, 4),
+                                   gbs=round(nb / t / 1e9, 1),
                                    frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
     del td, lp
     qt = torch.randn(B, A, device=dev, generator=g3)
     qc = torch.randn(B, A, device=dev, generator=g3)
-    t = _time(lambda: K.td_target(qt, r, d, 0.99, q_next_online=qn, double=True, q_cur=qc, actions=act))
+    t, te = _both(lambda: K.td_target(qt, r, d, 0.99, q_next_online=qn, double=True, q_cur=qc, actions=act))
     ub = 3 * 4 * A + 8 + 4 + 4 + 4 + 4 * A  # Q(s'), Qt(s'), Q(s) rows, a, r, d in; y, dL/dQ out
     nb = ub * B
-    out["td_target"] = dict(unit_bytes=ub, units=B, ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
+    out["td_target"] = dict(unit_bytes=ub, units=B, ms=round(t * 1e3, 4), ms_eager=round(te * 1e3, 4),
+                            gbs=round(nb / t / 1e9, 1),
                             frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
     # MADDPG critic target (a22): q, q', r, d in; y, dL/dq out
     q1, qn1 = qc[:, 0].contiguous(), qt[:, 0].contiguous()
-    t = _time(lambda: K.maddpg_critic_target(q1, qn1, r, d, 0.95))
+    t, te = _both(lambda: K.maddpg_critic_target(q1, qn1, r, d, 0.95))
     nb = 24 * B
-    out["maddpg_critic_target"] = dict(unit_bytes=24, units=B, ms=round(t * 1e3, 4), gbs=round(nb / t / 1e9, 1),
+    out["maddpg_critic_target"] = dict(unit_bytes=24, units=B, ms=round(t * 1e3, 4), ms_eager=round(te * 1e3, 4),
+                                       gbs=round(nb / t / 1e9, 1),
                                        frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
     del qn, qt, qc, q1, qn1
     # Polyak (a10) and clip + Adam (a8) over a population of flat parameter
