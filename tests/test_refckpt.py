@@ -12,6 +12,8 @@ stand-ins for every class the file names.
 * a file in the reference's layout naming classes of a module that is not
   importable at load time, one of which would run a function when unpickled
   the reference's way, loads with nothing run;
+* a MADDPG file in the multi-agent layout ({agent_id: state_dict} per network
+  and per optimizer) restores every network and Adam state;
 * (GPU) a PPO file in the reference's layout — one Adam over the actor's and
   the critic's parameter groups (ppo.py:329-333) — lands in the population
   rows: weights, both moments per parameter and the step."""
@@ -154,6 +156,65 @@ def test_reference_layout_loads_with_nothing_run(tmp_path):
         assert torch.equal(agent.actor.state_dict()[k], t)
     s0 = opt.state_dict()["state"][0]
     assert torch.equal(agent.optimizer.state_dict()["state"][0]["exp_avg"], s0["exp_avg"])
+
+
+def test_reference_layout_maddpg_loads(tmp_path):
+    """Multi-agent layout (algo_utils.py module_checkpoint_multiagent,
+    OptimizerWrapper.state_dict per agent): {agent_id: state_dict} per
+    network and per optimizer."""
+    import dill
+
+    from agilerl_amd.algorithms.maddpg import MADDPG
+    from agilerl_amd.envs import Box, Discrete
+
+    ids = ["speaker_0", "listener_0"]
+    spaces = ({"speaker_0": Box(-1, 1, (3,)), "listener_0": Box(-1, 1, (11,))},
+              {"speaker_0": Discrete(3), "listener_0": Discrete(5)})
+    torch.manual_seed(0)
+    src = MADDPG(*spaces, agent_ids=ids, device="cpu", batch_size=48)
+    for net in ("actors", "critics"):
+        for a in ids:
+            for p in getattr(src, net)[a].parameters():
+                p.data.normal_()
+    opts = {}
+    for a in ids:  # one step of each agent's Adams so the moments are non-trivial
+        for net, opt in (("actors", src.actor_optimizers), ("critics", src.critic_optimizers)):
+            for p in getattr(src, net)[a].parameters():
+                p.grad = torch.randn_like(p)
+            opt[a].step()
+    for n in ("actor_optimizers", "critic_optimizers"):
+        opts[n] = {a: o.state_dict() for a, o in getattr(src, n).items()}
+    mod = _fake_module()
+    sys.modules[mod.__name__] = mod
+    try:
+        info_mods = {}
+        for n in ("actors", "actor_targets", "critics", "critic_targets"):
+            info_mods.update({f"{n}_cls": {a: mod.QNetwork for a in ids}, f"{n}_init_dict": {a: {} for a in ids},
+                              f"{n}_state_dict": {a: OrderedDict(getattr(src, n)[a].state_dict()) for a in ids},
+                              f"{n}_module_dict_cls": mod.QNetwork})
+        ck = {"algo": "MADDPG", "agilerl_version": "2.2.0", "registry": mod.Registry(), "agent_ids": ids,
+              "batch_size": 48, "lr_actor": 0.001, "lr_critic": 0.01,
+              "network_info": {"modules": info_mods, "network_names": ["actors", "actor_targets", "critics",
+                                                                        "critic_targets"],
+                               "optimizers": {f"{n}_state_dict": opts[n] for n in opts},
+                               "optimizer_names": list(opts)}}
+        path = str(tmp_path / "ref_maddpg.pt")
+        torch.save(ck, path, pickle_module=dill)
+    finally:
+        del sys.modules[mod.__name__]
+    dst = MADDPG(*spaces, agent_ids=ids, device="cpu")
+    dst.load_checkpoint(path)
+    assert dst.batch_size == 48
+    for n in ("actors", "actor_targets", "critics", "critic_targets"):
+        for a in ids:
+            for k, t in getattr(src, n)[a].state_dict().items():
+                assert torch.equal(getattr(dst, n)[a].state_dict()[k], t), (n, a, k)
+    for n in ("actor_optimizers", "critic_optimizers"):
+        for a in ids:
+            s0, s1 = getattr(src, n)[a].state_dict()["state"], getattr(dst, n)[a].state_dict()["state"]
+            assert set(s0) == set(s1)
+            for i in s0:
+                assert torch.equal(s0[i]["exp_avg"], s1[i]["exp_avg"])
 
 
 def test_adam_rows_keys_by_network_order():
