@@ -351,14 +351,35 @@ class PPOPopulation:
         """One of two pinned [E, P, S] int64 host buffers, alternating (the H2D
         copy that last read a buffer finished long before it is reused: it
         precedes a whole learn() on the stream; checked by its event)."""
-        if self._perm_host is None:
-            shape = (self.update_epochs, self.P, self.S)
-            self._perm_host = [[torch.empty(shape, dtype=torch.int64, pin_memory=True), None] for _ in range(2)]
+        self._alloc_perm_host()
         slot = self._perm_host[self._perm_k]
         self._perm_k ^= 1
         if slot[1] is not None:
             slot[1].synchronize()
         return slot[0]
+
+    def _alloc_perm_host(self) -> None:
+        if self._perm_host is None:
+            shape = (self.update_epochs, self.P, self.S)
+            self._perm_host = [[torch.empty(shape, dtype=torch.int64, pin_memory=True), None] for _ in range(2)]
+
+    def prepare_learn(self) -> None:
+        """Do now what the next learn() would otherwise do on first use: build
+        the fused learner (device workspace) and the pinned permutation
+        staging, and draw the permutations.  The pipelined runner calls this
+        before launching a persistent rollout: between that launch and the
+        host pacing it, the device is waiting for this thread, so nothing
+        there may wait for the device — and a hipMalloc / hipHostMalloc, or an
+        event sync, can."""
+        if self.fused_descriptor() is not None:
+            if getattr(self, "_fused", None) is None or self._fused.epochs_ws < self.update_epochs:
+                from .learner import FusedLearner
+
+                self._fused = FusedLearner(self)
+        if self.perm_source == "numpy":
+            self._alloc_perm_host()
+        if self.prefetch_perms:
+            self.prefetch_permutations()
 
     def prefetch_permutations(self) -> None:
         """Draw the next learn's permutations now, off the critical path:

@@ -391,6 +391,7 @@ class PopulationRunner:
         if not self.started:
             self.env.reset(out_obs=self.obs_h.numpy())
             self.started = True
+        self.pop.prepare_learn()  # nothing between the launch and the pacing may wait for the device
         lib, ctl, base = self._launch_persistent(desc)
         self._finish_persistent()
         self.pop.finish_rollout(self.last_obs, self.last_done, self.last_value)
