@@ -56,14 +56,46 @@ class AgxRolloutIO(ctypes.Structure):
     ]
 
 
+# hipHostFree waits for the whole device.  A persistent rollout of this
+# process waits for the host from its launch until the host's final release,
+# so a free in that window (a garbage-collected runner's buffers, finalised in
+# the middle of another runner's env step) stalls the rollout until its
+# timeout.  Frees that come while a rollout is being paced are deferred to
+# the end of the pacing.
+_PACING = 0
+_DEFERRED_FREES: list[int] = []
+
+
+def _host_free(p: int) -> None:
+    if _PACING:
+        _DEFERRED_FREES.append(p)
+    else:
+        _lib.load().agx_host_free(p)
+
+
+def _pacing_begin() -> None:
+    global _PACING
+    _PACING += 1
+
+
+def _pacing_end() -> None:
+    global _PACING
+    _PACING -= 1
+    if not _PACING:
+        lib = _lib.load()
+        while _DEFERRED_FREES:
+            lib.agx_host_free(_DEFERRED_FREES.pop())
+
+
 def _coherent(owner, nbytes: int) -> torch.Tensor:
     """uint8 CPU tensor over agx_host_alloc memory (coherent, device-accessible
-    at the same address), freed with its owner."""
+    at the same address), freed with its owner (deferred while a persistent
+    rollout is being paced, see _host_free)."""
     lib = _lib.load()
     p = lib.agx_host_alloc(nbytes)
     if not p:
         raise _lib.AgxError(lib.agx_last_error().decode(errors="replace"))
-    weakref.finalize(owner, lib.agx_host_free, p)
+    weakref.finalize(owner, _host_free, p)
     return torch.from_numpy(np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)))
 
 
@@ -230,8 +262,12 @@ class PopulationRunner:
 
     def _collect_persistent(self, desc) -> None:
         """One launch for the whole rollout; the host paces it step by step."""
-        lib, ctl, base = self._launch_persistent(desc)
-        self._pace_persistent(lib, ctl, base)
+        _pacing_begin()
+        try:
+            lib, ctl, base = self._launch_persistent(desc)
+            self._pace_persistent(lib, ctl, base)
+        finally:
+            _pacing_end()
         self._finish_persistent()
 
     def _launch_persistent(self, desc):
@@ -392,11 +428,15 @@ class PopulationRunner:
             self.env.reset(out_obs=self.obs_h.numpy())
             self.started = True
         self.pop.prepare_learn()  # nothing between the launch and the pacing may wait for the device
-        lib, ctl, base = self._launch_persistent(desc)
-        self._finish_persistent()
-        self.pop.finish_rollout(self.last_obs, self.last_done, self.last_value)
-        loss = self.pop.learn(prefetch=False)
-        self._pace_persistent(lib, ctl, base)
+        _pacing_begin()
+        try:
+            lib, ctl, base = self._launch_persistent(desc)
+            self._finish_persistent()
+            self.pop.finish_rollout(self.last_obs, self.last_done, self.last_value)
+            loss = self.pop.learn(prefetch=False)
+            self._pace_persistent(lib, ctl, base)
+        finally:
+            _pacing_end()
         if self.pop.prefetch_perms:  # next learn's minibatch orders: host work while the GPU learns
             self.pop.prefetch_permutations()
         return loss
