@@ -819,11 +819,14 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 __syncthreads();
                 const int tid = vtid();
                 if (tid == 0) {
-                    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // the last partner to arrive learns it from its own ticket: no
+                    // poll round trip on the critical path of the hand-off
+                    const unsigned before = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     AGX_STAMP(st0);
                     unsigned spins = 0;
                     int ok = 1;
-                    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    while (before + 1u < target &&
+                           __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                         __builtin_amdgcn_s_sleep(1);
                         if (++spins > kSpinMax) {
                             __hip_atomic_store(g.cnt + g.P, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
