@@ -113,16 +113,23 @@ def read_reference(path: str) -> dict:
     known = {name for item in allowed if isinstance(item, tuple) for name in [item[1]]}
     known |= {f"{c.__module__}.{c.__qualname__}" for c in allowed if isinstance(c, type)}
     extra = [(_standin(n), n) for n in torch.serialization.get_unsafe_globals_in_checkpoint(path) if n not in known]
-    for _ in range(64):  # names the static scan could not see surface as UnpicklingError
-        with torch.serialization.safe_globals(allowed + extra):
-            try:
-                return torch.load(path, map_location="cpu", weights_only=True)
-            except pickle.UnpicklingError as err:
-                name = _unsupported_global(str(err))
-                if name is None or name in {n for _, n in extra}:
-                    raise
-                extra.append((_standin(name), name))
-    raise pickle.UnpicklingError(f"{path}: too many unknown globals")
+    before = list(torch.serialization.get_safe_globals())
+    try:
+        for _ in range(64):  # names the static scan could not see surface as UnpicklingError
+            with torch.serialization.safe_globals(allowed + extra):
+                try:
+                    return torch.load(path, map_location="cpu", weights_only=True)
+                except pickle.UnpicklingError as err:
+                    name = _unsupported_global(str(err))
+                    if name is None or name in {n for _, n in extra}:
+                        raise
+                    extra.append((_standin(name), name))
+        raise pickle.UnpicklingError(f"{path}: too many unknown globals")
+    finally:
+        # the stand-ins _safe_load_type allow-listed during the load go again
+        if list(torch.serialization.get_safe_globals()) != before:
+            torch.serialization.clear_safe_globals()
+            torch.serialization.add_safe_globals(before)
 
 
 def _unsupported_global(msg: str) -> str | None:
