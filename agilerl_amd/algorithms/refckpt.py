@@ -127,7 +127,7 @@ def read_reference(path: str) -> dict:
         raise pickle.UnpicklingError(f"{path}: too many unknown globals")
     finally:
         # the stand-ins _safe_load_type allow-listed during the load go again
-        if list(torch.serialization.get_safe_globals()) != before:
+        if set(torch.serialization.get_safe_globals()) != set(before):
             torch.serialization.clear_safe_globals()
             torch.serialization.add_safe_globals(before)
 

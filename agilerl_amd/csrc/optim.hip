@@ -64,12 +64,35 @@ __global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const float *__restric
             const int64_t j = j0 + 4 * (r * kOptBlock + threadIdx.x);
             x[r] = j < n ? *reinterpret_cast<const f4 *>(g + j) : f4{0.f, 0.f, 0.f, 0.f};
         }
+        const int64_t jl = (j0 + kSumChunk < n ? j0 + kSumChunk : n) - 1;
+        const int kb = group_of(gr, j0);
+        if (kb == group_of(gr, jl)) {
+            // the whole chunk in one group (all but the chunks a group boundary
+            // cuts): one accumulator, no per-element group lookup — the same
+            // additions in the same order as the general form, so the same bits
+            double a = 0.0;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const int64_t j = j0 + 4 * (r * kOptBlock + threadIdx.x);
-            if (j < n) {
+            for (int r = 0; r < 8; ++r) {
+                const int64_t j = j0 + 4 * (r * kOptBlock + threadIdx.x);
+                if (j < n) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) add(j + e, x[r][e]);
+                    for (int e = 0; e < 4; ++e) {
+                        const double xd = (double)x[r][e];
+                        a += xd * xd;
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kMaxGroups; ++q)
+                if (q == kb) acc[q] = a;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int64_t j = j0 + 4 * (r * kOptBlock + threadIdx.x);
+                if (j < n) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) add(j + e, x[r][e]);
+                }
             }
         }
     } else {

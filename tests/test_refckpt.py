@@ -92,7 +92,7 @@ def test_reference_dqn_checkpoint_loads():
     path = f"{REF_DQN}/lesson1_trained_agent.pt"
     allow_before = list(torch.serialization.get_safe_globals())
     raw = refckpt.read_reference(path)
-    assert list(torch.serialization.get_safe_globals()) == allow_before  # nothing stays allow-listed
+    assert set(torch.serialization.get_safe_globals()) == set(allow_before)  # nothing stays allow-listed
     assert isinstance(raw["registry"], refckpt.Inert) and isinstance(raw["observation_space"], refckpt.Inert)
     assert raw["observation_space"].attr("_shape") == (2, 6, 7)
     agent = DQN.load(path, device="cpu")
