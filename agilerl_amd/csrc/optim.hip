@@ -192,8 +192,8 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float *__restrict__ par
     const float step_size = lr / bc1;
     const size_t base = (size_t)p * n;
     const int64_t j0 = (int64_t)blockIdx.x * kOptChunk;
-    auto upd = [&](int64_t j, float g, float &pp, float &mm, float &vv) {
-        if (clip) g = g * coef[group_of(gr, j)];
+    auto upd = [&](int64_t j, float g, float &pp, float &mm, float &vv, int k = -1) {
+        if (clip) g = g * coef[k >= 0 ? k : group_of(gr, j)];
         mm = mm + (1.0f - b1) * (g - mm);  // lerp_(g, 1-b1)
         vv = vv * b2 + (1.0f - b2) * g * g;
         const float denom = sqrtf(vv) / bc2_sqrt + eps;
@@ -207,10 +207,16 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float *__restrict__ par
         f4 pp = *reinterpret_cast<const f4 *>(params + base + j);
         f4 mm = *reinterpret_cast<const f4 *>(m + base + j);
         f4 vv = *reinterpret_cast<const f4 *>(v + base + j);
+        // one group lookup per float4 unless a group boundary falls inside it
+        int k4 = -1;
+        if (clip) {
+            const int ka = group_of(gr, j);
+            if (ka == group_of(gr, j + 3)) k4 = ka;
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             float pe = pp[e], me = mm[e], ve = vv[e];
-            g[e] = upd(j + e, g[e], pe, me, ve);
+            g[e] = upd(j + e, g[e], pe, me, ve, k4);
             pp[e] = pe;
             mm[e] = me;
             vv[e] = ve;
