@@ -1897,7 +1897,7 @@ extern "C" size_t agx_ppo_learn_lds_bytes(const agx_ppo_net *net) {
 }
 
 // Workgroups per agent: the learner spreads an agent's sub-batches over up to
-// 4 partner workgroups (one CU each) when the population leaves CUs idle.
+// kMaxK = 8 partner workgroups (one CU each) when the population leaves CUs idle.
 static int cu_count() {
     static int n = 0;
     if (!n) {

@@ -265,8 +265,13 @@ class PPOPopulation:
             self.agent_lr[p] = float(value)
             return
         if name == "batch_size":
+            if int(value) < 1:
+                raise ValueError("batch_size must be >= 1")
+            # a minibatch larger than the rollout is the whole rollout (the
+            # reference's indices[start:start + batch_size] slice, ppo.py:843-845):
+            # the learner tables hold min(batch, S), the agent keeps its value
             self.agent_batch[p] = int(value)
-            self.hp_batch_d[p] = int(value)
+            self.hp_batch_d[p] = min(int(value), self.S)
         elif name == "update_epochs":
             if int(value) < 1:
                 raise ValueError("update_epochs must be >= 1")
@@ -291,7 +296,7 @@ class PPOPopulation:
     def _rederive(self) -> None:
         """Population maxima (they size the learner's workspace and partner
         split) and the heterogeneity flag, from the per-agent lists."""
-        self.batch_size = max(self.agent_batch)
+        self.batch_size = min(max(self.agent_batch), self.S)
         if max(self.agent_epochs) != self.update_epochs:
             self.update_epochs = max(self.agent_epochs)
             self._fused = None      # workspace is sized by the epochs

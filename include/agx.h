@@ -104,8 +104,8 @@ size_t agx_ppo_learn_lds_bytes(const agx_ppo_net *net);
 /* Device workspace bytes for agx_ppo_learn: arrival counters, the
  * minibatch-ordered copy of the rollout for `epochs` epochs of P agents x S
  * samples, and the gradient hand-off slabs of the partner workgroups (an
- * agent's sub-batches are spread over up to 4 workgroups when P leaves CUs
- * idle; AGX_LEARN_SPLIT=1..4 overrides the choice). */
+ * agent's sub-batches are spread over up to 8 workgroups when P leaves CUs
+ * idle; AGX_LEARN_SPLIT=1..8 lowers the choice). */
 size_t agx_ppo_learn_workspace_bytes(const agx_ppo_net *net, int64_t P, int64_t S, int64_t epochs);
 /* Validates that `net` is one of the instantiated shapes (the kernel plan is
  * compile-time); no device work.  AGX_EUNSUPPORTED otherwise. */

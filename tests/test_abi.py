@@ -11,10 +11,47 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "agx.h")
 
 
+INTEGRATION = os.path.join(ROOT, "INTEGRATION.md")
+
+
 def header_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(agx_[a-z0-9_]+)\s*\(", text)))
+
+
+def _top_level_args(s: str, start: int) -> tuple[int, str]:
+    """Argument text of the call whose '(' is at s[start]: (end index, text)."""
+    depth = 0
+    for i in range(start, len(s)):
+        if s[i] in "([{":
+            depth += 1
+        elif s[i] in ")]}":
+            depth -= 1
+            if depth == 0:
+                return i, s[start + 1:i]
+    raise ValueError("unbalanced call")
+
+
+def _count_args(text: str) -> int:
+    text = text.strip()
+    if text in ("", "void"):
+        return 0
+    depth, n = 0, 1
+    for ch in text:
+        if ch in "([{":
+            depth += 1
+        elif ch in ")]}":
+            depth -= 1
+        elif ch == "," and depth == 0:
+            n += 1
+    return n
+
+
+def header_arity() -> dict[str, int]:
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    return {m.group(1): _count_args(m.group(2))
+            for m in re.finditer(r"\b(agx_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text, flags=re.S)}
 
 
 @pytest.fixture(scope="module")
@@ -61,3 +98,22 @@ def test_library_is_gfx950_code_object():
 
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_integration_doc_calls_match_header():
+    """Every agx_* call INTEGRATION.md quotes (code blocks and inline) names a
+    header function and passes its number of arguments ('...' elisions are
+    checked by name only)."""
+    arity = header_arity()
+    doc = open(INTEGRATION).read()
+    seen = 0
+    for m in re.finditer(r"\b(agx_[a-z0-9_]+)\(", doc):
+        name = m.group(1)
+        assert name in arity, f"INTEGRATION.md calls {name}, which include/agx.h does not declare"
+        _, args = _top_level_args(doc, m.end() - 1)
+        if "..." in args:
+            continue
+        assert _count_args(args) == arity[name], \
+            f"INTEGRATION.md: {name}({args.strip()[:60]}...) has {_count_args(args)} arguments, the header {arity[name]}"
+        seen += 1
+    assert seen >= 12
