@@ -78,16 +78,27 @@ class SyntheticVecEnv:
         self.single_action_space = Discrete(n_actions)
         self.observation_space = self.single_observation_space
         self.action_space = self.single_action_space
-        rng = np.random.default_rng(seed)
-        self._obs = rng.standard_normal((ring, num_envs, obs_dim), dtype=np.float32)
-        self._rew = rng.standard_normal((ring, num_envs), dtype=np.float32)
-        self._term = rng.random((ring, num_envs)) < p_done
+        self._obs_dim, self._p_done, self._ring, self.seed = obs_dim, p_done, ring, seed
+        self._generate(seed)
         self._trunc = np.zeros(num_envs, dtype=bool)
         self.max_episode_steps = max_episode_steps
         self._len = np.zeros(num_envs, dtype=np.int64)
         self._k = 0
         self._ring = ring
         self.steps = 0
+
+    def _generate(self, seed: int) -> None:
+        rng = np.random.default_rng(seed)
+        ring, n = self._ring, self.num_envs
+        self._obs = rng.standard_normal((ring, n, self._obs_dim), dtype=np.float32)
+        self._rew = rng.standard_normal((ring, n), dtype=np.float32)
+        self._term = rng.random((ring, n)) < self._p_done
+
+    def reseed(self, seed: int) -> None:
+        """A different episode stream (StackedVecEnv.from_shared gives each
+        agent's copy its own)."""
+        self.seed = int(seed)
+        self._generate(self.seed)
 
     def reset(self, seed=None, options=None, out_obs: np.ndarray | None = None):
         self._k = 0
@@ -135,17 +146,21 @@ class SyntheticAtariVecEnv(SyntheticVecEnv):
         self.single_action_space = Discrete(n_actions)
         self.observation_space = self.single_observation_space
         self.action_space = self.single_action_space
-        rng = np.random.default_rng(seed)
-        self._obs = rng.integers(0, 256, (ring, num_envs, *frame_shape), dtype=np.uint8)
-        point = rng.random((ring, num_envs)) < 1 / 60
-        self._rew = np.where(point, np.where(rng.random((ring, num_envs)) < 0.5, -1.0, 1.0), 0.0).astype(np.float32)
-        self._term = rng.random((ring, num_envs)) < p_done
+        self._frame_shape, self._p_done, self._ring, self.seed = tuple(frame_shape), p_done, ring, seed
+        self._generate(seed)
         self._trunc = np.zeros(num_envs, dtype=bool)
         self.max_episode_steps = max_episode_steps
         self._len = np.zeros(num_envs, dtype=np.int64)
         self._k = 0
-        self._ring = ring
         self.steps = 0
+
+    def _generate(self, seed: int) -> None:
+        rng = np.random.default_rng(seed)
+        ring, n = self._ring, self.num_envs
+        self._obs = rng.integers(0, 256, (ring, n, *self._frame_shape), dtype=np.uint8)
+        point = rng.random((ring, n)) < 1 / 60
+        self._rew = np.where(point, np.where(rng.random((ring, n)) < 0.5, -1.0, 1.0), 0.0).astype(np.float32)
+        self._term = rng.random((ring, n)) < self._p_done
 
 
 class SyntheticMultiAgentVecEnv:
@@ -200,6 +215,24 @@ class SyntheticMultiAgentVecEnv:
         pass
 
 
+def _reseed_copy(env, k: int) -> None:
+    """Give a deep-copied env its own random stream: ``reseed(seed)`` when the
+    env offers it (the synthetic envs), else a fresh ``np_random`` generator on
+    the env and on each gymnasium sub-env."""
+    base = int(getattr(env, "seed", 0) or 0) if not callable(getattr(env, "seed", None)) else 0
+    seed = (base + 1_000_003 * k) & 0x7FFFFFFF
+    if callable(getattr(env, "reseed", None)):
+        env.reseed(seed)
+        return
+    subs = list(getattr(env, "envs", []) or [])
+    for j, e in enumerate([env, *subs]):
+        if hasattr(e, "np_random"):
+            try:
+                e.np_random = np.random.default_rng(seed + j)
+            except (AttributeError, TypeError):
+                pass
+
+
 class StackedVecEnv:
     """P vector envs side by side as ONE vector env of sum(num_envs) envs, in
     order (agent p of a population owns the p-th block).  Works with any
@@ -230,10 +263,16 @@ class StackedVecEnv:
         import copy
 
         try:
-            return cls([env] + [copy.deepcopy(env) for _ in range(copies - 1)])
+            clones = [copy.deepcopy(env) for _ in range(copies - 1)]
         except Exception as err:  # noqa: BLE001 - e.g. subprocess-backed vector envs
             raise TypeError(f"cannot clone {type(env).__name__} for {copies} agents ({err}); pass a vector env "
                             f"of population_size x num_envs environments or a StackedVecEnv of one env per agent")
+        # the reference's agents take turns on one env, so each sees different
+        # episodes: give every copy its own random stream instead of the
+        # original's (a deep copy would replay it)
+        for k, c in enumerate(clones, start=1):
+            _reseed_copy(c, k)
+        return cls([env] + clones)
 
     def _split(self, x):
         out, s = [], 0
@@ -260,7 +299,10 @@ class StackedVecEnv:
         return {}
 
     def reset(self, seed=None, options=None, out_obs: np.ndarray | None = None):
-        res = [e.reset() if seed is None else e.reset(seed=seed + k) for k, e in enumerate(self.envs)]
+        # a vector env seeds its sub-envs seed, seed + 1, ...: block k starts
+        # after the blocks before it, so no two sub-envs share a seed
+        offs = np.concatenate([[0], np.cumsum(self.sizes)[:-1]]).tolist()
+        res = [e.reset() if seed is None else e.reset(seed=seed + int(o)) for o, e in zip(offs, self.envs)]
         obs = self._cat([r[0] for r in res], out_obs, self._obs_dtype)
         return obs, self._infos([r[1] for r in res])
 

@@ -158,10 +158,10 @@ class Mutations:
     def _gaussian_parameter_mutation(self, weights: dict) -> None:
         """mutation.py:733-827 on ``weights`` (reference state-dict name ->
         device tensor, in state-dict order): the chosen keys, entries and the
-        normal / super / reset noise drawn exactly as the reference draws them
-        (self.rng, then torch.normal on the CPU generator); each chosen matrix
-        is updated on the host with the reference's CPU indexing semantics and
-        copied back in place."""
+        normal / super / reset noise drawn as a CPU-device reference agent
+        draws them (self.rng, then torch.normal on the global CPU generator);
+        each chosen matrix is updated on the host with the reference's CPU
+        indexing semantics and copied back in place."""
         potential = [k for k, w in weights.items() if w.dim() == 2 and "lstm" not in k and "norm" not in k]
         if not potential:
             return

@@ -123,6 +123,10 @@ class PPOPopulation:
         self._perm_host = None
         self._perm_k = 0
         self._gae_launch = None
+        # target-KL runs: numpy state before the current learn's shuffles, and
+        # the correction owed to the global stream once its epochs_run is known
+        self._perm_drawn_state = None
+        self._kl_pending = None
 
     # ------------------------------------------------------------------ #
     def _alloc_rollout(self):
@@ -229,10 +233,61 @@ class PPOPopulation:
 
             loss = fused_learn(self)
             self.last_kl = self._fused.kl
-            if prefetch and self.prefetch_perms:
+            self._record_kl_pending(self._fused.epochs_run)
+            # with target_kl the next learn's shuffles depend on this one's stops
+            if prefetch and self.prefetch_perms and self.target_kl is None:
                 self.prefetch_permutations()
             return loss
-        return self._learn_torch()
+        loss = self._learn_torch()
+        self._record_kl_pending(self.last_epochs_run)
+        return loss
+
+    # ------------------------------------------------------------------ #
+    # target_kl and the global numpy stream (ppo.py:836-842, 917-918)
+    #
+    # The reference's agents learn one after another, each drawing one
+    # np.random.shuffle per epoch it actually runs; an agent that stops early
+    # on target_kl draws fewer.  The engine draws every agent's E shuffles
+    # before the learn (all agents run at once), so after an early stop:
+    #   * agents after the first early-stopping agent learn from shuffles
+    #     that are shifted against the reference's (agent p's would start at
+    #     shuffle sum(epochs_run[:p]), which is only known once every agent
+    #     before it has finished — a serial dependency the population breaks);
+    #   * the GLOBAL stream is put back in step: once the learn's epochs_run
+    #     is known, the state is rewound to before the draw and advanced by
+    #     exactly sum(epochs_run) shuffles, the reference's count, so every
+    #     later consumer (tournament and mutation draws, the next learn) sees
+    #     the state the reference would.
+    # Without target_kl every agent runs all its epochs and both are exact.
+    def _record_kl_pending(self, epochs_run) -> None:
+        if self.target_kl is None or self.perm_source != "numpy" or self._perm_drawn_state is None:
+            return
+        planned = list(self.agent_epochs) if self.heterogeneous else [self.update_epochs] * self.P
+        ev = None
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+        self._kl_pending = (self._perm_drawn_state, planned, epochs_run, ev)
+        self._perm_drawn_state = None
+
+    def sync_numpy_stream(self) -> None:
+        """Apply the correction a target-KL learn owes the global numpy stream
+        (waits for that learn's epochs_run; see above).  Called before anything
+        draws from the stream: the next permutation draw, tournament and
+        mutation draws (discard_prefetch)."""
+        if self._kl_pending is None:
+            return
+        state, planned, epochs_run, ev = self._kl_pending
+        self._kl_pending = None
+        if ev is not None:
+            ev.synchronize()
+        ran = [int(x) for x in torch.as_tensor(epochs_run).cpu().tolist()]
+        if ran == planned:
+            return
+        np.random.set_state(state)
+        total = int(sum(ran))
+        if total:
+            numpy_shuffle_perms(1, total, self.S)
 
     def check_errors(self) -> None:
         """Raise AgxError if a fused learn() since the last check left an agent's
@@ -334,13 +389,16 @@ class PPOPopulation:
         device draw.  Returns the draw made ahead by prefetch_permutations()
         if there is one (the same draw, in the same order, as drawing here)."""
         if self._perm_next is not None:
-            perms, ev, _ = self._perm_next
+            perms, ev, state = self._perm_next
             self._perm_next = None
+            self._perm_drawn_state = state
             main = torch.cuda.current_stream(self.device)
             main.wait_event(ev)
             perms.record_stream(main)
             return perms
         if self.perm_source == "numpy":
+            self.sync_numpy_stream()
+            self._perm_drawn_state = np.random.get_state(legacy=True)
             host = self._host_perm_buffer()
             numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=host.numpy(),
                                 epochs_per_agent=self.agent_epochs if self.heterogeneous else None)
@@ -396,6 +454,8 @@ class PPOPopulation:
         so the draws stay in the reference's order."""
         if self._perm_next is not None or self.device.type != "cuda":
             return
+        if self.perm_source == "numpy":
+            self.sync_numpy_stream()  # waits for a target-KL learn's epochs_run (before any rollout launch)
         if self._perm_stream is None:
             self._perm_stream = torch.cuda.Stream(device=self.device)
         side = self._perm_stream
@@ -424,6 +484,7 @@ class PPOPopulation:
         before it, so the next consumer of the stream draws what it would have
         drawn without the prefetch (the permutations are re-drawn later)."""
         if self._perm_next is None or self._perm_next[2] is None:
+            self.sync_numpy_stream()
             return  # nothing drawn ahead from numpy (device draws use the pop's own generator)
         perms, ev, state = self._perm_next
         self._perm_next = None
@@ -447,12 +508,15 @@ class PPOPopulation:
             groups.setdefault((self.agent_batch[p], self.agent_epochs[p], self.agent_ent[p]), []).append(p)
         out = torch.zeros(self.P, dtype=torch.float32, device=self.device)
         kl = torch.zeros(self.P, dtype=torch.float32, device=self.device)
+        ran = torch.zeros(self.P, dtype=torch.int32, device=self.device)
         for (b, e, ent), rows in groups.items():
             loss = self._learn_torch_group(perms, rows, b, e, ent)
             idx = torch.tensor(rows, device=self.device)
             out[idx] = loss[idx]
             kl[idx] = self.last_kl[idx]
+            ran[idx] = self.last_epochs_run[idx]
         self.last_kl = kl
+        self.last_epochs_run = ran
         return out
 
     def _learn_torch_group(self, perms, rows, batch_size, epochs, ent_coef) -> torch.Tensor:
@@ -477,7 +541,9 @@ class PPOPopulation:
             member[torch.tensor(rows, device=self.device)] = 1
         active = member  # all (member) agents until one stops (u8 [P])
         plan = [(s, min(s + batch_size, S)) for s in range(0, S, batch_size)]
+        ran = torch.zeros(P, dtype=torch.int32, device=self.device)  # epochs each agent runs
         for e in range(epochs):
+            ran += 1 if active is None else active.int()
             for s0, s1 in plan:
                 idx = perms[e][:, s0:s1]  # [P, b]
                 ob = torch.gather(obs, 1, idx.unsqueeze(-1).expand(-1, -1, D))
@@ -509,6 +575,7 @@ class PPOPopulation:
                 if int(active.sum()) == 0:
                     break
         self.last_kl = (kl_sum / max(n_mb, 1)).float()
+        self.last_epochs_run = ran
         return total / (S * epochs)
 
     # ------------------------------------------------------------------ #

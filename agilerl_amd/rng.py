@@ -6,7 +6,13 @@
   (train_on_policy.py:210).  ``numpy_shuffle_perms`` draws all of a
   population's permutations natively (agx_host_shuffle_perms) from the global
   generator's state and advances that state exactly as the reference's
-  shuffles would, so a seeded run reproduces the reference's minibatches.
+  shuffles would, so a seeded run reproduces the reference's minibatches
+  as long as every agent runs all its epochs.  With ``target_kl`` an agent
+  that stops early draws fewer shuffles in the reference, which shifts every
+  later agent's minibatch order; the population draws all agents' shuffles
+  before its (parallel) learn, so those later agents' orders differ from the
+  reference's, while the global state itself is re-synchronised to the
+  reference's count afterwards (PPOPopulation.sync_numpy_stream).
 """
 
 from __future__ import annotations

@@ -353,3 +353,26 @@ def test_partner_stall_raises():
     fused_learn(pop)
     torch.cuda.synchronize()
     pop.check_errors()
+
+
+def test_target_kl_resyncs_global_numpy_stream():
+    """With target_kl, agents stop after different numbers of epochs and the
+    reference draws one np.random.shuffle per epoch run (ppo.py:836-842,
+    917-918).  After learn() the global numpy state must be the state after
+    exactly sum(epochs_run) shuffles from the state before the learn, so every
+    later consumer of the stream (tournament, mutations, the next learn) sees
+    the reference's state."""
+    from agilerl_amd.rng import numpy_shuffle_perms
+
+    pop, _, _ = _config2_population(0.0035, True)
+    np.random.seed(77)
+    pop.learn()
+    torch.cuda.synchronize()
+    pop.check_errors()
+    ran = pop._fused.epochs_run.cpu().numpy()
+    assert len(set(ran.tolist())) > 1 and ran.sum() < pop.P * 4, ran
+    pop.sync_numpy_stream()
+    got = np.random.randint(0, 2**31 - 1, 8)
+    np.random.seed(77)
+    numpy_shuffle_perms(1, int(ran.sum()), pop.S)
+    assert np.array_equal(got, np.random.randint(0, 2**31 - 1, 8))
