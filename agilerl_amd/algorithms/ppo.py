@@ -321,9 +321,9 @@ class PPO:
             self._counter += 1
             params = pop.params.data[self.row]
             _lib.call("agx_ppo_act", ctypes.byref(desc), 1, n, params.data_ptr(), o.data_ptr(), 0, _lib.ptr(mask), 0,
-                      1, pop.act_seed + 7919 * self.row, (1 << 40) + self._counter, out["actions"].data_ptr(),
-                      out["log_probs"].data_ptr(), out["values"].data_ptr(), out["entropy"].data_ptr(), 0, None,
-                      None, _lib.stream())
+                      1, pop.act_seed + 7919 * (pop.agent_offset + self.row), (1 << 40) + self._counter,
+                      out["actions"].data_ptr(), out["log_probs"].data_ptr(), out["values"].data_ptr(),
+                      out["entropy"].data_ptr(), 0, None, 0, _lib.stream())
         return tuple(out[k].cpu().numpy() for k in ("actions", "log_probs", "entropy", "values"))
 
     def learn(self, experiences=None) -> float:

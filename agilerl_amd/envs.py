@@ -259,20 +259,24 @@ class StackedVecEnv:
         self._obs_dtype = np.uint8 if getattr(space, "dtype", None) == np.uint8 else np.float32
 
     @classmethod
-    def from_shared(cls, env, copies: int) -> "StackedVecEnv":
+    def from_shared(cls, env, copies: int, offset: int = 0) -> "StackedVecEnv":
+        """``offset``: global index of the first agent (a population sharded
+        over ranks): copy k behaves as the unsharded population's copy
+        offset + k, copy 0 of the global population being ``env`` itself."""
         import copy
 
         try:
-            clones = [copy.deepcopy(env) for _ in range(copies - 1)]
+            clones = [copy.deepcopy(env) for _ in range(copies - (1 if offset == 0 else 0))]
         except Exception as err:  # noqa: BLE001 - e.g. subprocess-backed vector envs
             raise TypeError(f"cannot clone {type(env).__name__} for {copies} agents ({err}); pass a vector env "
                             f"of population_size x num_envs environments or a StackedVecEnv of one env per agent")
         # the reference's agents take turns on one env, so each sees different
         # episodes: give every copy its own random stream instead of the
         # original's (a deep copy would replay it)
-        for k, c in enumerate(clones, start=1):
+        first = 1 if offset == 0 else offset
+        for k, c in enumerate(clones, start=first):
             _reseed_copy(c, k)
-        return cls([env] + clones)
+        return cls(([env] if offset == 0 else []) + clones)
 
     def _split(self, x):
         out, s = [], 0

@@ -43,6 +43,10 @@ class PopulationSync:
         self._idx_h = None     # pinned parent indices -> device, non-blocking
         self._idx_d = None
         self._idx_ev = None
+        # gloo moves host tensors only: device rows cross through host staging
+        self.comm_device = pop.device
+        if world > 1 and dist.get_backend() == "gloo":
+            self.comm_device = torch.device("cpu")
 
     def _fitness_host(self) -> np.ndarray:
         """Every rank's fitness on the host.  The episode statistics are final
@@ -84,9 +88,10 @@ class PopulationSync:
     def _all_gather(self, x: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
             return x
-        out = torch.empty((self.world * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
-        dist.all_gather_into_tensor(out, x.contiguous())
-        return out
+        src = x.contiguous().to(self.comm_device)
+        out = torch.empty((self.world * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=self.comm_device)
+        dist.all_gather_into_tensor(out, src)
+        return out.to(x.device)
 
     def _dev_index(self, rows: list[int]) -> torch.Tensor:
         """A small index list on the device without a blocking copy: pinned
@@ -170,13 +175,13 @@ class PopulationSync:
             rows = need[dst][me]
             if rows:
                 idx = torch.as_tensor(rows, device=pop.device)
-                msg = torch.cat([b.index_select(0, idx) for b in bufs], dim=1).contiguous()
+                msg = torch.cat([b.index_select(0, idx) for b in bufs], dim=1).contiguous().to(self.comm_device)
                 sends.append(msg)
                 ops.append(dist.P2POp(dist.isend, msg, dst))
         for src in range(self.world):
             rows = need[me][src]
             if rows:
-                recv[src] = torch.empty(len(rows), offs[-1], dtype=bufs[0].dtype, device=pop.device)
+                recv[src] = torch.empty(len(rows), offs[-1], dtype=bufs[0].dtype, device=self.comm_device)
                 ops.append(dist.P2POp(dist.irecv, recv[src], src))
         local = [j for j in range(P) if mine[j] // P == me]
         snap = None
@@ -195,7 +200,7 @@ class PopulationSync:
             js = [j for j in range(P) if mine[j] // P == src]
             sel = torch.as_tensor([pos[mine[j] % P] for j in js], device=pop.device)
             dst_idx = torch.as_tensor(js, device=pop.device)
-            rows = msg.index_select(0, sel)
+            rows = msg.to(pop.device).index_select(0, sel)
             for k, b in enumerate(bufs):
                 b.index_copy_(0, dst_idx, rows[:, offs[k]:offs[k + 1]])
 

@@ -1,0 +1,236 @@
+"""The generation step of a population sharded over ranks, drawn once over
+the GLOBAL population.
+
+The reference mutates the whole population in one process, agent after
+agent (utils/utils.py:1185-1211 -> hpo/mutation.py:311-362): one
+``rng.choice`` over every agent, then each agent's own draws in population
+order (RL-hyperparameter draws from the global torch generator, parameter
+noise from ``Mutations.rng`` and torch.normal).  A rank that mutated only
+its own shard would hand local agent j of every rank the same choice and the
+same noise.  Here every rank runs the reference's loop over ALL G*P agents:
+
+  * its own agents are the real objects, mutated in place;
+  * the other ranks' agents are ``RemoteAgent`` stand-ins built from a
+    gathered host record (hyperparameters, mutation registry, weight shapes):
+    they take exactly the draws the real agent takes (the same calls run on
+    zero tensors of the same shapes) and their results are discarded — the
+    owning rank computes the same values for its real agent.
+
+So the draws happen once, in the global order, identically on every rank,
+and rank r keeps global slots r*P .. r*P + P - 1: the sharded population
+equals the single-process one.  Before the draws the host generators
+(numpy global, torch CPU, Python ``random``) are broadcast from rank 0, so a
+rank whose local work consumed a stream differently (an off-policy rank's
+own replay sampling) cannot desynchronise the selection or the mutations.
+
+A mutation registry shared by construction (``create_population`` hands
+every agent one ``hp_config`` object, whose ``RLParameter.value`` then
+carries over from one agent's mutation to the next, registry.py) is shared
+across ranks the same way: when every rank's agents share one object, the
+stand-ins use the local shared object, which every rank advances through
+the identical global sequence.
+"""
+
+from __future__ import annotations
+
+import copy
+import random
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+#: per-agent RL hyperparameters a PPO view exposes as properties (not in vars)
+_PPO_HP = ("lr", "batch_size", "update_epochs", "ent_coef", "learn_step")
+
+
+def world_rank(group=None) -> tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def all_ranks(flag: bool, group=None) -> bool:
+    """True on every rank iff ``flag`` holds on every rank (a decision that
+    ends a rank's loop must be the same everywhere)."""
+    world, _ = world_rank(group)
+    if world == 1:
+        return bool(flag)
+    box: list = [None] * world
+    dist.all_gather_object(box, bool(flag), group=group)
+    return all(box)
+
+
+def sync_host_rngs(group=None) -> None:
+    """Every rank takes rank 0's numpy global, torch CPU and Python random
+    states (one object broadcast, a few KB)."""
+    world, rank = world_rank(group)
+    if world == 1:
+        return
+    box = [(np.random.get_state(legacy=True), torch.get_rng_state(), random.getstate())] if rank == 0 else [None]
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast_object_list(box, src=src, group=group)
+    if rank != 0:
+        np_state, t_state, py_state = box[0]
+        np.random.set_state(np_state)
+        torch.set_rng_state(t_state)
+        random.setstate(py_state)
+
+
+def _weight_groups(agent) -> list[dict[str, torch.Tensor]]:
+    if hasattr(agent, "policy_weight_groups"):
+        return agent.policy_weight_groups()
+    if hasattr(agent, "policy_weights"):
+        return [agent.policy_weights()]
+    return []
+
+
+def host_record(agent) -> dict:
+    """What another rank needs to replay this agent's mutation draws and to
+    clone its host attributes: plain attributes, the hyperparameters the
+    registry can mutate, the registry itself, the learning-rate names and the
+    shapes of the policy's weights."""
+    from .sharded import plain_attributes
+
+    rec = plain_attributes(agent)
+    hp = {}
+    names = set(_PPO_HP) if hasattr(agent, "population") else set()
+    registry = getattr(agent, "registry", None)
+    cfg = getattr(registry, "hp_config", None)
+    if cfg:
+        names |= set(cfg.names())
+    for name in sorted(names):
+        try:
+            hp[name] = getattr(agent, name)
+        except (AttributeError, NotImplementedError):
+            pass
+    rec["_hp"] = hp
+    rec["_registry"] = registry
+    rec["_lr_names"] = list(agent.get_lr_names()) if hasattr(agent, "get_lr_names") else []
+    rec["_weights"] = [[(k, tuple(t.shape), str(t.dtype).replace("torch.", "")) for k, t in g.items()]
+                       for g in _weight_groups(agent)]
+    rec["_groups_api"] = hasattr(agent, "policy_weight_groups")
+    return rec
+
+
+class RemoteAgent:
+    """Stand-in for an agent another rank owns: takes the same mutation draws
+    (hyperparameter reads and writes, zero tensors of the policy's weight
+    shapes for parameter noise); nothing it computes is used."""
+
+    def __init__(self, rec: dict, registry) -> None:
+        d = self.__dict__
+        for k, v in rec.items():
+            if not k.startswith("_"):
+                d[k] = copy.deepcopy(v)
+        d["registry"] = registry
+        d["_hp"] = dict(rec["_hp"])
+        d["_lr_names"] = list(rec["_lr_names"])
+        d["_weights"] = rec["_weights"]
+        d["_groups_api"] = rec["_groups_api"]
+
+    def __getattr__(self, name):
+        hp = self.__dict__.get("_hp", {})
+        if name in hp:
+            return hp[name]
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value) -> None:
+        if name in self.__dict__.get("_hp", {}):
+            self.__dict__["_hp"][name] = value
+        else:
+            self.__dict__[name] = value
+
+    def _zeros(self) -> list[dict[str, torch.Tensor]]:
+        return [{k: torch.zeros(shape, dtype=getattr(torch, dt)) for k, shape, dt in g} for g in self._weights]
+
+    def policy_weight_groups(self):
+        return self._zeros()
+
+    def policy_weights(self):
+        return self._zeros()[0]
+
+    def get_lr_names(self) -> list[str]:
+        return list(self._lr_names)
+
+    def reinit_optimizers(self, *args, **kwargs) -> None:
+        pass
+
+    def sync_shared_networks(self) -> None:
+        pass
+
+    def mutation_hook(self) -> None:
+        pass
+
+
+def gather_records(pop, group=None) -> list[dict]:
+    """Every rank's agent records, in global agent order."""
+    world, _ = world_rank(group)
+    local = [host_record(a) for a in pop]
+    if world == 1:
+        return local
+    box: list = [None] * world
+    dist.all_gather_object(box, local, group=group)
+    if any(len(b) != len(pop) for b in box):
+        raise ValueError("every rank must hold the same number of agents")
+    return [r for b in box for r in b]
+
+
+def mark_shared(hp_config) -> None:
+    """Tag an hp_config that create_population hands to every agent; a deep
+    copy (a clone's) no longer matches its tag, so it counts as private."""
+    if hp_config is not None:
+        try:
+            hp_config._agx_share_id = id(hp_config)
+        except AttributeError:
+            pass
+
+
+def _locally_shared_registry(pop):
+    """A registry whose hp_config every local agent shares by construction
+    (create_population's), or None."""
+    regs = [getattr(a, "registry", None) for a in pop]
+    cfgs = [getattr(r, "hp_config", None) for r in regs]
+    c0 = cfgs[0] if cfgs else None
+    if c0 is not None and all(c is c0 for c in cfgs) and getattr(c0, "_agx_share_id", None) == id(c0):
+        return regs[0]
+    return None
+
+
+def global_view(pop, records: list[dict], group=None) -> list:
+    """The global population as seen from this rank: its own agents in their
+    global slots, RemoteAgent stand-ins elsewhere."""
+    world, rank = world_rank(group)
+    P = len(pop)
+    shared = _locally_shared_registry(pop)
+    flags = [shared is not None]
+    if world > 1:
+        box: list = [None] * world
+        dist.all_gather_object(box, flags, group=group)
+        all_shared = all(b[0] for b in box)
+    else:
+        all_shared = flags[0]
+    out = []
+    for g, rec in enumerate(records):
+        if g // P == rank:
+            out.append(pop[g % P])
+        else:
+            out.append(RemoteAgent(rec, shared if all_shared else copy.deepcopy(rec["_registry"])))
+    return out
+
+
+def mutate_population(mutation, pop, pre_training_mut: bool = False, group=None):
+    """``mutation.mutation(pop)`` over the global population; returns this
+    rank's slice (the real agents, mutated)."""
+    world, rank = world_rank(group)
+    if world == 1:
+        return mutation.mutation(pop, pre_training_mut=pre_training_mut)
+    sync_host_rngs(group)
+    records = gather_records(pop, group)
+    glob = global_view(pop, records, group)
+    out = mutation.mutation(glob, pre_training_mut=pre_training_mut)
+    P = len(pop)
+    mine = out[rank * P:(rank + 1) * P]
+    if any(isinstance(a, RemoteAgent) for a in mine):
+        raise RuntimeError("mutation returned a stand-in in this rank's slots")
+    return mine

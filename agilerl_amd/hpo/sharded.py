@@ -151,7 +151,8 @@ class ShardedTournamentSelection:
         t, world, me = self.tournament, self.world, self.rank
         P = len(population)
         nbytes = sum(x.numel() * x.element_size() for x in state_tensors(population[0]))
-        info = [dict(plain_attributes(a), _nbytes=sum(x.numel() * x.element_size() for x in state_tensors(a)))
+        info = [dict(plain_attributes(a), _nbytes=sum(x.numel() * x.element_size() for x in state_tensors(a)),
+                     _registry=getattr(a, "registry", None))  # a clone deep-copies the parent's (values included)
                 for a in population]
         if world > 1:
             gathered: list = [None] * world
@@ -209,8 +210,12 @@ class ShardedTournamentSelection:
                 child = population[0].clone(new_index[g], wrap=False)
                 unpack_agent(child, recv[src][k * nbytes:(k + 1) * nbytes])
                 for name, v in meta[q].items():
-                    if name != "_nbytes":
+                    if name not in ("_nbytes", "_registry"):
                         setattr(child, name, copy.deepcopy(v))
+                if meta[q]["_registry"] is not None:
+                    child.registry = copy.deepcopy(meta[q]["_registry"])
+                    if hasattr(child, "hp_config"):
+                        child.hp_config = child.registry.hp_config
                 child.index = new_index[g]
             new_pop.append(child)
         elite = new_pop[0].clone(wrap=False) if (t.elitism and me == 0) else None

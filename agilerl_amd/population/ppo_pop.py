@@ -42,7 +42,7 @@ import torch
 
 from .. import _lib
 from .. import kernels as K
-from ..rng import numpy_shuffle_perms
+from ..rng import numpy_shuffle_perms, numpy_shuffle_perms_shard
 from .nets import ActorCriticSpec, categorical
 
 
@@ -70,9 +70,18 @@ class PPOPopulation:
     def __init__(self, spec: ActorCriticSpec, pop_size: int, num_envs: int, *, learn_step=2048,
                  batch_size=128, lr=1e-3, gamma=0.99, gae_lambda=0.95, clip_coef=0.2, ent_coef=0.01,
                  vf_coef=0.5, max_grad_norm=0.5, update_epochs=4, target_kl=None, seeds=None,
-                 device="cuda", fused=True, perm_source="numpy", action_masks=False):
+                 device="cuda", fused=True, perm_source="numpy", action_masks=False, agent_offset=0,
+                 global_pop_size=None, seed_base=None):
         self.spec = spec
         self.P, self.N = int(pop_size), int(num_envs)
+        # a shard of a population spread over ranks: these P agents are global
+        # agents agent_offset .. agent_offset + P of global_pop_size (their
+        # sampling streams, env copies and minibatch shuffles are the global
+        # agents' own, so the sharded run draws what one process would)
+        self.agent_offset = int(agent_offset)
+        self.global_P = self.P if global_pop_size is None else int(global_pop_size)
+        if self.agent_offset < 0 or self.agent_offset + self.P > self.global_P:
+            raise ValueError("agent_offset / global_pop_size do not contain this shard")
         self.T = -(learn_step // -self.N)  # capacity = ceil(learn_step / num_envs), ppo.py:363
         self.S = self.T * self.N
         self.batch_size = int(batch_size)
@@ -82,15 +91,17 @@ class PPOPopulation:
         self.update_epochs = int(update_epochs)
         self.target_kl = target_kl
         self.device = torch.device(device)
-        seeds = list(range(self.P)) if seeds is None else list(seeds)
+        seeds = list(range(self.agent_offset, self.agent_offset + self.P)) if seeds is None else list(seeds)
         self.seeds = seeds
+        # population-level streams key off the global population's first seed
+        seed_base = int(seeds[0]) if seed_base is None else int(seed_base)
         self.params = torch.nn.Parameter(spec.init_params(self.P, seeds, self.device))
         self.params.grad = torch.zeros_like(self.params)
         lr_list = [float(lr)] * self.P if not isinstance(lr, (list, tuple)) else [float(x) for x in lr]
         self.opt = K.ClipAdam(self.params.data, spec.group_offsets, lr_list, max_norm=self.max_grad_norm,
                               grads=self.params.grad)
         self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(int(seeds[0]) * 7919 + 17)
+        self.gen.manual_seed(seed_base * 7919 + 17)
         if perm_source not in ("numpy", "device"):
             raise ValueError("perm_source must be 'numpy' or 'device'")
         self.perm_source = perm_source
@@ -111,7 +122,11 @@ class PPOPopulation:
         self.hp_ent_d = torch.full((self.P,), self.ent_coef, dtype=torch.float32, device=self.device)
         self._hetero = False
         self.fused = fused
-        self.act_seed = (int(seeds[0]) * 0x9E3779B97F4A7C15 + 0x5851F42D) & 0xFFFFFFFFFFFFFFFF
+        self.act_seed = (seed_base * 0x9E3779B97F4A7C15 + 0x5851F42D) & 0xFFFFFFFFFFFFFFFF
+        # every global agent's update_epochs (the shuffles each draws; ranks
+        # refresh the other shards' entries after a mutation)
+        self.global_epochs = [self.update_epochs] * self.global_P
+        self._shard_scratch: dict = {}
         self.act_counter = 0
         self._desc = None
         self._alloc_rollout()
@@ -400,8 +415,7 @@ class PPOPopulation:
             self.sync_numpy_stream()
             self._perm_drawn_state = np.random.get_state(legacy=True)
             host = self._host_perm_buffer()
-            numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=host.numpy(),
-                                epochs_per_agent=self.agent_epochs if self.heterogeneous else None)
+            self._draw_numpy_perms(host.numpy())
             perms = host.to(self.device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
@@ -409,6 +423,17 @@ class PPOPopulation:
             return perms
         keys = torch.rand(self.update_epochs, self.P, self.S, generator=self.gen, device=self.device)
         return torch.argsort(keys, dim=-1)
+
+    def _draw_numpy_perms(self, out: np.ndarray) -> None:
+        """[E, P, S] from the global numpy stream: this shard's agents' shuffles
+        in the global agent order (rng.py)."""
+        if self.global_P == self.P:
+            numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=out,
+                                epochs_per_agent=self.agent_epochs if self.heterogeneous else None)
+            return
+        eg = list(self.global_epochs)
+        eg[self.agent_offset:self.agent_offset + self.P] = self.agent_epochs
+        numpy_shuffle_perms_shard(out, self.agent_offset, self.global_P, eg, self._shard_scratch)
 
     def _host_perm_buffer(self) -> torch.Tensor:
         """One of two pinned [E, P, S] int64 host buffers, alternating (the H2D
@@ -463,8 +488,7 @@ class PPOPopulation:
         if self.perm_source == "numpy":
             state = np.random.get_state(legacy=True)
             host = self._host_perm_buffer()
-            numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=host.numpy(),
-                                epochs_per_agent=self.agent_epochs if self.heterogeneous else None)
+            self._draw_numpy_perms(host.numpy())
             with torch.cuda.stream(side):
                 perms = host.to(self.device, non_blocking=True)
                 ev = torch.cuda.Event()

@@ -53,6 +53,7 @@ class AgxRolloutIO(ctypes.Structure):
         ("slot_agent_stride", ctypes.c_int64), ("actions_flat", ctypes.c_void_p),
         ("scores", ctypes.c_void_p), ("return_sum", ctypes.c_void_p), ("episodes", ctypes.c_void_p),
         ("stage_mask", ctypes.c_void_p), ("mask_slot", ctypes.c_void_p), ("mask_agent_stride", ctypes.c_int64),
+        ("env_base", ctypes.c_int64),
     ]
 
 
@@ -206,6 +207,7 @@ class PopulationRunner:
                 io.values = self.last_value.data_ptr()
                 io.slot_agent_stride = N
             io.prev_agent_stride = T * N
+            io.env_base = pop.agent_offset * N  # a sharded population samples the global envs' streams
             ios[t] = io
         self._ios = ios
 

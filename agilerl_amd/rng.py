@@ -59,3 +59,35 @@ def numpy_shuffle_perms(P: int, epochs: int, S: int, out: np.ndarray | None = No
                "agx_host_shuffle_perms")
     np.random.set_state(("MT19937", key, int(pos_c.value), has_gauss, gauss))
     return out
+
+
+def numpy_shuffle_perms_shard(out: np.ndarray, offset: int, global_P: int, epochs_global: list[int],
+                              scratch: dict | None = None) -> np.ndarray:
+    """The local slice of a population sharded over ranks: agents
+    ``offset .. offset + P`` of the ``global_P`` agents that would learn one
+    after another in the reference.  The shuffles of the agents before and
+    after the slice are drawn too (into scratch, discarded), so the global
+    generator ends where the unsharded population's draw leaves it and every
+    rank's stream stays identical.  ``out``: [E, P, S] int64 (E >= the local
+    agents' epochs); ``epochs_global``: every global agent's epochs."""
+    E, P, S = out.shape
+    eg = [int(e) for e in epochs_global]
+    if len(eg) != global_P or offset < 0 or offset + P > global_P:
+        raise ValueError("shard outside the global population")
+    scratch = {} if scratch is None else scratch
+
+    def _skip(lo: int, hi: int) -> None:
+        if hi <= lo:
+            return
+        e = max(eg[lo:hi])
+        key = (e, hi - lo, S)
+        buf = scratch.get(key)
+        if buf is None:
+            buf = scratch[key] = np.empty(key, dtype=np.int64)
+        numpy_shuffle_perms(hi - lo, e, S, out=buf, epochs_per_agent=eg[lo:hi])
+
+    _skip(0, offset)
+    local = eg[offset:offset + P]
+    numpy_shuffle_perms(P, E, S, out=out, epochs_per_agent=None if all(x == E for x in local) else local)
+    _skip(offset + P, global_P)
+    return out

@@ -16,6 +16,7 @@ from __future__ import annotations
 import numpy as np
 
 from ..components.sampler import Sampler
+from ..hpo.shard import all_ranks, mutate_population, sync_host_rngs
 from ..hpo.sharded import select_population
 
 
@@ -28,7 +29,7 @@ def train_multi_agent_off_policy(env, env_name: str, algo: str, pop, memory, INI
                                  wb: bool = False, verbose: bool = True, accelerator=None, wandb_api_key=None,
                                  wandb_kwargs=None):
     if mutation is not None:  # pre-training mutation (the reference's :238-240 / :204-206)
-        pop = mutation.mutation(pop, pre_training_mut=True)
+        pop = mutate_population(mutation, pop, pre_training_mut=True)
     vec = hasattr(env, "num_envs")
     num_envs = env.num_envs if vec else 1
     sampler = Sampler(memory=memory)
@@ -83,10 +84,11 @@ def train_multi_agent_off_policy(env, env_name: str, algo: str, pop, memory, INI
             print(f"--- {env_name} {algo}: steps {[a.steps[-1] for a in pop]}, fitness {fitnesses}")
         for agent in pop:
             agent.steps.append(agent.steps[-1])
-        if target is not None and np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target)) \
+        if target is not None and all_ranks(np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target))) \
                 and len(pop[0].steps) >= 100:
             return pop, pop_fitnesses
         if tournament and mutation is not None:  # tournament_selection_and_mutation (:525-535)
+            sync_host_rngs()  # every rank draws the selection and mutations from one state
             _, pop = select_population(tournament, pop)
-            pop = mutation.mutation(pop)
+            pop = mutate_population(mutation, pop)
     return pop, pop_fitnesses

@@ -13,7 +13,15 @@ reference) the tournament (``TournamentSelection.select``, global numpy RNG)
 replaces the population and ``mutation.mutation`` mutates it (RL
 hyperparameters, Q-network parameters with the target synced).  The replay
 trees, TD / C51 losses and Polyak updates run in libagx.  Returns
-(pop, pop_fitnesses)."""
+(pop, pop_fitnesses).
+
+Sharded over ranks (``create_population`` under a process group), each rank
+runs its slice of the population on its own env and its own replay (a
+documented deviation from the one shared memory, SURVEY §8e option ii); the
+generation step is taken once over the global population on every rank:
+the host generators are synchronised, the tournament selects over every
+agent (hpo/sharded.py) and the mutations draw for every agent in the global
+order (hpo/shard.py), each rank keeping its slice."""
 
 from __future__ import annotations
 
@@ -21,6 +29,7 @@ import numpy as np
 
 from ..algorithms.dqn import DQN, RainbowDQN
 from ..components.sampler import Sampler
+from ..hpo.shard import all_ranks, mutate_population, sync_host_rngs, world_rank
 from ..hpo.sharded import select_population
 
 
@@ -33,7 +42,7 @@ def train_off_policy(env, env_name: str, algo: str, pop, memory, INIT_HP=None, M
                      elite_path=None, wb: bool = False, verbose: bool = True, accelerator=None, wandb_api_key=None,
                      wandb_kwargs=None):
     if mutation is not None:  # pre-training mutation (the reference's :238-240 / :204-206)
-        pop = mutation.mutation(pop, pre_training_mut=True)
+        pop = mutate_population(mutation, pop, pre_training_mut=True)
     num_envs = env.num_envs if hasattr(env, "num_envs") else 1
     sampler = Sampler(memory=memory)
     n_step_sampler = Sampler(memory=n_step_memory) if n_step_memory is not None else None
@@ -99,18 +108,27 @@ def train_off_policy(env, env_name: str, algo: str, pop, memory, INIT_HP=None, M
             eps_start = epsilon  # train_off_policy.py:456-458: the next generation starts where this one ended
         fitnesses = [agent.test(env, swap_channels=swap_channels, max_steps=eval_steps, loop=eval_loop)
                      for agent in pop]
-        pop_fitnesses.append(fitnesses)
+        world, _ = world_rank()
+        if world > 1:  # every global agent's fitness, as the single-process run returns
+            import torch.distributed as dist
+
+            box: list = [None] * world
+            dist.all_gather_object(box, fitnesses)
+            pop_fitnesses.append([f for b in box for f in b])
+        else:
+            pop_fitnesses.append(fitnesses)
         if verbose:
             print(f"--- {env_name} {algo}: steps {[a.steps[-1] for a in pop]}, fitness "
                   f"{[round(f, 2) for f in fitnesses]}")
         for agent in pop:
             agent.steps.append(agent.steps[-1])
-        if target is not None and np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target)) \
+        if target is not None and all_ranks(np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target))) \
                 and len(pop[0].steps) >= 100:
             return pop, pop_fitnesses
         if tournament and mutation is not None:
             # tournament_selection_and_mutation (utils.py:1137-1225, train_off_policy.py:557-565):
             # under an initialised process group each rank holds a shard of the population
+            sync_host_rngs()  # every rank draws the selection and mutations from one state
             _, pop = select_population(tournament, pop)
-            pop = mutation.mutation(pop)
+            pop = mutate_population(mutation, pop)
     return pop, pop_fitnesses

@@ -28,6 +28,14 @@ Per generation, as the reference:
     (save_population_checkpoint, utils.py:1087-1135): ``{path}_{i}.pt`` or
     ``{path}_{i}_{steps}.pt``.
 Returns (pop, pop_fitnesses) like the reference.
+
+Sharded over ranks (``create_population`` under a process group of G > 1:
+rank r holds global agents r*P ..), the run is the single-process run of the
+G*P-agent population: each agent samples its global env's stream, learns
+from its global shuffles, and the generation step (fitness all-gather,
+tournament, host attributes of the clones, mutations) is taken once over the
+global population on every rank (hpo/shard.py), each rank keeping its slice.
+``pop_fitnesses`` holds every global agent's fitness.
 """
 
 from __future__ import annotations
@@ -41,42 +49,53 @@ import torch.distributed as dist
 
 from ..envs import StackedVecEnv
 from ..hpo.population_sync import PopulationSync
+from ..hpo.shard import all_ranks, gather_records, mutate_population
 from ..population.runner import PopulationRunner
 
 
-def _population_env(env, P: int, N: int):
+def _population_env(env, P: int, N: int, offset: int = 0):
     if env.num_envs == P * N:
         return env
     if env.num_envs == N:
-        return env if P == 1 else StackedVecEnv.from_shared(env, P)
+        return env if P == 1 and offset == 0 else StackedVecEnv.from_shared(env, P, offset)
     raise ValueError(f"env has {env.num_envs} environments; the population needs num_envs = {N} (the reference's "
                      f"shared env, cloned per agent) or population_size x num_envs = {P * N}")
 
 
-def _clone_host_attributes(pop, parents: list[int], elitism: bool, fitness_of=None) -> None:
+def _clone_host_attributes(pop, parents: list[int], elitism: bool, records: list[dict], rank: int = 0) -> None:
     """The attributes TournamentSelection._select_standard_agents gives the
     clones (tournament.py:71-119 + clone/copy_attributes, core/base.py:
-    444-503, 871-937): new agent j is a copy of old agent parents[j]; the
-    elite keeps its index, every other clone gets max_id + 1, + 2, ...  With
-    several ranks a parent may live elsewhere: its fitness history comes
-    from the gathered record (``fitness_of``), the rest stays local."""
+    444-503, 871-937), over the GLOBAL population: new agent g is a copy of
+    old agent parents[g] (``records``: every global agent's host record,
+    taken before the clone); the elite keeps its index, every other clone
+    gets max_id + 1, + 2, ... in global slot order.  This rank applies its
+    own slots."""
+    import copy as _copy
+
     P = len(pop)
-    old = [dict(index=a.index, fitness=list(a.fitness), scores=list(a.scores), steps=list(a.steps),
-                registry=a.registry, mut=a.mut) for a in pop]
-    max_id = max(o["index"] for o in old)
-    for j, q in enumerate(parents):
-        a = pop[j]
-        src = old[q] if q < P and fitness_of is None else None
-        if src is not None:
-            a.fitness, a.scores, a.steps = (copy.deepcopy(src[k]) for k in ("fitness", "scores", "steps"))
-            a.registry, a.mut = copy.deepcopy(src["registry"]), src["mut"]
-        elif fitness_of is not None:
-            a.fitness = list(fitness_of(q))
-        if elitism and j == 0:
-            a.index = old[q]["index"] if src is not None else a.index
+    max_id = max(r["index"] for r in records)
+    for g, q in enumerate(parents):
+        if elitism and g == 0:
+            new_index = records[q]["index"]
         else:
             max_id += 1
-            a.index = max_id
+            new_index = max_id
+        if g // P != rank:
+            continue
+        a, src = pop[g % P], records[q]
+        a.fitness, a.scores, a.steps = (_copy.deepcopy(src[k]) for k in ("fitness", "scores", "steps"))
+        a.registry, a.mut = _copy.deepcopy(src["_registry"]), src.get("mut")
+        a.index = new_index
+
+
+def _sync_global_epochs(population) -> None:
+    """Every global agent's update_epochs (the shuffles each draws) after a
+    mutation may have changed another shard's."""
+    if population.global_P == population.P:
+        return
+    box: list = [None] * dist.get_world_size()
+    dist.all_gather_object(box, list(population.agent_epochs))
+    population.global_epochs = [int(e) for b in box for e in b]
 
 
 def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None, swap_channels: bool = False,
@@ -92,9 +111,11 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
     if any(a.population is not population for a in pop):
         raise ValueError("all agents must come from one agilerl_amd.utils.create_population call")
     P, N, T = population.P, population.N, population.T
-    env = _population_env(env, P, N)
-    runner = PopulationRunner(population, env)
     world, rank = (dist.get_world_size(), dist.get_rank()) if dist.is_initialized() else (1, 0)
+    if population.global_P not in (P, P * world) or population.agent_offset not in (0, rank * P):
+        raise ValueError("the population's shard does not match this process group")
+    env = _population_env(env, P, N, population.agent_offset)
+    runner = PopulationRunner(population, env)
     sync = None
     if tournament is not None and mutation is not None:  # the reference selects only with both (:440)
         sync = PopulationSync(population, runner, world, rank, seed=None, tournament_size=tournament.tournament_size,
@@ -103,7 +124,8 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
                  else f"{env_name}-EvoHPO-{algo}-{datetime.now().strftime('%m%d%Y%H%M%S')}")
     checkpoint_count = 0
     if mutation is not None:  # pre-training mutation (:200-201)
-        pop = mutation.mutation(pop, pre_training_mut=True)
+        pop = mutate_population(mutation, pop, pre_training_mut=True)
+        _sync_global_epochs(population)
     iters_per_gen = max(1, -(-evo_steps // (T * N)))
     pop_fitnesses: list[list[float]] = []
     t0 = time.time()
@@ -126,30 +148,35 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
                 agent.scores.append(float(r_sum[i] / r_cnt[i]))
             agent.fitness.append(fitness[i])
             agent.steps.append(agent.steps[-1])
-        pop_fitnesses.append(fitness)
-        if target is not None and np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target)) \
+        if world > 1:
+            box: list = [None] * world
+            dist.all_gather_object(box, fitness)
+            pop_fitnesses.append([f for b in box for f in b])
+        else:
+            pop_fitnesses.append(fitness)
+        if target is not None and all_ranks(np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target))) \
                 and len(pop[0].steps) >= 100:
             return pop, pop_fitnesses
         if sync is not None:  # tournament_selection_and_mutation (utils.py:1137-1225)
+            records = gather_records(pop)  # every global agent's host attributes, before the clone
             sync.fitness_override = np.asarray(fitness)  # reduced on the host already: hand it over
             parents = sync.generation()
-            mine = parents[rank * P:(rank + 1) * P]
-            hist = sync.history
-            fit_of = None if world == 1 else (lambda q: [h[q] for h in hist])
-            _clone_host_attributes(pop, [q % P if world == 1 else q for q in mine], tournament.elitism, fit_of)
+            _clone_host_attributes(pop, parents, tournament.elitism, records, rank)
             if save_elite and tournament.elitism and rank == 0:
                 # the reference saves ``elite``, the unmutated clone of the best agent
                 # (utils.py:1214-1223): slot 0 holds exactly that until mutation runs
                 elite_save_path = elite_path.split(".pt")[0] if elite_path is not None else f"{env_name}-elite_{algo}"
                 pop[0].save_checkpoint(f"{elite_save_path}.pt")
-            pop = mutation.mutation(pop)
+            pop = mutate_population(mutation, pop)
+            _sync_global_epochs(population)
         if verbose:
             fps = sum(a.steps[-1] for a in pop) / max(time.time() - t0, 1e-9)
             print(f"--- {env_name} {algo}: steps {[a.steps[-1] for a in pop]}, fitness "
                   f"{[round(f, 2) for f in fitness]}, mean loss {np.mean(losses):.4f}, "
                   f"mutations {[a.mut for a in pop]}, {fps:.0f} env-steps/s")
         if checkpoint is not None and pop[0].steps[-1] // checkpoint > checkpoint_count:
-            for i, agent in enumerate(pop):  # save_population_checkpoint (utils.py:1126-1135)
+            for j, agent in enumerate(pop):  # save_population_checkpoint (utils.py:1126-1135)
+                i = population.agent_offset + j  # the global slot
                 agent.save_checkpoint(f"{save_path}_{i}.pt" if overwrite_checkpoints
                                       else f"{save_path}_{i}_{agent.steps[-1]}.pt")
             checkpoint_count += 1

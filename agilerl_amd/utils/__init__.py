@@ -3,7 +3,17 @@
 For PPO the agents are views of ONE HBM-resident PPOPopulation (stacked
 parameters / Adam state / rollout SoA), so a whole population is trained with
 one launch per kernel; the INIT_HP keys and defaults follow the reference
-(utils.py:502-537)."""
+(utils.py:502-537).
+
+Sharding.  Under an initialised torch.distributed group of G > 1 ranks
+(``shard=None``, the default, or ``shard=True``) ``population_size`` is the
+GLOBAL population and each rank gets its slice: rank r holds global agents
+r*P .. r*P + P - 1 with P = population_size / G (their global indices, init
+seeds and sampling streams), so the same script trains the same population
+on 1 or G GPUs.  Object-level agents (DQN / Rainbow / MADDPG) are built for
+the whole population in order and the slice is kept, which leaves the
+torch generators where the unsharded build leaves them.  ``shard=False``
+keeps ``population_size`` agents per rank."""
 
 from __future__ import annotations
 
@@ -15,8 +25,22 @@ import torch
 def create_population(algo: str, net_config: dict[str, Any] | None, INIT_HP: dict[str, Any], observation_space=None,
                       action_space=None, hp_config=None, actor_network=None, critic_network=None,
                       agent_wrapper=None, wrapper_kwargs=None, population_size: int = 1, num_envs: int = 1,
-                      device="cuda", accelerator=None, torch_compiler=None, algo_kwargs=None, **_unused):
+                      device="cuda", accelerator=None, torch_compiler=None, algo_kwargs=None, shard=None, **_unused):
     algo_kwargs = dict(algo_kwargs or {})
+    import torch.distributed as dist
+
+    world, rank = (dist.get_world_size(), dist.get_rank()) if dist.is_initialized() else (1, 0)
+    if shard is None:
+        shard = world > 1
+    from ..hpo.shard import mark_shared
+
+    mark_shared(hp_config)  # one config object for every agent, as the reference hands it out
+    lo, P = 0, int(population_size)
+    if shard and world > 1:
+        if population_size % world:
+            raise ValueError(f"population_size {population_size} is not divisible by the {world} ranks")
+        P = population_size // world
+        lo = rank * P
     if algo == "PPO":
         from ..algorithms.ppo import PPO, spec_from_net_config
         from ..population.ppo_pop import PPOPopulation
@@ -32,18 +56,20 @@ def create_population(algo: str, net_config: dict[str, Any] | None, INIT_HP: dic
         if INIT_HP.get("RECURRENT", False):
             raise NotImplementedError("recurrent PPO is outside the agx hot path")
         spec = spec_from_net_config(observation_space, action_space, net_config)
-        pop = PPOPopulation(spec, population_size, num_envs, seeds=list(range(population_size)),
-                            device=torch.device(device), **hp)
-        return [PPO(observation_space, action_space, index=i, hp_config=hp_config, net_config=net_config,
+        G = population_size if shard and world > 1 else P
+        pop = PPOPopulation(spec, P, num_envs, seeds=list(range(lo, lo + P)), device=torch.device(device),
+                            agent_offset=lo, global_pop_size=G, seed_base=0, **hp)
+        return [PPO(observation_space, action_space, index=lo + i, hp_config=hp_config, net_config=net_config,
                     num_envs=num_envs, device=device, _population=pop, _row=i, **hp, **algo_kwargs)
-                for i in range(population_size)]
+                for i in range(P)]
     if algo in ("DQN", "Rainbow DQN", "RainbowDQN"):
         from ..algorithms.dqn import DQN, RainbowDQN
 
         cls = DQN if algo == "DQN" else RainbowDQN
-        return [cls.from_init_hp(observation_space, action_space, net_config, INIT_HP, index=i, device=device,
-                                 hp_config=hp_config, **algo_kwargs)
-                for i in range(population_size)]
+        agents = [cls.from_init_hp(observation_space, action_space, net_config, INIT_HP, index=i, device=device,
+                                   hp_config=hp_config, **algo_kwargs)
+                  for i in range(population_size if shard else P)]
+        return agents[lo:lo + P]
     if algo == "MADDPG":  # utils/utils.py:590-618
         from ..algorithms.maddpg import MADDPG
 
@@ -53,9 +79,10 @@ def create_population(algo: str, net_config: dict[str, Any] | None, INIT_HP: dic
                   O_U_noise=INIT_HP.get("O_U_NOISE", True), expl_noise=INIT_HP.get("EXPL_NOISE", 0.1),
                   vect_noise_dim=num_envs, mean_noise=INIT_HP.get("MEAN_NOISE", 0.0),
                   theta=INIT_HP.get("THETA", 0.15), dt=INIT_HP.get("DT", 0.01))
-        return [MADDPG(observation_space, action_space, agent_ids=INIT_HP["AGENT_IDS"], index=i,
-                       net_config=net_config, device=device, hp_config=hp_config, **hp, **algo_kwargs)
-                for i in range(population_size)]
+        agents = [MADDPG(observation_space, action_space, agent_ids=INIT_HP["AGENT_IDS"], index=i,
+                         net_config=net_config, device=device, hp_config=hp_config, **hp, **algo_kwargs)
+                  for i in range(population_size if shard else P)]
+        return agents[lo:lo + P]
     raise NotImplementedError(f"algorithm {algo!r} is outside the agx hot path (PPO, DQN, Rainbow DQN, MADDPG)")
 
 
