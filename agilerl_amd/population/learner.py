@@ -109,13 +109,13 @@ class FusedLearner:
         key = (pop.params.data.data_ptr(), opt.exp_avg.data_ptr(), opt.exp_avg_sq.data_ptr(), opt.lr.data_ptr(),
                opt.steps.data_ptr(), pop.obs.data_ptr(), pop.advantages.data_ptr(), pop.returns.data_ptr(),
                pop.values.data_ptr(), pop.log_probs.data_ptr(), pop.actions.data_ptr(), pop.adv_stats.data_ptr(),
-               None if masks is None else masks.data_ptr(), float(b1), float(b2), float(opt.eps), pop.batch_size,
+               None if masks is None else masks.data_ptr(), float(b1), float(b2), float(opt.eps), pop.split_batch,
                pop.update_epochs, float(pop.clip_coef), float(pop.vf_coef), float(pop.ent_coef),
                float(pop.max_grad_norm), float(pop.target_kl or 0.0), pop.err_word.data_ptr(),
                *((None, None, None) if pop._hp_dev is None else (t.data_ptr() for t in pop._hp_dev)))
         if self.key != key:
             a = self.args
-            a.P, a.S, a.epochs, a.batch = pop.P, pop.S, pop.update_epochs, pop.batch_size
+            a.P, a.S, a.epochs, a.batch = pop.P, pop.S, pop.update_epochs, pop.split_batch
             a.params, a.exp_avg, a.exp_avg_sq = key[0], key[1], key[2]
             a.lr, a.adam_step = key[3], key[4]
             a.beta1, a.beta2, a.eps, a.max_grad_norm = key[13], key[14], key[15], key[21]

@@ -126,6 +126,7 @@ class PPOPopulation:
         # every global agent's update_epochs (the shuffles each draws; ranks
         # refresh the other shards' entries after a mutation)
         self.global_epochs = [self.update_epochs] * self.global_P
+        self.global_batch = [self.batch_size] * self.global_P
         self._shard_scratch: dict = {}
         self.act_counter = 0
         self._desc = None
@@ -354,6 +355,29 @@ class PPOPopulation:
             raise NotImplementedError("learn_step is the rollout length every agent of the population engine shares")
         else:
             raise KeyError(f"no per-agent hyperparameter {name!r}")
+        self._rederive()
+
+    @property
+    def split_batch(self) -> int:
+        """The minibatch size that sizes the fused learner's partner split:
+        the largest of the GLOBAL population (a shard splits like the whole
+        population, so its agents' sums run in the same order)."""
+        gb = list(self.global_batch)
+        gb[self.agent_offset:self.agent_offset + self.P] = self.agent_batch
+        return min(max(gb), self.S)
+
+    def set_host_hparams(self, p: int, lr=None, batch_size=None, update_epochs=None, ent_coef=None) -> None:
+        """Exact host values of agent p's hyperparameters after a clone whose
+        device rows already hold them (a parent from another rank: the
+        device tables are f32 / int32, the host lists keep Python floats)."""
+        if lr is not None:
+            self.agent_lr[p] = float(lr)
+        if batch_size is not None:
+            self.agent_batch[p] = int(batch_size)
+        if update_epochs is not None:
+            self.agent_epochs[p] = int(update_epochs)
+        if ent_coef is not None:
+            self.agent_ent[p] = float(ent_coef)
         self._rederive()
 
     def reinit_agent_optimizer(self, p: int) -> None:

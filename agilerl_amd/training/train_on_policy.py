@@ -86,16 +86,23 @@ def _clone_host_attributes(pop, parents: list[int], elitism: bool, records: list
         a.fitness, a.scores, a.steps = (_copy.deepcopy(src[k]) for k in ("fitness", "scores", "steps"))
         a.registry, a.mut = _copy.deepcopy(src["_registry"]), src.get("mut")
         a.index = new_index
+        # the device rows (PopulationSync) carry the hyperparameters as f32 /
+        # int32; the host keeps the parent's exact values
+        hp = src.get("_hp", {})
+        a.population.set_host_hparams(a.row, lr=hp.get("lr"), batch_size=hp.get("batch_size"),
+                                      update_epochs=hp.get("update_epochs"), ent_coef=hp.get("ent_coef"))
 
 
 def _sync_global_epochs(population) -> None:
-    """Every global agent's update_epochs (the shuffles each draws) after a
-    mutation may have changed another shard's."""
+    """Every global agent's update_epochs (the shuffles each draws) and batch
+    size (the learner's partner split) after a mutation may have changed
+    another shard's."""
     if population.global_P == population.P:
         return
     box: list = [None] * dist.get_world_size()
-    dist.all_gather_object(box, list(population.agent_epochs))
-    population.global_epochs = [int(e) for b in box for e in b]
+    dist.all_gather_object(box, (list(population.agent_epochs), list(population.agent_batch)))
+    population.global_epochs = [int(e) for b in box for e in b[0]]
+    population.global_batch = [int(x) for b in box for x in b[1]]
 
 
 def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None, swap_channels: bool = False,

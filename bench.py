@@ -6,12 +6,14 @@ synthetic shape, plus the reference-style CPU baseline.
   python bench.py [--gpus N] [--steps K] [--warmup W]
   (N > 1: launched by torch.distributed.run, one rank per GPU over RCCL)
 
-A "step" = one PPO iteration of the whole per-GPU population: T vector steps
-of rollout for every agent (host env + HBM rollout SoA), bootstrap + GAE,
-and E x M minibatch learner updates per agent.  Scaling is weak: every GPU
-runs its own 8-agent population (a shard of an 8N-agent population); ranks
-exchange only fitness scalars (RCCL all-gather) and the selected parents'
-parameters at generation boundaries (--evo-every).
+A "step" = one PPO iteration of the population: T vector steps of rollout
+for every agent (host env + HBM rollout SoA), bootstrap + GAE, and E x M
+minibatch learner updates per agent.  The headline is the north-star's
+configuration, strong scaling: ONE 8-agent population (--pop, global) sharded
+P = 8 / N agents per GPU; ranks exchange only fitness scalars (RCCL
+all-gather) and the selected parents' parameters at generation boundaries
+(--evo-every).  With N > 1 a weak-scaling leg (--pop-per-gpu agents on
+every GPU, a shard of an N x 8 population) is reported as an extra key.
 """
 
 from __future__ import annotations
@@ -40,7 +42,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--pop", type=int, default=8, help="agents per GPU")
+    ap.add_argument("--pop", type=int, default=8, help="agents in the whole population (sharded over the GPUs)")
+    ap.add_argument("--pop-per-gpu", type=int, default=8, help="agents per GPU of the extra weak-scaling leg (N > 1)")
+    ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling leg")
     ap.add_argument("--num-envs", type=int, default=128)
     ap.add_argument("--learn-step", type=int, default=2048)
     ap.add_argument("--batch-size", type=int, default=128)
@@ -127,7 +131,8 @@ def dist_selftest(args, world, rank):
 
 
 # --------------------------------------------------------------------------- #
-def population_leg(args, world, rank):
+def population_leg(args, world, rank, P, steps=None):
+    """P agents on this rank, global agents rank*P .. of a world*P population."""
     from agilerl_amd.envs import SyntheticVecEnv
     from agilerl_amd.hpo.population_sync import PopulationSync
     from agilerl_amd.population.nets import ActorCriticSpec
@@ -136,11 +141,13 @@ def population_leg(args, world, rank):
 
     spec = ActorCriticSpec(obs_dim=8, n_actions=4, encoder_hidden=[64], latent_dim=64,
                            actor_hidden=[64], critic_hidden=[64])
-    P, N = args.pop, args.num_envs
+    N = args.num_envs
+    steps = args.steps if steps is None else steps
     seeds = [rank * P + i for i in range(P)]
     pop = PPOPopulation(spec, P, N, learn_step=args.learn_step, batch_size=args.batch_size, lr=1e-3,
                         update_epochs=args.epochs, seeds=seeds, device="cuda",
-                        fused=args.learner == "fused")
+                        fused=args.learner == "fused", agent_offset=rank * P, global_pop_size=world * P,
+                        seed_base=0)
     env = SyntheticVecEnv(P * N, seed=1000 + rank)
     runner = PopulationRunner(pop, env)
     sync = PopulationSync(pop, runner, world, rank, seed=42) if args.evo_every > 0 else None
@@ -158,15 +165,15 @@ def population_leg(args, world, rank):
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         step(i)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     dt = max_over_ranks(time.perf_counter() - t0, world)
     pop.check_errors()  # a partner timeout in any timed learn() fails the run loudly
-    env_steps = world * P * pop.S * args.steps
-    updates = world * P * args.epochs * pop.n_minibatches() * args.steps
+    env_steps = world * P * pop.S * steps
+    updates = world * P * args.epochs * pop.n_minibatches() * steps
     # the dominant kernel alone: learn() (gather prologue + fused learner) on the
     # last rollout, HIP events on the launch stream
     reps = 10
@@ -186,8 +193,11 @@ def population_leg(args, world, rank):
                    frac=round(flop / learn_s / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
                    bound="latency: 64 serial minibatch updates per agent, each a chain of barrier-separated "
                          "small GEMM / row phases and a 3-barrier partner hand-off (DESIGN §5)")
-    return dict(dt=dt, env_steps=env_steps, updates=updates, S=pop.S, T=pop.T, learner=learner,
-                generations=(args.steps // args.evo_every) if args.evo_every else 0)
+    out = dict(dt=dt, env_steps=env_steps, updates=updates, S=pop.S, T=pop.T, learner=learner,
+               generations=(steps // args.evo_every) if args.evo_every else 0)
+    del runner, pop, sync
+    torch.cuda.empty_cache()
+    return out
 
 
 # --------------------------------------------------------------------------- #
@@ -681,7 +691,16 @@ def main():
     from agilerl_amd import _lib
 
     _lib.load()
-    res = population_leg(args, world, rank)
+    if args.pop % world:
+        raise SystemExit(f"bench.py: --pop {args.pop} agents cannot be sharded over {world} GPUs")
+    res = population_leg(args, world, rank, args.pop // world)
+    weak = None
+    if world > 1 and not args.no_weak:
+        w = population_leg(args, world, rank, args.pop_per_gpu)
+        weak = {"value": round(w["env_steps"] / w["dt"], 1), "unit": "env-steps/s",
+                "ms_per_step": round(w["dt"] / args.steps * 1e3, 3),
+                "learner_updates_per_s": round(w["updates"] / w["dt"], 1),
+                "workload": f"{args.pop_per_gpu} agents per GPU ({args.pop_per_gpu * world}-agent population)"}
     roof = kern = None
     if not args.no_roofline:
         roof = roofline_leg(args)
@@ -695,7 +714,7 @@ def main():
     if rank == 0:
         value = res["env_steps"] / res["dt"]
         line = {
-            "metric": "population env-steps/sec (8-agent PPO per GPU, LunarLander-shaped synthetic envs)",
+            "metric": "population env-steps/sec + learner updates/sec, 8-agent PPO at 1/2/4/8 MI355X",
             "value": round(value, 1),
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -703,19 +722,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(res["dt"] / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32 (GAE carry f64)",
             "data": "synthetic (host SyntheticVecEnv: obs 8 f32, 4 actions, r~N(0,1), done~Bern(1/200))",
             "config": {
-                "workload": "config 2: PPO pop=8 per GPU x 128 vec envs, T=16, batch 128, 4 epochs, "
-                            "MLP enc[64]->64 + heads[64] (shared encoder), tournament every "
-                            f"{args.evo_every} iterations",
-                "pop_per_gpu": args.pop, "num_envs": args.num_envs, "learn_step": args.learn_step,
+                "workload": f"config 2: one {args.pop}-agent PPO population sharded {args.pop // world} agents per "
+                            "GPU, 128 vec envs per agent, T=16, batch 128, 4 epochs, MLP enc[64]->64 + heads[64] "
+                            f"(shared encoder), tournament every {args.evo_every} iterations",
+                "population": args.pop, "pop_per_gpu": args.pop // world, "num_envs": args.num_envs,
+                "learn_step": args.learn_step,
                 "batch_size": args.batch_size, "update_epochs": args.epochs, "learner": args.learner,
                 "parallelism": f"population-sharded x{world}",
             },
             "learner_updates_per_s": round(res["updates"] / res["dt"], 1),
+            "weak_scaling": weak,
             "learner": res["learner"],
             "generations": res["generations"],
             "generation_fitness": "mean return of the training episodes finished since the previous generation "
