@@ -240,6 +240,34 @@ def test_config3_pong_rainbow_generation():
     assert all(a.steps[-1] == 128 for a in pop)
     assert any(not torch.equal(a, b) for a, b in zip(p0, pop[0].actor.parameters()))
 
+    # one more learn of the trained agent 0 on a PER batch drawn from the 1M-transition
+    # memory, against the reference's loss (dqn_rainbow.py:284-440) on a plain-PyTorch
+    # twin at the config-3 network (84x84x4 frames, latent 256, head [256], +-200)
+    from test_dropin_gpu import _rainbow_reference_loss
+
+    torch.backends.cudnn.allow_tf32 = False
+    agent = pop[0]
+    ref_actor, ref_target = _torch_twin(agent.actor), _torch_twin(agent.actor_target)
+    ref_opt = torch.optim.Adam(ref_actor.parameters(), lr=agent.lr)
+    ref_opt.load_state_dict(agent.optimizer.state_dict())  # the agent's Adam moments and step
+    torch.manual_seed(11)
+    exp = memory.sample(64, beta=0.4)
+    ref_exp = {k: (v.float() / 255.0 if k in ("obs", "next_obs") else v) for k, v in exp.items()}
+    el_ref, loss_ref = _rainbow_reference_loss(agent, ref_actor, ref_target, ref_exp, agent.gamma, True)
+    ref_opt.zero_grad()
+    loss_ref.backward()
+    torch.nn.utils.clip_grad_norm_(ref_actor.parameters(), 10.0)
+    ref_opt.step()
+    loss, _, new_pri = agent.learn(exp, per=True)
+    assert abs(loss - loss_ref.item()) <= 1e-5 * abs(loss_ref.item())
+    for (n, p1), p2 in zip(agent.actor.named_parameters(), ref_actor.parameters()):
+        _close(p1.grad, p2.grad, 1e-4, n)
+        ok = p2.grad.abs() > 1e-3 * _scale(p2.grad)
+        d = (p1 - p2).detach().abs()
+        assert (float(d[ok].max()) if ok.any() else 0.0) <= 0.05 * agent.lr, n
+        assert float(d.max()) <= 2.1 * agent.lr, n
+    np.testing.assert_allclose(new_pri, el_ref.detach().cpu().numpy() + agent.prior_eps, rtol=1e-5)
+
 
 @pytest.mark.parametrize("shape", [SHAPES[0], SHAPES[1], SHAPES[2], SHAPES[5], SHAPES[8]])
 def test_grouped_conv_matches_per_group_torch(shape):

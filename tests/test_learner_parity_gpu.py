@@ -146,20 +146,27 @@ def _load_rows(pop, rows, t):
 
 @pytest.mark.parametrize("name", ["learn0", "learn1", "learn2"])
 def test_fused_single_updates_along_reference_trajectory(golden, name):
-    """One fused update from the reference's OWN state at points along its
-    learn() trajectory (every agent of one population starts from a different
+    """One fused update from the reference's OWN state at EVERY update of its
+    learn() trajectory (each agent of a population starts from a different
     update k of the reference run: parameters, Adam moments, step count, and
-    minibatch k as its rollout).  Each must land where the reference's update
-    k lands: no drift, every layer, at fp32 rounding level."""
+    minibatch k as its rollout; populations of 16 agents, the production
+    partner split).  Each must land where the reference's update k lands: no
+    drift, every layer, at fp32 rounding level."""
     g = golden(name)
     snaps = {}
     out = _golden_oracle(g, on_update=lambda k, sn: snaps.__setitem__(k, sn))
     n_upd = len(out["approx_kl"])
     b = int(g["batch"])
-    picks = [k for k in (0, 1, 7, 15, 16, 31, 32, 47, 48, 63) if k < n_upd and len(snaps[k]["idx"]) == b]
+    every = [k for k in range(n_upd) if len(snaps[k]["idx"]) == b]
     after = {k: (snaps[k + 1] if k + 1 in snaps else {"state": out["state"], "exp_avg": out["exp_avg"],
                                                        "exp_avg_sq": out["exp_avg_sq"], "step": out["step"]})
-             for k in picks}
+             for k in every}
+    assert len(every) >= n_upd - int(g["epochs"])  # only a short last chunk per epoch is skipped
+    for c in range(0, len(every), 16):
+        _single_updates(g, snaps, after, every[c:c + 16], b)
+
+
+def _single_updates(g, snaps, after, picks, b):
     P = len(picks)
     pop = _pop(P, b, 1, int(g["obs_dim"]), int(g["n_actions"]), g["enc"], int(g["latent"]), g["actor_hidden"],
                g["critic_hidden"], b, 1, float(g["lr"]), masks="masks" in g)
