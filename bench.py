@@ -637,6 +637,106 @@ def cpu_kernels_leg(seconds):
     return out
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or platform.machine()
+
+
+def _c51_torch_ops(q_next, target_dist, logp_cur, actions, r, d, support, v_min, v_max, gamma):
+    """RainbowDQN._dqn_loss's projection + elementwise loss as the reference's
+    torch ops (dqn_rainbow.py:313-367) on given network outputs."""
+    B, Z = target_dist.shape[0], support.shape[0]
+    delta_z = float(v_max - v_min) / (Z - 1)
+    next_actions = q_next.argmax(1)
+    tq = target_dist[torch.arange(B), next_actions]
+    t_z = (r + (1 - d) * gamma * support).clamp(min=v_min, max=v_max)
+    b = (t_z - v_min) / delta_z
+    L, u = b.floor().long(), b.ceil().long()
+    L[(u > 0) * (u == L)] -= 1
+    u[((Z - 1) > L) * (u == L)] += 1
+    offset = torch.linspace(0, (B - 1) * Z, B).long().unsqueeze(1).expand(B, Z)
+    proj = torch.zeros(tq.size())
+    proj.view(-1).index_add_(0, (L + offset).view(-1), (tq * (u.float() - b)).view(-1))
+    proj.view(-1).index_add_(0, (u + offset).view(-1), (tq * (b - L.float())).view(-1))
+    log_p = logp_cur[torch.arange(B), actions.squeeze(-1)]
+    return -(proj * log_p).sum(1)
+
+
+def cpu_offpolicy_leg(seconds):
+    """BASELINE.md §3 / SURVEY §8d CPU lines beside the off-policy kernels, on
+    1 host thread: the reference's Python-loop segment tree (oracle/per.py,
+    segment_tree.py:81-156 + replay_buffer.py:357-428) timed on 2^14-sample
+    slices of a 2^20-leaf tree and scaled per sample, and the torch-op C51
+    projection + loss (dqn_rainbow.py:313-367) on bounded 2^15-row slices of
+    the §8d C51 shape (A = 6, Z = 51, +-200)."""
+    from oracle import per as oper
+
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    out = {"cpu_model": _cpu_model(), "threads": 1}
+    cap = 1 << 20
+    rng = np.random.default_rng(2)
+    leaves = (np.abs(rng.standard_normal(cap)) + 1e-5) ** 0.6
+    buf = oper.PER(cap, alpha=0.6)
+    buf.sum_tree.tree = oper.build_tree_from_leaves(leaves, cap, "sum").tolist()
+    buf.min_tree.tree = oper.build_tree_from_leaves(leaves, cap, "min").tolist()
+    buf.size, buf.tree_ptr = cap, 0
+    n = 1 << 14
+    u = torch.rand(n, generator=torch.Generator().manual_seed(2)).numpy()
+    t0, reps = time.perf_counter(), 0
+    while True:
+        idx = buf.sample_indices(u)
+        buf.weights(idx, 0.4)
+        reps += 1
+        if time.perf_counter() - t0 >= seconds / 3:
+            break
+    dt = time.perf_counter() - t0
+    out["per_sample"] = dict(value=round(reps * n / dt, 1), unit="samples/s", cores=1, kind="port",
+                             sample=f"{reps} x 2^14 proportional samples + IS weights (Python loop) on a 2^20-leaf "
+                                    "tree, scaled per sample")
+    idx = rng.integers(0, cap, n)
+    pri = np.abs(rng.standard_normal(n)).astype(np.float32)
+    t0, reps = time.perf_counter(), 0
+    while True:
+        buf.update_priorities(idx, pri)
+        reps += 1
+        if time.perf_counter() - t0 >= seconds / 3:
+            break
+    dt = time.perf_counter() - t0
+    out["per_update"] = dict(value=round(reps * n / dt, 1), unit="updates/s", cores=1, kind="port",
+                             sample=f"{reps} x 2^14 update_priorities (Python loop, two 20-level root paths each), "
+                                    "scaled per update")
+    B, A, Z = 1 << 15, 6, 51
+    g = torch.Generator().manual_seed(3)
+    q_next = torch.randn(B, A, generator=g)
+    td = torch.softmax(torch.randn(B, A, Z, generator=g), -1).clamp(min=1e-3)
+    logp = torch.log_softmax(torch.randn(B, A, Z, generator=g), -1)
+    act = torch.randint(0, A, (B, 1), generator=g)
+    r = torch.randn(B, 1, generator=g)
+    d = (torch.rand(B, 1, generator=g) < 0.05).float()
+    support = torch.linspace(-200.0, 200.0, Z)
+    t0, reps = time.perf_counter(), 0
+    while True:
+        _c51_torch_ops(q_next, td, logp, act, r, d, support, -200.0, 200.0, 0.99 ** 4)
+        reps += 1
+        if time.perf_counter() - t0 >= seconds / 3:
+            break
+    dt = time.perf_counter() - t0
+    out["c51_project_loss"] = dict(value=round(reps * B / dt, 1), unit="rows/s", gbs=round(reps * B * 444 / dt / 1e9, 3),
+                                   cores=1, kind="port",
+                                   sample=f"{reps} x 2^15 rows of the reference's torch-op projection + loss")
+    torch.set_num_threads(threads)
+    return out
+
+
 # --------------------------------------------------------------------------- #
 def config5_leg(iters: int = 5):
     """Config 5's per-GPU shard (Atari Breakout PPO, ppo_image.yaml network:
@@ -711,6 +811,8 @@ def main():
         cpu = cpu_baseline_leg(args, res["S"])
         cpu["all_cores"] = cpu_population_all_cores(args, min(args.cpu_seconds, 10.0))
         cpu["roofline_workload"] = cpu_kernels_leg(min(args.cpu_seconds, 8.0))
+        cpu["off_policy"] = cpu_offpolicy_leg(min(args.cpu_seconds, 9.0))
+        cpu["cpu_model"] = cpu["off_policy"]["cpu_model"]
     if rank == 0:
         value = res["env_steps"] / res["dt"]
         line = {
