@@ -576,6 +576,7 @@ struct LearnArgs {
                            // (zeroed per call)
     int debug_stall;       // test hook: partner 1 of agent 0 never arrives
     int write_through;     // 1: always sc1 stores (AGX_LEARN_WRITETHROUGH=1; tests the cross-XCD form)
+    const unsigned *skip;  // non-null and nonzero when the learner starts: return untouched
 };
 
 #define IC(x) std::integral_constant<int, (x)>()
@@ -601,6 +602,9 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     constexpr LearnPlan pl = C::plan;
     // block b -> agent b % P, partner kk = b / P: with P % 8 == 0 an agent's K
     // workgroups share an XCD under round-robin dispatch (speed only)
+    // an aborted / timed-out rollout queued ahead of this learn leaves its
+    // control word set: the partial rollout must not update anything
+    if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const int b = blockIdx.x;
     const int p = b % g.P, kk = b / g.P;
     const int tid = threadIdx.x;
@@ -1746,8 +1750,9 @@ __global__ __launch_bounds__(kNT, 1) void ppo_rollout_persistent_kernel(const Ac
                 // relaxed: an acquire at system scope would invalidate the
                 // caches on every poll; one invalidate follows the wait
                 const unsigned v = __hip_atomic_load(rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (v == AGX_ROLLOUT_ABORT) {
+                if (v == AGX_ROLLOUT_ABORT) {  // host exception: the rollout is partial
                     go = 0;
+                    __hip_atomic_store(&ctl->timeout, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
                 if (v >= base + (unsigned)(t + 1)) break;
@@ -2067,6 +2072,7 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *x
     a.sums = reinterpret_cast<float *>(ws + w.sums);
     a.cnt = reinterpret_cast<unsigned *>(ws);
     a.debug_stall = K > 1 ? g_debug_stall() : 0;
+    a.skip = x->skip_if_set;
     {
         const char *wt = getenv("AGX_LEARN_WRITETHROUGH");
         a.write_through = wt && atoi(wt) != 0;

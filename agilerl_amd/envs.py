@@ -71,6 +71,9 @@ class SyntheticVecEnv:
     ``max_episode_steps`` truncates episodes like gymnasium's TimeLimit
     (LunarLander: 1000); None never truncates (the bench's default)."""
 
+    #: the step never touches the GPU (PopulationRunner may pace a persistent rollout)
+    agx_device_free = True
+
     def __init__(self, num_envs: int, obs_dim: int = 8, n_actions: int = 4, p_done: float = 1 / 200,
                  seed: int = 0, ring: int = 97, max_episode_steps: int | None = None):
         self.num_envs = int(num_envs)
@@ -277,6 +280,10 @@ class StackedVecEnv:
         for k, c in enumerate(clones, start=first):
             _reseed_copy(c, k)
         return cls(([env] if offset == 0 else []) + clones)
+
+    @property
+    def agx_device_free(self) -> bool:
+        return all(bool(getattr(e, "agx_device_free", False)) for e in self.envs)
 
     def _split(self, x):
         out, s = [], 0

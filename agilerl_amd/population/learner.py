@@ -72,7 +72,7 @@ class AgxPPOLearnArgs(ctypes.Structure):
         ("loss_out", ctypes.c_void_p), ("kl_out", ctypes.c_void_p), ("epochs_out", ctypes.c_void_p),
         ("error_word", ctypes.c_void_p),
         ("batch_per_agent", ctypes.c_void_p), ("epochs_per_agent", ctypes.c_void_p),
-        ("ent_coef_per_agent", ctypes.c_void_p),
+        ("ent_coef_per_agent", ctypes.c_void_p), ("skip_if_set", ctypes.c_void_p),
     ]
 
 
@@ -94,7 +94,7 @@ class FusedLearner:
         self.key = None
         self.fn = lib.agx_ppo_learn
 
-    def learn(self, pop, perms: torch.Tensor | None = None) -> torch.Tensor:
+    def learn(self, pop, perms: torch.Tensor | None = None, skip_if_set: int | None = None) -> torch.Tensor:
         """All epochs x minibatches of every agent in two launches (gather +
         learner).  Advantages are normalised on the fly from pop.adv_stats
         (ppo.py:829-834); pop.advantages itself is left untouched."""
@@ -130,6 +130,7 @@ class FusedLearner:
             self.aref = ctypes.byref(self.args)
             self.dref = ctypes.byref(self.desc)
         self.args.perms = perms.data_ptr()
+        self.args.skip_if_set = skip_if_set
         rc = self.fn(self.dref, self.aref, self.ws.data_ptr(), torch.cuda.current_stream(pop.device).cuda_stream)
         if rc != 0:
             _lib.check(rc, "agx_ppo_learn")
@@ -143,10 +144,10 @@ class FusedLearner:
         return bool(int(word.item()) != 0)
 
 
-def fused_learn(pop, perms=None) -> torch.Tensor:
+def fused_learn(pop, perms=None, skip_if_set: int | None = None) -> torch.Tensor:
     if getattr(pop, "_fused", None) is None or pop._fused.epochs_ws < pop.update_epochs:
         pop._fused = FusedLearner(pop)
-    return pop._fused.learn(pop, perms)
+    return pop._fused.learn(pop, perms, skip_if_set)
 
 
 def policy_step(pop, desc: AgxPPONet, obs: torch.Tensor, obs_agent_stride: int, *, sample: bool, counter: int,

@@ -238,7 +238,7 @@ class PPOPopulation:
         self._gae_launch = (key, launch, last_value, last_done)
 
     # ------------------------------------------------------------------ #
-    def learn(self, prefetch: bool = True) -> torch.Tensor:
+    def learn(self, prefetch: bool = True, skip_if_set: int | None = None) -> torch.Tensor:
         """One PPO update of every agent; returns the reference's mean_loss per
         agent (device tensor [P], no host sync).  ``prefetch``: draw the next
         learn's permutations right away (the pipelined runner passes False and
@@ -247,7 +247,7 @@ class PPOPopulation:
         if self.fused_descriptor() is not None:
             from .learner import fused_learn
 
-            loss = fused_learn(self)
+            loss = fused_learn(self, skip_if_set=skip_if_set)
             self.last_kl = self._fused.kl
             self._record_kl_pending(self._fused.epochs_run)
             # with target_kl the next learn's shuffles depend on this one's stops

@@ -16,7 +16,8 @@ kernel reads / writes directly (zero-copy over the host link: 40 KB in and
 8 KB out per step at config 2), so a step is one launch and one wait; with
 AGX_ZERO_COPY=0 the staging goes through one H2D and one D2H copy instead.
 
-Persistent mode (default; AGX_PERSISTENT_ROLLOUT=0 turns it off): the whole
+Persistent mode (AGX_PERSISTENT_ROLLOUT: "auto" default, "1" always, "0"
+never): the whole
 rollout is ONE launch (agx_ppo_rollout_persistent) whose workgroups keep the
 parameters in LDS and are paced step by step through a control block in
 coherent host memory — the host releases step t after the env step
@@ -24,6 +25,16 @@ coherent host memory — the host releases step t after the env step
 so a vector step costs no launch and no event wait.  Staging, actions and
 the control block then live in coherent (fine-grained) host memory, which
 the device re-reads within one launch.
+
+From the persistent launch to the host's final release the device waits
+for the host thread, so nothing the env does in its step may wait for the
+device (``torch.cuda.synchronize()``, a ``.item()`` on a CUDA tensor, a
+blocking copy, ``hipHostFree``): it would stall the rollout until its
+timeout.  "auto" therefore paces a persistent rollout only for envs that
+declare ``agx_device_free = True`` (the synthetic envs, and a StackedVecEnv
+whose every env declares it); any other env gets one launch per vector step,
+where its step may use the device freely.  A gymnasium env that does not touch
+the GPU can opt in by setting the attribute.
 
 Architectures outside the fused kernels use the plain-PyTorch policy step
 with per-field copies (``_collect_torch``).
@@ -122,8 +133,9 @@ class PopulationRunner:
         dev = pop.device
         self.zero_copy = os.environ.get("AGX_ZERO_COPY", "1") != "0"
         desc = pop.fused_descriptor()
-        self.persistent = (self.zero_copy and os.environ.get("AGX_PERSISTENT_ROLLOUT", "1") != "0"
-                           and desc is not None)
+        mode = os.environ.get("AGX_PERSISTENT_ROLLOUT", "auto")
+        self.persistent = (self.zero_copy and mode != "0" and desc is not None
+                           and (mode == "1" or bool(getattr(env, "agx_device_free", False))))
         if self.persistent:
             # every workgroup of the persistent launch must be co-resident (the
             # host paces them in lock step); larger grids take per-step launches
@@ -435,7 +447,10 @@ class PopulationRunner:
             lib, ctl, base = self._launch_persistent(desc)
             self._finish_persistent()
             self.pop.finish_rollout(self.last_obs, self.last_done, self.last_value)
-            loss = self.pop.learn(prefetch=False)
+            # the learner reads the control block's timeout word when it starts:
+            # set by an aborted (host exception) or timed-out rollout, so the
+            # partial rollout never updates the parameters or Adam state
+            loss = self.pop.learn(prefetch=False, skip_if_set=ctl + 4)
             self._pace_persistent(lib, ctl, base)
         finally:
             _pacing_end()

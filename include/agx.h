@@ -160,6 +160,13 @@ typedef struct agx_ppo_learn_args {
      * and entropy coefficient.  loss_out divides by S * epochs_per_agent[p]. */
     const int32_t *batch_per_agent, *epochs_per_agent;
     const float *ent_coef_per_agent;
+    /* NULL, or a word the learner reads when it starts (device or coherent
+     * host memory): nonzero -> the call leaves params, moments, steps and
+     * outputs untouched.  The pipelined PPO iteration passes the persistent
+     * rollout's agx_rollout_ctl.timeout word, so a learn queued behind a
+     * rollout the host aborted (env exception) or that timed out never runs
+     * on the partial rollout. */
+    const uint32_t *skip_if_set;
 } agx_ppo_learn_args;
 int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *args, void *workspace, void *stream);
 /* Rollout policy step (PPO.get_action / _get_action_and_values, ppo.py:
@@ -247,7 +254,8 @@ int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N, const flo
 #define AGX_ROLLOUT_ABORT 0xffffffffu
 typedef struct agx_rollout_ctl {
     uint32_t seq;     /* host -> device: last released step (base + t + 1) */
-    uint32_t timeout; /* device -> host: a workgroup stopped waiting       */
+    uint32_t timeout; /* device -> host: a workgroup stopped waiting (1:
+                         timeout, 2: abort); agx_ppo_learn_args.skip_if_set */
     uint32_t nwg;     /* workgroups (set by agx_ppo_rollout_persistent)    */
     uint32_t reserved;
     /* followed by nwg uint32 done words, then (64-byte aligned) one 64-byte

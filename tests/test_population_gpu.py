@@ -357,7 +357,7 @@ def test_collect_episode_accounting():
     np.testing.assert_allclose(runner.scores.view(P, N).cpu().numpy(), score, rtol=1e-6, atol=1e-6)
 
 
-def _runner_pair(monkeypatch, persistent, P=3, N=40, seed=5):
+def _runner_pair(monkeypatch, persistent, P=3, N=40, seed=5, perm_source="device"):
     from agilerl_amd.envs import SyntheticVecEnv
     from agilerl_amd.population.nets import ActorCriticSpec
     from agilerl_amd.population.ppo_pop import PPOPopulation
@@ -366,21 +366,28 @@ def _runner_pair(monkeypatch, persistent, P=3, N=40, seed=5):
     monkeypatch.setenv("AGX_PERSISTENT_ROLLOUT", "1" if persistent else "0")
     spec = ActorCriticSpec(obs_dim=8, n_actions=4)
     pop = PPOPopulation(spec, P, N, learn_step=8 * N, batch_size=64, update_epochs=2, device=DEV,
-                        seeds=list(range(P)), fused=True, perm_source="device")
+                        seeds=list(range(P)), fused=True, perm_source=perm_source)
     runner = PopulationRunner(pop, SyntheticVecEnv(P * N, seed=seed, p_done=0.2))
     assert runner.persistent == persistent
     return pop, runner
 
 
-def test_persistent_rollout_matches_per_step_launches(monkeypatch):
+@pytest.mark.parametrize("perm_source", ["device", "numpy"])
+def test_persistent_rollout_matches_per_step_launches(monkeypatch, perm_source):
     """ONE persistent launch per rollout (host-paced through the coherent
     control block) produces bit-identical rollouts, bootstrap values, episode
     statistics and — after learn() — parameters to one launch per step."""
-    a_pop, a_run = _runner_pair(monkeypatch, True)
-    b_pop, b_run = _runner_pair(monkeypatch, False)
+    a_pop, a_run = _runner_pair(monkeypatch, True, perm_source=perm_source)
+    b_pop, b_run = _runner_pair(monkeypatch, False, perm_source=perm_source)
     for _ in range(3):
-        for run in (a_run, b_run):
+        for run, seed in ((a_run, 77), (b_run, 77)):
+            if perm_source == "numpy":  # each run's own copy of the global stream
+                st = getattr(run, "_np_state", None)
+                np.random.set_state(st) if st is not None else np.random.seed(seed)
             run.iteration()
+            if perm_source == "numpy":
+                run.pop.discard_prefetch()
+                run._np_state = np.random.get_state()
         torch.cuda.synchronize()
         for name in ("obs", "actions", "log_probs", "values", "rewards", "dones", "advantages", "returns"):
             assert torch.equal(getattr(a_pop, name), getattr(b_pop, name)), name
@@ -532,3 +539,75 @@ def test_permutation_prefetch_keeps_the_draw_sequence(monkeypatch, source):
                     torch.as_tensor(np.random.random(4))))
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
+
+
+def test_env_exception_mid_rollout_leaves_learner_state_untouched(monkeypatch):
+    """The pipelined iteration queues GAE and the learner behind the
+    persistent rollout before the host paces it.  An env that raises mid
+    rollout aborts the rollout; the queued learner reads the control block's
+    timeout word when it starts and skips: parameters, both Adam moments and
+    the step counts stay bit-identical, and the next iteration runs."""
+    pop, run = _runner_pair(monkeypatch, True)
+    run.iteration()
+    torch.cuda.synchronize()
+    before = [t.clone() for t in (pop.params.data, pop.opt.exp_avg, pop.opt.exp_avg_sq, pop.opt.steps)]
+    real = run._env_step
+    calls = {"n": 0}
+
+    def flaky():
+        calls["n"] += 1
+        if calls["n"] == 4:
+            raise RuntimeError("env worker died")
+        real()
+
+    run._env_step = flaky
+    with pytest.raises(RuntimeError, match="env worker died"):
+        run.iteration()
+    torch.cuda.synchronize()
+    pop.check_errors()
+    after = (pop.params.data, pop.opt.exp_avg, pop.opt.exp_avg_sq, pop.opt.steps)
+    for name, a, b in zip(("params", "exp_avg", "exp_avg_sq", "steps"), before, after):
+        assert torch.equal(a, b), name
+    run._env_step = real
+    run.iteration()
+    torch.cuda.synchronize()
+    pop.check_errors()
+    assert not torch.equal(before[0], pop.params.data)  # the next learn does update
+    assert torch.equal(pop.opt.steps, before[3] + 2 * pop.n_minibatches())
+
+
+def test_env_that_synchronizes_the_device_completes(monkeypatch):
+    """An env whose step waits for the device (torch.cuda.synchronize()) would
+    stall a persistent rollout until its timeout (the device waits for the
+    host).  Under the default "auto" rule such an env — one that does not
+    declare agx_device_free — gets one launch per vector step, and the
+    iteration completes."""
+    import time
+
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+    from agilerl_amd.population.runner import PopulationRunner
+
+    class SyncingEnv(SyntheticVecEnv):
+        agx_device_free = False
+
+        def step(self, actions, **kw):
+            torch.cuda.synchronize()
+            return super().step(actions, **kw)
+
+    monkeypatch.delenv("AGX_PERSISTENT_ROLLOUT", raising=False)
+    monkeypatch.setenv("AGX_ROLLOUT_TIMEOUT", "5")
+    P, N = 2, 32
+    pop = PPOPopulation(ActorCriticSpec(obs_dim=8, n_actions=4), P, N, learn_step=8 * N, batch_size=64,
+                        update_epochs=2, device=DEV, fused=True)
+    run = PopulationRunner(pop, SyncingEnv(P * N, seed=1))
+    assert not run.persistent
+    assert PopulationRunner(pop, SyntheticVecEnv(P * N, seed=1)).persistent  # device-free envs keep the fast path
+    t0 = time.perf_counter()
+    for _ in range(2):
+        run.iteration()
+    torch.cuda.synchronize()
+    pop.check_errors()
+    assert time.perf_counter() - t0 < 4.0
+    assert torch.isfinite(pop.params.data).all()
