@@ -204,7 +204,7 @@ class ImageActorCriticSpec:
                 out[f"{net}.{name}.bias"] = (bo, (co,))
             out[f"{net}.{self.lin_out.name}.weight"] = (self.lin_out.w, (self.latent_dim, self.feat_dim))
             out[f"{net}.{self.lin_out.name}.bias"] = (self.lin_out.b, (self.latent_dim,))
-        for net, layers in (("actor.head_net.model", self.actor), ("critic.head_net.model", self.critic)):
+        for net, layers in (("actor.head_net._wrapped.model", self.actor), ("critic.head_net.model", self.critic)):
             for lay in layers:
                 out[f"{net}.{lay.name}.weight"] = (lay.w, (lay.fout, lay.fin))
                 out[f"{net}.{lay.name}.bias"] = (lay.b, (lay.fout,))

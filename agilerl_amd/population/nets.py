@@ -58,6 +58,20 @@ class ActorCriticSpec:
     # shares it (the reference default), so its layers are
     # shared_encoder_linear_layer_1, ... in the state dict
     encoder_name: str = "shared_encoder"
+    # architecture-mutation limits (population/arch.py): per MLP (min / max
+    # hidden layers, min / max nodes; EvolvableMLP's defaults 1, 3, 32, 500, or
+    # MlpNetConfig's 1, 3, 16, 500) and the latent's (min, max)
+    # (EvolvableNetwork: 8, 128)
+    encoder_limits: tuple = (1, 3, 32, 500)
+    actor_limits: tuple = (1, 3, 32, 500)
+    critic_limits: tuple = (1, 3, 32, 500)
+    latent_limits: tuple = (8, 128)
+
+    def shape_key(self) -> tuple:
+        """Agents with equal keys share a network layout (population groups)."""
+        return (self.obs_dim, self.n_actions, tuple(self.encoder_hidden), self.latent_dim, tuple(self.actor_hidden),
+                tuple(self.critic_hidden), self.layer_norm, self.encoder_name, tuple(self.encoder_limits),
+                tuple(self.actor_limits), tuple(self.critic_limits), tuple(self.latent_limits))
 
     def __post_init__(self) -> None:
         ln = "affine" if self.layer_norm else None
@@ -143,7 +157,10 @@ class ActorCriticSpec:
         out = {}
         # critic.encoder is the reference's detached copy of the shared actor encoder
         # (share_encoders, algo_utils.py:164-187): same offsets as actor.encoder
-        for net, layers in (("actor.encoder.model", self.encoder), ("actor.head_net.model", self.actor),
+        # the actor's head is an EvolvableDistribution wrapping the MLP
+        # (networks/actors.py:330-336, modules/base.py:740-760): its
+        # parameters sit under head_net._wrapped in the reference's state dict
+        for net, layers in (("actor.encoder.model", self.encoder), ("actor.head_net._wrapped.model", self.actor),
                             ("critic.encoder.model", self.encoder), ("critic.head_net.model", self.critic)):
             for lay in layers:
                 out[f"{net}.{lay.name}.weight"] = (lay.w, (lay.fout, lay.fin))

@@ -52,6 +52,14 @@ def _mlp(name: str, fin: int, hidden: list[int], fout: int, *, out_ln: bool, out
     return nn.Sequential(d)
 
 
+def reference_names(sd: dict) -> dict:
+    """Key names as the reference's PPO state dict has them: the golden
+    generator (tests/golden/gen_golden.py) names the actor's head MLP
+    ``actor.head_net.model.*``; the reference wraps it (``head_net._wrapped``)."""
+    return {(k.replace("actor.head_net.model.", "actor.head_net._wrapped.model.", 1)
+             if k.startswith("actor.head_net.model.") else k): v for k, v in sd.items()}
+
+
 class ActorCritic(nn.Module):
     """encoder [Linear-LN-ReLU]* -> Linear -> LN(plain) -> ReLU; actor head and
     critic ("value") head [Linear-LN-ReLU]* -> Linear."""
@@ -63,11 +71,13 @@ class ActorCritic(nn.Module):
         self.actor_head = _mlp("actor", latent, actor_hidden, n_actions, out_ln=False, out_act=False)
         self.critic_head = _mlp("value", latent, critic_hidden, 1, out_ln=False, out_act=False)
 
-    # reference state-dict prefixes of the three parts
-    PREFIX = {"encoder": "actor.encoder.model.", "actor_head": "actor.head_net.model.",
+    # reference state-dict prefixes of the three parts (the actor's head is an
+    # EvolvableDistribution wrapping the MLP: head_net._wrapped, actors.py:330-336)
+    PREFIX = {"encoder": "actor.encoder.model.", "actor_head": "actor.head_net._wrapped.model.",
               "critic_head": "critic.head_net.model."}
 
     def load_reference(self, sd: dict) -> None:
+        sd = reference_names(sd)
         with torch.no_grad():
             for part, pre in self.PREFIX.items():
                 mod = getattr(self, part)

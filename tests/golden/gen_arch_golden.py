@@ -1,0 +1,254 @@
+"""Golden vectors for PPO architecture mutations, from the reference's OWN code.
+
+Test infrastructure only (same rules as gen_golden.py: the reference's files
+are executed in place, path-loaded, with minimal ``sys.modules`` stand-ins for
+what is not installed here; only seeded inputs and the outputs the reference
+produced are written).  Skips when /root/reference is absent.
+
+Exercised (paths relative to /root/reference):
+  * agilerl/modules/base.py            EvolvableModule: mutation-method registry,
+                                       get_mutation_probs / sample_mutation_method
+                                       (:661-711), preserve_parameters, the
+                                       mutation wrapper that recreates the network
+  * agilerl/modules/mlp.py:213-312     EvolvableMLP add_layer / remove_layer /
+                                       add_node / remove_node
+  * agilerl/networks/base.py:445-503   EvolvableNetwork add_latent_node /
+                                       remove_latent_node, recreate_encoder
+  * agilerl/networks/actors.py         StochasticActor (PPO's actor, ppo.py:302-310)
+  * agilerl/networks/value_networks.py ValueNetwork (PPO's critic, ppo.py:312-320)
+  * agilerl/hpo/mutation.py:829-885    the single-agent architecture mutation:
+                                       the method sampled from the policy with
+                                       Mutations.rng, applied to the policy, the
+                                       same method + mutation dict applied to the
+                                       critic (_apply_arch_mutation :1013-1070)
+  * share_encoder_parameters (utils/algo_utils.py:164-187, the PPO mutation
+    hook): the critic's encoder takes the actor's encoder parameters —
+    restated here as a state-dict copy (tensordict is not installed).
+
+The module random generator (``EvolvableModule.rng``, which draws the layer
+and node counts) is seeded per case; the reference leaves it unseeded when the
+algorithm builds its networks, so the fixture pins what the draws DO, for
+given draws.  Fresh weights of a recreated network come from torch's global
+CPU generator (seeded per case), as in the reference.
+
+Usage:  python tests/golden/gen_arch_golden.py [--ref /root/reference]
+"""
+
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+# ---- gymnasium.spaces stand-ins (real classes: the reference checks isinstance) ----
+class Space:
+    def __init__(self, shape=None, dtype=None):
+        self.shape = tuple(shape) if shape is not None else None
+        self.dtype = np.dtype(dtype) if dtype is not None else None
+
+
+class Box(Space):
+    def __init__(self, low, high, shape, dtype=np.float32):
+        super().__init__(shape, dtype)
+        self.low = np.full(shape, low, dtype=dtype)
+        self.high = np.full(shape, high, dtype=dtype)
+
+
+class Discrete(Space):
+    def __init__(self, n):
+        super().__init__((), np.int64)
+        self.n = int(n)
+
+
+class _Other(Space):
+    pass
+
+
+def _flatdim(space):
+    if isinstance(space, Discrete):
+        return space.n
+    return int(np.prod(space.shape))
+
+
+def _package(name: str) -> types.ModuleType:
+    mod = types.ModuleType(name)
+    mod.__path__ = []
+    sys.modules[name] = mod
+    return mod
+
+
+class _AnyModule(types.ModuleType):
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        cls = type(name, (), {"__init__": lambda self, *a, **k: None})
+        setattr(self, name, cls)
+        return cls
+
+
+def _any(name: str) -> types.ModuleType:
+    mod = _AnyModule(name)
+    mod.__path__ = []
+    sys.modules[name] = mod
+    return mod
+
+
+def _load(ref: str, modname: str, relpath: str):
+    spec = importlib.util.spec_from_file_location(modname, os.path.join(ref, relpath))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[modname] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _setup(ref: str):
+    gym = _package("gymnasium")
+    sp = _package("gymnasium.spaces")
+    for cls in (Space, Box, Discrete):
+        setattr(sp, cls.__name__, cls)
+    for name in ("Dict", "Tuple", "MultiDiscrete", "MultiBinary", "Graph", "Text", "Sequence"):
+        setattr(sp, name, type(name, (_Other,), {}))
+    sp.flatdim = _flatdim
+    gym.spaces = sp
+    _any("tensordict")
+    _any("tensordict.nn")
+    agilerl = _package("agilerl")
+    agilerl.__path__ = [os.path.join(ref, "agilerl")]
+    _load(ref, "agilerl.protocols", "agilerl/protocols.py")
+    _any("agilerl.typing")  # annotations only
+    mods = _package("agilerl.modules")
+    cc = _load(ref, "agilerl.modules.custom_components", "agilerl/modules/custom_components.py")
+    base = _load(ref, "agilerl.modules.base", "agilerl/modules/base.py")
+    for name in ("EvolvableModule", "EvolvableWrapper", "ModuleDict"):
+        setattr(mods, name, getattr(base, name))
+    for name in ("GumbelSoftmax", "NewGELU", "NoisyLinear"):
+        setattr(mods, name, getattr(cc, name))
+    cfg = _load(ref, "agilerl.modules.configs", "agilerl/modules/configs.py")
+    utils = _package("agilerl.utils")
+    au = types.ModuleType("agilerl.utils.algo_utils")
+    au.get_output_size_from_space = lambda s: s.n if isinstance(s, Discrete) else int(np.prod(s.shape))
+    sys.modules["agilerl.utils.algo_utils"] = au
+    utils.algo_utils = au
+    _load(ref, "agilerl.utils.torch_utils", "agilerl/utils/torch_utils.py")
+    en = _load(ref, "agilerl.utils.evolvable_networks", "agilerl/utils/evolvable_networks.py")
+    mlp = _load(ref, "agilerl.modules.mlp", "agilerl/modules/mlp.py")
+    mods.EvolvableMLP = mlp.EvolvableMLP
+    for name in ("EvolvableCNN", "EvolvableLSTM", "EvolvableMultiInput", "EvolvableSimBa", "EvolvableResNet",
+                 "EvolvableBERT", "EvolvableGPT"):
+        setattr(mods, name, type(name, (base.EvolvableModule,), {}))
+    _package("agilerl.networks")
+    _load(ref, "agilerl.networks.distributions", "agilerl/networks/distributions.py")
+    nb = _load(ref, "agilerl.networks.base", "agilerl/networks/base.py")
+    act = _load(ref, "agilerl.networks.actors", "agilerl/networks/actors.py")
+    val = _load(ref, "agilerl.networks.value_networks", "agilerl/networks/value_networks.py")
+    return dict(base=base, cfg=cfg, en=en, mlp=mlp, nb=nb, actors=act, values=val)
+
+
+def _apply_arch_mutation(network, mut_method, applied_mut_dict=None):
+    """agilerl/hpo/mutation.py:1013-1070 (_apply_arch_mutation), restated
+    line by line on the loaded reference modules (the Mutations class itself
+    would pull in the algorithm hierarchy)."""
+    applied_mut_dict = applied_mut_dict or {}
+    mut_dict = None
+    if mut_method is None:
+        mut_dict = {}
+        network.last_mutation_attr = None
+        network.last_mutation = None
+    else:
+        mut_return = getattr(network, mut_method)(**applied_mut_dict)
+        mut_dict = mut_return if mut_return is not None else {}
+    return network.last_mutation_attr, mut_dict
+
+
+def _sd(prefix: str, net) -> dict:
+    return {f"{prefix}.{k}": v.detach().numpy().copy() for k, v in net.state_dict().items()}
+
+
+def _shape_info(net) -> dict:
+    return {"latent": int(net.latent_dim), "enc_hidden": list(net.encoder.hidden_size),
+            "head_hidden": list(net.head_net.net_config["hidden_size"]) if hasattr(net.head_net, "net_config")
+            else None}
+
+
+def gen_cases(m: dict, out: dict) -> None:
+    """One architecture mutation of a freshly built PPO actor / critic pair per
+    case — the situation of every mutation in training: tournament selection
+    clones each agent (a new network object built from its init dict) right
+    before the generation's mutation.  Starting shapes cover fresh and
+    previously mutated architectures; the seeds cover every method."""
+    actors, values = m["actors"], m["values"]
+    obs, act = Box(-np.inf, np.inf, (8,)), Discrete(4)
+    starts = [
+        ([64], [64], 64), ([64], [64], 64), ([80], [64], 96), ([64], [64, 64], 64), ([128], [96, 64, 64], 72),
+        ([64, 64], [64], 64), ([64], [64], 120), ([64], [64], 16), ([496], [496], 64), ([64], [64], 64),
+    ]
+    idx = 0
+    for k in range(24):
+        enc_h, head_h, latent = starts[k % len(starts)]
+        nlp = (0.2, 0.5, 1.0, 0.0)[k % 4]
+        enc = {"hidden_size": list(enc_h), "min_mlp_nodes": 64, "max_mlp_nodes": 500}
+        head = {"hidden_size": list(head_h), "min_hidden_layers": 1, "max_hidden_layers": 3, "min_mlp_nodes": 64,
+                "max_mlp_nodes": 500}
+        torch.manual_seed(100 + k)
+        # ppo.py:288-320: the critic gets a deep copy of the net config (and of the head config)
+        import copy
+
+        net_config = {"encoder_config": copy.deepcopy(enc), "head_config": copy.deepcopy(head), "latent_dim": latent}
+        critic_config = copy.deepcopy(net_config)
+        critic_config["head_config"]["output_activation"] = None
+        actor = actors.StochasticActor(obs, act, device="cpu", encoder_name="shared_encoder", **net_config)
+        critic = values.ValueNetwork(obs, device="cpu", encoder_name="shared_encoder", **critic_config)
+        critic.encoder.load_state_dict(actor.encoder.state_dict())  # share_encoder_parameters
+        actor.rng = np.random.default_rng(1000 + k)
+        rng = np.random.default_rng(2000 + k)
+        g = {"methods": np.array(actor.mutation_methods),
+             "probs": np.array(actor.get_mutation_probs(nlp), dtype=np.float64),
+             "new_layer_prob": np.array(nlp), "start": np.array(repr((enc_h, head_h, latent))),
+             "module_rng_seed": np.array(1000 + k), "mutations_rng_seed": np.array(2000 + k)}
+        before = {**_sd("actor", actor), **_sd("critic", critic)}
+        torch.manual_seed(5000 + k)  # the fresh weights of the recreated networks
+        g["torch_seed"] = np.array(5000 + k)
+        mut_method = actor.sample_mutation_method(nlp, rng)  # queries the actor's method table
+        applied, mut_dict = _apply_arch_mutation(actor, mut_method)
+        if applied in critic.mutation_methods:
+            _apply_arch_mutation(critic, applied, mut_dict)
+        critic.encoder.load_state_dict(actor.encoder.state_dict())  # the PPO mutation hook
+        g["sampled"] = np.array(str(mut_method))
+        g["applied"] = np.array("None" if applied is None else str(applied))
+        g["mut_dict"] = np.array(repr(sorted((kk, int(v)) for kk, v in (mut_dict or {}).items())))
+        g["shapes"] = np.array(repr({"actor": _shape_info(actor), "critic": _shape_info(critic)}))
+        for kk, v in before.items():
+            g[f"before.{kk}"] = v
+        for kk, v in {**_sd("actor", actor), **_sd("critic", critic)}.items():
+            g[f"after.{kk}"] = v
+        out[f"arch{idx}"] = g
+        idx += 1
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    args = ap.parse_args()
+    if not os.path.isdir(os.path.join(args.ref, "agilerl")):
+        print("reference checkout not found; skipping")
+        return
+    m = _setup(args.ref)
+    out: dict = {}
+    gen_cases(m, out)
+    for name, arrays in out.items():
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
+    print(f"wrote {len(out)} fixture groups: {sorted(out)}")
+
+
+if __name__ == "__main__":
+    main()

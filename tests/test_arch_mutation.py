@@ -1,0 +1,63 @@
+"""a20: PPO architecture mutations (population/arch.py) against the
+reference's own outputs (tests/golden/gen_arch_golden.py: StochasticActor /
+ValueNetwork built and mutated by agilerl/networks, modules/base.py and
+modules/mlp.py, one mutation of a freshly built pair per case, the situation
+of every mutation in training).  Bit-exact: the method table and its
+probabilities, the method sampled with Mutations.rng, the method applied
+(with the add_layer / remove_layer -> add_node fallbacks), the mutation
+dict, every resulting shape, and every parameter of actor and critic — the
+preserved slices and the freshly initialised entries (torch's global CPU
+generator, drawn in the reference's module construction order)."""
+
+import ast
+
+import numpy as np
+import pytest
+import torch
+
+CASES = [f"arch{i}" for i in range(24)]
+
+
+def _spec(g):
+    from agilerl_amd.population.nets import ActorCriticSpec
+
+    enc_h, head_h, latent = ast.literal_eval(str(g["start"]))
+    lim = (1, 3, 64, 500)  # ppo.yaml NET_CONFIG: min_mlp_nodes 64, max_mlp_nodes 500, 1-3 head layers
+    return ActorCriticSpec(obs_dim=8, n_actions=4, encoder_hidden=list(enc_h), latent_dim=latent,
+                           actor_hidden=list(head_h), critic_hidden=list(head_h), encoder_limits=lim,
+                           actor_limits=lim, critic_limits=lim)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_arch_mutation_matches_reference(golden, case):
+    from agilerl_amd.population import arch
+
+    g = golden(case)
+    spec = _spec(g)
+    assert list(g["methods"]) == arch.METHODS
+    np.testing.assert_allclose(arch.method_probs(float(g["new_layer_prob"])), g["probs"], rtol=0, atol=1e-15)
+    method = arch.sample_method(float(g["new_layer_prob"]), np.random.default_rng(int(g["mutations_rng_seed"])))
+    assert method == str(g["sampled"])
+    flat = torch.zeros(spec.n_params)
+    for k, (o, sh) in spec.state_dict_keys().items():
+        if not k.startswith("critic.encoder."):
+            flat[o:o + int(np.prod(sh))] = torch.from_numpy(g["before." + k]).reshape(-1)
+    # the pair shares its encoder (PPO's share_encoder_parameters)
+    for k in spec.state_dict_keys():
+        if k.startswith("critic.encoder."):
+            assert np.array_equal(g["before." + k], g["before." + k.replace("critic.", "actor.", 1)])
+    torch.manual_seed(int(g["torch_seed"]))
+    new_spec, new_flat, applied, mut_dict = arch.mutate(spec, flat, method,
+                                                        np.random.default_rng(int(g["module_rng_seed"])))
+    assert applied == str(g["applied"])
+    assert repr(sorted(mut_dict.items())) == str(g["mut_dict"])
+    shapes = ast.literal_eval(str(g["shapes"]))
+    assert new_spec.latent_dim == shapes["actor"]["latent"] == shapes["critic"]["latent"]
+    assert new_spec.encoder_hidden == shapes["actor"]["enc_hidden"]
+    assert new_spec.actor_hidden == shapes["actor"]["head_hidden"]
+    assert new_spec.critic_hidden == shapes["critic"]["head_hidden"]
+    keys = new_spec.state_dict_keys()
+    assert set("after." + k for k in keys) == {k for k in g.files if k.startswith("after.")}
+    for k, (o, sh) in keys.items():
+        got = new_flat[o:o + int(np.prod(sh))].view(sh).numpy()
+        assert np.array_equal(got, g["after." + k]), k

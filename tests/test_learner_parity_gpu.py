@@ -52,7 +52,9 @@ def _assert_close(name, a, b, rtol=RTOL, frac=1e-4):
 
 
 def _names(g, prefix):
-    return {k[len(prefix):]: g[k] for k in g if k.startswith(prefix)}
+    from oracle.ppo_learn import reference_names
+
+    return reference_names({k[len(prefix):]: g[k] for k in g if k.startswith(prefix)})
 
 
 def _pop(P, N, T, D, A, enc, lat, ah, ch, batch, epochs, lr, target_kl=None, masks=False, seeds=None):

@@ -199,7 +199,7 @@ def test_image_actor_critic_spec_layout():
     assert keys["actor.encoder.model.shared_encoder_conv_layer_1.weight"][1] == (32, 4, 8, 8)
     assert keys["actor.encoder.model.shared_encoder_conv_layer_3.weight"][1] == (128, 64, 3, 3)
     assert keys["actor.encoder.model.shared_encoder_linear_output.weight"][1] == (256, 128 * 7 * 7)
-    assert keys["actor.head_net.model.actor_linear_layer_1.weight"][1] == (256, 256)
+    assert keys["actor.head_net._wrapped.model.actor_linear_layer_1.weight"][1] == (256, 256)
     assert keys["critic.head_net.model.value_linear_layer_output.weight"][1] == (1, 256)
     assert keys["critic.encoder.model.shared_encoder_conv_layer_2.bias"] == \
         keys["actor.encoder.model.shared_encoder_conv_layer_2.bias"]
@@ -214,5 +214,5 @@ def test_image_actor_critic_spec_layout():
     flat = spec.init_params(2, [0, 1])
     w1 = flat[0, :32 * 4 * 64].view(32, 256)
     torch.testing.assert_close(w1 @ w1.T, 2.0 * torch.eye(32), rtol=0, atol=1e-4)  # orthogonal, gain sqrt 2
-    o, sh = keys["actor.head_net.model.actor_linear_layer_output.weight"]
+    o, sh = keys["actor.head_net._wrapped.model.actor_linear_layer_output.weight"]
     assert flat[0, o:o + 4 * 256].abs().max() < 0.2  # output_vanish x0.1
