@@ -57,7 +57,7 @@ def test_arch_mutation_matches_reference(golden, case):
     assert new_spec.actor_hidden == shapes["actor"]["head_hidden"]
     assert new_spec.critic_hidden == shapes["critic"]["head_hidden"]
     keys = new_spec.state_dict_keys()
-    assert set("after." + k for k in keys) == {k for k in g.files if k.startswith("after.")}
+    assert set("after." + k for k in keys) == {k for k in g if k.startswith("after.")}
     for k, (o, sh) in keys.items():
         got = new_flat[o:o + int(np.prod(sh))].view(sh).numpy()
         assert np.array_equal(got, g["after." + k]), k
