@@ -36,7 +36,7 @@ SIGNATURES = {
     "agx_ppo_learn_prepare": (_INT, [_P, _P, _P]),
     "agx_ppo_learn": (_INT, [_P, _P, _P, _P]),
     "agx_ppo_act": (_INT, [_P, _I, _I, _P, _P, _I, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P,
-                           _I, _P, _I, _P]),
+                           _I, _P, _P, _P]),
     "agx_ppo_rollout_step": (_INT, [_P, _I, _I, _P, _P, _INT, _INT, ctypes.c_uint64, ctypes.c_uint64, _P]),
     "agx_rollout_workgroups": (_I, [_I, _I]),
     "agx_rollout_max_workgroups": (_I, [_P]),

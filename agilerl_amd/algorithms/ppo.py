@@ -10,8 +10,9 @@ population of one.
 
 Supported: Discrete action spaces, Box observations, ``net_config`` with
 ``encoder_config`` / ``head_config`` MLP ``hidden_size`` lists and
-``latent_dim`` (the reference's defaults: encoder [64] -> latent 64, actor
-head [64], critic head [16] unless ``head_config`` is given, ppo.py:286-300),
+``latent_dim`` (the reference's defaults: encoder [64, 64] -> latent 32,
+actor head [32], critic head [16] unless ``head_config`` is given,
+ppo.py:286-320 via networks/base.py and networks/actors.py),
 LayerNorm on, shared encoder.  ``get_action`` / ``learn`` / ``test`` keep the
 reference's signatures and return types; recurrent policies,
 continuous actions and custom ``actor_network`` objects raise
@@ -57,7 +58,7 @@ def _image_spec(observation_space, action_space, net_config: dict, normalize_ima
     if enc.get("activation", "ReLU") != "ReLU" or enc.get("output_activation", "ReLU") not in (None, "ReLU"):
         raise NotImplementedError("agx image PPO: ReLU encoders")
     head = as_config(net_config.get("head_config"))
-    actor_hidden = _hidden(head, [64])
+    actor_hidden = _hidden(head, [32])
     critic_hidden = _hidden(head, [16])  # ppo.py:292-300 default critic head
     head_ln = bool((head or {}).get("layer_norm", True))
     dtype = torch.uint8 if np.dtype(observation_space.dtype) == np.uint8 else torch.float32
@@ -69,7 +70,26 @@ def _image_spec(observation_space, action_space, net_config: dict, normalize_ima
                                 obs_dtype=dtype, image_norm=norm)
 
 
+def _limits(cfg, config_default: bool) -> tuple:
+    """(min / max hidden layers, min / max nodes) of an MLP built from ``cfg``:
+    a dict falls back on EvolvableMLP's defaults (1, 3, 32, 500,
+    modules/mlp.py:61-82), an MlpNetConfig on its own (1, 3, 16, 500,
+    modules/configs.py:56-70)."""
+    d = (1, 3, 16, 500) if config_default else (1, 3, 32, 500)
+    if cfg is None:
+        return d
+    get = cfg.get if isinstance(cfg, dict) else (lambda k, v: getattr(cfg, k, v))
+    return (int(get("min_hidden_layers", d[0])), int(get("max_hidden_layers", d[1])),
+            int(get("min_mlp_nodes", d[2])), int(get("max_mlp_nodes", d[3])))
+
+
 def spec_from_net_config(observation_space, action_space, net_config: dict | None, normalize_images: bool = True):
+    """The networks ppo.py:286-320 builds, as the reference's defaults fill
+    them in: no encoder_config -> get_default_encoder_config's MlpNetConfig
+    [64, 64] (utils/evolvable_networks.py:168-217); latent_dim 32 with limits
+    8 / 128 (networks/base.py:191-194); no head_config -> actor head
+    MlpNetConfig [32] (networks/actors.py:300-303), critic head [16]
+    (ppo.py:292-300)."""
     if not hasattr(action_space, "n"):
         raise NotImplementedError("agx PPO supports Discrete action spaces")
     net_config = dict(net_config or {})
@@ -77,14 +97,20 @@ def spec_from_net_config(observation_space, action_space, net_config: dict | Non
 
     if is_image_space(observation_space):
         return _image_spec(observation_space, action_space, net_config, normalize_images)
-    enc = _hidden(net_config.get("encoder_config"), [64])
+    enc_cfg = net_config.get("encoder_config")
+    enc = _hidden(enc_cfg, [64, 64])
     head = net_config.get("head_config")
-    actor_hidden = _hidden(head, [64])
+    actor_hidden = _hidden(head, [32])
     critic_hidden = _hidden(head, [16])  # ppo.py:292-300 default critic head
-    latent = int(net_config.get("latent_dim", 64))
+    latent = int(net_config.get("latent_dim", 32))
     obs_dim = int(np.prod(observation_space.shape))
+    enc_lim = _limits(enc_cfg, enc_cfg is None or not isinstance(enc_cfg, dict))
+    head_lim = _limits(head, head is None or not isinstance(head, dict))
+    lat_lim = (int(net_config.get("min_latent_dim", 8)), int(net_config.get("max_latent_dim", 128)))
     return ActorCriticSpec(obs_dim=obs_dim, n_actions=int(action_space.n), encoder_hidden=enc, latent_dim=latent,
-                           actor_hidden=actor_hidden, critic_hidden=critic_hidden)
+                           actor_hidden=actor_hidden, critic_hidden=critic_hidden, encoder_limits=enc_lim,
+                           actor_limits=head_lim, critic_limits=head_lim if head is not None else (1, 3, 16, 500),
+                           latent_limits=lat_lim)
 
 
 class PPO:
@@ -134,6 +160,15 @@ class PPO:
             _row = 0
         self.population, self.row = _population, int(_row)
         self._counter = 0
+        # architecture / learn_step mutations waiting for the population engine
+        # to regroup the agents (population/engine.py)
+        self._pending_state = None
+        self._pending_learn_step = None
+        # the networks' own generators for node / layer counts (the reference's
+        # EvolvableModule.rng; seeded from the agent's initial index so a run
+        # is reproducible and a sharded population draws as the whole one)
+        self.module_rng = np.random.default_rng((0x5EED, int(index)))
+        self.critic_rng = np.random.default_rng((0x5EEE, int(index)))
         pop = self.population
         if _population is not None and (batch_size, update_epochs, ent_coef) != (
                 pop.agent_batch[self.row], pop.agent_epochs[self.row], pop.agent_ent[self.row]):
@@ -152,7 +187,14 @@ class PPO:
 
     def reinit_optimizers(self, optimizer=None) -> None:
         """core/base.py:760-775: a fresh Adam for this agent (zero moments and
-        step, current lr) — after an lr or a parameter mutation."""
+        step, current lr) — after an lr, a parameter or an architecture
+        mutation."""
+        if self._pending_state is not None:
+            s = self._pending_state
+            s.exp_avg.zero_()
+            s.exp_avg_sq.zero_()
+            s.step = 0
+            return
         self.population.reinit_agent_optimizer(self.row)
 
     @property
@@ -181,12 +223,45 @@ class PPO:
 
     @property
     def learn_step(self) -> int:
-        return self._learn_step
+        return self._pending_learn_step or self._learn_step
 
     @learn_step.setter
     def learn_step(self, value: int) -> None:
-        if int(value) != self._learn_step:
-            self.population.set_agent_hparam(self.row, "learn_step", int(value))  # raises: shared rollout length
+        """The rollout length (ppo.py:363 capacity ceil(learn_step / num_envs));
+        the population engine moves the agent to a group of its learn_step at
+        the next generation (the reference's create_rollout_buffer hook)."""
+        value = int(value)
+        if value < 1:
+            raise ValueError("learn_step must be >= 1")
+        self._pending_learn_step = value if value != self._learn_step else None
+        if self._pending_state is not None:
+            self._pending_state.learn_step = value
+
+    @property
+    def can_mutate_architecture(self) -> bool:
+        from ..population.nets import ActorCriticSpec
+
+        return isinstance(self.spec, ActorCriticSpec)
+
+    def architecture_mutation(self, new_layer_prob: float, rng) -> str | None:
+        """mutation.py:829-885 on this agent (population/arch.py): -> the
+        applied method.  The mutated networks wait in a pending state for the
+        engine's regroup (the row layout of the current group is another
+        shape's)."""
+        from ..population import arch
+        from ..population.engine import AgentState
+
+        method = arch.sample_method(new_layer_prob, rng)
+        spec, pop, r = self.spec, self.population, self.row
+        flat = (self._pending_state.params if self._pending_state is not None
+                else pop.params.data[r, :spec.n_params]).cpu()
+        new_spec, new_flat, applied, _ = arch.mutate(spec, flat, method, self.module_rng, self.critic_rng)
+        n = new_spec.n_params
+        zeros = torch.zeros(n, dtype=torch.float32, device=pop.device)
+        self._pending_state = AgentState(new_spec, self.learn_step, new_flat.to(pop.device), zeros.clone(),
+                                         zeros.clone(), 0, float(pop.agent_lr[r]), int(pop.agent_batch[r]),
+                                         int(pop.agent_epochs[r]), float(pop.agent_ent[r]))
+        return applied
 
     def get_lr_names(self) -> list[str]:
         return ["lr"]
@@ -209,12 +284,13 @@ class PPO:
     # ------------------------------------------------------------------ #
     @property
     def spec(self) -> ActorCriticSpec:
-        return self.population.spec
+        return self._pending_state.spec if self._pending_state is not None else self.population.spec
 
     def state_dict(self) -> dict[str, torch.Tensor]:
         """Reference-compatible parameter names (actor.encoder / head_net /
-        critic.head_net ...) -> tensors (views of the HBM row)."""
-        flat = self.population.params.data[self.row]
+        critic.head_net ...) -> tensors (views of the HBM row, or of the
+        pending mutated state)."""
+        flat = self._pending_state.params if self._pending_state is not None else self.population.params.data[self.row]
         return {k: flat[off:off + int(np.prod(shape))].view(shape)
                 for k, (off, shape) in self.spec.state_dict_keys().items()}
 
@@ -321,9 +397,9 @@ class PPO:
             self._counter += 1
             params = pop.params.data[self.row]
             _lib.call("agx_ppo_act", ctypes.byref(desc), 1, n, params.data_ptr(), o.data_ptr(), 0, _lib.ptr(mask), 0,
-                      1, pop.act_seed + 7919 * (pop.agent_offset + self.row), (1 << 40) + self._counter,
+                      1, pop.act_seed + 7919 * pop.agent_ids[self.row], (1 << 40) + self._counter,
                       out["actions"].data_ptr(), out["log_probs"].data_ptr(), out["values"].data_ptr(),
-                      out["entropy"].data_ptr(), 0, None, 0, _lib.stream())
+                      out["entropy"].data_ptr(), 0, None, None, _lib.stream())
         return tuple(out[k].cpu().numpy() for k in ("actions", "log_probs", "entropy", "values"))
 
     def learn(self, experiences=None) -> float:

@@ -260,7 +260,9 @@ constexpr LearnPlan make_plan(NetDims d) {
     X(4, 2, 2, 64, 64, 0, 64, 64)  /* CartPole */                        \
     X(6, 3, 2, 64, 64, 0, 64, 64)  /* Acrobot */                         \
     X(8, 4, 2, 64, 64, 0, 64, 16)  /* reference PPO default critic head [16] */ \
-    X(4, 2, 2, 64, 64, 0, 64, 16)
+    X(4, 2, 2, 64, 64, 0, 64, 16)                                        \
+    X(8, 4, 3, 64, 64, 32, 32, 16) /* PPO with no net_config: encoder [64, 64] -> latent 32, heads [32] / [16] */ \
+    X(4, 2, 3, 64, 64, 32, 32, 16)
 
 template <int D_, int A_, int NE_, int E0, int E1, int E2, int HA, int HC>
 struct Shape {
@@ -1587,7 +1589,7 @@ struct ActArgs {
     long long mask_pstride;
     unsigned char *mask_copy;
     long long mask_copy_pstride;
-    unsigned long long env_base;  // global index of env (agent 0, env 0): the Philox stream of a sharded population
+    const long long *env_base;  // [P] global index of each agent's env 0 (Philox stream), or null: p * N
 };
 
 // The env staging may be host memory that the host rewrites between the
@@ -1684,7 +1686,8 @@ __device__ __forceinline__ void act_body(const ActArgs &g, float *sm, bool resid
     const float H = -row_sum(a < pl.A ? pa * logf(pa + 1e-8f) : 0.f);
     float score = lg;
     if (g.sample) {
-        const unsigned long long env = g.env_base + (unsigned long long)p * g.N + n0 + r;
+        const unsigned long long env =
+            (g.env_base ? (unsigned long long)g.env_base[p] : (unsigned long long)p * g.N) + n0 + r;
         const uint4 rnd = philox(make_uint4((unsigned)env, (unsigned)(env >> 32), (unsigned)g.counter,
                                             (unsigned)(g.counter >> 32) ^ ((unsigned)(a >> 2) << 24)),
                                  make_uint2((unsigned)g.seed, (unsigned)(g.seed >> 32)));
@@ -2085,8 +2088,9 @@ extern "C" int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const f
                            int64_t obs_agent_stride, const uint8_t *action_mask, int64_t mask_agent_stride,
                            int sample, uint64_t seed, uint64_t counter,
                            int64_t *actions, float *log_probs, float *values, float *entropy,
-                           int64_t out_agent_stride, int64_t *actions_flat, int64_t env_base, void *stream) {
-    AGX_REQUIRE(net && params && obs && P > 0 && N > 0 && P <= 65535 && env_base >= 0, "agx_ppo_act: bad arguments");
+                           int64_t out_agent_stride, int64_t *actions_flat, const int64_t *agent_env_base,
+                           void *stream) {
+    AGX_REQUIRE(net && params && obs && P > 0 && N > 0 && P <= 65535, "agx_ppo_act: bad arguments");
     Launcher L;
     if (!find_launcher(net, L)) {
         set_error("agx_ppo_act: network shape not instantiated");
@@ -2122,7 +2126,7 @@ extern "C" int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const f
     a.mask_pstride = mask_agent_stride;
     a.mask_copy = nullptr;
     a.mask_copy_pstride = 0;
-    a.env_base = (unsigned long long)env_base;
+    a.env_base = reinterpret_cast<const long long *>(agent_env_base);
     dim3 grid((unsigned)ceil_div(N, kSB), (unsigned)P);
     L.act(a, grid, (size_t)L.plan->act_floats * sizeof(float), as_stream(stream));
     return check_launch("agx_ppo_act");
@@ -2159,7 +2163,7 @@ static void fill_rollout_args(ActArgs &a, const LearnPlan &pl, int64_t P, int64_
     a.mask_pstride = N * (int64_t)pl.A;
     a.mask_copy = io->mask_slot;
     a.mask_copy_pstride = io->mask_agent_stride;
-    a.env_base = (unsigned long long)io->env_base;
+    a.env_base = reinterpret_cast<const long long *>(io->agent_env_base);
 }
 
 static int check_rollout_io(const agx_rollout_io *io, int act, const float *params, const char *who) {

@@ -20,12 +20,18 @@ What runs, with the reference's draws from the reference's generators:
   (a few KB) is updated on the host with the reference's CPU indexing
   semantics and copied back to its HBM row.
 
-Not applied (the fused kernels are compiled per network shape, SURVEY §8 /
-DESIGN §7): architecture and activation mutations, and ``learn_step`` (the
-rollout length every agent of the lock-step engine shares).  Those choices
-are recorded as ``mut = "None"`` with a warning.  They would also draw from
-the generators in the reference, so a run that samples them leaves the
-reference's random stream from that point on.
+* ``architecture_mutate`` (:373-411, :829-885) on PPO agents: the method
+  sampled from the actor's mutation table with ``self.rng``, applied to the
+  actor, the applied method to the critic, shared encoder, fresh optimizer
+  (population/arch.py, bit-exact against the reference's own networks); the
+  population engine regroups agents by network shape;
+* ``learn_step`` as an RL hyperparameter: the agent's rollout length, applied
+  by the engine at the next generation (agents grouped by learn_step).
+
+Not applied: activation mutations of PPO / MADDPG (the reference itself
+skips them for policy-gradient algorithms, :469-479) and architecture /
+activation mutations of DQN / Rainbow / MADDPG agents (recorded as no
+mutation with a warning).
 """
 
 from __future__ import annotations
@@ -112,9 +118,26 @@ class Mutations:
         return individual
 
     def architecture_mutate(self, individual):
-        return self._not_applied(individual, "architecture")
+        """mutation.py:373-411 -> _architecture_mutate_single (:829-885) for
+        individuals that can change shape (PPO views: population/arch.py — the
+        method sampled from the actor's table with self.rng, applied to the
+        actor, the applied method to the critic, the shared encoder, then
+        mutation_hook and a fresh optimizer).  Other algorithms: not applied."""
+        fn = getattr(individual, "architecture_mutation", None)
+        if fn is None or not getattr(individual, "can_mutate_architecture", False):
+            return self._not_applied(individual, "architecture")
+        applied = fn(self.new_layer_prob, self.rng)
+        individual.mutation_hook()
+        individual.reinit_optimizers()
+        individual.mut = applied or "None"
+        return individual
 
     def activation_mutation(self, individual):
+        if getattr(individual, "algo", None) in ("PPO", "DDPG", "TD3", "IPPO", "MADDPG", "MATD3", "GRPO"):
+            # mutation.py:469-479: policy-gradient algorithms keep their activations
+            warnings.warn(f"Activation mutations are not supported for {individual.algo}.", stacklevel=2)
+            individual.mut = "None"
+            return individual
         return self._not_applied(individual, "activation")
 
     def rl_hyperparam_mutation(self, individual):

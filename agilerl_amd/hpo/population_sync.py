@@ -205,7 +205,9 @@ class PopulationSync:
                 b.index_copy_(0, dst_idx, rows[:, offs[k]:offs[k + 1]])
 
     @torch.no_grad()
-    def generation(self) -> list[int]:
+    def select(self) -> list[int]:
+        """Fitness all-gather and the tournament over the global population
+        (no row is moved): -> the parent of every global slot."""
         if self.rng_state is None and hasattr(self.pop, "discard_prefetch"):
             # the tournament draws from the global numpy stream: put back any
             # minibatch shuffles drawn ahead, so the draws keep the reference's order
@@ -217,6 +219,12 @@ class PopulationSync:
         # clones inherit their parent's fitness history (copy_attributes, core/base.py:444-503),
         # which the next generation's eval_loop window reads
         self.history = [np.asarray(h)[np.asarray(parents)] for h in self.history]
+        self.last_parents = parents
+        return parents
+
+    @torch.no_grad()
+    def generation(self) -> list[int]:
+        parents = self.select()
         self._clone_rows(parents)
         if hasattr(self.pop, "after_clone"):
             P = self.pop.P

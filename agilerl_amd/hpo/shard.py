@@ -110,6 +110,11 @@ def host_record(agent) -> dict:
     rec["_weights"] = [[(k, tuple(t.shape), str(t.dtype).replace("torch.", "")) for k, t in g.items()]
                        for g in _weight_groups(agent)]
     rec["_groups_api"] = hasattr(agent, "policy_weight_groups")
+    rec["algo"] = getattr(agent, "algo", None)
+    if hasattr(agent, "population"):  # a PPO view: what a clone of it on another rank is made of
+        rec["_spec"] = agent.spec
+        rec["_adam_step"] = int(agent.population.opt.steps[agent.row])
+        rec["_arch_rngs"] = (agent.module_rng.bit_generator.state, agent.critic_rng.bit_generator.state)
     return rec
 
 
@@ -128,6 +133,8 @@ class RemoteAgent:
         d["_lr_names"] = list(rec["_lr_names"])
         d["_weights"] = rec["_weights"]
         d["_groups_api"] = rec["_groups_api"]
+        d["_spec"] = rec.get("_spec")
+        d["_arch_rngs"] = rec.get("_arch_rngs")
 
     def __getattr__(self, name):
         hp = self.__dict__.get("_hp", {})
@@ -161,6 +168,28 @@ class RemoteAgent:
 
     def mutation_hook(self) -> None:
         pass
+
+    @property
+    def can_mutate_architecture(self) -> bool:
+        return self.__dict__.get("_spec") is not None
+
+    def architecture_mutation(self, new_layer_prob: float, rng):
+        """The draws of a PPO view's architecture mutation (population/arch.py):
+        the method from ``rng`` (Mutations.rng), the module generators' node /
+        layer draws, and torch's global CPU generator for the fresh weights
+        (the same modules built on zeros)."""
+        if self._spec is None:
+            raise AttributeError("architecture_mutation")
+        from ..population import arch
+
+        method = arch.sample_method(new_layer_prob, rng)
+        gens = []
+        for st in self._arch_rngs:
+            g = np.random.default_rng()
+            g.bit_generator.state = st
+            gens.append(g)
+        _, _, applied, _ = arch.mutate(self._spec, torch.zeros(self._spec.n_params), method, gens[0], gens[1])
+        return applied
 
 
 def gather_records(pop, group=None) -> list[dict]:

@@ -1,0 +1,329 @@
+"""The population engine of train_on_policy: agents with different networks
+and rollout lengths, as architecture and ``learn_step`` mutations make them.
+
+The reference trains the agents of a population one after another, each
+with its own networks and its own rollout length (train_on_policy.py:
+210-262: ``-(evo_steps // -agent.learn_step)`` collect + learn iterations of
+``ceil(learn_step / num_envs)`` vector steps per agent and generation).
+Here the agents are SLOTS (local slot j = global agent rank * P + j, which
+owns its env copy and its sampling streams) grouped by (network shape,
+learn_step): every group is one :class:`PPOPopulation` (stacked parameters,
+Adam state and rollout SoA in HBM; the fused HIP learner and rollout when the
+shape is instantiated, the autograd learner with the HIP loss / clip + Adam
+kernels otherwise) with its own :class:`PopulationRunner` over its slots'
+envs.  An unmutated population is ONE group: exactly the lock-step engine.
+
+Per generation:
+  * ``draw_generation_perms``: the minibatch shuffles of the whole
+    generation from numpy's global stream, agent after agent over the GLOBAL
+    population (each agent's K learns of E shuffles, ppo.py:836-842), each
+    group taking its agents' rows — the reference's draw order;
+  * ``train``: every group runs its agents' K iterations;
+  * fitness / episode scores per slot;
+  * the clone (tournament): a single unchanged group keeps PopulationSync's
+    device-row clone; otherwise every slot's full state (``AgentState``:
+    network shape, learn_step, parameters, Adam moments and step,
+    hyperparameters) is copied from its parent's (local: on device; another
+    rank's: one packed message per (source, destination) pair);
+  * mutations (hpo/shard.py over the global population): RL-hyperparameter
+    and parameter mutations act on the group rows; an architecture or
+    learn_step mutation leaves the view with a pending state;
+  * ``regroup``: groups rebuilt from the slots' states when anything moved.
+"""
+
+from __future__ import annotations
+
+import copy
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..envs import StackedVecEnv
+from ..rng import numpy_shuffle_perms
+from .ppo_pop import PPOPopulation
+from .runner import PopulationRunner
+
+
+@dataclass
+class AgentState:
+    """Everything one agent's learner carries between generations."""
+    spec: object
+    learn_step: int
+    params: torch.Tensor      # [n] f32 (device or host)
+    exp_avg: torch.Tensor     # [n]
+    exp_avg_sq: torch.Tensor  # [n]
+    step: int
+    lr: float
+    batch_size: int
+    update_epochs: int
+    ent_coef: float
+
+    def clone(self) -> "AgentState":
+        return AgentState(copy.deepcopy(self.spec), self.learn_step, self.params.clone(), self.exp_avg.clone(),
+                          self.exp_avg_sq.clone(), self.step, self.lr, self.batch_size, self.update_epochs,
+                          self.ent_coef)
+
+
+def export_state(pop: PPOPopulation, row: int, learn_step: int) -> AgentState:
+    n = pop.spec.n_params
+    return AgentState(copy.deepcopy(pop.spec), int(learn_step), pop.params.data[row, :n].clone(),
+                      pop.opt.exp_avg[row, :n].clone(), pop.opt.exp_avg_sq[row, :n].clone(),
+                      int(pop.opt.steps[row]), float(pop.agent_lr[row]), int(pop.agent_batch[row]),
+                      int(pop.agent_epochs[row]), float(pop.agent_ent[row]))
+
+
+class _Group:
+    def __init__(self, pop: PPOPopulation, runner: PopulationRunner, slots: list[int], learn_step: int):
+        self.pop, self.runner, self.slots, self.learn_step = pop, runner, list(slots), int(learn_step)
+
+
+class PopulationEngine:
+    def __init__(self, population: PPOPopulation, views: list, env, world: int = 1, rank: int = 0):
+        self.views = list(views)
+        self.P, self.N = population.P, population.N
+        self.world, self.rank = world, rank
+        self.device = population.device
+        learn_step = int(views[0].learn_step)
+        # per-slot envs: a StackedVecEnv splits into its agents' envs; one
+        # undivided vector env of P*N envs keeps the population in one group
+        self.slot_envs = list(env.envs) if isinstance(env, StackedVecEnv) and len(env.envs) == self.P else None
+        self._template = population
+        self.groups = [_Group(population, PopulationRunner(population, env), list(range(self.P)), learn_step)]
+        for j, v in enumerate(self.views):
+            v.population, v.row = population, j
+        # every global slot's (S, E, K-defining learn_step): refreshed after mutations
+        self.global_plan = [(population.S, population.update_epochs, learn_step)] * (self.P * world)
+        self._gen_state = None  # numpy state before the generation's shuffles (target_kl re-sync)
+        self.refresh_plan()
+
+    # ------------------------------------------------------------------ #
+    @property
+    def single_group(self) -> bool:
+        return len(self.groups) == 1
+
+    def group_of(self, slot: int) -> tuple[_Group, int]:
+        for g in self.groups:
+            if slot in g.slots:
+                return g, g.slots.index(slot)
+        raise KeyError(slot)
+
+    def iterations(self, evo_steps: int, learn_step: int) -> int:
+        """collect + learn iterations per generation (train_on_policy.py:231)."""
+        return max(1, -(int(evo_steps) // -int(learn_step)))
+
+    # ------------------------------------------------------------------ #
+    def refresh_plan(self) -> None:
+        """Every global slot's (rollout samples S, update epochs, learn_step)
+        — each rank knows its own; one gather when sharded."""
+        local = []
+        for j in range(self.P):
+            g, r = self.group_of(j)
+            local.append((g.pop.S, int(g.pop.agent_epochs[r]), g.learn_step, int(g.pop.agent_batch[r])))
+        if self.world > 1:
+            box: list = [None] * self.world
+            dist.all_gather_object(box, local)
+            plan = [tuple(x) for b in box for x in b]
+        else:
+            plan = local
+        self.global_plan = [x[:3] for x in plan]
+        gmax = max(x[3] for x in plan)
+        for g in self.groups:  # every group splits minibatches like the whole population
+            g.pop.global_batch_max = gmax
+
+    def draw_generation_perms(self, evo_steps: int) -> None:
+        """The generation's minibatch shuffles from numpy's global stream in
+        the reference's order: global agent after global agent, each its K
+        learns of E shuffles of arange(S) (cumulative within a learn), every
+        group taking the rows of its own agents."""
+        pops = [g.pop for g in self.groups]
+        if any(p.perm_source != "numpy" for p in pops):
+            return
+        for p in pops:
+            p.discard_prefetch()
+        self._gen_state = np.random.get_state(legacy=True)
+        blocks = {}
+        for g in self.groups:
+            K = self.iterations(evo_steps, g.learn_step)
+            blocks[id(g)] = np.zeros((K, g.pop.update_epochs, g.pop.P, g.pop.S), dtype=np.int64)
+        where = {self.rank * self.P + j: self.group_of(j) for j in range(self.P)}
+        scratch = {}
+        for gid, (S, E, ls) in enumerate(self.global_plan):
+            K = self.iterations(evo_steps, ls)
+            buf = scratch.get((E, S))
+            if buf is None:
+                buf = scratch[(E, S)] = np.empty((E, 1, S), dtype=np.int64)
+            for k in range(K):
+                numpy_shuffle_perms(1, E, S, out=buf)
+                if gid in where:
+                    g, r = where[gid]
+                    blocks[id(g)][k, :E, r] = buf[:, 0]
+        for g in self.groups:
+            g.pop.set_generation_perms(blocks[id(g)])
+
+    def resync_numpy_after_generation(self, evo_steps: int) -> None:
+        """target_kl: the reference draws one shuffle per epoch an agent
+        actually runs; re-advance the global stream from the generation's
+        start by exactly those (single process; see PPOPopulation)."""
+        pops = [g.pop for g in self.groups]
+        if self._gen_state is None or all(p.target_kl is None for p in pops) or self.world > 1:
+            return
+        ran_of = {}
+        for g in self.groups:
+            rows = [t.cpu().numpy() for t in g.pop._gen_ran]
+            for r, slot in enumerate(g.slots):
+                ran_of[slot] = [int(x[r]) for x in rows]
+        full = all(ran_of[j] == [self.global_plan[j][1]] * len(ran_of[j]) for j in range(self.P))
+        if full:
+            return
+        np.random.set_state(self._gen_state)
+        for j, (S, E, ls) in enumerate(self.global_plan):
+            for ran in ran_of[j]:
+                if ran:
+                    numpy_shuffle_perms(1, ran, S)
+        self._gen_state = None
+
+    # ------------------------------------------------------------------ #
+    def train(self, evo_steps: int, on_iteration=None) -> list:
+        """Every group runs its agents' iterations of the generation; ->
+        per-iteration mean losses (host arrays, slot order where known)."""
+        losses = []
+        for g in self.groups:
+            for _ in range(self.iterations(evo_steps, g.learn_step)):
+                loss = g.runner.iteration()
+                g.pop.check_errors()
+                losses.append(loss.cpu().numpy())
+                if on_iteration is not None:
+                    on_iteration(g)
+        return losses
+
+    def steps_per_generation(self, slot: int, evo_steps: int) -> int:
+        g, _ = self.group_of(slot)
+        return self.iterations(evo_steps, g.learn_step) * g.pop.T * self.N
+
+    def episode_stats(self) -> tuple[np.ndarray, np.ndarray]:
+        r_sum, r_cnt = np.zeros(self.P), np.zeros(self.P)
+        for g in self.groups:
+            s, c = g.runner.episode_return_sum.cpu().numpy(), g.runner.episodes.cpu().numpy()
+            g.runner.reset_episode_stats()
+            for r, slot in enumerate(g.slots):
+                r_sum[slot], r_cnt[slot] = s[r], c[r]
+        return r_sum, r_cnt
+
+    def evaluate(self, loop: int, max_steps) -> list[float]:
+        out = [0.0] * self.P
+        for g in self.groups:
+            f = g.runner.evaluate(loop=loop, max_steps=max_steps)
+            for r, slot in enumerate(g.slots):
+                out[slot] = float(f[r])
+        return out
+
+    # ------------------------------------------------------------------ #
+    def local_states(self) -> list[AgentState]:
+        out = []
+        for j in range(self.P):
+            v = self.views[j]
+            pending = getattr(v, "_pending_state", None)
+            if pending is not None:
+                out.append(pending)
+                continue
+            g, r = self.group_of(j)
+            out.append(export_state(g.pop, r, getattr(v, "_pending_learn_step", None) or g.learn_step))
+        return out
+
+    def clone_states(self, parents: list[int], records: list[dict]) -> list[AgentState]:
+        """New slot j <- the state of global agent parents[rank * P + j];
+        parents on other ranks cross once per (source, destination) pair."""
+        P, me = self.P, self.rank
+        mine = self.local_states()
+        new = [None] * P
+        if self.world > 1:
+            comm = torch.device("cpu") if dist.get_backend() == "gloo" else self.device
+            need = [[sorted({q % P for q in parents[r * P:(r + 1) * P] if q // P == src}) if src != r else []
+                     for src in range(self.world)] for r in range(self.world)]
+            ops, recv, sends = [], {}, []
+            for dst in range(self.world):
+                rows = need[dst][me]
+                if rows:
+                    msg = torch.cat([torch.cat([mine[q].params, mine[q].exp_avg, mine[q].exp_avg_sq]) for q in rows])
+                    sends.append(msg.to(comm))
+                    ops.append(dist.P2POp(dist.isend, sends[-1], dst))
+            for src in range(self.world):
+                rows = need[me][src]
+                if rows:
+                    n = sum(3 * records[src * P + q]["_spec"].n_params for q in rows)
+                    recv[src] = torch.empty(n, dtype=torch.float32, device=comm)
+                    ops.append(dist.P2POp(dist.irecv, recv[src], src))
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+            remote = {}
+            for src, buf in recv.items():
+                off = 0
+                for q in need[me][src]:
+                    rec = records[src * P + q]
+                    n = rec["_spec"].n_params
+                    t = buf[off:off + 3 * n].to(self.device)
+                    hp = rec["_hp"]
+                    remote[src * P + q] = AgentState(copy.deepcopy(rec["_spec"]), int(hp["learn_step"]), t[:n].clone(),
+                                                     t[n:2 * n].clone(), t[2 * n:].clone(), int(rec["_adam_step"]),
+                                                     float(hp["lr"]), int(hp["batch_size"]),
+                                                     int(hp["update_epochs"]), float(hp["ent_coef"]))
+                    off += 3 * n
+        for j in range(P):
+            q = parents[me * P + j]
+            new[j] = mine[q % P].clone() if q // P == me else remote[q].clone()
+        return new
+
+    def regroup(self, states: list[AgentState]) -> None:
+        """Groups rebuilt from every slot's state: slots with equal (network
+        shape, learn_step) share a PPOPopulation, in slot order."""
+        if self.slot_envs is None and len({(s.spec.shape_key(), s.learn_step) for s in states}) > 1:
+            raise NotImplementedError("agents with different networks or learn_step need one env per agent: pass "
+                                      "the reference's num_envs env (cloned per agent) or a StackedVecEnv")
+        order: dict[tuple, list[int]] = {}
+        for j, s in enumerate(states):
+            order.setdefault((s.spec.shape_key(), s.learn_step), []).append(j)
+        t = self._template
+        groups = []
+        for (_, learn_step), slots in order.items():
+            st = [states[j] for j in slots]
+            spec = st[0].spec
+            pop = PPOPopulation(spec, len(slots), self.N, learn_step=learn_step,
+                                batch_size=max(s.batch_size for s in st), lr=[s.lr for s in st], gamma=t.gamma,
+                                gae_lambda=t.gae_lambda, clip_coef=t.clip_coef, ent_coef=st[0].ent_coef,
+                                vf_coef=t.vf_coef, max_grad_norm=t.max_grad_norm,
+                                update_epochs=max(s.update_epochs for s in st), target_kl=t.target_kl,
+                                device=self.device, fused=t.fused, perm_source=t.perm_source,
+                                action_masks=t.use_action_masks, global_pop_size=t.global_P, seed_base=t.seed_base,
+                                agent_ids=[self.rank * self.P + j for j in slots])
+            n = spec.n_params
+            with torch.no_grad():
+                for r, s in enumerate(st):
+                    pop.params.data[r, :n].copy_(s.params)
+                    pop.opt.exp_avg[r, :n].copy_(s.exp_avg)
+                    pop.opt.exp_avg_sq[r, :n].copy_(s.exp_avg_sq)
+                    pop.opt.steps[r] = s.step
+                    pop.opt.lr[r] = s.lr
+                    pop.set_agent_hparam(r, "batch_size", s.batch_size)
+                    pop.set_agent_hparam(r, "update_epochs", s.update_epochs)
+                    pop.set_agent_hparam(r, "ent_coef", s.ent_coef)
+                    pop.set_host_hparams(r, lr=s.lr)
+            env = (StackedVecEnv([self.slot_envs[j] for j in slots]) if self.slot_envs is not None
+                   else self.groups[0].runner.env)
+            groups.append(_Group(pop, PopulationRunner(pop, env), slots, learn_step))
+        self.groups = groups
+        for g in groups:
+            for r, slot in enumerate(g.slots):
+                v = self.views[slot]
+                v.population, v.row = g.pop, r
+                v._pending_state = None
+                v._pending_learn_step = None
+                v._learn_step = g.learn_step
+        self.refresh_plan()
+
+    def pending(self) -> bool:
+        return any(getattr(v, "_pending_state", None) is not None or getattr(v, "_pending_learn_step", None)
+                   for v in self.views)

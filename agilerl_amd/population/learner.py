@@ -157,4 +157,4 @@ def policy_step(pop, desc: AgxPPONet, obs: torch.Tensor, obs_agent_stride: int, 
     _lib.call("agx_ppo_act", ctypes.byref(desc), pop.P, pop.N, pop.params.data.data_ptr(), obs.data_ptr(),
               obs_agent_stride, _lib.ptr(action_mask), mask_agent_stride, 1 if sample else 0, pop.act_seed, counter,
               _lib.ptr(actions), _lib.ptr(log_probs), _lib.ptr(values), _lib.ptr(entropy), out_agent_stride,
-              _lib.ptr(actions_flat), pop.agent_offset * pop.N, _lib.stream())
+              _lib.ptr(actions_flat), pop.env_base_d.data_ptr(), _lib.stream())

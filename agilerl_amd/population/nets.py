@@ -134,16 +134,24 @@ class ActorCriticSpec:
         return W, b, g, be
 
     def _run(self, flat, x, layers):
-        for lay in layers:
-            W, b, g, be = self.views(flat, lay)
-            x = torch.baddbmm(b.unsqueeze(1), x, W.transpose(1, 2))
-            if lay.ln is not None:
-                x = F.layer_norm(x, (lay.fout,), eps=1e-5)
-                if g is not None:
-                    x = x * g.unsqueeze(1) + be.unsqueeze(1)
-            if lay.act:
-                x = torch.relu(x)
-        return x
+        """Agent by agent: 2-D GEMMs whose kernel choice (and so rounding)
+        depends only on the agent's own shapes, never on how many agents the
+        population holds — a population split into groups or sharded over
+        ranks computes exactly what the whole one does."""
+        outs = []
+        for p in range(flat.shape[0]):
+            h = x[p]
+            for lay in layers:
+                W, b, g, be = self.views(flat[p:p + 1], lay)
+                h = torch.addmm(b[0], h, W[0].t())
+                if lay.ln is not None:
+                    h = F.layer_norm(h, (lay.fout,), eps=1e-5)
+                    if g is not None:
+                        h = h * g[0] + be[0]
+                if lay.act:
+                    h = torch.relu(h)
+            outs.append(h)
+        return torch.stack(outs)
 
     def forward(self, flat: torch.Tensor, obs: torch.Tensor):
         """obs [P, B, obs_dim] -> (logits [P, B, A], value [P, B])."""

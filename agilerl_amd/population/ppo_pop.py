@@ -71,7 +71,7 @@ class PPOPopulation:
                  batch_size=128, lr=1e-3, gamma=0.99, gae_lambda=0.95, clip_coef=0.2, ent_coef=0.01,
                  vf_coef=0.5, max_grad_norm=0.5, update_epochs=4, target_kl=None, seeds=None,
                  device="cuda", fused=True, perm_source="numpy", action_masks=False, agent_offset=0,
-                 global_pop_size=None, seed_base=None):
+                 global_pop_size=None, seed_base=None, agent_ids=None):
         self.spec = spec
         self.P, self.N = int(pop_size), int(num_envs)
         # a shard of a population spread over ranks: these P agents are global
@@ -82,6 +82,13 @@ class PPOPopulation:
         self.global_P = self.P if global_pop_size is None else int(global_pop_size)
         if self.agent_offset < 0 or self.agent_offset + self.P > self.global_P:
             raise ValueError("agent_offset / global_pop_size do not contain this shard")
+        # global index of each local agent (a contiguous shard by default; a
+        # group of the population engine holds any subset): keys its env
+        # copies' sampling streams
+        self.agent_ids = (list(range(self.agent_offset, self.agent_offset + self.P)) if agent_ids is None
+                          else [int(i) for i in agent_ids])
+        if len(self.agent_ids) != self.P:
+            raise ValueError("agent_ids must name every agent")
         self.T = -(learn_step // -self.N)  # capacity = ceil(learn_step / num_envs), ppo.py:363
         self.S = self.T * self.N
         self.batch_size = int(batch_size)
@@ -95,6 +102,7 @@ class PPOPopulation:
         self.seeds = seeds
         # population-level streams key off the global population's first seed
         seed_base = int(seeds[0]) if seed_base is None else int(seed_base)
+        self.seed_base = seed_base
         self.params = torch.nn.Parameter(spec.init_params(self.P, seeds, self.device))
         self.params.grad = torch.zeros_like(self.params)
         lr_list = [float(lr)] * self.P if not isinstance(lr, (list, tuple)) else [float(x) for x in lr]
@@ -126,11 +134,12 @@ class PPOPopulation:
         # every global agent's update_epochs (the shuffles each draws; ranks
         # refresh the other shards' entries after a mutation)
         self.global_epochs = [self.update_epochs] * self.global_P
-        self.global_batch = [self.batch_size] * self.global_P
+        self.global_batch_max = None
         self._shard_scratch: dict = {}
         self.act_counter = 0
         self._desc = None
         self._alloc_rollout()
+        self.env_base_d = torch.tensor([i * self.N for i in self.agent_ids], dtype=torch.int64, device=self.device)
         self.learn_steps = 0
         self.rollout_id = 0
         self.prefetch_perms = os.environ.get("AGX_PREFETCH_PERMS", "1") != "0"
@@ -143,6 +152,11 @@ class PPOPopulation:
         # the correction owed to the global stream once its epochs_run is known
         self._perm_drawn_state = None
         self._kl_pending = None
+        # a generation's shuffles drawn ahead by the population engine, agent by
+        # agent (set_generation_perms): [K, E, P, S], learn k reads row k
+        self._gen_block = None
+        self._gen_k = 0
+        self._gen_ran: list[torch.Tensor] = []
 
     # ------------------------------------------------------------------ #
     def _alloc_rollout(self):
@@ -166,11 +180,22 @@ class PPOPopulation:
 
     # ------------------------------------------------------------------ #
     @torch.no_grad()
-    def act(self, obs: torch.Tensor):
-        """obs [P, N, D] (device) -> action, log_prob, entropy, value, each [P, N]."""
+    def act(self, obs: torch.Tensor, counter: int | None = None):
+        """obs [P, N, D] (device) -> action, log_prob, entropy, value, each [P, N].
+        Gumbel-max sampling; with ``counter`` every agent draws from its own
+        generator keyed by (population seed, global agent id, counter), so an
+        agent's draws do not depend on which other agents share its population."""
         logits, value = self.spec.forward(self.params.data, obs)
         logp_all, ent = categorical(logits)
-        u = torch.rand(logits.shape, generator=self.gen, device=self.device).clamp_(min=1e-20)
+        if counter is None:
+            u = torch.rand(logits.shape, generator=self.gen, device=self.device)
+        else:
+            u = torch.empty(logits.shape, device=self.device)
+            g = torch.Generator(device=self.device)
+            for p, aid in enumerate(self.agent_ids):
+                g.manual_seed(((self.seed_base * 1_000_003 + aid) * 2_097_152 + int(counter)) & 0x7FFFFFFFFFFFFFFF)
+                u[p] = torch.rand(logits.shape[1:], generator=g, device=self.device)
+        u.clamp_(min=1e-20)
         action = torch.argmax(logits - torch.log(-torch.log(u)), dim=-1)
         logp = logp_all.gather(-1, action.unsqueeze(-1)).squeeze(-1)
         return action, logp, ent, value
@@ -193,7 +218,8 @@ class PPOPopulation:
         actions for the host env step)."""
         desc = self.fused_descriptor()
         if desc is None:
-            action, logp, _ent, value = self.act(self.obs[:, t])
+            self.act_counter += 1
+            action, logp, _ent, value = self.act(self.obs[:, t], counter=self.act_counter)
             self.actions[:, t].copy_(action)
             self.values[:, t].copy_(value)
             self.log_probs[:, t].copy_(logp)
@@ -276,6 +302,9 @@ class PPOPopulation:
     #     the state the reference would.
     # Without target_kl every agent runs all its epochs and both are exact.
     def _record_kl_pending(self, epochs_run) -> None:
+        if self.target_kl is not None and self._gen_block is not None:
+            self._gen_ran.append(torch.as_tensor(epochs_run).detach().clone())  # the engine re-syncs the stream
+            return
         if self.target_kl is None or self.perm_source != "numpy" or self._perm_drawn_state is None:
             return
         planned = list(self.agent_epochs) if self.heterogeneous else [self.update_epochs] * self.P
@@ -322,8 +351,12 @@ class PPOPopulation:
     @property
     def _hp_dev(self):
         """(batch i32 [P], epochs i32 [P], ent f32 [P]) for the learner, or None
-        while every agent shares the population's values."""
-        return (self.hp_batch_d, self.hp_epochs_d, self.hp_ent_d) if self._hetero else None
+        while every agent shares the population's values (and the partner
+        split is sized by that batch: a group split like a larger global
+        batch passes its agents' own sizes)."""
+        if self._hetero or self.split_batch != self.batch_size:
+            return (self.hp_batch_d, self.hp_epochs_d, self.hp_ent_d)
+        return None
 
     def set_agent_hparam(self, p: int, name: str, value) -> None:
         """Set one agent's RL hyperparameter (the HPO mutation of
@@ -360,11 +393,10 @@ class PPOPopulation:
     @property
     def split_batch(self) -> int:
         """The minibatch size that sizes the fused learner's partner split:
-        the largest of the GLOBAL population (a shard splits like the whole
+        the largest of the GLOBAL population (``global_batch_max``, set by the
+        population engine; a shard or a group splits like the whole
         population, so its agents' sums run in the same order)."""
-        gb = list(self.global_batch)
-        gb[self.agent_offset:self.agent_offset + self.P] = self.agent_batch
-        return min(max(gb), self.S)
+        return min(max(max(self.agent_batch), self.global_batch_max or 0), self.S)
 
     def set_host_hparams(self, p: int, lr=None, batch_size=None, update_epochs=None, ent_coef=None) -> None:
         """Exact host values of agent p's hyperparameters after a clone whose
@@ -428,7 +460,7 @@ class PPOPopulation:
         device draw.  Returns the draw made ahead by prefetch_permutations()
         if there is one (the same draw, in the same order, as drawing here)."""
         if self._perm_next is not None:
-            perms, ev, state = self._perm_next
+            perms, ev, state = self._perm_next[:3]
             self._perm_next = None
             self._perm_drawn_state = state
             main = torch.cuda.current_stream(self.device)
@@ -436,10 +468,8 @@ class PPOPopulation:
             perms.record_stream(main)
             return perms
         if self.perm_source == "numpy":
-            self.sync_numpy_stream()
-            self._perm_drawn_state = np.random.get_state(legacy=True)
             host = self._host_perm_buffer()
-            self._draw_numpy_perms(host.numpy())
+            self._perm_drawn_state = self._fill_numpy_perms(host.numpy())
             perms = host.to(self.device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
@@ -447,6 +477,34 @@ class PPOPopulation:
             return perms
         keys = torch.rand(self.update_epochs, self.P, self.S, generator=self.gen, device=self.device)
         return torch.argsort(keys, dim=-1)
+
+    def set_generation_perms(self, block: np.ndarray | None) -> None:
+        """The population engine's draw of this population's shuffles for a
+        whole generation ([K, E, P, S] int64: learn k of local agent p visits
+        block[k, e, p] in epoch e), drawn agent by agent over the global
+        population as the reference's agents learn one after another
+        (train_on_policy.py:210-248 -> ppo.py:836-842).  None: draw per learn."""
+        self.discard_prefetch()
+        if block is not None:
+            if block.ndim != 4 or block.shape[1:] != (self.update_epochs, self.P, self.S):
+                raise ValueError(f"generation shuffles {block.shape}, expected [K, {self.update_epochs}, {self.P}, "
+                                 f"{self.S}]")
+        self._gen_block, self._gen_k, self._gen_ran = block, 0, []
+
+    def _fill_numpy_perms(self, out: np.ndarray):
+        """The next learn's [E, P, S] numpy-stream permutations into ``out``;
+        -> the global numpy state before the draw (None when they come from
+        the engine's generation block, which owns the stream)."""
+        if self._gen_block is not None:
+            if self._gen_k >= self._gen_block.shape[0]:
+                raise RuntimeError("more learns than the generation's shuffles were drawn for")
+            np.copyto(out, self._gen_block[self._gen_k])
+            self._gen_k += 1
+            return None
+        self.sync_numpy_stream()
+        state = np.random.get_state(legacy=True)
+        self._draw_numpy_perms(out)
+        return state
 
     def _draw_numpy_perms(self, out: np.ndarray) -> None:
         """[E, P, S] from the global numpy stream: this shard's agents' shuffles
@@ -503,16 +561,18 @@ class PPOPopulation:
         so the draws stay in the reference's order."""
         if self._perm_next is not None or self.device.type != "cuda":
             return
-        if self.perm_source == "numpy":
-            self.sync_numpy_stream()  # waits for a target-KL learn's epochs_run (before any rollout launch)
+        if self._gen_block is not None and self._gen_k >= self._gen_block.shape[0]:
+            return  # the generation's learns are all served: the next block is drawn with the next generation
         if self._perm_stream is None:
             self._perm_stream = torch.cuda.Stream(device=self.device)
         side = self._perm_stream
         state = None
+        from_block = False
         if self.perm_source == "numpy":
-            state = np.random.get_state(legacy=True)
+            # waits for a target-KL learn's epochs_run (before any rollout launch)
+            from_block = self._gen_block is not None
             host = self._host_perm_buffer()
-            self._draw_numpy_perms(host.numpy())
+            state = self._fill_numpy_perms(host.numpy())
             with torch.cuda.stream(side):
                 perms = host.to(self.device, non_blocking=True)
                 ev = torch.cuda.Event()
@@ -525,16 +585,20 @@ class PPOPopulation:
                 perms = torch.argsort(keys, dim=-1)
                 ev = torch.cuda.Event()
                 ev.record(side)
-        self._perm_next = (perms, ev, state)
+        self._perm_next = (perms, ev, state, from_block)
 
     def discard_prefetch(self) -> None:
         """Undo a prefetched numpy draw: the global numpy state goes back to
         before it, so the next consumer of the stream draws what it would have
         drawn without the prefetch (the permutations are re-drawn later)."""
+        if self._perm_next is not None and len(self._perm_next) > 3 and self._perm_next[3]:
+            self._perm_next = None  # a generation-block row: served again by the next permutations()
+            self._gen_k -= 1
+            return
         if self._perm_next is None or self._perm_next[2] is None:
             self.sync_numpy_stream()
             return  # nothing drawn ahead from numpy (device draws use the pop's own generator)
-        perms, ev, state = self._perm_next
+        perms, ev, state = self._perm_next[:3]
         self._perm_next = None
         np.random.set_state(state)
 

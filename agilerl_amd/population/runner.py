@@ -64,7 +64,7 @@ class AgxRolloutIO(ctypes.Structure):
         ("slot_agent_stride", ctypes.c_int64), ("actions_flat", ctypes.c_void_p),
         ("scores", ctypes.c_void_p), ("return_sum", ctypes.c_void_p), ("episodes", ctypes.c_void_p),
         ("stage_mask", ctypes.c_void_p), ("mask_slot", ctypes.c_void_p), ("mask_agent_stride", ctypes.c_int64),
-        ("env_base", ctypes.c_int64),
+        ("agent_env_base", ctypes.c_void_p),
     ]
 
 
@@ -219,7 +219,7 @@ class PopulationRunner:
                 io.values = self.last_value.data_ptr()
                 io.slot_agent_stride = N
             io.prev_agent_stride = T * N
-            io.env_base = pop.agent_offset * N  # a sharded population samples the global envs' streams
+            io.agent_env_base = pop.env_base_d.data_ptr()  # each agent samples its global envs' streams
             ios[t] = io
         self._ios = ios
 
@@ -381,6 +381,8 @@ class PopulationRunner:
         obs_h = torch.empty(P * N * D, dtype=pop.obs.dtype, pin_memory=True)
         obs_d = torch.empty(P, N, D, dtype=pop.obs.dtype, device=pop.device)
         out = np.zeros((loop, P))
+        pop.eval_rounds = getattr(pop, "eval_rounds", 0) + 1
+        eval_base = (1 << 41) + (pop.eval_rounds << 24)
         for k in range(loop):
             obs, _ = env.reset()
             scores = np.zeros(P * N)
@@ -393,11 +395,14 @@ class PopulationRunner:
                 if desc is not None:
                     from .learner import policy_step
 
-                    pop.act_counter += 1
-                    policy_step(pop, desc, obs_d, N * D, sample=True, counter=pop.act_counter,
+                    # evaluation draws from its own counter space, one block per
+                    # evaluate() call: the rollout counters of an agent then depend
+                    # only on its own rollouts, never on how long the other agents of
+                    # its group take to finish their evaluation episodes
+                    policy_step(pop, desc, obs_d, N * D, sample=True, counter=eval_base + (k << 20) + step,
                                 out_agent_stride=N, actions_flat=act_d)
                 else:
-                    act_d.copy_(pop.act(obs_d)[0].view(-1))
+                    act_d.copy_(pop.act(obs_d, counter=eval_base + (k << 20) + step)[0].view(-1))
                 act_h.copy_(act_d, non_blocking=True)
                 self.ev.record()
                 self.ev.synchronize()

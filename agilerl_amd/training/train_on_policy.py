@@ -50,7 +50,7 @@ import torch.distributed as dist
 from ..envs import StackedVecEnv
 from ..hpo.population_sync import PopulationSync
 from ..hpo.shard import all_ranks, gather_records, mutate_population
-from ..population.runner import PopulationRunner
+from ..population.engine import PopulationEngine
 
 
 def _population_env(env, P: int, N: int, offset: int = 0):
@@ -93,16 +93,29 @@ def _clone_host_attributes(pop, parents: list[int], elitism: bool, records: list
                                       update_epochs=hp.get("update_epochs"), ent_coef=hp.get("ent_coef"))
 
 
-def _sync_global_epochs(population) -> None:
-    """Every global agent's update_epochs (the shuffles each draws) and batch
-    size (the learner's partner split) after a mutation may have changed
-    another shard's."""
-    if population.global_P == population.P:
-        return
-    box: list = [None] * dist.get_world_size()
-    dist.all_gather_object(box, (list(population.agent_epochs), list(population.agent_batch)))
-    population.global_epochs = [int(e) for b in box for e in b[0]]
-    population.global_batch = [int(x) for b in box for x in b[1]]
+def _all_one_group(engine) -> bool:
+    """Every rank holds one group, and all ranks the same (shape, learn_step):
+    the device-row clone of PopulationSync applies."""
+    mine = (engine.single_group, engine.groups[0].pop.spec.shape_key(), engine.groups[0].learn_step)
+    if engine.world == 1:
+        return mine[0]
+    box: list = [None] * engine.world
+    dist.all_gather_object(box, mine)
+    return all(b[0] for b in box) and len({(b[1], b[2]) for b in box}) == 1
+
+
+def _apply_mutations(engine) -> None:
+    """After mutations: agents whose architecture or learn_step changed move to
+    their group (regroup); every rank learns every global agent's plan."""
+    changed = engine.pending()
+    if engine.world > 1:
+        box: list = [None] * engine.world
+        dist.all_gather_object(box, changed)
+        changed = any(box)
+    if changed:
+        engine.regroup(engine.local_states())
+    else:
+        engine.refresh_plan()
 
 
 def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None, swap_channels: bool = False,
@@ -117,39 +130,40 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
     population = pop[0].population
     if any(a.population is not population for a in pop):
         raise ValueError("all agents must come from one agilerl_amd.utils.create_population call")
-    P, N, T = population.P, population.N, population.T
+    P, N = population.P, population.N
     world, rank = (dist.get_world_size(), dist.get_rank()) if dist.is_initialized() else (1, 0)
     if population.global_P not in (P, P * world) or population.agent_offset not in (0, rank * P):
         raise ValueError("the population's shard does not match this process group")
     env = _population_env(env, P, N, population.agent_offset)
-    runner = PopulationRunner(population, env)
+    # agents grouped by (network shape, learn_step): one group until a mutation splits them
+    engine = PopulationEngine(population, pop, env, world, rank)
     sync = None
     if tournament is not None and mutation is not None:  # the reference selects only with both (:440)
-        sync = PopulationSync(population, runner, world, rank, seed=None, tournament_size=tournament.tournament_size,
-                              elitism=tournament.elitism, eval_loop=tournament.eval_loop)
+        sync = PopulationSync(population, engine.groups[0].runner, world, rank, seed=None,
+                              tournament_size=tournament.tournament_size, elitism=tournament.elitism,
+                              eval_loop=tournament.eval_loop)
     save_path = (checkpoint_path.split(".pt")[0] if checkpoint_path is not None
                  else f"{env_name}-EvoHPO-{algo}-{datetime.now().strftime('%m%d%Y%H%M%S')}")
     checkpoint_count = 0
     if mutation is not None:  # pre-training mutation (:200-201)
         pop = mutate_population(mutation, pop, pre_training_mut=True)
-        _sync_global_epochs(population)
-    iters_per_gen = max(1, -(-evo_steps // (T * N)))
+        _apply_mutations(engine)
     pop_fitnesses: list[list[float]] = []
     t0 = time.time()
-    while min(agent.steps[-1] for agent in pop) < max_steps:
-        losses = []
-        for _ in range(iters_per_gen):
-            losses.append(runner.iteration().cpu().numpy())
-            population.check_errors()
-            for agent in pop:
-                agent.steps[-1] += T * N
+    # np.less([...], max_steps).all() (:204): every agent of every rank still below max_steps
+    while all_ranks(all(agent.steps[-1] < max_steps for agent in pop)):
+        # the generation's minibatch shuffles, agent after agent as the reference's
+        # agents learn (train_on_policy.py:210-248 -> ppo.py:836-842)
+        engine.draw_generation_perms(evo_steps)
+        losses = engine.train(evo_steps)
+        for j, agent in enumerate(pop):
+            agent.steps[-1] += engine.steps_per_generation(j, evo_steps)
+        engine.resync_numpy_after_generation(evo_steps)
         # training-episode scores (on_policy.py:147-172 -> agent.scores) ...
-        r_sum = runner.episode_return_sum.cpu().numpy()
-        r_cnt = runner.episodes.cpu().numpy()
-        runner.reset_episode_stats()
+        r_sum, r_cnt = engine.episode_stats()
         # ... then the population's fitness: agent.test for every agent
         # (train_on_policy.py:363-373), batched on device over the env slices
-        fitness = [float(f) for f in runner.evaluate(loop=eval_loop, max_steps=eval_steps)]
+        fitness = engine.evaluate(eval_loop, eval_steps)
         for i, agent in enumerate(pop):
             if r_cnt[i] > 0:
                 agent.scores.append(float(r_sum[i] / r_cnt[i]))
@@ -167,7 +181,13 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
         if sync is not None:  # tournament_selection_and_mutation (utils.py:1137-1225)
             records = gather_records(pop)  # every global agent's host attributes, before the clone
             sync.fitness_override = np.asarray(fitness)  # reduced on the host already: hand it over
-            parents = sync.generation()
+            if _all_one_group(engine):
+                # one network shape and rollout length everywhere: parent rows move in HBM
+                sync.pop, sync.runner = engine.groups[0].pop, engine.groups[0].runner
+                parents = sync.generation()
+            else:
+                parents = sync.select()
+                engine.regroup(engine.clone_states(parents, records))
             _clone_host_attributes(pop, parents, tournament.elitism, records, rank)
             if save_elite and tournament.elitism and rank == 0:
                 # the reference saves ``elite``, the unmutated clone of the best agent
@@ -175,11 +195,11 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
                 elite_save_path = elite_path.split(".pt")[0] if elite_path is not None else f"{env_name}-elite_{algo}"
                 pop[0].save_checkpoint(f"{elite_save_path}.pt")
             pop = mutate_population(mutation, pop)
-            _sync_global_epochs(population)
+            _apply_mutations(engine)
         if verbose:
             fps = sum(a.steps[-1] for a in pop) / max(time.time() - t0, 1e-9)
             print(f"--- {env_name} {algo}: steps {[a.steps[-1] for a in pop]}, fitness "
-                  f"{[round(f, 2) for f in fitness]}, mean loss {np.mean(losses):.4f}, "
+                  f"{[round(f, 2) for f in fitness]}, mean loss {np.mean([np.mean(x) for x in losses]):.4f}, "
                   f"mutations {[a.mut for a in pop]}, {fps:.0f} env-steps/s")
         if checkpoint is not None and pop[0].steps[-1] // checkpoint > checkpoint_count:
             for j, agent in enumerate(pop):  # save_population_checkpoint (utils.py:1126-1135)
@@ -188,4 +208,3 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
                                       else f"{save_path}_{i}_{agent.steps[-1]}.pt")
             checkpoint_count += 1
     return pop, pop_fitnesses
-

@@ -178,16 +178,17 @@ int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *args, void *
  * action_mask: NULL, or legal-action flags of agent p, env n at
  * action_mask + p*mask_agent_stride + n*n_actions (u8, 1 = legal): illegal
  * logits become -1e8 first (ppo.py:529-565, distributions.py:16-28).
- * env_base: global index of (agent 0, env 0) — the Philox stream of env n
- * of agent p is that of global env env_base + p*N + n, so a population
- * sharded over ranks (rank r holding agents r*P..) samples exactly what the
- * unsharded population samples (0 for an unsharded population). */
+ * agent_env_base: NULL, or [P] int64 device array — the global index of
+ * agent p's env 0: the Philox stream of its env n is that of global env
+ * agent_env_base[p] + n (NULL: p*N + n).  A population sharded over ranks,
+ * or split into groups of agents with equal networks, samples exactly what
+ * the whole population samples in one launch. */
 int agx_ppo_act(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
                 const float *obs, int64_t obs_agent_stride, const uint8_t *action_mask,
                 int64_t mask_agent_stride, int sample, uint64_t seed,
                 uint64_t counter, int64_t *actions, float *log_probs, float *values,
                 float *entropy, int64_t out_agent_stride, int64_t *actions_flat,
-                int64_t env_base, void *stream);
+                const int64_t *agent_env_base, void *stream);
 /* One vector step of rollout collection for all P agents x N envs
  * (rollouts/on_policy.py:23-203 loop body + RolloutBuffer.add,
  * rollout_buffer.py:235-411), fused into ONE launch:
@@ -228,8 +229,9 @@ typedef struct agx_rollout_io {
     const uint8_t *stage_mask;
     uint8_t *mask_slot;
     int64_t mask_agent_stride;
-    /* global index of (agent 0, env 0) for the Philox stream (agx_ppo_act) */
-    int64_t env_base;
+    /* [P] global index of each agent's env 0 for the Philox stream, or NULL
+     * (agx_ppo_act's agent_env_base) */
+    const int64_t *agent_env_base;
 } agx_rollout_io;
 int agx_ppo_rollout_step(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
                          const agx_rollout_io *io, int act, int sample, uint64_t seed,

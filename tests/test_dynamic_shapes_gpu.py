@@ -1,0 +1,183 @@
+"""a20: architecture and learn_step mutations in the population engine.
+
+* train_on_policy with ppo.yaml's MUTATION_PARAMS unchanged (NO_MUT 0.4,
+  ARCH_MUT 0.2, NEW_LAYER 0.2, PARAMS_MUT 0.2, ACT_MUT 0.2, RL_HP_MUT 0.2,
+  MUT_SD 0.1, RAND_SEED 42; lr / batch_size / learn_step ranges of
+  MUTATION_PARAMS) and its NET_CONFIG, on LunarLander-shaped synthetic envs:
+  agents end up with different networks and rollout lengths, each group
+  trains, nothing is lost between groups;
+* the grouped learner (the autograd path with the HIP loss and clip + Adam
+  kernels, the path of a mutated shape the fused kernel is not instantiated
+  for) on a MUTATED shape, one update from a continued Adam state, against
+  the PyTorch restatement of ppo.py:814-921 (oracle/ppo_learn.py): every
+  entry within 1e-5 x (|ref| + rms(ref)) (moments 1e-4) except at most
+  0.01 %;
+* a mutated agent keeps its preserved weights in HBM: the rows the engine
+  regroups equal population/arch.py's result.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _ppo_yaml_population(P=4, N=16):
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.registry import HyperparameterConfig, RLParameter
+    from agilerl_amd.utils import create_population
+
+    env = SyntheticVecEnv(N, seed=3, p_done=1 / 40)
+    INIT_HP = {"BATCH_SIZE": 128, "LR": 0.001, "LEARN_STEP": 256, "GAMMA": 0.99, "GAE_LAMBDA": 0.95,
+               "CLIP_COEF": 0.2, "ENT_COEF": 0.01, "VF_COEF": 0.5, "MAX_GRAD_NORM": 0.5, "TARGET_KL": None,
+               "UPDATE_EPOCHS": 4}
+    NET_CONFIG = {"latent_dim": 64,
+                  "encoder_config": {"hidden_size": [64], "activation": "ReLU", "min_mlp_nodes": 64,
+                                     "max_mlp_nodes": 500, "layer_norm": True},
+                  "head_config": {"hidden_size": [64], "activation": "ReLU", "min_hidden_layers": 1,
+                                  "max_hidden_layers": 3, "min_mlp_nodes": 64, "max_mlp_nodes": 500,
+                                  "output_vanish": True, "layer_norm": True}}
+    hp = HyperparameterConfig(lr=RLParameter(min=0.0001, max=0.01),
+                              batch_size=RLParameter(min=8, max=1024, dtype=int),
+                              learn_step=RLParameter(min=256, max=8192, dtype=int))
+    pop = create_population("PPO", NET_CONFIG, INIT_HP, env.single_observation_space, env.single_action_space,
+                            hp_config=hp, population_size=P, num_envs=N)
+    return env, pop, INIT_HP
+
+
+def test_ppo_yaml_mutation_params_train_on_policy():
+    import warnings
+
+    from agilerl_amd.hpo.mutation import Mutations
+    from agilerl_amd.hpo.tournament import TournamentSelection
+    from agilerl_amd.population import arch
+    from agilerl_amd.training import train_on_policy
+
+    np.random.seed(0)
+    torch.manual_seed(0)
+    env, pop, INIT_HP = _ppo_yaml_population()
+    mut = Mutations(no_mutation=0.4, architecture=0.2, new_layer_prob=0.2, parameters=0.2, activation=0.2,
+                    rl_hp=0.2, mutation_sd=0.1, rand_seed=42)
+    tour = TournamentSelection(2, True, 4, 1)
+    seen: set[str] = set()
+    shapes: set[tuple] = set()
+    steps: set[int] = set()
+    orig = mut.mutation
+
+    def record(population, pre_training_mut=False):
+        out = orig(population, pre_training_mut=pre_training_mut)
+        seen.update(a.mut for a in out)
+        shapes.update(a.spec.shape_key() for a in out)
+        steps.update(int(a.learn_step) for a in out)
+        return out
+
+    mut.mutation = record
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        pop, fits = train_on_policy(env, "LunarLanderSynthetic", "PPO", pop, INIT_HP=INIT_HP, max_steps=6 * 1024,
+                                    evo_steps=1024, eval_steps=30, tournament=tour, mutation=mut, verbose=False)
+    assert any(m in arch.METHODS or m.split(".")[-1] in ("add_node", "remove_node") for m in seen), seen
+    assert "learn_step" in seen or len(steps) > 1, seen
+    assert len(shapes) > 1, "architecture mutations should change some agent's networks"
+    assert all(len(f) == 4 and np.all(np.isfinite(f)) for f in fits)
+    for a in pop:
+        assert torch.isfinite(a.population.params.data[a.row]).all()
+        assert a.population.spec.shape_key() == a.spec.shape_key()
+        assert a.population.T == -(a.learn_step // -16)
+        obs = np.random.standard_normal((5, 8)).astype(np.float32)
+        act, _, _, v = a.get_action(obs)
+        assert act.shape == (5,) and np.all(np.isfinite(v))
+
+
+def test_regroup_keeps_the_mutated_weights():
+    """An architecture mutation's result (population/arch.py) lands in HBM
+    unchanged when the engine regroups the agent."""
+    from agilerl_amd.population import arch
+    from agilerl_amd.population.engine import PopulationEngine
+
+    np.random.seed(1)
+    torch.manual_seed(1)
+    env, pop, _ = _ppo_yaml_population(P=3)
+    from agilerl_amd.envs import StackedVecEnv
+
+    engine = PopulationEngine(pop[0].population, pop, StackedVecEnv.from_shared(env, 3))
+    rng = np.random.default_rng(7)
+    want = {}
+    for j in (0, 2):
+        a = pop[j]
+        for _ in range(10):  # until the shape changes
+            a.architecture_mutation(0.5, rng)
+            if a.spec.shape_key() != pop[1].spec.shape_key():
+                break
+        want[j] = (a.spec.shape_key(), a._pending_state.params.cpu().clone())
+    engine.regroup(engine.local_states())
+    assert len(engine.groups) >= 2
+    for j, (key, params) in want.items():
+        a = pop[j]
+        assert a.spec.shape_key() == key and a._pending_state is None
+        assert torch.equal(a.population.params.data[a.row].cpu(), params)
+        assert int(a.population.opt.steps[a.row]) == 0 and float(a.population.opt.exp_avg[a.row].abs().max()) == 0
+    assert arch.METHODS  # module imported
+
+
+def test_grouped_learner_single_update_on_mutated_shape():
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+    from oracle.ppo_learn import ActorCritic, reference_learn
+
+    # a shape three mutations away from ppo.yaml's: encoder node, latent node, head layer
+    spec = ActorCriticSpec(obs_dim=8, n_actions=4, encoder_hidden=[80], latent_dim=72, actor_hidden=[64, 64],
+                           critic_hidden=[64, 64], encoder_name="encoder")
+    P, N, T, lr = 2, 16, 8, 1e-3
+    S = T * N
+    pop = PPOPopulation(spec, P, N, learn_step=S, batch_size=S, update_epochs=1, lr=lr, seeds=[4, 5], device=DEV)
+    assert pop.fused_descriptor() is None  # the grouped autograd learner runs this shape
+    g = torch.Generator(device=DEV).manual_seed(3)
+    pop.obs.copy_(torch.randn(pop.obs.shape, device=DEV, generator=g))
+    pop.actions.copy_(torch.randint(0, 4, pop.actions.shape, device=DEV, generator=g))
+    pop.log_probs.copy_(-torch.rand(pop.log_probs.shape, device=DEV, generator=g) * 2 - 0.2)
+    pop.values.copy_(torch.randn(pop.values.shape, device=DEV, generator=g))
+    pop.advantages.copy_(torch.randn(pop.advantages.shape, device=DEV, generator=g))
+    pop.returns.copy_(torch.randn(pop.returns.shape, device=DEV, generator=g))
+    a = pop.advantages.view(P, -1).double()
+    pop.adv_stats[:, 0], pop.adv_stats[:, 1] = a.mean(1), a.std(1)
+    n = spec.n_params
+    pop.opt.exp_avg.copy_(torch.randn(P, n, device=DEV, generator=g) * 1e-3)
+    pop.opt.exp_avg_sq.copy_(torch.rand(P, n, device=DEV, generator=g) * 1e-5 + 1e-7)
+    pop.opt.steps.fill_(7)
+    init, m0, v0 = (x.clone() for x in (pop.params.data, pop.opt.exp_avg, pop.opt.exp_avg_sq))
+    raw_adv = pop.advantages.clone()
+    perms = torch.arange(S, device=DEV).repeat(1, P, 1).contiguous()
+    pop._learn_torch(perms)
+    torch.cuda.synchronize()
+    keys = spec.state_dict_keys()
+
+    def close(name, got, want, rtol):
+        got, want = got.double().numpy().ravel(), want.double().numpy().ravel()
+        bad = np.abs(got - want) > rtol * (np.abs(want) + np.sqrt(np.mean(want * want)))
+        assert bad.mean() <= 1e-4, (name, int(bad.sum()), want.size)
+
+    for p in range(P):
+        net = ActorCritic(8, 4, [80], 72, [64, 64], [64, 64])
+        sd = {k: init[p, o:o + int(np.prod(sh))].view(sh).cpu() for k, (o, sh) in keys.items()
+              if not k.startswith("critic.encoder.")}
+        net.load_reference(sd)
+        adam = {k: (m0[p, o:o + int(np.prod(sh))].view(sh).cpu().numpy(),
+                    v0[p, o:o + int(np.prod(sh))].view(sh).cpu().numpy())
+                for k, (o, sh) in keys.items() if not k.startswith("critic.encoder.")}
+        adam["step"] = 7
+        out = reference_learn(net, adam, pop.obs[p].reshape(S, -1).cpu().numpy(),
+                              pop.actions[p].reshape(-1).cpu().numpy(), pop.log_probs[p].reshape(-1).cpu().numpy(),
+                              raw_adv[p].reshape(-1).cpu().numpy(), pop.returns[p].reshape(-1).cpu().numpy(),
+                              pop.values[p].reshape(-1).cpu().numpy(), perms[:, p].cpu().numpy(), batch_size=S,
+                              epochs=1, lr=lr)
+        assert out["step"] == 8 and int(pop.opt.steps[p]) == 8
+        for name, ref in out["state"].items():
+            off, sh = keys[name]
+            k = ref.numel()
+            close(f"{p} {name}", pop.params.data[p, off:off + k].cpu(), ref.reshape(-1), 1e-5)
+            close(f"{p} {name} m", pop.opt.exp_avg[p, off:off + k].cpu(), out["exp_avg"][name].reshape(-1), 1e-4)
+            close(f"{p} {name} v", pop.opt.exp_avg_sq[p, off:off + k].cpu(), out["exp_avg_sq"][name].reshape(-1),
+                  1e-4)

@@ -223,7 +223,7 @@ def test_policy_step_rejects_unsupported_shape():
     d.obs_dim, d.n_actions, d.n_enc = 7, 3, 2
     lib = _lib.load()
     rc = lib.agx_ppo_act(ctypes_byref(d), 1, 1, None, None, 0, None, 0, 0, 0, 0, None, None, None, None, 0, None,
-                         0, None)
+                         None, None)
     assert rc != 0
 
 

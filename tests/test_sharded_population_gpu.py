@@ -62,7 +62,7 @@ class ActionRewardVecEnv:
         return self._obs[self._k].copy(), rew, np.zeros(self.num_envs, bool), trunc, {}
 
 
-def _run(world, rank, out_dir, port):
+def _run(world, rank, out_dir, port, arch=0.0):
     sys.path.insert(0, ROOT)
     os.environ["AGX_PERSISTENT_ROLLOUT"] = "0"  # two processes share the card: per-step launches
     torch.cuda.set_device(0)
@@ -86,50 +86,59 @@ def _run(world, rank, out_dir, port):
     env = ActionRewardVecEnv()
     hp = HyperparameterConfig(lr=RLParameter(min=1e-5, max=1e-2), batch_size=RLParameter(min=8, max=64, dtype=int),
                               update_epochs=RLParameter(min=1, max=4, dtype=int),
-                              ent_coef=RLParameter(min=1e-4, max=0.1))
-    net = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}, "latent_dim": 64}
+                              ent_coef=RLParameter(min=1e-4, max=0.1),
+                              **({"learn_step": RLParameter(min=32, max=256, dtype=int)} if arch else {}))
+    net = {"encoder_config": {"hidden_size": [64], "min_mlp_nodes": 32, "max_mlp_nodes": 128},
+           "head_config": {"hidden_size": [64], "min_mlp_nodes": 32, "max_mlp_nodes": 128}, "latent_dim": 64}
     init = {"BATCH_SIZE": 16, "LR": 1e-3, "LEARN_STEP": 64, "UPDATE_EPOCHS": 2}
     pop = create_population("PPO", net, init, env.observation_space, env.action_space, hp_config=hp,
                             population_size=G_TOTAL, num_envs=env.num_envs, device="cuda")
-    mutation = Mutations(no_mutation=0.2, architecture=0.0, new_layer_prob=0.2, parameters=0.4, activation=0.0,
+    mutation = Mutations(no_mutation=0.2, architecture=arch, new_layer_prob=0.2, parameters=0.4, activation=0.0,
                          rl_hp=0.4, mutation_sd=0.1, rand_seed=5)
     tournament = TournamentSelection(2, True, G_TOTAL, 1)
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
-        pop, fits = train_on_policy(env, "ActionReward", "PPO", pop, max_steps=3 * 128, evo_steps=128,
+        pop, fits = train_on_policy(env, "ActionReward", "PPO", pop, max_steps=(4 if arch else 3) * 128, evo_steps=128,
                                     tournament=tournament, mutation=mutation, verbose=False)
     torch.cuda.synchronize()
     population = pop[0].population
     out = [dict(index=a.index, mut=a.mut, lr=float(a.lr), batch_size=int(a.batch_size),
-                update_epochs=int(a.update_epochs), ent_coef=float(a.ent_coef),
-                fitness=[float(f) for f in a.fitness], steps=list(a.steps),
-                params=population.params.data[a.row].cpu().clone(),
-                exp_avg=population.opt.exp_avg[a.row].cpu().clone(),
-                exp_avg_sq=population.opt.exp_avg_sq[a.row].cpu().clone()) for a in pop]
+                update_epochs=int(a.update_epochs), ent_coef=float(a.ent_coef), learn_step=int(a.learn_step),
+                shape=repr(a.spec.shape_key()), fitness=[float(f) for f in a.fitness], steps=list(a.steps),
+                params=a.population.params.data[a.row].cpu().clone(),
+                exp_avg=a.population.opt.exp_avg[a.row].cpu().clone(),
+                exp_avg_sq=a.population.opt.exp_avg_sq[a.row].cpu().clone()) for a in pop]
     torch.save({"agents": out, "fits": fits}, os.path.join(out_dir, f"w{world}_r{rank}.pt"))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def _worker(rank, world, out_dir, port):
-    _run(world, rank, out_dir, port)
+def _worker(rank, world, out_dir, port, arch):
+    _run(world, rank, out_dir, port, arch)
 
 
-def _launch(world, out_dir):
-    mp.start_processes(_worker, args=(world, out_dir, _free_port()), nprocs=world, join=True, start_method="spawn")
+def _launch(world, out_dir, arch=0.0):
+    mp.start_processes(_worker, args=(world, out_dir, _free_port(), arch), nprocs=world, join=True,
+                       start_method="spawn")
     got = [torch.load(os.path.join(out_dir, f"w{world}_r{r}.pt"), weights_only=True) for r in range(world)]
     return [a for g in got for a in g["agents"]], got[0]["fits"]
 
 
-def test_sharded_train_on_policy_equals_single_process(tmp_path):
-    ref, ref_fits = _launch(1, str(tmp_path))
-    got, fits = _launch(2, str(tmp_path))
+@pytest.mark.parametrize("arch", [0.0, 0.4])
+def test_sharded_train_on_policy_equals_single_process(tmp_path, arch):
+    """arch > 0: architecture and learn_step mutations too — agents with
+    different networks and rollout lengths, in groups on each rank."""
+    ref, ref_fits = _launch(1, str(tmp_path), arch)
+    got, fits = _launch(2, str(tmp_path), arch)
     assert len(ref) == len(got) == G_TOTAL
     assert len({a["mut"] for a in ref}) > 1, [a["mut"] for a in ref]
+    if arch:
+        assert len({a["shape"] for a in ref}) > 1 or len({a["learn_step"] for a in ref}) > 1
     assert fits == ref_fits
     for g, (a, b) in enumerate(zip(got, ref)):
-        for key in ("index", "mut", "lr", "batch_size", "update_epochs", "ent_coef", "fitness", "steps"):
+        for key in ("index", "mut", "lr", "batch_size", "update_epochs", "ent_coef", "learn_step", "shape", "fitness",
+                    "steps"):
             assert a[key] == b[key], (g, key, a[key], b[key])
         for key in ("params", "exp_avg", "exp_avg_sq"):
             assert torch.equal(a[key], b[key]), (g, key, float((a[key] - b[key]).abs().max()))
