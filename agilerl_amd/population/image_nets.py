@@ -107,6 +107,12 @@ class ImageActorCriticSpec:
         self._chunks = chunks
         self._index = {c[0]: i for i, c in enumerate(chunks)}
 
+    def shape_key(self) -> tuple:
+        """Agents with equal keys share a network layout (population groups)."""
+        return (self.obs_shape, self.n_actions, tuple(self.channel_size), tuple(self.kernel_size),
+                tuple(self.stride_size), self.latent_dim, tuple(self.actor_hidden), tuple(self.critic_hidden),
+                self.head_layer_norm, self.encoder_name, self.obs_dtype, self.image_norm)
+
     # ------------------------------------------------------------------ #
     def init_params(self, P: int, seeds: list[int] | None = None, device="cpu") -> torch.Tensor:
         """Per agent, in module order: conv layers orthogonal (gain sqrt 2),

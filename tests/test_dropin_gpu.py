@@ -48,7 +48,7 @@ def test_create_population_train_on_policy():
 
     obs_space, act_space = _spaces()
     INIT_HP = {"BATCH_SIZE": 64, "LR": 1e-3, "LEARN_STEP": 128, "UPDATE_EPOCHS": 2}
-    net_config = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}}
+    net_config = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}, "latent_dim": 64}
     pop = create_population("PPO", net_config, INIT_HP, obs_space, act_space, population_size=4, num_envs=16)
     assert len(pop) == 4 and all(a.population is pop[0].population for a in pop)
     assert pop[0].population.fused_descriptor() is not None
@@ -78,7 +78,7 @@ def test_train_on_policy_reference_call_site(tmp_path):
 
     obs_space, act_space = _spaces()
     INIT_HP = {"BATCH_SIZE": 64, "LR": 1e-3, "LEARN_STEP": 128, "UPDATE_EPOCHS": 2}
-    net_config = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}}
+    net_config = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}, "latent_dim": 64}
     hp = HyperparameterConfig(lr=RLParameter(min=1e-4, max=1e-2), batch_size=RLParameter(min=32, max=256, dtype=int),
                               ent_coef=RLParameter(min=0.001, max=0.1),
                               update_epochs=RLParameter(min=1, max=4, dtype=int))

@@ -253,6 +253,7 @@ def test_fused_learner_partner_split_consistent(split, monkeypatch):
     if sb:
         monkeypatch.setenv("AGX_LEARN_SB", sb)  # 16-row sub-batches, several per partner
     for learn_step, epochs in ((128, 1), (512, 2)):
+        np.random.seed(learn_step)  # the minibatch shuffles: fixed, whatever ran before
         pop = _pop(P=4, N=16, learn_step=learn_step, batch=128, epochs=epochs, seed=11)
         st = _clone_state(pop)
         perms = pop.permutations()
