@@ -63,6 +63,7 @@ SIGNATURES = {
     "agx_td_target": (_INT, [_P] * 6 + [_I, _I, _D, _INT, _P, _P, _P, _P, _P]),
     "agx_maddpg_critic_target": (_INT, [_P] * 4 + [_I, _D, _P, _P, _P, _P, _P]),
     "agx_c51_project_loss": (_INT, [_P] * 7 + [_I, _I, _I, _D, _D, _D, _P, _P, _P]),
+    "agx_c51_project_loss_rows": (_INT, [_P] * 5 + [_I, _I, _D, _D, _D, _P, _P, _P]),
     "agx_adam_workspace_bytes": (_SZ, [_I, _I]),
     "agx_clip_adam": (_INT, [_P, _P, _P, _P, _I, _I, _P, _INT, _F, _P, _F, _F, _F, _P, _P, _P, _P]),
     "agx_polyak": (_INT, [_P, _P, _I, _F, _P]),
@@ -73,6 +74,8 @@ SIGNATURES = {
     "agx_rows_gather": (_INT, [_P, _P, _INT, _I, _P, _P, _P]),
     "agx_dueling_head_forward": (_INT, [_P, _P, _P, _I, _I, _I, _INT, _P, _P]),
     "agx_dueling_head_backward": (_INT, [_P, _P, _P, _P, _I, _I, _I, _INT, _P, _P, _P]),
+    "agx_dueling_head_forward_rows": (_INT, [_P, _P, _P, _I, _I, _I, _INT, _P, _P]),
+    "agx_dueling_head_backward_rows": (_INT, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "agx_conv2d_forward_grouped": (_INT, [_P, _I, _P, _I, _INT, _F, _F, _P, _I, _P, _I, _INT, _P, _I, _P]),
     "agx_conv2d_wgrad_workspace_bytes_grouped": (_SZ, [_P, _I]),
     "agx_conv2d_backward_grouped": (_INT, [_P, _I, _P, _I, _INT, _F, _F, _P, _I, _P, _P, _I, _P, _P, _P,

@@ -230,6 +230,24 @@ class _C51Loss(torch.autograd.Function):
         return (grad,) + (None,) * 9
 
 
+class _C51RowsLoss(torch.autograd.Function):
+    """The same loss on the selected rows (agx_c51_project_loss_rows): log p
+    of the taken action [B, Z] and the target distribution of a* [B, Z], as
+    the dueling head emits them; d loss / d logp_rows = -proj."""
+
+    @staticmethod
+    def forward(ctx, logp_rows, target_rows, rewards, dones, support, v_min, v_max, gamma):
+        loss, proj = K.c51_project_loss_rows(target_rows.contiguous(), logp_rows.contiguous(), rewards, dones, support,
+                                             v_min, v_max, gamma, with_proj=True)
+        ctx.save_for_backward(proj)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (proj,) = ctx.saved_tensors
+        return (-proj * g.unsqueeze(1),) + (None,) * 7
+
+
 class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
     """Drop-in RainbowDQN (agilerl/algorithms/dqn_rainbow.py:77-501) with the
     C51 projection + loss in agx_c51_project_loss and Polyak in agx_polyak."""
@@ -304,13 +322,24 @@ class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
         return np.argmax(np.ma.array(q, mask=1 - np.asarray(action_mask)), axis=-1)
 
     def _dqn_loss(self, obs, actions, rewards, next_obs, dones, gamma) -> torch.Tensor:
+        acts = actions.reshape(-1).long().contiguous()
+        rew = rewards.reshape(-1).float().contiguous()
+        done = dones.reshape(-1).float().contiguous()
+        if self.num_atoms == 51 and self.device.type == "cuda":
+            # the heads emit only the selected rows (target_dist[range(B), a*],
+            # log_p[range(B), action]); the C51 step streams them contiguously
+            with torch.no_grad():
+                a_star = self.actor(next_obs).argmax(1)     # first maximum, as the reference's argmax
+                target_rows = self.actor_target(next_obs, q=False, rows=a_star)
+            logp_rows = self.actor(obs, q=False, log=True, rows=acts)
+            return _C51RowsLoss.apply(logp_rows, target_rows, rew, done, self.support, float(self.v_min),
+                                      float(self.v_max), float(gamma))
         with torch.no_grad():
             q_next = self.actor(next_obs)                   # a* = argmax online Q(s')
             target_dist = self.actor_target(next_obs, q=False)
         logp = self.actor(obs, q=False, log=True)
-        return _C51Loss.apply(logp, q_next, target_dist, actions.reshape(-1).long().contiguous(),
-                              rewards.reshape(-1).float().contiguous(), dones.reshape(-1).float().contiguous(),
-                              self.support, float(self.v_min), float(self.v_max), float(gamma))
+        return _C51Loss.apply(logp, q_next, target_dist, acts, rew, done, self.support, float(self.v_min),
+                              float(self.v_max), float(gamma))
 
     @torch.no_grad()
     def test(self, env, swap_channels: bool = False, max_steps: int | None = None, loop: int = 3) -> float:

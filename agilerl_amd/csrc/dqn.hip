@@ -430,11 +430,16 @@ __global__ __launch_bounds__(kC51RowWaves * 64) void c51_rows_kernel(
 // atoms keep the scheduler from hoisting all Z address computations.
 constexpr int kC51LaneRows = 64;
 
+// ROWS: the caller hands over the two selected rows per batch element already
+// gathered ([B][Z] target distribution of a*, [B][Z] log p of the taken
+// action — agx_dueling_head_forward_rows emits exactly these), so both LDS-DMA
+// gathers read one contiguous Z x 64-float span per wave: no 128-B line is
+// fetched for a neighbouring action's atoms, and no Q row / action is read.
 // Z atoms at compile time (the gather's (row, atom) split is a multiply-shift,
 // the atom loops unroll into independent chains).  POW2: Δz is a power of two
 // (±200 or ±100 over 51 atoms: 8 or 4), so (tz − v_min)/Δz is the exact
 // product with 1/Δz and the f32 division sequence is skipped.
-template <int Z, bool POW2>
+template <int Z, bool POW2, bool ROWS = false>
 __global__ __launch_bounds__(64) void c51_dma_kernel(
     const float *__restrict__ qno, const float *__restrict__ tdist, const float *__restrict__ logp,
     const int64_t *__restrict__ act, const float *__restrict__ rew, const float *__restrict__ dn,
@@ -447,25 +452,27 @@ __global__ __launch_bounds__(64) void c51_dma_kernel(
     const int nrows = (int)(B - row0 < kC51LaneRows ? B - row0 : kC51LaneRows);
     const bool live = lane < nrows;
     const int64_t i = row0 + (live ? lane : nrows - 1);  // dead lanes shadow the last row
-    const int a_cur = (int)act[i];
+    const int a_cur = ROWS ? 0 : (int)act[i];
     const float r = rew[i];
     const float kk = (1.0f - dn[i]) * g;
-    const float *qr = qno + i * A;
-    float bv = qr[0];
     int astar = 0;
-    for (int a = 1; a < A; ++a) {  // first maximum
-        const float q = qr[a];
-        if (q > bv) {
-            bv = q;
-            astar = a;
+    if constexpr (!ROWS) {
+        const float *qr = qno + i * A;
+        float bv = qr[0];
+        for (int a = 1; a < A; ++a) {  // first maximum
+            const float q = qr[a];
+            if (q > bv) {
+                bv = q;
+                astar = a;
+            }
         }
     }
     const float supv = lane < Z ? support[lane] : 0.f;
-    const uint32_t blk = (uint32_t)(A * Z * 4);
+    const uint32_t blk = (uint32_t)((ROWS ? 1 : A) * Z * 4);
     // rows (row0 + rk, sel of lane rk) of a [B][A][Z] array -> sA[rk * Z + z];
     // rows past B read as 0 (buffer range = this wave's nrows rows)
     auto dma_rows = [&](const float *__restrict__ src, int sel) {
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(src) + row0 * A * Z, 0,
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(src) + row0 * (ROWS ? 1 : A) * Z, 0,
                                                           (int)(blk * (uint32_t)nrows), 0x00020000);
         // opaque lane id: keeps the Z offset computations here instead of
         // hoisted (and held in registers) across the passes
@@ -474,7 +481,7 @@ __global__ __launch_bounds__(64) void c51_dma_kernel(
 #pragma unroll
         for (int j = 0; j < Z; ++j) {
             const int e = ln + 64 * j, rk = e / Z, z = e - rk * Z;
-            const int srow = __shfl(sel, rk & 63, 64);
+            const int srow = ROWS ? 0 : __shfl(sel, rk & 63, 64);
             const uint32_t off = (uint32_t)rk * blk + (uint32_t)((srow * Z + z) * 4);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 rs, (__attribute__((address_space(3))) void *)(sA + 64 * j), 4, off, 0, 0, 0);
@@ -559,7 +566,7 @@ __global__ __launch_bounds__(64) void c51_dma_kernel(
         }
     }
     if (!mono) {  // never for a sorted support and gamma >= 0: ordered read-modify-writes, p re-read
-        const float *trow = tdist + ((size_t)i * A + astar) * Z;
+        const float *trow = tdist + ((size_t)i * (ROWS ? 1 : A) + astar) * Z;
         for (int bin = 0; bin < Z; ++bin) sA[bin * 64 + lane] = 0.f;
         for (int z = 0; z < Z; ++z) {
             int L, U;
@@ -636,6 +643,26 @@ extern "C" int agx_maddpg_critic_target(const float *q, const float *q_next, con
     if (rc) return rc;
     td_loss_finalize<<<1, 1024, 0, s>>>(part, nblk, B, loss);
     return check_launch("agx_maddpg_critic_target loss");
+}
+
+extern "C" int agx_c51_project_loss_rows(const float *target_rows, const float *logp_rows, const float *rewards,
+                                         const float *dones, const float *support, int64_t B, int64_t Z,
+                                         double v_min, double v_max, double gamma, float *loss, float *proj,
+                                         void *stream) {
+    AGX_REQUIRE(target_rows && logp_rows && rewards && dones && support && loss,
+                "agx_c51_project_loss_rows: null pointer");
+    AGX_REQUIRE(B >= 0 && Z == 51, "agx_c51_project_loss_rows: Z must be 51 (Rainbow's atoms)");
+    if (B == 0) return AGX_OK;
+    const float dz = (float)((v_max - v_min) / (double)(Z - 1));
+    int e2 = 0;
+    const double m = std::frexp((v_max - v_min) / (double)(Z - 1), &e2);
+    const bool pow2 = m == 0.5 && (double)dz == std::ldexp(1.0, e2 - 1) && e2 > -60 && e2 < 60;
+    const float inv = pow2 ? (float)std::ldexp(1.0, 1 - e2) : 0.f;
+    auto kern = pow2 ? c51_dma_kernel<51, true, true> : c51_dma_kernel<51, false, true>;
+    kern<<<(unsigned)ceil_div(B, kC51LaneRows), 64, 0, as_stream(stream)>>>(
+        nullptr, target_rows, logp_rows, nullptr, rewards, dones, support, B, 1, (float)v_min, (float)v_max, dz, inv,
+        (float)gamma, loss, proj);
+    return check_launch("agx_c51_project_loss_rows");
 }
 
 extern "C" int agx_c51_project_loss(const float *q_next_online, const float *target_dist,

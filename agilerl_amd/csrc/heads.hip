@@ -97,6 +97,63 @@ __global__ __launch_bounds__(64) void dueling_bwd_kernel(const float *__restrict
         if (live) db[a * Z + z] -= corr;
 }
 
+// Selected rows: only action sel[b] of each batch row is emitted ([B][Z]), the
+// value the full form writes at out[b][sel[b]] bit for bit (same mean, same
+// per-row softmax).  This is the reference's target_dist[range(B), a*] and
+// log_p[range(B), a] (dqn_rainbow.py:313-367) fused into the producer, so the
+// C51 step reads two contiguous [B][Z] arrays.
+__global__ __launch_bounds__(64) void dueling_fwd_rows_kernel(const float *__restrict__ v,
+                                                              const float *__restrict__ adv,
+                                                              const int64_t *__restrict__ sel, int A, int Z, int mode,
+                                                              float *__restrict__ out) {
+    const int64_t b = blockIdx.x;
+    const int z = threadIdx.x;
+    const bool live = z < Z;
+    const float *ab = adv + b * (int64_t)A * Z;
+    float s = 0.f;
+    for (int a = 0; a < A; ++a) s += live ? ab[a * Z + z] : 0.f;
+    const float mean = s / (float)A;
+    const float vz = live ? v[b * Z + z] : 0.f;
+    const int a = (int)sel[b];
+    const float x = live ? (vz + ab[a * Z + z]) - mean : -__builtin_inff();
+    const float mx = wave_max(x);
+    const float e = live ? expf(x - mx) : 0.f;
+    const float sum = wave_sum(e);
+    if (live) out[b * Z + z] = mode == 2 ? (x - mx) - logf(sum) : fmaxf(e / sum, kClampMin);
+}
+
+// log mode: g [B][Z] = dL/d(out[b][sel[b]]) (zero for every other action) ->
+// dv [B][Z], dadv [B][A][Z]; the full form's arithmetic with those zeros
+__global__ __launch_bounds__(64) void dueling_bwd_rows_kernel(const float *__restrict__ v,
+                                                              const float *__restrict__ adv,
+                                                              const int64_t *__restrict__ sel,
+                                                              const float *__restrict__ g, int A, int Z,
+                                                              float *__restrict__ dv, float *__restrict__ dadv) {
+    const int64_t b = blockIdx.x;
+    const int z = threadIdx.x;
+    const bool live = z < Z;
+    const float *ab = adv + b * (int64_t)A * Z;
+    float *db = dadv + b * (int64_t)A * Z;
+    float s = 0.f;
+    for (int a = 0; a < A; ++a) s += live ? ab[a * Z + z] : 0.f;
+    const float mean = s / (float)A;
+    const float vz = live ? v[b * Z + z] : 0.f;
+    const int a = (int)sel[b];
+    const float x = live ? (vz + ab[a * Z + z]) - mean : -__builtin_inff();
+    const float mx = wave_max(x);
+    const float e = live ? expf(x - mx) : 0.f;
+    const float sum = wave_sum(e);
+    const float p = e / sum;
+    const float gz = live ? g[b * Z + z] : 0.f;
+    float dx = gz - p * wave_sum(gz);
+    dx = live ? dx : 0.f;
+    const float dsum = dx;
+    if (live) dv[b * Z + z] = dsum;
+    const float corr = dsum / (float)A;
+    for (int k = 0; k < A; ++k)
+        if (live) db[k * Z + z] = (k == a ? dx : 0.f) - corr;
+}
+
 }  // namespace heads
 
 }  // namespace agx
@@ -127,4 +184,29 @@ extern "C" int agx_dueling_head_backward(const float *value, const float *advant
     heads::dueling_bwd_kernel<<<(unsigned)B, 64, 0, as_stream(stream)>>>(value, advantage, support, grad_out, (int)A,
                                                                         (int)Z, mode, grad_value, grad_advantage);
     return check_launch("agx_dueling_head_backward");
+}
+
+extern "C" int agx_dueling_head_forward_rows(const float *value, const float *advantage, const int64_t *sel, int64_t B,
+                                             int64_t A, int64_t Z, int mode, float *out, void *stream) {
+    AGX_REQUIRE(value && advantage && sel && out && B >= 0 && A > 0 && Z >= 1 && Z <= 64 && (mode == 1 || mode == 2),
+                "agx_dueling_head_forward_rows: bad arguments (need 1 <= Z <= 64, mode 1 or 2)");
+    if (B == 0) return AGX_OK;
+    AGX_REQUIRE(B < (1ll << 31), "agx_dueling_head_forward_rows: batch too large");
+    heads::dueling_fwd_rows_kernel<<<(unsigned)B, 64, 0, as_stream(stream)>>>(value, advantage, sel, (int)A, (int)Z,
+                                                                             mode, out);
+    return check_launch("agx_dueling_head_forward_rows");
+}
+
+extern "C" int agx_dueling_head_backward_rows(const float *value, const float *advantage, const int64_t *sel,
+                                              const float *grad_rows, int64_t B, int64_t A, int64_t Z,
+                                              float *grad_value, float *grad_advantage, void *stream) {
+    AGX_REQUIRE(value && advantage && sel && grad_rows && grad_value && grad_advantage && B >= 0 && A > 0 && Z >= 1 &&
+                    Z <= 64,
+                "agx_dueling_head_backward_rows: bad arguments (need 1 <= Z <= 64)");
+    if (B == 0) return AGX_OK;
+    AGX_REQUIRE(B < (1ll << 31), "agx_dueling_head_backward_rows: batch too large");
+    heads::dueling_bwd_rows_kernel<<<(unsigned)B, 64, 0, as_stream(stream)>>>(value, advantage, sel, grad_rows,
+                                                                             (int)A, (int)Z, grad_value,
+                                                                             grad_advantage);
+    return check_launch("agx_dueling_head_backward_rows");
 }

@@ -522,10 +522,15 @@ struct Fwd {
         if constexpr (L + 1 < pl.ne) enc_layer<L + 1>();
     }
 
-    __device__ __forceinline__ void run() {
+    // encoder + the merged head GEMM (Z_h in S2)
+    __device__ __forceinline__ void trunk() {
         enc_layer<0>();
         gemm_fwd<pl.l_s1, pl.ld_s, pl.lat, pl.l_hw, pl.l_hld, pl.l_hb, pl.H>();
         __syncthreads();
+    }
+
+    __device__ __forceinline__ void run() {
+        trunk();
         ln_rows<pl.H, pl.ha, pl.l_xh, pl.ld_xh, pl.l_rh, pl.l_hg, pl.l_hbe, true>();  // + output layers
         __syncthreads();
     }
@@ -588,7 +593,7 @@ constexpr unsigned kSpinMax = 1u << 23;  // ~ seconds of s_sleep polling: a miss
 
 #define AGX_STAMP(slot)                                                          \
     do {                                                                         \
-        if (g.stamps && b == 0 && e == 0 && mb == 0 && tid == 0 && (slot) < 80) \
+        if (g.stamps && b == 0 && e == (Ep > 1) && mb == (nmb > 1) && tid == 0 && (slot) < 80) \
             g.stamps[(slot)] = (long long)__builtin_readcyclecounter(); \
     } while (0)
 
@@ -893,33 +898,83 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 __syncthreads();
                 AGX_STAMP(stb + 1);
 
-                // ---- P1-P3: forward ------------------------------------------
-                fw.run();
+                // ---- P1-P3: forward trunk (encoder + merged head GEMM) ------------
+                fw.trunk();
                 AGX_STAMP(stb + 2);
 
-                // ---- P4: loss + d(logits), d(value); 16 lanes per row ------------
+                // ---- P4: ONE row pass over the head (16 lanes per row, nothing leaves
+                // the row's registers): LayerNorm(+affine)+ReLU forward, the output
+                // layers (logits, value), the loss and d(logits) / d(value), and the
+                // LayerNorm backward to dZ_h (S2) with the bias / LN-affine column sums.
+                // y_h goes to S1 and d(logits) / d(value) to LDS for the output-layer dW.
                 {
                     AGX_IDS;
+                    constexpr int F = pl.H, split = pl.ha, NC = F / 16, NA = pl.A;
+                    constexpr int F0 = split, F1 = F - split;
                     const int r = rrow, a = sub;
-                    const bool live = r < nrow;
-                    // illegal actions: logits -> -1e8 (apply_action_mask_discrete, distributions.py:16-28)
+                    // rows beyond the sub-batch (SB = 16: lanes 32-63) compute on zeros
+                    // and contribute exact zeros to the column reductions
+                    const bool rl = SB == kSB || r < SB;
+                    const bool live = rl && r < nrow;
+                    float z[NC], xh[NC];
+                    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) {
+                        z[i] = rl ? sm[pl.l_s2 + r * pl.ld_s + sub + 16 * i] : 0.f;
+                        if (16 * i < split) s0 += z[i];
+                        else s1 += z[i];
+                    }
+                    const float m0 = row_sum(s0) * (1.f / (float)F0);
+                    const float m1 = row_sum(s1) * (1.f / (float)F1);
+                    float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) {
+                        if (16 * i < split) v0 += (z[i] - m0) * (z[i] - m0);
+                        else v1 += (z[i] - m1) * (z[i] - m1);
+                    }
+                    const float r0 = 1.f / sqrtf(row_sum(v0) / (float)F0 + 1e-5f);
+                    const float r1 = 1.f / sqrtf(row_sum(v1) / (float)F1 + 1e-5f);
+                    float pa[NA], pv = 0.f;
+#pragma unroll
+                    for (int k = 0; k < NA; ++k) pa[k] = 0.f;
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) {
+                        const int j = sub + 16 * i;
+                        xh[i] = 16 * i < split ? (z[i] - m0) * r0 : (z[i] - m1) * r1;
+                        const float y = relu(xh[i] * sm[pl.l_hg + j] + sm[pl.l_hbe + j]);
+                        if (rl) sm[pl.l_s1 + r * pl.ld_s + j] = y;
+                        if (16 * i < split) {
+#pragma unroll
+                            for (int k = 0; k < NA; ++k) pa[k] += y * sm[pl.l_aow + k * pl.l_aold + j];
+                        } else {
+                            pv += y * sm[pl.l_cow + j - split];
+                        }
+                    }
+                    float mine = 0.f;
+#pragma unroll
+                    for (int k = 0; k < NA; ++k) {
+                        const float t = row_sum(pa[k]);
+                        mine = sub == k ? t : mine;
+                    }
+                    const float v = row_sum(pv) + sm[pl.l_cob];
+                    // loss + d(logits), d(value) (ppo.py:876-908); illegal actions:
+                    // logits -> -1e8 (apply_action_mask_discrete, distributions.py:16-28)
                     const bool ok_a = (legal[r] >> a) & 1u;
-                    const float lg = a < pl.A ? (ok_a ? sm[pl.l_lg + r * kMaxA + a] : -1.0e8f) : -3.0e38f;
+                    const float lg = a < NA ? (ok_a ? mine + sm[pl.l_aob + sub] : -1.0e8f) : -3.0e38f;
                     const float mx = row_max(lg);
-                    const float ex = a < pl.A ? expf(lg - mx) : 0.f;
+                    const float ex = a < NA ? expf(lg - mx) : 0.f;
                     const float lse = mx + logf(row_sum(ex));
-                    const float pa = a < pl.A ? expf(lg - lse) : 0.f;
-                    const float lpe = logf(pa + 1e-8f);
-                    const float Hs = -row_sum(a < pl.A ? pa * lpe : 0.f);  // H = -sum p log(p+1e-8)
-                    const float gh = -(lpe + pa / (pa + 1e-8f));            // dH/dp_a
-                    const float pg_dot = row_sum(a < pl.A ? pa * gh : 0.f);
+                    const float pa_ = a < NA ? expf(lg - lse) : 0.f;
+                    const float lpe = logf(pa_ + 1e-8f);
+                    const float Hs = -row_sum(a < NA ? pa_ * lpe : 0.f);  // H = -sum p log(p+1e-8)
+                    const float gh = -(lpe + pa_ / (pa_ + 1e-8f));          // dH/dp_a
+                    const float pg_dot = row_sum(a < NA ? pa_ * gh : 0.f);
                     const int a_t = acts[r];
                     const float logp = __builtin_bit_cast(
                                            float, __builtin_amdgcn_ds_bpermute((lane - sub + a_t) * 4,
                                                                                __builtin_bit_cast(int, lg))) -
                                        lse;
                     const float olp = rowf[r], A = rowf[kSB + r], R = rowf[2 * kSB + r], ov = rowf[3 * kSB + r];
-                    const float v = sm[pl.l_val + r];
                     const float lo = 1.f - g.clip, hi = 1.f + g.clip;
                     const float lrt = logp - olp;
                     const float ratio = expf(lrt);
@@ -937,68 +992,40 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     const float gc = lc > lu ? 1.f : (lu == lc ? 0.5f : 0.f);
                     const float inv = (dv >= -g.clip && dv <= g.clip) ? 1.f : 0.f;
                     const float g_H = -entp * inv_b;
-                    const float dl = g_logp * ((a == a_t ? 1.f : 0.f) - pa) + g_H * pa * (gh - pg_dot);
-                    if (a < pl.A) sm[pl.l_dlg + r * kMaxA + a] = (live && ok_a) ? dl : 0.f;
-                    if (a == 0) {
-                        sm[pl.l_dvb + r * kMaxA] =
-                            live ? g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv) : 0.f;
-                        if (live) {
-                            lsum += (fmaxf(p1, p2) + g.vf * 0.5f * fmaxf(lu, lc) - entp * Hs) * inv_b;
-                            klsum += ((ratio - 1.f) - lrt) * inv_b;  // approx_kl (ppo.py:899-902)
-                        }
+                    const float dl = g_logp * ((a == a_t ? 1.f : 0.f) - pa_) + g_H * pa_ * (gh - pg_dot);
+                    const float dlm = (a < NA && live && ok_a) ? dl : 0.f;
+                    const float dvr = live ? g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv) : 0.f;
+                    if (rl) {
+                        if (a < NA) sm[pl.l_dlg + r * kMaxA + a] = dlm;
+                        if (a == 0) sm[pl.l_dvb + r * kMaxA] = dvr;
                     }
-                }
-                __syncthreads();
-                AGX_STAMP(stb + 3);
-
-                AGX_STAMP(stb + 4);  // (output-layer backward: folded into P6)
-
-                // backward row pass through LN(+affine)+ReLU: S2 (dY) -> S2 (dZ)
-                // HO (the merged head layer): dY comes straight from the output
-                // layers' d(logits) / d(value) rows, dY[j] = sum_a dlg[a] W_out[a][j]
-                // (actor columns) or dv w_v[j] (critic columns), instead of S2
-                auto ln_bwd = [&](auto Fc, auto splitc, auto xbc, auto ldxc, auto rbc, auto gbc, auto bbc, auto redc,
-                                  auto affc, auto hoc) {
-                    constexpr int F = decltype(Fc)::value, split = decltype(splitc)::value;
-                    constexpr int xb = decltype(xbc)::value, ldx = decltype(ldxc)::value;
-                    constexpr int rb = decltype(rbc)::value, gb = decltype(gbc)::value, bb = decltype(bbc)::value;
-                    constexpr int red = decltype(redc)::value;
-                    constexpr bool aff = decltype(affc)::value, HO = decltype(hoc)::value;
-                    constexpr int NC = F / 16;
-                    constexpr int F0 = split < F ? split : F, F1 = F - F0;
-                    AGX_IDS;
-                    const int r = rrow;
-                    // rows beyond the sub-batch (SB = 16: lanes 32-63) hold stale LDS
-                    // data: they contribute exact zeros to the column reductions
-                    const bool rl = SB == kSB || r < SB;
-                    float xh[NC], dxh[NC], dyp[NC];
-                    float a1 = 0.f, a2 = 0.f, c1 = 0.f, c2 = 0.f;
-                    const float rs0 = rl ? sm[rb + 2 * r] : 0.f, rs1 = rl ? sm[rb + 2 * r + 1] : 0.f;
-                    constexpr int NA = HO ? pl.A : 1;
-                    float dl[NA], dvr = 0.f;
-                    if constexpr (HO) {
+                    if (a == 0 && live) {
+                        lsum += (fmaxf(p1, p2) + g.vf * 0.5f * fmaxf(lu, lc) - entp * Hs) * inv_b;
+                        klsum += ((ratio - 1.f) - lrt) * inv_b;  // approx_kl (ppo.py:899-902)
+                    }
+                    // LayerNorm backward: dY[j] = sum_a dlg[a] W_out[a][j] (actor columns)
+                    // or dv w_v[j] (critic columns)
+                    float dla[NA];
 #pragma unroll
-                        for (int a = 0; a < NA; ++a) dl[a] = rl ? sm[pl.l_dlg + r * kMaxA + a] : 0.f;
-                        dvr = rl ? sm[pl.l_dvb + r * kMaxA] : 0.f;
-                    }
+                    for (int k = 0; k < NA; ++k)
+                        dla[k] = __builtin_bit_cast(
+                            float, __builtin_amdgcn_ds_bpermute((lane - sub + k) * 4, __builtin_bit_cast(int, dlm)));
+                    float dxh[NC], dyp[NC];
+                    float a1 = 0.f, a2 = 0.f, c1 = 0.f, c2 = 0.f;
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
                         const int j = sub + 16 * i;
                         float dy;
-                        if constexpr (HO) {
-                            if (16 * i < split) {
-                                dy = 0.f;
+                        if (16 * i < split) {
+                            dy = 0.f;
 #pragma unroll
-                                for (int a = 0; a < NA; ++a) dy += dl[a] * sm[pl.l_aow + a * pl.l_aold + j];
-                            } else {
-                                dy = dvr * sm[pl.l_cow + j - split];
-                            }
+                            for (int k = 0; k < NA; ++k) dy += dla[k] * sm[pl.l_aow + k * pl.l_aold + j];
                         } else {
-                            dy = rl ? sm[pl.l_s2 + r * pl.ld_s + j] : 0.f;
+                            dy = dvr * sm[pl.l_cow + j - split];
                         }
-                        xh[i] = rl ? sm[xb + r * ldx + j] : 0.f;
-                        const float gam = aff ? sm[gb + j] : 1.f;
-                        const float y = aff ? xh[i] * gam + sm[bb + j] : xh[i];
+                        xh[i] = rl ? xh[i] : 0.f;
+                        const float gam = sm[pl.l_hg + j];
+                        const float y = xh[i] * gam + sm[pl.l_hbe + j];
                         dyp[i] = y > 0.f ? dy : 0.f;
                         dxh[i] = dyp[i] * gam;
                         if (16 * i < split) {
@@ -1009,9 +1036,83 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                             c2 += dxh[i] * xh[i];
                         }
                     }
+                    const float rs0 = rl ? r0 : 0.f, rs1 = rl ? r1 : 0.f;
                     const float ma1 = row_sum(a1) * (1.f / (float)F0), ma2 = row_sum(a2) * (1.f / (float)F0);
-                    const float mc1 = F1 > 0 ? row_sum(c1) * (1.f / (float)(F1 > 0 ? F1 : 1)) : 0.f;
-                    const float mc2 = F1 > 0 ? row_sum(c2) * (1.f / (float)(F1 > 0 ? F1 : 1)) : 0.f;
+                    const float mc1 = row_sum(c1) * (1.f / (float)F1), mc2 = row_sum(c2) * (1.f / (float)F1);
+                    float *rd = sm + pl.l_red + pl.red_h;
+                    float cs[3][NC];
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) {
+                        const int j = sub + 16 * i;
+                        const bool g0 = 16 * i < split;
+                        const float dz = (g0 ? rs0 : rs1) * (dxh[i] - (g0 ? ma1 : mc1) - xh[i] * (g0 ? ma2 : mc2));
+                        if (rl) sm[pl.l_s2 + r * pl.ld_s + j] = dz;
+                        cs[0][i] = rl ? dz : 0.f;
+                        cs[1][i] = dyp[i] * xh[i];
+                        cs[2][i] = dyp[i];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 3; ++k)
+#pragma unroll
+                        for (int i = 0; i < NC; ++i)
+                            cs[k][i] += __builtin_bit_cast(
+                                float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, cs[k][i]), 0x401f));  // lane ^ 16
+                    if constexpr (SB > 16) {
+#pragma unroll
+                        for (int k = 0; k < 3; ++k)
+#pragma unroll
+                            for (int i = 0; i < NC; ++i)
+                                cs[k][i] += __builtin_bit_cast(
+                                    float, __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, __builtin_bit_cast(int, cs[k][i])));
+                    }
+                    if (lane < 16) {
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            float o[NC];
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) o[i] = rd[(k * kNW + wave) * F + sub + 16 * i];
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) rd[(k * kNW + wave) * F + sub + 16 * i] = o[i] + cs[k][i];
+                        }
+                    }
+                }
+                __syncthreads();
+                AGX_STAMP(stb + 3);
+                AGX_STAMP(stb + 4);
+                AGX_STAMP(stb + 5);
+
+                // backward row pass through LN(+affine)+ReLU of an encoder layer:
+                // dY (dyb, stride ldy) -> dZ (S2)
+                auto ln_bwd = [&](auto Fc, auto dybc, auto ldyc, auto xbc, auto ldxc, auto rbc, auto gbc, auto bbc,
+                                  auto redc, auto affc) {
+                    constexpr int F = decltype(Fc)::value;
+                    constexpr int dyb = decltype(dybc)::value, ldy = decltype(ldyc)::value;
+                    constexpr int xb = decltype(xbc)::value, ldx = decltype(ldxc)::value;
+                    constexpr int rb = decltype(rbc)::value, gb = decltype(gbc)::value, bb = decltype(bbc)::value;
+                    constexpr int red = decltype(redc)::value;
+                    constexpr bool aff = decltype(affc)::value;
+                    constexpr int NC = F / 16;
+                    AGX_IDS;
+                    const int r = rrow;
+                    // rows beyond the sub-batch (SB = 16: lanes 32-63) hold stale LDS
+                    // data: they contribute exact zeros to the column reductions
+                    const bool rl = SB == kSB || r < SB;
+                    float xh[NC], dxh[NC], dyp[NC];
+                    float a1 = 0.f, a2 = 0.f;
+                    const float rs0 = rl ? sm[rb + 2 * r] : 0.f;
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) {
+                        const int j = sub + 16 * i;
+                        const float dy = rl ? sm[dyb + r * ldy + j] : 0.f;
+                        xh[i] = rl ? sm[xb + r * ldx + j] : 0.f;
+                        const float gam = aff ? sm[gb + j] : 1.f;
+                        const float y = aff ? xh[i] * gam + sm[bb + j] : xh[i];
+                        dyp[i] = y > 0.f ? dy : 0.f;
+                        dxh[i] = dyp[i] * gam;
+                        a1 += dxh[i];
+                        a2 += dxh[i] * xh[i];
+                    }
+                    const float ma1 = row_sum(a1) * (1.f / (float)F), ma2 = row_sum(a2) * (1.f / (float)F);
                     float *rd = sm + pl.l_red + red;
                     // dZ row pass; the column sums (bias, gamma, beta gradients) of the
                     // wave's rows are batched: all cross-row reductions, then all LDS
@@ -1022,8 +1123,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
                         const int j = sub + 16 * i;
-                        const bool g0 = 16 * i < split;
-                        const float dz = (g0 ? rs0 : rs1) * (dxh[i] - (g0 ? ma1 : mc1) - xh[i] * (g0 ? ma2 : mc2));
+                        const float dz = rs0 * (dxh[i] - ma1 - xh[i] * ma2);
                         if (rl) sm[pl.l_s2 + r * pl.ld_s + j] = dz;
                         cs[0][i] = rl ? dz : 0.f;
                         if constexpr (aff) {
@@ -1056,11 +1156,9 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         }
                     }
                 };
-                // ---- P6: head LN backward (dY_h in S2 -> dZ_h in S2) ----------
-                // (+ the output layers' dW tiles, bias = ones column: they read
-                // d(logits) / d(value) and y_h, nothing this row pass writes)
-                ln_bwd(IC(pl.H), IC(pl.ha), IC(pl.l_xh), IC(pl.ld_xh), IC(pl.l_rh), IC(pl.l_hg), IC(pl.l_hbe),
-                       IC(pl.red_h), BC(true), BC(true));
+                // ---- P6/P7: output-layer dW (bias = ones column; reads d(logits) /
+                // d(value) and y_h), head dW += dZ^T latent, d(latent) = dZ . W_h ->
+                // the dead head-xhat region (nothing in this phase reads it)
                 {
                     AGX_IDS;
                     constexpr int ga = pl.ne + 1, gc = pl.ne + 2;
@@ -1094,13 +1192,6 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         emit_tiles(IC(pl.ne + 1), slab_put);
                         emit_tiles(IC(pl.ne + 2), slab_put);
                     }
-                }
-                __syncthreads();
-                AGX_STAMP(stb + 5);
-
-                // ---- P7: head dW += dZ^T latent; d(latent) = dZ . W_h -> S1 --------
-                {
-                    AGX_IDS;
                     constexpr int gh = pl.ne, Le = pl.ne - 1;
 #pragma unroll
                     for (int j = 0; j < pl.nslot[gh]; ++j) {
@@ -1120,7 +1211,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         c = mfma_tile<pl.H>(c, [&](int m, int k) { return sm[pl.l_s2 + (m0 + m) * pl.ld_s + k]; },
                                             [&](int k, int n) { return sm[pl.l_hw + k * pl.l_hld + n0 + n]; });
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) sm[pl.l_s1 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i];
+                        for (int i = 0; i < 4; ++i) sm[pl.l_xh + (m0 + lq * 4 + i) * pl.ld_xh + n0 + lr16] = c[i];
                     }
                 }
                 __syncthreads();
@@ -1131,18 +1222,10 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     constexpr int L = decltype(Lc)::value;
                     constexpr int fin = pl.ein[L], fout = pl.eout[L];
                     AGX_IDS;
-                    {  // dY (S1) -> S2: the row pass works in place on S2
-                        const int r = rrow;
-                        if (SB == kSB || r < SB) {
-#pragma unroll
-                            for (int i = 0; i < fout / 16; ++i) {
-                                const int j = sub + 16 * i;
-                                sm[pl.l_s2 + r * pl.ld_s + j] = sm[pl.l_s1 + r * pl.ld_s + j];
-                            }
-                        }
-                    }
-                    ln_bwd(IC(fout), IC(fout), IC(pl.l_xe[L]), IC(pl.ld_xe[L]), IC(pl.l_re[L]), IC(pl.l_eg[L]),
-                           IC(pl.l_ebe[L]), IC(pl.red_e[L]), BC(pl.eaff[L] != 0), BC(false));
+                    constexpr int dyb = L == pl.ne - 1 ? pl.l_xh : pl.l_s1;
+                    constexpr int ldy = L == pl.ne - 1 ? pl.ld_xh : pl.ld_s;
+                    ln_bwd(IC(fout), IC(dyb), IC(ldy), IC(pl.l_xe[L]), IC(pl.ld_xe[L]), IC(pl.l_re[L]), IC(pl.l_eg[L]),
+                           IC(pl.l_ebe[L]), IC(pl.red_e[L]), BC(pl.eaff[L] != 0));
                     __syncthreads();
                     constexpr bool in_aff = L > 0 && pl.eaff[L > 0 ? L - 1 : 0];
                     constexpr int xb = L == 0 ? pl.l_x0 : pl.l_xe[L > 0 ? L - 1 : 0];

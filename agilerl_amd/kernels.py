@@ -274,6 +274,25 @@ def c51_project_loss(q_next_online, target_dist, logp_cur, actions, rewards, don
     return (loss, proj) if with_proj else loss
 
 
+def c51_project_loss_rows(target_rows, logp_rows, rewards, dones, support, v_min, v_max, gamma, with_proj=False):
+    """agx_c51_project_loss_rows: the projection + loss on the selected rows
+    ([B][Z] target distribution of a*, [B][Z] log p of the taken action)."""
+    B, Z = target_rows.shape
+    _need(target_rows, "target_rows", _f32, (B, Z))
+    _need(logp_rows, "logp_rows", _f32, (B, Z))
+    r = rewards.reshape(-1)
+    d = dones.reshape(-1)
+    _need(r, "rewards", _f32, (B,))
+    _need(d, "dones", _f32, (B,))
+    _need(support, "support", _f32, (Z,))
+    loss = torch.empty(B, dtype=_f32, device=r.device)
+    proj = torch.empty(B, Z, dtype=_f32, device=r.device) if with_proj else None
+    _lib.call("agx_c51_project_loss_rows", target_rows.data_ptr(), logp_rows.data_ptr(), r.data_ptr(), d.data_ptr(),
+              support.data_ptr(), B, Z, float(v_min), float(v_max), float(gamma), loss.data_ptr(), _lib.ptr(proj),
+              _lib.stream())
+    return (loss, proj) if with_proj else loss
+
+
 # --------------------------------------------------------------------------- #
 # optimiser                                                                   #
 # --------------------------------------------------------------------------- #

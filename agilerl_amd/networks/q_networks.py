@@ -72,6 +72,43 @@ class DuelingHeadFn(torch.autograd.Function):
         return dv, da, None, None, None, None
 
 
+class DuelingRowsFn(torch.autograd.Function):
+    """(value [B, Z], advantage [B, A*Z], rows [B]) -> the clamped
+    probabilities (mode 1) or log-probabilities (mode 2) of action rows[b]
+    only, [B, Z] (agx_dueling_head_forward_rows / _backward_rows): the
+    reference's ``out[range(B), rows]`` gather fused into the head."""
+
+    @staticmethod
+    def forward(ctx, value, adv, rows, A: int, Z: int, mode: int):
+        from .. import _lib
+
+        value, adv = value.contiguous(), adv.contiguous()
+        rows = rows.reshape(-1).to(torch.int64).contiguous()
+        B = value.shape[0]
+        if rows.shape[0] != B:
+            raise ValueError(f"rows: expected {B} action indices, got {rows.shape[0]}")
+        out = torch.empty((B, Z), dtype=torch.float32, device=value.device)
+        _lib.call("agx_dueling_head_forward_rows", value.data_ptr(), adv.data_ptr(), rows.data_ptr(), B, A, Z, mode,
+                  out.data_ptr(), _lib.stream())
+        ctx.save_for_backward(value, adv, rows)
+        ctx.meta = (A, Z, mode)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _lib
+
+        value, adv, rows = ctx.saved_tensors
+        A, Z, mode = ctx.meta
+        if mode != 2:
+            raise NotImplementedError("selected-row gradient: log mode only (the target distribution is no_grad)")
+        g = g.contiguous()
+        dv, da = torch.empty_like(value), torch.empty_like(adv)
+        _lib.call("agx_dueling_head_backward_rows", value.data_ptr(), adv.data_ptr(), rows.data_ptr(), g.data_ptr(),
+                  value.shape[0], A, Z, dv.data_ptr(), da.data_ptr(), _lib.stream())
+        return dv, da, None, None, None, None
+
+
 class DuelingDistributionalMLP(EvolvableMLP):
     """value stream = self.model (name "value"), advantage stream =
     self.advantage_net (name "advantage"); x = V + A - mean_a A; log-softmax
@@ -103,13 +140,24 @@ class DuelingDistributionalMLP(EvolvableMLP):
     def net_config(self) -> dict[str, Any]:
         return super().net_config
 
-    def forward(self, x: torch.Tensor, q: bool = True, log: bool = False) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, q: bool = True, log: bool = False, rows: torch.Tensor | None = None):
+        """rows (int64 [B], q=False): only action rows[b]'s distribution, [B, Z]."""
         value = self.model(x)
         advantage = self.advantage_net(x)
-        if value.is_cuda and self.num_atoms <= 64 and value.dtype == torch.float32:
+        if rows is not None and q:
+            raise ValueError("rows selects distributions: pass q=False")
+        if rows is not None and value.is_cuda and self.num_atoms <= 64 and value.dtype == torch.float32:
+            return DuelingRowsFn.apply(value, advantage, rows, self.num_actions, self.num_atoms, 2 if log else 1)
+        if value.is_cuda and self.num_atoms <= 64 and value.dtype == torch.float32 and rows is None:
             # the combine, softmax, clamp and support dot in one HIP launch (csrc/heads.hip)
             mode = 2 if log else (0 if q else 1)
             return DuelingHeadFn.apply(value, advantage, self.support, self.num_actions, self.num_atoms, mode)
+        out = self._combine(value, advantage, q, log)
+        if rows is not None:
+            return out[torch.arange(out.shape[0], device=out.device), rows.reshape(-1).long()]
+        return out
+
+    def _combine(self, value: torch.Tensor, advantage: torch.Tensor, q: bool, log: bool) -> torch.Tensor:
         b = value.size(0)
         x = value.view(b, 1, self.num_atoms) + advantage.view(b, self.num_actions, self.num_atoms)
         x = x - advantage.view(b, self.num_actions, self.num_atoms).mean(1, keepdim=True)
@@ -160,8 +208,10 @@ class RainbowQNetwork(EvolvableNetwork):
     def support(self) -> torch.Tensor:
         return self.head_net.support
 
-    def forward(self, obs: torch.Tensor, q: bool = True, log: bool = False) -> torch.Tensor:
-        return self.head_net(self.extract_features(obs), q=q, log=log)
+    def forward(self, obs: torch.Tensor, q: bool = True, log: bool = False, rows: torch.Tensor | None = None):
+        if rows is None:
+            return self.head_net(self.extract_features(obs), q=q, log=log)
+        return self.head_net(self.extract_features(obs), q=q, log=log, rows=rows)
 
 
 class ContinuousQNetwork(EvolvableNetwork):

@@ -388,6 +388,13 @@ int agx_c51_project_loss(const float *q_next_online, const float *target_dist,
                          const float *dones, const float *support, int64_t B, int64_t A,
                          int64_t Z, double v_min, double v_max, double gamma, float *loss,
                          float *proj, void *stream);
+/* The same projection + loss on the two selected rows already gathered
+ * (agx_dueling_head_forward_rows): target_rows [B][Z] = target_dist[b][a*_b],
+ * logp_rows [B][Z] = logp_cur[b][action_b].  Both stream contiguously: the
+ * 128-B lines of the neighbouring actions' atoms are never fetched.  Z = 51. */
+int agx_c51_project_loss_rows(const float *target_rows, const float *logp_rows, const float *rewards,
+                              const float *dones, const float *support, int64_t B, int64_t Z, double v_min,
+                              double v_max, double gamma, float *loss, float *proj, void *stream);
 
 /* ---- optimiser -----------------------------------------------------------
  * Fused per-agent gradient-norm clip + Adam over a population's flat
@@ -466,6 +473,16 @@ int agx_dueling_head_forward(const float *value, const float *advantage, const f
 int agx_dueling_head_backward(const float *value, const float *advantage, const float *support,
                               const float *grad_out, int64_t B, int64_t A, int64_t Z, int mode, float *grad_value,
                               float *grad_advantage, void *stream);
+/* Selected rows (dqn_rainbow.py:313-367 target_dist[range(B), a*] and
+ * log_p[range(B), action], fused into the head): out [B][Z] = the full form's
+ * out[b][sel[b]][:] bit for bit, mode 1 (clamped probabilities) or 2 (log);
+ * sel: device int64 [B].  The backward (log mode) takes dL/d(out rows) [B][Z]
+ * (zero gradient on every other action, as autograd through the gather). */
+int agx_dueling_head_forward_rows(const float *value, const float *advantage, const int64_t *sel, int64_t B,
+                                  int64_t A, int64_t Z, int mode, float *out, void *stream);
+int agx_dueling_head_backward_rows(const float *value, const float *advantage, const int64_t *sel,
+                                   const float *grad_rows, int64_t B, int64_t A, int64_t Z, float *grad_value,
+                                   float *grad_advantage, void *stream);
 
 /* ---- population row gather ---------------------------------------------------
  * The single-rank generation step's clone (tournament.py:71-119 + clone,

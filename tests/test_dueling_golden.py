@@ -112,6 +112,32 @@ def test_dueling_head_kernel_matches_torch(A, Z, B, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("A,Z,B", [(6, 51, 37), (18, 51, 256), (3, 11, 5), (4, 64, 9)])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_dueling_head_rows_equal_full_head(A, Z, B, mode):
+    """agx_dueling_head_forward_rows / _backward_rows: out[range(B), rows] of
+    the full HIP head bit for bit, and (log mode) the full head's gradients
+    under a gradient that is zero off the selected rows, bit for bit."""
+    from agilerl_amd.networks.q_networks import DuelingHeadFn, DuelingRowsFn
+
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(A * 7 + Z + mode)
+    value = (torch.randn(B, Z, device=dev, generator=g) * 2).requires_grad_(True)
+    adv = (torch.randn(B, A * Z, device=dev, generator=g) * 2).requires_grad_(True)
+    rows = torch.randint(0, A, (B,), device=dev, generator=g)
+    out = DuelingRowsFn.apply(value, adv, rows, A, Z, mode)
+    v2, a2 = value.detach().clone().requires_grad_(True), adv.detach().clone().requires_grad_(True)
+    full = DuelingHeadFn.apply(v2, a2, torch.linspace(-10, 10, Z, device=dev), A, Z, mode)
+    idx = torch.arange(B, device=dev)
+    assert torch.equal(out, full[idx, rows])
+    if mode == 2:
+        w = torch.randn(B, Z, device=dev, generator=g)
+        (out * w).sum().backward()
+        (full[idx, rows] * w).sum().backward()
+        assert torch.equal(value.grad, v2.grad) and torch.equal(adv.grad, a2.grad)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("case", ["dueling0", "dueling1"])
 def test_dueling_head_on_gpu_matches_reference_fixture(golden, case):
     """The module on cuda (the HIP combine) against the reference-run outputs."""

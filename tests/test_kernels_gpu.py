@@ -370,6 +370,55 @@ def test_c51_full_size_properties():
     np.testing.assert_allclose(loss[rows].cpu().numpy(), eloss, rtol=1e-5, atol=1e-5)
 
 
+def _lib_error():
+    from agilerl_amd._lib import AgxError
+
+    return AgxError
+
+
+@pytest.mark.parametrize("case", [f"c51_{i}" for i in range(4)])
+def test_c51_rows_golden(golden, case):
+    """agx_c51_project_loss_rows on the two selected rows gathered from the
+    fixture's [B][A][Z] arrays: the same projection bit for bit."""
+    g = golden(case)
+    B = g["q_next"].shape[0]
+    astar = torch.from_numpy(g["q_next"]).argmax(1).numpy()
+    td = np.ascontiguousarray(g["target_dist"][np.arange(B), astar])
+    lp = np.ascontiguousarray(g["logp_cur"][np.arange(B), g["a"].reshape(-1).astype(np.int64)])
+    if td.shape[1] != 51:  # the rows form is Rainbow's 51 atoms only
+        with pytest.raises(_lib_error()):
+            K().c51_project_loss_rows(T(td), T(lp), T(g["r"]), T(g["d"]), T(g["support"]), float(g["vmin"]),
+                                      float(g["vmax"]), float(g["gamma"]))
+        return
+    loss, proj = K().c51_project_loss_rows(T(td), T(lp), T(g["r"]), T(g["d"]), T(g["support"]), float(g["vmin"]),
+                                           float(g["vmax"]), float(g["gamma"]), with_proj=True)
+    _, eproj = odqn.c51_project(g["q_next"], g["target_dist"], g["r"], g["d"], g["support"],
+                                float(g["vmin"]), float(g["vmax"]), float(g["gamma"]))
+    assert np.array_equal(proj.cpu().numpy(), eproj)
+    np.testing.assert_allclose(loss.cpu().numpy(), g["loss"], rtol=1e-5, atol=1e-6)
+
+
+def test_c51_rows_full_size_equals_full_layout():
+    """§8d shape (2^20 rows, A=6, Z=51): the selected-rows kernel equals the
+    [B][A][Z] kernel bit for bit (loss and projection), incl. argmax ties."""
+    B, A, Z = 1 << 20, 6, 51
+    g = torch.Generator(device=DEV).manual_seed(5)
+    qn = torch.randn(B, A, device=DEV, generator=g)
+    qn[:4096] = 0.0  # ties -> the first maximum
+    td = torch.softmax(torch.randn(B, A, Z, device=DEV, generator=g), -1).clamp_(min=1e-3)
+    lp = torch.log_softmax(torch.randn(B, A, Z, device=DEV, generator=g), -1)
+    act = torch.randint(0, A, (B,), device=DEV, generator=g)
+    r = torch.randn(B, device=DEV, generator=g) * 50
+    d = (torch.rand(B, device=DEV, generator=g) < 0.05).float()
+    sup = torch.linspace(-200, 200, Z, device=DEV)
+    loss, proj = K().c51_project_loss(qn, td, lp, act, r, d, sup, -200.0, 200.0, 0.99 ** 4, with_proj=True)
+    idx = torch.arange(B, device=DEV)
+    tr, lr_ = td[idx, qn.argmax(1)].contiguous(), lp[idx, act].contiguous()
+    loss2, proj2 = K().c51_project_loss_rows(tr, lr_, r, d, sup, -200.0, 200.0, 0.99 ** 4, with_proj=True)
+    assert torch.equal(proj, proj2) and torch.equal(loss, loss2)
+    assert torch.equal(loss2, K().c51_project_loss_rows(tr, lr_, r, d, sup, -200.0, 200.0, 0.99 ** 4))
+
+
 @pytest.mark.parametrize("vmin,vmax,gamma,Z", [(-10.0, 10.0, 0.99 ** 3, 51),   # Δz = 0.4: division path
                                                  (-200.0, 200.0, -0.9, 51),       # L/U decreasing: RMW fallback
                                                  (-100.0, 100.0, 0.99, 41)])      # other Z: row-wave kernel

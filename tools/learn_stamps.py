@@ -1,8 +1,9 @@
 """Phase timing of the fused learner (diagnostic; uses agx_debug_learn_stamps).
 
 Slots (learner.hip AGX_STAMP): sub-batch k of agent 0's first minibatch at
-k*16 + {0 start, 1 gathered, 2 forward, 3 loss, 4 out-layer bwd, 5 head LN bwd,
-6 head dW/dX, 7 encoder bwd}; 64+9 gradients dumped, 64+10 Adam done;
+k*16 + {0 start, 1 gathered, 2 forward trunk, 3 head row pass (LN fwd + output
+layers + loss + LN bwd; 4 and 5 stamped with it), 6 output-layer + head dW / dX,
+7 encoder bwd}; 64+9 gradients dumped, 64+10 Adam done;
 partners: 64+11/12 first barrier ticket/passed, 64+13 reduce-scatter done,
 64+8/15 second barrier ticket/passed, 64+14 norm done."""
 import os
@@ -37,7 +38,7 @@ lib.agx_debug_learn_stamps(None)
 st = buf.cpu().tolist()
 nmb = pop.update_epochs * pop.n_minibatches()
 print(f"learn() wall {1e3 * (t1 - t0):.3f} ms  ({nmb} minibatch updates per agent, {P} agents)")
-names = ["gather", "fwd", "loss", "out bwd", "head LN bwd", "head dW+dX", "enc bwd"]
+names = ["gather", "trunk fwd", "head row pass", "-", "-", "out+head dW, dX", "enc bwd"]
 for sb in range(4):
     row = st[sb * 16: sb * 16 + 8]
     if not all(row):  # only workgroup 0 stamps: with K partners it runs 1 of every K sub-batches
