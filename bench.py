@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (Atari PPO) side measurement")
+    ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (Atari Rainbow) learner measurement")
     ap.add_argument("--roof-reps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--dist-selftest", action="store_true",
@@ -776,6 +777,158 @@ def config5_leg(iters: int = 5):
     return out
 
 
+CONFIG3_NET = {"latent_dim": 256, "min_latent_dim": 128, "max_latent_dim": 512,
+               "encoder_config": {"channel_size": [32, 64, 128], "kernel_size": [8, 4, 3], "stride_size": [4, 2, 1]},
+               "head_config": {"hidden_size": [256]}}
+
+
+def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15):
+    """Config 3 (Atari Pong Rainbow DQN, pop 8): learner updates/s of the
+    population-batched learner (algorithms/rainbow_pop.py) on uint8 4x84x84
+    frames, CNN 32/64/128 -> 256, dueling noisy heads [256], A = 6, Z = 51 on
+    +-200, B = 64, PER (alpha 0.6, beta 0.4) over a 1M-transition buffer
+    (2^20-leaf trees) holding `fill` synthetic transitions.  One iteration =
+    the P agents' samples in one draw (the same torch.rand stream as P
+    draws), one batched learn, the P priority updates in agent order.  The
+    per-agent loop of the reference (sample, agent.learn, update per agent)
+    is timed on the same agents beside it."""
+    from agilerl_amd.algorithms import RainbowDQN
+    from agilerl_amd.algorithms.rainbow_pop import RainbowPopulationLearner
+    from agilerl_amd.components import PrioritizedReplayBuffer
+    from agilerl_amd.envs import Box, Discrete
+
+    dev = torch.device("cuda")
+    obs_space, act_space = Box(0, 255, (4, 84, 84), dtype=np.uint8), Discrete(6)
+    torch.manual_seed(0)
+    agents = [RainbowDQN(obs_space, act_space, net_config=CONFIG3_NET, batch_size=B, lr=1e-4, gamma=0.99, tau=1e-3,
+                         v_min=-200.0, v_max=200.0, num_atoms=51) for _ in range(P)]
+    memory = PrioritizedReplayBuffer(1_000_000, alpha=0.6)
+    g = torch.Generator(device=dev).manual_seed(1)
+    for c in range(0, fill, 4096):
+        n = min(4096, fill - c)
+        memory.add({"obs": torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g),
+                    "action": torch.randint(0, 6, (n,), device=dev, generator=g),
+                    "reward": torch.randn(n, device=dev, generator=g),
+                    "next_obs": torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g),
+                    "done": (torch.rand(n, device=dev, generator=g) < 0.02).float()})
+    learner = RainbowPopulationLearner(agents)
+
+    def batched():
+        s = memory.sample(P * B, beta=0.4)
+        exps = [{k: v[p * B:(p + 1) * B] for k, v in s.items()} for p in range(P)]
+        outs = learner.learn(exps, per=True)
+        memory.update_priorities(torch.cat([o[1].reshape(-1) for o in outs]),
+                                 np.concatenate([o[2].reshape(-1) for o in outs]))
+
+    def per_agent():
+        for a in agents:
+            s = memory.sample(B, beta=0.4)
+            _, idxs, pri = a.learn(s, per=True)
+            memory.update_priorities(idxs, pri)
+
+    out = {"workload": f"config 3: Rainbow DQN pop={P}, B={B}, uint8 4x84x84 frames, CNN 32/64/128 -> 256, dueling "
+                       "noisy heads [256], A=6, Z=51 (+-200), PER alpha 0.6 / beta 0.4 on a 1M-transition buffer "
+                       f"(2^20-leaf trees, {fill} transitions stored)", "iterations": iters}
+    for name, fn in (("batched", batched), ("per_agent", per_agent)):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out[name] = {"learner_updates_per_s": round(P * iters / dt, 1), "ms_per_iteration": round(dt / iters * 1e3, 3)}
+    out["learner_updates_per_s"] = out["batched"]["learner_updates_per_s"]
+    del learner, agents, memory
+    torch.cuda.empty_cache()
+    return out
+
+
+def cpu_config3_learn(seconds: float, B: int = 64):
+    """The reference's Rainbow update (dqn_rainbow.py:284-490: three forwards,
+    the torch-op C51 projection + loss, backward, clip_grad_norm_(10), Adam,
+    soft update, noise reset) restated in plain torch ops on the host cores,
+    for ONE agent of the config-3 network; bounded to ~`seconds`."""
+    from torch import nn
+    from torch.nn import functional as F
+
+    threads = torch.get_num_threads()
+    A, Z = 6, 51
+
+    class Noisy(nn.Module):
+        def __init__(self, i, o):
+            super().__init__()
+            self.mu_w = nn.Parameter(torch.randn(o, i) / i ** 0.5)
+            self.sg_w = nn.Parameter(torch.full((o, i), 0.5 / i ** 0.5))
+            self.mu_b = nn.Parameter(torch.zeros(o))
+            self.sg_b = nn.Parameter(torch.full((o,), 0.5 / o ** 0.5))
+            self.reset()
+
+        def reset(self):
+            f = lambda n: (lambda x: x.sign() * x.abs().sqrt())(torch.randn(n))  # noqa: E731
+            ei, eo = f(self.mu_w.shape[1]), f(self.mu_w.shape[0])
+            self.eps_w, self.eps_b = torch.outer(eo, ei), eo
+
+        def forward(self, x):
+            return F.linear(x, self.mu_w + self.sg_w * self.eps_w, self.mu_b + self.sg_b * self.eps_b)
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.enc = nn.Sequential(nn.Conv2d(4, 32, 8, 4), nn.ReLU(), nn.Conv2d(32, 64, 4, 2), nn.ReLU(),
+                                     nn.Conv2d(64, 128, 3, 1), nn.ReLU(), nn.Flatten(), nn.Linear(128 * 7 * 7, 256),
+                                     nn.ReLU())
+            self.v1, self.v2, self.vn = Noisy(256, 256), Noisy(256, Z), nn.LayerNorm(256)
+            self.a1, self.a2, self.an = Noisy(256, 256), Noisy(256, A * Z), nn.LayerNorm(256)
+
+        def forward(self, x, log=False):
+            h = self.enc(x.float() / 255.0)
+            v = self.v2(F.relu(self.vn(self.v1(h)))).view(-1, 1, Z)
+            a = self.a2(F.relu(self.an(self.a1(h)))).view(-1, A, Z)
+            x = v + a - a.mean(1, keepdim=True)
+            return F.log_softmax(x, -1) if log else F.softmax(x, -1).clamp(min=1e-3)
+
+        def noise(self):
+            for m in (self.v1, self.v2, self.a1, self.a2):
+                m.reset()
+
+    torch.manual_seed(0)
+    net, tgt = Net(), Net()
+    tgt.load_state_dict(net.state_dict())
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    support = torch.linspace(-200.0, 200.0, Z)
+    g = torch.Generator().manual_seed(2)
+    obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, generator=g)
+    nobs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, generator=g)
+    act = torch.randint(0, A, (B, 1), generator=g)
+    r, d = torch.randn(B, 1, generator=g), (torch.rand(B, 1, generator=g) < 0.02).float()
+    w = torch.rand(B, 1, generator=g)
+    t0, reps = time.perf_counter(), 0
+    while True:
+        with torch.no_grad():
+            q_next = (net(nobs) * support).sum(2)
+            td = tgt(nobs)
+        logp = net(obs, log=True)
+        el = _c51_torch_ops(q_next, td, logp, act, r, d, support, -200.0, 200.0, 0.99)
+        loss = torch.mean(el * w)
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(net.parameters(), 10.0)
+        opt.step()
+        with torch.no_grad():
+            for pt, po in zip(tgt.parameters(), net.parameters()):
+                pt.copy_(1e-3 * po + (1 - 1e-3) * pt)
+        net.noise()
+        tgt.noise()
+        reps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=round(reps / dt, 2), unit="learner updates/s", cores=threads, kind="port",
+                sample=f"{reps} Rainbow updates of one config-3 agent (B={B}) in torch CPU ops on {threads} threads")
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -806,6 +959,7 @@ def main():
         roof = roofline_leg(args)
         kern = kernels_leg(roof["peak_measured"])
     c5 = config5_leg() if (world == 1 and not args.no_config5) else None
+    c3 = config3_leg() if (world == 1 and not args.no_config3) else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline_leg(args, res["S"])
@@ -813,6 +967,8 @@ def main():
         cpu["roofline_workload"] = cpu_kernels_leg(min(args.cpu_seconds, 8.0))
         cpu["off_policy"] = cpu_offpolicy_leg(min(args.cpu_seconds, 9.0))
         cpu["cpu_model"] = cpu["off_policy"]["cpu_model"]
+        if c3 is not None:
+            cpu["config3_learn"] = cpu_config3_learn(min(args.cpu_seconds, 10.0))
     if rank == 0:
         value = res["env_steps"] / res["dt"]
         line = {
@@ -849,6 +1005,7 @@ def main():
             "roofline": roof,
             "kernels": kern,
             "config5": c5,
+            "config3": c3,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
