@@ -402,6 +402,16 @@ class PPO:
                       out["entropy"].data_ptr(), 0, None, None, _lib.stream())
         return tuple(out[k].cpu().numpy() for k in ("actions", "log_probs", "entropy", "values"))
 
+    @property
+    def rollout_buffer(self) -> "AgentRolloutBuffer":
+        """The reference's ``agent.rollout_buffer`` (RolloutBuffer API: reset /
+        add / compute_returns_and_advantages / size) over this agent's rows
+        of the HBM rollout, for custom collectors (``collect_rollouts_fn``)."""
+        buf = getattr(self, "_rollout_buffer", None)
+        if buf is None or buf.pop is not self.population or buf.row != self.row:
+            buf = self._rollout_buffer = AgentRolloutBuffer(self.population, self.row)
+        return buf
+
     def learn(self, experiences=None) -> float:
         """One PPO update of this agent from the HBM rollout (ppo.py:635-921);
         returns the reference's mean loss (sum / (num_samples * epochs))."""
@@ -446,3 +456,59 @@ class PPO:
         mean_fit = float(np.mean(rewards))
         self.fitness.append(mean_fit)
         return mean_fit
+
+
+class AgentRolloutBuffer:
+    """RolloutBuffer (agilerl/components/rollout_buffer.py:61-481) calls on one
+    agent's slice of a population's HBM rollout SoA.  A custom collector
+    (train_on_policy's ``collect_rollouts_fn``, on_policy.py:23-203 shape)
+    ``reset()``s it, ``add()``s one vector step at a time (obs, action,
+    reward, done, value, log_prob of the agent's num_envs envs) and calls
+    ``compute_returns_and_advantages(last_value, last_done)``: the agx_gae
+    launch of the agent's population.  The population must hold this agent
+    alone (train_on_policy runs custom collectors with one agent per group),
+    so the GAE and the learn that follows touch no other agent's rollout."""
+
+    def __init__(self, pop, row: int):
+        self.pop, self.row = pop, int(row)
+        self.capacity, self.num_envs = pop.T, pop.N
+        self.pos, self.full = 0, False
+
+    def reset(self) -> None:
+        self.pos, self.full = 0, False
+
+    def size(self) -> int:
+        return self.capacity * self.num_envs if self.full else self.pos * self.num_envs
+
+    def _put(self, dst: torch.Tensor, value, dtype=None) -> None:
+        t = torch.as_tensor(np.asarray(value) if not isinstance(value, torch.Tensor) else value, device=dst.device)
+        dst.copy_(t.to(dtype or dst.dtype).reshape(dst.shape))
+
+    def add(self, obs, action, reward, done, value, log_prob, next_obs=None, hidden_state=None, **_kw) -> None:
+        if self.pos >= self.capacity:
+            raise ValueError(f"rollout buffer full ({self.capacity} vector steps); call reset()")
+        p, t = self.pop, self.pos
+        self._put(p.obs[self.row, t], obs)
+        self._put(p.actions[self.row, t], action)
+        self._put(p.rewards[self.row, t], reward)
+        self._put(p.dones[self.row, t], np.asarray(done, dtype=np.uint8) if not isinstance(done, torch.Tensor)
+                  else done.to(torch.uint8))
+        self._put(p.values[self.row, t], value)
+        self._put(p.log_probs[self.row, t], log_prob)
+        self.pos += 1
+        self.full = self.pos == self.capacity
+
+    def compute_returns_and_advantages(self, last_value, last_done) -> None:
+        p = self.pop
+        if p.P != 1:
+            raise NotImplementedError("a custom collector fills one agent's rollout: the agent must be alone in "
+                                      "its population (train_on_policy groups agents one per population when "
+                                      "collect_rollouts_fn is given)")
+        if not self.full:
+            raise ValueError(f"the rollout holds {self.pos} of {self.capacity} vector steps; the learner takes a "
+                             "full rollout (ceil(learn_step / num_envs) steps)")
+        lv = torch.as_tensor(np.asarray(last_value, dtype=np.float32) if not isinstance(last_value, torch.Tensor)
+                             else last_value, device=p.device).to(torch.float32).reshape(1, p.N).contiguous()
+        ld = torch.as_tensor(np.asarray(last_done) if not isinstance(last_done, torch.Tensor) else last_done,
+                             device=p.device).to(torch.uint8).reshape(1, p.N).contiguous()
+        p.finish_rollout(None, ld, lv)

@@ -81,8 +81,12 @@ class _Group:
 
 
 class PopulationEngine:
-    def __init__(self, population: PPOPopulation, views: list, env, world: int = 1, rank: int = 0):
+    def __init__(self, population: PPOPopulation, views: list, env, world: int = 1, rank: int = 0,
+                 singleton: bool = False):
+        """``singleton``: every agent in a group of its own (custom collectors
+        fill one agent's rollout at a time, as the reference's per-agent loop)."""
         self.views = list(views)
+        self.singleton = bool(singleton)
         self.P, self.N = population.P, population.N
         self.world, self.rank = world, rank
         self.device = population.device
@@ -98,6 +102,8 @@ class PopulationEngine:
         self.global_plan = [(population.S, population.update_epochs, learn_step)] * (self.P * world)
         self._gen_state = None  # numpy state before the generation's shuffles (target_kl re-sync)
         self.refresh_plan()
+        if self.singleton and self.P > 1:
+            self.regroup(self.local_states())
 
     # ------------------------------------------------------------------ #
     @property
@@ -280,15 +286,18 @@ class PopulationEngine:
     def regroup(self, states: list[AgentState]) -> None:
         """Groups rebuilt from every slot's state: slots with equal (network
         shape, learn_step) share a PPOPopulation, in slot order."""
-        if self.slot_envs is None and len({(s.spec.shape_key(), s.learn_step) for s in states}) > 1:
+        key = (lambda j, s: (j, s.spec.shape_key(), s.learn_step)) if self.singleton else \
+            (lambda j, s: (s.spec.shape_key(), s.learn_step))
+        if self.slot_envs is None and len({key(j, s) for j, s in enumerate(states)}) > 1:
             raise NotImplementedError("agents with different networks or learn_step need one env per agent: pass "
                                       "the reference's num_envs env (cloned per agent) or a StackedVecEnv")
         order: dict[tuple, list[int]] = {}
         for j, s in enumerate(states):
-            order.setdefault((s.spec.shape_key(), s.learn_step), []).append(j)
+            order.setdefault(key(j, s), []).append(j)
         t = self._template
         groups = []
-        for (_, learn_step), slots in order.items():
+        for k, slots in order.items():
+            learn_step = k[-1]
             st = [states[j] for j in slots]
             spec = st[0].spec
             pop = PPOPopulation(spec, len(slots), self.N, learn_step=learn_step,

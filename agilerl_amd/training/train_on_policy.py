@@ -118,16 +118,38 @@ def _apply_mutations(engine) -> None:
         engine.refresh_plan()
 
 
+def _train_with_collector(engine, pop, env, evo_steps: int, collect_fn) -> list:
+    """train_on_policy.py:216-248 with a custom ``collect_rollouts_fn``: agent
+    after agent on the caller's env, ``ceil(evo_steps / learn_step)`` times
+    ``collect_fn(agent, env, n_steps=..., last_obs=..., last_done=...,
+    last_scores=..., last_info=...)`` (filling ``agent.rollout_buffer``) then
+    ``agent.learn()``; the collector's completed episode scores become the
+    agent's training score."""
+    losses = []
+    for j, agent in enumerate(pop):
+        g, _ = engine.group_of(j)
+        n_steps = -(int(g.learn_step) // -engine.N)
+        last = {"last_obs": None, "last_done": None, "last_scores": None, "last_info": None}
+        completed: list[float] = []
+        for _ in range(engine.iterations(evo_steps, g.learn_step)):
+            out = collect_fn(agent, env, n_steps=n_steps, **last)
+            if isinstance(out, tuple) and len(out) == 5:
+                scores, last["last_obs"], last["last_done"], last["last_scores"], last["last_info"] = out
+                completed += [float(x) for x in scores]
+            losses.append(np.asarray([agent.learn()]))
+        if completed:
+            agent.scores.append(float(np.mean(completed)))
+    return losses
+
+
 def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None, swap_channels: bool = False,
                     max_steps: int = 1_000_000, evo_steps: int = 10_000, eval_steps=None, eval_loop: int = 1,
                     target: float | None = None, tournament=None, mutation=None, checkpoint=None,
                     checkpoint_path=None, overwrite_checkpoints: bool = False, save_elite: bool = False,
                     elite_path=None, wb: bool = False, verbose: bool = True, accelerator=None, wandb_api_key=None,
                     wandb_kwargs=None, collect_rollouts_fn=None):
-    if collect_rollouts_fn is not None:
-        raise NotImplementedError("custom collect_rollouts_fn: the population engine collects on device "
-                                  "(PopulationRunner); pass None")
     population = pop[0].population
+    user_env = env
     if any(a.population is not population for a in pop):
         raise ValueError("all agents must come from one agilerl_amd.utils.create_population call")
     P, N = population.P, population.N
@@ -136,7 +158,9 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
         raise ValueError("the population's shard does not match this process group")
     env = _population_env(env, P, N, population.agent_offset)
     # agents grouped by (network shape, learn_step): one group until a mutation splits them
-    engine = PopulationEngine(population, pop, env, world, rank)
+    # a custom collector fills one agent's rollout at a time (the reference's
+    # per-agent loop, :216-248): every agent then learns in a group of its own
+    engine = PopulationEngine(population, pop, env, world, rank, singleton=collect_rollouts_fn is not None)
     sync = None
     if tournament is not None and mutation is not None:  # the reference selects only with both (:440)
         sync = PopulationSync(population, engine.groups[0].runner, world, rank, seed=None,
@@ -155,7 +179,10 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
         # the generation's minibatch shuffles, agent after agent as the reference's
         # agents learn (train_on_policy.py:210-248 -> ppo.py:836-842)
         engine.draw_generation_perms(evo_steps)
-        losses = engine.train(evo_steps)
+        if collect_rollouts_fn is None:
+            losses = engine.train(evo_steps)
+        else:
+            losses = _train_with_collector(engine, pop, user_env, evo_steps, collect_rollouts_fn)
         for j, agent in enumerate(pop):
             agent.steps[-1] += engine.steps_per_generation(j, evo_steps)
         engine.resync_numpy_after_generation(evo_steps)
@@ -165,7 +192,7 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
         # (train_on_policy.py:363-373), batched on device over the env slices
         fitness = engine.evaluate(eval_loop, eval_steps)
         for i, agent in enumerate(pop):
-            if r_cnt[i] > 0:
+            if r_cnt[i] > 0 and collect_rollouts_fn is None:
                 agent.scores.append(float(r_sum[i] / r_cnt[i]))
             agent.fitness.append(fitness[i])
             agent.steps.append(agent.steps[-1])

@@ -448,7 +448,18 @@ def kernels_leg(peak_meas):
     out["c51_project_loss"] = dict(unit_bytes=444, units=B, ms=round(t * 1e3, 4), ms_eager=round(te * 1e3, 4),
                                    gbs=round(nb / t / 1e9, 1),
                                    frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
+    # the selected-rows form (the heads emit target_dist[b, a*] and log p[b, a]
+    # as two contiguous [B][Z] arrays): 204 + 204 + r, d in, loss out
+    tr = td[torch.arange(B, device=dev), qn.argmax(1)].contiguous()
+    lr_ = lp[torch.arange(B, device=dev), act].contiguous()
     del td, lp
+    t, te = _both(lambda: K.c51_project_loss_rows(tr, lr_, r, d, sup, -200.0, 200.0, 0.99 ** 4))
+    ub = 2 * 4 * Z + 4 + 4 + 4
+    nb = ub * B
+    out["c51_project_loss_rows"] = dict(unit_bytes=ub, units=B, ms=round(t * 1e3, 4), ms_eager=round(te * 1e3, 4),
+                                        gbs=round(nb / t / 1e9, 1),
+                                        frac_of_measured=round(nb / t / 1e9 / peak_meas, 4), bound="hbm")
+    del tr, lr_
     qt = torch.randn(B, A, device=dev, generator=g3)
     qc = torch.randn(B, A, device=dev, generator=g3)
     t, te = _both(lambda: K.td_target(qt, r, d, 0.99, q_next_online=qn, double=True, q_cur=qc, actions=act))

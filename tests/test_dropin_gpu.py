@@ -347,3 +347,91 @@ def test_ppo_checkpoint_round_trip(tmp_path):
     _, lp1, ent1, v1 = other.get_action(obs)
     np.testing.assert_array_equal(v0, v1)
     np.testing.assert_array_equal(ent0, ent1)
+
+
+def _reference_style_collect(agent, env, n_steps=None, last_obs=None, last_done=None, last_scores=None,
+                             last_info=None):
+    """A custom collector written against the reference's API
+    (rollouts/on_policy.py:23-203): agent.get_action + agent.rollout_buffer."""
+    buf = agent.rollout_buffer
+    buf.reset()
+    if last_obs is None:
+        obs, info = env.reset()
+        done, scores = np.zeros(env.num_envs, np.float32), np.zeros(env.num_envs)
+    else:
+        obs, done, scores, info = last_obs, last_done, last_scores, last_info
+    completed = []
+    for _ in range(n_steps):
+        action, log_prob, _, value = agent.get_action(obs)
+        next_obs, reward, term, trunc, info = env.step(action)
+        scores = scores + np.asarray(reward)
+        buf.add(obs=obs, action=action, reward=reward, done=done, value=value, log_prob=log_prob)
+        nd = np.logical_or(term, trunc).astype(np.float32)
+        for i in np.flatnonzero(nd):
+            completed.append(float(scores[i]))
+            scores[i] = 0.0
+        obs, done = next_obs, nd
+    _, _, _, last_value = agent.get_action(obs)
+    buf.compute_returns_and_advantages(last_value=last_value, last_done=done)
+    return completed, obs, done, scores, info
+
+
+@pytest.mark.parametrize("which", ["reference_style", "agx"])
+def test_train_on_policy_custom_collect_rollouts_fn(which):
+    """train_on_policy(collect_rollouts_fn=...) (train_on_policy.py:55-57,
+    216-248): agent after agent on the caller's env, the collector filling
+    agent.rollout_buffer, then agent.learn(); tournament + mutations."""
+    import warnings
+
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.mutation import Mutations
+    from agilerl_amd.hpo.tournament import TournamentSelection
+    from agilerl_amd.rollouts import collect_rollouts
+    from agilerl_amd.training import train_on_policy
+    from agilerl_amd.utils import create_population
+
+    np.random.seed(0)
+    torch.manual_seed(0)
+    env = SyntheticVecEnv(8, seed=2, p_done=1 / 10)
+    net = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}, "latent_dim": 64}
+    init = {"BATCH_SIZE": 32, "LR": 1e-3, "LEARN_STEP": 64, "UPDATE_EPOCHS": 2}
+    pop = create_population("PPO", net, init, env.single_observation_space, env.single_action_space,
+                            population_size=3, num_envs=8)
+    p0 = [a.population.params.data[a.row].clone() for a in pop]
+    fn = _reference_style_collect if which == "reference_style" else collect_rollouts
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        pop, fits = train_on_policy(env, "Synthetic", "PPO", pop, INIT_HP=init, max_steps=256, evo_steps=128,
+                                    eval_steps=20, tournament=TournamentSelection(2, True, 3, 1),
+                                    mutation=Mutations(0.4, 0, 0.2, 0.2, 0, 0.2, rand_seed=1), verbose=False,
+                                    collect_rollouts_fn=fn)
+    assert len(fits) == 2 and all(np.all(np.isfinite(f)) for f in fits)
+    assert all(a.steps[-1] == 256 for a in pop)
+    assert all(a.population.P == 1 for a in pop)  # one agent per group with a custom collector
+    assert any(len(a.scores) > 0 for a in pop)
+    moved = [not torch.equal(a.population.params.data[a.row], q) for a, q in zip(pop, p0)]
+    assert any(moved)
+
+
+def test_agent_rollout_buffer_writes_the_agent_rows():
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.utils import create_population
+
+    env = SyntheticVecEnv(4, seed=5)
+    net = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}, "latent_dim": 64}
+    (agent,) = create_population("PPO", net, {"BATCH_SIZE": 8, "LEARN_STEP": 8, "UPDATE_EPOCHS": 1},
+                                 env.single_observation_space, env.single_action_space, population_size=1, num_envs=4)
+    rng = np.random.default_rng(0)
+    buf = agent.rollout_buffer
+    obs = rng.standard_normal((2, 4, 8)).astype(np.float32)
+    for t in range(2):
+        buf.add(obs=obs[t], action=np.arange(4) % 4, reward=np.full(4, t, np.float32), done=np.zeros(4),
+                value=np.ones(4, np.float32), log_prob=np.full(4, -1.0, np.float32))
+    assert buf.full and buf.size() == 8
+    pop = agent.population
+    assert np.array_equal(pop.obs[0].cpu().numpy(), obs)
+    assert np.array_equal(pop.rewards[0, 1].cpu().numpy(), np.ones(4, np.float32))
+    buf.compute_returns_and_advantages(last_value=np.zeros(4, np.float32), last_done=np.ones(4))
+    # last step: done_{t+1} = 1 -> advantage = r - V = 1 - 1 = 0 exactly
+    assert np.array_equal(pop.advantages[0, 1].cpu().numpy(), np.zeros(4, np.float32))
+    assert np.isfinite(agent.learn())

@@ -16,4 +16,10 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o roof -- python tools/pmc_roofline.py > gpurun_out/pmc_write.log 2>&1 || { tail -20 gpurun_out/pmc_write.log; exit 1; }
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/c51_fetch -o c51 -- python tools/c51_pmc.py > gpurun_out/c51_fetch.log 2>&1 || { tail -20 gpurun_out/c51_fetch.log; exit 1; }
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/c51_write -o c51 -- python tools/c51_pmc.py > gpurun_out/c51_write.log 2>&1 || { tail -20 gpurun_out/c51_write.log; exit 1; }
+timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/c51r_fetch -o c51 -- python tools/prof_c51_rows.py > gpurun_out/c51r_fetch.log 2>&1 || { tail -20 gpurun_out/c51r_fetch.log; exit 1; }
+timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/c51r_write -o c51 -- python tools/prof_c51_rows.py > gpurun_out/c51r_write.log 2>&1 || { tail -20 gpurun_out/c51r_write.log; exit 1; }
+python tools/pmc_summarize.py gpurun_out/pmc_fetch gpurun_out/pmc_write > gpurun_out/${R}_pmc_traffic.json || exit 1
+python tools/pmc_c51_summary.py gpurun_out/c51_fetch gpurun_out/c51_write > gpurun_out/${R}_c51_pmc_traffic.json || exit 1
+python tools/pmc_c51_summary.py gpurun_out/c51r_fetch gpurun_out/c51r_write rows > gpurun_out/${R}_c51_rows_pmc_traffic.json || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3_$R -o c3 -- python tools/prof_config3.py > gpurun_out/prof_c3_$R.log 2>&1 || { tail -20 gpurun_out/prof_c3_$R.log; exit 1; }
 echo ALLOK
