@@ -83,7 +83,8 @@ def _limits(cfg, config_default: bool) -> tuple:
             int(get("min_mlp_nodes", d[2])), int(get("max_mlp_nodes", d[3])))
 
 
-def spec_from_net_config(observation_space, action_space, net_config: dict | None, normalize_images: bool = True):
+def spec_from_net_config(observation_space, action_space, net_config: dict | None, normalize_images: bool = True,
+                         share_encoders: bool = True):
     """The networks ppo.py:286-320 builds, as the reference's defaults fill
     them in: no encoder_config -> get_default_encoder_config's MlpNetConfig
     [64, 64] (utils/evolvable_networks.py:168-217); latent_dim 32 with limits
@@ -96,6 +97,8 @@ def spec_from_net_config(observation_space, action_space, net_config: dict | Non
     from ..networks.base import is_image_space
 
     if is_image_space(observation_space):
+        if not share_encoders:
+            raise NotImplementedError("agx image PPO: the shared CNN encoder (share_encoders=True)")
         return _image_spec(observation_space, action_space, net_config, normalize_images)
     enc_cfg = net_config.get("encoder_config")
     enc = _hidden(enc_cfg, [64, 64])
@@ -110,7 +113,8 @@ def spec_from_net_config(observation_space, action_space, net_config: dict | Non
     return ActorCriticSpec(obs_dim=obs_dim, n_actions=int(action_space.n), encoder_hidden=enc, latent_dim=latent,
                            actor_hidden=actor_hidden, critic_hidden=critic_hidden, encoder_limits=enc_lim,
                            actor_limits=head_lim, critic_limits=head_lim if head is not None else (1, 3, 16, 500),
-                           latent_limits=lat_lim)
+                           latent_limits=lat_lim, share_encoders=bool(share_encoders),
+                           encoder_name="shared_encoder" if share_encoders else "actor_encoder")
 
 
 class PPO:
@@ -130,8 +134,7 @@ class PPO:
             raise NotImplementedError("recurrent PPO is outside the agx hot path")
         if actor_network is not None or critic_network is not None:
             raise NotImplementedError("custom actor/critic modules: use net_config (MLP) networks")
-        if not share_encoders:
-            raise NotImplementedError("agx PPO uses the shared-encoder actor-critic (the reference default)")
+        self.share_encoders = bool(share_encoders)
         assert isinstance(batch_size, int) and batch_size >= 1, "Batch size must be an integer greater than or equal to one."
         assert lr > 0, "Learning rate must be greater than zero."
         assert isinstance(learn_step, int) and learn_step >= 1, "Learn step rate must be an integer greater than or equal to one."
@@ -152,7 +155,8 @@ class PPO:
         self.fitness: list[float] = []
         self.steps: list[int] = [0]
         if _population is None:
-            spec = spec_from_net_config(observation_space, action_space, net_config, normalize_images)
+            spec = spec_from_net_config(observation_space, action_space, net_config, normalize_images,
+                                        share_encoders=share_encoders)
             _population = PPOPopulation(spec, 1, num_envs, learn_step=learn_step, batch_size=batch_size, lr=lr,
                                         gamma=gamma, gae_lambda=gae_lambda, clip_coef=clip_coef, ent_coef=ent_coef,
                                         vf_coef=vf_coef, max_grad_norm=max_grad_norm, update_epochs=update_epochs,
@@ -241,7 +245,8 @@ class PPO:
     def can_mutate_architecture(self) -> bool:
         from ..population.nets import ActorCriticSpec
 
-        return isinstance(self.spec, ActorCriticSpec)
+        # population/arch.py mutates the shared-encoder layout
+        return isinstance(self.spec, ActorCriticSpec) and self.spec.share_encoders
 
     def architecture_mutation(self, new_layer_prob: float, rng) -> str | None:
         """mutation.py:829-885 on this agent (population/arch.py): -> the
@@ -304,7 +309,7 @@ class PPO:
                 raise KeyError(f"state_dict mismatch: missing {sorted(missing)}, unexpected {sorted(unexpected)}")
         flat = self.population.params.data[self.row]
         for k, (off, shape) in keys.items():
-            if k in state_dict and not k.startswith("critic.encoder."):
+            if k in state_dict and not self.spec.aliased(k):
                 t = torch.as_tensor(state_dict[k])
                 if tuple(t.shape) != tuple(shape):
                     raise ValueError(f"{k}: shape {tuple(t.shape)}, expected {tuple(shape)}")
@@ -321,10 +326,11 @@ class PPO:
         sd = self.state_dict()
         keys = self.spec.state_dict_keys()
         m, v = self._opt_rows()
+        spec = self.spec
         opt = {"exp_avg": {k: m[o:o + int(np.prod(sh))].view(sh) for k, (o, sh) in keys.items()
-                           if not k.startswith("critic.encoder.")},
+                           if not spec.aliased(k)},
                "exp_avg_sq": {k: v[o:o + int(np.prod(sh))].view(sh) for k, (o, sh) in keys.items()
-                              if not k.startswith("critic.encoder.")},
+                              if not spec.aliased(k)},
                "step": int(self.population.opt.steps[self.row])}
         mods = {net: {k[len(net) + 1:]: t for k, t in sd.items() if k.startswith(net + ".")}
                 for net in ("actor", "critic")}
@@ -343,7 +349,7 @@ class PPO:
         keys = self.spec.state_dict_keys()
         m, v = self._opt_rows()
         for k, t in opt["exp_avg"].items():
-            if k.startswith("critic.encoder."):  # shares the actor encoder's row (a reference file holds both)
+            if self.spec.aliased(k):  # shares the actor encoder's row (a reference file holds both)
                 continue
             o, sh = keys[k]
             m[o:o + t.numel()] = t.reshape(-1).to(m)
@@ -416,7 +422,7 @@ class PPO:
         """One PPO update of this agent from the HBM rollout (ppo.py:635-921);
         returns the reference's mean loss (sum / (num_samples * epochs))."""
         if experiences is not None:
-            raise NotImplementedError("agx PPO learns from its HBM rollout buffer (use_rollout_buffer=True path)")
+            return self._learn_from_experiences(experiences)
         # Views of one population learn together: the first view to call learn()
         # after a rollout runs the fused learner for every agent (each agent is
         # updated exactly once per rollout, as in the reference's per-agent loop).
@@ -426,6 +432,92 @@ class PPO:
             pop.check_errors()  # a partner timeout would leave the update incomplete: raise, never return it
             pop._learned_rollout = pop.rollout_id
         return float(pop._last_losses[self.row])
+
+    def _learn_from_experiences(self, experiences) -> float:
+        """The reference's deprecated ``learn(experiences)``
+        (ppo.py:655-812, use_rollout_buffer=False): (observations, actions,
+        log_probs, rewards, dones, values, next_obs, next_done) stacked over
+        time; GAE with next_non_terminal = 1 - dones[t + 1] (next_done at the
+        end) and the critic's value of next_obs; per epoch one numpy shuffle,
+        minibatches of ``batch_size`` (singletons skipped) with the advantage
+        normalised per minibatch, the clipped loss, the two-group gradient clip
+        and Adam (agx_clip_adam on this agent's row); target_kl checked after
+        each epoch on the last minibatch's approx_kl.  -> mean_loss /
+        (num_samples * update_epochs)."""
+        from ..population.nets import categorical
+
+        if not experiences:
+            raise ValueError("Experiences must be provided when use_rollout_buffer is False")
+        pop, r, spec = self.population, self.row, self.spec
+        if pop.fused_descriptor() is None and getattr(spec, "feat_dim", None) is not None:
+            raise NotImplementedError("learn(experiences): MLP actor-critics")
+
+        def stack(x, dtype):
+            if isinstance(x, torch.Tensor):
+                t = x
+            elif isinstance(x, (list, tuple)) and len(x) and isinstance(x[0], torch.Tensor):
+                t = torch.stack([torch.as_tensor(v) for v in x])
+            else:
+                t = torch.as_tensor(np.asarray(x))
+            return t.to(self.device, dtype)
+
+        obs, actions, log_probs, rewards, dones, values, next_obs, next_done = experiences
+        obs = stack(obs, torch.float32)
+        actions, log_probs = stack(actions, torch.int64), stack(log_probs, torch.float32)
+        rewards, dones, values = stack(rewards, torch.float32), stack(dones, torch.float32), stack(values, torch.float32)
+        next_obs, next_done = stack(next_obs, torch.float32), stack(next_done, torch.float32)
+        T = rewards.shape[0]
+        params = pop.params.data[r:r + 1]
+        with torch.no_grad():
+            _, next_value = spec.forward(params, next_obs.reshape(1, -1, spec.obs_dim))
+            next_value = next_value.reshape(-1)
+            adv = torch.zeros_like(rewards)
+            last = torch.zeros_like(rewards[0])
+            for t in reversed(range(T)):
+                nnt = 1.0 - (next_done if t == T - 1 else dones[t + 1])
+                nv = next_value if t == T - 1 else values[t + 1]
+                delta = rewards[t] + self.gamma * nv * nnt - values[t]
+                adv[t] = last = delta + self.gamma * self.gae_lambda * nnt * last
+            returns = adv + values
+        obs_f = obs.reshape(-1, spec.obs_dim)
+        act_f, lp_f, adv_f = actions.reshape(-1), log_probs.reshape(-1), adv.reshape(-1)
+        ret_f, val_f = returns.reshape(-1), values.reshape(-1)
+        n = obs_f.shape[0]
+        idxs = np.arange(n)
+        opt = pop.opt
+        active = torch.zeros(pop.P, dtype=torch.uint8, device=self.device)
+        active[r] = 1
+        mean_loss, approx_kl = 0.0, None
+        clip, vf, ent = self.clip_coef, self.vf_coef, float(self.ent_coef)
+        for _ in range(int(self.update_epochs)):
+            np.random.shuffle(idxs)
+            for start in range(0, n, int(self.batch_size)):
+                mb = idxs[start:start + int(self.batch_size)]
+                if len(mb) <= 1:
+                    continue
+                sel = torch.as_tensor(mb, device=self.device)
+                w = pop.params.data[r:r + 1].detach().clone().requires_grad_(True)
+                logits, value = spec.forward(w, obs_f[sel].unsqueeze(0))
+                logp_all, entropy = categorical(logits[0])
+                logp = logp_all.gather(-1, act_f[sel].unsqueeze(-1)).squeeze(-1)
+                logratio = logp - lp_f[sel]
+                ratio = logratio.exp()
+                with torch.no_grad():
+                    approx_kl = ((ratio - 1) - logratio).mean()
+                a = adv_f[sel]
+                a = (a - a.mean()) / (a.std() + 1e-8)
+                pg_loss = torch.max(-a * ratio, -a * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+                v = value[0].view(-1)
+                v_clipped = val_f[sel] + torch.clamp(v - val_f[sel], -clip, clip)
+                v_loss = 0.5 * torch.max((v - ret_f[sel]) ** 2, (v_clipped - ret_f[sel]) ** 2).mean()
+                loss = pg_loss - ent * entropy.mean() + v_loss * vf
+                loss.backward()
+                opt.grads[r].copy_(w.grad[0])
+                opt.step(active)
+                mean_loss += loss.item()
+            if self.target_kl is not None and approx_kl is not None and approx_kl > self.target_kl:
+                break
+        return mean_loss / (n * int(self.update_epochs))
 
     @torch.no_grad()
     def test(self, env, swap_channels: bool = False, max_steps: int | None = None, loop: int = 3,

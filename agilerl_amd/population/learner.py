@@ -32,7 +32,7 @@ def net_descriptor(spec: ActorCriticSpec) -> AgxPPONet | None:
     """The fused-kernel descriptor, or None when the architecture is outside
     what agx_ppo_learn covers (then the torch learner runs)."""
     if (len(spec.actor) != 2 or len(spec.critic) != 2 or not spec.layer_norm
-            or not 2 <= len(spec.encoder) <= 3):
+            or not 2 <= len(spec.encoder) <= 3 or not getattr(spec, "share_encoders", True)):
         return None
     d = AgxPPONet()
     d.obs_dim, d.n_actions, d.n_enc = spec.obs_dim, spec.n_actions, len(spec.encoder)

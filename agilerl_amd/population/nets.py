@@ -66,25 +66,34 @@ class ActorCriticSpec:
     actor_limits: tuple = (1, 3, 32, 500)
     critic_limits: tuple = (1, 3, 32, 500)
     latent_limits: tuple = (8, 128)
+    # share_encoders=False (ppo.py:292-320): the critic has its own encoder
+    # ("critic_encoder", the actor's is then "actor_encoder"), laid out after
+    # the actor head in the reference's state-dict order
+    share_encoders: bool = True
+    critic_encoder_name: str = "critic_encoder"
 
     def shape_key(self) -> tuple:
         """Agents with equal keys share a network layout (population groups)."""
         return (self.obs_dim, self.n_actions, tuple(self.encoder_hidden), self.latent_dim, tuple(self.actor_hidden),
                 tuple(self.critic_hidden), self.layer_norm, self.encoder_name, tuple(self.encoder_limits),
-                tuple(self.actor_limits), tuple(self.critic_limits), tuple(self.latent_limits))
+                tuple(self.actor_limits), tuple(self.critic_limits), tuple(self.latent_limits), self.share_encoders,
+                self.critic_encoder_name)
 
     def __post_init__(self) -> None:
         ln = "affine" if self.layer_norm else None
         enc = [self.obs_dim, *self.encoder_hidden]
-        e = self.encoder_name
-        self.encoder = [Layer(f"{e}_linear_layer_{i}", enc[i - 1], enc[i], ln, True)
-                        for i in range(1, len(enc))]
-        self.encoder.append(Layer(f"{e}_linear_layer_output", enc[-1], self.latent_dim,
-                                  "plain" if self.layer_norm else None, True))
+        def encoder(e):
+            layers = [Layer(f"{e}_linear_layer_{i}", enc[i - 1], enc[i], ln, True) for i in range(1, len(enc))]
+            layers.append(Layer(f"{e}_linear_layer_output", enc[-1], self.latent_dim,
+                                "plain" if self.layer_norm else None, True))
+            return layers
+
+        self.encoder = encoder(self.encoder_name)
+        self.critic_encoder = [] if self.share_encoders else encoder(self.critic_encoder_name)
         self.actor = self._head("actor", self.actor_hidden, self.n_actions, ln)
         self.critic = self._head("value", self.critic_hidden, 1, ln)  # ValueNetwork head name (value_networks.py:96)
         off = 0
-        for lay in self.encoder + self.actor + self.critic:
+        for lay in self.encoder + self.actor + self.critic_encoder + self.critic:
             lay.w = off
             off += lay.fin * lay.fout
             lay.b = off
@@ -108,7 +117,12 @@ class ActorCriticSpec:
 
     @property
     def layers(self) -> list[Layer]:
-        return self.encoder + self.actor + self.critic
+        return self.encoder + self.actor + self.critic_encoder + self.critic
+
+    def aliased(self, key: str) -> bool:
+        """A state-dict key whose tensor is another key's (the shared
+        encoder's critic copy)."""
+        return self.share_encoders and key.startswith("critic.encoder.")
 
     # ------------------------------------------------------------------ #
     def init_params(self, P: int, seeds: list[int] | None = None, device="cpu") -> torch.Tensor:
@@ -157,7 +171,8 @@ class ActorCriticSpec:
         """obs [P, B, obs_dim] -> (logits [P, B, A], value [P, B])."""
         lat = self._run(flat, obs, self.encoder)
         logits = self._run(flat, lat, self.actor)
-        value = self._run(flat, lat, self.critic).squeeze(-1)
+        lat_c = lat if self.share_encoders else self._run(flat, obs, self.critic_encoder)
+        value = self._run(flat, lat_c, self.critic).squeeze(-1)
         return logits, value
 
     def state_dict_keys(self) -> dict[str, tuple[int, tuple[int, ...]]]:
@@ -169,7 +184,8 @@ class ActorCriticSpec:
         # (networks/actors.py:330-336, modules/base.py:740-760): its
         # parameters sit under head_net._wrapped in the reference's state dict
         for net, layers in (("actor.encoder.model", self.encoder), ("actor.head_net._wrapped.model", self.actor),
-                            ("critic.encoder.model", self.encoder), ("critic.head_net.model", self.critic)):
+                            ("critic.encoder.model", self.encoder if self.share_encoders else self.critic_encoder),
+                            ("critic.head_net.model", self.critic)):
             for lay in layers:
                 out[f"{net}.{lay.name}.weight"] = (lay.w, (lay.fout, lay.fin))
                 out[f"{net}.{lay.name}.bias"] = (lay.b, (lay.fout,))

@@ -55,7 +55,8 @@ def create_population(algo: str, net_config: dict[str, Any] | None, INIT_HP: dic
                   update_epochs=INIT_HP.get("UPDATE_EPOCHS", 4))
         if INIT_HP.get("RECURRENT", False):
             raise NotImplementedError("recurrent PPO is outside the agx hot path")
-        spec = spec_from_net_config(observation_space, action_space, net_config)
+        spec = spec_from_net_config(observation_space, action_space, net_config,
+                                    share_encoders=bool(algo_kwargs.get("share_encoders", True)))
         G = population_size if shard and world > 1 else P
         pop = PPOPopulation(spec, P, num_envs, seeds=list(range(lo, lo + P)), device=torch.device(device),
                             agent_offset=lo, global_pop_size=G, seed_base=0, **hp)

@@ -435,3 +435,105 @@ def test_agent_rollout_buffer_writes_the_agent_rows():
     # last step: done_{t+1} = 1 -> advantage = r - V = 1 - 1 = 0 exactly
     assert np.array_equal(pop.advantages[0, 1].cpu().numpy(), np.zeros(4, np.float32))
     assert np.isfinite(agent.learn())
+
+
+def test_ppo_learn_from_experiences_matches_torch_restatement():
+    """PPO.learn(experiences) — the reference's deprecated path (ppo.py:
+    655-812): GAE with next_non_terminal = 1 - dones[t+1], per-minibatch
+    advantage normalisation, two clip groups, Adam — against the same
+    algorithm on the oracle's plain-PyTorch ActorCritic (CPU, fp32)."""
+    from torch.nn.utils import clip_grad_norm_
+
+    from agilerl_amd.algorithms import PPO
+    from oracle.ppo_learn import ActorCritic
+
+    obs_space, act_space = _spaces(8, 4)
+    net = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}, "latent_dim": 64}
+    agent = PPO(obs_space, act_space, net_config=net, batch_size=16, lr=1e-3, update_epochs=2, num_envs=4,
+                learn_step=32)
+    ref = ActorCritic(8, 4, [64], 64, [64], [64])
+    ref.load_reference({k: v.cpu().numpy() for k, v in agent.state_dict().items()})
+    rng = np.random.default_rng(4)
+    T, N = 8, 4
+    exp = ([rng.standard_normal((N, 8)).astype(np.float32) for _ in range(T)],
+           [rng.integers(0, 4, N) for _ in range(T)],
+           [(-rng.random(N) - 0.5).astype(np.float32) for _ in range(T)],
+           [rng.standard_normal(N).astype(np.float32) for _ in range(T)],
+           [(rng.random(N) < 0.2).astype(np.float32) for _ in range(T)],
+           [rng.standard_normal(N).astype(np.float32) for _ in range(T)],
+           rng.standard_normal((N, 8)).astype(np.float32), (rng.random(N) < 0.2).astype(np.float32))
+    np.random.seed(9)
+    loss = agent.learn(exp)
+    # the restatement
+    obs, act, lp, rew, dn, val = (torch.as_tensor(np.stack(x)) for x in exp[:6])
+    nobs, ndone = torch.as_tensor(exp[6]), torch.as_tensor(exp[7])
+    with torch.no_grad():
+        _, _, nv = ref.evaluate(nobs, torch.zeros(N, dtype=torch.long))
+        adv, last = torch.zeros_like(rew), torch.zeros(N)
+        for t in reversed(range(T)):
+            nnt = 1.0 - (ndone if t == T - 1 else dn[t + 1])
+            nval = nv if t == T - 1 else val[t + 1]
+            delta = rew[t] + 0.99 * nval * nnt - val[t]
+            adv[t] = last = delta + 0.99 * 0.95 * nnt * last
+        ret = adv + val
+    o, a, l_, ad, rt, v0 = (x.reshape(T * N, *x.shape[2:]) for x in (obs, act, lp, adv, ret, val))
+    names, params = zip(*ref.named_reference_params())
+    opt = torch.optim.Adam(list(params), lr=1e-3)
+    actor_p = list(ref.encoder.parameters()) + list(ref.actor_head.parameters())
+    critic_p = list(ref.critic_head.parameters())
+    np.random.seed(9)
+    idxs, total = np.arange(T * N), 0.0
+    for _ in range(2):
+        np.random.shuffle(idxs)
+        for s0 in range(0, T * N, 16):
+            mb = torch.as_tensor(idxs[s0:s0 + 16])
+            logp, ent, value = ref.evaluate(o[mb], a[mb])
+            lr_ = logp - l_[mb]
+            ratio = lr_.exp()
+            m = (ad[mb] - ad[mb].mean()) / (ad[mb].std() + 1e-8)
+            pg = torch.max(-m * ratio, -m * torch.clamp(ratio, 0.8, 1.2)).mean()
+            vc = v0[mb] + torch.clamp(value - v0[mb], -0.2, 0.2)
+            vl = 0.5 * torch.max((value - rt[mb]) ** 2, (vc - rt[mb]) ** 2).mean()
+            lo = pg - 0.01 * ent.mean() + vl * 0.5
+            opt.zero_grad()
+            lo.backward()
+            clip_grad_norm_(actor_p, 0.5)
+            clip_grad_norm_(critic_p, 0.5)
+            opt.step()
+            total += lo.item()
+    want = total / (T * N * 2)
+    assert abs(loss - want) <= 1e-4 * abs(want) + 1e-7, (loss, want)
+    got = agent.state_dict()
+    for k, w in ref.reference_state().items():
+        torch.testing.assert_close(got[k].cpu(), w, rtol=1e-4, atol=5e-5, msg=lambda m: f"{k}: {m}")
+
+
+def test_ppo_unshared_encoders():
+    """share_encoders=False (ppo.py:292-320): actor_encoder / critic_encoder
+    with their own parameters (reference key names); the torch learner
+    trains both; with vf_coef = 0 the critic's encoder and head get no
+    gradient and stay bit-identical while the actor's move."""
+    from agilerl_amd.algorithms import PPO
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.rollouts import collect_rollouts
+
+    obs_space, act_space = _spaces()
+    net = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}, "latent_dim": 64}
+    for vf in (0.5, 0.0):
+        agent = PPO(obs_space, act_space, net_config=net, share_encoders=False, num_envs=8, learn_step=64,
+                    batch_size=32, vf_coef=vf, update_epochs=2)
+        sd0 = {k: v.clone() for k, v in agent.state_dict().items()}
+        assert "actor.encoder.model.actor_encoder_linear_layer_1.weight" in sd0
+        assert "critic.encoder.model.critic_encoder_linear_layer_1.weight" in sd0
+        assert agent.population.fused_descriptor() is None and not agent.can_mutate_architecture
+        env = SyntheticVecEnv(8, seed=1)
+        collect_rollouts(agent, env)
+        loss = agent.learn()
+        assert np.isfinite(loss)
+        sd1 = agent.state_dict()
+        moved = {k: not torch.equal(sd0[k], sd1[k]) for k in sd0}
+        assert moved["actor.encoder.model.actor_encoder_linear_layer_1.weight"]
+        if vf == 0.0:
+            assert not any(v for k, v in moved.items() if k.startswith("critic.")), moved
+        else:
+            assert moved["critic.encoder.model.critic_encoder_linear_layer_1.weight"]
