@@ -1,4 +1,4 @@
-"""Population-batched Rainbow learner: one launch chain for all P agents.
+"""Population-batched Rainbow / DQN learner: one launch chain for all P agents.
 
 The reference learns agent after agent (train_off_policy.py:249 ->
 RainbowDQN.learn, dqn_rainbow.py:369-490): per agent a forward of the online
@@ -26,6 +26,8 @@ One ``learn`` over P agents' batches is then:
     norm, lr and step count) and one Polyak launch over ``[P, n]``;
   * the agents' noise resets in agent order (the reference's torch draws).
 
+DQN agents (dqn.py:274-348) take the same chain with their Q head, the
+TD target + MSE (agx_td_target, per agent) and Adam without clipping.
 Agents whose hyperparameters differ in a way the batched chain does not
 carry (batch size, gamma, tau, n-step / combined-reward settings) are
 learned in groups of equal settings.
@@ -80,7 +82,8 @@ def _module_ops(net: nn.Module) -> list[tuple[str, nn.Module]]:
 
 
 class RainbowPopulationLearner:
-    """Batched learner over ``agents`` (RainbowDQN objects of one architecture).
+    """Batched learner over ``agents`` (RainbowDQN or DQN objects of one
+    architecture).
 
     Construction moves every agent's online / target parameters, noise
     buffers and Adam state into rows of flat device buffers and leaves the
@@ -99,6 +102,9 @@ class RainbowPopulationLearner:
         if a0.device.type != "cuda":
             raise NotImplementedError("population learner runs on the GPU")
         self.agents = list(agents)
+        self.rainbow = hasattr(a0, "num_atoms")
+        if any(hasattr(a, "num_atoms") != self.rainbow for a in agents):
+            raise ValueError("population learner: one algorithm per population")
         self.P = P = len(agents)
         self.device = a0.device
         pnames = [(k, p.shape) for k, p in a0.actor.named_parameters()]
@@ -212,6 +218,8 @@ class RainbowPopulationLearner:
         lat = self._seq(x, _module_ops(net), params, rows, noise)
         head = net.head_net
         v = self._seq(lat, [(f"head_net.model.{k}", m) for k, m in head.model.named_children()], params, rows, noise)
+        if not self.rainbow:  # QNetwork: the "value" head is Q [P, B, A]
+            return v
         a = self._seq(lat, [(f"head_net.advantage_net.{k}", m) for k, m in head.advantage_net.named_children()],
                       params, rows, noise)
         return v.reshape(P * B, -1), a.reshape(P * B, -1)
@@ -221,6 +229,20 @@ class RainbowPopulationLearner:
         return bool(getattr(net, "flatten_obs", False))
 
     # ------------------------------------------------------------------ #
+    def _td_losses(self, obs, acts, rew, done, next_obs, gamma):
+        """DQN: per-agent TD target + MSE (dqn.py:274-324) -> loss [P]."""
+        from .dqn import _TDLoss
+
+        a0 = self.agents[0]
+        with torch.no_grad():
+            q_next_t = self._head_streams(a0.actor_target, next_obs, None, self.tgt, self.tnoise)
+            q_next_o = self._head_streams(a0.actor, next_obs, None, self.prm, self.noise) if a0.double else None
+        q_cur = self._head_streams(a0.actor, obs, self.leaf, self.prm, self.noise)
+        return torch.stack([_TDLoss.apply(q_cur[p], q_next_t[p].contiguous(),
+                                          q_next_o[p].contiguous() if q_next_o is not None else None,
+                                          acts[p].contiguous(), rew[p].contiguous(), done[p].contiguous(),
+                                          float(gamma), bool(a0.double)) for p in range(self.P)])
+
     def _loss(self, obs, acts, rew, done, next_obs, gamma):
         """Elementwise C51 loss [P, B] of every agent (dqn_rainbow.py:313-367)."""
         from ..networks.q_networks import DuelingHeadFn, DuelingRowsFn
@@ -254,11 +276,41 @@ class RainbowPopulationLearner:
                 xs.append(t.to(self.device))
         return torch.stack(xs)
 
+    def _adam(self, max_norm: float) -> None:
+        """One agx_clip_adam launch over [P, n]: per-agent norm clip (max_norm
+        <= 0: none), per-agent lr and step count."""
+        lr = torch.tensor([float(a.lr) for a in self.agents], dtype=torch.float32).to(self.device)
+        K._lib.call("agx_clip_adam", self.prm.data.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(),
+                    self.v.data_ptr(), self.P, self.prm.n, self.offsets.data_ptr(), 1, float(max_norm),
+                    lr.data_ptr(), 0.9, 0.999, 1e-8, self.steps.data_ptr(), None, self.workspace.data_ptr(),
+                    K._lib.stream())
+
+    def _learn_dqn(self, experiences: list) -> list:
+        """DQN.learn per agent (dqn.py:326-348): TD loss, Adam (no clipping),
+        Polyak -> [loss] per agent."""
+        a0 = self.agents[0]
+        for a in self.agents[1:]:
+            for attr in ("gamma", "tau", "double"):
+                if getattr(a, attr) != getattr(a0, attr):
+                    raise NotImplementedError(f"population learner: agents differ in {attr}")
+        obs, next_obs = self._stack(experiences, "obs", True), self._stack(experiences, "next_obs", True)
+        acts = self._stack(experiences, "action").reshape(self.P, -1).long()
+        rew = self._stack(experiences, "reward").reshape(self.P, -1).float()
+        done = self._stack(experiences, "done").reshape(self.P, -1).float()
+        self.grad.zero_()
+        loss = self._td_losses(obs, acts, rew, done, next_obs, a0.gamma)
+        loss.sum().backward()
+        self._adam(0.0)
+        K.polyak_(self.tgt.data.view(-1), self.prm.data.view(-1), float(a0.tau))
+        return [float(x) for x in loss.detach().cpu().tolist()]
+
     def learn(self, experiences: list, n_experiences: list | None = None, per: bool = False) -> list:
         """-> [(loss, idxs, new_priorities)] per agent, as ``agent.learn``."""
         a0 = self.agents[0]
         if len(experiences) != self.P:
             raise ValueError(f"need one experience batch per agent ({self.P})")
+        if not self.rainbow:
+            return self._learn_dqn(experiences)
         for a in self.agents[1:]:
             for attr in ("gamma", "tau", "n_step", "combined_reward", "v_min", "v_max", "num_atoms", "prior_eps"):
                 if getattr(a, attr) != getattr(a0, attr):
@@ -286,10 +338,7 @@ class RainbowPopulationLearner:
         else:
             loss = el.mean(1)
         loss.sum().backward()
-        lr = torch.tensor([float(a.lr) for a in self.agents], dtype=torch.float32).to(self.device)
-        K._lib.call("agx_clip_adam", self.prm.data.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(),
-                    self.v.data_ptr(), self.P, self.prm.n, self.offsets.data_ptr(), 1, 10.0, lr.data_ptr(), 0.9,
-                    0.999, 1e-8, self.steps.data_ptr(), None, self.workspace.data_ptr(), K._lib.stream())
+        self._adam(10.0)
         K.polyak_(self.tgt.data.view(-1), self.prm.data.view(-1), float(a0.tau))
         for a in self.agents:  # the reference's per-agent noise draws, in agent order
             a.actor.reset_noise()

@@ -24,7 +24,6 @@ def collect_rollouts(agent, env, n_steps: int | None = None, last_obs=None, last
     runner.reset_episode_stats()
     runner.collect()
     pop.finish_rollout(runner.last_obs, runner.last_done, runner.last_value if runner.last_value_valid else None)
-    agent.steps[-1] += pop.T * pop.N
     s = float(runner.episode_return_sum[agent.row].item())
     c = int(runner.episodes[agent.row].item())
     scores = [s / c] * c if c else []
