@@ -902,48 +902,68 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 fw.trunk();
                 AGX_STAMP(stb + 2);
 
-                // ---- P4: ONE row pass over the head (16 lanes per row, nothing leaves
+                // ---- P4: ONE row pass over the head (W lanes per row, nothing leaves
                 // the row's registers): LayerNorm(+affine)+ReLU forward, the output
                 // layers (logits, value), the loss and d(logits) / d(value), and the
                 // LayerNorm backward to dZ_h (S2) with the bias / LN-affine column sums.
                 // y_h goes to S1 and d(logits) / d(value) to LDS for the output-layer dW.
+                // 16-row sub-batches use 32 lanes per row (2 rows per wave, every lane
+                // busy, half the per-lane columns: the pass is VALU-issue bound); the
+                // row sums then add the other 16-lane half by ds_swizzle (lane ^ 16).
                 {
-                    AGX_IDS;
-                    constexpr int F = pl.H, split = pl.ha, NC = F / 16, NA = pl.A;
+                    constexpr int W = (SB == 16 && pl.H % 32 == 0 && pl.ha % 32 == 0) ? 32 : 16;
+                    const int lane = vlane(), wave = swave();
+                    const int sub = lane & (W - 1);
+                    const int r = W == 32 ? wave * 2 + (lane >> 5) : wave + kNW * (lane >> 4);
+                    constexpr int F = pl.H, split = pl.ha, NC = F / W, NA = pl.A;
                     constexpr int F0 = split, F1 = F - split;
-                    const int r = rrow, a = sub;
-                    // rows beyond the sub-batch (SB = 16: lanes 32-63) compute on zeros
-                    // and contribute exact zeros to the column reductions
-                    const bool rl = SB == kSB || r < SB;
+                    const int a = sub;
+                    auto swz16 = [](float v) {
+                        return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401f));
+                    };
+                    auto rsum = [&](float v) {
+                        v = row_sum(v);
+                        if constexpr (W == 32) v += swz16(v);
+                        return v;
+                    };
+                    auto rmax = [&](float v) {
+                        v = row_max(v);
+                        if constexpr (W == 32) v = fmaxf(v, swz16(v));
+                        return v;
+                    };
+                    // rows beyond the sub-batch (16-lane rows of a 16-row sub-batch:
+                    // lanes 32-63) compute on zeros and contribute exact zeros to the
+                    // column reductions
+                    const bool rl = W == 32 || SB == kSB || r < SB;
                     const bool live = rl && r < nrow;
                     float z[NC], xh[NC];
                     float s0 = 0.f, s1 = 0.f;
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
-                        z[i] = rl ? sm[pl.l_s2 + r * pl.ld_s + sub + 16 * i] : 0.f;
-                        if (16 * i < split) s0 += z[i];
+                        z[i] = rl ? sm[pl.l_s2 + r * pl.ld_s + sub + W * i] : 0.f;
+                        if (W * i < split) s0 += z[i];
                         else s1 += z[i];
                     }
-                    const float m0 = row_sum(s0) * (1.f / (float)F0);
-                    const float m1 = row_sum(s1) * (1.f / (float)F1);
+                    const float m0 = rsum(s0) * (1.f / (float)F0);
+                    const float m1 = rsum(s1) * (1.f / (float)F1);
                     float v0 = 0.f, v1 = 0.f;
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
-                        if (16 * i < split) v0 += (z[i] - m0) * (z[i] - m0);
+                        if (W * i < split) v0 += (z[i] - m0) * (z[i] - m0);
                         else v1 += (z[i] - m1) * (z[i] - m1);
                     }
-                    const float r0 = 1.f / sqrtf(row_sum(v0) / (float)F0 + 1e-5f);
-                    const float r1 = 1.f / sqrtf(row_sum(v1) / (float)F1 + 1e-5f);
+                    const float r0 = 1.f / sqrtf(rsum(v0) / (float)F0 + 1e-5f);
+                    const float r1 = 1.f / sqrtf(rsum(v1) / (float)F1 + 1e-5f);
                     float pa[NA], pv = 0.f;
 #pragma unroll
                     for (int k = 0; k < NA; ++k) pa[k] = 0.f;
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
-                        const int j = sub + 16 * i;
-                        xh[i] = 16 * i < split ? (z[i] - m0) * r0 : (z[i] - m1) * r1;
+                        const int j = sub + W * i;
+                        xh[i] = W * i < split ? (z[i] - m0) * r0 : (z[i] - m1) * r1;
                         const float y = relu(xh[i] * sm[pl.l_hg + j] + sm[pl.l_hbe + j]);
                         if (rl) sm[pl.l_s1 + r * pl.ld_s + j] = y;
-                        if (16 * i < split) {
+                        if (W * i < split) {
 #pragma unroll
                             for (int k = 0; k < NA; ++k) pa[k] += y * sm[pl.l_aow + k * pl.l_aold + j];
                         } else {
@@ -953,22 +973,22 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     float mine = 0.f;
 #pragma unroll
                     for (int k = 0; k < NA; ++k) {
-                        const float t = row_sum(pa[k]);
+                        const float t = rsum(pa[k]);
                         mine = sub == k ? t : mine;
                     }
-                    const float v = row_sum(pv) + sm[pl.l_cob];
+                    const float v = rsum(pv) + sm[pl.l_cob];
                     // loss + d(logits), d(value) (ppo.py:876-908); illegal actions:
                     // logits -> -1e8 (apply_action_mask_discrete, distributions.py:16-28)
                     const bool ok_a = (legal[r] >> a) & 1u;
                     const float lg = a < NA ? (ok_a ? mine + sm[pl.l_aob + sub] : -1.0e8f) : -3.0e38f;
-                    const float mx = row_max(lg);
+                    const float mx = rmax(lg);
                     const float ex = a < NA ? expf(lg - mx) : 0.f;
-                    const float lse = mx + logf(row_sum(ex));
+                    const float lse = mx + logf(rsum(ex));
                     const float pa_ = a < NA ? expf(lg - lse) : 0.f;
                     const float lpe = logf(pa_ + 1e-8f);
-                    const float Hs = -row_sum(a < NA ? pa_ * lpe : 0.f);  // H = -sum p log(p+1e-8)
+                    const float Hs = -rsum(a < NA ? pa_ * lpe : 0.f);  // H = -sum p log(p+1e-8)
                     const float gh = -(lpe + pa_ / (pa_ + 1e-8f));          // dH/dp_a
-                    const float pg_dot = row_sum(a < NA ? pa_ * gh : 0.f);
+                    const float pg_dot = rsum(a < NA ? pa_ * gh : 0.f);
                     const int a_t = acts[r];
                     const float logp = __builtin_bit_cast(
                                            float, __builtin_amdgcn_ds_bpermute((lane - sub + a_t) * 4,
@@ -1014,9 +1034,9 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     float a1 = 0.f, a2 = 0.f, c1 = 0.f, c2 = 0.f;
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
-                        const int j = sub + 16 * i;
+                        const int j = sub + W * i;
                         float dy;
-                        if (16 * i < split) {
+                        if (W * i < split) {
                             dy = 0.f;
 #pragma unroll
                             for (int k = 0; k < NA; ++k) dy += dla[k] * sm[pl.l_aow + k * pl.l_aold + j];
@@ -1028,7 +1048,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         const float y = xh[i] * gam + sm[pl.l_hbe + j];
                         dyp[i] = y > 0.f ? dy : 0.f;
                         dxh[i] = dyp[i] * gam;
-                        if (16 * i < split) {
+                        if (W * i < split) {
                             a1 += dxh[i];
                             a2 += dxh[i] * xh[i];
                         } else {
@@ -1037,27 +1057,27 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         }
                     }
                     const float rs0 = rl ? r0 : 0.f, rs1 = rl ? r1 : 0.f;
-                    const float ma1 = row_sum(a1) * (1.f / (float)F0), ma2 = row_sum(a2) * (1.f / (float)F0);
-                    const float mc1 = row_sum(c1) * (1.f / (float)F1), mc2 = row_sum(c2) * (1.f / (float)F1);
+                    const float ma1 = rsum(a1) * (1.f / (float)F0), ma2 = rsum(a2) * (1.f / (float)F0);
+                    const float mc1 = rsum(c1) * (1.f / (float)F1), mc2 = rsum(c2) * (1.f / (float)F1);
                     float *rd = sm + pl.l_red + pl.red_h;
                     float cs[3][NC];
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
-                        const int j = sub + 16 * i;
-                        const bool g0 = 16 * i < split;
+                        const int j = sub + W * i;
+                        const bool g0 = W * i < split;
                         const float dz = (g0 ? rs0 : rs1) * (dxh[i] - (g0 ? ma1 : mc1) - xh[i] * (g0 ? ma2 : mc2));
                         if (rl) sm[pl.l_s2 + r * pl.ld_s + j] = dz;
                         cs[0][i] = rl ? dz : 0.f;
                         cs[1][i] = dyp[i] * xh[i];
                         cs[2][i] = dyp[i];
                     }
+                    if constexpr (W == 16) {  // the two rows of a 32-lane group
 #pragma unroll
-                    for (int k = 0; k < 3; ++k)
+                        for (int k = 0; k < 3; ++k)
 #pragma unroll
-                        for (int i = 0; i < NC; ++i)
-                            cs[k][i] += __builtin_bit_cast(
-                                float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, cs[k][i]), 0x401f));  // lane ^ 16
-                    if constexpr (SB > 16) {
+                            for (int i = 0; i < NC; ++i) cs[k][i] += swz16(cs[k][i]);  // lane ^ 16
+                    }
+                    if constexpr (W == 32 || SB > 16) {  // rows in lanes 32-63 too
 #pragma unroll
                         for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -1065,14 +1085,14 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                 cs[k][i] += __builtin_bit_cast(
                                     float, __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, __builtin_bit_cast(int, cs[k][i])));
                     }
-                    if (lane < 16) {
+                    if (lane < W) {
 #pragma unroll
                         for (int k = 0; k < 3; ++k) {
                             float o[NC];
 #pragma unroll
-                            for (int i = 0; i < NC; ++i) o[i] = rd[(k * kNW + wave) * F + sub + 16 * i];
+                            for (int i = 0; i < NC; ++i) o[i] = rd[(k * kNW + wave) * F + sub + W * i];
 #pragma unroll
-                            for (int i = 0; i < NC; ++i) rd[(k * kNW + wave) * F + sub + 16 * i] = o[i] + cs[k][i];
+                            for (int i = 0; i < NC; ++i) rd[(k * kNW + wave) * F + sub + W * i] = o[i] + cs[k][i];
                         }
                     }
                 }

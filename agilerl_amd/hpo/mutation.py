@@ -28,10 +28,16 @@ What runs, with the reference's draws from the reference's generators:
 * ``learn_step`` as an RL hyperparameter: the agent's rollout length, applied
   by the engine at the next generation (agents grouped by learn_step).
 
-Not applied: activation mutations of PPO / MADDPG (the reference itself
-skips them for policy-gradient algorithms, :469-479) and architecture /
-activation mutations of DQN / Rainbow / MADDPG agents (recorded as no
-mutation with a warning).
+* ``activation_mutation`` (:457-513, _permutate_activation :710-731) on DQN /
+  Rainbow agents: the new activation drawn with ``self.rng`` from
+  ``activation_selection`` minus the current one, every evolvable module of
+  the Q network recreated with it (the encoder's output activation too), the
+  target network re-made from the mutated network (reinit_shared_networks,
+  :104-160) and fresh optimizers.  Policy-gradient algorithms (PPO, MADDPG)
+  keep their activations, as the reference's :469-479.
+
+Not applied: architecture mutations of DQN / Rainbow / MADDPG agents
+(recorded as no mutation with a warning).
 """
 
 from __future__ import annotations
@@ -138,7 +144,27 @@ class Mutations:
             warnings.warn(f"Activation mutations are not supported for {individual.algo}.", stacklevel=2)
             individual.mut = "None"
             return individual
-        return self._not_applied(individual, "activation")
+        net = getattr(individual, "actor", None)
+        if net is None or not hasattr(net, "change_activation"):
+            return self._not_applied(individual, "activation")
+        if net.activation is None:  # :489-499
+            warnings.warn("Found no activation mutation capabilities. We advise setting the probability to "
+                          "0.0 to disable activation mutations.", stacklevel=2)
+            individual.mut = "None"
+            return individual
+        options = list(self.activation_selection)  # _permutate_activation (:710-731)
+        if len(options) > 1 and net.activation in options:
+            options.remove(net.activation)
+        net.change_activation(str(self.rng.choice(options, size=1)[0]), output=False)
+        individual.reinit_optimizers()
+        individual.mut = "act"
+        # reinit_shared_networks (:104-160): the target network re-made from the
+        # mutated evaluation network (its modules and weights)
+        if hasattr(individual, "actor_target"):
+            import copy
+
+            individual.actor_target = copy.deepcopy(individual.actor)
+        return individual
 
     def rl_hyperparam_mutation(self, individual):
         """mutation.py:413-453."""

@@ -245,6 +245,32 @@ class EvolvableCNN(nn.Module):
     def clear_image_norm(self) -> None:
         getattr(self.model, f"{self.name}_conv_layer_1").image_norm = None
 
+    def change_activation(self, activation: str, output: bool = False) -> None:
+        """modules/cnn.py:473-485: a new activation (and output activation
+        when ``output``), the network recreated with its parameters kept."""
+        if output:
+            self.output_activation = activation
+        self.activation = activation
+        self.recreate_network()
+
+    def recreate_network(self) -> None:
+        """Rebuild ``model`` from the current hyperparameters; parameters of
+        equal name and shape are kept (preserve_parameters), as is the uint8
+        normalisation of the first convolution."""
+        from .mlp import preserve_parameters
+
+        first = getattr(self.model, f"{self.name}_conv_layer_1")
+        norm = first.image_norm
+        dev = first.weight.device
+        net = create_cnn(self.input_shape[0], self.channel_size, self.kernel_size, self.stride_size, self.name,
+                         self.init_layers, self.layer_norm, self.activation, dev)
+        c, h, w = self.cnn_output_size[1:]
+        net[f"{self.name}_flatten"] = nn.Flatten()
+        net[f"{self.name}_linear_output"] = nn.Linear(c * h * w, self.num_outputs, device=dev)
+        net[f"{self.name}_output_activation"] = get_activation(self.output_activation)
+        self.model = preserve_parameters(self.model, nn.Sequential(net))
+        getattr(self.model, f"{self.name}_conv_layer_1").image_norm = norm
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not isinstance(x, torch.Tensor):
             x = torch.as_tensor(x, dtype=torch.float32, device=self.model[0].weight.device)

@@ -152,6 +152,19 @@ class EvolvableNetwork(nn.Module):
                            name=self.encoder_name, **cfg)
         self.encoder = preserve_parameters(self.encoder, new)
 
+    @property
+    def activation(self) -> str | None:
+        """networks/base.py:298-305: the encoder's activation."""
+        return getattr(self.encoder, "activation", None)
+
+    def change_activation(self, activation: str, output: bool = False) -> None:
+        """networks/base.py:445-455: every evolvable module of the network
+        takes the activation; the encoder's output activation too."""
+        for name in ("encoder", "head_net"):
+            mod = getattr(self, name, None)
+            if mod is not None and hasattr(mod, "change_activation"):
+                mod.change_activation(activation, output=True if name == "encoder" else output)
+
     def reset_noise(self) -> None:
         from ..modules.custom_components import NoisyLinear
 

@@ -132,3 +132,37 @@ def test_rl_hyperparameter_mutation_reinits_only_the_mutated_optimizer():
         assert any(not torch.equal(before[a][k], v) for k, v in agent.actors[a].state_dict().items()), a
         for k, v in agent.actor_targets[a].state_dict().items():
             assert torch.equal(v, agent.actors[a].state_dict()[k])
+
+
+@pytest.mark.parametrize("algo", ["DQN", "Rainbow DQN"])
+def test_activation_mutation_dqn_family(algo):
+    """mutation.py:457-513 on DQN / Rainbow: a new activation from
+    activation_selection minus the current one (Mutations.rng), every module
+    of the Q network recreated with it (encoder output activation too),
+    parameters kept, the target re-made from the mutated network, fresh Adam."""
+    from torch import nn
+
+    from agilerl_amd.algorithms import DQN, RainbowDQN
+    from agilerl_amd.envs import Box, Discrete
+    from agilerl_amd.hpo.mutation import Mutations
+
+    obs_space, act_space = Box(-np.inf, np.inf, (6,)), Discrete(3)
+    cls = DQN if algo == "DQN" else RainbowDQN
+    agent = cls(obs_space, act_space, device="cpu")
+    before = {k: v.clone() for k, v in agent.actor.state_dict().items() if "epsilon" not in k}
+    mut = Mutations(0, 0, 0, 0, 1.0, 0, rand_seed=3)
+    (agent,) = mut.mutation([agent])
+    assert agent.mut == "act"
+    new = agent.actor.activation
+    assert new in ("ELU", "GELU") and agent.actor.encoder.output_activation == new
+    acts = {type(m).__name__ for m in agent.actor.modules()}
+    assert {"ELU": "ELU", "GELU": "GELU"}[new] in acts and "ReLU" not in acts
+    after = agent.actor.state_dict()
+    assert all(torch.equal(after[k], v) for k, v in before.items())
+    t = agent.actor_target.state_dict()
+    assert all(torch.equal(t[k], v) for k, v in after.items())
+    assert agent.actor_target is not agent.actor
+    assert all(p is q for p, q in zip(agent.optimizer.param_groups[0]["params"], agent.actor.parameters()))
+    x = torch.randn(4, 6)
+    assert agent.actor(x).shape == (4, 3) and agent.actor_target(x).shape == (4, 3)
+    assert not isinstance(agent.actor.encoder.model[1], nn.ReLU)
