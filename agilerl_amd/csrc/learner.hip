@@ -292,6 +292,20 @@ __device__ __forceinline__ float row_max(float v) {
     v = fmaxf(v, dpp<0x140>(v));
     return v;
 }
+// W-lane row sum (W = 16: one DPP row; W = 32: + the other 16-lane half, lane ^ 16)
+template <int W>
+__device__ __forceinline__ float wrow_sum(float v) {
+    v = row_sum(v);
+    if constexpr (W == 32)
+        v += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401f));
+    return v;
+}
+// row slot of this lane: W = 16: wave + 8 * (lane / 16) (4 rows per wave);
+// W = 32: 2 * wave + lane / 32 (2 rows per wave, a 16-row sub-batch fills all lanes)
+template <int W>
+__device__ __forceinline__ int wrow(int lane, int wave) {
+    return W == 32 ? wave * 2 + (lane >> 5) : wave + kNW * (lane >> 4);
+}
 // sum over the 4 row-groups (lanes l, l^16, l^32, l^48) of a wave
 __device__ __forceinline__ float rowgroup_sum(float v) {
     // ds_swizzle bit mode (offset[15] = 0): and_mask 0x1f, xor_mask 0x10 -> lane ^ 16
@@ -434,30 +448,33 @@ struct Fwd {
     // then a DPP row sum — and land in lg / val: no separate output phase.
     template <int F, int split, int xb, int ldx, int rb, int gb, int bb, bool OUT = false>
     __device__ __forceinline__ void ln_rows() {
-        constexpr int NC = F / 16;
+        // 16-row sub-batches: 32 lanes per row (every lane busy, half the columns per lane)
+        constexpr int W = (SB == 16 && !OUT && F % 32 == 0 && split >= F) ? 32 : 16;
+        constexpr int NC = F / W;
         constexpr int F0 = split < F ? split : F, F1 = F - F0;
-        AGX_IDS;
-        const int r = rrow;
-        if (SB < kSB && r >= SB) return;  // whole 16-lane rows beyond the sub-batch idle
+        const int lane = vlane(), wave = swave();
+        const int sub = lane & (W - 1);
+        const int r = wrow<W>(lane, wave);
+        if (W == 16 && SB < kSB && r >= SB) return;  // whole 16-lane rows beyond the sub-batch idle
         float z[NC];
         float s0 = 0.f, s1 = 0.f;
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
-            z[i] = sm[pl.l_s2 + r * pl.ld_s + sub + 16 * i];
-            if (16 * i < split) s0 += z[i];
+            z[i] = sm[pl.l_s2 + r * pl.ld_s + sub + W * i];
+            if (W * i < split) s0 += z[i];
             else s1 += z[i];
         }
-        const float m0 = row_sum(s0) * (1.f / (float)F0);
-        const float m1 = F1 > 0 ? row_sum(s1) * (1.f / (float)(F1 > 0 ? F1 : 1)) : 0.f;
+        const float m0 = wrow_sum<W>(s0) * (1.f / (float)F0);
+        const float m1 = F1 > 0 ? wrow_sum<W>(s1) * (1.f / (float)(F1 > 0 ? F1 : 1)) : 0.f;
         float v0 = 0.f, v1 = 0.f;
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
-            if (16 * i < split) v0 += (z[i] - m0) * (z[i] - m0);
+            if (W * i < split) v0 += (z[i] - m0) * (z[i] - m0);
             else v1 += (z[i] - m1) * (z[i] - m1);
         }
-        const float r0 = 1.f / sqrtf(row_sum(v0) / (float)F0 + 1e-5f);
-        const float r1 = F1 > 0 ? 1.f / sqrtf(row_sum(v1) / (float)(F1 > 0 ? F1 : 1) + 1e-5f) : 0.f;
-        if ((lane & 15) == 0) {
+        const float r0 = 1.f / sqrtf(wrow_sum<W>(v0) / (float)F0 + 1e-5f);
+        const float r1 = F1 > 0 ? 1.f / sqrtf(wrow_sum<W>(v1) / (float)(F1 > 0 ? F1 : 1) + 1e-5f) : 0.f;
+        if ((lane & (W - 1)) == 0) {
             sm[rb + 2 * r] = r0;
             sm[rb + 2 * r + 1] = r1;
         }
@@ -467,13 +484,13 @@ struct Fwd {
         for (int a = 0; a < NA; ++a) pa[a] = 0.f;
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
-            const int j = sub + 16 * i;
-            const float xh = 16 * i < split ? (z[i] - m0) * r0 : (z[i] - m1) * r1;
+            const int j = sub + W * i;
+            const float xh = W * i < split ? (z[i] - m0) * r0 : (z[i] - m1) * r1;
             sm[xb + r * ldx + j] = xh;
             const float y = gb >= 0 ? relu(xh * sm[gb + j] + sm[bb + j]) : relu(xh);
             sm[pl.l_s1 + r * pl.ld_s + j] = y;
             if constexpr (OUT) {
-                if (16 * i < split) {
+                if (W * i < split) {
 #pragma unroll
                     for (int a = 0; a < NA; ++a) pa[a] += y * sm[pl.l_aow + a * pl.l_aold + j];
                 } else {
@@ -1111,18 +1128,22 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     constexpr int rb = decltype(rbc)::value, gb = decltype(gbc)::value, bb = decltype(bbc)::value;
                     constexpr int red = decltype(redc)::value;
                     constexpr bool aff = decltype(affc)::value;
-                    constexpr int NC = F / 16;
-                    AGX_IDS;
-                    const int r = rrow;
-                    // rows beyond the sub-batch (SB = 16: lanes 32-63) hold stale LDS
-                    // data: they contribute exact zeros to the column reductions
-                    const bool rl = SB == kSB || r < SB;
+                    // 16-row sub-batches: 32 lanes per row (as the forward pass)
+                    constexpr int W = (SB == 16 && F % 32 == 0) ? 32 : 16;
+                    constexpr int NC = F / W;
+                    const int lane = vlane(), wave = swave();
+                    const int sub = lane & (W - 1);
+                    const int r = wrow<W>(lane, wave);
+                    // rows beyond the sub-batch (16-lane rows of a 16-row sub-batch:
+                    // lanes 32-63) hold stale LDS data: they contribute exact zeros
+                    // to the column reductions
+                    const bool rl = W == 32 || SB == kSB || r < SB;
                     float xh[NC], dxh[NC], dyp[NC];
                     float a1 = 0.f, a2 = 0.f;
                     const float rs0 = rl ? sm[rb + 2 * r] : 0.f;
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
-                        const int j = sub + 16 * i;
+                        const int j = sub + W * i;
                         const float dy = rl ? sm[dyb + r * ldy + j] : 0.f;
                         xh[i] = rl ? sm[xb + r * ldx + j] : 0.f;
                         const float gam = aff ? sm[gb + j] : 1.f;
@@ -1132,7 +1153,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         a1 += dxh[i];
                         a2 += dxh[i] * xh[i];
                     }
-                    const float ma1 = row_sum(a1) * (1.f / (float)F), ma2 = row_sum(a2) * (1.f / (float)F);
+                    const float ma1 = wrow_sum<W>(a1) * (1.f / (float)F), ma2 = wrow_sum<W>(a2) * (1.f / (float)F);
                     float *rd = sm + pl.l_red + red;
                     // dZ row pass; the column sums (bias, gamma, beta gradients) of the
                     // wave's rows are batched: all cross-row reductions, then all LDS
@@ -1142,7 +1163,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     float cs[NV][NC];
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
-                        const int j = sub + 16 * i;
+                        const int j = sub + W * i;
                         const float dz = rs0 * (dxh[i] - ma1 - xh[i] * ma2);
                         if (rl) sm[pl.l_s2 + r * pl.ld_s + j] = dz;
                         cs[0][i] = rl ? dz : 0.f;
@@ -1151,13 +1172,15 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                             cs[2][i] = dyp[i];
                         }
                     }
+                    if constexpr (W == 16) {  // the two rows of a 32-lane group
 #pragma unroll
-                    for (int k = 0; k < NV; ++k)
+                        for (int k = 0; k < NV; ++k)
 #pragma unroll
-                        for (int i = 0; i < NC; ++i)
-                            cs[k][i] += __builtin_bit_cast(
-                                float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, cs[k][i]), 0x401f));  // lane ^ 16
-                    if constexpr (SB > 16) {  // rows in lanes 32-63 too
+                            for (int i = 0; i < NC; ++i)
+                                cs[k][i] += __builtin_bit_cast(
+                                    float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, cs[k][i]), 0x401f));  // lane ^ 16
+                    }
+                    if constexpr (W == 32 || SB > 16) {  // rows in lanes 32-63 too
 #pragma unroll
                         for (int k = 0; k < NV; ++k)
 #pragma unroll
@@ -1165,14 +1188,14 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                 cs[k][i] += __builtin_bit_cast(
                                     float, __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, __builtin_bit_cast(int, cs[k][i])));
                     }
-                    if (lane < 16) {
+                    if (lane < W) {
 #pragma unroll
                         for (int k = 0; k < NV; ++k) {
                             float o[NC];
 #pragma unroll
-                            for (int i = 0; i < NC; ++i) o[i] = rd[(k * kNW + wave) * F + sub + 16 * i];
+                            for (int i = 0; i < NC; ++i) o[i] = rd[(k * kNW + wave) * F + sub + W * i];
 #pragma unroll
-                            for (int i = 0; i < NC; ++i) rd[(k * kNW + wave) * F + sub + 16 * i] = o[i] + cs[k][i];
+                            for (int i = 0; i < NC; ++i) rd[(k * kNW + wave) * F + sub + W * i] = o[i] + cs[k][i];
                         }
                     }
                 };
