@@ -1213,8 +1213,11 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                             acc[pl.slot0[ga] + j] = mfma_tile<SB>(
                                 acc[pl.slot0[ga] + j], [&](int m, int k) { return sm[pl.l_dlg + k * kMaxA + m]; },
                                 [&](int k, int n) {
+                                    // branch-free: a clamped load (a finite y) scaled to the
+                                    // ones / zero columns (a select would be sunk into a branch)
                                     const int c = i0 + n;
-                                    return c < pl.ha ? sm[pl.l_s1 + k * pl.ld_s + c] : (c == pl.ha ? 1.f : 0.f);
+                                    const float x = sm[pl.l_s1 + k * pl.ld_s + (c < pl.ha ? c : pl.ha - 1)];
+                                    return x * (c < pl.ha ? 1.f : 0.f) + (c == pl.ha ? 1.f : 0.f);
                                 });
                         }
                     }
@@ -1227,7 +1230,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                 acc[pl.slot0[gc] + j], [&](int m, int k) { return sm[pl.l_dvb + k * kMaxA + m]; },
                                 [&](int k, int n) {
                                     const int c = i0 + n;
-                                    return c < pl.hc ? sm[pl.l_s1 + k * pl.ld_s + pl.ha + c] : (c == pl.hc ? 1.f : 0.f);
+                                    const float x = sm[pl.l_s1 + k * pl.ld_s + pl.ha + (c < pl.hc ? c : pl.hc - 1)];
+                                    return x * (c < pl.hc ? 1.f : 0.f) + (c == pl.hc ? 1.f : 0.f);
                                 });
                         }
                     }
