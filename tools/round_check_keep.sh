@@ -1,0 +1,14 @@
+# Round check, then keep only the summaries that go to profiles/ (gpurun copies back <= 64 MiB)
+set -o pipefail
+R=${R:-r3}
+R=$R bash tools/gpu_round_check.sh > gpurun_out/round_check.log 2>&1
+rc=$?
+mkdir -p gpurun_keep
+cp gpurun_out/round_check.log gpurun_out/pytest_gpu.log gpurun_out/bench_full.log gpurun_keep/ 2>/dev/null
+cp gpurun_out/${R}_*.json gpurun_keep/ 2>/dev/null
+find gpurun_out/prof_$R -name "*kernel_stats.csv" -exec cp {} gpurun_keep/${R}_kernel_stats.csv \; 2>/dev/null
+find gpurun_out/prof_c3_$R -name "*kernel_stats.csv" -exec cp {} gpurun_keep/${R}_config3_kernel_stats.csv \; 2>/dev/null
+rm -rf gpurun_out/*
+mv gpurun_keep gpurun_out/keep
+echo rc=$rc
+exit $rc
