@@ -18,6 +18,8 @@ from __future__ import annotations
 
 import torch
 
+from ..modules.mlp import EvolvableMLP
+
 
 class EvolvableAgentMixin:
     #: learning-rate attribute -> the optimizer attribute it drives
@@ -36,6 +38,37 @@ class EvolvableAgentMixin:
 
     def _fresh_optimizer(self, lr_name: str):
         raise NotImplementedError
+
+    @property
+    def can_mutate_architecture(self) -> bool:
+        """MLP-encoder Q networks (the encoder's and head's node / layer
+        mutations and the latent's); CNN encoders and multi-agent ModuleDicts
+        are not mutated."""
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            # a sharded population replays every global agent's draws on every
+            # rank (hpo/shard.py RemoteAgent); the module and init draws of a
+            # Q-network mutation are not replayed: not applied anywhere
+            return False
+        net = getattr(self, self._policy_group[0])
+        return isinstance(getattr(net, "encoder", None), EvolvableMLP) and \
+            isinstance(getattr(net, "head_net", None), EvolvableMLP)
+
+    def architecture_mutation(self, new_layer_prob: float, rng) -> str:
+        """mutation.py:829-885 on the policy network: the method sampled from
+        its mutation table with ``rng`` (Mutations.rng; the table of an
+        EvolvableNetwork with an MLP encoder, population/arch.py), applied
+        with the modules' own generators; the shared (target) network re-made
+        from the mutated one (reinit_shared_networks, mutation.py:104-160)."""
+        import copy
+
+        from ..population import arch
+
+        net = getattr(self, self._policy_group[0])
+        applied = net.apply_mutation(arch.sample_method(new_layer_prob, rng))
+        setattr(self, self._policy_group[1], copy.deepcopy(net))
+        return applied
 
     def reinit_optimizers(self, optimizer=None) -> None:
         names = self.get_lr_names() if optimizer is None else [optimizer]

@@ -36,8 +36,15 @@ What runs, with the reference's draws from the reference's generators:
   :104-160) and fresh optimizers.  Policy-gradient algorithms (PPO, MADDPG)
   keep their activations, as the reference's :469-479.
 
-Not applied: architecture mutations of DQN / Rainbow / MADDPG agents
-(recorded as no mutation with a warning).
+* ``architecture_mutate`` on DQN / Rainbow agents with MLP encoders: the
+  method from the same table (an EvolvableNetwork's: head layer / node,
+  encoder node, latent node), applied to the Q network with the modules' own
+  generators, the target network re-made from it, fresh optimizers.
+
+Not applied: architecture mutations of CNN-encoder Q networks and of MADDPG,
+and architecture / activation mutations of DQN / Rainbow agents in a
+population sharded over ranks (recorded as no mutation with a warning, on
+every rank alike).
 """
 
 from __future__ import annotations
@@ -128,7 +135,9 @@ class Mutations:
         individuals that can change shape (PPO views: population/arch.py — the
         method sampled from the actor's table with self.rng, applied to the
         actor, the applied method to the critic, the shared encoder, then
-        mutation_hook and a fresh optimizer).  Other algorithms: not applied."""
+        mutation_hook and a fresh optimizer; DQN / Rainbow with MLP encoders:
+        algorithms/evolvable.py, the target re-made from the mutated network).
+        Other agents: not applied."""
         fn = getattr(individual, "architecture_mutation", None)
         if fn is None or not getattr(individual, "can_mutate_architecture", False):
             return self._not_applied(individual, "architecture")
@@ -145,7 +154,12 @@ class Mutations:
             individual.mut = "None"
             return individual
         net = getattr(individual, "actor", None)
-        if net is None or not hasattr(net, "change_activation"):
+        import torch.distributed as dist
+
+        if net is None or not hasattr(net, "change_activation") or (
+                dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+            # sharded populations: the recreated modules' draws are not replayed on
+            # the other ranks (hpo/shard.py), so no rank applies it
             return self._not_applied(individual, "activation")
         if net.activation is None:  # :489-499
             warnings.warn("Found no activation mutation capabilities. We advise setting the probability to "

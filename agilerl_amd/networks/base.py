@@ -92,6 +92,7 @@ class EvolvableNetwork(nn.Module):
         self.observation_space, self.action_space = observation_space, action_space
         self.latent_dim, self.min_latent_dim, self.max_latent_dim = latent_dim, min_latent_dim, max_latent_dim
         self.device, self.random_seed, self.encoder_name = device, random_seed, encoder_name
+        self.rng = np.random.default_rng(seed=random_seed)  # latent-node draws (EvolvableModule.rng)
         encoder_config = as_config(encoder_config)
         image = not multi and is_image_space(observation_space)
         if encoder_config is None:  # get_default_encoder_config (utils/evolvable_networks.py:168-216)
@@ -151,6 +152,49 @@ class EvolvableNetwork(nn.Module):
         new = EvolvableMLP(num_inputs=self.encoder.num_inputs, num_outputs=self.latent_dim, device=self.device,
                            name=self.encoder_name, **cfg)
         self.encoder = preserve_parameters(self.encoder, new)
+
+    # ---- architecture mutations (networks/base.py:457-491, modules/mlp.py:213-312)
+    def add_latent_node(self, numb_new_nodes: int | None = None) -> dict:
+        if numb_new_nodes is None:
+            numb_new_nodes = int(self.rng.choice([8, 16, 32]))
+        old = self.latent_dim
+        if self.latent_dim + numb_new_nodes < self.max_latent_dim:
+            self.latent_dim += numb_new_nodes
+        self.recreate_network(old)
+        return {"numb_new_nodes": numb_new_nodes}
+
+    def remove_latent_node(self, numb_new_nodes: int | None = None) -> dict:
+        if numb_new_nodes is None:
+            numb_new_nodes = int(self.rng.choice([8, 16, 32]))
+        old = self.latent_dim
+        if self.latent_dim - numb_new_nodes > self.min_latent_dim:
+            self.latent_dim -= numb_new_nodes
+        self.recreate_network(old)
+        return {"numb_new_nodes": numb_new_nodes}
+
+    def recreate_network(self, old_latent: int | None = None) -> None:
+        """Encoder (output = latent) and head (input = latent [+ whatever the
+        head concatenates]) rebuilt with their parameters kept where the
+        shapes overlap (preserve_parameters)."""
+        old_latent = self.latent_dim if old_latent is None else old_latent
+        self.encoder.num_outputs = self.latent_dim
+        self.encoder.recreate_network()
+        head = getattr(self, "head_net", None)
+        if head is not None:
+            head.num_inputs = head.num_inputs - old_latent + self.latent_dim
+            head.recreate_network()
+
+    def apply_mutation(self, method: str) -> str:
+        """One method of the mutation table (population/arch.py METHODS) on this
+        network -> the method actually applied (layer mutations at a limit
+        fall back to add_node, mlp.py:227-252)."""
+        if method in ("add_latent_node", "remove_latent_node"):
+            getattr(self, method)()
+            return method
+        owner, name = method.split(".")
+        mod = getattr(self, owner)
+        getattr(mod, name)()
+        return f"{owner}.{mod.last_mutation_attr}"
 
     @property
     def activation(self) -> str | None:

@@ -542,3 +542,53 @@ def test_ppo_unshared_encoders():
             assert not any(v for k, v in moved.items() if k.startswith("critic.")), moved
         else:
             assert moved["critic.encoder.model.critic_encoder_linear_layer_1.weight"]
+
+
+@pytest.mark.parametrize("algo", ["DQN", "Rainbow DQN"])
+def test_train_off_policy_with_dqn_yaml_mutations(algo):
+    """dqn.yaml / dqn_rainbow.yaml MUTATION_PARAMS (NO_MUT 0.4, ARCH_MUT 0.2,
+    NEW_LAYER 0.2, PARAMS_MUT 0.2, ACT_MUT 0.2, RL_HP_MUT 0.2): architecture and
+    activation mutations reshape the Q networks between generations and
+    training continues on the mutated agents (fresh optimizers, targets re-made)."""
+    import warnings
+
+    from agilerl_amd.components import ReplayBuffer
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.mutation import Mutations
+    from agilerl_amd.hpo.tournament import TournamentSelection
+    from agilerl_amd.training import train_off_policy
+    from agilerl_amd.utils import create_population
+
+    obs_space, act_space = _spaces()
+    INIT_HP = {"BATCH_SIZE": 32, "LR": 1e-3, "LEARN_STEP": 4, "GAMMA": 0.99, "TAU": 1e-2}
+    net_config = {"encoder_config": {"hidden_size": [64]}, "head_config": {"hidden_size": [64]}}
+    torch.manual_seed(1)
+    np.random.seed(1)
+    pop = create_population(algo, net_config, INIT_HP, obs_space, act_space, population_size=4)
+    mut = Mutations(no_mutation=0.4, architecture=0.2, new_layer_prob=0.2, parameters=0.2, activation=0.2,
+                    rl_hp=0.2, rand_seed=3)
+    seen = []
+    orig = mut.mutation
+
+    def record(population, pre_training_mut=False):
+        out = orig(population, pre_training_mut=pre_training_mut)
+        seen.extend(a.mut for a in out)
+        return out
+
+    mut.mutation = record
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        pop, fits = train_off_policy(env := SyntheticVecEnv(8, seed=4, p_done=0.1), "Synthetic", algo, pop,
+                                     ReplayBuffer(4000), INIT_HP=INIT_HP, max_steps=5 * 128, evo_steps=128,
+                                     eval_steps=20, eval_loop=1, tournament=TournamentSelection(2, True, 4, 1),
+                                     mutation=mut, verbose=False)
+    assert len(fits) == 5 and all(np.all(np.isfinite(f)) for f in fits)
+    assert any(m == "act" for m in seen) and any("node" in m or "layer" in m for m in seen), seen
+    shapes = {tuple(tuple(p.shape) for p in a.actor.parameters()) for a in pop}
+    acts = {a.actor.activation for a in pop}
+    assert len(shapes) > 1 or len(acts) > 1
+    for a in pop:
+        x = torch.as_tensor(np.random.standard_normal((3, 8)).astype(np.float32), device=a.device)
+        assert torch.isfinite(a.actor(x)).all()
+        # the target network tracks the (possibly reshaped) online network
+        assert [p.shape for p in a.actor.parameters()] == [p.shape for p in a.actor_target.parameters()]

@@ -90,7 +90,10 @@ def _run(world: int, rank: int, out_dir: str, port: int) -> None:
     pop = create_population("DQN", {"head_config": {"hidden_size": [16]}}, {"BATCH_SIZE": 16, "LR": 1e-3},
                             env.observation_space, env.action_space, hp_config=hp, population_size=G_TOTAL,
                             device="cpu")
-    mutation = Mutations(no_mutation=0.2, architecture=0.1, new_layer_prob=0.2, parameters=0.4, activation=0.1,
+    # architecture / activation mutations of Q networks apply in single-process
+    # runs only (hpo/mutation.py): the sharded run equals the single-process run
+    # of the mutations both apply
+    mutation = Mutations(no_mutation=0.2, architecture=0.0, new_layer_prob=0.2, parameters=0.4, activation=0.0,
                          rl_hp=0.4, mutation_sd=0.1, rand_seed=5)
     tournament = TournamentSelection(2, True, G_TOTAL, 1)
     memory = ReplayBuffer(500, device="cpu")
