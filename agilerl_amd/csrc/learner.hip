@@ -46,6 +46,7 @@
 //     norm, Adam from registers.
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "agx_common.h"
 
@@ -86,7 +87,7 @@ struct LearnPlan {
     int l_x0, ld_x0, l_xe[3], ld_xe[3], l_re[3], l_xh, ld_xh, l_rh;
     int l_s1, l_s2, ld_s;
     int l_lg, l_dlg, l_dvb, l_val, l_row;
-    int l_red, red_e[3], red_h, l_stat;
+    int l_red, red_e[3], red_h, l_stat, l_stamp;
     int l_grad;  // gradient image of [0, param_end) (aliases the activations)
     int lds_floats, act_floats;
     int slab;  // floats per cross-workgroup gradient slab (parameter image + loss)
@@ -201,6 +202,8 @@ constexpr LearnPlan make_plan(NetDims d) {
     red += 3 * kNW * pl.H;
     pl.l_red = off; off += red;
     pl.l_stat = off; off += 5 * kNW;
+    off = rup(off, 2);
+    pl.l_stamp = off; off += 2 * 80;  // diagnostic phase stamps (agx_debug_learn_stamps)
     pl.lds_floats = off;
     if (pl.lds_floats * 4 > 160 * 1024) return pl;
     // + the loss / approx_kl chunk + the partners' per-wave partial gradient norms
@@ -608,10 +611,13 @@ struct LearnArgs {
 
 constexpr unsigned kSpinMax = 1u << 23;  // ~ seconds of s_sleep polling: a missing partner is a bug
 
+// phase stamps go to LDS (a global store would sit in vmcnt and every
+// s_waitcnt vmcnt(0) after it would wait for its write); flushed at the end
 #define AGX_STAMP(slot)                                                          \
     do {                                                                         \
-        if (g.stamps && b == 0 && e == (Ep > 1) && mb == (nmb > 1) && tid == 0 && (slot) < 80) \
-            g.stamps[(slot)] = (long long)__builtin_readcyclecounter(); \
+        if constexpr (ST)                                                        \
+            if (b == 0 && e == (Ep > 1) && mb == (nmb > 1) && tid == 0 && (slot) < 80) \
+                reinterpret_cast<long long *>(sm + pl.l_stamp)[(slot)] = (long long)__builtin_readcyclecounter(); \
     } while (0)
 
 // ---------------------------------------------------------------------------
@@ -620,7 +626,9 @@ constexpr unsigned kSpinMax = 1u << 23;  // ~ seconds of s_sleep polling: a miss
 // JN > 0: every partner owns at most JN float4 chunk rounds (kNT chunks each) —
 // with 8 partners one round, and the per-slot Adam / norm code is instantiated
 // for that round only (a smaller kernel body); JN = 0: any split (K = 1 owns all)
-template <class C, int SB, int JN = 0>
+// ST: the diagnostic build with phase stamps (agx_debug_learn_stamps; the bench
+// shape only) — the product kernel carries no stamp code
+template <class C, int SB, int JN = 0, bool ST = false>
 __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     constexpr LearnPlan pl = C::plan;
@@ -697,14 +705,21 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     unsigned *legal = reinterpret_cast<unsigned *>(sm + pl.l_row + 5 * kSB);
     if (g.debug_stall && p == 0 && kk == 1) return;  // test hook: a partner that never arrives
 
-    // one thread's share of a sub-batch's inputs: obs words (LDS x0 image incl.
-    // padding) and one row word (old_logp/adv/ret/old_v, action or legal mask)
-    constexpr int kPreObs = (SB * pl.ld_x0 + kNT - 1) / kNT;
+    // one thread's share of a sub-batch's inputs: obs words (the SB x D real
+    // columns, contiguous in the minibatch-ordered rows; the padding columns of
+    // the LDS x0 image are zero-filled on commit) and one row word
+    // (old_logp/adv/ret/old_v, action or legal mask)
+    constexpr int kPreObs = (SB * pl.D + kNT - 1) / kNT;
+    constexpr bool kPrefetch = kPreObs == 1;  // carried in registers across the update
     struct Pre {
         int e, mb, sb;
         float ob[kPreObs];
         unsigned rv;
     };
+    // Every load is unconditional from an always-valid address (rows beyond the
+    // sub-batch read row 0 of the (epoch, agent) block) and the row predicates
+    // are applied on commit: a zero-then-masked-load form makes the next write
+    // of those registers wait (vmcnt) for the prefetch just issued.
     auto fetch = [&](int e_, int mb_, int sb_) {
         Pre r;
         r.e = e_;
@@ -715,28 +730,22 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
         const int bsz_ = (int)((s0_ + Bp <= S) ? Bp : S - s0_);
         const int nrow_ = e_ >= Ep ? 0 : (bsz_ - sb_ < SB ? bsz_ - sb_ : SB);
         const size_t ep = (size_t)(e_ < Ep ? e_ : 0) * g.P + p;
+        const size_t row0 = (size_t)(s0_ + sb_);
         const float *eo = g.gobs + ep * S * pl.D;
 #pragma unroll
         for (int k = 0; k < kPreObs; ++k) {
             const int i = tid + k * kNT;
-            const int rr = i / pl.ld_x0, dd = i % pl.ld_x0;
-            r.ob[k] = (rr < nrow_ && dd < pl.D) ? eo[(s0_ + sb_ + rr) * pl.D + dd] : 0.f;
+            r.ob[k] = eo[i < nrow_ * pl.D ? row0 * pl.D + i : 0];
         }
-        r.rv = 0u;
-        if (tid < 4 * kSB) {
-            const int k = tid / kSB, rr = tid % kSB;
-            r.rv = rr < nrow_ ? __builtin_bit_cast(unsigned, g.grow[ep * 4 * S + (size_t)k * S + s0_ + sb_ + rr]) : 0u;
-        } else if (tid < 5 * kSB) {
-            const int rr = tid - 4 * kSB;
-            r.rv = rr < nrow_ ? (unsigned)g.gact[ep * S + s0_ + sb_ + rr] : 0u;
-        } else if (tid < 6 * kSB) {
-            const int rr = tid - 5 * kSB;
-            r.rv = (g.gmask && rr < nrow_) ? g.gmask[ep * S + s0_ + sb_ + rr] : 0xffffffffu;
-        }
+        const int rr = tid < 4 * kSB ? tid % kSB : (tid < 5 * kSB ? tid - 4 * kSB : tid - 5 * kSB);
+        const unsigned *src = tid < 4 * kSB ? reinterpret_cast<const unsigned *>(g.grow) + (ep * 4 + tid / kSB) * S
+                              : (tid < 5 * kSB || !g.gmask) ? reinterpret_cast<const unsigned *>(g.gact) + ep * S
+                                                            : g.gmask + ep * S;
+        r.rv = src[(tid < 6 * kSB && rr < nrow_) ? row0 + rr : 0];
         return r;
     };
     Pre pre{};
-    if constexpr (kPreObs == 1) pre = fetch(0, 0, kk * SB);
+    if constexpr (kPrefetch) pre = fetch(0, 0, kk * SB);
 
     // Partners that share one XCD share its L2: plain stores (the line stays in
     // that L2) + sc1 loads (L1 bypassed) hand data over without the write-through
@@ -889,18 +898,32 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 // (padding columns rewritten too: the gradient image aliases them)
                 {
                     auto commit = [&](const Pre &x) {
+                        // the prefetch landed during the previous update (nothing is
+                        // outstanding here): an explicit vmcnt(0) the waitcnt pass sees,
+                        // so the commit's reads of the prefetch registers do not wait
+                        // on the next prefetch's loads (memory ops stay ordered after it)
+                        __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
-                        for (int k = 0; k < kPreObs; ++k)
-                            if (tid + k * kNT < SB * pl.ld_x0) sm[pl.l_x0 + tid + k * kNT] = x.ob[k];
-                        if (tid < 4 * kSB) rowf[tid] = __builtin_bit_cast(float, x.rv);
-                        else if (tid < 5 * kSB) acts[tid - 4 * kSB] = (int)x.rv;
-                        else if (tid < 6 * kSB) legal[tid - 5 * kSB] = x.rv;
+                        for (int k = 0; k < kPreObs; ++k) {
+                            const int i = tid + k * kNT;
+                            if (i < SB * pl.D) sm[pl.l_x0 + (i / pl.D) * pl.ld_x0 + i % pl.D] = i < nrow * pl.D ? x.ob[k] : 0.f;
+                        }
+                        constexpr int npad = pl.ld_x0 - pl.D;
+#pragma unroll
+                        for (int k = 0; k < (SB * npad + kNT - 1) / kNT; ++k) {
+                            const int i = tid + k * kNT;
+                            if (i < SB * npad) sm[pl.l_x0 + (i / npad) * pl.ld_x0 + pl.D + i % npad] = 0.f;
+                        }
+                        if (tid < 4 * kSB) rowf[tid] = tid % kSB < nrow ? __builtin_bit_cast(float, x.rv) : 0.f;
+                        else if (tid < 5 * kSB) acts[tid - 4 * kSB] = tid - 4 * kSB < nrow ? (int)x.rv : 0;
+                        else if (tid < 6 * kSB) legal[tid - 5 * kSB] = (g.gmask && tid - 5 * kSB < nrow) ? x.rv : 0xffffffffu;
                     };
-                    if constexpr (kPreObs > 1) {  // 32-row sub-batches: registers too tight to carry
+                    if constexpr (!kPrefetch) {  // wide observations: registers too tight to carry
                         commit(fetch(e, mb, sb));
                     } else {
                         if (pre.e != e || pre.mb != mb || pre.sb != sb) pre = fetch(e, mb, sb);
                         commit(pre);
+                        AGX_STAMP(stb + 4);
                         int ne = e, nm = mb, ns = sb + g.K * SB;
                         if (ns >= bsz) {
                             ns = kk * SB;
@@ -910,6 +933,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                             }
                         }
                         pre = fetch(ne, nm, ns);
+                        AGX_STAMP(stb + 5);
                     }
                 }
                 __syncthreads();
@@ -1115,8 +1139,6 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 }
                 __syncthreads();
                 AGX_STAMP(stb + 3);
-                AGX_STAMP(stb + 4);
-                AGX_STAMP(stb + 5);
 
                 // backward row pass through LN(+affine)+ReLU of an encoder layer:
                 // dY (dyb, stride ldy) -> dZ (S2)
@@ -1622,6 +1644,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             gv[f] = av[i];
         }
     }
+    if constexpr (ST)
+        if (g.stamps && b == 0 && tid < 80) g.stamps[tid] = reinterpret_cast<const long long *>(sm + pl.l_stamp)[tid];
     if (tid == 0 && kk == 0) {
         if (g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)Ep);
         if (g.kl_out) g.kl_out[p] = n_done ? (float)(kl_total / (double)n_done) : 0.f;
@@ -1964,6 +1988,14 @@ static void launch_learn(const LearnArgs &a, int nblocks, size_t lds, hipStream_
     // one owned chunk round per thread when the K-way split leaves <= kNT chunks per partner
     constexpr int n4s = C::plan.param_end / 4 + 1;
     const bool one_round = (n4s + a.K - 1) / a.K + 1 <= kNT;
+    if constexpr (std::is_same_v<C, Shape<8, 4, 2, 64, 64, 0, 64, 64>>) {
+        if (a.stamps && sb == 16 && one_round) {
+            (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 16, 1, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            ppo_learn_kernel<C, 16, 1, true><<<(unsigned)nblocks, kNT, lds, s>>>(a);
+            return;
+        }
+    }
     if (sb == 16 && one_round) ppo_learn_kernel<C, 16, 1><<<(unsigned)nblocks, kNT, lds, s>>>(a);
     else if (sb == 16) ppo_learn_kernel<C, 16><<<(unsigned)nblocks, kNT, lds, s>>>(a);
     else ppo_learn_kernel<C, 32><<<(unsigned)nblocks, kNT, lds, s>>>(a);

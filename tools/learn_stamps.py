@@ -1,9 +1,9 @@
 """Phase timing of the fused learner (diagnostic; uses agx_debug_learn_stamps).
 
 Slots (learner.hip AGX_STAMP): sub-batch k of agent 0's first minibatch at
-k*16 + {0 start, 1 gathered, 2 forward trunk, 3 head row pass (LN fwd + output
-layers + loss + LN bwd; 4 and 5 stamped with it), 6 output-layer + head dW / dX,
-7 encoder bwd}; 64+9 gradients dumped, 64+10 Adam done;
+k*16 + {0 start, 4 sub-batch committed to LDS, 5 next prefetch issued,
+1 barrier passed, 2 forward trunk, 3 head row pass (LN fwd + output layers +
+loss + LN bwd), 6 output-layer + head dW / dX, 7 encoder bwd}; 64+9 gradients dumped, 64+10 Adam done;
 partners: 64+11/12 first barrier ticket/passed, 64+13 reduce-scatter done,
 64+8/15 second barrier ticket/passed, 64+14 norm done."""
 import os
@@ -38,9 +38,12 @@ lib.agx_debug_learn_stamps(None)
 st = buf.cpu().tolist()
 nmb = pop.update_epochs * pop.n_minibatches()
 print(f"learn() wall {1e3 * (t1 - t0):.3f} ms  ({nmb} minibatch updates per agent, {P} agents)")
-names = ["gather", "trunk fwd", "head row pass", "-", "-", "out+head dW, dX", "enc bwd"]
+# slots in time order: 0 start, 4 committed, 5 next prefetch issued, 1 barrier,
+# 2 trunk, 3 head row pass, 6 output/head dW + dX, 7 encoder bwd
+order = [0, 4, 5, 1, 2, 3, 6, 7]
+names = ["commit", "prefetch issue", "barrier", "trunk fwd", "head row pass", "out+head dW, dX", "enc bwd"]
 for sb in range(4):
-    row = st[sb * 16: sb * 16 + 8]
+    row = [st[sb * 16 + k] for k in order]
     if not all(row):  # only workgroup 0 stamps: with K partners it runs 1 of every K sub-batches
         continue
     seg = [row[i + 1] - row[i] for i in range(7)]
