@@ -595,6 +595,7 @@ struct LearnArgs {
     unsigned *err;         // sticky error word (partner timeout)
     long long *stamps;
     int K;                 // workgroups per agent (data-parallel over sub-batches)
+    int Q;                 // agent stride of the block index (>= P; blocks with b % Q >= P exit)
     float *slabs;          // [P][2][K][slab] gradient hand-off (double-buffered)
     float *sums;           // [P][2][slab] reduce-scattered gradient sums (double-buffered)
     unsigned *cnt;         // [P] arrival counters, [P] timeout word, [P+1+p] second-barrier,
@@ -632,13 +633,16 @@ template <class C, int SB, int JN = 0, bool ST = false>
 __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     constexpr LearnPlan pl = C::plan;
-    // block b -> agent b % P, partner kk = b / P: with P % 8 == 0 an agent's K
-    // workgroups share an XCD under round-robin dispatch (speed only)
+    // block b -> agent b % Q, partner kk = b / Q with Q = P rounded up to a
+    // multiple of the 8 XCDs (partners only): under round-robin dispatch an
+    // agent's K workgroups then share one XCD (and its L2) for every P, the
+    // strong-scaling shards P = 1, 2, 4 included; padding blocks exit at once
     // an aborted / timed-out rollout queued ahead of this learn leaves its
     // control word set: the partial rollout must not update anything
     if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const int b = blockIdx.x;
-    const int p = b % g.P, kk = b / g.P;
+    const int p = b % g.Q, kk = b / g.Q;
+    if (p >= g.P) return;
     const int tid = threadIdx.x;
     float *gp = g.params + (size_t)p * pl.n;
     float *gm = g.m + (size_t)p * pl.n;
@@ -2192,7 +2196,11 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *x
     float *grow = reinterpret_cast<float *>(ws + w.grow);
     int K = 1, SB = kSB;
     pick_split(P, batch, K, SB);
-    AGX_REQUIRE(P * K <= 65535, "agx_ppo_learn: too many workgroups");
+    // partners: agents strided by a multiple of 8 blocks (one XCD per agent, see
+    // the kernel) while the padded grid still fits the CUs
+    long long Q = K > 1 ? (P + 7) / 8 * 8 : P;
+    if (Q * K > cu_count()) Q = P;
+    AGX_REQUIRE(Q * K <= 65535, "agx_ppo_learn: too many workgroups");
     // counters + timeout word: one 16-byte-multiple block at the workspace start, zeroed by the gather
     dim3 ggrid((unsigned)ceil_div(S, 256), (unsigned)(epochs * P));
     ppo_gather_kernel<<<ggrid, 256, 0, s>>>(x->obs, reinterpret_cast<const long long *>(x->actions), x->old_logp,
@@ -2233,6 +2241,7 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *x
     a.err = x->error_word;
     a.stamps = g_stamps_ptr();
     a.K = K;
+    a.Q = (int)Q;
     a.slabs = reinterpret_cast<float *>(ws + w.slabs);
     a.sums = reinterpret_cast<float *>(ws + w.sums);
     a.cnt = reinterpret_cast<unsigned *>(ws);
@@ -2242,7 +2251,7 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *x
         const char *wt = getenv("AGX_LEARN_WRITETHROUGH");
         a.write_through = wt && atoi(wt) != 0;
     }
-    L.learn(a, (int)(P * K), (size_t)pl.lds_floats * sizeof(float), s, SB);
+    L.learn(a, (int)(Q * K), (size_t)pl.lds_floats * sizeof(float), s, SB);
     return check_launch("agx_ppo_learn");
 }
 
