@@ -319,6 +319,22 @@ __device__ __forceinline__ float rowgroup_sum(float v) {
     const int l = (int)(threadIdx.x & 63);
     return v + __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((l ^ 32) << 2, __builtin_bit_cast(int, v)));
 }
+// A uniform pointer kept in a VGPR pair (opaque to the compiler): kernel-argument
+// pointers otherwise live as 8-SGPR tuples (s_load_dwordx8) that are spilled and
+// restored whole whenever one of them is used
+template <class T>
+__device__ __forceinline__ T *in_vgpr(T *ptr) {
+    asm volatile("" : "+v"(ptr));
+    return ptr;
+}
+// ... and back to SGPRs where an instruction needs a scalar base (buffer resources)
+template <class T>
+__device__ __forceinline__ T *to_sgpr(T *ptr) {
+    const unsigned long long u = reinterpret_cast<unsigned long long>(ptr);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+    return reinterpret_cast<T *>(((unsigned long long)hi << 32) | lo);
+}
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
@@ -644,9 +660,18 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     const int p = b % g.Q, kk = b / g.Q;
     if (p >= g.P) return;
     const int tid = threadIdx.x;
-    float *gp = g.params + (size_t)p * pl.n;
-    float *gm = g.m + (size_t)p * pl.n;
-    float *gv = g.v + (size_t)p * pl.n;
+    float *gp = in_vgpr(g.params + (size_t)p * pl.n);
+    float *gm = in_vgpr(g.m + (size_t)p * pl.n);
+    float *gv = in_vgpr(g.v + (size_t)p * pl.n);
+    // cold arguments (timeout path, per-epoch test, end-of-learn outputs) in VGPRs
+    unsigned *const err_v = in_vgpr(g.err);
+    unsigned *const tmo_v = in_vgpr(g.cnt + g.P);
+    float *const loss_out_v = in_vgpr(g.loss_out);
+    float *const kl_out_v = in_vgpr(g.kl_out);
+    int *const epochs_out_v = in_vgpr(g.epochs_out);
+    long long *const step_v = in_vgpr(g.step + p);
+    double tkl_v = g.target_kl;
+    asm volatile("" : "+v"(tkl_v));
     const long long S = g.S;
     Fwd<C, SB> fw{sm};
 
@@ -659,8 +684,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     // i.e. slot i is float (i & 3) of chunk oc0 + tid + kNT*(i >> 2).  K == 1:
     // every chunk, thread t owning t, t + kNT, ...
     constexpr int n4 = pl.param_end / 4, n4s = n4 + 1;
-    const int oc0 = (int)((long long)n4s * kk / g.K), oc1 = (int)((long long)n4s * (kk + 1) / g.K);
-    const int pc1 = oc1 < n4 ? oc1 : n4;  // own parameter chunks [oc0, pc1)
+    int oc0 = n4s * kk / g.K, oc1 = n4s * (kk + 1) / g.K;
+    int pc1 = oc1 < n4 ? oc1 : n4;  // own parameter chunks [oc0, pc1)
     constexpr int kUsed4 = JN > 0 ? JN : (n4 + kNT - 1) / kNT;  // owned chunk rounds per thread, at most
     static_assert(pl.param_end % 4 == 0 && pl.slab >= pl.param_end + 4 + 2 * kNW * kMaxK, "sum slab layout");
     static_assert(4 * kUsed4 <= kMaxPT, "owned slots");
@@ -668,6 +693,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     // owned chunk rounds: a block-uniform trip count (1 with 8 partners), so the
     // unrolled per-slot loops below skip the rounds no thread owns
     const int jn_own = __builtin_amdgcn_readfirstlane((oc1 - oc0 + kNT - 1) / kNT);
+    // the bounds only enter per-lane index math: VGPRs (not spilled SGPR pairs)
+    asm volatile("" : "+v"(oc0), "+v"(oc1), "+v"(pc1));
     // Adam moments of the owned LDS parameter slots -> registers; group bits
     float am[kMaxPT], av[kMaxPT];
     unsigned gbits = 0, vbits = 0;
@@ -700,7 +727,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     float loss_total = 0.f;
     double kl_total = 0.0;  // sum of per-minibatch approx_kl (np.mean over all minibatches so far, ppo.py:917)
     int n_done = 0, epochs_done = 0;
-    const long long step0 = g.step[p];
+    const long long step0 = *step_v;
     double pb1 = pow((double)g.b1, (double)step0), pb2 = pow((double)g.b2, (double)step0);
     const float lr_p = g.lr[p];
     float *rowf = sm + pl.l_row;  // [4][SB]: old_logp, adv, ret, old_v
@@ -724,6 +751,19 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     // sub-batch read row 0 of the (epoch, agent) block) and the row predicates
     // are applied on commit: a zero-then-masked-load form makes the next write
     // of those registers wait (vmcnt) for the prefetch just issued.
+    // per-thread pointers of this thread's words at epoch 0 (VGPRs) and their
+    // per-epoch strides: threads < 4*kSB one row of old_logp/adv/ret/old_v, then
+    // the actions, then the legal-action masks (actions again without masks)
+    const bool has_mask = g.gmask != nullptr;
+    const int tid0 = vtid();
+    const int rw_rr = tid0 < 4 * kSB ? tid0 % kSB : (tid0 < 5 * kSB ? tid0 - 4 * kSB : tid0 - 5 * kSB);
+    const bool rw_on = tid0 < 6 * kSB;
+    const unsigned *rw0 = in_vgpr(tid0 < 4 * kSB ? reinterpret_cast<const unsigned *>(g.grow) + ((size_t)p * 4 + tid0 / kSB) * S
+                                  : (tid0 < 5 * kSB || !has_mask) ? reinterpret_cast<const unsigned *>(g.gact) + (size_t)p * S
+                                                                   : g.gmask + (size_t)p * S);
+    const size_t rw_es = (size_t)g.P * S * (tid0 < 4 * kSB ? 4 : 1);
+    const float *ob0 = in_vgpr(g.gobs + (size_t)p * S * pl.D);
+    const size_t ob_es = (size_t)g.P * S * pl.D;
     auto fetch = [&](int e_, int mb_, int sb_) {
         Pre r;
         r.e = e_;
@@ -733,19 +773,15 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
         const long long s0_ = (long long)mb_ * Bp;
         const int bsz_ = (int)((s0_ + Bp <= S) ? Bp : S - s0_);
         const int nrow_ = e_ >= Ep ? 0 : (bsz_ - sb_ < SB ? bsz_ - sb_ : SB);
-        const size_t ep = (size_t)(e_ < Ep ? e_ : 0) * g.P + p;
+        const size_t ee = (size_t)(e_ < Ep ? e_ : 0);
         const size_t row0 = (size_t)(s0_ + sb_);
-        const float *eo = g.gobs + ep * S * pl.D;
+        const float *eo = ob0 + ee * ob_es;
 #pragma unroll
         for (int k = 0; k < kPreObs; ++k) {
             const int i = tid + k * kNT;
             r.ob[k] = eo[i < nrow_ * pl.D ? row0 * pl.D + i : 0];
         }
-        const int rr = tid < 4 * kSB ? tid % kSB : (tid < 5 * kSB ? tid - 4 * kSB : tid - 5 * kSB);
-        const unsigned *src = tid < 4 * kSB ? reinterpret_cast<const unsigned *>(g.grow) + (ep * 4 + tid / kSB) * S
-                              : (tid < 5 * kSB || !g.gmask) ? reinterpret_cast<const unsigned *>(g.gact) + ep * S
-                                                            : g.gmask + ep * S;
-        r.rv = src[(tid < 6 * kSB && rr < nrow_) ? row0 + rr : 0];
+        r.rv = rw0[ee * rw_es + ((rw_on && rw_rr < nrow_) ? row0 + rw_rr : 0)];
         return r;
     };
     Pre pre{};
@@ -771,8 +807,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)g.K) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > kSpinMax) {
-                    __hip_atomic_store(g.cnt + g.P, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (g.err) __hip_atomic_fetch_or(g.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(tmo_v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (err_v) __hip_atomic_fetch_or(err_v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     ok = 0;
                     break;
                 }
@@ -789,6 +825,12 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
         local = same && !g.write_through;
     }
 
+    // this agent's slab / sum slab pairs and barrier counters (VGPR-held, see in_vgpr)
+    float *slab_p = in_vgpr(g.slabs + (g.K > 1 ? (size_t)p * 2 * g.K * pl.slab : 0));
+    float *sum_p = in_vgpr(g.sums + (g.K > 1 ? (size_t)p * 2 * pl.slab : 0));
+    unsigned *ctr1 = in_vgpr(g.cnt + p);
+    unsigned *ctr2 = in_vgpr(g.cnt + g.P + 1 + p);
+    unsigned *ctr3 = in_vgpr(g.cnt + 3 * g.P + 1 + (size_t)g.P * kMaxK + p);
     for (int e = 0; e < Ep; ++e) {
         for (int mb = 0; mb < nmb; ++mb) {
             const long long s0 = (long long)mb * Bp;
@@ -802,7 +844,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             float lsum = 0.f, klsum = 0.f;
             // this update's gradient slabs (double-buffered by update parity)
             const int upd = e * nmb + mb;
-            float *base = g.K > 1 ? g.slabs + ((size_t)p * 2 + (upd & 1)) * g.K * pl.slab : nullptr;
+            float *base = g.K > 1 ? to_sgpr(slab_p + (size_t)(upd & 1) * g.K * pl.slab) : nullptr;
             const auto slab_rsrc = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)kk * pl.slab, 0,
                                                                      __builtin_amdgcn_readfirstlane(pl.slab * 4),
                                                                      0x00020000);
@@ -847,7 +889,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             };
             // this agent's summed-gradient slab (written by the reduce-scatter)
             const auto sum_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-                g.K > 1 ? g.sums + ((size_t)p * 2 + (upd & 1)) * pl.slab : nullptr, 0,
+                g.K > 1 ? to_sgpr(sum_p + (size_t)(upd & 1) * pl.slab) : nullptr, 0,
                 __builtin_amdgcn_readfirstlane(pl.slab * 4), 0x00020000);
             // Partner barrier (MI355X_MICROARCH visibility rules): every wave drains its
             // write-through (sc1) stores (vmcnt) -> workgroup barrier -> one relaxed
@@ -870,8 +912,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                            __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                         __builtin_amdgcn_s_sleep(1);
                         if (++spins > kSpinMax) {
-                            __hip_atomic_store(g.cnt + g.P, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            if (g.err) __hip_atomic_fetch_or(g.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(tmo_v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (err_v) __hip_atomic_fetch_or(err_v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             ok = 0;
                             break;
                         }
@@ -920,7 +962,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         }
                         if (tid < 4 * kSB) rowf[tid] = tid % kSB < nrow ? __builtin_bit_cast(float, x.rv) : 0.f;
                         else if (tid < 5 * kSB) acts[tid - 4 * kSB] = tid - 4 * kSB < nrow ? (int)x.rv : 0;
-                        else if (tid < 6 * kSB) legal[tid - 5 * kSB] = (g.gmask && tid - 5 * kSB < nrow) ? x.rv : 0xffffffffu;
+                        else if (tid < 6 * kSB) legal[tid - 5 * kSB] = (has_mask && tid - 5 * kSB < nrow) ? x.rv : 0xffffffffu;
                     };
                     if constexpr (!kPrefetch) {  // wide observations: registers too tight to carry
                         commit(fetch(e, mb, sb));
@@ -1404,7 +1446,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     slab_put(pl.param_end, lmb);
                     slab_put(pl.param_end + 1, klmb);
                 }
-                if (!partner_sync(g.cnt + p, (unsigned)(g.K * (upd + 1)), 64 + 11, 64 + 12)) return;
+                if (!partner_sync(ctr1, (unsigned)(g.K * (upd + 1)), 64 + 11, 64 + 12)) return;
                 // ---- reduce-scatter: partner kk sums its own float4 chunks [oc0, oc1)
                 // of the parameter image (+ the chunk holding the loss / approx_kl
                 // words) over the K slabs in partner order; the sums stay in its
@@ -1467,7 +1509,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     }
                 }
                 AGX_STAMP(64 + 13);
-                if (!partner_sync(g.cnt + g.P + 1 + p, (unsigned)(g.K * (upd + 1)), 64 + 8, 64 + 15)) return;
+                if (!partner_sync(ctr2, (unsigned)(g.K * (upd + 1)), 64 + 8, 64 + 15)) return;
                 // the minibatch loss and approx_kl: partner-order sums of the K words
                 // (uniform: the early-stop branch depends on it)
                 lmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
@@ -1600,7 +1642,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             }
             if (direct) {
                 // ---- P11: every partner's updated chunks -> this LDS image --------
-                if (!partner_sync(g.cnt + 3 * g.P + 1 + (size_t)g.P * kMaxK + p, (unsigned)(g.K * (upd + 1)), 64 + 0,
+                if (!partner_sync(ctr3, (unsigned)(g.K * (upd + 1)), 64 + 0,
                                   64 + 1))
                     return;
                 const int tid = vtid();
@@ -1632,7 +1674,13 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
         ++epochs_done;
         // target-KL early stop after the epoch (ppo.py:917-918); every partner
         // holds the same fixed-order kl words, so all take the same branch
-        if (g.target_kl > 0.0 && kl_total / (double)n_done > g.target_kl) break;
+        {
+            const unsigned long long tb = __builtin_bit_cast(unsigned long long, tkl_v);
+            const double tkl = __builtin_bit_cast(
+                double, ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(tb >> 32)) << 32) |
+                            __builtin_amdgcn_readfirstlane((unsigned)tb));
+            if (tkl > 0.0 && kl_total / (double)n_done > tkl) break;
+        }
     }  // epochs
 
     // ---- write parameters and moments back (partners hold identical parameter
@@ -1651,10 +1699,10 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     if constexpr (ST)
         if (g.stamps && b == 0 && tid < 80) g.stamps[tid] = reinterpret_cast<const long long *>(sm + pl.l_stamp)[tid];
     if (tid == 0 && kk == 0) {
-        if (g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)Ep);
-        if (g.kl_out) g.kl_out[p] = n_done ? (float)(kl_total / (double)n_done) : 0.f;
-        if (g.epochs_out) g.epochs_out[p] = epochs_done;
-        g.step[p] = step0 + n_done;
+        if (loss_out_v) loss_out_v[p] = loss_total / ((float)S * (float)Ep);
+        if (kl_out_v) kl_out_v[p] = n_done ? (float)(kl_total / (double)n_done) : 0.f;
+        if (epochs_out_v) epochs_out_v[p] = epochs_done;
+        *step_v = step0 + n_done;
     }
 #undef IC
 #undef BC
