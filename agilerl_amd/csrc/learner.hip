@@ -883,9 +883,22 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
             };
             // write-through (sc1) store of one gradient word into this workgroup's slab
             // (plain store when the partners share this XCD's L2, else write-through)
+            auto put_l = [&](int l, float x) {
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), slab_rsrc, l * 4, 0, 0);
+            };
+            auto put_w = [&](int l, float x) {
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), slab_rsrc, l * 4, 0, 16);
+            };
             auto slab_put = [&](int l, float x) {
-                if (local) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), slab_rsrc, l * 4, 0, 0);
-                else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), slab_rsrc, l * 4, 0, 16);
+                if (local) put_l(l, x);
+                else put_w(l, x);
+            };
+            // a group's dW tiles -> the slab: the store form is chosen once per group
+            // (the cache-policy operand is an immediate; a branch per store cost
+            // ~90 scalar branches per update)
+            auto emit_slab = [&](auto gc) {
+                if (local) emit_tiles(gc, put_l);
+                else emit_tiles(gc, put_w);
             };
             // this agent's summed-gradient slab (written by the reduce-scatter)
             const auto sum_rsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -1304,8 +1317,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         }
                     }
                     if (direct && last_sb) {
-                        emit_tiles(IC(pl.ne + 1), slab_put);
-                        emit_tiles(IC(pl.ne + 2), slab_put);
+                        emit_slab(IC(pl.ne + 1));
+                        emit_slab(IC(pl.ne + 2));
                     }
                     constexpr int gh = pl.ne, Le = pl.ne - 1;
 #pragma unroll
@@ -1318,7 +1331,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                 [&](int k, int n) { return relu(sm[pl.l_xe[Le] + k * pl.ld_xe[Le] + i0 + n]); });
                         }
                     }
-                    if (direct && last_sb) emit_tiles(IC(gh), slab_put);
+                    if (direct && last_sb) emit_slab(IC(gh));
                     constexpr int nt = (SB / 16) * (pl.lat / 16);
                     for (int t = wave; t < nt; t += kNW) {
                         const int m0 = (t % (SB / 16)) * 16, n0 = (t / (SB / 16)) * 16;
@@ -1365,7 +1378,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                 });
                         }
                     }
-                    if (direct && last_sb) emit_tiles(IC(L), slab_put);
+                    if (direct && last_sb) emit_slab(IC(L));
                     if constexpr (L > 0) {
                         constexpr int nt = (SB / 16) * (fin / 16);
                         for (int t = wave; t < nt; t += kNW) {
@@ -1396,15 +1409,15 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 emit_tiles(IC(pl.ne + 1), gput);
                 emit_tiles(IC(pl.ne + 2), gput);
             } else if (kk * SB >= bsz) {  // no sub-batch this update: publish zeros
-                emit_tiles(IC(0), slab_put);
-                emit_tiles(IC(1), slab_put);
-                if constexpr (pl.ne == 3) emit_tiles(IC(2), slab_put);
-                emit_tiles(IC(pl.ne), slab_put);
-                emit_tiles(IC(pl.ne + 1), slab_put);
-                emit_tiles(IC(pl.ne + 2), slab_put);
+                emit_slab(IC(0));
+                emit_slab(IC(1));
+                if constexpr (pl.ne == 3) emit_slab(IC(2));
+                emit_slab(IC(pl.ne));
+                emit_slab(IC(pl.ne + 1));
+                emit_slab(IC(pl.ne + 2));
             }
             // LN / bias vectors: fixed-order sums of the per-wave partials
-            auto vdump = [&](auto Lc) {
+            auto vdump = [&](auto Lc, auto put) {
                 constexpr int L = decltype(Lc)::value;
                 constexpr int F = L < pl.ne ? pl.eout[L < pl.ne ? L : 0] : pl.H;
                 constexpr int nv = (L < pl.ne && !pl.eaff[L < pl.ne ? L : 0]) ? 1 : 3;
@@ -1421,14 +1434,18 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     } else {
                         l = (k == 0 ? pl.l_hb : (k == 1 ? pl.l_hg : pl.l_hbe)) + j;
                     }
-                    if (direct) slab_put(l, x);
-                    else G[l] = x;
+                    put(l, x);
                 }
             };
-            vdump(IC(0));
-            vdump(IC(1));
-            if constexpr (pl.ne == 3) vdump(IC(2));
-            vdump(IC(pl.ne));
+            auto vdump_all = [&](auto put) {
+                vdump(IC(0), put);
+                vdump(IC(1), put);
+                if constexpr (pl.ne == 3) vdump(IC(2), put);
+                vdump(IC(pl.ne), put);
+            };
+            if (!direct) vdump_all(gput);
+            else if (local) vdump_all(put_l);
+            else vdump_all(put_w);
             AGX_STAMP(64 + 9);
             __syncthreads();
             float lmb = lsum, klmb = klsum;
@@ -1676,9 +1693,9 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
         // holds the same fixed-order kl words, so all take the same branch
         {
             const unsigned long long tb = __builtin_bit_cast(unsigned long long, tkl_v);
-            const double tkl = __builtin_bit_cast(
-                double, ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(tb >> 32)) << 32) |
-                            __builtin_amdgcn_readfirstlane((unsigned)tb));
+            const unsigned thi = __builtin_amdgcn_readfirstlane((unsigned)(tb >> 32));
+            const unsigned tlo = __builtin_amdgcn_readfirstlane((unsigned)tb);  // unsigned: no sign extension
+            const double tkl = __builtin_bit_cast(double, ((unsigned long long)thi << 32) | tlo);
             if (tkl > 0.0 && kl_total / (double)n_done > tkl) break;
         }
     }  // epochs
