@@ -1423,11 +1423,19 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 constexpr int nv = (L < pl.ne && !pl.eaff[L < pl.ne ? L : 0]) ? 1 : 3;
                 constexpr int red = L < pl.ne ? pl.red_e[L < pl.ne ? L : 0] : pl.red_h;
                 const int tid = vtid();
-                for (int idx = tid; idx < nv * F; idx += kNT) {
+                // compile-time rounds; all kNW partial loads issued before the
+                // fixed-order sum (a load-add chain waited on every LDS round trip)
+#pragma unroll
+                for (int rnd = 0; rnd < (nv * F + kNT - 1) / kNT; ++rnd) {
+                    const int idx = tid + rnd * kNT;
+                    if (idx >= nv * F) break;
                     const int k = idx / F, j = idx % F;
+                    float pv[kNW];
+#pragma unroll
+                    for (int w = 0; w < kNW; ++w) pv[w] = sm[pl.l_red + red + (k * kNW + w) * F + j];
                     float x = 0.f;
 #pragma unroll
-                    for (int w = 0; w < kNW; ++w) x += sm[pl.l_red + red + (k * kNW + w) * F + j];
+                    for (int w = 0; w < kNW; ++w) x += pv[w];
                     int l;
                     if constexpr (L < pl.ne) {
                         l = (k == 0 ? pl.l_eb[L < pl.ne ? L : 0] : (k == 1 ? pl.l_eg[L < pl.ne ? L : 0] : pl.l_ebe[L < pl.ne ? L : 0])) + j;
