@@ -49,7 +49,10 @@ struct Smem {
     float As[2][BK][LDA];  // As[k][m]
     float Bs[2][BK][LDB];  // Bs[k][n]
     int tabA[kTab], tabB[kTab];
-    int col[BN][2 * kTapMax];  // dgrad: per output column, oh of tap kh / ow of tap kw (-1: no tap)
+    // dgrad: per output column, oh of tap kh / ow of tap kw (-1: no tap); rows padded
+    // to an odd word count: lanes read 64 different columns' entry a, and a 32-word
+    // row stride put them all in one LDS bank
+    int col[BN][2 * kTapMax + 1];
 };
 
 __device__ __forceinline__ float ld_x(const void *x, int o, bool u8, float lo, float rng) {
@@ -77,6 +80,7 @@ struct FwdOps {
         o.y = y + (size_t)g * gy;
         return o;
     }
+    __device__ int kend(int k1) const { return k1; }
     struct Ctx {
         int xbase;  // input offset of this thread's output pixel, -1 past N
     };
@@ -139,6 +143,7 @@ struct WgradOps {
         o.part = part + (size_t)g * gp;
         return o;
     }
+    __device__ int kend(int k1) const { return k1; }
     struct Ctx {
         int koff;  // im2col offset of this thread's weight column; -2: the ones column, -1: past N
     };
@@ -195,22 +200,41 @@ struct WgradOps {
 // = (ph, pw) are reached only by the taps kh = ph + s*a, kw = pw + s*b, at
 // output (ih' - a, iw' - b) where ih = ih'*s + ph.  One GEMM per phase over just
 // those taps (K / s^2 of the full tap set: no MFMA work on structural zeros).
+// All s^2 phases of all groups go out in ONE launch (blockIdx.z = (group * s^2
+// + phase) * splits + split): per-phase launches gave a few hundred workgroups
+// each, under two per CU, and the gathers' latency went unhidden.  A GEMM too
+// short in N to fill the chip splits K (partials summed in a fixed order by
+// dgrad_reduce_kernel; the split count depends on the layer shape only, so a
+// group's result does not depend on how many groups share the launch).
 struct DgradOps {
     const float *w;      // [Cout][Cin][KH][KW]
     const float *dy, *yact;
     float *dx;           // [B][Cin][H][W]
+    float *part;         // split-K partials [group*nph + phase][split][M][Nmax], or null (one split)
     Shape s;
     int M, N, K;         // M = Cin, N = B*Hp*Wp (this phase's pixels), K = Cout*nA*nB (its taps)
     int ph, pw, Hp, Wp, nA, nB;
+    int nph, Nmax, splits;
     long long gw, gy, gx;
-    __device__ DgradOps at(int g) const {
+    __device__ DgradOps at(int gi) const {
         DgradOps o = *this;
+        const int g = gi / nph, phase = gi % nph;
+        o.ph = phase / s.S;
+        o.pw = phase % s.S;
+        o.Hp = (s.H - o.ph + s.S - 1) / s.S;
+        o.Wp = (s.W - o.pw + s.S - 1) / s.S;
+        o.nA = s.KH > o.ph ? (s.KH - o.ph + s.S - 1) / s.S : 0;
+        o.nB = s.KW > o.pw ? (s.KW - o.pw + s.S - 1) / s.S : 0;
+        o.N = s.B * o.Hp * o.Wp;
+        o.K = s.Cout * o.nA * o.nB;
         o.w = w + (size_t)g * gw;
         o.dy = dy + (size_t)g * gy;
         o.yact = yact ? yact + (size_t)g * gy : nullptr;
         o.dx = dx + (size_t)g * gx;
+        o.part = part ? part + (size_t)gi * splits * M * Nmax : nullptr;
         return o;
     }
+    __device__ int kend(int) const { return K; }  // this phase's taps (0: zeros)
     struct Ctx {
         int dbase;  // dy offset of this thread's image (channel 0), -1 past N
         int c;      // column within the tile
@@ -273,12 +297,29 @@ struct DgradOps {
             rb[i] = g;
         }
     }
-    __device__ void store(int ci, int n, float v, int) const {
+    __device__ void store(int ci, int n, float v, int z) const {
         if (ci >= M || n >= N) return;
+        if (part) {
+            part[((size_t)z * M + ci) * Nmax + n] = v;
+            return;
+        }
         const int iwp = n % Wp, t2 = n / Wp, ihp = t2 % Hp, bb = t2 / Hp;
         dx[(((size_t)bb * s.Cin + ci) * s.H + ihp * s.S + ph) * s.W + iwp * s.S + pw] = v;
     }
 };
+
+// dx of every (group, phase) from its split partials, summed in split order
+__global__ void dgrad_reduce_kernel(DgradOps o_g) {
+    const DgradOps o = o_g.at((int)blockIdx.y);
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ci = i / o.Nmax, n = i % o.Nmax;
+    if (ci >= o.M || n >= o.N) return;
+    const size_t MN = (size_t)o.M * o.Nmax;
+    float t = 0.f;
+    for (int z = 0; z < o.splits; ++z) t += o.part[z * MN + i];
+    const int iwp = n % o.Wp, t2 = n / o.Wp, ihp = t2 % o.Hp, bb = t2 / o.Hp;
+    o.dx[(((size_t)bb * o.s.Cin + ci) * o.s.H + ihp * o.s.S + o.ph) * o.s.W + iwp * o.s.S + o.pw] = t;
+}
 
 // K range [k0, k1); chunk > 0 splits it over blockIdx.z (split-K, partial tiles per z)
 // blockIdx.z = group * zsub + split: groups are the population's agents (each
@@ -289,6 +330,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
     constexpr int NA = BM * BK / NT, NB = BK * BN / NT;
     const int split = (int)blockIdx.z % zsub;
     const Ops ops = ops_g.at((int)blockIdx.z / zsub);
+    k1 = ops.kend(k1);
     if (chunk > 0) {
         k0 += split * chunk;
         k1 = k0 + chunk < k1 ? k0 + chunk : k1;
@@ -415,6 +457,37 @@ static void wgrad_plan(const Shape &s, int groups, int &splits, int &chunk) {
     splits = (int)ceil_div(P, chunk);
 }
 
+// dgrad: the largest phase's GEMM (phase 0) and a split-K plan from the layer
+// shape alone: one group's (phase, tile, split) workgroups >= kDgradFill, each
+// split at least 16 K steps
+constexpr int kDgradFill = 384;
+struct DgradPlan {
+    int nph, Nmax, Kmax, splits, chunk;
+};
+static DgradPlan dgrad_plan(const Shape &s) {
+    DgradPlan d;
+    d.nph = s.S * s.S;
+    d.Nmax = s.B * (int)ceil_div(s.H, s.S) * (int)ceil_div(s.W, s.S);
+    d.Kmax = s.Cout * (int)ceil_div(s.KH, s.S) * (int)ceil_div(s.KW, s.S);
+    const int M = s.Cin;
+    const int tiles = (M <= 32 ? (int)ceil_div(d.Nmax, 128) : (int)(ceil_div(d.Nmax, 64) * ceil_div(M, 64))) * d.nph;
+    int want = (int)ceil_div(kDgradFill, tiles);
+    const int most = d.Kmax / (16 * BK);
+    if (want > most) want = most;
+    if (want < 1) want = 1;
+    d.chunk = (int)(ceil_div(ceil_div(d.Kmax, want), BK) * BK);
+    d.splits = (int)ceil_div(d.Kmax, d.chunk);
+    if (d.splits <= 1) {
+        d.splits = 1;
+        d.chunk = 0;
+    }
+    return d;
+}
+static size_t dgrad_workspace_bytes(const Shape &s, int groups) {
+    const DgradPlan d = dgrad_plan(s);
+    return d.splits > 1 ? (size_t)groups * d.nph * d.splits * s.Cin * d.Nmax * sizeof(float) : 0;
+}
+
 }  // namespace conv
 
 }  // namespace agx
@@ -475,7 +548,10 @@ extern "C" size_t agx_conv2d_wgrad_workspace_bytes_grouped(const agx_conv2d_shap
     if (check_shape(shape, s, "agx_conv2d_wgrad_workspace_bytes") || groups < 1) return 0;
     int splits = 1, chunk = 0;
     wgrad_plan(s, (int)groups, splits, chunk);
-    return (size_t)groups * splits * s.Cout * (s.Cin * s.KH * s.KW + 1) * sizeof(float);
+    // one workspace serves the wgrad partials and then (stream-ordered) the dgrad ones
+    const size_t wb = (size_t)groups * splits * s.Cout * (s.Cin * s.KH * s.KW + 1) * sizeof(float);
+    const size_t db = dgrad_workspace_bytes(s, (int)groups);
+    return wb > db ? wb : db;
 }
 
 extern "C" size_t agx_conv2d_wgrad_workspace_bytes(const agx_conv2d_shape *shape) {
@@ -516,15 +592,13 @@ extern "C" int agx_conv2d_backward_grouped(const agx_conv2d_shape *shape, int64_
     if (int rc = check_launch("agx_conv2d_backward wgrad")) return rc;
     if (dx) {
         AGX_REQUIRE(!x_is_u8, "agx_conv2d_backward: no data gradient for a u8 input layer");
-        for (int ph = 0; ph < s.S; ++ph)
-            for (int pw = 0; pw < s.S; ++pw) {
-                const int Hp = (int)ceil_div(s.H - ph, s.S), Wp = (int)ceil_div(s.W - pw, s.S);
-                const int nA = (int)ceil_div(s.KH - ph, s.S), nB = (int)ceil_div(s.KW - pw, s.S);
-                if (Hp <= 0 || Wp <= 0) continue;
-                DgradOps o{w, dy, y_act, dx, s, s.Cin, s.B * Hp * Wp, s.Cout * (nA > 0 ? nA : 0) * (nB > 0 ? nB : 0),
-                           ph, pw, Hp, Wp, nA, nB, w_gstride, y_gstride, x_gstride};
-                launch(o, o.M, o.N, 0, o.K, 0, 1, G, st);  // K = 0 (no tap reaches this phase): zeros
-            }
+        const DgradPlan d = dgrad_plan(s);
+        DgradOps o{w, dy, y_act, dx, d.splits > 1 ? part : nullptr, s, s.Cin, 0, 0, 0, 0, 0, 0, 0, 0,
+                   d.nph, d.Nmax, d.splits, w_gstride, y_gstride, x_gstride};
+        const int gp_ = G * d.nph;  // (group, phase) pairs
+        launch(o, o.M, d.Nmax, 0, d.Kmax, d.chunk, d.splits, gp_, st);
+        if (d.splits > 1)
+            dgrad_reduce_kernel<<<dim3((unsigned)ceil_div((size_t)s.Cin * d.Nmax, 256), (unsigned)gp_), 256, 0, st>>>(o);
         if (int rc = check_launch("agx_conv2d_backward dgrad")) return rc;
     }
     return AGX_OK;

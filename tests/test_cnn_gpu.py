@@ -38,6 +38,7 @@ SHAPES = [
     (3, 7, 11, 11, 9, 2, 2),
     (2, 72, 12, 12, 40, 5, 1),  # K = 1800: gather tables rebuilt per 1024-entry chunk
     (2, 3, 14, 14, 6, 2, 3),    # k < stride: input phases no tap reaches (zero data gradient)
+    (128, 64, 9, 9, 128, 3, 1),  # config 5's third layer at its batch: the dgrad split-K plan of the bench
 ]
 
 
@@ -270,11 +271,22 @@ def test_config3_pong_rainbow_generation():
     for h in hooks:
         h.remove()
     clip = min(1.0, 10.0 / (float(torch.nn.utils.clip_grad_norm_(ref_actor.parameters(), 10.0)) + 1e-6))
+    # below the top conv, grad output itself carries the rounding of the data
+    # gradients above it: its conditioning is |grad output| propagated down
+    # through |W| and the ReLU masks (a summation-order change in any dgrad moves
+    # it by that much, not by |grad output|)
+    gyc = [None] * len(convs)
+    gyc[-1] = seen[convs[-1]][1].abs()
+    for i in range(len(convs) - 2, -1, -1):
+        up = convs[i + 1]
+        x_up = seen[up][0]
+        prop = torch.nn.grad.conv2d_input(x_up.shape, up.weight.detach().abs(), gyc[i + 1], stride=up.stride)
+        gyc[i] = torch.maximum(seen[convs[i]][1].abs(), prop * (x_up > 0))
     cond = {}
-    for m in convs:
-        x, gy = seen[m]
-        cond[id(m.weight)] = clip * torch.nn.grad.conv2d_weight(x.abs(), m.weight.shape, gy.abs(), stride=m.stride)
-        cond[id(m.bias)] = clip * gy.abs().sum((0, 2, 3))
+    for m, gc in zip(convs, gyc):
+        x = seen[m][0]
+        cond[id(m.weight)] = clip * torch.nn.grad.conv2d_weight(x.abs(), m.weight.shape, gc, stride=m.stride)
+        cond[id(m.bias)] = clip * gc.sum((0, 2, 3))
     ref_opt.step()
     loss, _, new_pri = agent.learn(exp, per=True)
     assert abs(loss - loss_ref.item()) <= 1e-5 * abs(loss_ref.item())
