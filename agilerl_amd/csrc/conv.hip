@@ -49,15 +49,25 @@ struct Smem {
     float As[2][BK][LDA];  // As[k][m]
     float Bs[2][BK][LDB];  // Bs[k][n]
     int tabA[kTab], tabB[kTab];
+    float lut[256];  // u8 inputs: the normalised value of each byte, (b - low) / (high - low)
     // dgrad: per output column, oh of tap kh / ow of tap kw (-1: no tap); rows padded
     // to an odd word count: lanes read 64 different columns' entry a, and a 32-word
     // row stride put them all in one LDS bank
     int col[BN][2 * kTapMax + 1];
 };
 
-__device__ __forceinline__ float ld_x(const void *x, int o, bool u8, float lo, float rng) {
-    if (u8) return ((float)static_cast<const unsigned char *>(x)[o] - lo) / rng;  // IEEE division, as the reference
-    return static_cast<const float *>(x)[o];
+// u8 layers: the per-element IEEE division (a dozen VALU ops in every gather)
+// becomes a read of the workgroup's 256-entry table of the same quotients
+template <bool U8, class SM>
+__device__ __forceinline__ float ld_xt(const void *x, int o, const SM &sm) {
+    if constexpr (U8) return sm.lut[static_cast<const unsigned char *>(x)[o]];
+    else return static_cast<const float *>(x)[o];
+}
+template <bool U8, class SM>
+__device__ __forceinline__ void fill_lut(SM &sm, int tid, float lo, float rng) {
+    // visible to the gathers after the barrier that opens the first K chunk
+    if constexpr (U8)
+        if (tid < 256) sm.lut[tid] = ((float)tid - lo) / rng;
 }
 
 // ---- forward -------------------------------------------------------------
@@ -85,7 +95,8 @@ struct FwdOps {
         int xbase;  // input offset of this thread's output pixel, -1 past N
     };
     template <class SM>
-    __device__ void setup(Ctx &c, SM &, int, int n, int) const {
+    __device__ void setup(Ctx &c, SM &sm, int, int n, int tid) const {
+        fill_lut<U8>(sm, tid, lo, rng);
         if (n < N) {
             const int ow = n % s.OW, t = n / s.OW, oh = t % s.OH, bb = t / s.OH;
             c.xbase = ((bb * s.Cin) * s.H + oh * s.S) * s.W + ow * s.S;
@@ -112,7 +123,7 @@ struct FwdOps {
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
             const int kk = kb + tid / BN + i * (NT / BN);
-            rb[i] = (c.xbase >= 0 && kk < k1) ? ld_x(x, c.xbase + sm.tabB[kk - kc], U8, lo, rng) : 0.f;
+            rb[i] = (c.xbase >= 0 && kk < k1) ? ld_xt<U8>(x, c.xbase + sm.tabB[kk - kc], sm) : 0.f;
         }
     }
     __device__ void store(int m, int n, float v, int) const {
@@ -148,7 +159,8 @@ struct WgradOps {
         int koff;  // im2col offset of this thread's weight column; -2: the ones column, -1: past N
     };
     template <class SM>
-    __device__ void setup(Ctx &c, SM &, int, int n, int) const {
+    __device__ void setup(Ctx &c, SM &sm, int, int n, int tid) const {
+        fill_lut<U8>(sm, tid, lo, rng);
         if (n < N - 1) {
             const int kw = n % s.KW, t = n / s.KW, kh = t % s.KH, ci = t / s.KH;
             c.koff = (ci * s.H + kh) * s.W + kw;
@@ -186,7 +198,7 @@ struct WgradOps {
         for (int i = 0; i < NB; ++i) {
             const int pp = kb + tid / BN + i * (NT / BN);
             float v = 0.f;
-            if (pp < k1) v = c.koff >= 0 ? ld_x(x, sm.tabB[pp - kc] + c.koff, U8, lo, rng) : (c.koff == -2 ? 1.f : 0.f);
+            if (pp < k1) v = c.koff >= 0 ? ld_xt<U8>(x, sm.tabB[pp - kc] + c.koff, sm) : (c.koff == -2 ? 1.f : 0.f);
             rb[i] = v;
         }
     }
