@@ -91,6 +91,7 @@ struct FwdOps {
         return o;
     }
     __device__ int kend(int k1) const { return k1; }
+    static constexpr bool kRowSum = false;
     struct Ctx {
         int xbase;  // input offset of this thread's output pixel, -1 past N
     };
@@ -155,8 +156,12 @@ struct WgradOps {
         return o;
     }
     __device__ int kend(int k1) const { return k1; }
+    // db (column N - 1) is the row sum of the A operand (dZ), taken from LDS by
+    // the n_blk == 0 tiles: a GEMM ones column would cost a whole extra column
+    // tile (re-gathering all of A) when Cin*KH*KW is a multiple of the tile width
+    static constexpr bool kRowSum = true;
     struct Ctx {
-        int koff;  // im2col offset of this thread's weight column; -2: the ones column, -1: past N
+        int koff;  // im2col offset of this thread's weight column, -1 past the weights
     };
     template <class SM>
     __device__ void setup(Ctx &c, SM &sm, int, int n, int tid) const {
@@ -165,7 +170,7 @@ struct WgradOps {
             const int kw = n % s.KW, t = n / s.KW, kh = t % s.KH, ci = t / s.KH;
             c.koff = (ci * s.H + kh) * s.W + kw;
         } else {
-            c.koff = n == N - 1 ? -2 : -1;
+            c.koff = -1;
         }
     }
     template <class SM>
@@ -198,7 +203,7 @@ struct WgradOps {
         for (int i = 0; i < NB; ++i) {
             const int pp = kb + tid / BN + i * (NT / BN);
             float v = 0.f;
-            if (pp < k1) v = c.koff >= 0 ? ld_xt<U8>(x, sm.tabB[pp - kc] + c.koff, sm) : (c.koff == -2 ? 1.f : 0.f);
+            if (pp < k1 && c.koff >= 0) v = ld_xt<U8>(x, sm.tabB[pp - kc] + c.koff, sm);
             rb[i] = v;
         }
     }
@@ -247,6 +252,7 @@ struct DgradOps {
         return o;
     }
     __device__ int kend(int) const { return K; }  // this phase's taps (0: zeros)
+    static constexpr bool kRowSum = false;
     struct Ctx {
         int dbase;  // dy offset of this thread's image (channel 0), -1 past N
         int c;      // column within the tile
@@ -367,6 +373,8 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
         for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
     const int wm = (wave % (BM / 32)) * 32, wn = (wave / (BM / 32)) * 32;  // this wave's 32x32 sub-tile
     const int r = lane & 15, q = lane >> 4;
+    const bool rsum = Ops::kRowSum && n_blk == 0 && tid < BM;  // wgrad db: A's row sums
+    float rs = 0.f;
     for (int kc = k0; kc < k1; kc += kTab) {
         const int kce = kc + kTab < k1 ? kc + kTab : k1;
         __syncthreads();  // previous chunk's tables and operands consumed
@@ -388,6 +396,11 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
                 acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
                 acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
             }
+            if constexpr (Ops::kRowSum)
+                if (rsum) {
+#pragma unroll
+                    for (int kk = 0; kk < BK; ++kk) rs += sm.As[buf][kk][tid];
+                }
             if (more) {
                 stash(buf ^ 1);
                 __syncthreads();
@@ -401,8 +414,13 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-                ops.store(m_blk + wm + 16 * i + 4 * q + e, n_blk + wn + 16 * j + r, acc[i][j][e], split);
+            for (int e = 0; e < 4; ++e) {
+                const int n = n_blk + wn + 16 * j + r;
+                if (!Ops::kRowSum || n < ops.N - 1)  // column N - 1 (db) belongs to the row sums
+                    ops.store(m_blk + wm + 16 * i + 4 * q + e, n, acc[i][j][e], split);
+            }
+    if constexpr (Ops::kRowSum)
+        if (rsum) ops.store(m_blk + tid, ops.N - 1, rs, split);
 }
 
 // fixed-order sum of the wgrad split partials, in two parallel stages (a
@@ -461,7 +479,7 @@ static void launch(const Ops &o, int M, int N, int k0, int k1, int chunk, int sp
 // several times over, each split a multiple of BK and at least 64 reduction
 // steps long
 static void wgrad_plan(const Shape &s, int groups, int &splits, int &chunk) {
-    const int M = s.Cout, N = s.Cin * s.KH * s.KW + 1, P = s.B * s.OH * s.OW;
+    const int M = s.Cout, N = s.Cin * s.KH * s.KW, P = s.B * s.OH * s.OW;  // N: the GEMM's weight columns
     const int tiles = (M <= 32 ? (int)ceil_div(N, 128) : (int)(ceil_div(N, 64) * ceil_div(M, 64))) * groups;
     int want = (int)ceil_div(1024, tiles);
     chunk = (int)(ceil_div(ceil_div(P, want), BK) * BK);
@@ -590,10 +608,10 @@ extern "C" int agx_conv2d_backward_grouped(const agx_conv2d_shape *shape, int64_
     const long long gp = (long long)splits * M * N;
     if (x_is_u8) {
         WgradOps<true> o{dy, y_act, x, x_low, x_high - x_low, part, s, M, N, P, x_gstride, y_gstride, gp};
-        launch(o, M, N, 0, P, chunk, splits, G, st);
+        launch(o, M, N - 1, 0, P, chunk, splits, G, st);
     } else {
         WgradOps<false> o{dy, y_act, x, 0.f, 1.f, part, s, M, N, P, x_gstride, y_gstride, gp};
-        launch(o, M, N, 0, P, chunk, splits, G, st);
+        launch(o, M, N - 1, 0, P, chunk, splits, G, st);
     }
     // dW / db of group g land densely at dw + g*Cout*K, db + g*Cout
     const int rgroups = (int)ceil_div(splits, kRedG);
