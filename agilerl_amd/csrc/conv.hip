@@ -43,7 +43,7 @@ struct Shape {
 };
 
 // per-workgroup LDS: operand double buffers + gather tables
-template <int BM, int BN>
+template <int BM, int BN, bool COLS>
 struct Smem {
     static constexpr int LDA = BM + 16, LDB = BN + 16;
     float As[2][BK][LDA];  // As[k][m]
@@ -53,7 +53,8 @@ struct Smem {
     // dgrad: per output column, oh of tap kh / ow of tap kw (-1: no tap); rows padded
     // to an odd word count: lanes read 64 different columns' entry a, and a 32-word
     // row stride put them all in one LDS bank
-    int col[BN][2 * kTapMax + 1];
+    // (dgrad only: the forward / wgrad workgroups leave its ~17 KB to occupancy)
+    int col[COLS ? BN : 1][2 * kTapMax + 1];
 };
 
 // u8 layers: the per-element IEEE division (a dozen VALU ops in every gather)
@@ -91,7 +92,7 @@ struct FwdOps {
         return o;
     }
     __device__ int kend(int k1) const { return k1; }
-    static constexpr bool kRowSum = false;
+    static constexpr bool kRowSum = false, kCols = false;
     struct Ctx {
         int xbase;  // input offset of this thread's output pixel, -1 past N
     };
@@ -159,7 +160,7 @@ struct WgradOps {
     // db (column N - 1) is the row sum of the A operand (dZ), taken from LDS by
     // the n_blk == 0 tiles: a GEMM ones column would cost a whole extra column
     // tile (re-gathering all of A) when Cin*KH*KW is a multiple of the tile width
-    static constexpr bool kRowSum = true;
+    static constexpr bool kRowSum = true, kCols = false;
     struct Ctx {
         int koff;  // im2col offset of this thread's weight column, -1 past the weights
     };
@@ -252,7 +253,7 @@ struct DgradOps {
         return o;
     }
     __device__ int kend(int) const { return K; }  // this phase's taps (0: zeros)
-    static constexpr bool kRowSum = false;
+    static constexpr bool kRowSum = false, kCols = true;
     struct Ctx {
         int dbase;  // dy offset of this thread's image (channel 0), -1 past N
         int c;      // column within the tile
@@ -354,7 +355,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
         k1 = k0 + chunk < k1 ? k0 + chunk : k1;
     }
     if (k0 >= k1) k1 = k0;  // empty split: stores zeros
-    __shared__ Smem<BM, BN> sm;
+    __shared__ Smem<BM, BN, Ops::kCols> sm;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int m_blk = blockIdx.y * BM, n_blk = blockIdx.x * BN;
     typename Ops::Ctx ctx;
