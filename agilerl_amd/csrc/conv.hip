@@ -43,18 +43,18 @@ struct Shape {
 };
 
 // per-workgroup LDS: operand double buffers + gather tables
-template <int BM, int BN, bool COLS>
+template <int BM, int BN, bool COLS, bool LUT, int TAB>
 struct Smem {
     static constexpr int LDA = BM + 16, LDB = BN + 16;
     float As[2][BK][LDA];  // As[k][m]
     float Bs[2][BK][LDB];  // Bs[k][n]
-    int tabA[kTab], tabB[kTab];
-    float lut[256];  // u8 inputs: the normalised value of each byte, (b - low) / (high - low)
-    // dgrad: per output column, oh of tap kh / ow of tap kw (-1: no tap); rows padded
-    // to an odd word count: lanes read 64 different columns' entry a, and a 32-word
-    // row stride put them all in one LDS bank
-    // (dgrad only: the forward / wgrad workgroups leave its ~17 KB to occupancy)
-    int col[COLS ? BN : 1][2 * kTapMax + 1];
+    int tabA[TAB], tabB[TAB];
+    float lut[LUT ? 256 : 1];  // u8 inputs: the normalised value of each byte, (b - low) / (high - low)
+    // dgrad: per output column, oh of tap kh / ow of tap kw (-1: no tap), int16;
+    // rows padded to an odd word count: lanes read 64 different columns' entry a,
+    // and an even row stride put them in few LDS banks (forward / wgrad
+    // workgroups do not allocate it)
+    short col[COLS ? BN : 1][2 * kTapMax + 2];
 };
 
 // u8 layers: the per-element IEEE division (a dozen VALU ops in every gather)
@@ -92,7 +92,8 @@ struct FwdOps {
         return o;
     }
     __device__ int kend(int k1) const { return k1; }
-    static constexpr bool kRowSum = false, kCols = false;
+    static constexpr bool kRowSum = false, kCols = false, kLut = U8;
+    static constexpr int kTabN = kTab;
     struct Ctx {
         int xbase;  // input offset of this thread's output pixel, -1 past N
     };
@@ -160,7 +161,8 @@ struct WgradOps {
     // db (column N - 1) is the row sum of the A operand (dZ), taken from LDS by
     // the n_blk == 0 tiles: a GEMM ones column would cost a whole extra column
     // tile (re-gathering all of A) when Cin*KH*KW is a multiple of the tile width
-    static constexpr bool kRowSum = true, kCols = false;
+    static constexpr bool kRowSum = true, kCols = false, kLut = U8;
+    static constexpr int kTabN = kTab;
     struct Ctx {
         int koff;  // im2col offset of this thread's weight column, -1 past the weights
     };
@@ -253,7 +255,8 @@ struct DgradOps {
         return o;
     }
     __device__ int kend(int) const { return K; }  // this phase's taps (0: zeros)
-    static constexpr bool kRowSum = false, kCols = true;
+    static constexpr bool kRowSum = false, kCols = true, kLut = false;
+    static constexpr int kTabN = kTab / 2;  // with the tap table: 4 (32x128) / 5 (64x64) workgroups per CU
     struct Ctx {
         int dbase;  // dy offset of this thread's image (channel 0), -1 past N
         int c;      // column within the tile
@@ -355,7 +358,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
         k1 = k0 + chunk < k1 ? k0 + chunk : k1;
     }
     if (k0 >= k1) k1 = k0;  // empty split: stores zeros
-    __shared__ Smem<BM, BN, Ops::kCols> sm;
+    __shared__ Smem<BM, BN, Ops::kCols, Ops::kLut, Ops::kTabN> sm;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int m_blk = blockIdx.y * BM, n_blk = blockIdx.x * BN;
     typename Ops::Ctx ctx;
@@ -376,8 +379,8 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
     const int r = lane & 15, q = lane >> 4;
     const bool rsum = Ops::kRowSum && n_blk == 0 && tid < BM;  // wgrad db: A's row sums
     float rs = 0.f;
-    for (int kc = k0; kc < k1; kc += kTab) {
-        const int kce = kc + kTab < k1 ? kc + kTab : k1;
+    for (int kc = k0; kc < k1; kc += Ops::kTabN) {
+        const int kce = kc + Ops::kTabN < k1 ? kc + Ops::kTabN : k1;
         __syncthreads();  // previous chunk's tables and operands consumed
         ops.build(sm, kc, kce, tid);
         __syncthreads();
@@ -543,6 +546,7 @@ static int check_shape(const agx_conv2d_shape *sh, Shape &s, const char *who) {
                 who, kTapMax);
     s.OH = (s.H - s.KH) / s.S + 1;
     s.OW = (s.W - s.KW) / s.S + 1;
+    AGX_REQUIRE(s.OH < 32768 && s.OW < 32768, "%s: output height / width >= 32768 (int16 tap tables)", who);
     AGX_REQUIRE((int64_t)s.B * s.Cout * s.OH * s.OW < (1ll << 31) && (int64_t)s.B * s.Cin * s.H * s.W < (1ll << 31),
                 "%s: tensor too large for 32-bit indexing", who);
     return AGX_OK;
