@@ -47,6 +47,14 @@ import torch
 from ..modules.mlp import create_mlp
 from .nets import ActorCriticSpec
 
+# The reference collects each class's methods into ``list(set(...))``
+# (modules/base.py:570-571), so the table order is that of Python's string-hash
+# seed.  The order below is the one PYTHONHASHSEED=0 produces — the seed the
+# reference's own test runner sets (pyproject.toml:91) and the seed the
+# fixtures of tests/golden/gen_arch_golden.py are made under (META.json
+# ``arch_fixtures``).  A reference run under another seed samples from a
+# permuted table and draws other methods from the same Mutations.rng stream.
+METHOD_ORDER_HASH_SEED = "0"
 LAYER_METHODS = ["head_net.remove_layer", "head_net.add_layer"]
 NODE_METHODS = ["remove_latent_node", "add_latent_node", "encoder.add_node", "encoder.remove_node",
                 "head_net.add_node", "head_net.remove_node"]

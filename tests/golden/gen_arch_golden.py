@@ -31,16 +31,36 @@ algorithm builds its networks, so the fixture pins what the draws DO, for
 given draws.  Fresh weights of a recreated network come from torch's global
 CPU generator (seeded per case), as in the reference.
 
+Hash seed.  The reference builds each module's mutation-method table with
+``list(set(...))`` (agilerl/modules/base.py:570-571), so the table's ORDER —
+and with it which method ``rng.choice`` samples — depends on Python's string
+hash seed.  The reference's own test runner fixes it (pyproject.toml:91,
+``PYTHONHASHSEED=0``), and so does this generator: it refuses to run under any
+other seed and re-launches itself with ``PYTHONHASHSEED=0`` when the variable
+is unset, before anything is imported.  META.json records the seed under
+``arch_fixtures``; population/arch.py hard-codes the order that seed produces.
+
 Usage:  python tests/golden/gen_arch_golden.py [--ref /root/reference]
 """
 
 from __future__ import annotations
 
-import argparse
-import importlib.util
 import os
+import subprocess
 import sys
-import types
+
+HASH_SEED = "0"  # the reference's pytest setting, pyproject.toml:91
+if __name__ == "__main__" and os.environ.get("PYTHONHASHSEED") is None:
+    # the hash seed is fixed at interpreter start-up: re-launch before importing anything
+    sys.exit(subprocess.call([sys.executable, *sys.argv], env={**os.environ, "PYTHONHASHSEED": HASH_SEED}))
+if __name__ == "__main__" and os.environ.get("PYTHONHASHSEED") != HASH_SEED:
+    sys.exit(f"gen_arch_golden.py: PYTHONHASHSEED={os.environ['PYTHONHASHSEED']!r}; the fixtures pin the "
+             f"reference's method-table order under PYTHONHASHSEED={HASH_SEED} (agilerl/modules/base.py:570-571)")
+
+import argparse  # noqa: E402
+import importlib.util  # noqa: E402
+import json  # noqa: E402
+import types  # noqa: E402
 
 sys.dont_write_bytecode = True
 
@@ -247,6 +267,19 @@ def main() -> None:
     gen_cases(m, out)
     for name, arrays in out.items():
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
+    meta_path = os.path.join(HERE, "META.json")
+    meta = json.load(open(meta_path)) if os.path.exists(meta_path) else {}
+    meta["arch_fixtures"] = {
+        "generator": "tests/golden/gen_arch_golden.py",
+        "PYTHONHASHSEED": os.environ["PYTHONHASHSEED"],
+        "hash_seed_reason": "method tables are list(set(...)) (agilerl/modules/base.py:570-571); "
+                            "the reference's pytest runs under PYTHONHASHSEED=0 (pyproject.toml:91)",
+        "torch": torch.__version__,
+        "numpy": np.__version__,
+        "groups": sorted(out),
+    }
+    with open(meta_path, "w") as f:
+        json.dump(meta, f, indent=1)
     print(f"wrote {len(out)} fixture groups: {sorted(out)}")
 
 

@@ -989,7 +989,9 @@ def main() -> None:
         groups_all = sorted(set(old.get("groups", [])) | set(groups))
     else:
         groups_all = sorted(groups)
+    prev = json.load(open(os.path.join(HERE, "META.json"))) if os.path.exists(os.path.join(HERE, "META.json")) else {}
     meta = {
+        **{k: v for k, v in prev.items() if k == "arch_fixtures"},  # gen_arch_golden.py's record
         "generator": "tests/golden/gen_golden.py",
         "torch": torch.__version__,
         "numpy": np.__version__,

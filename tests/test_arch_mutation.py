@@ -61,3 +61,21 @@ def test_arch_mutation_matches_reference(golden, case):
     for k, (o, sh) in keys.items():
         got = new_flat[o:o + int(np.prod(sh))].view(sh).numpy()
         assert np.array_equal(got, g["after." + k]), k
+
+
+def test_arch_fixtures_record_the_reference_hash_seed():
+    """The method tables are list(set(...)) in the reference
+    (agilerl/modules/base.py:570-571): their order, and so every sampled
+    method, depends on PYTHONHASHSEED.  The fixtures were made under the
+    reference's pytest seed (pyproject.toml:91) and META.json must say so;
+    population/arch.py's METHODS is the order that seed produces."""
+    import json
+    import os
+
+    from agilerl_amd.population import arch
+
+    meta = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "META.json")))
+    rec = meta["arch_fixtures"]
+    assert rec["PYTHONHASHSEED"] == "0"
+    assert sorted(rec["groups"]) == sorted(CASES)
+    assert arch.METHOD_ORDER_HASH_SEED == rec["PYTHONHASHSEED"]
