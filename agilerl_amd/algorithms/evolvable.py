@@ -22,6 +22,8 @@ from ..modules.mlp import EvolvableMLP
 
 
 class EvolvableAgentMixin:
+    sharded = False  # set by create_population when the agent is one shard of a global population
+
     #: learning-rate attribute -> the optimizer attribute it drives
     _lr_optimizers: dict[str, str] = {"lr": "optimizer"}
     #: (eval network attribute, shared network attribute) of the policy group
@@ -44,12 +46,12 @@ class EvolvableAgentMixin:
         """MLP-encoder Q networks (the encoder's and head's node / layer
         mutations and the latent's); CNN encoders and multi-agent ModuleDicts
         are not mutated."""
-        import torch.distributed as dist
-
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            # a sharded population replays every global agent's draws on every
-            # rank (hpo/shard.py RemoteAgent); the module and init draws of a
-            # Q-network mutation are not replayed: not applied anywhere
+        if getattr(self, "sharded", False):
+            # a population sharded over ranks replays every global agent's draws
+            # on every rank (hpo/shard.py RemoteAgent); the module and init draws
+            # of a Q-network mutation are not replayed: not applied anywhere.
+            # (Ranks that each train a population of their own, create_population
+            # shard=False, mutate as a single process does.)
             return False
         net = getattr(self, self._policy_group[0])
         return isinstance(getattr(net, "encoder", None), EvolvableMLP) and \

@@ -57,8 +57,11 @@ import torch
 
 
 def set_global_seed(seed: int | None) -> None:
-    """mutation.py:41-54 (fastrand is not installed: its pcg32 stream only
-    feeds architecture mutations, which are not applied here)."""
+    """mutation.py:41-54.  The reference also seeds fastrand there; fastrand
+    is not installed, and nothing on this path draws from it (the reference
+    only seeds it: the architecture mutations draw from Mutations.rng, the
+    modules' numpy generators and torch's global generator, all seeded or
+    replayed here)."""
     if seed is None:
         return
     np.random.seed(seed)
@@ -154,12 +157,9 @@ class Mutations:
             individual.mut = "None"
             return individual
         net = getattr(individual, "actor", None)
-        import torch.distributed as dist
-
-        if net is None or not hasattr(net, "change_activation") or (
-                dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
-            # sharded populations: the recreated modules' draws are not replayed on
-            # the other ranks (hpo/shard.py), so no rank applies it
+        if net is None or not hasattr(net, "change_activation") or getattr(individual, "sharded", False):
+            # populations sharded over ranks: the recreated modules' draws are not
+            # replayed on the other ranks (hpo/shard.py), so no rank applies it
             return self._not_applied(individual, "activation")
         if net.activation is None:  # :489-499
             warnings.warn("Found no activation mutation capabilities. We advise setting the probability to "

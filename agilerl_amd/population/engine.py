@@ -101,6 +101,16 @@ class PopulationEngine:
         # every global slot's (S, E, K-defining learn_step): refreshed after mutations
         self.global_plan = [(population.S, population.update_epochs, learn_step)] * (self.P * world)
         self._gen_state = None  # numpy state before the generation's shuffles (target_kl re-sync)
+        # Sampling-noise counters.  A slot's Philox / Gumbel key is (seed_base,
+        # global env index, counter); a group built by regroup() starts at
+        # counter 0, so the counters are set from engine-level counts that every
+        # rank shares: generation g's rollouts use counters from g << 24 (a
+        # generation's vector steps stay far below 2^24), and the k-th
+        # evaluation of the run its own round.  Neither depends on how slots are
+        # grouped, so a sharded run and the single-process run draw alike.
+        self._generation = 0
+        self._eval_calls = getattr(population, "eval_rounds", 0)
+        self._counter0 = -(-int(population.act_counter) // (1 << 24)) << 24  # past any earlier use
         self.refresh_plan()
         if self.singleton and self.P > 1:
             self.regroup(self.local_states())
@@ -172,16 +182,25 @@ class PopulationEngine:
     def resync_numpy_after_generation(self, evo_steps: int) -> None:
         """target_kl: the reference draws one shuffle per epoch an agent
         actually runs; re-advance the global stream from the generation's
-        start by exactly those (single process; see PPOPopulation)."""
+        start by exactly those, over the global population (every rank
+        replays the same re-advance; see PPOPopulation)."""
         pops = [g.pop for g in self.groups]
-        if self._gen_state is None or all(p.target_kl is None for p in pops) or self.world > 1:
+        if self._gen_state is None or all(p.target_kl is None for p in pops):
             return
-        ran_of = {}
+        ran_local = [None] * self.P
         for g in self.groups:
             rows = [t.cpu().numpy() for t in g.pop._gen_ran]
             for r, slot in enumerate(g.slots):
-                ran_of[slot] = [int(x[r]) for x in rows]
-        full = all(ran_of[j] == [self.global_plan[j][1]] * len(ran_of[j]) for j in range(self.P))
+                ran_local[slot] = [int(x[r]) for x in rows]
+        if self.world > 1:
+            # every rank replays the GLOBAL re-advance: each slot's epochs run
+            # (a few ints per agent) gathered like refresh_plan's plan
+            box: list = [None] * self.world
+            dist.all_gather_object(box, ran_local)
+            ran_of = [x for b in box for x in b]
+        else:
+            ran_of = ran_local
+        full = all(ran_of[j] == [self.global_plan[j][1]] * len(ran_of[j]) for j in range(len(ran_of)))
         if full:
             return
         np.random.set_state(self._gen_state)
@@ -196,7 +215,12 @@ class PopulationEngine:
         """Every group runs its agents' iterations of the generation; ->
         per-iteration mean losses (host arrays, slot order where known)."""
         losses = []
+        base = self._counter0 + (self._generation << 24)
+        self._generation += 1
         for g in self.groups:
+            if g.pop.act_counter > base:
+                raise RuntimeError(f"rollout counter {g.pop.act_counter} overran generation {self._generation - 2}")
+            g.pop.act_counter = base
             for _ in range(self.iterations(evo_steps, g.learn_step)):
                 loss = g.runner.iteration()
                 g.pop.check_errors()
@@ -220,7 +244,9 @@ class PopulationEngine:
 
     def evaluate(self, loop: int, max_steps) -> list[float]:
         out = [0.0] * self.P
+        self._eval_calls += 1
         for g in self.groups:
+            g.pop.eval_rounds = self._eval_calls - 1  # runner.evaluate counts this round in
             f = g.runner.evaluate(loop=loop, max_steps=max_steps)
             for r, slot in enumerate(g.slots):
                 out[slot] = float(f[r])

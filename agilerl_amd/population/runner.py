@@ -438,9 +438,11 @@ class PopulationRunner:
         runs rollout -> GAE -> learner back to back with no host launch gap
         (the host-side launch work overlaps the rollout instead of sitting
         between it and the learner).  Same launches, same order, same data as
-        collect() + finish_rollout() + learn().  If the host loop raises, the
-        workgroups are released and the queued GAE / learner run on the
-        partial rollout before the exception propagates."""
+        collect() + finish_rollout() + learn().  If the host loop raises (or
+        the pacing times out), the workgroups are released with the abort /
+        timeout word set in the control block; the queued learner reads that
+        word first (``skip_if_set``) and returns without touching parameters
+        or Adam state, and the exception propagates."""
         if self._ios is None:
             self._build_ios()
         if not self.started:

@@ -62,6 +62,23 @@ def _population_env(env, P: int, N: int, offset: int = 0):
                      f"shared env, cloned per agent) or population_size x num_envs = {P * N}")
 
 
+def _check_env_allows_mutations(engine, mutation, pop) -> None:
+    """Architecture and learn_step mutations give agents their own networks /
+    rollout lengths, and such agents need an env each (the reference's
+    shared N-env, cloned per agent, or a StackedVecEnv).  One undivided
+    vector env of P x N envs keeps the whole population in one group: refuse
+    it at start-up rather than after the first such mutation."""
+    if mutation is None or engine.slot_envs is not None or engine.P == 1:
+        return
+    arch = float(getattr(mutation, "architecture_mut", 0.0) or 0.0) > 0
+    hp = getattr(getattr(pop[0], "registry", None), "hp_config", None)
+    ls = bool(hp) and "learn_step" in hp.names() and float(getattr(mutation, "rl_hp_mut", 0.0) or 0.0) > 0
+    if arch or ls:
+        raise ValueError("architecture / learn_step mutations need one env per agent: pass the reference's "
+                         f"num_envs = {engine.N} env (cloned per agent) or a StackedVecEnv of "
+                         f"{engine.P} envs, not one vector env of {engine.P * engine.N}")
+
+
 def _clone_host_attributes(pop, parents: list[int], elitism: bool, records: list[dict], rank: int = 0) -> None:
     """The attributes TournamentSelection._select_standard_agents gives the
     clones (tournament.py:71-119 + clone/copy_attributes, core/base.py:
@@ -161,6 +178,7 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
     # a custom collector fills one agent's rollout at a time (the reference's
     # per-agent loop, :216-248): every agent then learns in a group of its own
     engine = PopulationEngine(population, pop, env, world, rank, singleton=collect_rollouts_fn is not None)
+    _check_env_allows_mutations(engine, mutation, pop)
     sync = None
     if tournament is not None and mutation is not None:  # the reference selects only with both (:440)
         sync = PopulationSync(population, engine.groups[0].runner, world, rank, seed=None,

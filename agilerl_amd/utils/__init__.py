@@ -70,6 +70,8 @@ def create_population(algo: str, net_config: dict[str, Any] | None, INIT_HP: dic
         agents = [cls.from_init_hp(observation_space, action_space, net_config, INIT_HP, index=i, device=device,
                                    hp_config=hp_config, **algo_kwargs)
                   for i in range(population_size if shard else P)]
+        for a in agents:
+            a.sharded = bool(shard and world > 1)
         return agents[lo:lo + P]
     if algo == "MADDPG":  # utils/utils.py:590-618
         from ..algorithms.maddpg import MADDPG
@@ -83,6 +85,8 @@ def create_population(algo: str, net_config: dict[str, Any] | None, INIT_HP: dic
         agents = [MADDPG(observation_space, action_space, agent_ids=INIT_HP["AGENT_IDS"], index=i,
                          net_config=net_config, device=device, hp_config=hp_config, **hp, **algo_kwargs)
                   for i in range(population_size if shard else P)]
+        for a in agents:
+            a.sharded = bool(shard and world > 1)
         return agents[lo:lo + P]
     raise NotImplementedError(f"algorithm {algo!r} is outside the agx hot path (PPO, DQN, Rainbow DQN, MADDPG)")
 

@@ -181,3 +181,47 @@ def test_grouped_learner_single_update_on_mutated_shape():
             close(f"{p} {name} m", pop.opt.exp_avg[p, off:off + k].cpu(), out["exp_avg"][name].reshape(-1), 1e-4)
             close(f"{p} {name} v", pop.opt.exp_avg_sq[p, off:off + k].cpu(), out["exp_avg_sq"][name].reshape(-1),
                   1e-4)
+
+
+def test_regroup_does_not_replay_sampling_noise():
+    """a group that regroup() builds starts a fresh PPOPopulation
+    (act_counter 0).  The engine sets every group's counter from the
+    generation count, so the counters one slot's rollouts use in the
+    generation after a regroup lie beyond every counter of the generation
+    before it (its Philox / Gumbel draws are not replayed), and evaluation
+    rounds keep counting."""
+    from agilerl_amd.envs import StackedVecEnv
+    from agilerl_amd.population.engine import PopulationEngine
+
+    np.random.seed(2)
+    torch.manual_seed(2)
+    env, pop, _ = _ppo_yaml_population(P=2)
+    engine = PopulationEngine(pop[0].population, pop, StackedVecEnv.from_shared(env, 2))
+    used: dict[int, list[tuple[int, int]]] = {0: [], 1: []}
+
+    def record(gen):
+        def hook(g):
+            for slot in g.slots:
+                used[gen].append((slot, int(g.pop.act_counter)))
+        return hook
+
+    engine.draw_generation_perms(256)
+    engine.train(256, on_iteration=record(0))
+    ev0 = [g.pop.eval_rounds for g in engine.groups if hasattr(g.pop, "eval_rounds")]
+    engine.evaluate(1, 8)
+    a = pop[1]
+    rng = np.random.default_rng(3)
+    for _ in range(10):
+        a.architecture_mutation(0.5, rng)
+        if a.spec.shape_key() != pop[0].spec.shape_key():
+            break
+    engine.regroup(engine.local_states())
+    assert len(engine.groups) == 2
+    engine.draw_generation_perms(256)
+    engine.train(256, on_iteration=record(1))
+    engine.evaluate(1, 8)
+    for slot in (0, 1):
+        before = max(c for s, c in used[0] if s == slot)
+        after = min(c for s, c in used[1] if s == slot)
+        assert after > before, (slot, before, after)
+    assert all(g.pop.eval_rounds == 2 for g in engine.groups), (ev0, [g.pop.eval_rounds for g in engine.groups])
