@@ -56,7 +56,7 @@ constexpr int kNT = 512;
 constexpr int kNW = kNT / kWave;  // 8 waves
 constexpr int kSB = 32;           // rows per sub-batch
 constexpr int kMaxSlot = 10;      // dW tiles per wave
-constexpr int kMaxK = 8;          // partner workgroups per agent
+constexpr int kMaxK = 16;         // partner workgroups per agent
 constexpr int kMaxPT = 32;        // LDS parameter slots per thread: 8 float4 chunks
 constexpr int kMaxA = 16;
 constexpr int kMaxBlk = 28;
@@ -258,6 +258,9 @@ constexpr LearnPlan make_plan(NetDims d) {
 // ---------------------------------------------------------------------------
 // instantiated shapes: (obs_dim, actions, encoder widths..., head_actor, head_critic)
 // ---------------------------------------------------------------------------
+#ifdef AGX_BENCH_SHAPE_ONLY  // diagnostic builds (tools/): the config-2 shape alone, a quarter of the compile time
+#define AGX_PPO_SHAPES(X) X(8, 4, 2, 64, 64, 0, 64, 64)
+#else
 #define AGX_PPO_SHAPES(X)                 \
     X(8, 4, 2, 64, 64, 0, 64, 64)  /* LunarLander config 2 (ppo.yaml) */ \
     X(4, 2, 2, 64, 64, 0, 64, 64)  /* CartPole */                        \
@@ -266,6 +269,7 @@ constexpr LearnPlan make_plan(NetDims d) {
     X(4, 2, 2, 64, 64, 0, 64, 16)                                        \
     X(8, 4, 3, 64, 64, 32, 32, 16) /* PPO with no net_config: encoder [64, 64] -> latent 32, heads [32] / [16] */ \
     X(4, 2, 3, 64, 64, 32, 32, 16)
+#endif
 
 template <int D_, int A_, int NE_, int E0, int E1, int E2, int HA, int HC>
 struct Shape {
@@ -295,20 +299,39 @@ __device__ __forceinline__ float row_max(float v) {
     v = fmaxf(v, dpp<0x140>(v));
     return v;
 }
-// W-lane row sum (W = 16: one DPP row; W = 32: + the other 16-lane half, lane ^ 16)
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+// W-lane row sum (W = 16: one DPP row; W = 32: + the other 16-lane half,
+// lane ^ 16; W = 64: + the other 32-lane half through two readlanes, a
+// wave-uniform sum in the fixed order (lanes 0-31) + (lanes 32-63))
 template <int W>
 __device__ __forceinline__ float wrow_sum(float v) {
     v = row_sum(v);
-    if constexpr (W == 32)
+    if constexpr (W >= 32)
         v += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401f));
+    if constexpr (W == 64) v = readlane_f(v, 0) + readlane_f(v, 32);
+    return v;
+}
+template <int W>
+__device__ __forceinline__ float wrow_max(float v) {
+    v = row_max(v);
+    if constexpr (W >= 32)
+        v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401f)));
+    if constexpr (W == 64) v = fmaxf(readlane_f(v, 0), readlane_f(v, 32));
     return v;
 }
 // row slot of this lane: W = 16: wave + 8 * (lane / 16) (4 rows per wave);
-// W = 32: 2 * wave + lane / 32 (2 rows per wave, a 16-row sub-batch fills all lanes)
+// W = 32: 2 * wave + lane / 32 (2 rows per wave, a 16-row sub-batch fills all lanes);
+// W = 64: the wave (one row per wave, an 8-row sub-batch fills all lanes)
 template <int W>
 __device__ __forceinline__ int wrow(int lane, int wave) {
-    return W == 32 ? wave * 2 + (lane >> 5) : wave + kNW * (lane >> 4);
+    return W == 64 ? wave : (W == 32 ? wave * 2 + (lane >> 5) : wave + kNW * (lane >> 4));
 }
+// M tiles (16 rows each) of a sub-batch's GEMMs: an 8-row sub-batch fills
+// rows 0-7 of one tile (rows 8-15 are zero and never stored)
+template <int SB>
+constexpr int m_tiles() { return SB < 16 ? 1 : SB / 16; }
 // sum over the 4 row-groups (lanes l, l^16, l^32, l^48) of a wave
 __device__ __forceinline__ float rowgroup_sum(float v) {
     // ds_swizzle bit mode (offset[15] = 0): and_mask 0x1f, xor_mask 0x10 -> lane ^ 16
@@ -334,9 +357,6 @@ __device__ __forceinline__ T *to_sgpr(T *ptr) {
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
     const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
     return reinterpret_cast<T *>(((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ float readlane_f(float v, int l) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 // Lane / wave ids re-derived through an opaque asm at the start of each phase:
 // otherwise LICM hoists every lane-dependent LDS address of the whole
@@ -387,8 +407,11 @@ __device__ __forceinline__ void block_sum2(float &a, float &b, float *stat, int 
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
-// C[16x16] += A[16 x K] B[K x 16], K % 16 == 0 (operands batched 4 k-steps
-// at a time so LDS latency overlaps the MFMA chain)
+// C[16x16] += A[16 x K] B[K x 16], K % 4 == 0.  Software-pipelined: the
+// operands of k-batch i+1 (KB k values, KB/2 LDS reads per lane) are issued
+// before the MFMAs of batch i, and scheduling barriers keep the compiler from
+// sinking each read next to its MFMA (left alone it serialises every MFMA
+// behind its own LDS round trip: read -> lgkmcnt(0) -> MFMA).
 #ifndef AGX_MFMA_KB
 #define AGX_MFMA_KB 16
 #endif
@@ -397,16 +420,28 @@ __device__ __forceinline__ f4 mfma_tile(f4 acc, FA a, FB b) {
     const int lane = vlane();
     const int r = lane & 15, q = lane >> 4;
     constexpr int KB = K < AGX_MFMA_KB ? K : AGX_MFMA_KB;  // k values whose operands are loaded per batch
+    constexpr int NB = K / KB;
+    static_assert(K % KB == 0 && KB % 4 == 0, "k batches");
+    float av[2][KB / 4], bv[2][KB / 4];
 #pragma unroll
-    for (int k0 = 0; k0 < K; k0 += KB) {
-        float av[KB / 4], bv[KB / 4];
+    for (int j = 0; j < KB / 4; ++j) {
+        av[0][j] = a(r, 4 * j + q);
+        bv[0][j] = b(4 * j + q, r);
+    }
 #pragma unroll
-        for (int j = 0; j < KB / 4; ++j) {
-            av[j] = a(r, k0 + 4 * j + q);
-            bv[j] = b(k0 + 4 * j + q, r);
+    for (int i = 0; i < NB; ++i) {
+        if (i + 1 < NB) {
+#pragma unroll
+            for (int j = 0; j < KB / 4; ++j) {
+                av[(i + 1) & 1][j] = a(r, (i + 1) * KB + 4 * j + q);
+                bv[(i + 1) & 1][j] = b((i + 1) * KB + 4 * j + q, r);
+            }
         }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < KB / 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
+        for (int j = 0; j < KB / 4; ++j)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i & 1][j], bv[i & 1][j], acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
 }
@@ -456,7 +491,7 @@ __device__ __forceinline__ int lds_to_flat(int l, int &group) {
 template <class C, int SB = kSB>
 struct Fwd {
     static constexpr LearnPlan pl = C::plan;
-    static_assert(SB == 16 || SB == 32, "sub-batch rows");
+    static_assert(SB == 8 || SB == 16 || SB == 32, "sub-batch rows");
     float *sm;
 
     // LayerNorm(+affine)+ReLU of Z (S2, width F; LN groups [0,split), [split,F))
@@ -467,14 +502,16 @@ struct Fwd {
     // then a DPP row sum — and land in lg / val: no separate output phase.
     template <int F, int split, int xb, int ldx, int rb, int gb, int bb, bool OUT = false>
     __device__ __forceinline__ void ln_rows() {
-        // 16-row sub-batches: 32 lanes per row (every lane busy, half the columns per lane)
-        constexpr int W = (SB == 16 && !OUT && F % 32 == 0 && split >= F) ? 32 : 16;
+        // 16-row sub-batches: 32 lanes per row (every lane busy, half the columns
+        // per lane); 8-row sub-batches: 64 lanes per row (one row per wave)
+        constexpr int W = (!OUT && split >= F) ? ((SB == 8 && F % 64 == 0) ? 64 : (SB <= 16 && F % 32 == 0) ? 32 : 16)
+                                               : 16;
         constexpr int NC = F / W;
         constexpr int F0 = split < F ? split : F, F1 = F - F0;
         const int lane = vlane(), wave = swave();
         const int sub = lane & (W - 1);
         const int r = wrow<W>(lane, wave);
-        if (W == 16 && SB < kSB && r >= SB) return;  // whole 16-lane rows beyond the sub-batch idle
+        if (SB < kSB && r >= SB) return;  // whole W-lane rows beyond the sub-batch idle
         float z[NC];
         float s0 = 0.f, s1 = 0.f;
 #pragma unroll
@@ -493,7 +530,7 @@ struct Fwd {
         }
         const float r0 = 1.f / sqrtf(wrow_sum<W>(v0) / (float)F0 + 1e-5f);
         const float r1 = F1 > 0 ? 1.f / sqrtf(wrow_sum<W>(v1) / (float)(F1 > 0 ? F1 : 1) + 1e-5f) : 0.f;
-        if ((lane & (W - 1)) == 0) {
+        if (sub == 0) {
             sm[rb + 2 * r] = r0;
             sm[rb + 2 * r + 1] = r1;
         }
@@ -530,19 +567,23 @@ struct Fwd {
         }
     }
 
-    // Z[SB x fout] = X W^T + b  -> S2
+    // Z[SB x fout] = X W^T + b  -> S2 (rows beyond an 8-row sub-batch are not
+    // stored: they stay zero, so no garbage circulates through the padding rows)
     template <int xb, int ldx, int K, int wb, int ldw, int bias, int fout>
     __device__ __forceinline__ void gemm_fwd() {
-        constexpr int nt = (SB / 16) * (fout / 16);
+        constexpr int MT = m_tiles<SB>();
+        constexpr int nt = MT * (fout / 16);
         AGX_IDS;
         for (int t = wave; t < nt; t += kNW) {
-            const int m0 = (t % (SB / 16)) * 16, n0 = (t / (SB / 16)) * 16;
+            const int m0 = (t % MT) * 16, n0 = (t / MT) * 16;
             f4 c = f4{0.f, 0.f, 0.f, 0.f};
             c = mfma_tile<K>(c, [&](int m, int k) { return sm[xb + (m0 + m) * ldx + k]; },
                              [&](int k, int n) { return sm[wb + (n0 + n) * ldw + k]; });
             const float bv = sm[bias + n0 + lr16];
+            if (SB >= 16 || lq * 4 < SB) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) sm[pl.l_s2 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i] + bv;
+                for (int i = 0; i < 4; ++i) sm[pl.l_s2 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i] + bv;
+            }
         }
     }
 
@@ -649,6 +690,9 @@ template <class C, int SB, int JN = 0, bool ST = false>
 __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     constexpr LearnPlan pl = C::plan;
+    // partners per agent this instantiation handles: 16 with 8-row sub-batches,
+    // else 8 (the register arrays of the exchange are sized by it)
+    constexpr int KM = SB == 8 ? kMaxK : 8;
     // block b -> agent b % Q, partner kk = b / Q with Q = P rounded up to a
     // multiple of the 8 XCDs (partners only): under round-robin dispatch an
     // agent's K workgroups then share one XCD (and its L2) for every P, the
@@ -1011,30 +1055,24 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 // busy, half the per-lane columns: the pass is VALU-issue bound); the
                 // row sums then add the other 16-lane half by ds_swizzle (lane ^ 16).
                 {
-                    constexpr int W = (SB == 16 && pl.H % 32 == 0 && pl.ha % 32 == 0) ? 32 : 16;
+                    // 8-row sub-batches: 64 lanes per row (one row per wave)
+                    constexpr int W = (SB == 8 && pl.H % 64 == 0 && pl.ha % 64 == 0)
+                                          ? 64
+                                          : ((SB <= 16 && pl.H % 32 == 0 && pl.ha % 32 == 0) ? 32 : 16);
                     const int lane = vlane(), wave = swave();
                     const int sub = lane & (W - 1);
-                    const int r = W == 32 ? wave * 2 + (lane >> 5) : wave + kNW * (lane >> 4);
+                    const int r = wrow<W>(lane, wave);
                     constexpr int F = pl.H, split = pl.ha, NC = F / W, NA = pl.A;
                     constexpr int F0 = split, F1 = F - split;
                     const int a = sub;
                     auto swz16 = [](float v) {
                         return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401f));
                     };
-                    auto rsum = [&](float v) {
-                        v = row_sum(v);
-                        if constexpr (W == 32) v += swz16(v);
-                        return v;
-                    };
-                    auto rmax = [&](float v) {
-                        v = row_max(v);
-                        if constexpr (W == 32) v = fmaxf(v, swz16(v));
-                        return v;
-                    };
-                    // rows beyond the sub-batch (16-lane rows of a 16-row sub-batch:
-                    // lanes 32-63) compute on zeros and contribute exact zeros to the
-                    // column reductions
-                    const bool rl = W == 32 || SB == kSB || r < SB;
+                    auto rsum = [&](float v) { return wrow_sum<W>(v); };
+                    auto rmax = [&](float v) { return wrow_max<W>(v); };
+                    // rows beyond the sub-batch (W-lane rows past SB) compute on zeros
+                    // and contribute exact zeros to the column reductions
+                    const bool rl = r < SB;
                     const bool live = rl && r < nrow;
                     float z[NC], xh[NC];
                     float s0 = 0.f, s1 = 0.f;
@@ -1079,7 +1117,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     const float v = rsum(pv) + sm[pl.l_cob];
                     // loss + d(logits), d(value) (ppo.py:876-908); illegal actions:
                     // logits -> -1e8 (apply_action_mask_discrete, distributions.py:16-28)
-                    const bool ok_a = (legal[r] >> a) & 1u;
+                    const bool ok_a = (legal[rl ? r : 0] >> a) & 1u;
                     const float lg = a < NA ? (ok_a ? mine + sm[pl.l_aob + sub] : -1.0e8f) : -3.0e38f;
                     const float mx = rmax(lg);
                     const float ex = a < NA ? expf(lg - mx) : 0.f;
@@ -1089,12 +1127,13 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     const float Hs = -rsum(a < NA ? pa_ * lpe : 0.f);  // H = -sum p log(p+1e-8)
                     const float gh = -(lpe + pa_ / (pa_ + 1e-8f));          // dH/dp_a
                     const float pg_dot = rsum(a < NA ? pa_ * gh : 0.f);
-                    const int a_t = acts[r];
+                    const int a_t = acts[rl ? r : 0];
                     const float logp = __builtin_bit_cast(
                                            float, __builtin_amdgcn_ds_bpermute((lane - sub + a_t) * 4,
                                                                                __builtin_bit_cast(int, lg))) -
                                        lse;
-                    const float olp = rowf[r], A = rowf[kSB + r], R = rowf[2 * kSB + r], ov = rowf[3 * kSB + r];
+                    const int rr = rl ? r : 0;
+                    const float olp = rowf[rr], A = rowf[kSB + rr], R = rowf[2 * kSB + rr], ov = rowf[3 * kSB + rr];
                     const float lo = 1.f - g.clip, hi = 1.f + g.clip;
                     const float lrt = logp - olp;
                     const float ratio = expf(lrt);
@@ -1177,7 +1216,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
 #pragma unroll
                             for (int i = 0; i < NC; ++i) cs[k][i] += swz16(cs[k][i]);  // lane ^ 16
                     }
-                    if constexpr (W == 32 || SB > 16) {  // rows in lanes 32-63 too
+                    if constexpr (W == 32 || (W == 16 && SB > 16)) {  // rows in lanes 32-63 too
 #pragma unroll
                         for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -1209,16 +1248,15 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     constexpr int rb = decltype(rbc)::value, gb = decltype(gbc)::value, bb = decltype(bbc)::value;
                     constexpr int red = decltype(redc)::value;
                     constexpr bool aff = decltype(affc)::value;
-                    // 16-row sub-batches: 32 lanes per row (as the forward pass)
-                    constexpr int W = (SB == 16 && F % 32 == 0) ? 32 : 16;
+                    // 16-row sub-batches: 32 lanes per row, 8-row: 64 (as the forward pass)
+                    constexpr int W = (SB == 8 && F % 64 == 0) ? 64 : ((SB <= 16 && F % 32 == 0) ? 32 : 16);
                     constexpr int NC = F / W;
                     const int lane = vlane(), wave = swave();
                     const int sub = lane & (W - 1);
                     const int r = wrow<W>(lane, wave);
-                    // rows beyond the sub-batch (16-lane rows of a 16-row sub-batch:
-                    // lanes 32-63) hold stale LDS data: they contribute exact zeros
-                    // to the column reductions
-                    const bool rl = W == 32 || SB == kSB || r < SB;
+                    // rows beyond the sub-batch hold stale LDS data: they contribute
+                    // exact zeros to the column reductions
+                    const bool rl = r < SB;
                     float xh[NC], dxh[NC], dyp[NC];
                     float a1 = 0.f, a2 = 0.f;
                     const float rs0 = rl ? sm[rb + 2 * r] : 0.f;
@@ -1261,7 +1299,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                 cs[k][i] += __builtin_bit_cast(
                                     float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, cs[k][i]), 0x401f));  // lane ^ 16
                     }
-                    if constexpr (W == 32 || SB > 16) {  // rows in lanes 32-63 too
+                    if constexpr (W == 32 || (W == 16 && SB > 16)) {  // rows in lanes 32-63 too
 #pragma unroll
                         for (int k = 0; k < NV; ++k)
 #pragma unroll
@@ -1332,14 +1370,17 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                         }
                     }
                     if (direct && last_sb) emit_slab(IC(gh));
-                    constexpr int nt = (SB / 16) * (pl.lat / 16);
+                    constexpr int MT = m_tiles<SB>();
+                    constexpr int nt = MT * (pl.lat / 16);
                     for (int t = wave; t < nt; t += kNW) {
-                        const int m0 = (t % (SB / 16)) * 16, n0 = (t / (SB / 16)) * 16;
+                        const int m0 = (t % MT) * 16, n0 = (t / MT) * 16;
                         f4 c = f4{0.f, 0.f, 0.f, 0.f};
                         c = mfma_tile<pl.H>(c, [&](int m, int k) { return sm[pl.l_s2 + (m0 + m) * pl.ld_s + k]; },
                                             [&](int k, int n) { return sm[pl.l_hw + k * pl.l_hld + n0 + n]; });
+                        if (SB >= 16 || lq * 4 < SB) {
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) sm[pl.l_xh + (m0 + lq * 4 + i) * pl.ld_xh + n0 + lr16] = c[i];
+                            for (int i = 0; i < 4; ++i) sm[pl.l_xh + (m0 + lq * 4 + i) * pl.ld_xh + n0 + lr16] = c[i];
+                        }
                     }
                 }
                 __syncthreads();
@@ -1380,14 +1421,17 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     }
                     if (direct && last_sb) emit_slab(IC(L));
                     if constexpr (L > 0) {
-                        constexpr int nt = (SB / 16) * (fin / 16);
+                        constexpr int MT = m_tiles<SB>();
+                        constexpr int nt = MT * (fin / 16);
                         for (int t = wave; t < nt; t += kNW) {
-                            const int m0 = (t % (SB / 16)) * 16, n0 = (t / (SB / 16)) * 16;
+                            const int m0 = (t % MT) * 16, n0 = (t / MT) * 16;
                             f4 c = f4{0.f, 0.f, 0.f, 0.f};
                             c = mfma_tile<fout>(c, [&](int m, int k) { return sm[pl.l_s2 + (m0 + m) * pl.ld_s + k]; },
                                                 [&](int k, int n) { return sm[pl.l_ew[L] + k * pl.l_eld[L] + n0 + n]; });
+                            if (SB >= 16 || lq * 4 < SB) {
 #pragma unroll
-                            for (int i = 0; i < 4; ++i) sm[pl.l_s1 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i];
+                                for (int i = 0; i < 4; ++i) sm[pl.l_s1 + (m0 + lq * 4 + i) * pl.ld_s + n0 + lr16] = c[i];
+                            }
                         }
                     }
                     __syncthreads();
@@ -1492,15 +1536,15 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                             continue;
                         }
                         if (c < oc1) {
-                            f4 x[kMaxK];  // all K loads in flight at once
+                            f4 x[KM];  // all K loads in flight at once
 #pragma unroll
-                            for (int q = 0; q < kMaxK; ++q)
+                            for (int q = 0; q < KM; ++q)
                                 x[q] = q < g.K ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
                                                                            rs, (q * pl.slab + 4 * c) * 4, 0, 16))
                                                : f4{0.f, 0.f, 0.f, 0.f};
                             t = x[0];  // partner order
 #pragma unroll
-                            for (int q = 1; q < kMaxK; ++q)
+                            for (int q = 1; q < KM; ++q)
                                 if (q < g.K) t += x[q];
                             if (c == n4) {  // the loss / approx_kl chunk: every partner reads it
                                 if (local) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 0);
@@ -1588,14 +1632,16 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 // ([partner][wave][group]: group = index parity), summed in one
                 // fixed order by every wave of every partner -> identical clip
                 const int lane = vlane();
-                const int np = 2 * kNW * g.K;  // <= 128
-                const float v0 = lane < np ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                                           sum_rsrc, (pl.param_end + 4 + lane) * 4, 0, 16))
-                                           : 0.f;
-                const float v1 = lane + 64 < np ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                                                sum_rsrc, (pl.param_end + 68 + lane) * 4, 0, 16))
-                                                : 0.f;
-                const float v = v0 + v1;
+                const int np = 2 * kNW * g.K;  // <= 256: word lane + 64 q holds [partner][wave][group]
+                float vq[(2 * kNW * KM + 63) / 64];
+#pragma unroll
+                for (int q = 0; q < (2 * kNW * KM + 63) / 64; ++q)
+                    vq[q] = lane + 64 * q < np ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                            sum_rsrc, (pl.param_end + 4 + 64 * q + lane) * 4, 0, 16))
+                                               : 0.f;
+                float v = vq[0];
+#pragma unroll
+                for (int q = 1; q < (2 * kNW * KM + 63) / 64; ++q) v += vq[q];
                 const float x0 = row_sum((lane & 1) ? 0.f : v), x1 = row_sum((lane & 1) ? v : 0.f);
                 t0 = readlane_f(x0, 0) + readlane_f(x0, 16) + readlane_f(x0, 32) + readlane_f(x0, 48);
                 t1 = readlane_f(x1, 0) + readlane_f(x1, 16) + readlane_f(x1, 32) + readlane_f(x1, 48);
@@ -1676,10 +1722,10 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 // round r: chunk qc0 + tid + kNT*r of every other partner q, all loads in flight
                 const int span = (n4s + g.K - 1) / g.K + 1;
                 for (int r0 = 0; r0 < span; r0 += kNT) {
-                    f4 x[kMaxK];
-                    int cq[kMaxK];
+                    f4 x[KM];
+                    int cq[KM];
 #pragma unroll
-                    for (int q = 0; q < kMaxK; ++q) {
+                    for (int q = 0; q < KM; ++q) {
                         const int qc0 = (int)((long long)n4s * q / g.K), qc1 = (int)((long long)n4s * (q + 1) / g.K);
                         const int c = qc0 + tid + r0;
                         cq[q] = (q < g.K && q != kk && c < qc1 && c < n4) ? c : -1;
@@ -1688,7 +1734,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                                           : f4{0.f, 0.f, 0.f, 0.f};
                     }
 #pragma unroll
-                    for (int q = 0; q < kMaxK; ++q)
+                    for (int q = 0; q < KM; ++q)
                         if (cq[q] >= 0) sm4[cq[q]] = x[q];
                 }
                 AGX_STAMP(64 + 2);
@@ -2054,6 +2100,10 @@ template <class C>
 static void launch_learn(const LearnArgs &a, int nblocks, size_t lds, hipStream_t s, int sb) {
     static bool attr = false;
     if (!attr) {
+        (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
         (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 16, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2066,6 +2116,12 @@ static void launch_learn(const LearnArgs &a, int nblocks, size_t lds, hipStream_
     constexpr int n4s = C::plan.param_end / 4 + 1;
     const bool one_round = (n4s + a.K - 1) / a.K + 1 <= kNT;
     if constexpr (std::is_same_v<C, Shape<8, 4, 2, 64, 64, 0, 64, 64>>) {
+        if (a.stamps && sb == 8 && one_round) {
+            (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 8, 1, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            ppo_learn_kernel<C, 8, 1, true><<<(unsigned)nblocks, kNT, lds, s>>>(a);
+            return;
+        }
         if (a.stamps && sb == 16 && one_round) {
             (void)hipFuncSetAttribute((const void *)ppo_learn_kernel<C, 16, 1, true>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -2073,7 +2129,9 @@ static void launch_learn(const LearnArgs &a, int nblocks, size_t lds, hipStream_
             return;
         }
     }
-    if (sb == 16 && one_round) ppo_learn_kernel<C, 16, 1><<<(unsigned)nblocks, kNT, lds, s>>>(a);
+    if (sb == 8 && one_round) ppo_learn_kernel<C, 8, 1><<<(unsigned)nblocks, kNT, lds, s>>>(a);
+    else if (sb == 8) ppo_learn_kernel<C, 8><<<(unsigned)nblocks, kNT, lds, s>>>(a);
+    else if (sb == 16 && one_round) ppo_learn_kernel<C, 16, 1><<<(unsigned)nblocks, kNT, lds, s>>>(a);
     else if (sb == 16) ppo_learn_kernel<C, 16><<<(unsigned)nblocks, kNT, lds, s>>>(a);
     else ppo_learn_kernel<C, 32><<<(unsigned)nblocks, kNT, lds, s>>>(a);
 }
@@ -2145,7 +2203,7 @@ extern "C" size_t agx_ppo_learn_lds_bytes(const agx_ppo_net *net) {
 }
 
 // Workgroups per agent: the learner spreads an agent's sub-batches over up to
-// kMaxK = 8 partner workgroups (one CU each) when the population leaves CUs idle.
+// kMaxK = 16 partner workgroups (one CU each) when the population leaves CUs idle.
 static int cu_count() {
     static int n = 0;
     if (!n) {
@@ -2169,19 +2227,20 @@ static int max_partners(int64_t P) {
     if (fit < k) k = fit < 1 ? 1 : (int)fit;
     return k;
 }
-// Sub-batch rows and partner count of one learn: 16-row sub-batches over up to
-// 8 partners when the population leaves that many CUs per agent (shorter MFMA
-// chains per CU), else 32-row sub-batches over up to 4.  AGX_LEARN_SB = 16 / 32
+// Sub-batch rows and partner count of one learn: 8-row sub-batches over up to
+// 16 partners when the population leaves that many CUs per agent (row passes
+// at 64 lanes per row, half the dW contraction per CU), 16-row sub-batches over
+// up to 8, else 32-row sub-batches over up to 4.  AGX_LEARN_SB = 8 / 16 / 32
 // forces the row count.
 static void pick_split(int64_t P, int64_t batch, int &K, int &SB) {
     const int kmax = max_partners(P);
-    int sb = kmax >= 8 ? 16 : 32;
+    int sb = kmax >= 16 ? 8 : (kmax >= 8 ? 16 : 32);
     if (const char *e = getenv("AGX_LEARN_SB")) {
         const int v = atoi(e);
-        if (v == 16 || v == 32) sb = v;
+        if (v == 8 || v == 16 || v == 32) sb = v;
     }
     const int64_t nsb = (batch + sb - 1) / sb;
-    K = sb == 32 && kmax > 4 ? 4 : kmax;
+    K = sb == 32 ? (kmax > 4 ? 4 : kmax) : (sb == 16 ? (kmax > 8 ? 8 : kmax) : kmax);
     if (K > nsb) K = (int)nsb;
     if (K < 1) K = 1;
     SB = sb;
