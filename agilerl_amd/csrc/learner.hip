@@ -302,23 +302,41 @@ __device__ __forceinline__ float row_max(float v) {
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
+// DPP row broadcast (GFX9 row_bcast:15 = 0x142, row_bcast:31 = 0x143): the
+// rows enabled in RM receive lane 15 (resp. 31) of the preceding row(s); the
+// other rows keep `old`
+template <int C, int RM>
+__device__ __forceinline__ float bcast(float v, float old) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                                 C, RM, 0xf, false));
+}
 // W-lane row sum (W = 16: one DPP row; W = 32: + the other 16-lane half,
-// lane ^ 16; W = 64: + the other 32-lane half through two readlanes, a
-// wave-uniform sum in the fixed order (lanes 0-31) + (lanes 32-63))
+// lane ^ 16; W = 64: the whole wave, by DPP alone — row sums, then row 1 +=
+// row 0 and row 3 += row 2 (row_bcast:15), then rows 2-3 += lane 31
+// (row_bcast:31): lane 63 holds (r3 + r2) + (r1 + r0), read back as a
+// wave-uniform value.  No LDS-crossbar (ds_swizzle) round trip on the chain.)
 template <int W>
 __device__ __forceinline__ float wrow_sum(float v) {
     v = row_sum(v);
-    if constexpr (W >= 32)
+    if constexpr (W == 32)
         v += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401f));
-    if constexpr (W == 64) v = readlane_f(v, 0) + readlane_f(v, 32);
+    if constexpr (W == 64) {
+        v += bcast<0x142, 0xa>(v, 0.f);
+        v += bcast<0x143, 0xc>(v, 0.f);
+        v = readlane_f(v, 63);
+    }
     return v;
 }
 template <int W>
 __device__ __forceinline__ float wrow_max(float v) {
     v = row_max(v);
-    if constexpr (W >= 32)
+    if constexpr (W == 32)
         v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401f)));
-    if constexpr (W == 64) v = fmaxf(readlane_f(v, 0), readlane_f(v, 32));
+    if constexpr (W == 64) {
+        v = fmaxf(v, bcast<0x142, 0xa>(v, -__builtin_huge_valf()));
+        v = fmaxf(v, bcast<0x143, 0xc>(v, -__builtin_huge_valf()));
+        v = readlane_f(v, 63);
+    }
     return v;
 }
 // row slot of this lane: W = 16: wave + 8 * (lane / 16) (4 rows per wave);
