@@ -605,21 +605,25 @@ struct Fwd {
         }
     }
 
-    template <int L>
-    __device__ __forceinline__ void enc_layer() {
+    template <int L, class F>
+    __device__ __forceinline__ void enc_layer(F st) {
         constexpr int K = rup(pl.ein[L], 16);
         gemm_fwd<L == 0 ? pl.l_x0 : pl.l_s1, L == 0 ? pl.ld_x0 : pl.ld_s, K, pl.l_ew[L], pl.l_eld[L], pl.l_eb[L],
                  pl.eout[L]>();
         __syncthreads();
+        st(8 + 2 * L);
         ln_rows<pl.eout[L], pl.eout[L], pl.l_xe[L], pl.ld_xe[L], pl.l_re[L], pl.eaff[L] ? pl.l_eg[L] : -1,
                 pl.l_ebe[L]>();
         __syncthreads();
-        if constexpr (L + 1 < pl.ne) enc_layer<L + 1>();
+        st(9 + 2 * L);
+        if constexpr (L + 1 < pl.ne) enc_layer<L + 1>(st);
     }
 
-    // encoder + the merged head GEMM (Z_h in S2)
-    __device__ __forceinline__ void trunk() {
-        enc_layer<0>();
+    // encoder + the merged head GEMM (Z_h in S2); st(slot): diagnostic phase
+    // stamps of the learner's stamped build (a no-op elsewhere)
+    template <class F = void (*)(int)>
+    __device__ __forceinline__ void trunk(F st = [](int) {}) {
+        enc_layer<0>(st);
         gemm_fwd<pl.l_s1, pl.ld_s, pl.lat, pl.l_hw, pl.l_hld, pl.l_hb, pl.H>();
         __syncthreads();
     }
@@ -1061,7 +1065,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 AGX_STAMP(stb + 1);
 
                 // ---- P1-P3: forward trunk (encoder + merged head GEMM) ------------
-                fw.trunk();
+                fw.trunk([&](int k) { AGX_STAMP(stb + k); });
                 AGX_STAMP(stb + 2);
 
                 // ---- P4: ONE row pass over the head (W lanes per row, nothing leaves

@@ -48,6 +48,11 @@ for sb in range(4):
         continue
     seg = [row[i + 1] - row[i] for i in range(7)]
     print(f"sb{sb}: " + "  ".join(f"{n}={c}" for n, c in zip(names, seg)) + f"  total={row[7] - row[0]}")
+    # trunk sub-phases (slots 8..11: encoder layer L GEMM / LN passed, 2 = the head GEMM passed)
+    sub = [st[sb * 16 + 1]] + [st[sb * 16 + k] for k in (8, 9, 10, 11)] + [st[sb * 16 + 2]]
+    if all(sub):
+        print("   trunk: " + "  ".join(f"{n}={sub[i + 1] - sub[i]}" for i, n in
+                                     enumerate(["enc0 gemm", "enc0 LN", "enc1 gemm", "enc1 LN", "head gemm"])))
 last = max(v for v in st[:64] if v)
 if st[64 + 1]:  # partners: reduce-scatter + distributed Adam (three barriers)
     print("dump", st[64 + 9] - last, "| publish", st[64 + 11] - st[64 + 9], "wait", st[64 + 12] - st[64 + 11],
