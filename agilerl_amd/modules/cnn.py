@@ -23,6 +23,7 @@ from __future__ import annotations
 import ctypes
 from collections import OrderedDict
 
+import numpy as np
 import torch
 from torch import nn
 
@@ -191,7 +192,60 @@ def create_cnn(in_channels: int, channel_size: list[int], kernel_size: list, str
     return d
 
 
+def max_kernel_sizes(kernel_size: list[int], channel_size: list[int], stride_size: list[int],
+                     input_shape: list[int]) -> list[int]:
+    """MutableKernelSizes.calc_max_kernel_sizes (modules/cnn.py:110-148): per
+    layer a quarter of its output's smaller side (float arithmetic as the
+    reference: np.floor of a true division), clamped to [1, 9]."""
+    out = []
+    h_in, w_in = input_shape[-2:]
+    for idx, _ in enumerate(channel_size):
+        h_out = 1 + np.floor((h_in + 2 * 0 - kernel_size[idx]) / stride_size[idx])
+        w_out = 1 + np.floor((w_in + 2 * 0 - kernel_size[idx]) / stride_size[idx])
+        k = int(min(h_out, w_out) * 0.25)
+        out.append(1 if k <= 0 else (9 if k > 9 else k))
+        h_in, w_in = h_out, w_out
+    return out
+
+
+def shrink_preserve_parameters(old_net: nn.Module, new_net: nn.Module) -> nn.Module:
+    """EvolvableCNN.shrink_preserve_parameters (modules/cnn.py:418-456): equal
+    shapes shared, otherwise the leading [:min0] / [:min0, :min1] block copied
+    (spatial kernel dimensions are never sliced); norms left fresh."""
+    old = dict(old_net.named_parameters())
+    for key, param in new_net.named_parameters():
+        if key in old:
+            o = old[key]
+            if o.data.size() == param.data.size():
+                param.data = o.data
+            elif "norm" not in key:
+                m0 = min(o.data.size(0), param.data.size(0))
+                if param.data.dim() == 1:
+                    param.data[:m0] = o.data[:m0]
+                else:
+                    m1 = min(o.data.size(1), param.data.size(1))
+                    param.data[:m0, :m1] = o.data[:m0, :m1]
+    return new_net
+
+
 class EvolvableCNN(nn.Module):
+    """Architecture mutations (modules/cnn.py:582-760): ``add_layer`` /
+    ``remove_layer`` (LAYER), ``change_kernel`` / ``add_channel`` /
+    ``remove_channel`` (NODE), drawing from the module's ``rng`` as the
+    reference's methods do (the kernel-size helper shares it), with the
+    reference's fallbacks (add_layer -> add_channel at a limit or when the
+    last output is too small; remove_layer -> add_channel at the minimum;
+    change_kernel -> add_layer on a one-layer network).  As under the
+    reference's MutationContext (modules/base.py:57-160), the network is
+    recreated once, after the outermost method, with the outermost method's
+    parameter copy (shrink for remove_layer / remove_channel); a fallback to
+    a method the owner disabled (``disabled``: an EvolvableNetwork disables
+    its encoder's LAYER methods, networks/base.py:266-268) applies nothing.
+    ``last_mutation_attr`` names the method that actually ran."""
+
+    LAYER_METHODS = ("add_layer", "remove_layer")
+    NODE_METHODS = ("change_kernel", "add_channel", "remove_channel")
+
     def __init__(self, input_shape: list[int], num_outputs: int, channel_size: list[int], kernel_size: list,
                  stride_size: list[int], sample_input: torch.Tensor | None = None, block_type: str = "Conv2d",
                  activation: str = "ReLU", output_activation: str | None = None, min_hidden_layers: int = 1,
@@ -215,18 +269,32 @@ class EvolvableCNN(nn.Module):
         self.min_hidden_layers, self.max_hidden_layers = min_hidden_layers, max_hidden_layers
         self.min_channel_size, self.max_channel_size = min_channel_size, max_channel_size
         self.layer_norm, self.init_layers, self.name, self.device = layer_norm, init_layers, name, device
-        net = create_cnn(input_shape[0], channel_size, kernel_size, stride_size, name, init_layers, layer_norm,
-                         activation, device)
-        # flattened size (cnn.py:527-544), from the shapes
-        c, h, w = input_shape
-        for ch, k, s in zip(channel_size, kernel_size, stride_size):
-            k = k[0] if isinstance(k, (tuple, list)) else k
+        self.kernel_size = [int(k[0] if isinstance(k, (tuple, list)) else k) for k in self.kernel_size]
+        self.random_seed = random_seed
+        self.rng = np.random.default_rng(seed=random_seed)  # EvolvableModule.rng (modules/base.py)
+        self.last_mutation_attr: str | None = None
+        self.disabled: set[str] = set()
+        self._depth = 0
+        self.model = self._build(device)
+
+    def _build(self, device) -> nn.Sequential:
+        """EvolvableCNN.create_cnn (modules/cnn.py:487-544): conv blocks, then
+        flatten -> Linear(flattened, num_outputs) -> output activation; the
+        flattened size follows from the shapes (the reference runs a sample
+        input through the block — no random draws either way)."""
+        net = create_cnn(self.input_shape[0], self.channel_size, self.kernel_size, self.stride_size, self.name,
+                         self.init_layers, self.layer_norm, self.activation, device)
+        c, h, w = self.input_shape
+        for ch, k, s in zip(self.channel_size, self.kernel_size, self.stride_size):
             h, w, c = (h - k) // s + 1, (w - k) // s + 1, ch
+        if h < 1 or w < 1:
+            raise ValueError(f"EvolvableCNN: kernels {self.kernel_size} / strides {self.stride_size} leave no "
+                             f"output for input {self.input_shape}")
         self.cnn_output_size = torch.Size([1, c, h, w])
-        net[f"{name}_flatten"] = nn.Flatten()
-        net[f"{name}_linear_output"] = nn.Linear(c * h * w, self.num_outputs, device=device)
-        net[f"{name}_output_activation"] = get_activation(output_activation)
-        self.model = nn.Sequential(net)
+        net[f"{self.name}_flatten"] = nn.Flatten()
+        net[f"{self.name}_linear_output"] = nn.Linear(c * h * w, self.num_outputs, device=device)
+        net[f"{self.name}_output_activation"] = get_activation(self.output_activation)
+        return nn.Sequential(net)
 
     @property
     def net_config(self) -> dict:
@@ -253,23 +321,133 @@ class EvolvableCNN(nn.Module):
         self.activation = activation
         self.recreate_network()
 
-    def recreate_network(self) -> None:
-        """Rebuild ``model`` from the current hyperparameters; parameters of
-        equal name and shape are kept (preserve_parameters), as is the uint8
+    def recreate_network(self, shrink_params: bool = False) -> None:
+        """Rebuild ``model`` from the current hyperparameters (cnn.py:769-790):
+        parameters of equal name are kept, overlapping slices copied
+        (shrink_preserve_parameters for shrinking mutations), as is the uint8
         normalisation of the first convolution."""
         from .mlp import preserve_parameters
 
         first = getattr(self.model, f"{self.name}_conv_layer_1")
         norm = first.image_norm
         dev = first.weight.device
-        net = create_cnn(self.input_shape[0], self.channel_size, self.kernel_size, self.stride_size, self.name,
-                         self.init_layers, self.layer_norm, self.activation, dev)
-        c, h, w = self.cnn_output_size[1:]
-        net[f"{self.name}_flatten"] = nn.Flatten()
-        net[f"{self.name}_linear_output"] = nn.Linear(c * h * w, self.num_outputs, device=dev)
-        net[f"{self.name}_output_activation"] = get_activation(self.output_activation)
-        self.model = preserve_parameters(self.model, nn.Sequential(net))
+        new = self._build(dev)
+        self.model = (shrink_preserve_parameters if shrink_params else preserve_parameters)(self.model, new)
         getattr(self.model, f"{self.name}_conv_layer_1").image_norm = norm
+
+    # ---- architecture mutations (modules/cnn.py:582-760) --------------------
+    @property
+    def mutation_methods(self) -> list[str]:
+        return [m for m in (*self.LAYER_METHODS, *self.NODE_METHODS) if m not in self.disabled]
+
+    def disable_mutations(self, kind: str | None = None) -> None:
+        """EvolvableModule.disable_mutations: "layer", "node" or both (None)."""
+        if kind in (None, "layer"):
+            self.disabled.update(self.LAYER_METHODS)
+        if kind in (None, "node"):
+            self.disabled.update(self.NODE_METHODS)
+
+    def _mutate(self, name: str, body, shrink: bool = False):
+        """One mutation method under the MutationContext rules."""
+        self._depth += 1
+        self.last_mutation_attr = name
+        try:
+            if name in self.disabled:
+                self.last_mutation_attr = None
+                return None
+            return body()
+        finally:
+            self._depth -= 1
+            if self._depth == 0 and self.last_mutation_attr is not None:
+                self.recreate_network(shrink_params=shrink)
+
+    def add_layer(self):
+        return self._mutate("add_layer", self._add_layer)
+
+    def remove_layer(self):
+        return self._mutate("remove_layer", self._remove_layer, shrink=True)
+
+    def change_kernel(self, kernel_size: int | None = None, hidden_layer: int | None = None):
+        return self._mutate("change_kernel", lambda: self._change_kernel(kernel_size, hidden_layer))
+
+    def add_channel(self, hidden_layer: int | None = None, numb_new_channels: int | None = None):
+        return self._mutate("add_channel", lambda: self._add_channel(hidden_layer, numb_new_channels))
+
+    def remove_channel(self, hidden_layer: int | None = None, numb_new_channels: int | None = None):
+        return self._mutate("remove_channel", lambda: self._remove_channel(hidden_layer, numb_new_channels),
+                            shrink=True)
+
+    def _add_layer(self):
+        dims = self.cnn_output_size[-2:]
+        maxk = max_kernel_sizes(self.kernel_size, self.channel_size, self.stride_size, self.input_shape)
+        if len(self.channel_size) < self.max_hidden_layers and not any(i <= 2 for i in dims) and maxk \
+                and maxk[-1] > 2:
+            l_in = int(self.cnn_output_size[-1])
+            if l_in < 2:
+                return self.add_channel()
+            k_new = int(self.rng.integers(2, l_in + 1))
+            max_s = l_in - k_new + 1
+            if max_s < 1:
+                return self.add_channel()
+            s_new = int(self.rng.integers(1, max_s + 1))
+            self.channel_size = [*self.channel_size, self.channel_size[-1]]
+            self.kernel_size = [*self.kernel_size, k_new]
+            self.stride_size = [*self.stride_size, s_new]
+            return None
+        return self.add_channel()
+
+    def _remove_layer(self):
+        if len(self.channel_size) > self.min_hidden_layers:
+            self.channel_size = self.channel_size[:-1]
+            self.kernel_size = self.kernel_size[:-1]
+            self.stride_size = self.stride_size[:-1]
+            return None
+        return self.add_channel()
+
+    def _change_kernel(self, kernel_size, hidden_layer):
+        if len(self.channel_size) > 1:
+            if hidden_layer is None:
+                hidden_layer = int(self.rng.integers(1, min(4, len(self.channel_size))))
+            if kernel_size is not None:
+                new_k = int(kernel_size)
+            else:  # MutableKernelSizes.change_kernel_size (cnn.py:150-221)
+                maxk = max_kernel_sizes(self.kernel_size, self.channel_size, self.stride_size,
+                                        self.input_shape)[hidden_layer]
+                cur = self.kernel_size[hidden_layer]
+                if maxk == 1:
+                    new_k = 1
+                else:
+                    cand = [k for k in range(1, maxk + 1) if k != cur]
+                    new_k = int(self.rng.choice(cand)) if cand else int(self.rng.integers(1, maxk + 1))
+            ks = list(self.kernel_size)
+            ks[hidden_layer] = new_k
+            self.kernel_size = ks
+            return {"hidden_layer": hidden_layer, "kernel_size": new_k}
+        return self.add_layer()
+
+    def _add_channel(self, hidden_layer, numb):
+        hidden_layer = int(self.rng.integers(0, len(self.channel_size))) if hidden_layer is None else \
+            min(hidden_layer, len(self.channel_size) - 1)
+        if numb is None:
+            numb = int(self.rng.choice([8, 16, 32]))
+        if self.channel_size[hidden_layer] + numb <= self.max_channel_size:
+            ch = list(self.channel_size)
+            ch[hidden_layer] += numb
+            self.channel_size = ch
+        return {"hidden_layer": hidden_layer, "numb_new_channels": numb}
+
+    def _remove_channel(self, hidden_layer, numb):
+        hidden_layer = int(self.rng.integers(0, len(self.channel_size))) if hidden_layer is None else \
+            min(hidden_layer, len(self.channel_size) - 1)
+        if numb is None:
+            numb = int(self.rng.choice([8, 16, 32]))
+        if self.channel_size[hidden_layer] - numb >= self.min_channel_size:
+            ch = list(self.channel_size)
+            ch[hidden_layer] -= numb
+            self.channel_size = ch
+        else:
+            numb = 0
+        return {"hidden_layer": hidden_layer, "numb_new_channels": numb}
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not isinstance(x, torch.Tensor):

@@ -58,6 +58,7 @@ if __name__ == "__main__" and os.environ.get("PYTHONHASHSEED") != HASH_SEED:
              f"reference's method-table order under PYTHONHASHSEED={HASH_SEED} (agilerl/modules/base.py:570-571)")
 
 import argparse  # noqa: E402
+import copy  # noqa: E402
 import importlib.util  # noqa: E402
 import json  # noqa: E402
 import types  # noqa: E402
@@ -166,12 +167,16 @@ def _setup(ref: str):
     for name in ("EvolvableCNN", "EvolvableLSTM", "EvolvableMultiInput", "EvolvableSimBa", "EvolvableResNet",
                  "EvolvableBERT", "EvolvableGPT"):
         setattr(mods, name, type(name, (base.EvolvableModule,), {}))
+    cnn = _load(ref, "agilerl.modules.cnn", "agilerl/modules/cnn.py")
+    mods.EvolvableCNN = cnn.EvolvableCNN
     _package("agilerl.networks")
     _load(ref, "agilerl.networks.distributions", "agilerl/networks/distributions.py")
     nb = _load(ref, "agilerl.networks.base", "agilerl/networks/base.py")
     act = _load(ref, "agilerl.networks.actors", "agilerl/networks/actors.py")
     val = _load(ref, "agilerl.networks.value_networks", "agilerl/networks/value_networks.py")
-    return dict(base=base, cfg=cfg, en=en, mlp=mlp, nb=nb, actors=act, values=val)
+    _load(ref, "agilerl.networks.custom_modules", "agilerl/networks/custom_modules.py")
+    qn = _load(ref, "agilerl.networks.q_networks", "agilerl/networks/q_networks.py")
+    return dict(base=base, cfg=cfg, en=en, mlp=mlp, cnn=cnn, nb=nb, actors=act, values=val, qnets=qn)
 
 
 def _apply_arch_mutation(network, mut_method, applied_mut_dict=None):
@@ -255,6 +260,134 @@ def gen_cases(m: dict, out: dict) -> None:
         idx += 1
 
 
+# ---------------------------------------------------------------------------
+# EvolvableCNN (configs 3 and 5): module-level mutations, CNN-encoder network
+# tables, and one architecture mutation of a PPO image actor / critic pair
+# ---------------------------------------------------------------------------
+CNN_STARTS = [  # (channels, kernels, strides, min / max channels)
+    ([8, 16, 16], [8, 4, 3], [4, 2, 1], 8, 64),
+    ([8], [8], [4], 8, 64),
+    ([8, 16], [8, 4], [4, 2], 8, 24),
+    ([16, 16, 16], [8, 4, 3], [4, 2, 1], 16, 32),
+]
+CNN_METHODS = ["add_layer", "remove_layer", "change_kernel", "add_channel", "remove_channel"]
+
+
+def _cnn_state(net) -> dict:
+    return {k: v.detach().numpy().copy() for k, v in net.state_dict().items()}
+
+
+def gen_cnn_cases(m: dict, out: dict) -> None:
+    """EvolvableCNN (agilerl/modules/cnn.py:582-760, MutableKernelSizes
+    :55-221): every mutation method from several starting architectures
+    (limits included), the module's own generator seeded per case, fresh
+    weights of the recreated network from torch's global CPU generator; the
+    MutationContext fallbacks (add_layer -> add_channel, change_kernel ->
+    add_layer, remove_layer -> add_channel) and the shrink / preserve
+    parameter copies (cnn.py:418-456, base.py:472-502) as the reference
+    applies them."""
+    EvolvableCNN = m["cnn"].EvolvableCNN
+    idx = 0
+    for si, (ch, ks, ss, cmin, cmax) in enumerate(CNN_STARTS):
+        for mi, meth in enumerate(CNN_METHODS):
+            for rep in range(2):
+                k = 100 * si + 10 * mi + rep
+                torch.manual_seed(7000 + k)
+                net = EvolvableCNN(input_shape=[4, 52, 52], num_outputs=8, channel_size=list(ch),
+                                   kernel_size=list(ks), stride_size=list(ss), min_channel_size=cmin,
+                                   max_channel_size=cmax, name="feature_net", output_activation="ReLU")
+                net.rng = np.random.default_rng(8000 + k)
+                net.mut_kernel_size.rng = net.rng
+                before = _cnn_state(net)
+                torch.manual_seed(9000 + k)
+                ret = getattr(net, meth)()
+                g = {"start": np.array(repr((ch, ks, ss, cmin, cmax))), "method": np.array(meth),
+                     "module_rng_seed": np.array(8000 + k), "init_seed": np.array(7000 + k),
+                     "torch_seed": np.array(9000 + k),
+                     "applied": np.array("None" if net.last_mutation_attr is None else str(net.last_mutation_attr)),
+                     "ret": np.array(repr(sorted((kk, int(v)) for kk, v in (ret or {}).items()))),
+                     "after_cfg": np.array(repr((list(map(int, net.channel_size)), list(map(int, net.kernel_size)),
+                                                 list(map(int, net.stride_size)))))}
+                for kk, v in before.items():
+                    g[f"before.{kk}"] = v
+                for kk, v in _cnn_state(net).items():
+                    g[f"after.{kk}"] = v
+                out[f"cnnmut{idx}"] = g
+                idx += 1
+
+
+def gen_cnn_net_cases(m: dict, out: dict) -> None:
+    """Mutation tables of CNN-encoder networks (the encoder's LAYER methods
+    disabled, networks/base.py:266-268): QNetwork (DQN), RainbowQNetwork, and
+    PPO's StochasticActor / ValueNetwork; then one architecture mutation of a
+    PPO image actor / critic pair per case (mutation.py:829-885 restated as
+    in gen_cases, share_encoder_parameters after), small CNNs on 4x52x52."""
+    actors, values, qn = m["actors"], m["values"], m["qnets"]
+    obs, act = Box(0, 255, (4, 52, 52), dtype=np.uint8), Discrete(6)
+    enc = {"channel_size": [8, 16, 16], "kernel_size": [8, 4, 3], "stride_size": [4, 2, 1],
+           "min_channel_size": 8, "max_channel_size": 64}
+    head = {"hidden_size": [16], "min_hidden_layers": 1, "max_hidden_layers": 3, "min_mlp_nodes": 8,
+            "max_mlp_nodes": 64}
+    tables = {}
+    torch.manual_seed(1)
+    q = qn.QNetwork(obs, act, encoder_config=copy.deepcopy(enc), head_config=copy.deepcopy(head), latent_dim=16)
+    tables["qnet"] = q
+    rq = qn.RainbowQNetwork(obs, act, support=torch.linspace(-10, 10, 11), encoder_config=copy.deepcopy(enc),
+                            head_config=copy.deepcopy(head), latent_dim=16)
+    tables["rainbow"] = rq
+    for name, net in tables.items():
+        out[f"cnntab_{name}"] = {"methods": np.array(net.mutation_methods),
+                                 "probs02": np.array(net.get_mutation_probs(0.2), dtype=np.float64),
+                                 "probs05": np.array(net.get_mutation_probs(0.5), dtype=np.float64)}
+    idx = 0
+    for k in range(12):
+        nlp = (0.2, 0.5, 1.0, 0.0)[k % 4]
+        net_config = {"encoder_config": copy.deepcopy(enc), "head_config": copy.deepcopy(head), "latent_dim": 16,
+                      "min_latent_dim": 8, "max_latent_dim": 64}
+        torch.manual_seed(300 + k)
+        critic_config = copy.deepcopy(net_config)
+        critic_config["head_config"]["output_activation"] = None
+        actor = actors.StochasticActor(obs, act, device="cpu", encoder_name="shared_encoder", **net_config)
+        critic = values.ValueNetwork(obs, device="cpu", encoder_name="shared_encoder", **critic_config)
+        critic.encoder.load_state_dict(actor.encoder.state_dict())
+        actor.rng = np.random.default_rng(1300 + k)
+        for mod in actor.modules().values():
+            mod.rng = np.random.default_rng(1400 + k)
+            if hasattr(mod, "mut_kernel_size"):
+                mod.mut_kernel_size.rng = mod.rng
+        for mod in critic.modules().values():
+            mod.rng = np.random.default_rng(1500 + k)
+            if hasattr(mod, "mut_kernel_size"):
+                mod.mut_kernel_size.rng = mod.rng
+        critic.rng = np.random.default_rng(1600 + k)
+        rng = np.random.default_rng(2300 + k)
+        g = {"methods": np.array(actor.mutation_methods), "critic_methods": np.array(critic.mutation_methods),
+             "probs": np.array(actor.get_mutation_probs(nlp), dtype=np.float64), "new_layer_prob": np.array(nlp),
+             "seeds": np.array([300 + k, 1300 + k, 1400 + k, 1500 + k, 1600 + k, 2300 + k, 5300 + k])}
+        before = {**_sd("actor", actor), **_sd("critic", critic)}
+        torch.manual_seed(5300 + k)
+        mut_method = actor.sample_mutation_method(nlp, rng)
+        applied, mut_dict = _apply_arch_mutation(actor, mut_method)
+        if applied in critic.mutation_methods:
+            _apply_arch_mutation(critic, applied, mut_dict)
+        critic.encoder.load_state_dict(actor.encoder.state_dict())
+        g["sampled"] = np.array(str(mut_method))
+        g["applied"] = np.array("None" if applied is None else str(applied))
+        g["mut_dict"] = np.array(repr(sorted((kk, int(v)) for kk, v in (mut_dict or {}).items())))
+        g["shapes"] = np.array(repr({"actor_enc": (list(map(int, actor.encoder.channel_size)),
+                                                   list(map(int, actor.encoder.kernel_size)),
+                                                   list(map(int, actor.encoder.stride_size))),
+                                     "latent": int(actor.latent_dim),
+                                     "actor_head": list(actor.head_net.net_config["hidden_size"]),
+                                     "critic_head": list(critic.head_net.net_config["hidden_size"])}))
+        for kk, v in before.items():
+            g[f"before.{kk}"] = v
+        for kk, v in {**_sd("actor", actor), **_sd("critic", critic)}.items():
+            g[f"after.{kk}"] = v
+        out[f"cnnarch{idx}"] = g
+        idx += 1
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -265,6 +398,8 @@ def main() -> None:
     m = _setup(args.ref)
     out: dict = {}
     gen_cases(m, out)
+    gen_cnn_cases(m, out)
+    gen_cnn_net_cases(m, out)
     for name, arrays in out.items():
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
     meta_path = os.path.join(HERE, "META.json")

@@ -79,3 +79,36 @@ def test_arch_fixtures_record_the_reference_hash_seed():
     assert rec["PYTHONHASHSEED"] == "0"
     assert sorted(rec["groups"]) == sorted(CASES)
     assert arch.METHOD_ORDER_HASH_SEED == rec["PYTHONHASHSEED"]
+
+
+# ---- EvolvableCNN (configs 3, 5): modules/cnn.py:582-760 ------------------
+CNN_CASES = [f"cnnmut{i}" for i in range(40)]
+
+
+@pytest.mark.parametrize("case", CNN_CASES)
+def test_cnn_mutation_matches_reference(golden, case):
+    """One mutation method of the reference's EvolvableCNN per case
+    (tests/golden/gen_arch_golden.py gen_cnn_cases): the method actually
+    applied (fallbacks), its returned dict, the new channel / kernel / stride
+    lists and every parameter — preserved (or shrunk) slices and the fresh
+    entries drawn from torch's global generator — bit for bit."""
+    from agilerl_amd.modules.cnn import EvolvableCNN
+
+    g = golden(case)
+    ch, ks, ss, cmin, cmax = ast.literal_eval(str(g["start"]))
+    net = EvolvableCNN(input_shape=[4, 52, 52], num_outputs=8, channel_size=list(ch), kernel_size=list(ks),
+                       stride_size=list(ss), min_channel_size=cmin, max_channel_size=cmax, name="feature_net",
+                       output_activation="ReLU")
+    before = {k[len("before."):]: torch.from_numpy(g[k]) for k in g if k.startswith("before.")}
+    net.load_state_dict(before)
+    net.rng = np.random.default_rng(int(g["module_rng_seed"]))
+    torch.manual_seed(int(g["torch_seed"]))
+    ret = getattr(net, str(g["method"]))()
+    assert str(g["applied"]) == ("None" if net.last_mutation_attr is None else net.last_mutation_attr)
+    assert repr(sorted((k, int(v)) for k, v in (ret or {}).items())) == str(g["ret"])
+    assert repr((net.channel_size, net.kernel_size, net.stride_size)) == str(g["after_cfg"])
+    after = {k[len("after."):]: g[k] for k in g if k.startswith("after.")}
+    sd = net.state_dict()
+    assert sorted(sd) == sorted(after)
+    for k, v in after.items():
+        assert np.array_equal(sd[k].numpy(), v), k
