@@ -272,6 +272,9 @@ class EvolvableCNN(nn.Module):
         self.kernel_size = [int(k[0] if isinstance(k, (tuple, list)) else k) for k in self.kernel_size]
         self.random_seed = random_seed
         self.rng = np.random.default_rng(seed=random_seed)  # EvolvableModule.rng (modules/base.py)
+        # MutableKernelSizes keeps the generator the CNN was built with (cnn.py:367-372):
+        # an owner that shares its own generator into this module leaves it in place
+        self.kernel_rng = self.rng
         self.last_mutation_attr: str | None = None
         self.disabled: set[str] = set()
         self._depth = 0
@@ -418,7 +421,8 @@ class EvolvableCNN(nn.Module):
                     new_k = 1
                 else:
                     cand = [k for k in range(1, maxk + 1) if k != cur]
-                    new_k = int(self.rng.choice(cand)) if cand else int(self.rng.integers(1, maxk + 1))
+                    new_k = int(self.kernel_rng.choice(cand)) if cand else \
+                        int(self.kernel_rng.integers(1, maxk + 1))
             ks = list(self.kernel_size)
             ks[hidden_layer] = new_k
             self.kernel_size = ks

@@ -54,6 +54,14 @@ class ImageActorCriticSpec:
     encoder_name: str = "shared_encoder"
     obs_dtype: torch.dtype = torch.uint8
     image_norm: tuple[float, float] | None = (0.0, 255.0)
+    # architecture-mutation limits (population/image_arch.py): the CNN's
+    # (min / max hidden layers, min / max channels; CnnNetConfig's defaults
+    # 1, 6, 16, 256), the heads' (min / max hidden layers, min / max nodes)
+    # and the latent's (min, max) (EvolvableNetwork: 8, 128)
+    cnn_limits: tuple = (1, 6, 16, 256)
+    actor_limits: tuple = (1, 3, 16, 500)
+    critic_limits: tuple = (1, 3, 16, 500)
+    latent_limits: tuple = (8, 128)
 
     def __post_init__(self) -> None:
         if not (len(self.channel_size) == len(self.kernel_size) == len(self.stride_size)):
@@ -111,7 +119,8 @@ class ImageActorCriticSpec:
         """Agents with equal keys share a network layout (population groups)."""
         return (self.obs_shape, self.n_actions, tuple(self.channel_size), tuple(self.kernel_size),
                 tuple(self.stride_size), self.latent_dim, tuple(self.actor_hidden), tuple(self.critic_hidden),
-                self.head_layer_norm, self.encoder_name, self.obs_dtype, self.image_norm)
+                self.head_layer_norm, self.encoder_name, self.obs_dtype, self.image_norm, tuple(self.cnn_limits),
+                tuple(self.actor_limits), tuple(self.critic_limits), tuple(self.latent_limits))
 
     # ------------------------------------------------------------------ #
     def init_params(self, P: int, seeds: list[int] | None = None, device="cpu") -> torch.Tensor:

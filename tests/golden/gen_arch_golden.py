@@ -350,16 +350,14 @@ def gen_cnn_net_cases(m: dict, out: dict) -> None:
         actor = actors.StochasticActor(obs, act, device="cpu", encoder_name="shared_encoder", **net_config)
         critic = values.ValueNetwork(obs, device="cpu", encoder_name="shared_encoder", **critic_config)
         critic.encoder.load_state_dict(actor.encoder.state_dict())
+        # EvolvableModule.rng is shared by a network and its modules (ModuleMeta,
+        # modules/base.py:253-255; the setter propagates); the CNN's kernel-size
+        # helper keeps the generator the CNN was built with (MutableKernelSizes
+        # is not a module), so it is seeded on its own
         actor.rng = np.random.default_rng(1300 + k)
-        for mod in actor.modules().values():
-            mod.rng = np.random.default_rng(1400 + k)
-            if hasattr(mod, "mut_kernel_size"):
-                mod.mut_kernel_size.rng = mod.rng
-        for mod in critic.modules().values():
-            mod.rng = np.random.default_rng(1500 + k)
-            if hasattr(mod, "mut_kernel_size"):
-                mod.mut_kernel_size.rng = mod.rng
-        critic.rng = np.random.default_rng(1600 + k)
+        actor.encoder.mut_kernel_size.rng = np.random.default_rng(1400 + k)
+        critic.rng = np.random.default_rng(1500 + k)
+        critic.encoder.mut_kernel_size.rng = np.random.default_rng(1600 + k)
         rng = np.random.default_rng(2300 + k)
         g = {"methods": np.array(actor.mutation_methods), "critic_methods": np.array(critic.mutation_methods),
              "probs": np.array(actor.get_mutation_probs(nlp), dtype=np.float64), "new_layer_prob": np.array(nlp),

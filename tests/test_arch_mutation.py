@@ -102,6 +102,7 @@ def test_cnn_mutation_matches_reference(golden, case):
     before = {k[len("before."):]: torch.from_numpy(g[k]) for k in g if k.startswith("before.")}
     net.load_state_dict(before)
     net.rng = np.random.default_rng(int(g["module_rng_seed"]))
+    net.kernel_rng = net.rng  # the generator set both (mut_kernel_size.rng = rng)
     torch.manual_seed(int(g["torch_seed"]))
     ret = getattr(net, str(g["method"]))()
     assert str(g["applied"]) == ("None" if net.last_mutation_attr is None else net.last_mutation_attr)
@@ -112,3 +113,64 @@ def test_cnn_mutation_matches_reference(golden, case):
     assert sorted(sd) == sorted(after)
     for k, v in after.items():
         assert np.array_equal(sd[k].numpy(), v), k
+
+
+IMAGE_CASES = [f"cnnarch{i}" for i in range(12)]
+
+
+def test_cnn_network_tables_match_reference(golden):
+    """QNetwork / RainbowQNetwork / StochasticActor with an EvolvableCNN
+    encoder: the reference's method table (encoder LAYER methods disabled)
+    and its probabilities, under PYTHONHASHSEED=0."""
+    from agilerl_amd.population import image_arch
+
+    for name in ("cnntab_qnet", "cnntab_rainbow"):
+        g = golden(name)
+        assert list(g["methods"]) == image_arch.METHODS
+        np.testing.assert_allclose(image_arch.method_probs(0.2), g["probs02"], rtol=0, atol=1e-15)
+        np.testing.assert_allclose(image_arch.method_probs(0.5), g["probs05"], rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize("case", IMAGE_CASES)
+def test_image_actor_critic_mutation_matches_reference(golden, case):
+    """One architecture mutation of a PPO image actor / critic pair
+    (population/image_arch.py) against the reference's StochasticActor /
+    ValueNetwork with EvolvableCNN encoders (gen_cnn_net_cases): the table,
+    the sampled and applied method, the mutation dict, the new shapes and every
+    parameter of actor and critic, bit for bit."""
+    from agilerl_amd.population import image_arch
+    from agilerl_amd.population.image_nets import ImageActorCriticSpec
+
+    g = golden(case)
+    assert list(g["methods"]) == image_arch.METHODS and list(g["critic_methods"]) == image_arch.METHODS
+    nlp = float(g["new_layer_prob"])
+    np.testing.assert_allclose(image_arch.method_probs(nlp), g["probs"], rtol=0, atol=1e-15)
+    s = [int(x) for x in g["seeds"]]
+    spec = ImageActorCriticSpec(obs_shape=(4, 52, 52), n_actions=6, channel_size=[8, 16, 16], kernel_size=[8, 4, 3],
+                                stride_size=[4, 2, 1], latent_dim=16, actor_hidden=[16], critic_hidden=[16],
+                                head_layer_norm=True, cnn_limits=(1, 6, 8, 64), actor_limits=(1, 3, 8, 64),
+                                critic_limits=(1, 3, 8, 64), latent_limits=(8, 64))
+    flat = torch.zeros(spec.n_params)
+    for key, (off, shape) in spec.state_dict_keys().items():
+        v = torch.from_numpy(g[f"before.{key}"])
+        assert tuple(v.shape) == tuple(shape), key
+        flat[off:off + v.numel()] = v.reshape(-1)
+    method = image_arch.sample_method(nlp, np.random.default_rng(s[5]))
+    assert method == str(g["sampled"])
+    torch.manual_seed(s[6])
+    new_spec, new_flat, applied, mut_dict = image_arch.mutate(
+        spec, flat, method, np.random.default_rng(s[1]), np.random.default_rng(s[2]), np.random.default_rng(s[3]),
+        np.random.default_rng(s[4]))
+    assert ("None" if applied is None else applied) == str(g["applied"])
+    assert repr(sorted((k, int(v)) for k, v in (mut_dict or {}).items())) == str(g["mut_dict"])
+    shapes = ast.literal_eval(str(g["shapes"]))
+    assert (new_spec.channel_size, new_spec.kernel_size, new_spec.stride_size) == tuple(shapes["actor_enc"])
+    assert new_spec.latent_dim == shapes["latent"]
+    assert new_spec.actor_hidden == shapes["actor_head"] and new_spec.critic_hidden == shapes["critic_head"]
+    keys = new_spec.state_dict_keys()
+    after = {k[len("after."):] for k in g if k.startswith("after.")}
+    assert sorted(keys) == sorted(after)
+    for key, (off, shape) in keys.items():
+        want = g[f"after.{key}"]
+        got = new_flat[off:off + int(np.prod(shape))].view(shape).numpy()
+        assert np.array_equal(got, want), key
