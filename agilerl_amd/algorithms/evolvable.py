@@ -53,22 +53,23 @@ class EvolvableAgentMixin:
             # (Ranks that each train a population of their own, create_population
             # shard=False, mutate as a single process does.)
             return False
+        from ..modules.cnn import EvolvableCNN
+
         net = getattr(self, self._policy_group[0])
-        return isinstance(getattr(net, "encoder", None), EvolvableMLP) and \
+        return isinstance(getattr(net, "encoder", None), (EvolvableMLP, EvolvableCNN)) and \
             isinstance(getattr(net, "head_net", None), EvolvableMLP)
 
     def architecture_mutation(self, new_layer_prob: float, rng) -> str:
         """mutation.py:829-885 on the policy network: the method sampled from
         its mutation table with ``rng`` (Mutations.rng; the table of an
-        EvolvableNetwork with an MLP encoder, population/arch.py), applied
+        EvolvableNetwork with an MLP encoder, population/arch.py, or a CNN
+        encoder, population/image_arch.py), applied
         with the modules' own generators; the shared (target) network re-made
         from the mutated one (reinit_shared_networks, mutation.py:104-160)."""
         import copy
 
-        from ..population import arch
-
         net = getattr(self, self._policy_group[0])
-        applied = net.apply_mutation(arch.sample_method(new_layer_prob, rng))
+        applied = net.apply_mutation(net.sample_mutation_method(new_layer_prob, rng))
         setattr(self, self._policy_group[1], copy.deepcopy(net))
         return applied
 

@@ -118,6 +118,15 @@ class MADDPG(EvolvableAgentMixin):
         for a in self.agent_ids:
             self.actor_targets[a].load_state_dict(self.actors[a].state_dict())
             self.critic_targets[a].load_state_dict(self.critics[a].state_dict())
+        # the networks' own generators (EvolvableModule.rng, shared with their
+        # modules; seeded from the agent's initial index so a run is reproducible)
+        for i, a in enumerate(self.agent_ids):
+            self.actors[a].rng = np.random.default_rng((0x5EED, int(index), i))
+            self.critics[a].rng = np.random.default_rng((0x5EEE, int(index), i))
+            # maddpg.py:346-347: the actors' encoders do not mutate (the critic's
+            # encoder is of another type)
+            self.actors[a].encoder.disable_mutations()
+            self.actor_targets[a].encoder.disable_mutations()
         self.actor_optimizers = {a: torch.optim.Adam(self.actors[a].parameters(), lr=lr_actor) for a in self.agent_ids}
         self.critic_optimizers = {a: torch.optim.Adam(self.critics[a].parameters(), lr=lr_critic)
                                   for a in self.agent_ids}
@@ -161,6 +170,84 @@ class MADDPG(EvolvableAgentMixin):
     def _critic(self, cfg) -> ContinuousQNetwork:
         return ContinuousQNetwork(self.possible_observation_spaces, [self.action_space[a] for a in self.agent_ids],
                                   device=self.device, **copy.deepcopy(cfg))
+
+    # ---- architecture mutation (hpo/mutation.py:887-1011, 1163-1203) --------
+    @property
+    def can_mutate_architecture(self) -> bool:
+        # a population sharded over ranks does not replay the module draws
+        return not getattr(self, "sharded", False)
+
+    def policy_mutation_methods(self) -> list[str]:
+        """The actors ModuleDict's table: every agent's LAYER methods, then
+        every agent's NODE methods, each prefixed by its agent id (the
+        reference's ModuleDict under PYTHONHASHSEED=0, tests/golden
+        maddpgarch*: actor_methods)."""
+        layer, node = [], []
+        for a in self.agent_ids:
+            net = self.actors[a]
+            for m in net.mutation_methods:
+                (layer if net.is_layer_method(m) else node).append(f"{a}.{m}")
+        return layer + node
+
+    @staticmethod
+    def _find_analogous_mutation(sampled: str | None, available: list[str], policy_agent: str) -> str | None:
+        """Mutations._find_analogous_mutation (hpo/mutation.py:1163-1203)."""
+        if not sampled:
+            return None
+        if sampled in available:
+            return sampled
+        bottom = sampled.split(".")[-1]
+        for method in available:
+            parts = method.split(".")
+            if parts[-1] == bottom and (policy_agent in parts or "vector_mlp" in parts):
+                return method
+        return None
+
+    def architecture_mutation(self, new_layer_prob: float, rng) -> str | None:
+        """_architecture_mutate_multi (hpo/mutation.py:887-1011): a method
+        sampled from the actors' table with ``rng`` (Mutations.rng), applied to
+        the sampled agent's actor; the method it applied (with its mutation
+        dict) to every other actor that has it; then, per critic and once per
+        mutated agent (the reference's repeat guard), the analogous method.
+        The targets are re-made from the mutated networks
+        (reinit_shared_networks, :104-160).  -> the mutation label (the
+        applied method without its agent id) or None."""
+        from ..networks.base import mutation_probs
+
+        table = self.policy_mutation_methods()
+        mut_method = str(rng.choice(table, p=mutation_probs(table, new_layer_prob), size=1)[0])
+        agent, method = mut_method.split(".", 1)
+        applied, mut_dict = self.actors[agent].apply_mutation_dict(method)
+        mutated = []
+        if applied is not None:
+            sampled_agent, sampled = agent, applied
+            mutated.append(agent)
+        else:
+            sampled_agent, sampled = agent, None
+        for a in self.agent_ids:
+            if a == sampled_agent:
+                continue
+            if sampled in self.actors[a].mutation_methods:
+                done, _ = self.actors[a].apply_mutation_dict(sampled, mut_dict)
+                if done is not None:
+                    mutated.append(a)
+        self.critic_mutations = []
+        for a in self.agent_ids:
+            critic = self.critics[a]
+            analogous, last = False, None
+            for m_agent in mutated:
+                if analogous and last == analogous:
+                    continue
+                analogous = self._find_analogous_mutation(sampled, critic.mutation_methods, m_agent)
+                if analogous is None:
+                    raise RuntimeError(f"MADDPG architecture mutation: no analogous method for {sampled!r} in "
+                                       f"critic {a!r} ({critic.mutation_methods})")
+                last, _ = critic.apply_mutation_dict(analogous, mut_dict)
+                self.critic_mutations.append((a, analogous, str(last)))
+        for a in self.agent_ids:
+            self.actor_targets[a] = copy.deepcopy(self.actors[a])
+            self.critic_targets[a] = copy.deepcopy(self.critics[a])
+        return sampled
 
     # ---- acting (maddpg.py:456-625) ---------------------------------------
     def set_training_mode(self, training: bool) -> None:

@@ -61,13 +61,21 @@ def _image_spec(observation_space, action_space, net_config: dict, normalize_ima
     actor_hidden = _hidden(head, [32])
     critic_hidden = _hidden(head, [16])  # ppo.py:292-300 default critic head
     head_ln = bool((head or {}).get("layer_norm", True))
+    # architecture-mutation limits: the CNN's (CnnNetConfig defaults 1, 6, 16,
+    # 256, modules/configs.py:114-127), the heads' (MlpNetConfig: 1, 3, 16, 500)
+    # and the latent's (EvolvableNetwork: 8, 128)
+    cnn_limits = (int(enc.get("min_hidden_layers", 1)), int(enc.get("max_hidden_layers", 6)),
+                  int(enc.get("min_channel_size", 16)), int(enc.get("max_channel_size", 256)))
+    head_limits = _limits(head, head is None or not isinstance(head, dict))
+    latent_limits = (int(net_config.get("min_latent_dim", 8)), int(net_config.get("max_latent_dim", 128)))
     dtype = torch.uint8 if np.dtype(observation_space.dtype) == np.uint8 else torch.float32
     norm = image_norm_bounds(observation_space) if normalize_images else None
     return ImageActorCriticSpec(obs_shape=tuple(observation_space.shape), n_actions=int(action_space.n),
                                 channel_size=list(enc["channel_size"]), kernel_size=list(enc["kernel_size"]),
                                 stride_size=list(enc["stride_size"]), latent_dim=int(net_config.get("latent_dim", 32)),
                                 actor_hidden=actor_hidden, critic_hidden=critic_hidden, head_layer_norm=head_ln,
-                                obs_dtype=dtype, image_norm=norm)
+                                obs_dtype=dtype, image_norm=norm, cnn_limits=cnn_limits, actor_limits=head_limits,
+                                critic_limits=head_limits, latent_limits=latent_limits)
 
 
 def _limits(cfg, config_default: bool) -> tuple:
@@ -173,6 +181,10 @@ class PPO:
         # is reproducible and a sharded population draws as the whole one)
         self.module_rng = np.random.default_rng((0x5EED, int(index)))
         self.critic_rng = np.random.default_rng((0x5EEE, int(index)))
+        # CNN encoders' kernel-size helpers keep generators of their own
+        # (MutableKernelSizes, modules/cnn.py:55-72)
+        self.kernel_rng = np.random.default_rng((0x5EEF, int(index)))
+        self.critic_kernel_rng = np.random.default_rng((0x5EF0, int(index)))
         pop = self.population
         if _population is not None and (batch_size, update_epochs, ent_coef) != (
                 pop.agent_batch[self.row], pop.agent_epochs[self.row], pop.agent_ent[self.row]):
@@ -243,10 +255,13 @@ class PPO:
 
     @property
     def can_mutate_architecture(self) -> bool:
+        from ..population.image_nets import ImageActorCriticSpec
         from ..population.nets import ActorCriticSpec
 
-        # population/arch.py mutates the shared-encoder layout
-        return isinstance(self.spec, ActorCriticSpec) and self.spec.share_encoders
+        # population/arch.py (MLP) and population/image_arch.py (CNN encoder)
+        # mutate the shared-encoder layouts
+        return (isinstance(self.spec, ActorCriticSpec) and self.spec.share_encoders) or \
+            isinstance(self.spec, ImageActorCriticSpec)
 
     def architecture_mutation(self, new_layer_prob: float, rng) -> str | None:
         """mutation.py:829-885 on this agent (population/arch.py): -> the
@@ -256,11 +271,19 @@ class PPO:
         from ..population import arch
         from ..population.engine import AgentState
 
-        method = arch.sample_method(new_layer_prob, rng)
+        from ..population import image_arch
+        from ..population.image_nets import ImageActorCriticSpec
+
         spec, pop, r = self.spec, self.population, self.row
         flat = (self._pending_state.params if self._pending_state is not None
                 else pop.params.data[r, :spec.n_params]).cpu()
-        new_spec, new_flat, applied, _ = arch.mutate(spec, flat, method, self.module_rng, self.critic_rng)
+        if isinstance(spec, ImageActorCriticSpec):
+            method = image_arch.sample_method(new_layer_prob, rng)
+            new_spec, new_flat, applied, _ = image_arch.mutate(spec, flat, method, self.module_rng, self.kernel_rng,
+                                                               self.critic_rng, self.critic_kernel_rng)
+        else:
+            method = arch.sample_method(new_layer_prob, rng)
+            new_spec, new_flat, applied, _ = arch.mutate(spec, flat, method, self.module_rng, self.critic_rng)
         n = new_spec.n_params
         zeros = torch.zeros(n, dtype=torch.float32, device=pop.device)
         self._pending_state = AgentState(new_spec, self.learn_step, new_flat.to(pop.device), zeros.clone(),

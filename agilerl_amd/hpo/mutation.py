@@ -36,14 +36,25 @@ What runs, with the reference's draws from the reference's generators:
   :104-160) and fresh optimizers.  Policy-gradient algorithms (PPO, MADDPG)
   keep their activations, as the reference's :469-479.
 
-* ``architecture_mutate`` on DQN / Rainbow agents with MLP encoders: the
-  method from the same table (an EvolvableNetwork's: head layer / node,
-  encoder node, latent node), applied to the Q network with the modules' own
-  generators, the target network re-made from it, fresh optimizers.
+* ``architecture_mutate`` on PPO agents with CNN encoders (config 5):
+  population/image_arch.py on the flat rows, the CNN table (encoder channel /
+  kernel methods; its LAYER methods disabled), bit-exact against the
+  reference's own networks; the engine regroups them as the MLP agents.
 
-Not applied: architecture mutations of CNN-encoder Q networks and of MADDPG,
-and architecture / activation mutations of DQN / Rainbow agents in a
-population sharded over ranks (recorded as no mutation with a warning, on
+* ``architecture_mutate`` on DQN / Rainbow agents with MLP or CNN encoders:
+  the method from the network's table (head layer / node, latent node, and
+  the encoder's node methods: MLP nodes or CNN channels / kernels), applied
+  to the Q network with the network's generator, the target network re-made
+  from it, fresh optimizers (modules/cnn.py bit-exact per method).
+
+* ``architecture_mutate`` on MADDPG (config 4): _architecture_mutate_multi
+  (:887-1011) in algorithms/maddpg.py — the actors' ModuleDict table, the
+  applied method on every actor that has it, the analogous method on every
+  critic, targets re-made; bit-exact against the reference's own networks.
+
+Not applied: architecture / activation mutations of DQN / Rainbow / MADDPG
+agents in a population sharded over ranks (the modules' draws are not
+replayed on the other ranks; recorded as no mutation with a warning, on
 every rank alike).
 """
 
@@ -128,8 +139,8 @@ class Mutations:
         return individual
 
     def _not_applied(self, individual, what: str):
-        warnings.warn(f"agx Mutations: {what} mutations change the network shape the fused kernels are compiled "
-                      "for; not applied (recorded as no mutation)", stacklevel=3)
+        warnings.warn(f"agx Mutations: {what} mutations are not applied to this agent (a population sharded "
+                      "over ranks, or a network without evolvable modules); recorded as no mutation", stacklevel=3)
         individual.mut = "None"
         return individual
 
@@ -138,9 +149,11 @@ class Mutations:
         individuals that can change shape (PPO views: population/arch.py — the
         method sampled from the actor's table with self.rng, applied to the
         actor, the applied method to the critic, the shared encoder, then
-        mutation_hook and a fresh optimizer; DQN / Rainbow with MLP encoders:
-        algorithms/evolvable.py, the target re-made from the mutated network).
-        Other agents: not applied."""
+        mutation_hook and a fresh optimizer; CNN-encoder PPO agents:
+        population/image_arch.py; DQN / Rainbow with MLP or CNN encoders:
+        algorithms/evolvable.py, the target re-made from the mutated network;
+        MADDPG: _architecture_mutate_multi in algorithms/maddpg.py).  Sharded
+        object-level populations: not applied."""
         fn = getattr(individual, "architecture_mutation", None)
         if fn is None or not getattr(individual, "can_mutate_architecture", False):
             return self._not_applied(individual, "architecture")

@@ -128,6 +128,7 @@ class EvolvableMLP(nn.Module):
         self.init_layers, self.hidden_size = init_layers, list(hidden_size)
         self.noisy, self.noise_std = noisy, noise_std
         self.last_mutation_attr: str | None = None
+        self.disabled: set[str] = set()
         self.model = self._create()
 
     def _create(self) -> nn.Sequential:
@@ -184,6 +185,18 @@ class EvolvableMLP(nn.Module):
         self._init_gaussian(self.get_output_dense(), output_coeff)
 
     # ---- architecture mutations (mlp.py:214-336) ---------------------------
+    LAYER_METHODS = ("add_layer", "remove_layer")
+    NODE_METHODS = ("add_node", "remove_node")
+
+    def disable_mutations(self, kind: str | None = None) -> None:
+        """EvolvableModule.disable_mutations: "layer", "node" or both (None);
+        a disabled method leaves the owner's mutation table (networks/base.py
+        filters it)."""
+        if kind in (None, "layer"):
+            self.disabled.update(self.LAYER_METHODS)
+        if kind in (None, "node"):
+            self.disabled.update(self.NODE_METHODS)
+
     def change_activation(self, activation: str, output: bool = False) -> None:
         if output:
             self.output_activation = activation

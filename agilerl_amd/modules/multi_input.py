@@ -38,6 +38,32 @@ class EvolvableMultiInput(nn.Module):
         self.final_layernorm = nn.LayerNorm(num_outputs, device=device, elementwise_affine=False) \
             if output_layernorm else None
         self.output = get_activation(output_activation)
+        self.rng = np.random.default_rng(seed=random_seed)
+        self.last_mutation_attr: str | None = None
+        self.disabled: set[str] = set()
+
+    def disable_mutations(self, kind: str | None = None) -> None:
+        self.disabled.update(("add_latent_node", "remove_latent_node") if kind in (None, "node") else ())
+
+    def recreate_network(self) -> None:
+        """recreate_encoder (networks/base.py:493-503) for this encoder: a new
+        ``final_dense`` for the current ``num_outputs`` (torch's default
+        nn.Linear init, the module's only random draw), parameters kept where
+        the shapes overlap (preserve_parameters, modules/base.py:472-502)."""
+        old = self.final_dense
+        dev = old.weight.device
+        new = nn.Linear(self.total_vector_dims, self.num_outputs, device=dev)
+        with torch.no_grad():
+            for name in ("weight", "bias"):
+                o, n = getattr(old, name), getattr(new, name)
+                if o.shape == n.shape:
+                    setattr(new, name, o)
+                else:
+                    sl = tuple(slice(0, min(a, b)) for a, b in zip(o.shape, n.shape))
+                    n.data[sl] = o.data[sl]
+        self.final_dense = new
+        if self.final_layernorm is not None:
+            self.final_layernorm = nn.LayerNorm(self.num_outputs, device=dev, elementwise_affine=False)
 
     def forward(self, x) -> torch.Tensor:
         if isinstance(x, (tuple, list)):

@@ -76,6 +76,16 @@ def flatdim(space) -> int:
     return int(np.prod(space.shape))
 
 
+def mutation_probs(table: list[str], new_layer_prob: float) -> list[float]:
+    """EvolvableModule.get_mutation_probs (modules/base.py:661-685) over a
+    table of method names."""
+    layer = [m for m in table if m.split(".")[-1] in ("add_layer", "remove_layer")]
+    nl, nn_ = len(layer), len(table) - len(layer)
+    if nl == 0 or nn_ == 0:
+        return [1 / len(table)] * len(table)
+    return [new_layer_prob / nl if m in layer else (1 - new_layer_prob) / nn_ for m in table]
+
+
 class EvolvableNetwork(nn.Module):
     def __init__(self, observation_space, encoder_cls=None, encoder_config=None, action_space=None,
                  min_latent_dim: int = 8, max_latent_dim: int = 128, latent_dim: int = 32, simba: bool = False,
@@ -114,6 +124,8 @@ class EvolvableNetwork(nn.Module):
             self.encoder_config = encoder_config
             self.encoder = EvolvableCNN(input_shape=list(observation_space.shape), num_outputs=latent_dim,
                                         device=device, name=encoder_name, **encoder_config)
+            # the encoder's LAYER mutations are disabled (networks/base.py:266-268)
+            self.encoder.disable_mutations("layer")
             return
         # MLP encoders: output LayerNorm follows layer_norm, no output vanish (base.py:547-554)
         encoder_config["output_layernorm"] = encoder_config.get("layer_norm", True)
@@ -146,9 +158,13 @@ class EvolvableNetwork(nn.Module):
             self.encoder.set_image_norm(*bounds)
 
     def recreate_encoder(self) -> None:
-        cfg = dict(self.encoder.net_config)
+        """networks/base.py:493-503: the encoder rebuilt for the current latent,
+        parameters kept where the shapes overlap."""
         if isinstance(self.encoder, EvolvableCNN):
-            raise NotImplementedError("CNN architecture mutations change the conv shapes (not applied)")
+            self.encoder.num_outputs = self.latent_dim
+            self.encoder.recreate_network()
+            return
+        cfg = dict(self.encoder.net_config)
         new = EvolvableMLP(num_inputs=self.encoder.num_inputs, num_outputs=self.latent_dim, device=self.device,
                            name=self.encoder_name, **cfg)
         self.encoder = preserve_parameters(self.encoder, new)
@@ -184,17 +200,78 @@ class EvolvableNetwork(nn.Module):
             head.num_inputs = head.num_inputs - old_latent + self.latent_dim
             head.recreate_network()
 
-    def apply_mutation(self, method: str) -> str:
-        """One method of the mutation table (population/arch.py METHODS) on this
-        network -> the method actually applied (layer mutations at a limit
-        fall back to add_node, mlp.py:227-252)."""
+    # a multi-input encoder's (the MADDPG critic's) table, in the reference's
+    # order under PYTHONHASHSEED=0 (tests/golden maddpgarch*: critic_methods)
+    MULTI_INPUT_METHODS = ["head_net.remove_layer", "head_net.add_layer", "remove_latent_node", "add_latent_node",
+                           "encoder.remove_latent_node", "encoder.add_latent_node", "head_net.add_node",
+                           "head_net.remove_node"]
+
+    @property
+    def mutation_methods(self) -> list[str]:
+        """The network's mutation table in the reference's order under
+        PYTHONHASHSEED=0 (population/arch.py for MLP encoders,
+        population/image_arch.py for CNN encoders), without the methods its
+        modules disabled (EvolvableModule.disable_mutations)."""
+        from ..population import arch, image_arch
+        from ..modules.multi_input import EvolvableMultiInput
+
+        if isinstance(self.encoder, EvolvableCNN):
+            table = image_arch.METHODS
+        elif isinstance(self.encoder, EvolvableMultiInput):
+            table = self.MULTI_INPUT_METHODS
+        else:
+            table = arch.METHODS
+
+        def on(m: str) -> bool:
+            if "." not in m:
+                return True
+            owner, name = m.split(".", 1)
+            return name not in getattr(getattr(self, owner, None), "disabled", ())
+
+        return [m for m in table if on(m)]
+
+    @staticmethod
+    def is_layer_method(method: str) -> bool:
+        return method.split(".")[-1] in ("add_layer", "remove_layer")
+
+    def sample_mutation_method(self, new_layer_prob: float, rng) -> str:
+        """EvolvableModule.sample_mutation_method (modules/base.py:661-711):
+        layer methods share new_layer_prob, node methods the rest (uniform
+        when one kind is empty)."""
+        table = self.mutation_methods
+        return str(rng.choice(table, p=mutation_probs(table, new_layer_prob), size=1)[0])
+
+    def share_rng(self) -> None:
+        """ModuleMeta (modules/base.py:253-255): a network's evolvable modules
+        draw from the network's generator (a CNN's kernel-size helper keeps
+        its own)."""
+        for name in ("encoder", "head_net"):
+            mod = getattr(self, name, None)
+            if mod is not None and hasattr(mod, "rng"):
+                mod.rng = self.rng
+
+    def apply_mutation(self, method: str) -> str | None:
+        """One method of the mutation table on this network -> the method
+        actually applied (layer mutations at a limit fall back to add_node,
+        mlp.py:227-252; a CNN falls back as modules/cnn.py does), or None when
+        the fallback is a disabled method (MutationContext, base.py:181-190)."""
+        return self.apply_mutation_dict(method)[0]
+
+    def apply_mutation_dict(self, method: str, mut_dict: dict | None = None) -> tuple[str | None, dict]:
+        """_apply_arch_mutation (hpo/mutation.py:1013-1070) on this network:
+        ``method`` called with ``mut_dict`` as its arguments -> (the method
+        actually applied or None, the mutation dict it returned)."""
+        self.share_rng()
+        kw = dict(mut_dict or {})
         if method in ("add_latent_node", "remove_latent_node"):
-            getattr(self, method)()
-            return method
+            d = getattr(self, method)(**kw)
+            return method, d or {}
         owner, name = method.split(".")
         mod = getattr(self, owner)
-        getattr(mod, name)()
-        return f"{owner}.{mod.last_mutation_attr}"
+        d = getattr(mod, name)(**kw)
+        if mod.last_mutation_attr is None:
+            return None, d or {}
+        return f"{owner}.{mod.last_mutation_attr}", d or {}
 
     @property
     def activation(self) -> str | None:

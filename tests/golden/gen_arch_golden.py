@@ -95,9 +95,34 @@ class _Other(Space):
     pass
 
 
+class Dict(Space):
+    def __init__(self, spaces_=None):
+        super().__init__(None, None)
+        from collections import OrderedDict
+
+        self.spaces = OrderedDict(spaces_ or {})
+
+    def __getitem__(self, key):
+        return self.spaces[key]
+
+    def keys(self):
+        return self.spaces.keys()
+
+    def items(self):
+        return self.spaces.items()
+
+    def values(self):
+        return self.spaces.values()
+
+    def __len__(self):
+        return len(self.spaces)
+
+
 def _flatdim(space):
     if isinstance(space, Discrete):
         return space.n
+    if isinstance(space, Dict):
+        return sum(_flatdim(v) for v in space.spaces.values())
     return int(np.prod(space.shape))
 
 
@@ -135,9 +160,9 @@ def _load(ref: str, modname: str, relpath: str):
 def _setup(ref: str):
     gym = _package("gymnasium")
     sp = _package("gymnasium.spaces")
-    for cls in (Space, Box, Discrete):
+    for cls in (Space, Box, Discrete, Dict):
         setattr(sp, cls.__name__, cls)
-    for name in ("Dict", "Tuple", "MultiDiscrete", "MultiBinary", "Graph", "Text", "Sequence"):
+    for name in ("Tuple", "MultiDiscrete", "MultiBinary", "Graph", "Text", "Sequence"):
         setattr(sp, name, type(name, (_Other,), {}))
     sp.flatdim = _flatdim
     gym.spaces = sp
@@ -169,6 +194,9 @@ def _setup(ref: str):
         setattr(mods, name, type(name, (base.EvolvableModule,), {}))
     cnn = _load(ref, "agilerl.modules.cnn", "agilerl/modules/cnn.py")
     mods.EvolvableCNN = cnn.EvolvableCNN
+    mods.ModuleDict = base.ModuleDict
+    mi = _load(ref, "agilerl.modules.multi_input", "agilerl/modules/multi_input.py")
+    mods.EvolvableMultiInput = mi.EvolvableMultiInput
     _package("agilerl.networks")
     _load(ref, "agilerl.networks.distributions", "agilerl/networks/distributions.py")
     nb = _load(ref, "agilerl.networks.base", "agilerl/networks/base.py")
@@ -176,7 +204,7 @@ def _setup(ref: str):
     val = _load(ref, "agilerl.networks.value_networks", "agilerl/networks/value_networks.py")
     _load(ref, "agilerl.networks.custom_modules", "agilerl/networks/custom_modules.py")
     qn = _load(ref, "agilerl.networks.q_networks", "agilerl/networks/q_networks.py")
-    return dict(base=base, cfg=cfg, en=en, mlp=mlp, cnn=cnn, nb=nb, actors=act, values=val, qnets=qn)
+    return dict(base=base, cfg=cfg, en=en, mlp=mlp, cnn=cnn, nb=nb, actors=act, values=val, qnets=qn, mi=mi)
 
 
 def _apply_arch_mutation(network, mut_method, applied_mut_dict=None):
@@ -386,6 +414,134 @@ def gen_cnn_net_cases(m: dict, out: dict) -> None:
         idx += 1
 
 
+# ---------------------------------------------------------------------------
+# MADDPG (config 4): the multi-agent architecture mutation
+# ---------------------------------------------------------------------------
+MA_AGENTS = ("speaker_0", "listener_0")
+
+
+def _find_analogous_mutation(sampled_mutation, available_methods, policy_agent):
+    """agilerl/hpo/mutation.py:1163-1203, restated line by line."""
+    if not sampled_mutation:
+        return None
+    if sampled_mutation in available_methods:
+        return sampled_mutation
+    bottom = sampled_mutation.split(".")[-1]
+    for method in available_methods:
+        parts = method.split(".")
+        if parts[-1] == bottom and (policy_agent in parts or "vector_mlp" in parts):
+            return method
+    return None
+
+
+def _architecture_mutate_multi(actors, critics, new_layer_prob, rng):
+    """agilerl/hpo/mutation.py:887-1011 (_architecture_mutate_multi), restated
+    line by line on the reference's ModuleDicts (the algorithm object itself
+    would pull in the whole algorithm hierarchy): the method sampled from the
+    policy ModuleDict's table, applied to the sampled agent's actor, then to
+    the other actors that have it, then an analogous method to every critic
+    once per mutated agent (the repeat guard as written)."""
+    mut_method = actors.sample_mutation_method(new_layer_prob, rng)
+    applied_mutation, mut_dict = _apply_arch_mutation(actors, mut_method)
+    applied_mutations = []
+    if applied_mutation is not None:
+        split = applied_mutation.split(".")
+        sampled_agent_id, sampled_mutation = split[0], ".".join(split[1:])
+        applied_mutations.append(sampled_agent_id)
+    else:
+        sampled_agent_id, sampled_mutation = mut_method.split(".")[0], None
+    for agent_id, policy in actors.items():
+        if agent_id == sampled_agent_id:
+            continue
+        applied_agent = None
+        if sampled_mutation in policy.mutation_methods:
+            applied_agent, _ = _apply_arch_mutation(policy, sampled_mutation, mut_dict)
+        if applied_agent is not None:
+            applied_mutations.append(agent_id)
+    critic_applied = []
+    for agent_id, agent_eval in critics.items():
+        analogous = False
+        for mutated_agent in applied_mutations:
+            if analogous and agent_eval.last_mutation_attr == analogous:
+                continue
+            analogous = _find_analogous_mutation(sampled_mutation, agent_eval.mutation_methods, mutated_agent)
+            if analogous is None:
+                raise RuntimeError(f"no analogous method for {sampled_mutation}")
+            _apply_arch_mutation(agent_eval, analogous, mut_dict)
+            critic_applied.append((agent_id, analogous, str(agent_eval.last_mutation_attr)))
+    return mut_method, applied_mutation, sampled_mutation, mut_dict, applied_mutations, critic_applied
+
+
+def gen_maddpg_cases(m: dict, out: dict) -> None:
+    """MADDPG on simple_speaker_listener's spaces (speaker obs 3, listener obs
+    11; Discrete 3 / 5 actions) with maddpg.yaml's NET_CONFIG scaled down
+    (latent 24, encoder [16], head [16, 16]): actors DeterministicActor with
+    their encoders' mutations disabled (maddpg.py:338-348), critics
+    ContinuousQNetwork on the Dict of all observations + all actions with
+    the shared-critic encoder config (maddpg.py:306-335,
+    utils/algo_utils.py:606-665).  One architecture mutation per case."""
+    actors_mod, qn, base = m["actors"], m["qnets"], m["base"]
+    obs = {"speaker_0": Box(-np.inf, np.inf, (3,)), "listener_0": Box(-np.inf, np.inf, (11,))}
+    acts = {"speaker_0": Discrete(3), "listener_0": Discrete(5)}
+    enc = {"hidden_size": [16], "min_mlp_nodes": 8, "max_mlp_nodes": 64}
+    head = {"hidden_size": [16, 16], "activation": "ReLU", "min_hidden_layers": 1, "max_hidden_layers": 2,
+            "min_mlp_nodes": 8, "max_mlp_nodes": 64}
+    agent_cfg = {"latent_dim": 24, "min_latent_dim": 8, "max_latent_dim": 64, "encoder_config": enc,
+                 "head_config": head}
+    critic_cfg = {"encoder_config": {"mlp_config": copy.deepcopy(enc), "latent_dim": 16, "min_latent_dim": 8,
+                                     "max_latent_dim": 64},
+                  "head_config": copy.deepcopy(head), "latent_dim": 24, "min_latent_dim": 8, "max_latent_dim": 64}
+    idx = 0
+    for k in range(20):
+        nlp = (0.2, 0.5, 1.0, 0.0)[k % 4]
+        torch.manual_seed(600 + k)
+        a_nets, c_nets = {}, {}
+        for a in MA_AGENTS:
+            net = actors_mod.DeterministicActor(obs[a], acts[a], device="cpu", **copy.deepcopy(agent_cfg))
+            net.encoder.disable_mutations()
+            a_nets[a] = net
+        for a in MA_AGENTS:
+            c_nets[a] = qn.ContinuousQNetwork(observation_space=Dict(obs), action_space=Discrete(8), device="cpu",
+                                              **copy.deepcopy(critic_cfg))
+        actors = base.ModuleDict(a_nets)
+        critics = base.ModuleDict(c_nets)
+        for i, a in enumerate(MA_AGENTS):
+            a_nets[a].rng = np.random.default_rng(1700 + 10 * k + i)
+            c_nets[a].rng = np.random.default_rng(1800 + 10 * k + i)
+        g = {"actor_methods": np.array(actors.mutation_methods),
+             "actor_probs": np.array(actors.get_mutation_probs(nlp), dtype=np.float64),
+             "critic_methods": np.array(c_nets["speaker_0"].mutation_methods),
+             "single_actor_methods": np.array(a_nets["speaker_0"].mutation_methods),
+             "new_layer_prob": np.array(nlp),
+             "seeds": np.array([600 + k, 1700 + 10 * k, 1800 + 10 * k, 2600 + k, 5600 + k])}
+        before = {}
+        for a in MA_AGENTS:
+            before.update(_sd(f"actors.{a}", a_nets[a]))
+            before.update(_sd(f"critics.{a}", c_nets[a]))
+        torch.manual_seed(5600 + k)
+        rng = np.random.default_rng(2600 + k)
+        mut_method, applied, sampled, mut_dict, mutated, critic_applied = _architecture_mutate_multi(
+            actors, critics, nlp, rng)
+        g["sampled"] = np.array(str(mut_method))
+        g["applied"] = np.array("None" if applied is None else str(applied))
+        g["mut"] = np.array(sampled or "None")
+        g["mut_dict"] = np.array(repr(sorted((kk, int(v)) for kk, v in (mut_dict or {}).items())))
+        g["mutated_agents"] = np.array(repr(mutated))
+        g["critic_applied"] = np.array(repr(critic_applied))
+        g["shapes"] = np.array(repr({a: {"actor_latent": int(a_nets[a].latent_dim),
+                                         "actor_head": list(a_nets[a].head_net.net_config["hidden_size"]),
+                                         "critic_latent": int(c_nets[a].latent_dim),
+                                         "critic_head": list(c_nets[a].head_net.net_config["hidden_size"])}
+                                     for a in MA_AGENTS}))
+        for kk, v in before.items():
+            g[f"before.{kk}"] = v
+        for a in MA_AGENTS:
+            for kk, v in {**_sd(f"actors.{a}", a_nets[a]), **_sd(f"critics.{a}", c_nets[a])}.items():
+                g[f"after.{kk}"] = v
+        out[f"maddpgarch{idx}"] = g
+        idx += 1
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -398,6 +554,7 @@ def main() -> None:
     gen_cases(m, out)
     gen_cnn_cases(m, out)
     gen_cnn_net_cases(m, out)
+    gen_maddpg_cases(m, out)
     for name, arrays in out.items():
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
     meta_path = os.path.join(HERE, "META.json")
