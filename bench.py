@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (Atari PPO) side measurement")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (Atari Rainbow) learner measurement")
+    ap.add_argument("--no-train-on-policy", action="store_true",
+                    help="skip the end-to-end train_on_policy (ppo.yaml generations) measurement")
     ap.add_argument("--roof-reps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--dist-selftest", action="store_true",
@@ -544,26 +546,48 @@ def _cpu_threads() -> int:
         return os.cpu_count() or 1
 
 
-def cpu_population_all_cores(args, seconds):
-    """The same CPU PPO port with torch intra-op threads on every allowed core
-    (OMP_NUM_THREADS / affinity; 16 on a 1-GPU box)."""
+def _cpu_agent_worker(cfg, seconds, seed, q):
+    """One single-threaded CPU PPO agent (oracle/ppo_cpu.py) in its own
+    process: (env-steps, seconds) of whole iterations until ``seconds``."""
+    torch.set_num_threads(1)
     from agilerl_amd.envs import SyntheticVecEnv
     from oracle.ppo_cpu import CpuPPOAgent
 
-    threads = torch.get_num_threads()
-    n_thr = int(os.environ.get("OMP_NUM_THREADS", _cpu_threads()))
-    torch.set_num_threads(n_thr)
-    agent = CpuPPOAgent(num_envs=args.num_envs, learn_step=args.learn_step, batch_size=args.batch_size,
-                        update_epochs=args.epochs)
-    env = SyntheticVecEnv(args.num_envs, seed=7)
+    agent = CpuPPOAgent(**cfg)
+    env = SyntheticVecEnv(cfg["num_envs"], seed=seed)
+    agent.iteration(env)  # warm-up
     t0, steps = time.perf_counter(), 0
     while True:
         steps += agent.iteration(env)
         if time.perf_counter() - t0 >= seconds:
             break
-    dt = time.perf_counter() - t0
-    torch.set_num_threads(threads)
-    return dict(value=round(steps / dt, 1), unit="env-steps/s", cores=n_thr, kind="port")
+    q.put((steps, time.perf_counter() - t0))
+
+
+def cpu_population_all_cores(args, seconds, P: int = 8):
+    """The population on every host core the box gives this job: P agents as
+    P single-threaded processes of the CPU PPO port side by side (the
+    reference's agents are independent between generations), summed
+    env-steps/s.  (Torch intra-op threads on one agent's tiny ops were slower
+    than one thread: round-3 VERDICT.)  Processes are started with
+    ``spawn`` before nothing else — no GPU state is inherited."""
+    import multiprocessing as mp
+
+    n = max(1, min(P, _cpu_threads(), int(os.environ.get("OMP_NUM_THREADS", P))))
+    cfg = dict(num_envs=args.num_envs, learn_step=args.learn_step, batch_size=args.batch_size,
+               update_epochs=args.epochs)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cpu_agent_worker, args=(cfg, seconds, 7 + i, q)) for i in range(n)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=seconds + 300) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=60)
+    value = sum(s / t for s, t in res)
+    return dict(value=round(value, 1), unit="env-steps/s", cores=n, kind="port",
+                sample=f"{n} agents of oracle/ppo_cpu.py as {n} single-threaded processes side by side, "
+                       f"~{seconds:.0f}s of whole iterations each ({_cpu_threads()} CPUs allowed)")
 
 
 def _ppo_loss_torch_batched(logp, old_logp, adv, ret, old_v, v, H, b, clip, vf, ent):
@@ -793,6 +817,78 @@ CONFIG3_NET = {"latent_dim": 256, "min_latent_dim": 128, "max_latent_dim": 512,
                "head_config": {"hidden_size": [256]}}
 
 
+def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
+    """The end-to-end entry point: ``train_on_policy`` (training/train_on_policy.py)
+    on an 8-agent population with ppo.yaml's INIT_HP / NET_CONFIG /
+    MUTATION_PARAMS (LEARN_STEP 2048, BATCH 128, 4 epochs, EVO_STEPS 10240,
+    EVAL_STEPS empty = each evaluation episode runs to its end, tournament 2 with
+    elitism), N synthetic LunarLander-shaped envs per agent (the reference's
+    N-env cloned per agent).  Per generation: 5 collect + learn iterations per
+    agent, agent.test evaluation, tournament, mutations (RL hyperparameters,
+    parameters, architecture, learn_step) and the regroup.  Timed over
+    ``generations`` generations after one warm-up generation; env-steps are
+    the training steps the reference counts (agent.steps), evaluation steps
+    not included.  Reported twice: with ppo.yaml's mutation probabilities, and
+    with ARCH_MUT = 0 (every agent stays on the fused kernels)."""
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.mutation import Mutations
+    from agilerl_amd.hpo.registry import HyperparameterConfig, RLParameter
+    from agilerl_amd.hpo.tournament import TournamentSelection
+    from agilerl_amd.training import train_on_policy
+    from agilerl_amd.utils import create_population
+
+    INIT_HP = {"BATCH_SIZE": 128, "LR": 0.001, "LEARN_STEP": 2048, "GAMMA": 0.99, "GAE_LAMBDA": 0.95,
+               "CLIP_COEF": 0.2, "ENT_COEF": 0.01, "VF_COEF": 0.5, "MAX_GRAD_NORM": 0.5, "TARGET_KL": None,
+               "UPDATE_EPOCHS": 4}
+    NET_CONFIG = {"latent_dim": 64,
+                  "encoder_config": {"hidden_size": [64], "activation": "ReLU", "min_mlp_nodes": 64,
+                                     "max_mlp_nodes": 500, "layer_norm": True},
+                  "head_config": {"hidden_size": [64], "activation": "ReLU", "min_hidden_layers": 1,
+                                  "max_hidden_layers": 3, "min_mlp_nodes": 64, "max_mlp_nodes": 500,
+                                  "output_vanish": True, "layer_norm": True}}
+    evo_steps = 10_240
+    out = {"workload": f"train_on_policy, {P}-agent PPO population, ppo.yaml (evo_steps {evo_steps}, eval to "
+                       f"episode end, tournament 2 + elitism, MUT_P of ppo.yaml), {N} synthetic envs per agent",
+           "generations_timed": generations}
+
+    def run(arch: float, gens: int, seed: int):
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+        env = SyntheticVecEnv(N, seed=seed, p_done=1 / 200)
+        hp = HyperparameterConfig(lr=RLParameter(min=0.0001, max=0.01),
+                                  batch_size=RLParameter(min=8, max=1024, dtype=int),
+                                  learn_step=RLParameter(min=256, max=8192, dtype=int, grow_factor=1.5,
+                                                         shrink_factor=0.75),
+                                  ent_coef=RLParameter(min=0.001, max=0.1),
+                                  update_epochs=RLParameter(min=1, max=10, dtype=int))
+        pop = create_population("PPO", NET_CONFIG, INIT_HP, env.single_observation_space,
+                                env.single_action_space, hp_config=hp, population_size=P, num_envs=N)
+        mut = Mutations(no_mutation=0.4, architecture=arch, new_layer_prob=0.2, parameters=0.2, activation=0.2,
+                        rl_hp=0.2, mutation_sd=0.1, rand_seed=42)
+        tour = TournamentSelection(2, True, P, 1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pop, _ = train_on_policy(env, "LunarLanderSynthetic", "PPO", pop, INIT_HP=INIT_HP, max_steps=gens * evo_steps,
+                                 evo_steps=evo_steps, eval_steps=None, eval_loop=1, tournament=tour, mutation=mut,
+                                 verbose=False)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, pop
+
+    import warnings
+
+    for name, arch in (("ppo_yaml", 0.2), ("no_arch_mutation", 0.0)):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            run(arch, 1, 5)  # warm-up (first-use allocations, library start-up)
+            dt, pop = run(arch, generations, 6)
+        steps = sum(a.steps[-1] for a in pop)
+        fused = sum(a.population.fused_descriptor() is not None for a in pop)
+        out[name] = {"env_steps_per_s": round(steps / dt, 1), "ms_per_generation": round(dt / generations * 1e3, 2),
+                     "env_steps": int(steps), "agents_on_fused_kernels_at_end": int(fused),
+                     "final_shapes": sorted({str(a.spec.shape_key()[2:6]) for a in pop})}
+    return out
+
+
 def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15):
     """Config 3 (Atari Pong Rainbow DQN, pop 8): learner updates/s of the
     population-batched learner (algorithms/rainbow_pop.py) on uint8 4x84x84
@@ -850,7 +946,12 @@ def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         out[name] = {"learner_updates_per_s": round(P * iters / dt, 1), "ms_per_iteration": round(dt / iters * 1e3, 3)}
-    out["learner_updates_per_s"] = out["batched"]["learner_updates_per_s"]
+    # the headline is what the drop-in entry point runs: train_off_policy learns
+    # agent after agent (the reference's train_off_policy.py:355-429); the
+    # population-batched learner (one launch chain for all P agents, lock-step
+    # sampling) is reported beside it as an extra, not as the config-3 number
+    out["learner_updates_per_s"] = out["per_agent"]["learner_updates_per_s"]
+    out["entry_point"] = "per_agent (train_off_policy); batched = algorithms/rainbow_pop.py, not on the entry point"
     del learner, agents, memory
     torch.cuda.empty_cache()
     return out
@@ -971,6 +1072,7 @@ def main():
         kern = kernels_leg(roof["peak_measured"])
     c5 = config5_leg() if (world == 1 and not args.no_config5) else None
     c3 = config3_leg() if (world == 1 and not args.no_config3) else None
+    tp = train_on_policy_leg() if (world == 1 and not args.no_train_on_policy) else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline_leg(args, res["S"])
@@ -1017,6 +1119,7 @@ def main():
             "kernels": kern,
             "config5": c5,
             "config3": c3,
+            "train_on_policy": tp,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
