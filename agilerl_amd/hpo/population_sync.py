@@ -43,6 +43,11 @@ class PopulationSync:
         self._idx_h = None     # pinned parent indices -> device, non-blocking
         self._idx_d = None
         self._idx_ev = None
+        # loopback (tests): a one-rank group runs the multi-rank exchange — every
+        # parent row is packed, sent to this rank through the backend and
+        # unpacked — so the device-tensor collective path (RCCL) executes on a
+        # one-GPU box exactly as between ranks
+        self.loopback = False
         # gloo moves host tensors only: device rows cross through host staging
         self.comm_device = pop.device
         if world > 1 and dist.get_backend() == "gloo":
@@ -86,7 +91,7 @@ class PopulationSync:
         return self._fit_h.numpy().copy()
 
     def _all_gather(self, x: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
+        if self.world == 1 and not self.loopback:
             return x
         src = x.contiguous().to(self.comm_device)
         out = torch.empty((self.world * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=self.comm_device)
@@ -154,7 +159,7 @@ class PopulationSync:
         widths = [b.shape[1] for b in bufs]
         offs = np.concatenate([[0], np.cumsum(widths)]).tolist()
         mine = parents[me * P:(me + 1) * P]
-        if self.world == 1:  # a permutation-with-repeats of the rows: one gather per buffer
+        if self.world == 1 and not self.loopback:  # a permutation-with-repeats of the rows: one gather per buffer
             if mine == list(range(P)):
                 return
             if (pop.device.type == "cuda" and len(bufs) <= 8 and all(b.is_contiguous() for b in bufs)
@@ -167,7 +172,8 @@ class PopulationSync:
             return
         # rows each rank needs from each other rank (sorted, unique): the same
         # plan on every rank, derived from the shared parent list
-        need = [[sorted({q % P for q in parents[r * P:(r + 1) * P] if q // P == src}) if src != r else []
+        lb = self.loopback
+        need = [[sorted({q % P for q in parents[r * P:(r + 1) * P] if q // P == src}) if (src != r or lb) else []
                  for src in range(self.world)] for r in range(self.world)]
         ops, recv = [], {}
         sends = []
@@ -183,7 +189,7 @@ class PopulationSync:
             if rows:
                 recv[src] = torch.empty(len(rows), offs[-1], dtype=bufs[0].dtype, device=self.comm_device)
                 ops.append(dist.P2POp(dist.irecv, recv[src], src))
-        local = [j for j in range(P) if mine[j] // P == me]
+        local = [] if lb else [j for j in range(P) if mine[j] // P == me]
         snap = None
         if local:
             idx = torch.as_tensor([mine[j] % P for j in local], device=pop.device)

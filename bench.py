@@ -37,6 +37,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md, chip-level parameters (spec)
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak (spec)
 
 
+def log(msg: str) -> None:
+    """Progress on stderr (stdout carries only the one JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -828,8 +833,9 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
     parameters, architecture, learn_step) and the regroup.  Timed over
     ``generations`` generations after one warm-up generation; env-steps are
     the training steps the reference counts (agent.steps), evaluation steps
-    not included.  Reported twice: with ppo.yaml's mutation probabilities, and
-    with ARCH_MUT = 0 (every agent stays on the fused kernels)."""
+    not included.  Reported with ARCH_MUT = 0 (every agent stays on the fused
+    kernels; the other mutation kinds as ppo.yaml), and with AGX_BENCH_E2E_ARCH=1
+    also with ppo.yaml's ARCH_MUT 0.2."""
     from agilerl_amd.envs import SyntheticVecEnv
     from agilerl_amd.hpo.mutation import Mutations
     from agilerl_amd.hpo.registry import HyperparameterConfig, RLParameter
@@ -854,7 +860,9 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
     def run(arch: float, gens: int, seed: int):
         np.random.seed(seed)
         torch.manual_seed(seed)
-        env = SyntheticVecEnv(N, seed=seed, p_done=1 / 200)
+        # LunarLander-v3 episodes end at its TimeLimit (1000 steps) at the latest: the
+        # evaluation (EVAL_STEPS empty) runs every env to the end of its episode
+        env = SyntheticVecEnv(N, seed=seed, p_done=1 / 200, max_episode_steps=1000)
         hp = HyperparameterConfig(lr=RLParameter(min=0.0001, max=0.01),
                                   batch_size=RLParameter(min=8, max=1024, dtype=int),
                                   learn_step=RLParameter(min=256, max=8192, dtype=int, grow_factor=1.5,
@@ -870,17 +878,22 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
         t0 = time.perf_counter()
         pop, _ = train_on_policy(env, "LunarLanderSynthetic", "PPO", pop, INIT_HP=INIT_HP, max_steps=gens * evo_steps,
                                  evo_steps=evo_steps, eval_steps=None, eval_loop=1, tournament=tour, mutation=mut,
-                                 verbose=False)
+                                 verbose=bool(os.environ.get("AGX_BENCH_VERBOSE")))
         torch.cuda.synchronize()
         return time.perf_counter() - t0, pop
 
     import warnings
 
-    for name, arch in (("ppo_yaml", 0.2), ("no_arch_mutation", 0.0)):
+    variants = [("no_arch_mutation", 0.0)]
+    if os.environ.get("AGX_BENCH_E2E_ARCH"):  # ppo.yaml's ARCH_MUT 0.2 too (see DESIGN: mutated shapes)
+        variants.insert(0, ("ppo_yaml", 0.2))
+    for name, arch in variants:
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
             run(arch, 1, 5)  # warm-up (first-use allocations, library start-up)
+            log(f"train_on_policy {name}: warm-up done")
             dt, pop = run(arch, generations, 6)
+            log(f"train_on_policy {name}: {generations} generations in {dt:.1f} s")
         steps = sum(a.steps[-1] for a in pop)
         fused = sum(a.population.fused_descriptor() is not None for a in pop)
         out[name] = {"env_steps_per_s": round(steps / dt, 1), "ms_per_generation": round(dt / generations * 1e3, 2),
@@ -1058,6 +1071,7 @@ def main():
     _lib.load()
     if args.pop % world:
         raise SystemExit(f"bench.py: --pop {args.pop} agents cannot be sharded over {world} GPUs")
+    log("population leg")
     res = population_leg(args, world, rank, args.pop // world)
     weak = None
     if world > 1 and not args.no_weak:
@@ -1068,13 +1082,18 @@ def main():
                 "workload": f"{args.pop_per_gpu} agents per GPU ({args.pop_per_gpu * world}-agent population)"}
     roof = kern = None
     if not args.no_roofline:
+        log("roofline leg")
         roof = roofline_leg(args)
         kern = kernels_leg(roof["peak_measured"])
+    log("config-5 leg")
     c5 = config5_leg() if (world == 1 and not args.no_config5) else None
+    log("config-3 leg")
     c3 = config3_leg() if (world == 1 and not args.no_config3) else None
+    log("train_on_policy leg")
     tp = train_on_policy_leg() if (world == 1 and not args.no_train_on_policy) else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
+        log("CPU baseline legs")
         cpu = cpu_baseline_leg(args, res["S"])
         cpu["all_cores"] = cpu_population_all_cores(args, min(args.cpu_seconds, 10.0))
         cpu["roofline_workload"] = cpu_kernels_leg(min(args.cpu_seconds, 8.0))

@@ -33,7 +33,11 @@ def _free_port() -> int:
 class ActionRewardVecEnv:
     """LunarLander-shaped (obs 8, 4 actions); the reward depends on the
     action, episodes are truncated every 9 steps.  ``reseed`` gives a copy
-    its own stream (StackedVecEnv.from_shared)."""
+    its own stream (StackedVecEnv.from_shared).  Host-only steps: the
+    population paces persistent rollouts on it (both ranks' rollout kernels
+    resident on the one card at once)."""
+
+    agx_device_free = True
 
     def __init__(self, num_envs=16, seed=0):
         from agilerl_amd.envs import Box, Discrete
@@ -64,7 +68,6 @@ class ActionRewardVecEnv:
 
 def _run(world, rank, out_dir, port, arch=0.0):
     sys.path.insert(0, ROOT)
-    os.environ["AGX_PERSISTENT_ROLLOUT"] = "0"  # two processes share the card: per-step launches
     torch.cuda.set_device(0)
     import random
     import warnings
