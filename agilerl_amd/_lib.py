@@ -1,4 +1,5 @@
-"""ctypes binding of libagx.so (the C ABI declared in include/agx.h).
+"""ctypes binding of libagx.so (the C ABI declared in include/agx.h and
+include/agx_graph.h).
 
 This is the binding a maintainer of the reference would add (see
 INTEGRATION.md).  The product path has NO CPU fallback: if the library is
@@ -34,6 +35,10 @@ SIGNATURES = {
     "agx_ppo_learn_lds_bytes": (_SZ, [_P]),
     "agx_ppo_learn_workspace_bytes": (_SZ, [_P, _I, _I, _I]),
     "agx_ppo_learn_prepare": (_INT, [_P, _P, _P]),
+    # include/agx_graph.h: the runtime-shape learner
+    "agx_ppo_graph_check": (_INT, [_P]),
+    "agx_ppo_learn_graph_workspace_bytes": (_SZ, [_P, _I, _I, _I, _I]),
+    "agx_ppo_learn_graph": (_INT, [_P, _P, _P, _P]),
     "agx_ppo_learn": (_INT, [_P, _P, _P, _P]),
     "agx_ppo_act": (_INT, [_P, _I, _I, _P, _P, _I, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P,
                            _I, _P, _P, _P]),

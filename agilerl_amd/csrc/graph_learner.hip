@@ -1,0 +1,685 @@
+// Runtime-shape fused PPO learner (include/agx_graph.h): the learner for the
+// network shapes architecture mutations produce.
+//
+// agx_ppo_learn (learner.hip) compiles one plan per network shape: parameters
+// in LDS, Adam moments in registers, every offset a constant.  An
+// architecture mutation (hpo/mutation.py:829-885) moves an agent to one of
+// thousands of shapes — any depth of encoder / head, any width, a latent of
+// any size — so this kernel interprets a runtime LAYER LIST instead:
+//
+//   * one 512-thread workgroup per agent runs every epoch x minibatch update
+//     of PPO.learn (ppo.py:836-920) in one launch, like agx_ppo_learn;
+//   * a minibatch is processed layer by layer over all its rows: every Linear
+//     (forward, dW, dX) is ONE operand form, C = A . B^T with both operands
+//     contiguous along the contraction, on f32 MFMA 16x16x4 tiles read
+//     straight from the agent's L2-resident scratch.  The layouts that make
+//     that true are written where the data is produced: the row passes write
+//     each activation row-major (the next layer's forward) AND feature-major
+//     (the next layer's dW contracts over rows), and Adam writes every weight
+//     both as nn.Linear [out][in] (forward) and transposed (dX);
+//   * LayerNorm / ReLU forward and backward and the PPO loss are row passes,
+//     16 lanes per row (DPP row reductions); bias and LN-affine gradients are
+//     column passes over the feature-major buffers: every sum runs in one
+//     fixed order (an agent's update does not depend on its population);
+//   * two-group gradient-norm clip (ppo.py:910-911) and Adam
+//     (optimizer_wrapper.py:444-452) over the flat gradient row.
+#include <cmath>
+#include <cstdlib>
+
+#include "agx_common.h"
+#include "../../include/agx_graph.h"
+
+namespace agx {
+
+// the gather prologue of agx_ppo_learn (learner.hip): permuted, advantage-
+// normalised, minibatch-ordered copy of the rollout
+__global__ void ppo_gather_kernel(const float *__restrict__ obs, const long long *__restrict__ act,
+                                  const float *__restrict__ old_logp, const float *__restrict__ adv,
+                                  const float *__restrict__ ret, const float *__restrict__ old_v,
+                                  const double *__restrict__ adv_stats, const long long *__restrict__ perms,
+                                  const unsigned char *__restrict__ masks, int A, long long S, int D, int P,
+                                  float *__restrict__ gobs, int *__restrict__ gact, unsigned *__restrict__ gmask,
+                                  float *__restrict__ grow, unsigned *__restrict__ counters, int ncounters);
+
+namespace {
+
+constexpr int kGT = 512;
+constexpr int kGW = kGT / kWave;
+constexpr int kGL = AGX_PPO_GRAPH_MAX_LAYERS;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+struct GLay {
+    int fin, fout, w, b, g, be, ln, relu, src;
+    int acc;  // dX adds into the source's dY (a consumer processed earlier wrote it)
+    // per-agent scratch offsets (floats; -1: not kept): output row-major,
+    // output feature-major, xhat, rstd, d(output), transposed weight
+    long long yr, yc, xh, rs, dy, wt;
+};
+
+struct GArgs {
+    GLay L[kGL];
+    int nl, aout, cout, A, D, n, cstart, bp;
+    long long oc, dzr, dzc, t1, t2, gr, ws_agent;
+    float *ws;
+    float *params, *m, *v;
+    const float *lr;
+    float b1, b2, eps;
+    long long *step;
+    const float *gobs;
+    const int *gact;
+    const unsigned *gmask;
+    const float *grow;
+    long long S;
+    int E, B, P;
+    float clip, vf, ent, max_norm;
+    double target_kl;
+    const int *batch_p, *epochs_p;
+    const float *ent_p;
+    float *loss_out, *kl_out;
+    int *epochs_out;
+    const unsigned *skip;
+};
+
+template <int C>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), C, 0xf, 0xf, true));
+}
+// sum / max over the 16 lanes of a DPP row
+__device__ __forceinline__ float rsum16(float v) {
+    v += dpp<0xb1>(v);
+    v += dpp<0x4e>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return v;
+}
+__device__ __forceinline__ float rmax16(float v) {
+    v = fmaxf(v, dpp<0xb1>(v));
+    v = fmaxf(v, dpp<0x4e>(v));
+    v = fmaxf(v, dpp<0x141>(v));
+    v = fmaxf(v, dpp<0x140>(v));
+    return v;
+}
+__device__ __forceinline__ float bperm(int lane, float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(lane << 2, __builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+
+// C[M x N] = A[M x K] . B[N x K]^T, both operands contiguous along k; one
+// 16x16 tile per wave at a time, 64 k per round trip (32 loads in flight per
+// lane).  MFMA j of a 16-k block takes k = 4q + (j & 3) from lane group q, so
+// each lane's four k of a block are adjacent words.  epi(m, n, c) per element.
+template <class FE>
+__device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B, int ldb, int M, int N, int K,
+                                        FE epi) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, q = lane >> 4;
+    const int mt = (M + 15) >> 4, nt = (N + 15) >> 4;
+    for (int t = wave; t < mt * nt; t += kGW) {
+        const int m0 = (t % mt) << 4, n0 = (t / mt) << 4;
+        const bool aok = m0 + r < M, bok = n0 + r < N;
+        const float *ap = A + (size_t)(aok ? m0 + r : 0) * lda;
+        const float *bp = B + (size_t)(bok ? n0 + r : 0) * ldb;
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int k0 = 0; k0 < K; k0 += 64) {
+            float a[16], b[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int k = k0 + 16 * (j >> 2) + 4 * q + (j & 3);
+                a[j] = (aok && k < K) ? ap[k] : 0.f;
+                b[j] = (bok && k < K) ? bp[k] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = m0 + 4 * q + i, n = n0 + r;
+            if (m < M && n < N) epi(m, n, acc[i]);
+        }
+    }
+}
+
+// fixed-order workgroup sum of two per-thread values
+__device__ __forceinline__ void block_sum2(float &a, float &b, float *red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    a = wave_sum(a);
+    b = wave_sum(b);
+    __syncthreads();  // red may still be read by the previous call
+    if (lane == 0) {
+        red[wave] = a;
+        red[kGW + wave] = b;
+    }
+    __syncthreads();
+    float ta = 0.f, tb = 0.f;
+    for (int i = 0; i < kGW; ++i) {
+        ta += red[i];
+        tb += red[kGW + i];
+    }
+    a = ta;
+    b = tb;
+}
+
+__global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
+    __shared__ float red[2 * kGW];
+    if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
+    const int p = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = lane & 15, rq = lane >> 4;
+    float *const pr = g.params + (size_t)p * g.n;
+    float *const gm = g.m + (size_t)p * g.n;
+    float *const gv = g.v + (size_t)p * g.n;
+    float *const base = g.ws + (size_t)p * g.ws_agent;
+    float *const G = base + g.gr;
+    const int bp = g.bp, A = g.A, D = g.D;
+    const long long S = g.S;
+
+    // transposed weight copies (the dX operand)
+    for (int l = 0; l < g.nl; ++l) {
+        const GLay &L = g.L[l];
+        if (L.wt < 0) continue;
+        float *wt = base + L.wt;
+        for (int i = tid; i < L.fout * L.fin; i += kGT) {
+            const int o = i / L.fin, c = i - o * L.fin;
+            wt[(size_t)c * L.fout + o] = pr[L.w + i];
+        }
+    }
+    __syncthreads();
+
+    int Bp = g.batch_p ? g.batch_p[p] : g.B;
+    if (Bp > g.B) Bp = g.B;  // the scratch holds g.B rows (the caller's batch: the population's largest)
+    const int Ep = g.epochs_p ? g.epochs_p[p] : g.E;
+    const float entp = g.ent_p ? g.ent_p[p] : g.ent;
+    const int nmb = (int)((S + Bp - 1) / Bp);
+    float loss_total = 0.f;
+    double kl_total = 0.0;
+    int n_done = 0, epochs_done = 0;
+    const long long step0 = g.step[p];
+    double pb1 = pow((double)g.b1, (double)step0), pb2 = pow((double)g.b2, (double)step0);
+    const float lr_p = g.lr[p];
+
+    for (int e = 0; e < Ep; ++e) {
+        const size_t ge = (size_t)e * g.P + p;
+        const float *gobs_e = g.gobs + ge * S * D;
+        const int *gact_e = g.gact + ge * S;
+        const unsigned *gmask_e = g.gmask ? g.gmask + ge * S : nullptr;
+        const float *grow_e = g.grow + ge * 4 * S;
+        for (int mb = 0; mb < nmb; ++mb) {
+            const long long s0 = (long long)mb * Bp;
+            const int bsz = (int)((s0 + Bp <= S) ? Bp : S - s0);
+            const float inv_b = 1.f / (float)bsz;
+            const float *xobs = gobs_e + s0 * D;
+
+            // observation, feature-major (the first layer's dW operand)
+            for (int i = tid; i < bsz * D; i += kGT) {
+                const int b = i / D, d = i - b * D;
+                base[g.oc + (size_t)d * bp + b] = xobs[i];
+            }
+
+            // ---- forward, layer by layer ------------------------------------
+            for (int l = 0; l < g.nl; ++l) {
+                const GLay &L = g.L[l];
+                const float *x = L.src < 0 ? xobs : base + g.L[L.src].yr;
+                float *yr = base + L.yr;
+                const int F = L.fout;
+                const float *bias = pr + L.b;
+                gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin,
+                        [&](int m, int n, float c) { yr[(size_t)m * F + n] = c + bias[n]; });
+                __syncthreads();
+                if (L.ln == 0 && !L.relu && L.yc < 0) continue;
+                // LayerNorm(+affine) / ReLU, 16 lanes per row
+                const float invF = 1.f / (float)F;
+                for (int r0 = 0; r0 < bsz; r0 += 4 * kGW) {
+                    const int row = r0 + 4 * wave + rq;
+                    const bool live = row < bsz;
+                    // three passes over the row's columns (re-reads hit L1): sum,
+                    // centred sum of squares, then xhat / y out
+                    float s = 0.f;
+                    if (live)
+                        for (int j = sub; j < F; j += 16) s += yr[(size_t)row * F + j];
+                    float mean = 0.f, rstd = 1.f;
+                    if (L.ln) {
+                        mean = rsum16(s) * invF;
+                        float vs = 0.f;
+                        if (live)
+                            for (int j = sub; j < F; j += 16) {
+                                const float dz = yr[(size_t)row * F + j] - mean;
+                                vs += dz * dz;
+                            }
+                        rstd = 1.f / sqrtf(rsum16(vs) / (float)F + 1e-5f);
+                        if (live && sub == 0) base[L.rs + row] = rstd;
+                    }
+                    if (!live) continue;
+                    for (int j = sub; j < F; j += 16) {
+                        float y = yr[(size_t)row * F + j];
+                        if (L.ln) {
+                            const float xh = (y - mean) * rstd;
+                            base[L.xh + (size_t)row * F + j] = xh;
+                            y = L.ln == 2 ? xh * pr[L.g + j] + pr[L.be + j] : xh;
+                        }
+                        if (L.relu) y = relu(y);
+                        yr[(size_t)row * F + j] = y;
+                        if (L.yc >= 0) base[L.yc + (size_t)j * bp + row] = y;
+                    }
+                }
+                __syncthreads();
+            }
+
+            // ---- loss row pass: logits / value -> d(logits), d(value) (ppo.py:876-908)
+            float lsum = 0.f, klsum = 0.f;
+            {
+                const GLay &La = g.L[g.aout];
+                const GLay &Lc = g.L[g.cout];
+                const float *lgp = base + La.yr;
+                const float *vp = base + Lc.yr;
+                float *dla = base + La.dy;
+                float *dlv = base + Lc.dy;
+                const int a0 = sub, a1 = sub + 16;
+                for (int r0 = 0; r0 < bsz; r0 += 4 * kGW) {
+                    const int row0 = r0 + 4 * wave + rq;
+                    const bool live = row0 < bsz;
+                    const int row = live ? row0 : 0;
+                    const unsigned bits = gmask_e ? gmask_e[s0 + row] : 0xffffffffu;
+                    const bool ok0 = (bits >> a0) & 1u, ok1 = (bits >> a1) & 1u;
+                    const float lg0 = a0 < A ? (ok0 ? lgp[(size_t)row * A + a0] : -1.0e8f) : -3.0e38f;
+                    const float lg1 = a1 < A ? (ok1 ? lgp[(size_t)row * A + a1] : -1.0e8f) : -3.0e38f;
+                    const float mx = rmax16(fmaxf(lg0, lg1));
+                    const float ex0 = a0 < A ? expf(lg0 - mx) : 0.f, ex1 = a1 < A ? expf(lg1 - mx) : 0.f;
+                    const float lse = mx + logf(rsum16(ex0 + ex1));
+                    const float p0 = a0 < A ? expf(lg0 - lse) : 0.f, p1 = a1 < A ? expf(lg1 - lse) : 0.f;
+                    const float lpe0 = logf(p0 + 1e-8f), lpe1 = logf(p1 + 1e-8f);
+                    const float Hs = -rsum16((a0 < A ? p0 * lpe0 : 0.f) + (a1 < A ? p1 * lpe1 : 0.f));
+                    const float gh0 = -(lpe0 + p0 / (p0 + 1e-8f)), gh1 = -(lpe1 + p1 / (p1 + 1e-8f));
+                    const float pg = rsum16((a0 < A ? p0 * gh0 : 0.f) + (a1 < A ? p1 * gh1 : 0.f));
+                    const int a_t = gact_e[s0 + row];
+                    const int srcl = (lane & ~15) + (a_t & 15);
+                    const float t0 = bperm(srcl, lg0), t1 = bperm(srcl, lg1);
+                    const float logp = (a_t < 16 ? t0 : t1) - lse;
+                    const float olp = grow_e[s0 + row], Ad = grow_e[S + s0 + row], R = grow_e[2 * S + s0 + row],
+                                ov = grow_e[3 * S + s0 + row];
+                    const float lo = 1.f - g.clip, hi = 1.f + g.clip;
+                    const float lrt = logp - olp;
+                    const float ratio = expf(lrt);
+                    const float rcl = fminf(fmaxf(ratio, lo), hi);
+                    const float q1 = -Ad * ratio, q2 = -Ad * rcl;
+                    const float g1 = q1 > q2 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
+                    const float g2 = q2 > q1 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
+                    const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+                    const float g_logp = ((g1 * -Ad + g2 * -Ad * inr) * inv_b) * ratio;
+                    const float v = vp[row];
+                    const float dv = v - ov;
+                    const float vcl = ov + fminf(fmaxf(dv, -g.clip), g.clip);
+                    const float eu = v - R, ec = vcl - R;
+                    const float lu = eu * eu, lc = ec * ec;
+                    const float gu = lu > lc ? 1.f : (lu == lc ? 0.5f : 0.f);
+                    const float gc = lc > lu ? 1.f : (lu == lc ? 0.5f : 0.f);
+                    const float inv = (dv >= -g.clip && dv <= g.clip) ? 1.f : 0.f;
+                    const float g_H = -entp * inv_b;
+                    const float dl0 = g_logp * ((a0 == a_t ? 1.f : 0.f) - p0) + g_H * p0 * (gh0 - pg);
+                    const float dl1 = g_logp * ((a1 == a_t ? 1.f : 0.f) - p1) + g_H * p1 * (gh1 - pg);
+                    if (live) {
+                        if (a0 < A) dla[(size_t)row * A + a0] = ok0 ? dl0 : 0.f;
+                        if (a1 < A) dla[(size_t)row * A + a1] = ok1 ? dl1 : 0.f;
+                        if (sub == 0) {
+                            dlv[row] = g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv);
+                            lsum += (fmaxf(q1, q2) + g.vf * 0.5f * fmaxf(lu, lc) - entp * Hs) * inv_b;
+                            klsum += ((ratio - 1.f) - lrt) * inv_b;  // approx_kl (ppo.py:899-902)
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+
+            // ---- backward, layer by layer (reverse) ----------------------------
+            float *dzr = base + g.dzr, *dzc = base + g.dzc, *t1c = base + g.t1, *t2c = base + g.t2;
+            for (int l = g.nl - 1; l >= 0; --l) {
+                const GLay &L = g.L[l];
+                const int F = L.fout;
+                const float *dy = base + L.dy;
+                const float invF = 1.f / (float)F;
+                // dY -> dZ through ReLU and LayerNorm(+affine)
+                for (int r0 = 0; r0 < bsz; r0 += 4 * kGW) {
+                    const int row = r0 + 4 * wave + rq;
+                    const bool live = row < bsz;
+                    // d(pre-activation) of column j: dY masked by the ReLU
+                    auto dpre = [&](int j) {
+                        const float d = dy[(size_t)row * F + j];
+                        return (!L.relu || base[L.yr + (size_t)row * F + j] > 0.f) ? d : 0.f;
+                    };
+                    float m1 = 0.f, m2 = 0.f, rstd = 1.f;
+                    if (L.ln) {
+                        float s1 = 0.f, s2 = 0.f;
+                        if (live)
+                            for (int j = sub; j < F; j += 16) {
+                                const float dx = L.ln == 2 ? dpre(j) * pr[L.g + j] : dpre(j);
+                                s1 += dx;
+                                s2 += dx * base[L.xh + (size_t)row * F + j];
+                            }
+                        m1 = rsum16(s1) * invF;
+                        m2 = rsum16(s2) * invF;
+                        rstd = live ? base[L.rs + row] : 0.f;
+                    }
+                    if (!live) continue;
+                    for (int j = sub; j < F; j += 16) {
+                        const float d = dpre(j);
+                        float dz = d;
+                        if (L.ln) {
+                            const float xh = base[L.xh + (size_t)row * F + j];
+                            const float dx = L.ln == 2 ? d * pr[L.g + j] : d;
+                            dz = rstd * (dx - m1 - xh * m2);
+                            if (L.ln == 2) {
+                                t1c[(size_t)j * bp + row] = d * xh;
+                                t2c[(size_t)j * bp + row] = d;
+                            }
+                        }
+                        dzr[(size_t)row * F + j] = dz;
+                        dzc[(size_t)j * bp + row] = dz;
+                    }
+                }
+                __syncthreads();
+                // bias / LN-affine gradients: column sums over the rows (fixed order)
+                for (int o0 = 0; o0 < F; o0 += 4 * kGW) {
+                    const int o = o0 + 4 * wave + rq;
+                    const bool on = o < F;
+                    float sb = 0.f, sg = 0.f, sbe = 0.f;
+                    if (on) {
+                        for (int b = sub; b < bsz; b += 16) {
+                            sb += dzc[(size_t)o * bp + b];
+                            if (L.ln == 2) {
+                                sg += t1c[(size_t)o * bp + b];
+                                sbe += t2c[(size_t)o * bp + b];
+                            }
+                        }
+                    }
+                    sb = rsum16(sb);
+                    if (L.ln == 2) {
+                        sg = rsum16(sg);
+                        sbe = rsum16(sbe);
+                    }
+                    if (on && sub == 0) {
+                        G[L.b + o] = sb;
+                        if (L.ln == 2) {
+                            G[L.g + o] = sg;
+                            G[L.be + o] = sbe;
+                        }
+                    }
+                }
+                // dW = dZ^T X (contraction over the rows)
+                const float *xc = L.src < 0 ? base + g.oc : base + g.L[L.src].yc;
+                float *gw = G + L.w;
+                const int fin = L.fin;
+                gemm_nt(dzc, bp, xc, bp, F, fin, bsz, [&](int m, int n, float c) { gw[(size_t)m * fin + n] = c; });
+                // dX = dZ W into the source's dY
+                if (L.src >= 0) {
+                    float *dys = base + g.L[L.src].dy;
+                    const bool acc = L.acc != 0;
+                    gemm_nt(dzr, F, base + L.wt, F, bsz, fin, F, [&](int m, int n, float c) {
+                        float *d = dys + (size_t)m * fin + n;
+                        *d = acc ? *d + c : c;
+                    });
+                }
+                __syncthreads();
+            }
+
+            // ---- loss / kl, clip, Adam ------------------------------------------
+            block_sum2(lsum, klsum, red);
+            if (tid == 0) loss_total += lsum;
+            kl_total += (double)klsum;
+            ++n_done;
+            float q0 = 0.f, q1 = 0.f;
+            for (int f = tid; f < g.n; f += kGT) {
+                const float x = G[f];
+                if (f < g.cstart) q0 += x * x;
+                else q1 += x * x;
+            }
+            block_sum2(q0, q1, red);
+            const float c0 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(q0) + 1e-6f), 1.f) : 1.f;
+            const float c1 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(q1) + 1e-6f), 1.f) : 1.f;
+            pb1 *= (double)g.b1;
+            pb2 *= (double)g.b2;
+            const float bc1 = (float)(1.0 - pb1);
+            const float bc2s = (float)sqrt(1.0 - pb2);
+            const float step_size = lr_p / bc1;
+            const float ob1 = 1.f - g.b1, ob2 = 1.f - g.b2;
+            auto adam = [&](int f) {
+                const float gc = G[f] * (f < g.cstart ? c0 : c1);
+                const float m = gm[f] + ob1 * (gc - gm[f]);
+                const float v = gv[f] * g.b2 + ob2 * gc * gc;
+                gm[f] = m;
+                gv[f] = v;
+                const float np = pr[f] - step_size * (m / (sqrtf(v) / bc2s + g.eps));
+                pr[f] = np;
+                return np;
+            };
+            for (int l = 0; l < g.nl; ++l) {
+                const GLay &L = g.L[l];
+                const int nw = L.fout * L.fin;
+                for (int i = tid; i < nw; i += kGT) {
+                    const float np = adam(L.w + i);
+                    if (L.wt >= 0) {
+                        const int o = i / L.fin, c = i - o * L.fin;
+                        base[L.wt + (size_t)c * L.fout + o] = np;
+                    }
+                }
+                for (int i = tid; i < L.fout; i += kGT) {
+                    adam(L.b + i);
+                    if (L.ln == 2) {
+                        adam(L.g + i);
+                        adam(L.be + i);
+                    }
+                }
+            }
+            __syncthreads();
+        }  // minibatches
+        ++epochs_done;
+        if (g.target_kl > 0.0 && kl_total / (double)n_done > g.target_kl) break;  // ppo.py:917-918
+    }  // epochs
+    if (tid == 0) {
+        if (g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)Ep);
+        if (g.kl_out) g.kl_out[p] = n_done ? (float)(kl_total / (double)n_done) : 0.f;
+        if (g.epochs_out) g.epochs_out[p] = epochs_done;
+        g.step[p] = step0 + n_done;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+long long r4(long long x) { return (x + 3) & ~3ll; }
+
+// validate the layer list; fill the layer table and the per-agent scratch plan
+int plan_graph(const agx_ppo_graph *net, int64_t batch, GArgs &a) {
+    AGX_REQUIRE(net, "agx_ppo_graph: null graph");
+    const int nl = net->n_layers;
+    AGX_REQUIRE(nl >= 2 && nl <= kGL, "agx_ppo_graph: %d layers (2..%d)", nl, kGL);
+    AGX_REQUIRE(net->obs_dim >= 1 && net->n_params > 0 && net->critic_start > 0 && net->critic_start < net->n_params,
+                "agx_ppo_graph: bad sizes");
+    AGX_REQUIRE(net->n_actions >= 1 && net->n_actions <= AGX_PPO_GRAPH_MAX_ACTIONS,
+                "agx_ppo_graph: %d actions (1..%d)", net->n_actions, AGX_PPO_GRAPH_MAX_ACTIONS);
+    AGX_REQUIRE(net->actor_out >= 0 && net->actor_out < nl && net->critic_out >= 0 && net->critic_out < nl &&
+                    net->actor_out != net->critic_out,
+                "agx_ppo_graph: bad output layers");
+    const int64_t bp = (batch + 15) / 16 * 16;
+    AGX_REQUIRE(batch >= 1 && bp < (1 << 30), "agx_ppo_graph: bad batch %lld", (long long)batch);
+    bool is_src[kGL] = {};
+    int maxw = 0;
+    long long nw = 0;
+    for (int l = 0; l < nl; ++l) {
+        const agx_ppo_layer &x = net->layers[l];
+        AGX_REQUIRE(x.src >= -1 && x.src < l, "agx_ppo_graph: layer %d reads layer %d (not topological)", l, x.src);
+        const int fin = x.src < 0 ? net->obs_dim : net->layers[x.src].fout;
+        AGX_REQUIRE(x.fin == fin && x.fout >= 1, "agx_ppo_graph: layer %d width mismatch", l);
+        AGX_REQUIRE(x.ln >= 0 && x.ln <= 2, "agx_ppo_graph: layer %d ln %d", l, x.ln);
+        AGX_REQUIRE((x.ln == 0 && !x.relu) || x.fout <= AGX_PPO_GRAPH_MAX_WIDTH,
+                    "agx_ppo_graph: layer %d width %d > %d", l, x.fout, AGX_PPO_GRAPH_MAX_WIDTH);
+        auto in = [&](long long off, long long len) { return off >= 0 && off + len <= net->n_params; };
+        AGX_REQUIRE(in(x.w, (long long)x.fin * x.fout) && in(x.b, x.fout) &&
+                        (x.ln != 2 || (in(x.ln_w, x.fout) && in(x.ln_b, x.fout))),
+                    "agx_ppo_graph: layer %d parameters outside the row", l);
+        if (x.src >= 0) is_src[x.src] = true;
+        maxw = x.fout > maxw ? x.fout : maxw;
+        nw += (long long)x.fin * x.fout + x.fout * (x.ln == 2 ? 3 : 1);
+    }
+    AGX_REQUIRE(nw == net->n_params, "agx_ppo_graph: layers cover %lld of %d parameters", nw, net->n_params);
+    const agx_ppo_layer &la = net->layers[net->actor_out], &lc = net->layers[net->critic_out];
+    AGX_REQUIRE(la.fout == net->n_actions && lc.fout == 1 && la.ln == 0 && lc.ln == 0 && !la.relu && !lc.relu &&
+                    !is_src[net->actor_out] && !is_src[net->critic_out],
+                "agx_ppo_graph: the output layers must be plain Linear(-> n_actions) / Linear(-> 1)");
+    long long off = 0;
+    bool seen[kGL] = {};
+    for (int l = nl - 1; l >= 0; --l) {  // backward order: the first consumer writes dY, later ones add
+        const int s = net->layers[l].src;
+        a.L[l].acc = (s >= 0 && seen[s]) ? 1 : 0;
+        if (s >= 0) seen[s] = true;
+    }
+    for (int l = 0; l < nl; ++l) {
+        const agx_ppo_layer &x = net->layers[l];
+        GLay &L = a.L[l];
+        L.fin = x.fin;
+        L.fout = x.fout;
+        L.w = x.w;
+        L.b = x.b;
+        L.g = x.ln == 2 ? x.ln_w : -1;
+        L.be = x.ln == 2 ? x.ln_b : -1;
+        L.ln = x.ln;
+        L.relu = x.relu ? 1 : 0;
+        L.src = x.src;
+        L.yr = off;
+        off = r4(off + bp * x.fout);
+        L.yc = -1;
+        if (is_src[l]) {
+            L.yc = off;
+            off = r4(off + (long long)x.fout * bp);
+        }
+        L.xh = L.rs = -1;
+        if (x.ln) {
+            L.xh = off;
+            off = r4(off + bp * x.fout);
+            L.rs = off;
+            off = r4(off + bp);
+        }
+        L.dy = off;
+        off = r4(off + bp * x.fout);
+        L.wt = -1;
+        if (x.src >= 0) {
+            L.wt = off;
+            off = r4(off + (long long)x.fin * x.fout);
+        }
+    }
+    a.oc = off;
+    off = r4(off + (long long)net->obs_dim * bp);
+    a.dzr = off;
+    off = r4(off + bp * maxw);
+    a.dzc = off;
+    off = r4(off + bp * maxw);
+    a.t1 = off;
+    off = r4(off + bp * maxw);
+    a.t2 = off;
+    off = r4(off + bp * maxw);
+    a.gr = off;
+    off = r4(off + net->n_params);
+    a.ws_agent = (off + 63) & ~63ll;  // 256-byte aligned agent blocks
+    a.nl = nl;
+    a.aout = net->actor_out;
+    a.cout = net->critic_out;
+    a.A = net->n_actions;
+    a.D = net->obs_dim;
+    a.n = net->n_params;
+    a.cstart = net->critic_start;
+    a.bp = (int)bp;
+    return AGX_OK;
+}
+
+struct GraphWs {
+    size_t gobs, gact, gmask, grow, agents, total;
+};
+GraphWs graph_ws(const GArgs &a, int64_t P, int64_t S, int64_t epochs) {
+    GraphWs w;
+    const size_t per = (size_t)epochs * P * S;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    w.gobs = 0;
+    w.gact = up(per * a.D * 4);
+    w.gmask = w.gact + up(per * 4);
+    w.grow = w.gmask + up(per * 4);
+    w.agents = w.grow + up(per * 4 * 4);
+    w.total = w.agents + (size_t)P * a.ws_agent * 4;
+    return w;
+}
+
+}  // namespace
+}  // namespace agx
+
+using namespace agx;
+
+extern "C" int agx_ppo_graph_check(const agx_ppo_graph *net) {
+    GArgs a{};
+    return plan_graph(net, 1, a);
+}
+
+extern "C" size_t agx_ppo_learn_graph_workspace_bytes(const agx_ppo_graph *net, int64_t P, int64_t S,
+                                                      int64_t epochs, int64_t batch) {
+    GArgs a{};
+    if (P <= 0 || S <= 0 || epochs <= 0 || batch <= 0) return 0;
+    if (plan_graph(net, batch < S ? batch : S, a) != AGX_OK) return 0;
+    return graph_ws(a, P, S, epochs).total;
+}
+
+extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn_args *x, void *workspace,
+                                   void *stream) {
+    AGX_REQUIRE(net && x && workspace, "agx_ppo_learn_graph: null net / args / workspace");
+    AGX_REQUIRE(x->params && x->exp_avg && x->exp_avg_sq && x->adam_step && x->lr && x->obs && x->actions &&
+                    x->old_logp && x->adv && x->ret && x->old_value && x->perms,
+                "agx_ppo_learn_graph: null pointer");
+    const int64_t P = x->P, S = x->S, epochs = x->epochs, batch = x->batch;
+    AGX_REQUIRE(P > 0 && P <= 65535 && S > 0 && S < (1ll << 31) && epochs > 0 && batch > 0 && epochs * P <= 65535,
+                "agx_ppo_learn_graph: bad sizes P=%lld S=%lld epochs=%lld batch=%lld", (long long)P, (long long)S,
+                (long long)epochs, (long long)batch);
+    GArgs a{};
+    const int rc = plan_graph(net, batch < S ? batch : S, a);
+    if (rc != AGX_OK) return rc;
+    const GraphWs w = graph_ws(a, P, S, epochs);
+    char *ws = static_cast<char *>(workspace);
+    hipStream_t s = as_stream(stream);
+    float *gobs = reinterpret_cast<float *>(ws + w.gobs);
+    int *gact = reinterpret_cast<int *>(ws + w.gact);
+    unsigned *gmask = x->action_masks ? reinterpret_cast<unsigned *>(ws + w.gmask) : nullptr;
+    float *grow = reinterpret_cast<float *>(ws + w.grow);
+    dim3 ggrid((unsigned)ceil_div(S, 256), (unsigned)(epochs * P));
+    ppo_gather_kernel<<<ggrid, 256, 0, s>>>(x->obs, reinterpret_cast<const long long *>(x->actions), x->old_logp,
+                                            x->adv, x->ret, x->old_value, x->adv_stats,
+                                            reinterpret_cast<const long long *>(x->perms), x->action_masks, a.A, S,
+                                            a.D, (int)P, gobs, gact, gmask, grow, nullptr, 0);
+    const int rc2 = check_launch("agx_ppo_learn_graph gather");
+    if (rc2) return rc2;
+    a.ws = reinterpret_cast<float *>(ws + w.agents);
+    a.params = x->params;
+    a.m = x->exp_avg;
+    a.v = x->exp_avg_sq;
+    a.lr = x->lr;
+    a.b1 = x->beta1;
+    a.b2 = x->beta2;
+    a.eps = x->eps;
+    a.step = reinterpret_cast<long long *>(x->adam_step);
+    a.gobs = gobs;
+    a.gact = gact;
+    a.gmask = gmask;
+    a.grow = grow;
+    a.S = S;
+    a.E = (int)epochs;
+    a.B = (int)(batch < S ? batch : S);
+    a.P = (int)P;
+    a.clip = x->clip_coef;
+    a.vf = x->vf_coef;
+    a.ent = x->ent_coef;
+    a.max_norm = x->max_grad_norm;
+    a.target_kl = x->target_kl;
+    a.batch_p = x->batch_per_agent;
+    a.epochs_p = x->epochs_per_agent;
+    a.ent_p = x->ent_coef_per_agent;
+    a.loss_out = x->loss_out;
+    a.kl_out = x->kl_out;
+    a.epochs_out = x->epochs_out;
+    a.skip = x->skip_if_set;
+    ppo_learn_graph_kernel<<<(unsigned)P, kGT, 0, s>>>(a);
+    return check_launch("agx_ppo_learn_graph");
+}

@@ -1,4 +1,7 @@
-"""Host side of the fused PPO learner (agx_ppo_learn in learner.hip)."""
+"""Host side of the fused PPO learners: agx_ppo_learn (learner.hip, the
+compiled network shapes) and agx_ppo_learn_graph (graph_learner.hip, any MLP
+actor-critic as a runtime layer list: the shapes architecture mutations
+produce)."""
 
 from __future__ import annotations
 
@@ -55,6 +58,61 @@ def net_descriptor(spec: ActorCriticSpec) -> AgxPPONet | None:
     return d
 
 
+class AgxPPOLayer(ctypes.Structure):
+    """Mirror of ``agx_ppo_layer`` (include/agx_graph.h)."""
+
+    _fields_ = [(n, _i32) for n in ("fin", "fout", "w", "b", "ln_w", "ln_b", "ln", "relu", "src")]
+
+
+GRAPH_MAX_LAYERS = 16
+
+
+class AgxPPOGraph(ctypes.Structure):
+    """Mirror of ``agx_ppo_graph`` (include/agx_graph.h)."""
+
+    _fields_ = [("obs_dim", _i32), ("n_actions", _i32), ("n_layers", _i32), ("actor_out", _i32),
+                ("critic_out", _i32), ("n_params", _i32), ("critic_start", _i32),
+                ("layers", AgxPPOLayer * GRAPH_MAX_LAYERS)]
+
+
+_LN_KIND = {None: 0, "plain": 1, "affine": 2}
+
+
+def graph_descriptor(spec) -> AgxPPOGraph | None:
+    """The runtime layer list of an MLP actor-critic (encoder chain -> latent;
+    actor head and critic head on the latent, or the critic on its own encoder
+    chain when share_encoders is off), or None when agx_ppo_learn_graph does
+    not cover it (more than 16 layers, a LayerNorm / ReLU layer wider than 512,
+    more than 32 actions): then the torch learner runs."""
+    if not isinstance(spec, ActorCriticSpec):
+        return None
+    layers: list[tuple] = []
+
+    def chain(lays, src):
+        for lay in lays:
+            layers.append((lay, src))
+            src = len(layers) - 1
+        return src
+
+    latent = chain(spec.encoder, -1)
+    actor_out = chain(spec.actor, latent)
+    critic_latent = chain(spec.critic_encoder, -1) if spec.critic_encoder else latent
+    critic_out = chain(spec.critic, critic_latent)
+    if len(layers) > GRAPH_MAX_LAYERS:
+        return None
+    d = AgxPPOGraph()
+    d.obs_dim, d.n_actions, d.n_layers = spec.obs_dim, spec.n_actions, len(layers)
+    d.actor_out, d.critic_out, d.n_params, d.critic_start = actor_out, critic_out, spec.n_params, spec.actor_end
+    for i, (lay, src) in enumerate(layers):
+        x = d.layers[i]
+        x.fin, x.fout, x.w, x.b = lay.fin, lay.fout, lay.w, lay.b
+        x.ln_w, x.ln_b, x.ln, x.relu, x.src = lay.g, lay.beta, _LN_KIND[lay.ln], int(lay.act), src
+    lib = _lib.load(require_gpu=False)  # pure host-side validation
+    if lib.agx_ppo_graph_check(ctypes.byref(d)) != 0:
+        return None
+    return d
+
+
 class AgxPPOLearnArgs(ctypes.Structure):
     """Mirror of ``agx_ppo_learn_args`` (include/agx.h)."""
 
@@ -77,6 +135,8 @@ class AgxPPOLearnArgs(ctypes.Structure):
 
 
 class FusedLearner:
+    batch_ws = None  # the graph learner's scratch is sized by the minibatch
+
     def __init__(self, pop):
         self.desc = net_descriptor(pop.spec)
         if self.desc is None:
@@ -86,13 +146,16 @@ class FusedLearner:
         self.ws = torch.empty(max(16, nbytes), dtype=torch.uint8, device=pop.device)
         _lib.check(lib.agx_ppo_learn_prepare(ctypes.byref(self.desc), self.ws.data_ptr(), _lib.stream()),
                    "agx_ppo_learn_prepare")
+        self._outputs(pop)
+        self.fn = lib.agx_ppo_learn
+
+    def _outputs(self, pop) -> None:
         self.epochs_ws = pop.update_epochs
         self.loss = torch.zeros(pop.P, dtype=torch.float32, device=pop.device)
         self.kl = torch.zeros(pop.P, dtype=torch.float32, device=pop.device)
         self.epochs_run = torch.zeros(pop.P, dtype=torch.int32, device=pop.device)
         self.args = AgxPPOLearnArgs()
         self.key = None
-        self.fn = lib.agx_ppo_learn
 
     def learn(self, pop, perms: torch.Tensor | None = None, skip_if_set: int | None = None) -> torch.Tensor:
         """All epochs x minibatches of every agent in two launches (gather +
@@ -144,9 +207,42 @@ class FusedLearner:
         return bool(int(word.item()) != 0)
 
 
+class GraphLearner(FusedLearner):
+    """agx_ppo_learn_graph: the same learn() over a runtime layer list (one
+    workgroup per agent, scratch sized by the largest minibatch)."""
+
+    def __init__(self, pop):
+        self.desc = graph_descriptor(pop.spec)
+        if self.desc is None:
+            raise _lib.AgxError("network outside the graph learner's coverage")
+        lib = _lib.load()
+        self.batch_ws = pop.split_batch
+        nbytes = lib.agx_ppo_learn_graph_workspace_bytes(ctypes.byref(self.desc), pop.P, pop.S, pop.update_epochs,
+                                                         self.batch_ws)
+        if nbytes == 0:
+            raise _lib.AgxError(f"agx_ppo_learn_graph_workspace_bytes: {lib.agx_last_error().decode()}")
+        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=pop.device)
+        self._outputs(pop)
+        self.fn = lib.agx_ppo_learn_graph
+
+    def timed_out(self, pop) -> bool:
+        return False  # one workgroup per agent: no partner hand-off to time out
+
+
+def make_learner(pop) -> FusedLearner:
+    return FusedLearner(pop) if pop.fused_descriptor() is not None else GraphLearner(pop)
+
+
+def learner_stale(pop) -> bool:
+    """True when pop has no learner yet or its workspace is too small."""
+    L = getattr(pop, "_fused", None)
+    return (L is None or L.epochs_ws < pop.update_epochs
+            or (L.batch_ws is not None and L.batch_ws < pop.split_batch))
+
+
 def fused_learn(pop, perms=None, skip_if_set: int | None = None) -> torch.Tensor:
-    if getattr(pop, "_fused", None) is None or pop._fused.epochs_ws < pop.update_epochs:
-        pop._fused = FusedLearner(pop)
+    if learner_stale(pop):
+        pop._fused = make_learner(pop)
     return pop._fused.learn(pop, perms, skip_if_set)
 
 

@@ -138,6 +138,7 @@ class PPOPopulation:
         self._shard_scratch: dict = {}
         self.act_counter = 0
         self._desc = None
+        self._gdesc = None
         self._alloc_rollout()
         self.env_base_d = torch.tensor([i * self.N for i in self.agent_ids], dtype=torch.int64, device=self.device)
         self.learn_steps = 0
@@ -211,6 +212,19 @@ class PPOPopulation:
             self._desc = net_descriptor(self.spec) or False
         return self._desc or None
 
+    def learn_descriptor(self):
+        """The network the fused learn() runs: agx_ppo_net for the compiled
+        shapes, else agx_ppo_graph (agx_ppo_learn_graph: any MLP actor-critic
+        an architecture mutation produces); None: the plain-PyTorch learner."""
+        desc = self.fused_descriptor()
+        if desc is not None or not self.fused or not isinstance(self.spec, ActorCriticSpec):
+            return desc
+        if self._gdesc is None:
+            from .learner import graph_descriptor
+
+            self._gdesc = graph_descriptor(self.spec) or False
+        return self._gdesc or None
+
     @torch.no_grad()
     def act_into(self, t: int, actions_flat: torch.Tensor | None = None) -> None:
         """Rollout policy step for slot t: reads obs[:, t], writes actions /
@@ -270,7 +284,7 @@ class PPOPopulation:
         learn's permutations right away (the pipelined runner passes False and
         prefetches after pacing the rollout instead)."""
         self.learn_steps += 1
-        if self.fused_descriptor() is not None:
+        if self.learn_descriptor() is not None:
             from .learner import fused_learn
 
             loss = fused_learn(self, skip_if_set=skip_if_set)
@@ -541,11 +555,11 @@ class PPOPopulation:
         host pacing it, the device is waiting for this thread, so nothing
         there may wait for the device — and a hipMalloc / hipHostMalloc, or an
         event sync, can."""
-        if self.fused_descriptor() is not None:
-            if getattr(self, "_fused", None) is None or self._fused.epochs_ws < self.update_epochs:
-                from .learner import FusedLearner
+        if self.learn_descriptor() is not None:
+            from .learner import learner_stale, make_learner
 
-                self._fused = FusedLearner(self)
+            if learner_stale(self):
+                self._fused = make_learner(self)
         if self.perm_source == "numpy":
             self._alloc_perm_host()
         if self.prefetch_perms:

@@ -1,0 +1,60 @@
+/* Runtime-shape PPO learner: any MLP actor-critic the reference's
+ * architecture mutations produce (agilerl/hpo/mutation.py:829-885 ->
+ * EvolvableMLP add/remove layer/node, EvolvableNetwork latent nodes).
+ *
+ * agx_ppo_learn (agx.h) runs a compile-time plan per network shape; after an
+ * architecture mutation an agent's shape is one of thousands, so this entry
+ * point takes the network as a runtime LAYER LIST instead and runs the same
+ * PPO.learn (agilerl/algorithms/ppo.py:836-920: every epoch x minibatch
+ * update, clipped loss, two-group gradient clip ppo.py:910-911, Adam
+ * optimizer_wrapper.py:444-452) in one launch, one workgroup per agent.
+ * Same argument block, same outputs and error behaviour as agx_ppo_learn.
+ *
+ * Replaces, for mutated architectures, the call PPO.learn makes
+ * (agilerl/algorithms/ppo.py:787-920); binding: INTEGRATION.md. */
+#ifndef AGX_GRAPH_H
+#define AGX_GRAPH_H
+
+#include "agx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AGX_PPO_GRAPH_MAX_LAYERS 16
+#define AGX_PPO_GRAPH_MAX_WIDTH 512   /* widest LayerNorm / ReLU layer */
+#define AGX_PPO_GRAPH_MAX_ACTIONS 32
+
+/* One Linear [-> LayerNorm] [-> ReLU] of the network, nn.Linear layout:
+ * weight [fout][fin] at flat offset w, bias [fout] at b; ln 0: none,
+ * 1: LayerNorm without affine, 2: LayerNorm with affine (weight at ln_w,
+ * bias at ln_b); src: -1 = the observation, else the index of the layer
+ * whose output this layer reads (layers are listed in topological order). */
+typedef struct agx_ppo_layer {
+    int32_t fin, fout, w, b, ln_w, ln_b, ln, relu, src;
+} agx_ppo_layer;
+
+/* The actor-critic: layers[actor_out] produces the n_actions logits,
+ * layers[critic_out] the value (both plain Linear); flat parameter rows of
+ * n_params floats; clip groups [0, critic_start) and [critic_start, n_params). */
+typedef struct agx_ppo_graph {
+    int32_t obs_dim, n_actions, n_layers, actor_out, critic_out, n_params, critic_start;
+    agx_ppo_layer layers[AGX_PPO_GRAPH_MAX_LAYERS];
+} agx_ppo_graph;
+
+/* AGX_OK when the graph is one agx_ppo_learn_graph runs (AGX_EINVAL with the
+ * reason in agx_last_error otherwise).  Host-side only. */
+int agx_ppo_graph_check(const agx_ppo_graph *net);
+/* Device workspace bytes of agx_ppo_learn_graph for P agents x S samples,
+ * `epochs` epochs and minibatches of at most `batch` rows (0: bad graph). */
+size_t agx_ppo_learn_graph_workspace_bytes(const agx_ppo_graph *net, int64_t P, int64_t S, int64_t epochs,
+                                           int64_t batch);
+/* agx_ppo_learn over a runtime layer list (args as for agx_ppo_learn;
+ * args->batch must not exceed the workspace's batch). */
+int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn_args *args, void *workspace, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,21 +1,26 @@
 """CPU-side checks of the C-ABI library: it loads, exports every entry point
-include/agx.h declares, and the Python binding covers exactly those."""
+include/*.h declares, and the Python binding covers exactly those."""
 
 import ctypes
+import glob
 import os
 import re
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "agx.h")
+HEADERS = sorted(glob.glob(os.path.join(ROOT, "include", "*.h")))
 
 
 INTEGRATION = os.path.join(ROOT, "INTEGRATION.md")
 
 
+def _header_text() -> str:
+    return "\n".join(open(h).read() for h in HEADERS)
+
+
 def header_functions():
-    text = open(HEADER).read()
+    text = _header_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(agx_[a-z0-9_]+)\s*\(", text)))
 
@@ -49,7 +54,7 @@ def _count_args(text: str) -> int:
 
 
 def header_arity() -> dict[str, int]:
-    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    text = re.sub(r"/\*.*?\*/", "", _header_text(), flags=re.S)
     return {m.group(1): _count_args(m.group(2))
             for m in re.finditer(r"\b(agx_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text, flags=re.S)}
 
@@ -109,7 +114,7 @@ def test_integration_doc_calls_match_header():
     seen = 0
     for m in re.finditer(r"\b(agx_[a-z0-9_]+)\(", doc):
         name = m.group(1)
-        assert name in arity, f"INTEGRATION.md calls {name}, which include/agx.h does not declare"
+        assert name in arity, f"INTEGRATION.md calls {name}, which include/*.h does not declare"
         _, args = _top_level_args(doc, m.end() - 1)
         if "..." in args:
             continue
