@@ -39,6 +39,9 @@ SIGNATURES = {
     "agx_ppo_graph_check": (_INT, [_P]),
     "agx_ppo_learn_graph_workspace_bytes": (_SZ, [_P, _I, _I, _I, _I]),
     "agx_ppo_learn_graph": (_INT, [_P, _P, _P, _P]),
+    "agx_ppo_act_graph_workspace_bytes": (_SZ, [_P, _I, _I]),
+    "agx_ppo_act_graph": (_INT, [_P, _I, _I, _P, _P, _I, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P,
+                                 _P, _I, _P, _P, _P, _P]),
     "agx_ppo_learn": (_INT, [_P, _P, _P, _P]),
     "agx_ppo_act": (_INT, [_P, _I, _I, _P, _P, _I, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P,
                            _I, _P, _P, _P]),

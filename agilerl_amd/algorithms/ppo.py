@@ -411,7 +411,19 @@ class PPO:
                    log_probs=torch.empty(n, device=self.device), values=torch.empty(n, device=self.device),
                    entropy=torch.empty(n, device=self.device))
         desc = pop.fused_descriptor()
-        if desc is None:
+        gdesc = pop.learn_descriptor() if desc is None else None
+        if gdesc is not None:  # a mutated MLP shape: agx_ppo_act_graph on this agent's row
+            self._counter += 1
+            ws = getattr(self, "_act_graph_ws", None)
+            if ws is None or ws[0] is not gdesc or ws[1] < n:
+                nbytes = _lib.load().agx_ppo_act_graph_workspace_bytes(ctypes.byref(gdesc), 1, n)
+                ws = self._act_graph_ws = (gdesc, n, torch.empty(nbytes, dtype=torch.uint8, device=self.device))
+            params = pop.params.data[self.row]
+            _lib.call("agx_ppo_act_graph", ctypes.byref(gdesc), 1, n, params.data_ptr(), o.data_ptr(), 0,
+                      _lib.ptr(mask), 0, 1, pop.act_seed + 7919 * pop.agent_ids[self.row], (1 << 40) + self._counter,
+                      out["actions"].data_ptr(), out["log_probs"].data_ptr(), out["values"].data_ptr(),
+                      out["entropy"].data_ptr(), 0, None, None, ws[2].data_ptr(), _lib.stream())
+        elif desc is None:
             logits, value = pop.spec.forward(pop.params.data[self.row:self.row + 1], o.unsqueeze(0))
             from ..population.nets import categorical
 

@@ -160,6 +160,64 @@ __device__ __forceinline__ void block_sum2(float &a, float &b, float *red) {
     b = tb;
 }
 
+// Forward of a minibatch (or a block of env rows) through the layer list:
+// GEMM + bias -> Ls[l].yr, then LayerNorm(+affine) / ReLU as a row pass
+// (16 lanes per row), keeping xhat / rstd / the feature-major copy where the
+// plan has room for them (the learner; the policy step keeps outputs only).
+// xobs: the observation rows (stride = the first layer's fin).
+__device__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bsz, float *base, const float *pr,
+                               int bp) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane & 15, rq = lane >> 4;
+    for (int l = 0; l < nl; ++l) {
+        const GLay &L = Ls[l];
+        const float *x = L.src < 0 ? xobs : base + Ls[L.src].yr;
+        float *yr = base + L.yr;
+        const int F = L.fout;
+        const float *bias = pr + L.b;
+        gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin,
+                [&](int m, int n, float c) { yr[(size_t)m * F + n] = c + bias[n]; });
+        __syncthreads();
+        if (L.ln == 0 && !L.relu && L.yc < 0) continue;
+        // LayerNorm(+affine) / ReLU, 16 lanes per row
+        const float invF = 1.f / (float)F;
+        for (int r0 = 0; r0 < bsz; r0 += 4 * kGW) {
+            const int row = r0 + 4 * wave + rq;
+            const bool live = row < bsz;
+            // three passes over the row's columns (re-reads hit L1): sum,
+            // centred sum of squares, then xhat / y out
+            float s = 0.f;
+            if (live)
+                for (int j = sub; j < F; j += 16) s += yr[(size_t)row * F + j];
+            float mean = 0.f, rstd = 1.f;
+            if (L.ln) {
+                mean = rsum16(s) * invF;
+                float vs = 0.f;
+                if (live)
+                    for (int j = sub; j < F; j += 16) {
+                        const float dz = yr[(size_t)row * F + j] - mean;
+                        vs += dz * dz;
+                    }
+                rstd = 1.f / sqrtf(rsum16(vs) / (float)F + 1e-5f);
+                if (live && sub == 0 && L.rs >= 0) base[L.rs + row] = rstd;
+            }
+            if (!live) continue;
+            for (int j = sub; j < F; j += 16) {
+                float y = yr[(size_t)row * F + j];
+                if (L.ln) {
+                    const float xh = (y - mean) * rstd;
+                    if (L.xh >= 0) base[L.xh + (size_t)row * F + j] = xh;
+                    y = L.ln == 2 ? xh * pr[L.g + j] + pr[L.be + j] : xh;
+                }
+                if (L.relu) y = relu(y);
+                yr[(size_t)row * F + j] = y;
+                if (L.yc >= 0) base[L.yc + (size_t)j * bp + row] = y;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
     __shared__ float red[2 * kGW];
     if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
@@ -217,53 +275,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
             }
 
             // ---- forward, layer by layer ------------------------------------
-            for (int l = 0; l < g.nl; ++l) {
-                const GLay &L = g.L[l];
-                const float *x = L.src < 0 ? xobs : base + g.L[L.src].yr;
-                float *yr = base + L.yr;
-                const int F = L.fout;
-                const float *bias = pr + L.b;
-                gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin,
-                        [&](int m, int n, float c) { yr[(size_t)m * F + n] = c + bias[n]; });
-                __syncthreads();
-                if (L.ln == 0 && !L.relu && L.yc < 0) continue;
-                // LayerNorm(+affine) / ReLU, 16 lanes per row
-                const float invF = 1.f / (float)F;
-                for (int r0 = 0; r0 < bsz; r0 += 4 * kGW) {
-                    const int row = r0 + 4 * wave + rq;
-                    const bool live = row < bsz;
-                    // three passes over the row's columns (re-reads hit L1): sum,
-                    // centred sum of squares, then xhat / y out
-                    float s = 0.f;
-                    if (live)
-                        for (int j = sub; j < F; j += 16) s += yr[(size_t)row * F + j];
-                    float mean = 0.f, rstd = 1.f;
-                    if (L.ln) {
-                        mean = rsum16(s) * invF;
-                        float vs = 0.f;
-                        if (live)
-                            for (int j = sub; j < F; j += 16) {
-                                const float dz = yr[(size_t)row * F + j] - mean;
-                                vs += dz * dz;
-                            }
-                        rstd = 1.f / sqrtf(rsum16(vs) / (float)F + 1e-5f);
-                        if (live && sub == 0) base[L.rs + row] = rstd;
-                    }
-                    if (!live) continue;
-                    for (int j = sub; j < F; j += 16) {
-                        float y = yr[(size_t)row * F + j];
-                        if (L.ln) {
-                            const float xh = (y - mean) * rstd;
-                            base[L.xh + (size_t)row * F + j] = xh;
-                            y = L.ln == 2 ? xh * pr[L.g + j] + pr[L.be + j] : xh;
-                        }
-                        if (L.relu) y = relu(y);
-                        yr[(size_t)row * F + j] = y;
-                        if (L.yc >= 0) base[L.yc + (size_t)j * bp + row] = y;
-                    }
-                }
-                __syncthreads();
-            }
+            forward_layers(g.L, g.nl, xobs, bsz, base, pr, bp);
 
             // ---- loss row pass: logits / value -> d(logits), d(value) (ppo.py:876-908)
             float lsum = 0.f, klsum = 0.f;
@@ -482,6 +494,110 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
     }
 }
 
+
+// Philox4x32-10 (Salmon et al., SC'11): the counter-based stream of
+// agx_ppo_act (learner.hip), so an agent's draws are keyed the same way
+// whichever kernel runs its network
+__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const unsigned long long p0 = (unsigned long long)0xD2511F53u * c.x;
+        const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c.z;
+        const unsigned h0 = (unsigned)(p0 >> 32), l0 = (unsigned)p0, h1 = (unsigned)(p1 >> 32), l1 = (unsigned)p1;
+        c = make_uint4(h1 ^ c.y ^ k.x, l1, h0 ^ c.w ^ k.y, l0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+
+struct GActArgs {
+    GLay L[kGL];
+    int nl, aout, cout, A, D, n, rows;
+    long long ws_block;  // scratch floats per (agent, row block)
+    float *ws;
+    const float *params;
+    const float *obs;  // agent p, env n at obs + p*obs_pstride + n*D
+    long long obs_pstride;
+    int N, P, sample;
+    unsigned long long seed, counter;
+    long long *act_out;
+    float *logp_out, *value_out, *ent_out;
+    long long out_pstride;
+    long long *act_flat;
+    const unsigned char *mask;
+    long long mask_pstride;
+    const long long *env_base;
+};
+
+// Rollout policy step (PPO.get_action, ppo.py:567-633) of workgroup (p, row
+// block): forward through the layer list, then the categorical over 16 lanes
+// per row (actions a and a + 16 per lane): masked logits (illegal -> -1e8,
+// distributions.py:16-28), Gumbel-max sample from the Philox stream of
+// agx_ppo_act, log-prob, entropy, value.
+__global__ __launch_bounds__(kGT) void ppo_act_graph_kernel(const GActArgs g) {
+    const int p = blockIdx.y, n0 = blockIdx.x * g.rows;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane & 15, rq = lane >> 4;
+    const int nrow = g.N - n0 < g.rows ? g.N - n0 : g.rows;
+    float *base = g.ws + ((size_t)p * gridDim.x + blockIdx.x) * g.ws_block;
+    const float *pr = g.params + (size_t)p * g.n;
+    forward_layers(g.L, g.nl, g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * g.D, nrow, base, pr, g.rows);
+    const float *lgp = base + g.L[g.aout].yr;
+    const float *vp = base + g.L[g.cout].yr;
+    const int A = g.A;
+    const int a0 = sub, a1 = sub + 16;
+    for (int r0 = 0; r0 < nrow; r0 += 4 * kGW) {
+        const int r = r0 + 4 * wave + rq;
+        const bool live = r < nrow;
+        const int rr = live ? r : 0;
+        float lg0 = a0 < A ? lgp[(size_t)rr * A + a0] : -3.0e38f;
+        float lg1 = a1 < A ? lgp[(size_t)rr * A + a1] : -3.0e38f;
+        if (g.mask && live) {
+            const unsigned char *mk = g.mask + (size_t)p * g.mask_pstride + (size_t)(n0 + r) * A;
+            if (a0 < A && !mk[a0]) lg0 = -1.0e8f;
+            if (a1 < A && !mk[a1]) lg1 = -1.0e8f;
+        }
+        const float mx = rmax16(fmaxf(lg0, lg1));
+        const float lse = mx + logf(rsum16((a0 < A ? expf(lg0 - mx) : 0.f) + (a1 < A ? expf(lg1 - mx) : 0.f)));
+        const float p0 = a0 < A ? expf(lg0 - lse) : 0.f, p1 = a1 < A ? expf(lg1 - lse) : 0.f;
+        const float H = -rsum16((a0 < A ? p0 * logf(p0 + 1e-8f) : 0.f) + (a1 < A ? p1 * logf(p1 + 1e-8f) : 0.f));
+        float sc0 = lg0, sc1 = lg1;
+        if (g.sample) {
+            const unsigned long long env =
+                (g.env_base ? (unsigned long long)g.env_base[p] : (unsigned long long)p * g.N) + n0 + rr;
+            auto gumbel = [&](int a, float lg) {
+                const uint4 rnd = philox(make_uint4((unsigned)env, (unsigned)(env >> 32), (unsigned)g.counter,
+                                                    (unsigned)(g.counter >> 32) ^ ((unsigned)(a >> 2) << 24)),
+                                         make_uint2((unsigned)g.seed, (unsigned)(g.seed >> 32)));
+                const unsigned w = (a & 3) == 0 ? rnd.x : (a & 3) == 1 ? rnd.y : (a & 3) == 2 ? rnd.z : rnd.w;
+                const float u = ((float)(w >> 8) + 0.5f) * (1.0f / 16777216.0f);
+                return a < A ? lg - logf(-logf(u)) : -3.0e38f;
+            };
+            sc0 = gumbel(a0, lg0);
+            sc1 = A > 16 ? gumbel(a1, lg1) : -3.0e38f;
+        }
+        // first maximum over the actions: lane-local (a0 < a1), then the lowest
+        // index among the lanes holding the row maximum
+        const float bl = fmaxf(sc0, sc1);
+        const int il = sc0 >= sc1 ? a0 : a1;
+        const float best = rmax16(bl);
+        const int choice = (int)(-rmax16(bl == best ? -(float)il : -1.0e9f));
+        const int srcl = (lane & ~15) + (choice & 15);
+        const float c0 = bperm(srcl, lg0), c1 = bperm(srcl, lg1);
+        if (live && sub == 0) {
+            const size_t o = (size_t)p * g.out_pstride + n0 + r;
+            if (g.act_out) g.act_out[o] = choice;
+            if (g.logp_out) g.logp_out[o] = (choice < 16 ? c0 : c1) - lse;
+            if (g.ent_out) g.ent_out[o] = H;
+            if (g.value_out) g.value_out[o] = vp[r];
+            if (g.act_flat)  // host staging: system-scope (write-through) store
+                __hip_atomic_store(g.act_flat + (size_t)p * g.N + n0 + r, (long long)choice, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -590,6 +706,30 @@ int plan_graph(const agx_ppo_graph *net, int64_t batch, GArgs &a) {
     return AGX_OK;
 }
 
+
+constexpr int kActRows = 4 * kGW;  // env rows per policy-step workgroup (one row pass)
+
+// the policy step keeps each layer's output only
+long long act_plan(const GArgs &full, GActArgs &a) {
+    long long off = 0;
+    for (int l = 0; l < full.nl; ++l) {
+        a.L[l] = full.L[l];
+        GLay &L = a.L[l];
+        L.yr = off;
+        off = r4(off + (long long)kActRows * L.fout);
+        L.yc = L.xh = L.rs = L.dy = L.wt = -1;
+    }
+    a.nl = full.nl;
+    a.aout = full.aout;
+    a.cout = full.cout;
+    a.A = full.A;
+    a.D = full.D;
+    a.n = full.n;
+    a.rows = kActRows;
+    a.ws_block = (off + 63) & ~63ll;
+    return a.ws_block;
+}
+
 struct GraphWs {
     size_t gobs, gact, gmask, grow, agents, total;
 };
@@ -682,4 +822,46 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
     a.skip = x->skip_if_set;
     ppo_learn_graph_kernel<<<(unsigned)P, kGT, 0, s>>>(a);
     return check_launch("agx_ppo_learn_graph");
+}
+
+extern "C" size_t agx_ppo_act_graph_workspace_bytes(const agx_ppo_graph *net, int64_t P, int64_t N) {
+    GArgs full{};
+    GActArgs a{};
+    if (P <= 0 || N <= 0 || plan_graph(net, 1, full) != AGX_OK) return 0;
+    return (size_t)P * ceil_div(N, kActRows) * act_plan(full, a) * sizeof(float);
+}
+
+extern "C" int agx_ppo_act_graph(const agx_ppo_graph *net, int64_t P, int64_t N, const float *params,
+                                 const float *obs, int64_t obs_agent_stride, const uint8_t *action_mask,
+                                 int64_t mask_agent_stride, int sample, uint64_t seed, uint64_t counter,
+                                 int64_t *actions, float *log_probs, float *values, float *entropy,
+                                 int64_t out_agent_stride, int64_t *actions_flat, const int64_t *agent_env_base,
+                                 void *workspace, void *stream) {
+    AGX_REQUIRE(net && params && obs && workspace && P > 0 && N > 0 && P <= 65535, "agx_ppo_act_graph: bad arguments");
+    GArgs full{};
+    const int rc = plan_graph(net, 1, full);
+    if (rc != AGX_OK) return rc;
+    GActArgs a{};
+    act_plan(full, a);
+    a.ws = static_cast<float *>(workspace);
+    a.params = params;
+    a.obs = obs;
+    a.obs_pstride = obs_agent_stride;
+    a.N = (int)N;
+    a.P = (int)P;
+    a.sample = sample;
+    a.seed = seed;
+    a.counter = counter;
+    a.act_out = reinterpret_cast<long long *>(actions);
+    a.logp_out = log_probs;
+    a.value_out = values;
+    a.ent_out = entropy;
+    a.out_pstride = out_agent_stride;
+    a.act_flat = reinterpret_cast<long long *>(actions_flat);
+    a.mask = action_mask;
+    a.mask_pstride = mask_agent_stride;
+    a.env_base = reinterpret_cast<const long long *>(agent_env_base);
+    dim3 grid((unsigned)ceil_div(N, kActRows), (unsigned)P);
+    ppo_act_graph_kernel<<<grid, kGT, 0, as_stream(stream)>>>(a);
+    return check_launch("agx_ppo_act_graph");
 }

@@ -254,3 +254,23 @@ def policy_step(pop, desc: AgxPPONet, obs: torch.Tensor, obs_agent_stride: int, 
               obs_agent_stride, _lib.ptr(action_mask), mask_agent_stride, 1 if sample else 0, pop.act_seed, counter,
               _lib.ptr(actions), _lib.ptr(log_probs), _lib.ptr(values), _lib.ptr(entropy), out_agent_stride,
               _lib.ptr(actions_flat), pop.env_base_d.data_ptr(), _lib.stream())
+
+
+def policy_step_graph(pop, desc: AgxPPOGraph, obs: torch.Tensor, obs_agent_stride: int, *, sample: bool,
+                      counter: int, actions=None, log_probs=None, values=None, entropy=None,
+                      out_agent_stride: int = 0, actions_flat=None, action_mask=None,
+                      mask_agent_stride: int = 0) -> None:
+    """agx_ppo_act_graph over all P agents x N envs: the policy step of
+    policy_step for a mutated (runtime-shape) network, same Philox stream."""
+    ws = getattr(pop, "_act_ws", None)
+    if ws is None or ws[0] is not desc:
+        lib = _lib.load()
+        nbytes = lib.agx_ppo_act_graph_workspace_bytes(ctypes.byref(desc), pop.P, pop.N)
+        if nbytes == 0:
+            raise _lib.AgxError(f"agx_ppo_act_graph_workspace_bytes: {lib.agx_last_error().decode()}")
+        ws = pop._act_ws = (desc, torch.empty(nbytes, dtype=torch.uint8, device=pop.device))
+    _lib.call("agx_ppo_act_graph", ctypes.byref(desc), pop.P, pop.N, pop.params.data.data_ptr(), obs.data_ptr(),
+              obs_agent_stride, _lib.ptr(action_mask), mask_agent_stride, 1 if sample else 0, pop.act_seed, counter,
+              _lib.ptr(actions), _lib.ptr(log_probs), _lib.ptr(values), _lib.ptr(entropy), out_agent_stride,
+              _lib.ptr(actions_flat), pop.env_base_d.data_ptr(), ws[1].data_ptr(), _lib.stream())
+

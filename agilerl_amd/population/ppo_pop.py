@@ -231,6 +231,15 @@ class PPOPopulation:
         log_probs / values[:, t] in place (and a contiguous [P*N] copy of the
         actions for the host env step)."""
         desc = self.fused_descriptor()
+        if desc is None and self.learn_descriptor() is not None:  # a mutated shape: the runtime-shape kernel
+            from .learner import policy_step_graph
+
+            self.act_counter += 1
+            TN = self.T * self.N
+            policy_step_graph(self, self.learn_descriptor(), self.obs[:, t], TN * self.spec.obs_dim, sample=True,
+                              counter=self.act_counter, actions=self.actions[:, t], log_probs=self.log_probs[:, t],
+                              values=self.values[:, t], out_agent_stride=TN, actions_flat=actions_flat)
+            return
         if desc is None:
             self.act_counter += 1
             action, logp, _ent, value = self.act(self.obs[:, t], counter=self.act_counter)

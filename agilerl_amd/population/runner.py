@@ -376,6 +376,7 @@ class PopulationRunner:
         pop, env = self.pop, self.env
         P, N, D = pop.P, pop.N, pop.spec.obs_dim
         desc = pop.fused_descriptor()
+        gdesc = pop.learn_descriptor() if desc is None else None
         act_d = torch.empty(P * N, dtype=torch.int64, device=pop.device)
         act_h = torch.empty(P * N, dtype=torch.int64, pin_memory=True)
         obs_h = torch.empty(P * N * D, dtype=pop.obs.dtype, pin_memory=True)
@@ -401,6 +402,11 @@ class PopulationRunner:
                     # its group take to finish their evaluation episodes
                     policy_step(pop, desc, obs_d, N * D, sample=True, counter=eval_base + (k << 20) + step,
                                 out_agent_stride=N, actions_flat=act_d)
+                elif gdesc is not None:  # a mutated shape: agx_ppo_act_graph, same counters
+                    from .learner import policy_step_graph
+
+                    policy_step_graph(pop, gdesc, obs_d, N * D, sample=True, counter=eval_base + (k << 20) + step,
+                                      out_agent_stride=N, actions_flat=act_d)
                 else:
                     act_d.copy_(pop.act(obs_d, counter=eval_base + (k << 20) + step)[0].view(-1))
                 act_h.copy_(act_d, non_blocking=True)

@@ -779,7 +779,7 @@ def cpu_offpolicy_leg(seconds):
 
 
 # --------------------------------------------------------------------------- #
-def config5_leg(iters: int = 5):
+def config5_leg(iters: int = 5, P: int = 4):
     """Config 5's per-GPU shard (Atari Breakout PPO, ppo_image.yaml network:
     conv 32/64/128 k8/4/3 s4/2/1 -> latent 256 -> heads [256]): 4 agents x 64
     envs of uint8 4x84x84 frames (32 agents / 2048 envs over 8 GPUs), learn_step
@@ -789,7 +789,7 @@ def config5_leg(iters: int = 5):
     from agilerl_amd.population.runner import PopulationRunner
     from agilerl_amd.utils import create_population
 
-    P, N = 4, 64
+    N = 64
     hp = {"BATCH_SIZE": 128, "LR": 1e-3, "LEARN_STEP": 256, "UPDATE_EPOCHS": 4}
     net = {"latent_dim": 256,
            "encoder_config": {"channel_size": [32, 64, 128], "kernel_size": [8, 4, 3], "stride_size": [4, 2, 1]},
@@ -807,8 +807,9 @@ def config5_leg(iters: int = 5):
         runner.iteration()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    out = {"workload": "config 5 shard: PPO pop=4 x 64 envs, uint8 4x84x84 frames, T=4, batch 128, 4 epochs, "
-                       "CNN 32/64/128 -> 256, heads [256]",
+    out = {"workload": f"config 5 {'shard' if P < 32 else 'whole population on one GPU'}: PPO pop={P} x 64 envs, "
+                       "uint8 4x84x84 frames, T=4, batch 128, 4 epochs, CNN 32/64/128 -> 256, heads [256]",
+           "rollout_bytes": int(pop.obs.numel() * pop.obs.element_size()),
            "iterations": iters, "ms_per_iteration": round(dt / iters * 1e3, 2),
            "env_steps_per_s": round(P * N * pop.T * iters / dt, 1),
            "learner_updates_per_s": round(pop.n_updates() * iters / dt, 1)}
@@ -1087,6 +1088,11 @@ def main():
         kern = kernels_leg(roof["peak_measured"])
     log("config-5 leg")
     c5 = config5_leg() if (world == 1 and not args.no_config5) else None
+    if c5 is not None:
+        log("config-5 whole-population leg")
+        # config 5's whole 32-agent population on one GPU (2048 envs, ~230 MB of
+        # uint8 rollout): what one MI355X holds that the 8-GPU shard does not need
+        c5["pop32_one_gpu"] = config5_leg(iters=2, P=32)
     log("config-3 leg")
     c3 = config3_leg() if (world == 1 and not args.no_config3) else None
     log("train_on_policy leg")

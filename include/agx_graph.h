@@ -53,6 +53,18 @@ size_t agx_ppo_learn_graph_workspace_bytes(const agx_ppo_graph *net, int64_t P, 
  * args->batch must not exceed the workspace's batch). */
 int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn_args *args, void *workspace, void *stream);
 
+/* The rollout policy step of agx_ppo_act (agx.h: same arguments, outputs,
+ * Philox stream and masks) over a runtime layer list, for n_actions <= 32;
+ * `workspace` holds agx_ppo_act_graph_workspace_bytes(net, P, N) bytes of
+ * activation scratch.  Replaces, for mutated architectures, PPO.get_action
+ * (agilerl/algorithms/ppo.py:567-633). */
+size_t agx_ppo_act_graph_workspace_bytes(const agx_ppo_graph *net, int64_t P, int64_t N);
+int agx_ppo_act_graph(const agx_ppo_graph *net, int64_t P, int64_t N, const float *params, const float *obs,
+                      int64_t obs_agent_stride, const uint8_t *action_mask, int64_t mask_agent_stride, int sample,
+                      uint64_t seed, uint64_t counter, int64_t *actions, float *log_probs, float *values,
+                      float *entropy, int64_t out_agent_stride, int64_t *actions_flat,
+                      const int64_t *agent_env_base, void *workspace, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,7 +74,17 @@ def test_ppo_yaml_mutation_params_train_on_policy():
         return out
 
     mut.mutation = record
-    with warnings.catch_warnings():
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+
+    def no_torch(*a, **k):
+        raise AssertionError("a mutated agent fell back to the PyTorch learner / policy step")
+
+    with warnings.catch_warnings(), pytest.MonkeyPatch.context() as mp:
+        # every agent, whatever its mutated shape, learns and acts on HIP kernels
+        # (agx_ppo_learn / agx_ppo_act for the compiled shapes, agx_ppo_learn_graph
+        # / agx_ppo_act_graph for the others)
+        mp.setattr(PPOPopulation, "_learn_torch", no_torch)
+        mp.setattr(PPOPopulation, "act", no_torch)
         warnings.simplefilter("ignore")
         pop, fits = train_on_policy(env, "LunarLanderSynthetic", "PPO", pop, INIT_HP=INIT_HP, max_steps=6 * 1024,
                                     evo_steps=1024, eval_steps=30, tournament=tour, mutation=mut, verbose=False)
@@ -83,6 +93,7 @@ def test_ppo_yaml_mutation_params_train_on_policy():
     assert len(shapes) > 1, "architecture mutations should change some agent's networks"
     assert all(len(f) == 4 and np.all(np.isfinite(f)) for f in fits)
     for a in pop:
+        assert a.population.learn_descriptor() is not None
         assert torch.isfinite(a.population.params.data[a.row]).all()
         assert a.population.spec.shape_key() == a.spec.shape_key()
         assert a.population.T == -(a.learn_step // -16)
@@ -122,7 +133,11 @@ def test_regroup_keeps_the_mutated_weights():
     assert arch.METHODS  # module imported
 
 
-def test_grouped_learner_single_update_on_mutated_shape():
+@pytest.mark.parametrize("learner", ["graph", "torch"])
+def test_grouped_learner_single_update_on_mutated_shape(learner):
+    """The runtime-shape HIP learner (agx_ppo_learn_graph, what learn() runs
+    on a mutated shape) and the autograd learner, each against the oracle."""
+    from agilerl_amd.population.learner import GraphLearner, fused_learn
     from agilerl_amd.population.nets import ActorCriticSpec
     from agilerl_amd.population.ppo_pop import PPOPopulation
     from oracle.ppo_learn import ActorCritic, reference_learn
@@ -150,7 +165,12 @@ def test_grouped_learner_single_update_on_mutated_shape():
     init, m0, v0 = (x.clone() for x in (pop.params.data, pop.opt.exp_avg, pop.opt.exp_avg_sq))
     raw_adv = pop.advantages.clone()
     perms = torch.arange(S, device=DEV).repeat(1, P, 1).contiguous()
-    pop._learn_torch(perms)
+    if learner == "graph":
+        assert pop.learn_descriptor() is not None
+        fused_learn(pop, perms)
+        assert isinstance(pop._fused, GraphLearner)
+    else:
+        pop._learn_torch(perms)
     torch.cuda.synchronize()
     keys = spec.state_dict_keys()
 

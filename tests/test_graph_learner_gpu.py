@@ -100,8 +100,12 @@ def test_graph_learner_single_update_tight(shape):
     _restore(pop, st)
     fused_learn(pop, perms)
     torch.cuda.synchronize()
-    np.testing.assert_allclose(pop.opt.exp_avg.cpu().numpy(), m_t.cpu().numpy(), rtol=1e-4, atol=1e-9)
-    np.testing.assert_allclose((pop.opt.exp_avg / 0.1).cpu().numpy(), g_t.cpu().numpy(), rtol=1e-3, atol=1e-8)
+    # entries that are sums with cancellation get an absolute floor of 1e-6 of
+    # the largest gradient
+    m, mt = pop.opt.exp_avg.cpu().numpy(), m_t.cpu().numpy()
+    np.testing.assert_allclose(m, mt, rtol=1e-4, atol=1e-6 * np.abs(mt).max())
+    gt = g_t.cpu().numpy()
+    np.testing.assert_allclose(m / 0.1, gt, rtol=1e-3, atol=1e-6 * np.abs(gt).max())
 
 
 @pytest.mark.parametrize("shape,N,learn_step,batch,epochs", [
@@ -158,3 +162,49 @@ def test_graph_learner_target_kl_stops_like_torch():
     pop = _pop("latent_56", N=16, learn_step=128, batch=32, epochs=4, target_kl=1e-4)
     _compare(pop, pop.permutations())
     assert int(pop._fused.epochs_run.min()) < 4
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+def test_graph_policy_step_matches_torch_forward(shape):
+    """agx_ppo_act_graph (greedy) against the plain-PyTorch forward: actions,
+    log-probs, entropy, values; 40 envs = two row blocks."""
+    from agilerl_amd.population.learner import policy_step_graph
+
+    P, N = 3, 40
+    pop = _pop(shape, P=P, N=N)
+    obs = torch.randn(P, N, 8, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+    act = torch.empty(P, N, dtype=torch.int64, device=DEV)
+    lp, v, ent = (torch.empty(P, N, device=DEV) for _ in range(3))
+    policy_step_graph(pop, pop.learn_descriptor(), obs, N * 8, sample=False, counter=0, actions=act, log_probs=lp,
+                      values=v, entropy=ent, out_agent_stride=N)
+    logits, value = pop.spec.forward(pop.params.data, obs)
+    logp_all = torch.log_softmax(logits, -1)
+    assert torch.equal(act, logits.argmax(-1))
+    torch.testing.assert_close(lp, logp_all.gather(-1, act.unsqueeze(-1)).squeeze(-1), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(v, value.view(P, N), rtol=1e-4, atol=1e-5)
+    pa = logp_all.exp()
+    torch.testing.assert_close(ent, -(pa * torch.log(pa + 1e-8)).sum(-1), rtol=1e-4, atol=1e-5)
+
+
+def test_graph_policy_step_samples_the_fused_stream():
+    """On a compiled shape both policy steps draw from the same Philox stream:
+    the sampled actions agree (up to logits within rounding of a tie)."""
+    from agilerl_amd.population.learner import graph_descriptor, policy_step, policy_step_graph
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+
+    P, N = 4, 64
+    spec = ActorCriticSpec(obs_dim=8, n_actions=4)
+    pop = PPOPopulation(spec, P, N, learn_step=N, batch_size=N, device=DEV, fused=True, seeds=list(range(P)))
+    assert pop.fused_descriptor() is not None
+    obs = torch.randn(P, N, 8, device=DEV, generator=torch.Generator(device=DEV).manual_seed(2))
+    a_f, a_g = (torch.empty(P, N, dtype=torch.int64, device=DEV) for _ in range(2))
+    agree = []
+    for counter in range(1, 6):
+        policy_step(pop, pop.fused_descriptor(), obs, N * 8, sample=True, counter=counter, actions=a_f,
+                    out_agent_stride=N)
+        policy_step_graph(pop, graph_descriptor(spec), obs, N * 8, sample=True, counter=counter, actions=a_g,
+                          out_agent_stride=N)
+        agree.append((a_f == a_g).float().mean().item())
+    assert min(agree) >= 0.99, agree
+    assert len({tuple(a_g.view(-1).tolist())}) == 1

@@ -222,3 +222,35 @@ def test_config5_breakout_ppo_train_on_policy(tmp_path):
     assert torch.isfinite(population.params.data).all()
     a, lp, ent, v = pop[0].get_action(np.random.randint(0, 256, (3, 4, 84, 84), dtype=np.uint8))
     assert a.shape == (3,) and np.all((a >= 0) & (a < 4)) and np.all(np.isfinite(v))
+
+
+def test_config5_whole_population_on_one_gpu():
+    """Config 5's WHOLE population — 32 agents x 64 envs (2048 envs, ~230 MB
+    of uint8 rollout) — on one MI355X: one iteration (4-step rollout, GAE,
+    4 epochs x 2 minibatches) with property checks: the rollout holds every
+    agent's frames, every agent's loss is finite and every agent's parameters
+    moved (and stayed finite)."""
+    from agilerl_amd.envs import StackedVecEnv, SyntheticAtariVecEnv
+    from agilerl_amd.population.runner import PopulationRunner
+    from agilerl_amd.utils import create_population
+
+    P, N = 32, 64
+    hp = {"BATCH_SIZE": 128, "LR": 1e-3, "LEARN_STEP": 256, "UPDATE_EPOCHS": 4}
+    net = {"latent_dim": 256,
+           "encoder_config": {"channel_size": [32, 64, 128], "kernel_size": [8, 4, 3], "stride_size": [4, 2, 1]},
+           "head_config": {"hidden_size": [256], "layer_norm": False}}
+    env = SyntheticAtariVecEnv(N, n_actions=4, seed=1)
+    agents = create_population("PPO", net, hp, env.single_observation_space, env.single_action_space,
+                               population_size=P, num_envs=N)
+    pop = agents[0].population
+    assert pop.P == P and pop.obs.dtype == torch.uint8
+    assert pop.obs.numel() * pop.obs.element_size() == P * 4 * N * 4 * 84 * 84  # ~231 MB
+    runner = PopulationRunner(pop, StackedVecEnv.from_shared(env, P))
+    before = pop.params.data.clone()
+    loss = runner.iteration()
+    torch.cuda.synchronize()
+    assert loss.shape == (P,) and torch.isfinite(loss).all()
+    assert torch.isfinite(pop.params.data).all()
+    assert bool(((pop.params.data - before).abs().amax(1) > 0).all())
+    assert bool((pop.obs.view(P, -1)[:, ::97].float().std(1) > 0).all())
+    assert int(pop.opt.steps.min()) == int(pop.opt.steps.max()) == 4 * 2
