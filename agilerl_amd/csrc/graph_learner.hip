@@ -105,37 +105,59 @@ __device__ __forceinline__ float bperm(int lane, float v) {
 }
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
-// C[M x N] = A[M x K] . B[N x K]^T, both operands contiguous along k; one
-// 16x16 tile per wave at a time, 64 k per round trip (32 loads in flight per
-// lane).  MFMA j of a 16-k block takes k = 4q + (j & 3) from lane group q, so
-// each lane's four k of a block are adjacent words.  epi(m, n, c) per element.
+// C[M x N] = A[M x K] . B[N x K]^T, both operands contiguous along k.  Each
+// wave works on TWO 16x16 tiles at a time (tiles t and t + kGW), 64 k per
+// round trip: 64 loads in flight per lane before the MFMAs (the operands are
+// L2 hits; the chain is latency, not bandwidth).  MFMA j of a 16-k block takes
+// k = 4q + (j & 3) from lane group q, so each lane's four k of a block are
+// adjacent words.  epi(m, n, c) per element.
 template <class FE>
 __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B, int ldb, int M, int N, int K,
                                         FE epi) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 15, q = lane >> 4;
-    const int mt = (M + 15) >> 4, nt = (N + 15) >> 4;
-    for (int t = wave; t < mt * nt; t += kGW) {
-        const int m0 = (t % mt) << 4, n0 = (t / mt) << 4;
-        const bool aok = m0 + r < M, bok = n0 + r < N;
-        const float *ap = A + (size_t)(aok ? m0 + r : 0) * lda;
-        const float *bp = B + (size_t)(bok ? n0 + r : 0) * ldb;
-        f4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int mt = (M + 15) >> 4, nt = (N + 15) >> 4, T = mt * nt;
+    for (int t0 = wave; t0 < T; t0 += 2 * kGW) {
+        const bool two = t0 + kGW < T;  // wave-uniform
+        int m0[2], n0[2];
+        bool aok[2], bok[2];
+        const float *ap[2], *bp[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int t = u ? (two ? t0 + kGW : t0) : t0;
+            m0[u] = (t % mt) << 4;
+            n0[u] = (t / mt) << 4;
+            aok[u] = m0[u] + r < M;
+            bok[u] = n0[u] + r < N;
+            ap[u] = A + (size_t)(aok[u] ? m0[u] + r : 0) * lda;
+            bp[u] = B + (size_t)(bok[u] ? n0[u] + r : 0) * ldb;
+        }
+        f4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
         for (int k0 = 0; k0 < K; k0 += 64) {
-            float a[16], b[16];
+            float a[2][16], b[2][16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int k = k0 + 16 * (j >> 2) + 4 * q + (j & 3);
-                a[j] = (aok && k < K) ? ap[k] : 0.f;
-                b[j] = (bok && k < K) ? bp[k] : 0.f;
-            }
+            for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+                for (int j = 0; j < 16; ++j) {
+                    const int k = k0 + 16 * (j >> 2) + 4 * q + (j & 3);
+                    const bool on = (u == 0 || two) && k < K;
+                    a[u][j] = (on && aok[u]) ? ap[u][k] : 0.f;
+                    b[u][j] = (on && bok[u]) ? bp[u][k] : 0.f;
+                }
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][j], b[u][j], acc[u], 0, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int m = m0 + 4 * q + i, n = n0 + r;
-            if (m < M && n < N) epi(m, n, acc[i]);
+        for (int u = 0; u < 2; ++u) {
+            if (u == 1 && !two) break;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = m0[u] + 4 * q + i, n = n0[u] + r;
+                if (m < M && n < N) epi(m, n, acc[u][i]);
+            }
         }
     }
 }
