@@ -7,7 +7,7 @@
 // thousands of shapes — any depth of encoder / head, any width, a latent of
 // any size — so this kernel interprets a runtime LAYER LIST instead:
 //
-//   * one 512-thread workgroup per agent runs every epoch x minibatch update
+//   * one 256-thread workgroup per agent runs every epoch x minibatch update
 //     of PPO.learn (ppo.py:836-920) in one launch, like agx_ppo_learn;
 //   * a minibatch is processed layer by layer over all its rows: every Linear
 //     (forward, dW, dX) is ONE operand form, C = A . B^T with both operands
@@ -43,7 +43,7 @@ __global__ void ppo_gather_kernel(const float *__restrict__ obs, const long long
 
 namespace {
 
-constexpr int kGT = 512;
+constexpr int kGT = 256;  // 4 waves, one per SIMD: the whole 512-VGPR file per wave
 constexpr int kGW = kGT / kWave;
 constexpr int kGL = AGX_PPO_GRAPH_MAX_LAYERS;
 
@@ -79,6 +79,7 @@ struct GArgs {
     float *loss_out, *kl_out;
     int *epochs_out;
     const unsigned *skip;
+    int dbg;  // diagnostic phase skips (AGX_GRAPH_DEBUG; timing attribution only, results wrong)
 };
 
 template <int C>
@@ -105,61 +106,102 @@ __device__ __forceinline__ float bperm(int lane, float v) {
 }
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
-// C[M x N] = A[M x K] . B[N x K]^T, both operands contiguous along k.  Each
-// wave works on TWO 16x16 tiles at a time (tiles t and t + kGW), 64 k per
-// round trip: 64 loads in flight per lane before the MFMAs (the operands are
-// L2 hits; the chain is latency, not bandwidth).  MFMA j of a 16-k block takes
-// k = 4q + (j & 3) from lane group q, so each lane's four k of a block are
-// adjacent words.  epi(m, n, c) per element.
+// C[M x N] = A[M x K] . B[N x K]^T, both operands contiguous along k (the
+// only operand form the learner needs, see the layouts above), in blocks of
+// up to 128 x 128.  The block's A and B panels go through LDS 32 k at a time,
+// double-buffered: every global load is a dword load of 64 consecutive lanes
+// over 2 rows x 32 contiguous k (two full 128-byte lines), and the next
+// chunk's loads fly under the current chunk's MFMAs.  Each wave owns up to 8
+// of the block's 16x16 f32 MFMA tiles; MFMA kk takes k = 4kk + q from lane
+// group q (LDS rows padded to 36 floats: the 64 lanes' reads hit 64 banks).
+// lds: kGemmLds floats.  epi(m, n, c) per element.
+constexpr int kBM = 128, kBN = 64, kKC = 32, kLdS = kKC + 4;
+constexpr int kRS = kGT / kKC;                           // staging row stride
+constexpr int kTPW = (kBM / 16) * (kBN / 16) / kGW;      // tiles per wave
+constexpr int kPanel = (kBM + kBN) * kLdS;  // A rows then B rows
+constexpr int kGemmLds = 2 * kPanel;        // double-buffered
+
 template <class FE>
 __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B, int ldb, int M, int N, int K,
-                                        FE epi) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                                        float *lds, FE epi) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, q = lane >> 4;
-    const int mt = (M + 15) >> 4, nt = (N + 15) >> 4, T = mt * nt;
-    for (int t0 = wave; t0 < T; t0 += 2 * kGW) {
-        const bool two = t0 + kGW < T;  // wave-uniform
-        int m0[2], n0[2];
-        bool aok[2], bok[2];
-        const float *ap[2], *bp[2];
+    const int lr = tid / kKC, lk = tid % kKC;  // staging: rows lr + kRS i, column lk
+    for (int mb = 0; mb < M; mb += kBM)
+        for (int nb = 0; nb < N; nb += kBN) {
+            const int BM = M - mb < kBM ? M - mb : kBM, BN = N - nb < kBN ? N - nb : kBN;
+            const int mtn = (BM + 15) >> 4, T = mtn * ((BN + 15) >> 4);
+            const float *Ab = A + (size_t)mb * lda, *Bb = B + (size_t)nb * ldb;
+            float ra[kBM / kRS], rb[kBN / kRS];
+            auto fetch = [&](int kc) {
+                const int k = kc + lk;
+                const bool kin = k < K;
+                const int kk = kin ? k : 0;
+                // unconditional loads from clamped (valid) addresses, then the predicate
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int t = u ? (two ? t0 + kGW : t0) : t0;
-            m0[u] = (t % mt) << 4;
-            n0[u] = (t / mt) << 4;
-            aok[u] = m0[u] + r < M;
-            bok[u] = n0[u] + r < N;
-            ap[u] = A + (size_t)(aok[u] ? m0[u] + r : 0) * lda;
-            bp[u] = B + (size_t)(bok[u] ? n0[u] + r : 0) * ldb;
-        }
-        f4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-        for (int k0 = 0; k0 < K; k0 += 64) {
-            float a[2][16], b[2][16];
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int k = k0 + 16 * (j >> 2) + 4 * q + (j & 3);
-                    const bool on = (u == 0 || two) && k < K;
-                    a[u][j] = (on && aok[u]) ? ap[u][k] : 0.f;
-                    b[u][j] = (on && bok[u]) ? bp[u][k] : 0.f;
+                for (int i = 0; i < kBM / kRS; ++i) {
+                    const int row = lr + kRS * i;
+                    const float va = Ab[(size_t)(row < BM ? row : 0) * lda + kk];
+                    ra[i] = (row < BM && kin) ? va : 0.f;
                 }
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
+                for (int i = 0; i < kBN / kRS; ++i) {
+                    const int row = lr + kRS * i;
+                    const float vb = Bb[(size_t)(row < BN ? row : 0) * ldb + kk];
+                    rb[i] = (row < BN && kin) ? vb : 0.f;
+                }
+            };
+            auto commit = [&](int buf) {
+                float *As = lds + buf * kPanel, *Bs = As + kBM * kLdS;
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
-                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][j], b[u][j], acc[u], 0, 0, 0);
-        }
+                for (int i = 0; i < kBM / kRS; ++i) As[(lr + kRS * i) * kLdS + lk] = ra[i];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (u == 1 && !two) break;
+                for (int i = 0; i < kBN / kRS; ++i) Bs[(lr + kRS * i) * kLdS + lk] = rb[i];
+            };
+            f4 acc[kTPW];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int m = m0[u] + 4 * q + i, n = n0[u] + r;
-                if (m < M && n < N) epi(m, n, acc[u][i]);
+            for (int j = 0; j < kTPW; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+            fetch(0);
+            commit(0);
+            __syncthreads();
+            int buf = 0;
+            for (int kc = 0; kc < K; kc += kKC) {
+                const bool more = kc + kKC < K;
+                if (more) fetch(kc + kKC);
+                const float *As = lds + buf * kPanel, *Bs = As + kBM * kLdS;
+#pragma unroll
+                for (int j = 0; j < kTPW; ++j) {
+                    const int t = wave + kGW * j;
+                    if (t < T) {  // wave-uniform
+                        const int m0 = (t % mtn) << 4, n0 = (t / mtn) << 4;
+                        float av[8], bv[8];
+#pragma unroll
+                        for (int kk = 0; kk < 8; ++kk) {
+                            av[kk] = As[(m0 + r) * kLdS + 4 * kk + q];
+                            bv[kk] = Bs[(n0 + r) * kLdS + 4 * kk + q];
+                        }
+#pragma unroll
+                        for (int kk = 0; kk < 8; ++kk)
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc[j], 0, 0, 0);
+                    }
+                }
+                if (more) commit(buf ^ 1);
+                __syncthreads();
+                buf ^= 1;
+            }
+#pragma unroll
+            for (int j = 0; j < kTPW; ++j) {
+                const int t = wave + kGW * j;
+                if (t < T) {
+                    const int m0 = (t % mtn) << 4, n0 = (t / mtn) << 4;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int m = m0 + 4 * q + i, n = n0 + r;
+                        if (m < BM && n < BN) epi(mb + m, nb + n, acc[j][i]);
+                    }
+                }
             }
         }
-    }
 }
 
 // fixed-order workgroup sum of two per-thread values
@@ -182,32 +224,74 @@ __device__ __forceinline__ void block_sum2(float &a, float &b, float *red) {
     b = tb;
 }
 
-// Forward of a minibatch (or a block of env rows) through the layer list:
-// GEMM + bias -> Ls[l].yr, then LayerNorm(+affine) / ReLU as a row pass
-// (16 lanes per row), keeping xhat / rstd / the feature-major copy where the
-// plan has room for them (the learner; the policy step keeps outputs only).
-// xobs: the observation rows (stride = the first layer's fin).
-__device__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bsz, float *base, const float *pr,
-                               int bp) {
+// LayerNorm(+affine) / ReLU forward of one layer's rows, 16 lanes per row;
+// rows r, r + 32, r + 64, r + 96 of a 128-row block are processed together
+// with C columns per lane cached in registers (F <= 16 C): all loads of the
+// block are issued before the first reduction (one round trip, not three per
+// row).  C = 0: any width, three passes over the row per 32 rows.
+template <int C>
+__device__ __forceinline__ void fwd_rows(const GLay &L, float *base, const float *pr, int bsz, int bp) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane & 15, rq = lane >> 4;
-    for (int l = 0; l < nl; ++l) {
-        const GLay &L = Ls[l];
-        const float *x = L.src < 0 ? xobs : base + Ls[L.src].yr;
-        float *yr = base + L.yr;
-        const int F = L.fout;
-        const float *bias = pr + L.b;
-        gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin,
-                [&](int m, int n, float c) { yr[(size_t)m * F + n] = c + bias[n]; });
-        __syncthreads();
-        if (L.ln == 0 && !L.relu && L.yc < 0) continue;
-        // LayerNorm(+affine) / ReLU, 16 lanes per row
-        const float invF = 1.f / (float)F;
+    float *yr = base + L.yr;
+    const int F = L.fout;
+    const float invF = 1.f / (float)F;
+    auto out = [&](int row, int j, float y, float mean, float rstd) {
+        if (L.ln) {
+            const float xh = (y - mean) * rstd;
+            if (L.xh >= 0) base[L.xh + (size_t)row * F + j] = xh;
+            y = L.ln == 2 ? xh * pr[L.g + j] + pr[L.be + j] : xh;
+        }
+        if (L.relu) y = relu(y);
+        yr[(size_t)row * F + j] = y;
+        if (L.yc >= 0) base[L.yc + (size_t)j * bp + row] = y;
+    };
+    if constexpr (C > 0) {
+        constexpr int R = 4;
+        for (int r0 = 0; r0 < bsz; r0 += R * 4 * kGW) {
+            float z[R][C];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int row = r0 + 4 * wave + rq + 4 * kGW * u;
+#pragma unroll
+                for (int i = 0; i < C; ++i) {
+                    const int j = sub + 16 * i;
+                    const bool on = row < bsz && j < F;
+                    const float v = yr[on ? (size_t)row * F + j : 0];
+                    z[u][i] = on ? v : 0.f;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int row = r0 + 4 * wave + rq + 4 * kGW * u;
+                float mean = 0.f, rstd = 1.f;
+                if (L.ln) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int i = 0; i < C; ++i) s += z[u][i];
+                    mean = rsum16(s) * invF;
+                    float vs = 0.f;
+#pragma unroll
+                    for (int i = 0; i < C; ++i) {
+                        const float d = z[u][i] - mean;
+                        vs += (sub + 16 * i < F) ? d * d : 0.f;
+                    }
+                    rstd = 1.f / sqrtf(rsum16(vs) / (float)F + 1e-5f);
+                    if (row < bsz && sub == 0 && L.rs >= 0) base[L.rs + row] = rstd;
+                }
+                if (row < bsz) {
+#pragma unroll
+                    for (int i = 0; i < C; ++i) {
+                        const int j = sub + 16 * i;
+                        if (j < F) out(row, j, z[u][i], mean, rstd);
+                    }
+                }
+            }
+        }
+    } else {
         for (int r0 = 0; r0 < bsz; r0 += 4 * kGW) {
             const int row = r0 + 4 * wave + rq;
             const bool live = row < bsz;
-            // three passes over the row's columns (re-reads hit L1): sum,
-            // centred sum of squares, then xhat / y out
             float s = 0.f;
             if (live)
                 for (int j = sub; j < F; j += 16) s += yr[(size_t)row * F + j];
@@ -224,24 +308,152 @@ __device__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bs
                 if (live && sub == 0 && L.rs >= 0) base[L.rs + row] = rstd;
             }
             if (!live) continue;
-            for (int j = sub; j < F; j += 16) {
-                float y = yr[(size_t)row * F + j];
-                if (L.ln) {
-                    const float xh = (y - mean) * rstd;
-                    if (L.xh >= 0) base[L.xh + (size_t)row * F + j] = xh;
-                    y = L.ln == 2 ? xh * pr[L.g + j] + pr[L.be + j] : xh;
+            for (int j = sub; j < F; j += 16) out(row, j, yr[(size_t)row * F + j], mean, rstd);
+        }
+    }
+}
+
+// LayerNorm(+affine) / ReLU backward of one layer's rows: dY -> dZ (row-major
+// dzr and feature-major dzc), plus dY' xhat and dY' feature-major (t1c, t2c)
+// for the LN-affine gradients.  As fwd_rows: C columns per lane cached for
+// 16 / C rows at once (F <= 16 C); C = 0: any width, re-reading the row.
+template <int C>
+__device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float *pr, int bsz, int bp, float *dzr,
+                                         float *dzc, float *t1c, float *t2c) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane & 15, rq = lane >> 4;
+    const int F = L.fout;
+    const float invF = 1.f / (float)F;
+    const float *dy = base + L.dy;
+    auto put = [&](int row, int j, float d, float xh, float dz) {
+        if (L.ln == 2) {
+            t1c[(size_t)j * bp + row] = d * xh;
+            t2c[(size_t)j * bp + row] = d;
+        }
+        dzr[(size_t)row * F + j] = dz;
+        dzc[(size_t)j * bp + row] = dz;
+    };
+    if constexpr (C > 0) {
+        constexpr int R = 8 / C;  // 8 cached columns per lane: three loads each in flight
+        float gam[C];
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+            const int j = sub + 16 * i;
+            const float v = pr[L.ln == 2 ? L.g + (j < F ? j : 0) : 0];
+            gam[i] = L.ln == 2 ? v : 1.f;
+        }
+        for (int r0 = 0; r0 < bsz; r0 += R * 4 * kGW) {
+            float dp[R][C], xh[R][C], rs[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int row = r0 + 4 * wave + rq + 4 * kGW * u;
+                const int rr = row < bsz ? row : 0;
+                const float rv = base[L.ln ? L.rs + rr : 0];
+                rs[u] = L.ln ? rv : 1.f;
+#pragma unroll
+                for (int i = 0; i < C; ++i) {
+                    const int j = sub + 16 * i;
+                    const bool on = row < bsz && j < F;
+                    const size_t o = on ? (size_t)row * F + j : 0;
+                    const float d = dy[o];
+                    const float y = base[L.relu ? L.yr + o : 0];
+                    const float x = base[L.ln ? L.xh + o : 0];
+                    dp[u][i] = (on && (!L.relu || y > 0.f)) ? d : 0.f;
+                    xh[u][i] = (on && L.ln) ? x : 0.f;
                 }
-                if (L.relu) y = relu(y);
-                yr[(size_t)row * F + j] = y;
-                if (L.yc >= 0) base[L.yc + (size_t)j * bp + row] = y;
+            }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int row = r0 + 4 * wave + rq + 4 * kGW * u;
+                float m1 = 0.f, m2 = 0.f;
+                if (L.ln) {
+                    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                    for (int i = 0; i < C; ++i) {
+                        const float dx = dp[u][i] * gam[i];
+                        s1 += dx;
+                        s2 += dx * xh[u][i];
+                    }
+                    m1 = rsum16(s1) * invF;
+                    m2 = rsum16(s2) * invF;
+                }
+                if (row < bsz) {
+#pragma unroll
+                    for (int i = 0; i < C; ++i) {
+                        const int j = sub + 16 * i;
+                        if (j < F) {
+                            const float dz = L.ln ? rs[u] * (dp[u][i] * gam[i] - m1 - xh[u][i] * m2) : dp[u][i];
+                            put(row, j, dp[u][i], xh[u][i], dz);
+                        }
+                    }
+                }
             }
         }
+    } else {
+        for (int r0 = 0; r0 < bsz; r0 += 4 * kGW) {
+            const int row = r0 + 4 * wave + rq;
+            const bool live = row < bsz;
+            // d(pre-activation) of column j: dY masked by the ReLU
+            auto dpre = [&](int j) {
+                const float d = dy[(size_t)row * F + j];
+                return (!L.relu || base[L.yr + (size_t)row * F + j] > 0.f) ? d : 0.f;
+            };
+            float m1 = 0.f, m2 = 0.f, rstd = 1.f;
+            if (L.ln) {
+                float s1 = 0.f, s2 = 0.f;
+                if (live)
+                    for (int j = sub; j < F; j += 16) {
+                        const float dx = L.ln == 2 ? dpre(j) * pr[L.g + j] : dpre(j);
+                        s1 += dx;
+                        s2 += dx * base[L.xh + (size_t)row * F + j];
+                    }
+                m1 = rsum16(s1) * invF;
+                m2 = rsum16(s2) * invF;
+                rstd = live ? base[L.rs + row] : 0.f;
+            }
+            if (!live) continue;
+            for (int j = sub; j < F; j += 16) {
+                const float d = dpre(j);
+                float dz = d, xh = 0.f;
+                if (L.ln) {
+                    xh = base[L.xh + (size_t)row * F + j];
+                    const float dx = L.ln == 2 ? d * pr[L.g + j] : d;
+                    dz = rstd * (dx - m1 - xh * m2);
+                }
+                put(row, j, d, xh, dz);
+            }
+        }
+    }
+}
+
+// Forward of a minibatch (or a block of env rows) through the layer list:
+// GEMM + bias -> Ls[l].yr, then LayerNorm(+affine) / ReLU as a row pass,
+// keeping xhat / rstd / the feature-major copy where the plan has room for
+// them (the learner; the policy step keeps outputs only).  xobs: the
+// observation rows (stride = the first layer's fin).
+__device__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bsz, float *base, const float *pr,
+                               int bp, float *lds, int dbg = 0) {
+    for (int l = 0; l < nl; ++l) {
+        const GLay &L = Ls[l];
+        const float *x = L.src < 0 ? xobs : base + Ls[L.src].yr;
+        float *yr = base + L.yr;
+        const int F = L.fout;
+        const float *bias = pr + L.b;
+        if (!(dbg & 1))
+            gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds,
+                    [&](int m, int n, float c) { yr[(size_t)m * F + n] = c + bias[n]; });
+        __syncthreads();
+        if ((L.ln == 0 && !L.relu && L.yc < 0) || (dbg & 8)) continue;
+        if (F <= 64) fwd_rows<4>(L, base, pr, bsz, bp);
+        else if (F <= 128) fwd_rows<8>(L, base, pr, bsz, bp);
+        else fwd_rows<0>(L, base, pr, bsz, bp);
         __syncthreads();
     }
 }
 
 __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
     __shared__ float red[2 * kGW];
+    __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
     if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const int p = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -297,11 +509,11 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
             }
 
             // ---- forward, layer by layer ------------------------------------
-            forward_layers(g.L, g.nl, xobs, bsz, base, pr, bp);
+            forward_layers(g.L, g.nl, xobs, bsz, base, pr, bp, lds, g.dbg);
 
             // ---- loss row pass: logits / value -> d(logits), d(value) (ppo.py:876-908)
             float lsum = 0.f, klsum = 0.f;
-            {
+            if (!(g.dbg & 8)) {
                 const GLay &La = g.L[g.aout];
                 const GLay &Lc = g.L[g.cout];
                 const float *lgp = base + La.yr;
@@ -309,14 +521,36 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                 float *dla = base + La.dy;
                 float *dlv = base + Lc.dy;
                 const int a0 = sub, a1 = sub + 16;
-                for (int r0 = 0; r0 < bsz; r0 += 4 * kGW) {
-                    const int row0 = r0 + 4 * wave + rq;
+                // four rows per 16-lane group at once: every input of the 128-row
+                // block is loaded before the first reduction
+                constexpr int R = 4;
+                for (int rb = 0; rb < bsz; rb += R * 4 * kGW) {
+                    unsigned pbits[R];
+                    int pact[R];
+                    float plg0[R], plg1[R], polp[R], pad[R], pret[R], pov[R], pv[R];
+#pragma unroll
+                    for (int u = 0; u < R; ++u) {
+                        const int row0 = rb + 4 * wave + rq + 4 * kGW * u;
+                        const int row = row0 < bsz ? row0 : 0;
+                        pbits[u] = gmask_e ? gmask_e[s0 + row] : 0xffffffffu;
+                        plg0[u] = lgp[(size_t)row * A + (a0 < A ? a0 : 0)];
+                        plg1[u] = lgp[(size_t)row * A + (a1 < A ? a1 : 0)];
+                        pact[u] = gact_e[s0 + row];
+                        polp[u] = grow_e[s0 + row];
+                        pad[u] = grow_e[S + s0 + row];
+                        pret[u] = grow_e[2 * S + s0 + row];
+                        pov[u] = grow_e[3 * S + s0 + row];
+                        pv[u] = vp[row];
+                    }
+#pragma unroll
+                    for (int u = 0; u < R; ++u) {
+                    const int row0 = rb + 4 * wave + rq + 4 * kGW * u;
                     const bool live = row0 < bsz;
                     const int row = live ? row0 : 0;
-                    const unsigned bits = gmask_e ? gmask_e[s0 + row] : 0xffffffffu;
+                    const unsigned bits = pbits[u];
                     const bool ok0 = (bits >> a0) & 1u, ok1 = (bits >> a1) & 1u;
-                    const float lg0 = a0 < A ? (ok0 ? lgp[(size_t)row * A + a0] : -1.0e8f) : -3.0e38f;
-                    const float lg1 = a1 < A ? (ok1 ? lgp[(size_t)row * A + a1] : -1.0e8f) : -3.0e38f;
+                    const float lg0 = a0 < A ? (ok0 ? plg0[u] : -1.0e8f) : -3.0e38f;
+                    const float lg1 = a1 < A ? (ok1 ? plg1[u] : -1.0e8f) : -3.0e38f;
                     const float mx = rmax16(fmaxf(lg0, lg1));
                     const float ex0 = a0 < A ? expf(lg0 - mx) : 0.f, ex1 = a1 < A ? expf(lg1 - mx) : 0.f;
                     const float lse = mx + logf(rsum16(ex0 + ex1));
@@ -325,12 +559,11 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                     const float Hs = -rsum16((a0 < A ? p0 * lpe0 : 0.f) + (a1 < A ? p1 * lpe1 : 0.f));
                     const float gh0 = -(lpe0 + p0 / (p0 + 1e-8f)), gh1 = -(lpe1 + p1 / (p1 + 1e-8f));
                     const float pg = rsum16((a0 < A ? p0 * gh0 : 0.f) + (a1 < A ? p1 * gh1 : 0.f));
-                    const int a_t = gact_e[s0 + row];
+                    const int a_t = pact[u];
                     const int srcl = (lane & ~15) + (a_t & 15);
                     const float t0 = bperm(srcl, lg0), t1 = bperm(srcl, lg1);
                     const float logp = (a_t < 16 ? t0 : t1) - lse;
-                    const float olp = grow_e[s0 + row], Ad = grow_e[S + s0 + row], R = grow_e[2 * S + s0 + row],
-                                ov = grow_e[3 * S + s0 + row];
+                    const float olp = polp[u], Ad = pad[u], Rt = pret[u], ov = pov[u];
                     const float lo = 1.f - g.clip, hi = 1.f + g.clip;
                     const float lrt = logp - olp;
                     const float ratio = expf(lrt);
@@ -340,10 +573,10 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                     const float g2 = q2 > q1 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
                     const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
                     const float g_logp = ((g1 * -Ad + g2 * -Ad * inr) * inv_b) * ratio;
-                    const float v = vp[row];
+                    const float v = pv[u];
                     const float dv = v - ov;
                     const float vcl = ov + fminf(fmaxf(dv, -g.clip), g.clip);
-                    const float eu = v - R, ec = vcl - R;
+                    const float eu = v - Rt, ec = vcl - Rt;
                     const float lu = eu * eu, lc = ec * ec;
                     const float gu = lu > lc ? 1.f : (lu == lc ? 0.5f : 0.f);
                     const float gc = lc > lu ? 1.f : (lu == lc ? 0.5f : 0.f);
@@ -360,6 +593,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                             klsum += ((ratio - 1.f) - lrt) * inv_b;  // approx_kl (ppo.py:899-902)
                         }
                     }
+                    }
                 }
             }
             __syncthreads();
@@ -369,50 +603,15 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
             for (int l = g.nl - 1; l >= 0; --l) {
                 const GLay &L = g.L[l];
                 const int F = L.fout;
-                const float *dy = base + L.dy;
-                const float invF = 1.f / (float)F;
                 // dY -> dZ through ReLU and LayerNorm(+affine)
-                for (int r0 = 0; r0 < bsz; r0 += 4 * kGW) {
-                    const int row = r0 + 4 * wave + rq;
-                    const bool live = row < bsz;
-                    // d(pre-activation) of column j: dY masked by the ReLU
-                    auto dpre = [&](int j) {
-                        const float d = dy[(size_t)row * F + j];
-                        return (!L.relu || base[L.yr + (size_t)row * F + j] > 0.f) ? d : 0.f;
-                    };
-                    float m1 = 0.f, m2 = 0.f, rstd = 1.f;
-                    if (L.ln) {
-                        float s1 = 0.f, s2 = 0.f;
-                        if (live)
-                            for (int j = sub; j < F; j += 16) {
-                                const float dx = L.ln == 2 ? dpre(j) * pr[L.g + j] : dpre(j);
-                                s1 += dx;
-                                s2 += dx * base[L.xh + (size_t)row * F + j];
-                            }
-                        m1 = rsum16(s1) * invF;
-                        m2 = rsum16(s2) * invF;
-                        rstd = live ? base[L.rs + row] : 0.f;
-                    }
-                    if (!live) continue;
-                    for (int j = sub; j < F; j += 16) {
-                        const float d = dpre(j);
-                        float dz = d;
-                        if (L.ln) {
-                            const float xh = base[L.xh + (size_t)row * F + j];
-                            const float dx = L.ln == 2 ? d * pr[L.g + j] : d;
-                            dz = rstd * (dx - m1 - xh * m2);
-                            if (L.ln == 2) {
-                                t1c[(size_t)j * bp + row] = d * xh;
-                                t2c[(size_t)j * bp + row] = d;
-                            }
-                        }
-                        dzr[(size_t)row * F + j] = dz;
-                        dzc[(size_t)j * bp + row] = dz;
-                    }
+                if (!(g.dbg & 8)) {
+                    if (F <= 64) bwd_rows<4>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
+                    else if (F <= 128) bwd_rows<8>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
+                    else bwd_rows<0>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
                 }
                 __syncthreads();
                 // bias / LN-affine gradients: column sums over the rows (fixed order)
-                for (int o0 = 0; o0 < F; o0 += 4 * kGW) {
+                for (int o0 = 0; o0 < ((g.dbg & 16) ? 0 : F); o0 += 4 * kGW) {
                     const int o = o0 + 4 * wave + rq;
                     const bool on = o < F;
                     float sb = 0.f, sg = 0.f, sbe = 0.f;
@@ -442,12 +641,14 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                 const float *xc = L.src < 0 ? base + g.oc : base + g.L[L.src].yc;
                 float *gw = G + L.w;
                 const int fin = L.fin;
-                gemm_nt(dzc, bp, xc, bp, F, fin, bsz, [&](int m, int n, float c) { gw[(size_t)m * fin + n] = c; });
+                if (!(g.dbg & 2))
+                    gemm_nt(dzc, bp, xc, bp, F, fin, bsz, lds,
+                            [&](int m, int n, float c) { gw[(size_t)m * fin + n] = c; });
                 // dX = dZ W into the source's dY
-                if (L.src >= 0) {
+                if (L.src >= 0 && !(g.dbg & 4)) {
                     float *dys = base + g.L[L.src].dy;
                     const bool acc = L.acc != 0;
-                    gemm_nt(dzr, F, base + L.wt, F, bsz, fin, F, [&](int m, int n, float c) {
+                    gemm_nt(dzr, F, base + L.wt, F, bsz, fin, F, lds, [&](int m, int n, float c) {
                         float *d = dys + (size_t)m * fin + n;
                         *d = acc ? *d + c : c;
                     });
@@ -475,32 +676,47 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
             const float bc2s = (float)sqrt(1.0 - pb2);
             const float step_size = lr_p / bc1;
             const float ob1 = 1.f - g.b1, ob2 = 1.f - g.b2;
-            auto adam = [&](int f) {
-                const float gc = G[f] * (f < g.cstart ? c0 : c1);
-                const float m = gm[f] + ob1 * (gc - gm[f]);
-                const float v = gv[f] * g.b2 + ob2 * gc * gc;
-                gm[f] = m;
-                gv[f] = v;
-                const float np = pr[f] - step_size * (m / (sqrtf(v) / bc2s + g.eps));
-                pr[f] = np;
-                return np;
-            };
-            for (int l = 0; l < g.nl; ++l) {
-                const GLay &L = g.L[l];
-                const int nw = L.fout * L.fin;
-                for (int i = tid; i < nw; i += kGT) {
-                    const float np = adam(L.w + i);
-                    if (L.wt >= 0) {
-                        const int o = i / L.fin, c = i - o * L.fin;
-                        base[L.wt + (size_t)c * L.fout + o] = np;
+            // Adam over each parameter region, four elements per thread per round:
+            // all loads of a round issued before its stores (the stores could
+            // alias the loads as far as the compiler knows)
+            auto adam_region = [&](int f0, int cnt, long long wt, int fin, int fout) {
+                for (int i0 = tid; i0 < cnt; i0 += 4 * kGT) {
+                    float gg[4], mm[4], vv[4], pp[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int i = i0 + k * kGT;
+                        const int f = f0 + (i < cnt ? i : 0);
+                        gg[k] = G[f];
+                        mm[k] = gm[f];
+                        vv[k] = gv[f];
+                        pp[k] = pr[f];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int i = i0 + k * kGT;
+                        if (i >= cnt) break;
+                        const int f = f0 + i;
+                        const float gc = gg[k] * (f < g.cstart ? c0 : c1);
+                        const float m = mm[k] + ob1 * (gc - mm[k]);
+                        const float v = vv[k] * g.b2 + ob2 * gc * gc;
+                        const float np = pp[k] - step_size * (m / (sqrtf(v) / bc2s + g.eps));
+                        gm[f] = m;
+                        gv[f] = v;
+                        pr[f] = np;
+                        if (wt >= 0) {
+                            const int o = i / fin, c = i - o * fin;
+                            base[wt + (size_t)c * fout + o] = np;
+                        }
                     }
                 }
-                for (int i = tid; i < L.fout; i += kGT) {
-                    adam(L.b + i);
-                    if (L.ln == 2) {
-                        adam(L.g + i);
-                        adam(L.be + i);
-                    }
+            };
+            for (int l = 0; l < ((g.dbg & 32) ? 0 : g.nl); ++l) {
+                const GLay &L = g.L[l];
+                adam_region(L.w, L.fout * L.fin, L.wt, L.fin, L.fout);
+                adam_region(L.b, L.fout, -1, 1, 1);
+                if (L.ln == 2) {
+                    adam_region(L.g, L.fout, -1, 1, 1);
+                    adam_region(L.be, L.fout, -1, 1, 1);
                 }
             }
             __syncthreads();
@@ -558,13 +774,14 @@ struct GActArgs {
 // distributions.py:16-28), Gumbel-max sample from the Philox stream of
 // agx_ppo_act, log-prob, entropy, value.
 __global__ __launch_bounds__(kGT) void ppo_act_graph_kernel(const GActArgs g) {
+    __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
     const int p = blockIdx.y, n0 = blockIdx.x * g.rows;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane & 15, rq = lane >> 4;
     const int nrow = g.N - n0 < g.rows ? g.N - n0 : g.rows;
     float *base = g.ws + ((size_t)p * gridDim.x + blockIdx.x) * g.ws_block;
     const float *pr = g.params + (size_t)p * g.n;
-    forward_layers(g.L, g.nl, g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * g.D, nrow, base, pr, g.rows);
+    forward_layers(g.L, g.nl, g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * g.D, nrow, base, pr, g.rows, lds);
     const float *lgp = base + g.L[g.aout].yr;
     const float *vp = base + g.L[g.cout].yr;
     const int A = g.A;
@@ -842,6 +1059,10 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
     a.kl_out = x->kl_out;
     a.epochs_out = x->epochs_out;
     a.skip = x->skip_if_set;
+    {
+        const char *d = getenv("AGX_GRAPH_DEBUG");
+        a.dbg = d ? atoi(d) : 0;
+    }
     ppo_learn_graph_kernel<<<(unsigned)P, kGT, 0, s>>>(a);
     return check_launch("agx_ppo_learn_graph");
 }

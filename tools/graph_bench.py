@@ -46,18 +46,23 @@ def timed(fn, reps=REPS):
     return round((time.perf_counter() - t0) / reps * 1e3, 3)
 
 
-out = {"P": P, "S": 2048, "batch": 128, "epochs": 4}
-pop = make()
-perms = pop.permutations()
-fl, gl = FusedLearner(pop), GraphLearner(pop)
-out["config2_fused_ms"] = timed(lambda: fl.learn(pop, perms))
-out["config2_graph_ms"] = timed(lambda: gl.learn(pop, perms))
-for name, kw in {"mutated_enc80_lat56_head2": dict(encoder_hidden=[80], latent_dim=56, actor_hidden=[64, 64]),
-                 "mutated_wide": dict(encoder_hidden=[192], latent_dim=96, actor_hidden=[128], critic_hidden=[128])
-                 }.items():
-    pop = make(**kw)
+def main():
+    out = {"P": P, "S": 2048, "batch": 128, "epochs": 4}
+    pop = make()
     perms = pop.permutations()
-    gl = GraphLearner(pop)
-    out[name + "_graph_ms"] = timed(lambda: gl.learn(pop, perms))
-    out[name + "_torch_ms"] = timed(lambda: pop._learn_torch(perms), reps=1)
-print(json.dumps(out), flush=True)
+    fl, gl = FusedLearner(pop), GraphLearner(pop)
+    out["config2_fused_ms"] = timed(lambda: fl.learn(pop, perms))
+    out["config2_graph_ms"] = timed(lambda: gl.learn(pop, perms))
+    for name, kw in {"mutated_enc80_lat56_head2": dict(encoder_hidden=[80], latent_dim=56, actor_hidden=[64, 64]),
+                     "mutated_wide": dict(encoder_hidden=[192], latent_dim=96, actor_hidden=[128], critic_hidden=[128])
+                     }.items():
+        pop = make(**kw)
+        perms = pop.permutations()
+        gl = GraphLearner(pop)
+        out[name + "_graph_ms"] = timed(lambda: gl.learn(pop, perms))
+        out[name + "_torch_ms"] = timed(lambda: pop._learn_torch(perms), reps=1)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
