@@ -51,10 +51,12 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 struct GLay {
     int fin, fout, w, b, g, be, ln, relu, src;
-    int acc;  // dX adds into the source's dY (a consumer processed earlier wrote it)
+    int acc;  // dX goes to the source's second dY buffer (a consumer processed earlier wrote the first)
     // per-agent scratch offsets (floats; -1: not kept): output row-major,
-    // output feature-major, xhat, rstd, d(output), transposed weight
-    long long yr, yc, xh, rs, dy, wt;
+    // output feature-major, xhat, rstd, d(output), d(output) from a second
+    // consumer (the latent feeding both heads: the row pass adds the two),
+    // transposed weight
+    long long yr, yc, xh, rs, dy, dy2, wt;
 };
 
 struct GArgs {
@@ -121,9 +123,9 @@ constexpr int kTPW = (kBM / 16) * (kBN / 16) / kGW;      // tiles per wave
 constexpr int kPanel = (kBM + kBN) * kLdS;  // A rows then B rows
 constexpr int kGemmLds = 2 * kPanel;        // double-buffered
 
-template <class FE>
+template <class FA, class FE>
 __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B, int ldb, int M, int N, int K,
-                                        float *lds, FE epi) {
+                                        float *lds, FA addend, FE epi) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, q = lane >> 4;
     const int lr = tid / kKC, lk = tid % kKC;  // staging: rows lr + kRS i, column lk
@@ -189,6 +191,19 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 __syncthreads();
                 buf ^= 1;
             }
+            // epilogue: every addend load of the block before its first store (a
+            // load issued after a store waits for that store too: one vmcnt)
+            float add[kTPW][4];
+#pragma unroll
+            for (int j = 0; j < kTPW; ++j) {
+                const int t = wave + kGW * j;
+                const int m0 = (t % mtn) << 4, n0 = (t / mtn) << 4;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m = m0 + 4 * q + i, n = n0 + r;
+                    add[j][i] = (t < T && m < BM && n < BN) ? addend(mb + m, nb + n) : 0.f;
+                }
+            }
 #pragma unroll
             for (int j = 0; j < kTPW; ++j) {
                 const int t = wave + kGW * j;
@@ -197,7 +212,7 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int m = m0 + 4 * q + i, n = n0 + r;
-                        if (m < BM && n < BN) epi(mb + m, nb + n, acc[j][i]);
+                        if (m < BM && n < BN) epi(mb + m, nb + n, acc[j][i] + add[j][i]);
                     }
                 }
             }
@@ -236,11 +251,11 @@ __device__ __forceinline__ void fwd_rows(const GLay &L, float *base, const float
     float *yr = base + L.yr;
     const int F = L.fout;
     const float invF = 1.f / (float)F;
-    auto out = [&](int row, int j, float y, float mean, float rstd) {
+    auto out = [&](int row, int j, float y, float mean, float rstd, float ga, float be) {
         if (L.ln) {
             const float xh = (y - mean) * rstd;
             if (L.xh >= 0) base[L.xh + (size_t)row * F + j] = xh;
-            y = L.ln == 2 ? xh * pr[L.g + j] + pr[L.be + j] : xh;
+            y = L.ln == 2 ? xh * ga + be : xh;
         }
         if (L.relu) y = relu(y);
         yr[(size_t)row * F + j] = y;
@@ -248,6 +263,15 @@ __device__ __forceinline__ void fwd_rows(const GLay &L, float *base, const float
     };
     if constexpr (C > 0) {
         constexpr int R = 4;
+        // the LN affine of the lane's columns, loaded before any store
+        float ga[C], be[C];
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+            const int j = sub + 16 * i < F ? sub + 16 * i : 0;
+            const float a = pr[L.ln == 2 ? L.g + j : 0], b = pr[L.ln == 2 ? L.be + j : 0];
+            ga[i] = a;
+            be[i] = b;
+        }
         for (int r0 = 0; r0 < bsz; r0 += R * 4 * kGW) {
             float z[R][C];
 #pragma unroll
@@ -283,7 +307,7 @@ __device__ __forceinline__ void fwd_rows(const GLay &L, float *base, const float
 #pragma unroll
                     for (int i = 0; i < C; ++i) {
                         const int j = sub + 16 * i;
-                        if (j < F) out(row, j, z[u][i], mean, rstd);
+                        if (j < F) out(row, j, z[u][i], mean, rstd, ga[i], be[i]);
                     }
                 }
             }
@@ -308,7 +332,9 @@ __device__ __forceinline__ void fwd_rows(const GLay &L, float *base, const float
                 if (live && sub == 0 && L.rs >= 0) base[L.rs + row] = rstd;
             }
             if (!live) continue;
-            for (int j = sub; j < F; j += 16) out(row, j, yr[(size_t)row * F + j], mean, rstd);
+            for (int j = sub; j < F; j += 16)
+                out(row, j, yr[(size_t)row * F + j], mean, rstd, L.ln == 2 ? pr[L.g + j] : 1.f,
+                    L.ln == 2 ? pr[L.be + j] : 0.f);
         }
     }
 }
@@ -334,7 +360,7 @@ __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float
         dzc[(size_t)j * bp + row] = dz;
     };
     if constexpr (C > 0) {
-        constexpr int R = 8 / C;  // 8 cached columns per lane: three loads each in flight
+        constexpr int R = 8 / C;  // 8 cached columns per lane: four loads each in flight
         float gam[C];
 #pragma unroll
         for (int i = 0; i < C; ++i) {
@@ -355,10 +381,10 @@ __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float
                     const int j = sub + 16 * i;
                     const bool on = row < bsz && j < F;
                     const size_t o = on ? (size_t)row * F + j : 0;
-                    const float d = dy[o];
+                    const float d = dy[o], d2 = base[L.dy2 >= 0 ? L.dy2 + o : 0];
                     const float y = base[L.relu ? L.yr + o : 0];
                     const float x = base[L.ln ? L.xh + o : 0];
-                    dp[u][i] = (on && (!L.relu || y > 0.f)) ? d : 0.f;
+                    dp[u][i] = (on && (!L.relu || y > 0.f)) ? (L.dy2 >= 0 ? d + d2 : d) : 0.f;
                     xh[u][i] = (on && L.ln) ? x : 0.f;
                 }
             }
@@ -395,7 +421,7 @@ __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float
             const bool live = row < bsz;
             // d(pre-activation) of column j: dY masked by the ReLU
             auto dpre = [&](int j) {
-                const float d = dy[(size_t)row * F + j];
+                const float d = dy[(size_t)row * F + j] + (L.dy2 >= 0 ? base[L.dy2 + (size_t)row * F + j] : 0.f);
                 return (!L.relu || base[L.yr + (size_t)row * F + j] > 0.f) ? d : 0.f;
             };
             float m1 = 0.f, m2 = 0.f, rstd = 1.f;
@@ -440,8 +466,8 @@ __device__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bs
         const int F = L.fout;
         const float *bias = pr + L.b;
         if (!(dbg & 1))
-            gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds,
-                    [&](int m, int n, float c) { yr[(size_t)m * F + n] = c + bias[n]; });
+            gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, [&](int, int n) { return bias[n]; },
+                    [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; });
         __syncthreads();
         if ((L.ln == 0 && !L.relu && L.yc < 0) || (dbg & 8)) continue;
         if (F <= 64) fwd_rows<4>(L, base, pr, bsz, bp);
@@ -610,30 +636,40 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                     else bwd_rows<0>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
                 }
                 __syncthreads();
-                // bias / LN-affine gradients: column sums over the rows (fixed order)
-                for (int o0 = 0; o0 < ((g.dbg & 16) ? 0 : F); o0 += 4 * kGW) {
-                    const int o = o0 + 4 * wave + rq;
-                    const bool on = o < F;
-                    float sb = 0.f, sg = 0.f, sbe = 0.f;
-                    if (on) {
-                        for (int b = sub; b < bsz; b += 16) {
-                            sb += dzc[(size_t)o * bp + b];
-                            if (L.ln == 2) {
-                                sg += t1c[(size_t)o * bp + b];
-                                sbe += t2c[(size_t)o * bp + b];
+                // bias / LN-affine gradients: column sums over the rows (fixed order);
+                // up to 8 feature groups summed before the first store
+                for (int ob = 0; ob < ((g.dbg & 16) ? 0 : F); ob += 8 * 4 * kGW) {
+                    float rb_[8], rg_[8], rbe_[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int o = ob + 4 * kGW * k + 4 * wave + rq;
+                        const bool on = o < F;
+                        float sb = 0.f, sg = 0.f, sbe = 0.f;
+                        if (ob + 4 * kGW * k < F) {  // wave-uniform
+                            for (int b = sub; b < bsz; b += 16) {
+                                const size_t x = (size_t)(on ? o : 0) * bp + b;
+                                const float v0 = dzc[x];
+                                sb += on ? v0 : 0.f;
+                                if (L.ln == 2) {
+                                    const float v1 = t1c[x], v2 = t2c[x];
+                                    sg += on ? v1 : 0.f;
+                                    sbe += on ? v2 : 0.f;
+                                }
                             }
                         }
+                        rb_[k] = rsum16(sb);
+                        rg_[k] = L.ln == 2 ? rsum16(sg) : 0.f;
+                        rbe_[k] = L.ln == 2 ? rsum16(sbe) : 0.f;
                     }
-                    sb = rsum16(sb);
-                    if (L.ln == 2) {
-                        sg = rsum16(sg);
-                        sbe = rsum16(sbe);
-                    }
-                    if (on && sub == 0) {
-                        G[L.b + o] = sb;
-                        if (L.ln == 2) {
-                            G[L.g + o] = sg;
-                            G[L.be + o] = sbe;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int o = ob + 4 * kGW * k + 4 * wave + rq;
+                        if (o < F && sub == 0) {
+                            G[L.b + o] = rb_[k];
+                            if (L.ln == 2) {
+                                G[L.g + o] = rg_[k];
+                                G[L.be + o] = rbe_[k];
+                            }
                         }
                     }
                 }
@@ -642,16 +678,13 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                 float *gw = G + L.w;
                 const int fin = L.fin;
                 if (!(g.dbg & 2))
-                    gemm_nt(dzc, bp, xc, bp, F, fin, bsz, lds,
+                    gemm_nt(dzc, bp, xc, bp, F, fin, bsz, lds, [](int, int) { return 0.f; },
                             [&](int m, int n, float c) { gw[(size_t)m * fin + n] = c; });
                 // dX = dZ W into the source's dY
                 if (L.src >= 0 && !(g.dbg & 4)) {
-                    float *dys = base + g.L[L.src].dy;
-                    const bool acc = L.acc != 0;
-                    gemm_nt(dzr, F, base + L.wt, F, bsz, fin, F, lds, [&](int m, int n, float c) {
-                        float *d = dys + (size_t)m * fin + n;
-                        *d = acc ? *d + c : c;
-                    });
+                    float *dys = base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy);
+                    gemm_nt(dzr, F, base + L.wt, F, bsz, fin, F, lds, [](int, int) { return 0.f; },
+                            [&](int m, int n, float c) { dys[(size_t)m * fin + n] = c; });
                 }
                 __syncthreads();
             }
@@ -680,10 +713,11 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
             // all loads of a round issued before its stores (the stores could
             // alias the loads as far as the compiler knows)
             auto adam_region = [&](int f0, int cnt, long long wt, int fin, int fout) {
-                for (int i0 = tid; i0 < cnt; i0 += 4 * kGT) {
-                    float gg[4], mm[4], vv[4], pp[4];
+                constexpr int U = 16;  // elements per thread per round: all loads, then all stores
+                for (int i0 = tid; i0 < cnt; i0 += U * kGT) {
+                    float gg[U], mm[U], vv[U], pp[U];
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
+                    for (int k = 0; k < U; ++k) {
                         const int i = i0 + k * kGT;
                         const int f = f0 + (i < cnt ? i : 0);
                         gg[k] = G[f];
@@ -692,7 +726,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                         pp[k] = pr[f];
                     }
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
+                    for (int k = 0; k < U; ++k) {
                         const int i = i0 + k * kGT;
                         if (i >= cnt) break;
                         const int f = f0 + i;
@@ -857,6 +891,7 @@ int plan_graph(const agx_ppo_graph *net, int64_t batch, GArgs &a) {
     const int64_t bp = (batch + 15) / 16 * 16;
     AGX_REQUIRE(batch >= 1 && bp < (1 << 30), "agx_ppo_graph: bad batch %lld", (long long)batch);
     bool is_src[kGL] = {};
+    int consumers[kGL] = {};
     int maxw = 0;
     long long nw = 0;
     for (int l = 0; l < nl; ++l) {
@@ -871,7 +906,10 @@ int plan_graph(const agx_ppo_graph *net, int64_t batch, GArgs &a) {
         AGX_REQUIRE(in(x.w, (long long)x.fin * x.fout) && in(x.b, x.fout) &&
                         (x.ln != 2 || (in(x.ln_w, x.fout) && in(x.ln_b, x.fout))),
                     "agx_ppo_graph: layer %d parameters outside the row", l);
-        if (x.src >= 0) is_src[x.src] = true;
+        if (x.src >= 0) {
+            is_src[x.src] = true;
+            AGX_REQUIRE(++consumers[x.src] <= 2, "agx_ppo_graph: layer %d feeds more than two layers", x.src);
+        }
         maxw = x.fout > maxw ? x.fout : maxw;
         nw += (long long)x.fin * x.fout + x.fout * (x.ln == 2 ? 3 : 1);
     }
@@ -915,6 +953,11 @@ int plan_graph(const agx_ppo_graph *net, int64_t batch, GArgs &a) {
         }
         L.dy = off;
         off = r4(off + bp * x.fout);
+        L.dy2 = -1;
+        if (consumers[l] == 2) {
+            L.dy2 = off;
+            off = r4(off + bp * x.fout);
+        }
         L.wt = -1;
         if (x.src >= 0) {
             L.wt = off;
@@ -956,7 +999,7 @@ long long act_plan(const GArgs &full, GActArgs &a) {
         GLay &L = a.L[l];
         L.yr = off;
         off = r4(off + (long long)kActRows * L.fout);
-        L.yc = L.xh = L.rs = L.dy = L.wt = -1;
+        L.yc = L.xh = L.rs = L.dy = L.dy2 = L.wt = -1;
     }
     a.nl = full.nl;
     a.aout = full.aout;

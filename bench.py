@@ -823,6 +823,57 @@ CONFIG3_NET = {"latent_dim": 256, "min_latent_dim": 128, "max_latent_dim": 512,
                "head_config": {"hidden_size": [256]}}
 
 
+def mutated_learner_leg(P: int = 8):
+    """One learn() of an architecture-mutated agent population (config-2 sizes:
+    S = 2048 samples per agent, batch 128, 4 epochs) on the
+    runtime-shape HIP learner (agx_ppo_learn_graph) against the plain-PyTorch
+    learner it replaces, beside the compiled fused learner on the unmutated
+    shape.  Shape: encoder [80] -> latent 56 -> actor head [64, 64] / critic
+    [64] (three mutations from ppo.yaml's network)."""
+    from agilerl_amd.population.learner import FusedLearner, GraphLearner
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+
+    dev = torch.device("cuda:0")
+
+    def make(**kw):
+        spec = ActorCriticSpec(obs_dim=8, n_actions=4, **kw)
+        pop = PPOPopulation(spec, P, 16, learn_step=2048, batch_size=128, update_epochs=4, device=dev, fused=True,
+                            seeds=list(range(P)), perm_source="device")
+        g = torch.Generator(device=dev).manual_seed(0)
+        pop.obs.copy_(torch.randn(pop.obs.shape, device=dev, generator=g))
+        pop.actions.copy_(torch.randint(0, 4, pop.actions.shape, device=dev, generator=g))
+        pop.rewards.copy_(torch.randn(pop.rewards.shape, device=dev, generator=g))
+        pop.values.copy_(torch.randn(pop.values.shape, device=dev, generator=g))
+        pop.log_probs.copy_(-torch.rand(pop.log_probs.shape, device=dev, generator=g) - 0.5)
+        pop.finish_rollout(torch.randn(P, 16, 8, device=dev, generator=g),
+                           torch.zeros(P, 16, dtype=torch.uint8, device=dev))
+        return pop, pop.permutations()
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return round((time.perf_counter() - t0) / reps * 1e3, 3)
+
+    pop, perms = make()
+    fl = FusedLearner(pop)
+    out = {"workload": f"{P} agents x S 2048, batch 128, 4 epochs (64 updates per agent per learn)",
+           "compiled_shape_fused_ms": timed(lambda: fl.learn(pop, perms), 5)}
+    del fl, pop
+    pop, perms = make(encoder_hidden=[80], latent_dim=56, actor_hidden=[64, 64])
+    gl = GraphLearner(pop)
+    out["mutated_shape"] = "encoder [80] -> latent 56 -> actor [64, 64] / critic [64]"
+    out["mutated_graph_ms"] = timed(lambda: gl.learn(pop, perms), 5)
+    out["mutated_torch_ms"] = timed(lambda: pop._learn_torch(perms), 1)
+    del gl, pop
+    torch.cuda.empty_cache()
+    return out
+
+
 def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
     """The end-to-end entry point: ``train_on_policy`` (training/train_on_policy.py)
     on an 8-agent population with ppo.yaml's INIT_HP / NET_CONFIG /
@@ -1097,6 +1148,8 @@ def main():
     c3 = config3_leg() if (world == 1 and not args.no_config3) else None
     log("train_on_policy leg")
     tp = train_on_policy_leg() if (world == 1 and not args.no_train_on_policy) else None
+    log("mutated-shape learner leg")
+    ml = mutated_learner_leg() if world == 1 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         log("CPU baseline legs")
@@ -1145,6 +1198,7 @@ def main():
             "config5": c5,
             "config3": c3,
             "train_on_policy": tp,
+            "mutated_shape_learner": ml,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
