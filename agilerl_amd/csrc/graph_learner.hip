@@ -470,8 +470,7 @@ __device__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bs
                     [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; });
         __syncthreads();
         if ((L.ln == 0 && !L.relu && L.yc < 0) || (dbg & 8)) continue;
-        if (F <= 64) fwd_rows<4>(L, base, pr, bsz, bp);
-        else if (F <= 128) fwd_rows<8>(L, base, pr, bsz, bp);
+        if (F <= 128) fwd_rows<8>(L, base, pr, bsz, bp);
         else fwd_rows<0>(L, base, pr, bsz, bp);
         __syncthreads();
     }
@@ -631,8 +630,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                 const int F = L.fout;
                 // dY -> dZ through ReLU and LayerNorm(+affine)
                 if (!(g.dbg & 8)) {
-                    if (F <= 64) bwd_rows<4>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
-                    else if (F <= 128) bwd_rows<8>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
+                    if (F <= 128) bwd_rows<8>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
                     else bwd_rows<0>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
                 }
                 __syncthreads();
@@ -673,18 +671,18 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                         }
                     }
                 }
-                // dW = dZ^T X (contraction over the rows)
+                // dW = dZ^T X (contraction over the rows), then dX = dZ W into the
+                // source's dY (one GEMM call site for both: instruction-cache footprint)
                 const float *xc = L.src < 0 ? base + g.oc : base + g.L[L.src].yc;
-                float *gw = G + L.w;
                 const int fin = L.fin;
-                if (!(g.dbg & 2))
-                    gemm_nt(dzc, bp, xc, bp, F, fin, bsz, lds, [](int, int) { return 0.f; },
-                            [&](int m, int n, float c) { gw[(size_t)m * fin + n] = c; });
-                // dX = dZ W into the source's dY
-                if (L.src >= 0 && !(g.dbg & 4)) {
-                    float *dys = base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy);
-                    gemm_nt(dzr, F, base + L.wt, F, bsz, fin, F, lds, [](int, int) { return 0.f; },
-                            [&](int m, int n, float c) { dys[(size_t)m * fin + n] = c; });
+                for (int job = 0; job < (L.src >= 0 ? 2 : 1); ++job) {
+                    if (g.dbg & (job ? 4 : 2)) continue;
+                    const float *ga = job ? dzr : dzc, *gb = job ? base + L.wt : xc;
+                    const int lda = job ? F : bp, ldb = job ? F : bp;
+                    const int M = job ? bsz : F, K = job ? F : bsz;
+                    float *dst = job ? base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy) : G + L.w;
+                    gemm_nt(ga, lda, gb, ldb, M, fin, K, lds, [](int, int) { return 0.f; },
+                            [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; });
                 }
                 __syncthreads();
             }
@@ -744,14 +742,14 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                     }
                 }
             };
-            for (int l = 0; l < ((g.dbg & 32) ? 0 : g.nl); ++l) {
-                const GLay &L = g.L[l];
-                adam_region(L.w, L.fout * L.fin, L.wt, L.fin, L.fout);
-                adam_region(L.b, L.fout, -1, 1, 1);
-                if (L.ln == 2) {
-                    adam_region(L.g, L.fout, -1, 1, 1);
-                    adam_region(L.be, L.fout, -1, 1, 1);
-                }
+            // regions: per layer W (with its transposed copy), b, LN weight, LN bias
+            for (int rg = 0; rg < ((g.dbg & 32) ? 0 : 4 * g.nl); ++rg) {
+                const GLay &L = g.L[rg >> 2];
+                const int kind = rg & 3;
+                if (kind >= 2 && L.ln != 2) continue;
+                const int f0 = kind == 0 ? L.w : kind == 1 ? L.b : kind == 2 ? L.g : L.be;
+                adam_region(f0, kind == 0 ? L.fout * L.fin : L.fout, kind == 0 ? L.wt : -1, kind == 0 ? L.fin : 1,
+                            kind == 0 ? L.fout : 1);
             }
             __syncthreads();
         }  // minibatches
