@@ -360,13 +360,17 @@ __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float
         dzc[(size_t)j * bp + row] = dz;
     };
     if constexpr (C > 0) {
-        constexpr int R = 8 / C;  // 8 cached columns per lane: four loads each in flight
-        float gam[C];
+        constexpr int R = 16 / C;  // 16 cached columns per lane: three loads each in flight
+        // LN affine of the lane's columns (the ReLU mask of an LN layer is
+        // recomputed from xhat: the same float ops as the forward, no y load)
+        float gam[C], bet[C];
 #pragma unroll
         for (int i = 0; i < C; ++i) {
             const int j = sub + 16 * i;
             const float v = pr[L.ln == 2 ? L.g + (j < F ? j : 0) : 0];
+            const float b = pr[L.ln == 2 ? L.be + (j < F ? j : 0) : 0];
             gam[i] = L.ln == 2 ? v : 1.f;
+            bet[i] = L.ln == 2 ? b : 0.f;
         }
         for (int r0 = 0; r0 < bsz; r0 += R * 4 * kGW) {
             float dp[R][C], xh[R][C], rs[R];
@@ -382,9 +386,10 @@ __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float
                     const bool on = row < bsz && j < F;
                     const size_t o = on ? (size_t)row * F + j : 0;
                     const float d = dy[o], d2 = base[L.dy2 >= 0 ? L.dy2 + o : 0];
-                    const float y = base[L.relu ? L.yr + o : 0];
+                    const float y = base[(L.relu && !L.ln) ? L.yr + o : 0];
                     const float x = base[L.ln ? L.xh + o : 0];
-                    dp[u][i] = (on && (!L.relu || y > 0.f)) ? (L.dy2 >= 0 ? d + d2 : d) : 0.f;
+                    const float pre = L.ln == 2 ? x * gam[i] + bet[i] : (L.ln ? x : y);
+                    dp[u][i] = (on && (!L.relu || pre > 0.f)) ? (L.dy2 >= 0 ? d + d2 : d) : 0.f;
                     xh[u][i] = (on && L.ln) ? x : 0.f;
                 }
             }
