@@ -928,17 +928,23 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
         tour = TournamentSelection(2, True, P, 1)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        pop, _ = train_on_policy(env, "LunarLanderSynthetic", "PPO", pop, INIT_HP=INIT_HP, max_steps=gens * evo_steps,
-                                 evo_steps=evo_steps, eval_steps=None, eval_loop=1, tournament=tour, mutation=mut,
-                                 verbose=bool(os.environ.get("AGX_BENCH_VERBOSE")))
+        import contextlib
+
+        with contextlib.redirect_stdout(sys.stderr):  # stdout carries the one JSON line only
+            pop, _ = train_on_policy(env, "LunarLanderSynthetic", "PPO", pop, INIT_HP=INIT_HP,
+                                     max_steps=gens * evo_steps, evo_steps=evo_steps, eval_steps=None, eval_loop=1,
+                                     tournament=tour, mutation=mut, verbose=bool(os.environ.get("AGX_BENCH_VERBOSE")))
         torch.cuda.synchronize()
         return time.perf_counter() - t0, pop
 
     import warnings
 
-    variants = [("no_arch_mutation", 0.0)]
-    if os.environ.get("AGX_BENCH_E2E_ARCH"):  # ppo.yaml's ARCH_MUT 0.2 too (see DESIGN: mutated shapes)
-        variants.insert(0, ("ppo_yaml", 0.2))
+    # ppo.yaml's MUTATION_PARAMS as they are (ARCH_MUT 0.2: mutated agents run the
+    # runtime-shape kernels, agx_ppo_learn_graph / agx_ppo_act_graph), and with
+    # architecture mutations off (every agent stays on the compiled kernels)
+    variants = [("ppo_yaml", 0.2), ("no_arch_mutation", 0.0)]
+    if os.environ.get("AGX_BENCH_E2E_NO_ARCH_ONLY"):
+        variants = variants[1:]
     for name, arch in variants:
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
@@ -948,8 +954,10 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
             log(f"train_on_policy {name}: {generations} generations in {dt:.1f} s")
         steps = sum(a.steps[-1] for a in pop)
         fused = sum(a.population.fused_descriptor() is not None for a in pop)
+        hip = sum(a.population.learn_descriptor() is not None for a in pop)
         out[name] = {"env_steps_per_s": round(steps / dt, 1), "ms_per_generation": round(dt / generations * 1e3, 2),
-                     "env_steps": int(steps), "agents_on_fused_kernels_at_end": int(fused),
+                     "env_steps": int(steps), "agents_on_compiled_kernels_at_end": int(fused),
+                     "agents_on_hip_kernels_at_end": int(hip),
                      "final_shapes": sorted({str(a.spec.shape_key()[2:6]) for a in pop})}
     return out
 
