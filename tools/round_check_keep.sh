@@ -12,7 +12,7 @@ mkdir -p gpurun_keep
 cp gpurun_out/learner_pmc.txt gpurun_keep/${R}_learner_pmc.txt 2>/dev/null
 cp gpurun_out/learn_sweep.log gpurun_keep/${R}_learn_sweep.log 2>/dev/null
 cp gpurun_out/learner_pmc_run.log gpurun_keep/ 2>/dev/null
-cp gpurun_out/round_check.log gpurun_out/pytest_gpu.log gpurun_out/bench_full.log gpurun_keep/ 2>/dev/null
+cp gpurun_out/round_check.log gpurun_out/pytest_gpu.log gpurun_out/bench_full.json gpurun_out/bench_full.err gpurun_keep/ 2>/dev/null
 cp gpurun_out/${R}_*.json gpurun_keep/ 2>/dev/null
 find gpurun_out/prof_$R -name "*kernel_stats.csv" -exec cp {} gpurun_keep/${R}_kernel_stats.csv \; 2>/dev/null
 find gpurun_out/prof_c3_$R -name "*kernel_stats.csv" -exec cp {} gpurun_keep/${R}_config3_kernel_stats.csv \; 2>/dev/null
