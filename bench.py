@@ -933,7 +933,7 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
         with contextlib.redirect_stdout(sys.stderr):  # stdout carries the one JSON line only
             pop, _ = train_on_policy(env, "LunarLanderSynthetic", "PPO", pop, INIT_HP=INIT_HP,
                                      max_steps=gens * evo_steps, evo_steps=evo_steps, eval_steps=None, eval_loop=1,
-                                     tournament=tour, mutation=mut, verbose=bool(os.environ.get("AGX_BENCH_VERBOSE")))
+                                     tournament=tour, mutation=mut, verbose=True)  # per-generation progress
         torch.cuda.synchronize()
         return time.perf_counter() - t0, pop
 
