@@ -123,9 +123,9 @@ constexpr int kTPW = (kBM / 16) * (kBN / 16) / kGW;      // tiles per wave
 constexpr int kPanel = (kBM + kBN) * kLdS;  // A rows then B rows
 constexpr int kGemmLds = 2 * kPanel;        // double-buffered
 
-template <class FA, class FE>
+template <class FE>
 __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B, int ldb, int M, int N, int K,
-                                        float *lds, FA addend, FE epi) {
+                                        float *lds, const float *bias, FE epi) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, q = lane >> 4;
     const int lr = tid / kKC, lk = tid % kKC;  // staging: rows lr + kRS i, column lk
@@ -161,8 +161,17 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 for (int i = 0; i < kBN / kRS; ++i) Bs[(lr + kRS * i) * kLdS + lk] = rb[i];
             };
             f4 acc[kTPW];
+            // the bias of each of the wave's tiles (column n0 + r), loaded with the
+            // first chunk: its latency hides under the panel fetch
+            float bv_[kTPW];
 #pragma unroll
-            for (int j = 0; j < kTPW; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < kTPW; ++j) {
+                acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+                const int t = wave + kGW * j;
+                const int n = (t / mtn << 4) + r;
+                const float v = bias ? bias[nb + (t < T && n < BN ? n : 0)] : 0.f;
+                bv_[j] = v;
+            }
             fetch(0);
             commit(0);
             __syncthreads();
@@ -191,19 +200,6 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 __syncthreads();
                 buf ^= 1;
             }
-            // epilogue: every addend load of the block before its first store (a
-            // load issued after a store waits for that store too: one vmcnt)
-            float add[kTPW][4];
-#pragma unroll
-            for (int j = 0; j < kTPW; ++j) {
-                const int t = wave + kGW * j;
-                const int m0 = (t % mtn) << 4, n0 = (t / mtn) << 4;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int m = m0 + 4 * q + i, n = n0 + r;
-                    add[j][i] = (t < T && m < BM && n < BN) ? addend(mb + m, nb + n) : 0.f;
-                }
-            }
 #pragma unroll
             for (int j = 0; j < kTPW; ++j) {
                 const int t = wave + kGW * j;
@@ -212,7 +208,7 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int m = m0 + 4 * q + i, n = n0 + r;
-                        if (m < BM && n < BN) epi(mb + m, nb + n, acc[j][i] + add[j][i]);
+                        if (m < BM && n < BN) epi(mb + m, nb + n, acc[j][i] + bv_[j]);
                     }
                 }
             }
@@ -343,9 +339,12 @@ __device__ __forceinline__ void fwd_rows(const GLay &L, float *base, const float
 // dzr and feature-major dzc), plus dY' xhat and dY' feature-major (t1c, t2c)
 // for the LN-affine gradients.  As fwd_rows: C columns per lane cached for
 // 16 / C rows at once (F <= 16 C); C = 0: any width, re-reading the row.
+// C > 0 also takes the bias / LN-affine column sums: per lane over its rows,
+// across the wave's four row groups, then per wave into colp (LDS, [3][kGW][F]);
+// the caller adds the waves in order.  No t1c / t2c round trip through memory.
 template <int C>
 __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float *pr, int bsz, int bp, float *dzr,
-                                         float *dzc, float *t1c, float *t2c) {
+                                         float *dzc, float *t1c, float *t2c, float *colp = nullptr) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane & 15, rq = lane >> 4;
     const int F = L.fout;
@@ -372,6 +371,9 @@ __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float
             gam[i] = L.ln == 2 ? v : 1.f;
             bet[i] = L.ln == 2 ? b : 0.f;
         }
+        float cb[C], cg[C], cbe[C];  // the lane's column partial sums (dz, dy' xhat, dy')
+#pragma unroll
+        for (int i = 0; i < C; ++i) cb[i] = cg[i] = cbe[i] = 0.f;
         for (int r0 = 0; r0 < bsz; r0 += R * 4 * kGW) {
             float dp[R][C], xh[R][C], rs[R];
 #pragma unroll
@@ -414,9 +416,36 @@ __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float
                         const int j = sub + 16 * i;
                         if (j < F) {
                             const float dz = L.ln ? rs[u] * (dp[u][i] * gam[i] - m1 - xh[u][i] * m2) : dp[u][i];
-                            put(row, j, dp[u][i], xh[u][i], dz);
+                            dzr[(size_t)row * F + j] = dz;
+                            dzc[(size_t)j * bp + row] = dz;
+                            cb[i] += dz;
+                            cg[i] += dp[u][i] * xh[u][i];
+                            cbe[i] += dp[u][i];
                         }
                     }
+                }
+            }
+        }
+        // the four row groups of the wave (lanes l, l ^ 16, l ^ 32, l ^ 48), one fixed order
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+            cb[i] += __shfl_xor(cb[i], 16, 64);
+            cb[i] += __shfl_xor(cb[i], 32, 64);
+            if (L.ln == 2) {
+                cg[i] += __shfl_xor(cg[i], 16, 64);
+                cg[i] += __shfl_xor(cg[i], 32, 64);
+                cbe[i] += __shfl_xor(cbe[i], 16, 64);
+                cbe[i] += __shfl_xor(cbe[i], 32, 64);
+            }
+        }
+        if (rq == 0) {
+#pragma unroll
+            for (int i = 0; i < C; ++i) {
+                const int j = sub + 16 * i;
+                if (j < F) {
+                    colp[wave * F + j] = cb[i];
+                    colp[(kGW + wave) * F + j] = cg[i];
+                    colp[(2 * kGW + wave) * F + j] = cbe[i];
                 }
             }
         }
@@ -471,7 +500,7 @@ __device__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bs
         const int F = L.fout;
         const float *bias = pr + L.b;
         if (!(dbg & 1))
-            gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, [&](int, int n) { return bias[n]; },
+            gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
                     [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; });
         __syncthreads();
         if ((L.ln == 0 && !L.relu && L.yc < 0) || (dbg & 8)) continue;
@@ -484,6 +513,7 @@ __device__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bs
 __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
     __shared__ float red[2 * kGW];
     __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
+    __shared__ float colp[3 * kGW * 128];  // per-wave bias / LN-affine column partials (F <= 128)
     if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const int p = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -635,13 +665,28 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                 const int F = L.fout;
                 // dY -> dZ through ReLU and LayerNorm(+affine)
                 if (!(g.dbg & 8)) {
-                    if (F <= 128) bwd_rows<8>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
+                    if (F <= 128) bwd_rows<8>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c, colp);
                     else bwd_rows<0>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
                 }
                 __syncthreads();
                 // bias / LN-affine gradients: column sums over the rows (fixed order);
                 // up to 8 feature groups summed before the first store
-                for (int ob = 0; ob < ((g.dbg & 16) ? 0 : F); ob += 8 * 4 * kGW) {
+                if (F <= 128 && !(g.dbg & 24)) {  // the row pass left per-wave partials in LDS
+                    for (int o = tid; o < F; o += kGT) {
+                        float sb = 0.f, sg = 0.f, sbe = 0.f;
+                        for (int w = 0; w < kGW; ++w) {
+                            sb += colp[w * F + o];
+                            sg += colp[(kGW + w) * F + o];
+                            sbe += colp[(2 * kGW + w) * F + o];
+                        }
+                        G[L.b + o] = sb;
+                        if (L.ln == 2) {
+                            G[L.g + o] = sg;
+                            G[L.be + o] = sbe;
+                        }
+                    }
+                }
+                for (int ob = 0; ob < ((g.dbg & 16) || F <= 128 ? 0 : F); ob += 8 * 4 * kGW) {
                     float rb_[8], rg_[8], rbe_[8];
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
@@ -686,7 +731,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                     const int lda = job ? F : bp, ldb = job ? F : bp;
                     const int M = job ? bsz : F, K = job ? F : bsz;
                     float *dst = job ? base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy) : G + L.w;
-                    gemm_nt(ga, lda, gb, ldb, M, fin, K, lds, [](int, int) { return 0.f; },
+                    gemm_nt(ga, lda, gb, ldb, M, fin, K, lds, nullptr,
                             [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; });
                 }
                 __syncthreads();
