@@ -123,16 +123,37 @@ constexpr int kTPW = (kBM / 16) * (kBN / 16) / kGW;      // tiles per wave
 constexpr int kPanel = (kBM + kBN) * kLdS;  // A rows then B rows
 constexpr int kGemmLds = 2 * kPanel;        // double-buffered
 
-template <class FE>
+// LNE: the forward of a layer at most kBN = 64 wide with its LayerNorm(+affine)
+// / ReLU in the epilogue.  Each wave then owns WHOLE rows (m-tiles wave and
+// wave + kGW, all four n-tile slots), so a row's statistics are register sums
+// over the wave's tiles plus one DPP row reduction over the 16 column lanes:
+// no separate row pass, no re-read of the pre-activations.  L / base / pr / bp
+// describe the layer's outputs (as fwd_rows).
+template <bool LNE = false, class FE>
 __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B, int ldb, int M, int N, int K,
-                                        float *lds, const float *bias, FE epi) {
+                                        float *lds, const float *bias, FE epi, const GLay &L,
+                                        float *base = nullptr, const float *pr = nullptr, int bp = 0) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, q = lane >> 4;
     const int lr = tid / kKC, lk = tid % kKC;  // staging: rows lr + kRS i, column lk
     for (int mb = 0; mb < M; mb += kBM)
         for (int nb = 0; nb < N; nb += kBN) {
             const int BM = M - mb < kBM ? M - mb : kBM, BN = N - nb < kBN ? N - nb : kBN;
-            const int mtn = (BM + 15) >> 4, T = mtn * ((BN + 15) >> 4);
+            const int mtn = (BM + 15) >> 4, ntn = (BN + 15) >> 4, T = mtn * ntn;
+            // slot j of this wave -> tile (m0, n0), valid (wave-uniform)
+            auto tile = [&](int j, int &m0, int &n0) -> bool {
+                if constexpr (LNE) {
+                    const int mt = wave + kGW * (j >> 2), nt = j & 3;
+                    m0 = mt << 4;
+                    n0 = nt << 4;
+                    return mt < mtn && nt < ntn;
+                } else {
+                    const int t = wave + kGW * j;
+                    m0 = (t % mtn) << 4;
+                    n0 = (t / mtn) << 4;
+                    return t < T;
+                }
+            };
             const float *Ab = A + (size_t)mb * lda, *Bb = B + (size_t)nb * ldb;
             float ra[kBM / kRS], rb[kBN / kRS];
             auto fetch = [&](int kc) {
@@ -161,15 +182,15 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 for (int i = 0; i < kBN / kRS; ++i) Bs[(lr + kRS * i) * kLdS + lk] = rb[i];
             };
             f4 acc[kTPW];
-            // the bias of each of the wave's tiles (column n0 + r), loaded with the
-            // first chunk: its latency hides under the panel fetch
+            // per slot: the bias of column n0 + r (and with LNE the LN affine),
+            // loaded with the first chunk: the latency hides under the panel fetch
             float bv_[kTPW];
 #pragma unroll
             for (int j = 0; j < kTPW; ++j) {
                 acc[j] = f4{0.f, 0.f, 0.f, 0.f};
-                const int t = wave + kGW * j;
-                const int n = (t / mtn << 4) + r;
-                const float v = bias ? bias[nb + (t < T && n < BN ? n : 0)] : 0.f;
+                int m0, n0;
+                const bool ok = tile(j, m0, n0) && n0 + r < BN;
+                const float v = bias ? bias[nb + (ok ? n0 + r : 0)] : 0.f;
                 bv_[j] = v;
             }
             fetch(0);
@@ -182,9 +203,8 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 const float *As = lds + buf * kPanel, *Bs = As + kBM * kLdS;
 #pragma unroll
                 for (int j = 0; j < kTPW; ++j) {
-                    const int t = wave + kGW * j;
-                    if (t < T) {  // wave-uniform
-                        const int m0 = (t % mtn) << 4, n0 = (t / mtn) << 4;
+                    int m0, n0;
+                    if (tile(j, m0, n0)) {  // wave-uniform
                         float av[8], bv[8];
 #pragma unroll
                         for (int kk = 0; kk < 8; ++kk) {
@@ -200,15 +220,71 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 __syncthreads();
                 buf ^= 1;
             }
+            if constexpr (LNE) {
+                const float invF = 1.f / (float)N;
+                // the LN affine of the lane's four columns, loaded before any store
+                float ga_[4], be_[4];
 #pragma unroll
-            for (int j = 0; j < kTPW; ++j) {
-                const int t = wave + kGW * j;
-                if (t < T) {
-                    const int m0 = (t % mtn) << 4, n0 = (t / mtn) << 4;
+                for (int nt = 0; nt < 4; ++nt) {
+                    const int n = (nt < ntn && (nt << 4) + r < BN) ? (nt << 4) + r : 0;
+                    const float gv = pr[L.ln == 2 ? L.g + n : 0], bb = pr[L.ln == 2 ? L.be + n : 0];
+                    ga_[nt] = L.ln == 2 ? gv : 1.f;
+                    be_[nt] = L.ln == 2 ? bb : 0.f;
+                }
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    if (wave + kGW * a >= mtn) break;  // wave-uniform
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const int m = m0 + 4 * q + i, n = n0 + r;
-                        if (m < BM && n < BN) epi(mb + m, nb + n, acc[j][i] + bv_[j]);
+                        const int row = mb + ((wave + kGW * a) << 4) + 4 * q + i;
+                        float v[4], s = 0.f;
+#pragma unroll
+                        for (int nt = 0; nt < 4; ++nt) {
+                            const bool on = nt < ntn && (nt << 4) + r < BN;
+                            v[nt] = on ? acc[4 * a + nt][i] + bv_[4 * a + nt] : 0.f;
+                            s += v[nt];
+                        }
+                        float mean = 0.f, rstd = 1.f;
+                        if (L.ln) {
+                            mean = rsum16(s) * invF;
+                            float vs = 0.f;
+#pragma unroll
+                            for (int nt = 0; nt < 4; ++nt) {
+                                const float d = v[nt] - mean;
+                                vs += (nt < ntn && (nt << 4) + r < BN) ? d * d : 0.f;
+                            }
+                            rstd = 1.f / sqrtf(rsum16(vs) / (float)N + 1e-5f);
+                            if (r == 0 && row < M && L.rs >= 0) base[L.rs + row] = rstd;
+                        }
+                        if (row < M) {
+#pragma unroll
+                            for (int nt = 0; nt < 4; ++nt) {
+                                const int n = (nt << 4) + r;
+                                if (nt < ntn && n < BN) {
+                                    float y = v[nt];
+                                    if (L.ln) {
+                                        const float xh = (y - mean) * rstd;
+                                        if (L.xh >= 0) base[L.xh + (size_t)row * N + n] = xh;
+                                        y = L.ln == 2 ? xh * ga_[nt] + be_[nt] : xh;
+                                    }
+                                    if (L.relu) y = relu(y);
+                                    epi(row, n, y);
+                                    if (L.yc >= 0) base[L.yc + (size_t)n * bp + row] = y;
+                                }
+                            }
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < kTPW; ++j) {
+                    int m0, n0;
+                    if (tile(j, m0, n0)) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int m = m0 + 4 * q + i, n = n0 + r;
+                            if (m < BM && n < BN) epi(mb + m, nb + n, acc[j][i] + bv_[j]);
+                        }
                     }
                 }
             }
@@ -491,7 +567,7 @@ __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float
 // keeping xhat / rstd / the feature-major copy where the plan has room for
 // them (the learner; the policy step keeps outputs only).  xobs: the
 // observation rows (stride = the first layer's fin).
-__device__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bsz, float *base, const float *pr,
+__device__ __forceinline__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bsz, float *base, const float *pr,
                                int bp, float *lds, int dbg = 0) {
     for (int l = 0; l < nl; ++l) {
         const GLay &L = Ls[l];
@@ -499,11 +575,17 @@ __device__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bs
         float *yr = base + L.yr;
         const int F = L.fout;
         const float *bias = pr + L.b;
-        if (!(dbg & 1))
-            gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
-                    [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; });
+        const bool lne = F <= kBN && (L.ln || L.relu);  // LayerNorm / ReLU in the GEMM epilogue
+        if (!(dbg & 1)) {
+            if (lne)
+                gemm_nt<true>(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
+                              [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; }, L, base, pr, bp);
+            else
+                gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
+                        [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; }, L);
+        }
         __syncthreads();
-        if ((L.ln == 0 && !L.relu && L.yc < 0) || (dbg & 8)) continue;
+        if (lne || (L.ln == 0 && !L.relu && L.yc < 0) || (dbg & 8)) continue;
         if (F <= 128) fwd_rows<8>(L, base, pr, bsz, bp);
         else fwd_rows<0>(L, base, pr, bsz, bp);
         __syncthreads();
@@ -732,7 +814,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                     const int M = job ? bsz : F, K = job ? F : bsz;
                     float *dst = job ? base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy) : G + L.w;
                     gemm_nt(ga, lda, gb, ldb, M, fin, K, lds, nullptr,
-                            [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; });
+                            [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; }, L);
                 }
                 __syncthreads();
             }
