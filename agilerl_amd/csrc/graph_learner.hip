@@ -57,6 +57,7 @@ struct GLay {
     // consumer (the latent feeding both heads: the row pass adds the two),
     // transposed weight
     long long yr, yc, xh, rs, dy, dy2, wt;
+    long long dyc;  // output layers: d(output) feature-major, written by the loss pass (-1 otherwise)
 };
 
 struct GArgs {
@@ -596,6 +597,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
     __shared__ float red[2 * kGW];
     __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
     __shared__ float colp[3 * kGW * 128];  // per-wave bias / LN-affine column partials (F <= 128)
+    __shared__ float colo[kGW * 33];       // per-wave output-layer bias partials (32 logits + the value)
     if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const int p = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -661,8 +663,10 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                 const float *lgp = base + La.yr;
                 const float *vp = base + Lc.yr;
                 float *dla = base + La.dy;
+                float *dlac = base + La.dyc;
                 float *dlv = base + Lc.dy;
                 const int a0 = sub, a1 = sub + 16;
+                float cb0 = 0.f, cb1 = 0.f, cbv = 0.f;  // output-layer bias gradients (column partials)
                 // four rows per 16-lane group at once: every input of the 128-row
                 // block is loaded before the first reduction
                 constexpr int R = 4;
@@ -727,33 +731,64 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                     const float dl0 = g_logp * ((a0 == a_t ? 1.f : 0.f) - p0) + g_H * p0 * (gh0 - pg);
                     const float dl1 = g_logp * ((a1 == a_t ? 1.f : 0.f) - p1) + g_H * p1 * (gh1 - pg);
                     if (live) {
-                        if (a0 < A) dla[(size_t)row * A + a0] = ok0 ? dl0 : 0.f;
-                        if (a1 < A) dla[(size_t)row * A + a1] = ok1 ? dl1 : 0.f;
+                        const float d0 = ok0 ? dl0 : 0.f, d1 = ok1 ? dl1 : 0.f;
+                        if (a0 < A) {
+                            dla[(size_t)row * A + a0] = d0;
+                            dlac[(size_t)a0 * bp + row] = d0;
+                            cb0 += d0;
+                        }
+                        if (a1 < A) {
+                            dla[(size_t)row * A + a1] = d1;
+                            dlac[(size_t)a1 * bp + row] = d1;
+                            cb1 += d1;
+                        }
                         if (sub == 0) {
-                            dlv[row] = g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv);
+                            const float dvv = g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv);
+                            dlv[row] = dvv;
+                            cbv += dvv;
                             lsum += (fmaxf(q1, q2) + g.vf * 0.5f * fmaxf(lu, lc) - entp * Hs) * inv_b;
                             klsum += ((ratio - 1.f) - lrt) * inv_b;  // approx_kl (ppo.py:899-902)
                         }
                     }
                     }
                 }
+                // bias gradients of the output layers: the wave's four row groups,
+                // then per wave into LDS (summed over the waves in order below)
+                cb0 += __shfl_xor(cb0, 16, 64);
+                cb0 += __shfl_xor(cb0, 32, 64);
+                cb1 += __shfl_xor(cb1, 16, 64);
+                cb1 += __shfl_xor(cb1, 32, 64);
+                cbv += __shfl_xor(cbv, 16, 64);
+                cbv += __shfl_xor(cbv, 32, 64);
+                if (rq == 0) {
+                    colo[wave * 33 + a0] = cb0;
+                    colo[wave * 33 + a1] = cb1;
+                    if (sub == 0) colo[wave * 33 + 32] = cbv;
+                }
             }
             __syncthreads();
+            if (!(g.dbg & 8) && tid <= A) {
+                float sb = 0.f;
+                for (int w = 0; w < kGW; ++w) sb += colo[w * 33 + (tid < A ? tid : 32)];
+                G[tid < A ? g.L[g.aout].b + tid : g.L[g.cout].b] = sb;
+            }
 
             // ---- backward, layer by layer (reverse) ----------------------------
             float *dzr = base + g.dzr, *dzc = base + g.dzc, *t1c = base + g.t1, *t2c = base + g.t2;
             for (int l = g.nl - 1; l >= 0; --l) {
                 const GLay &L = g.L[l];
                 const int F = L.fout;
+                // output layers: the loss pass wrote dZ in both layouts and the bias gradient
+                const bool outl = L.dyc >= 0;
                 // dY -> dZ through ReLU and LayerNorm(+affine)
-                if (!(g.dbg & 8)) {
+                if (!(g.dbg & 8) && !outl) {
                     if (F <= 128) bwd_rows<8>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c, colp);
                     else bwd_rows<0>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
                 }
-                __syncthreads();
+                if (!outl) __syncthreads();
                 // bias / LN-affine gradients: column sums over the rows (fixed order);
                 // up to 8 feature groups summed before the first store
-                if (F <= 128 && !(g.dbg & 24)) {  // the row pass left per-wave partials in LDS
+                if (F <= 128 && !(g.dbg & 24) && !outl) {  // the row pass left per-wave partials in LDS
                     for (int o = tid; o < F; o += kGT) {
                         float sb = 0.f, sg = 0.f, sbe = 0.f;
                         for (int w = 0; w < kGW; ++w) {
@@ -768,7 +803,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                         }
                     }
                 }
-                for (int ob = 0; ob < ((g.dbg & 16) || F <= 128 ? 0 : F); ob += 8 * 4 * kGW) {
+                for (int ob = 0; ob < ((g.dbg & 16) || F <= 128 || outl ? 0 : F); ob += 8 * 4 * kGW) {
                     float rb_[8], rg_[8], rbe_[8];
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
@@ -809,7 +844,8 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                 const int fin = L.fin;
                 for (int job = 0; job < (L.src >= 0 ? 2 : 1); ++job) {
                     if (g.dbg & (job ? 4 : 2)) continue;
-                    const float *ga = job ? dzr : dzc, *gb = job ? base + L.wt : xc;
+                    const float *ga = job ? (outl ? base + L.dy : dzr) : (outl ? base + L.dyc : dzc);
+                    const float *gb = job ? base + L.wt : xc;
                     const int lda = job ? F : bp, ldb = job ? F : bp;
                     const int M = job ? bsz : F, K = job ? F : bsz;
                     float *dst = job ? base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy) : G + L.w;
@@ -1093,6 +1129,13 @@ int plan_graph(const agx_ppo_graph *net, int64_t batch, GArgs &a) {
             L.wt = off;
             off = r4(off + (long long)x.fin * x.fout);
         }
+        L.dyc = -1;
+        if (l == net->actor_out) {  // the value layer's (width 1) row- and feature-major forms coincide
+            L.dyc = off;
+            off = r4(off + (long long)x.fout * bp);
+        } else if (l == net->critic_out) {
+            L.dyc = L.dy;
+        }
     }
     a.oc = off;
     off = r4(off + (long long)net->obs_dim * bp);
@@ -1129,7 +1172,7 @@ long long act_plan(const GArgs &full, GActArgs &a) {
         GLay &L = a.L[l];
         L.yr = off;
         off = r4(off + (long long)kActRows * L.fout);
-        L.yc = L.xh = L.rs = L.dy = L.dy2 = L.wt = -1;
+        L.yc = L.xh = L.rs = L.dy = L.dy2 = L.wt = L.dyc = -1;
     }
     a.nl = full.nl;
     a.aout = full.aout;
