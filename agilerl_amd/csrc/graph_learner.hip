@@ -58,12 +58,14 @@ struct GLay {
     // transposed weight
     long long yr, yc, xh, rs, dy, dy2, wt;
     long long dyc;  // output layers: d(output) feature-major, written by the loss pass (-1 otherwise)
+    int fuse;       // this layer's dX GEMM runs its source's LayerNorm / ReLU backward in the epilogue
+    int fused;      // this layer's dZ (and column partials) come from its consumer's dX epilogue
 };
 
 struct GArgs {
     GLay L[kGL];
     int nl, aout, cout, A, D, n, cstart, bp;
-    long long oc, dzr, dzc, t1, t2, gr, ws_agent;
+    long long oc, dzr, dzc, dzr1, dzc1, t1, t2, gr, ws_agent;  // dZ buffers by layer parity
     float *ws;
     float *params, *m, *v;
     const float *lr;
@@ -130,20 +132,27 @@ constexpr int kGemmLds = 2 * kPanel;        // double-buffered
 // over the wave's tiles plus one DPP row reduction over the 16 column lanes:
 // no separate row pass, no re-read of the pre-activations.  L / base / pr / bp
 // describe the layer's outputs (as fwd_rows).
-template <bool LNE = false, class FE>
+// MODE 2: the dX GEMM of a layer whose source S = L (passed as L) is at most
+// kBN wide: the epilogue runs S's ReLU / LayerNorm(+affine) backward on the
+// whole rows of dY it holds and writes S's dZ (dzr_s / dzc_s) and per-wave
+// bias / LN-affine column partials (colp_s): S needs no row pass of its own.
+template <int MODE = 0, class FE>
 __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B, int ldb, int M, int N, int K,
                                         float *lds, const float *bias, FE epi, const GLay &L,
-                                        float *base = nullptr, const float *pr = nullptr, int bp = 0) {
+                                        float *base = nullptr, const float *pr = nullptr, int bp = 0,
+                                        float *dzr_s = nullptr, float *dzc_s = nullptr, float *colp_s = nullptr) {
+    constexpr bool LNE = MODE == 1, ROWS = MODE != 0;  // ROWS: each wave owns whole rows
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, q = lane >> 4;
     const int lr = tid / kKC, lk = tid % kKC;  // staging: rows lr + kRS i, column lk
+    float cb[4] = {0.f, 0.f, 0.f, 0.f}, cg[4] = {0.f, 0.f, 0.f, 0.f}, cbe[4] = {0.f, 0.f, 0.f, 0.f};
     for (int mb = 0; mb < M; mb += kBM)
         for (int nb = 0; nb < N; nb += kBN) {
             const int BM = M - mb < kBM ? M - mb : kBM, BN = N - nb < kBN ? N - nb : kBN;
             const int mtn = (BM + 15) >> 4, ntn = (BN + 15) >> 4, T = mtn * ntn;
             // slot j of this wave -> tile (m0, n0), valid (wave-uniform)
             auto tile = [&](int j, int &m0, int &n0) -> bool {
-                if constexpr (LNE) {
+                if constexpr (ROWS) {
                     const int mt = wave + kGW * (j >> 2), nt = j & 3;
                     m0 = mt << 4;
                     n0 = nt << 4;
@@ -276,6 +285,74 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                         }
                     }
                 }
+            } else if constexpr (MODE == 2) {
+                const float invF = 1.f / (float)N;
+                // every load of the epilogue before its first store: the LN affine of
+                // the lane's columns, each row's rstd and the lane's xhat (or y)
+                float ga_[4], be_[4];
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) {
+                    const int n = (nt < ntn && (nt << 4) + r < BN) ? (nt << 4) + r : 0;
+                    const float gv = pr[L.ln == 2 ? L.g + n : 0], bb = pr[L.ln == 2 ? L.be + n : 0];
+                    ga_[nt] = L.ln == 2 ? gv : 1.f;
+                    be_[nt] = L.ln == 2 ? bb : 0.f;
+                }
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    if (wave + kGW * a >= mtn) break;  // wave-uniform
+                    // the m-tile's loads (16 rows of xhat or y, their rstd) ahead of its stores
+                    float xv[4][4], rsv[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = mb + ((wave + kGW * a) << 4) + 4 * q + i;
+                        const bool rok = row < M;
+                        const float rv = base[L.ln && rok ? L.rs + row : 0];
+                        rsv[i] = L.ln ? rv : 1.f;
+#pragma unroll
+                        for (int nt = 0; nt < 4; ++nt) {
+                            const int n = (nt << 4) + r;
+                            const bool on = rok && nt < ntn && n < BN;
+                            const size_t o = on ? (size_t)row * N + n : 0;
+                            const float x = base[L.ln ? L.xh + o : (L.relu ? L.yr + o : 0)];
+                            xv[i][nt] = on ? x : 0.f;
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = mb + ((wave + kGW * a) << 4) + 4 * q + i;
+                        float dp[4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                        for (int nt = 0; nt < 4; ++nt) {
+                            const bool on = nt < ntn && (nt << 4) + r < BN && row < M;
+                            const float x = xv[i][nt];
+                            const float pre = L.ln == 2 ? x * ga_[nt] + be_[nt] : x;
+                            dp[nt] = (on && (!L.relu || pre > 0.f)) ? acc[4 * a + nt][i] : 0.f;
+                            const float dx = dp[nt] * ga_[nt];
+                            s1 += dx;
+                            s2 += dx * x;
+                        }
+                        float m1 = 0.f, m2 = 0.f;
+                        if (L.ln) {
+                            m1 = rsum16(s1) * invF;
+                            m2 = rsum16(s2) * invF;
+                        }
+                        if (row < M) {
+#pragma unroll
+                            for (int nt = 0; nt < 4; ++nt) {
+                                const int n = (nt << 4) + r;
+                                if (nt < ntn && n < BN) {
+                                    const float x = xv[i][nt];
+                                    const float dz = L.ln ? rsv[i] * (dp[nt] * ga_[nt] - m1 - x * m2) : dp[nt];
+                                    dzr_s[(size_t)row * N + n] = dz;
+                                    dzc_s[(size_t)n * bp + row] = dz;
+                                    cb[nt] += dz;
+                                    cg[nt] += dp[nt] * x;
+                                    cbe[nt] += dp[nt];
+                                }
+                            }
+                        }
+                    }
+                }
             } else {
 #pragma unroll
                 for (int j = 0; j < kTPW; ++j) {
@@ -290,6 +367,30 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 }
             }
         }
+    if constexpr (MODE == 2) {
+        // the wave's four row groups (lanes l, l ^ 16, l ^ 32, l ^ 48), then per
+        // wave into colp_s (the caller sums the waves in order)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            cb[nt] += __shfl_xor(cb[nt], 16, 64);
+            cb[nt] += __shfl_xor(cb[nt], 32, 64);
+            cg[nt] += __shfl_xor(cg[nt], 16, 64);
+            cg[nt] += __shfl_xor(cg[nt], 32, 64);
+            cbe[nt] += __shfl_xor(cbe[nt], 16, 64);
+            cbe[nt] += __shfl_xor(cbe[nt], 32, 64);
+        }
+        if (q == 0) {
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const int n = (nt << 4) + r;
+                if (n < N) {
+                    colp_s[wave * N + n] = cb[nt];
+                    colp_s[(kGW + wave) * N + n] = cg[nt];
+                    colp_s[(2 * kGW + wave) * N + n] = cbe[nt];
+                }
+            }
+        }
+    }
 }
 
 // fixed-order workgroup sum of two per-thread values
@@ -579,7 +680,7 @@ __device__ __forceinline__ void forward_layers(const GLay *Ls, int nl, const flo
         const bool lne = F <= kBN && (L.ln || L.relu);  // LayerNorm / ReLU in the GEMM epilogue
         if (!(dbg & 1)) {
             if (lne)
-                gemm_nt<true>(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
+                gemm_nt<1>(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
                               [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; }, L, base, pr, bp);
             else
                 gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
@@ -596,7 +697,7 @@ __device__ __forceinline__ void forward_layers(const GLay *Ls, int nl, const flo
 __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
     __shared__ float red[2 * kGW];
     __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
-    __shared__ float colp[3 * kGW * 128];  // per-wave bias / LN-affine column partials (F <= 128)
+    __shared__ float colp[2 * 3 * kGW * 128];  // per-wave bias / LN-affine column partials (F <= 128), by layer parity
     __shared__ float colo[kGW * 33];       // per-wave output-layer bias partials (32 logits + the value)
     if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const int p = blockIdx.x;
@@ -774,27 +875,30 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
             }
 
             // ---- backward, layer by layer (reverse) ----------------------------
-            float *dzr = base + g.dzr, *dzc = base + g.dzc, *t1c = base + g.t1, *t2c = base + g.t2;
+            float *t1c = base + g.t1, *t2c = base + g.t2;
             for (int l = g.nl - 1; l >= 0; --l) {
                 const GLay &L = g.L[l];
                 const int F = L.fout;
-                // output layers: the loss pass wrote dZ in both layouts and the bias gradient
+                float *dzr = base + ((l & 1) ? g.dzr1 : g.dzr), *dzc = base + ((l & 1) ? g.dzc1 : g.dzc);
+                float *colp_l = colp + (l & 1) * 3 * kGW * 128;
+                // output layers: the loss pass wrote dZ in both layouts and the bias gradient;
+                // fused layers: the consumer's dX epilogue wrote dZ and the column partials
                 const bool outl = L.dyc >= 0;
                 // dY -> dZ through ReLU and LayerNorm(+affine)
-                if (!(g.dbg & 8) && !outl) {
-                    if (F <= 128) bwd_rows<8>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c, colp);
+                if (!(g.dbg & 8) && !outl && !L.fused) {
+                    if (F <= 128) bwd_rows<8>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c, colp_l);
                     else bwd_rows<0>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
                 }
-                if (!outl) __syncthreads();
+                if (!outl && !L.fused) __syncthreads();
                 // bias / LN-affine gradients: column sums over the rows (fixed order);
                 // up to 8 feature groups summed before the first store
                 if (F <= 128 && !(g.dbg & 24) && !outl) {  // the row pass left per-wave partials in LDS
                     for (int o = tid; o < F; o += kGT) {
                         float sb = 0.f, sg = 0.f, sbe = 0.f;
                         for (int w = 0; w < kGW; ++w) {
-                            sb += colp[w * F + o];
-                            sg += colp[(kGW + w) * F + o];
-                            sbe += colp[(2 * kGW + w) * F + o];
+                            sb += colp_l[w * F + o];
+                            sg += colp_l[(kGW + w) * F + o];
+                            sbe += colp_l[(2 * kGW + w) * F + o];
                         }
                         G[L.b + o] = sb;
                         if (L.ln == 2) {
@@ -849,8 +953,15 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                     const int lda = job ? F : bp, ldb = job ? F : bp;
                     const int M = job ? bsz : F, K = job ? F : bsz;
                     float *dst = job ? base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy) : G + L.w;
-                    gemm_nt(ga, lda, gb, ldb, M, fin, K, lds, nullptr,
-                            [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; }, L);
+                    if (job && L.fuse) {  // the source's dZ (other parity) from the epilogue
+                        const int s_ = L.src;
+                        gemm_nt<2>(ga, lda, gb, ldb, M, fin, K, lds, nullptr, [](int, int, float) {}, g.L[s_], base, pr,
+                                   bp, base + ((s_ & 1) ? g.dzr1 : g.dzr), base + ((s_ & 1) ? g.dzc1 : g.dzc),
+                                   colp + (s_ & 1) * 3 * kGW * 128);
+                    } else {
+                        gemm_nt(ga, lda, gb, ldb, M, fin, K, lds, nullptr,
+                                [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; }, L);
+                    }
                 }
                 __syncthreads();
             }
@@ -1143,6 +1254,24 @@ int plan_graph(const agx_ppo_graph *net, int64_t batch, GArgs &a) {
     off = r4(off + bp * maxw);
     a.dzc = off;
     off = r4(off + bp * maxw);
+    a.dzr1 = off;
+    off = r4(off + bp * maxw);
+    a.dzc1 = off;
+    off = r4(off + bp * maxw);
+    // backward fusion: a layer whose only consumer is the next layer, at most
+    // kBN wide with a LayerNorm / ReLU, gets its dZ from that consumer's dX
+    // epilogue (dZ buffers alternate by layer parity, so the consumer's own dZ
+    // and its source's never share one)
+    for (int l = 0; l < nl; ++l) {
+        a.L[l].fuse = a.L[l].fused = 0;
+    }
+    for (int l = 1; l < nl; ++l) {
+        const agx_ppo_layer &x = net->layers[l], &sx = net->layers[l - 1];
+        if (x.src == l - 1 && consumers[l - 1] == 1 && sx.fout <= kBN && (sx.ln || sx.relu)) {
+            a.L[l].fuse = 1;
+            a.L[l - 1].fused = 1;
+        }
+    }
     a.t1 = off;
     off = r4(off + bp * maxw);
     a.t2 = off;
@@ -1173,6 +1302,7 @@ long long act_plan(const GArgs &full, GActArgs &a) {
         L.yr = off;
         off = r4(off + (long long)kActRows * L.fout);
         L.yc = L.xh = L.rs = L.dy = L.dy2 = L.wt = L.dyc = -1;
+        L.fuse = L.fused = 0;
     }
     a.nl = full.nl;
     a.aout = full.aout;
