@@ -592,3 +592,40 @@ def test_train_off_policy_with_dqn_yaml_mutations(algo):
         assert torch.isfinite(a.actor(x)).all()
         # the target network tracks the (possibly reshaped) online network
         assert [p.shape for p in a.actor.parameters()] == [p.shape for p in a.actor_target.parameters()]
+
+
+def test_config1_cartpole_dqn_population_of_one():
+    """Config 1's shape (CartPole DQN, pop_size 1, 4 sync vec envs; dqn.yaml's
+    INIT_HP, NET_CONFIG and MUTATION_PARAMS) through train_off_policy: the
+    reference runs it on the CPU; here it runs on the GPU kernels (DESIGN §1:
+    no CPU fallback).  Properties: fitness finite every generation, the agent
+    stepped max_steps, the replay filled, epsilon decayed, the network moved."""
+    from agilerl_amd.components import ReplayBuffer
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.hpo.mutation import Mutations
+    from agilerl_amd.hpo.tournament import TournamentSelection
+    from agilerl_amd.training import train_off_policy
+    from agilerl_amd.utils import create_population
+
+    env = SyntheticVecEnv(4, obs_dim=4, n_actions=2, seed=11, p_done=1 / 25, max_episode_steps=500)
+    INIT_HP = {"BATCH_SIZE": 128, "LR": 6.3e-4, "LEARN_STEP": 4, "GAMMA": 0.99, "TAU": 1e-3, "DOUBLE": False,
+               "EPS_START": 1.0, "EPS_END": 0.1, "EPS_DECAY": 0.99}
+    net_config = {"latent_dim": 128, "encoder_config": {"hidden_size": [256]}, "head_config": {"hidden_size": [256]}}
+    torch.manual_seed(1)
+    np.random.seed(1)
+    pop = create_population("DQN", net_config, INIT_HP, env.single_observation_space, env.single_action_space,
+                            population_size=1)
+    mut = Mutations(no_mutation=0.4, architecture=0.2, new_layer_prob=0.2, parameters=0.2, activation=0.2,
+                    rl_hp=0.2, mutation_sd=0.1, rand_seed=42)
+    memory = ReplayBuffer(50000)
+    p0 = [p.detach().clone() for p in pop[0].actor.parameters()]
+    pop, fits = train_off_policy(env, "CartPoleSynthetic", "DQN", pop, memory, INIT_HP=INIT_HP, max_steps=2000,
+                                 evo_steps=1000, eval_steps=100, eval_loop=1, eps_start=1.0, eps_end=0.1,
+                                 eps_decay=0.99, tournament=TournamentSelection(2, True, 1, 1), mutation=mut,
+                                 verbose=False)
+    assert len(fits) == 2 and all(len(f) == 1 and np.isfinite(f[0]) for f in fits)
+    assert pop[0].steps[-1] >= 2000 and len(memory) >= 1900
+    params = list(pop[0].actor.parameters())
+    assert all(torch.isfinite(p).all() for p in params)
+    assert [tuple(p.shape) for p in params] != [tuple(p.shape) for p in p0] or \
+        any(not torch.equal(a, b) for a, b in zip(p0, params))
