@@ -35,6 +35,8 @@ learned in groups of equal settings.
 
 from __future__ import annotations
 
+import warnings
+
 import numpy as np
 import torch
 from torch import nn
@@ -126,7 +128,11 @@ class RainbowPopulationLearner:
                                      device=self.device)
         self.offsets = torch.tensor([0, n], dtype=torch.int64)
         # stacked leaf views ([P, *shape]) of the online parameters, their
-        # gradients accumulating in place into the flat gradient rows
+        # gradients accumulating in place into the flat gradient rows.  The
+        # leaves are strided row views by design, so autograd's "gradient layout
+        # contract" notice (AccumulateGrad adds into the preset strided .grad in
+        # place; no copy) is expected here and silenced for this message only
+        warnings.filterwarnings("ignore", message="grad and param do not obey the gradient layout contract")
         self.leaf: dict[str, torch.Tensor] = {}
         for k in self.pnames:
             t = self.prm.view(k).detach().requires_grad_(True)
