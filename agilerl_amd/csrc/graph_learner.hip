@@ -11,16 +11,18 @@
 //     of PPO.learn (ppo.py:836-920) in one launch, like agx_ppo_learn;
 //   * a minibatch is processed layer by layer over all its rows: every Linear
 //     (forward, dW, dX) is ONE operand form, C = A . B^T with both operands
-//     contiguous along the contraction, on f32 MFMA 16x16x4 tiles read
-//     straight from the agent's L2-resident scratch.  The layouts that make
-//     that true are written where the data is produced: the row passes write
-//     each activation row-major (the next layer's forward) AND feature-major
-//     (the next layer's dW contracts over rows), and Adam writes every weight
-//     both as nn.Linear [out][in] (forward) and transposed (dX);
-//   * LayerNorm / ReLU forward and backward and the PPO loss are row passes,
-//     16 lanes per row (DPP row reductions); bias and LN-affine gradients are
-//     column passes over the feature-major buffers: every sum runs in one
-//     fixed order (an agent's update does not depend on its population);
+//     contiguous along the contraction, on f32 MFMA 16x16x4 tiles whose
+//     operand panels are staged through LDS from the agent's L2-resident
+//     scratch.  The layouts that make that true are written where the data is
+//     produced: activations row-major (the next layer's forward) AND
+//     feature-major (the next layer's dW contracts over rows), and Adam writes
+//     every weight both as nn.Linear [out][in] (forward) and transposed (dX);
+//   * LayerNorm / ReLU forward runs in the forward GEMM's epilogue for layers
+//     up to 64 wide (each wave owns whole rows), its backward in the
+//     consumer's dX epilogue for single-consumer layers; wider / shared layers
+//     and the PPO loss are row passes, 16 lanes per row (DPP row reductions);
+//     bias and LN-affine gradients are per-wave partials summed in one fixed
+//     order (an agent's update does not depend on its population);
 //   * two-group gradient-norm clip (ppo.py:910-911) and Adam
 //     (optimizer_wrapper.py:444-452) over the flat gradient row.
 #include <cmath>
