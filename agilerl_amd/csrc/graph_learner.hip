@@ -206,6 +206,7 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 bv_[j] = v;
             }
             fetch(0);
+            if (mb | nb) __syncthreads();  // the previous block's last panels may still be read
             commit(0);
             __syncthreads();
             int buf = 0;
@@ -228,8 +229,12 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                             acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc[j], 0, 0, 0);
                     }
                 }
-                if (more) commit(buf ^ 1);
-                __syncthreads();
+                // the last chunk needs no barrier: the epilogue touches no panel, and
+                // every caller separates two GEMMs by a workgroup barrier
+                if (more) {
+                    commit(buf ^ 1);
+                    __syncthreads();
+                }
                 buf ^= 1;
             }
             if constexpr (LNE) {
@@ -949,6 +954,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
                 const float *xc = L.src < 0 ? base + g.oc : base + g.L[L.src].yc;
                 const int fin = L.fin;
                 for (int job = 0; job < (L.src >= 0 ? 2 : 1); ++job) {
+                    if (job) __syncthreads();  // the dW GEMM's last panels are still being read
                     if (g.dbg & (job ? 4 : 2)) continue;
                     const float *ga = job ? (outl ? base + L.dy : dzr) : (outl ? base + L.dyc : dzc);
                     const float *gb = job ? base + L.wt : xc;

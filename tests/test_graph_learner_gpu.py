@@ -117,7 +117,8 @@ def test_graph_learner_single_update_tight(shape):
 
 @pytest.mark.parametrize("shape,N,learn_step,batch,epochs", [
     ("latent_56", 16, 128, 64, 2), ("enc_80_two_head_layers", 8, 100, 32, 2), ("deep_encoder", 16, 400, 128, 1),
-    ("wide_500", 16, 128, 48, 1), ("no_layer_norm", 16, 256, 64, 2), ("own_critic_encoder", 16, 128, 64, 2)])
+    ("wide_500", 16, 128, 48, 1), ("no_layer_norm", 16, 256, 64, 2), ("own_critic_encoder", 16, 128, 64, 2),
+    ("latent_56", 16, 512, 256, 1), ("wide_500", 16, 256, 200, 1)])  # > 128 rows: several GEMM row blocks
 def test_graph_learner_matches_torch_learner(shape, N, learn_step, batch, epochs):
     pop = _pop(shape, N=N, learn_step=learn_step, batch=batch, epochs=epochs)
     _compare(pop, pop.permutations())
