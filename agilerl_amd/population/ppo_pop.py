@@ -531,14 +531,21 @@ class PPOPopulation:
 
     def _draw_numpy_perms(self, out: np.ndarray) -> None:
         """[E, P, S] from the global numpy stream: this shard's agents' shuffles
-        in the global agent order (rng.py)."""
+        in the global agent order (rng.py).  An agent with fewer epochs than E
+        draws fewer shuffles; its rows beyond get arange(S), so no row of the
+        (reused, uninitialised pinned) buffer ever holds an out-of-range index
+        — the gather prologue and the PyTorch learner index with every row."""
         if self.global_P == self.P:
             numpy_shuffle_perms(self.P, self.update_epochs, self.S, out=out,
                                 epochs_per_agent=self.agent_epochs if self.heterogeneous else None)
-            return
-        eg = list(self.global_epochs)
-        eg[self.agent_offset:self.agent_offset + self.P] = self.agent_epochs
-        numpy_shuffle_perms_shard(out, self.agent_offset, self.global_P, eg, self._shard_scratch)
+        else:
+            eg = list(self.global_epochs)
+            eg[self.agent_offset:self.agent_offset + self.P] = self.agent_epochs
+            numpy_shuffle_perms_shard(out, self.agent_offset, self.global_P, eg, self._shard_scratch)
+        E = out.shape[0]
+        for p, e in enumerate(self.agent_epochs):
+            if e < E:
+                out[e:, p, :] = np.arange(self.S, dtype=np.int64)
 
     def _host_perm_buffer(self) -> torch.Tensor:
         """One of two pinned [E, P, S] int64 host buffers, alternating (the H2D

@@ -260,3 +260,27 @@ def test_architecture_mutation_cnn_q_networks(algo):
         assert all(torch.equal(t[k], v) for k, v in after.items())
         assert all(p is q for p, q in zip(agent.optimizer.param_groups[0]["params"], agent.actor.parameters()))
     assert any(m.startswith("encoder.") for m in seen) and changed >= 4, (seen, changed)
+
+
+def test_heterogeneous_epoch_permutation_rows_stay_in_range():
+    """An agent with fewer update_epochs than the population maximum draws
+    fewer shuffles; its remaining rows of the (reused, uninitialised) host
+    buffer must still be valid indices: the gather prologue and the PyTorch
+    learner index with every row.  They get arange(S)."""
+    import numpy as np
+
+    from types import SimpleNamespace
+
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+
+    # the host-side state _draw_numpy_perms reads (a population of 3, S = 32,
+    # agent 1 mutated to 1 update epoch)
+    pop = SimpleNamespace(P=3, global_P=3, S=32, update_epochs=3, agent_epochs=[3, 1, 3], heterogeneous=True)
+    out = np.full((3, 3, pop.S), -7, dtype=np.int64)  # garbage a reused buffer may hold
+    np.random.seed(0)
+    PPOPopulation._draw_numpy_perms(pop, out)
+    assert out.min() >= 0 and out.max() < pop.S
+    assert np.array_equal(out[1:, 1], np.tile(np.arange(pop.S), (2, 1)))
+    for e in range(3):
+        for p in (0, 2):
+            assert sorted(out[e, p]) == list(range(pop.S))
