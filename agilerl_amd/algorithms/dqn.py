@@ -21,6 +21,7 @@ import torch
 from .. import kernels as K
 from . import checkpoint as C
 from .evolvable import EvolvableAgentMixin
+from .flat_state import flat_state
 from ..networks import QNetwork, RainbowQNetwork
 from ..networks.base import image_norm_bounds, is_image_space, mlp_net_config
 
@@ -144,7 +145,9 @@ class DQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
                              float(self.gamma), bool(self.double))
         self.optimizer.zero_grad()
         loss.backward()
-        self.optimizer.step()
+        fs = flat_state(self)
+        if fs is None or not fs.step(0.0):  # Adam over the flat buffers: one launch (flat_state.py)
+            self.optimizer.step()
         return loss.detach()
 
     def learn(self, experiences) -> float:
@@ -171,8 +174,13 @@ class DQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
 
     @torch.no_grad()
     def soft_update(self) -> None:
-        """target <- tau * online + (1 - tau) * target (dqn.py:349-358), one
-        agx_polyak launch per parameter tensor."""
+        """target <- tau * online + (1 - tau) * target (dqn.py:349-358): one
+        agx_polyak launch over the flat buffers (flat_state.py), else one per
+        parameter tensor."""
+        fs = flat_state(self)
+        if fs is not None:
+            fs.polyak(self.tau)
+            return
         for t, o in zip(self.actor_target.parameters(), self.actor.parameters()):
             K.polyak_(t.data.view(-1), o.data.reshape(-1), float(self.tau))
 
@@ -373,9 +381,13 @@ class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
             loss = torch.mean(el)
         self.optimizer.zero_grad()
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(self.actor.parameters(), 10.0)
-        self.optimizer.step()
-        self.soft_update()
+        fs = flat_state(self)
+        if fs is not None and fs.step(10.0):  # clip_grad_norm_(10) + Adam: one launch (flat_state.py)
+            fs.polyak(self.tau)
+        else:
+            torch.nn.utils.clip_grad_norm_(self.actor.parameters(), 10.0)
+            self.optimizer.step()
+            self.soft_update()
         self.actor.reset_noise()
         self.actor_target.reset_noise()
         if per:
@@ -396,5 +408,9 @@ class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
 
     @torch.no_grad()
     def soft_update(self) -> None:
+        fs = flat_state(self)
+        if fs is not None:
+            fs.polyak(self.tau)
+            return
         for t, o in zip(self.actor_target.parameters(), self.actor.parameters()):
             K.polyak_(t.data.view(-1), o.data.reshape(-1), float(self.tau))

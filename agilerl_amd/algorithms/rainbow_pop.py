@@ -171,6 +171,9 @@ class RainbowPopulationLearner:
                               "exp_avg": self.prm.row_view(p, k, self.m),
                               "exp_avg_sq": self.prm.row_view(p, k, self.v)}
         self.steps[p] = step
+        # the agent's own flat learner state (flat_state.py) stands aside while its
+        # tensors are rows here
+        a.__dict__["_pop_rows_ptr"] = next(iter(a.actor.parameters())).data_ptr()
 
     def sync_optimizers(self) -> None:
         """Write the device step counts into the agents' torch Adam states

@@ -9,6 +9,8 @@
 //   p -= (lr / (1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
 // clip: coef = max_norm / (||g||_2 + 1e-6), g *= min(coef, 1).
 // Polyak: agilerl/algorithms/dqn.py:349-358 — t = tau*o + (1-tau)*t.
+// Noise reset: NoisyLinear.reset_noise (agilerl/modules/custom_components.py:
+// 116-131) for every noisy layer of a network in one launch.
 //
 // Two launches: (1) per-(agent, 8192-element chunk) partial sums of squares
 // per group into the workspace, (2) every 1024-element block re-reduces its
@@ -245,9 +247,60 @@ __global__ void polyak_kernel(float *__restrict__ t, const float *__restrict__ o
         t[i] = tau * o[i] + (1.0f - tau) * t[i];
 }
 
+// NoisyLinear.reset_noise over up to kMaxNoisy layers (custom_components.py:
+// 116-131): from the layer's two N(0,1) draws, f(x) = sign(x) * sqrt(|x|)
+// (torch's sign: (0 < x) - (x < 0); correctly rounded sqrt, as torch's),
+// weight_epsilon[o][i] = f(out_o) * f(in_i) (eps_out.ger(eps_in)),
+// bias_epsilon[o] = f(out_o).  blockIdx.y = layer; grid-stride over the
+// layer's out*in + out outputs.
+constexpr int kMaxNoisy = 16;
+struct NoisySet {
+    agx_noisy_layer l[kMaxNoisy];
+};
+
+__device__ __forceinline__ float scale_noise(float x) {
+    const float s = (float)((0.0f < x) - (x < 0.0f));
+    return s * sqrtf(fabsf(x));  // llvm.sqrt.f32: correctly rounded (__fsqrt_rn is the native approximation here)
+}
+
+__global__ __launch_bounds__(256) void noisy_reset_kernel(NoisySet set) {
+    const agx_noisy_layer &L = set.l[blockIdx.y];
+    const int64_t nin = L.in_features, nout = L.out_features, nw = nin * nout;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nw + nout;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        if (e < nw) {
+            const int64_t o = e / nin, i = e - o * nin;
+            L.weight_epsilon[e] = scale_noise(L.eps_out[o]) * scale_noise(L.eps_in[i]);
+        } else {
+            L.bias_epsilon[e - nw] = scale_noise(L.eps_out[e - nw]);
+        }
+    }
+}
+
 }  // namespace agx
 
 using namespace agx;
+
+extern "C" int agx_noisy_reset(const agx_noisy_layer *layers, int n_layers, void *stream) {
+    AGX_REQUIRE(layers && n_layers >= 0 && n_layers <= kMaxNoisy, "agx_noisy_reset: bad layer list (n=%d, max %d)",
+                n_layers, kMaxNoisy);
+    if (n_layers == 0) return AGX_OK;
+    NoisySet set;
+    int64_t most = 0;
+    for (int k = 0; k < n_layers; ++k) {
+        const agx_noisy_layer &L = layers[k];
+        AGX_REQUIRE(L.eps_in && L.eps_out && L.weight_epsilon && L.bias_epsilon && L.in_features > 0 &&
+                        L.out_features > 0,
+                    "agx_noisy_reset: layer %d: bad arguments", k);
+        set.l[k] = L;
+        const int64_t n = L.in_features * L.out_features + L.out_features;
+        most = n > most ? n : most;
+    }
+    const int64_t blocks = ceil_div(most, 256);
+    noisy_reset_kernel<<<dim3((unsigned)(blocks > 1024 ? 1024 : blocks), (unsigned)n_layers), 256, 0,
+                         as_stream(stream)>>>(set);
+    return check_launch("agx_noisy_reset");
+}
 
 extern "C" size_t agx_adam_workspace_bytes(int64_t P, int64_t n) {
     // partials [P][nblk][8] f64, then clip coefficients [P][8] f32, then bias corrections [P][2] f32

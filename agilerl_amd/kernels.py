@@ -7,6 +7,8 @@ stream and returns without synchronising.  No CPU fallback exists.
 
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -329,6 +331,26 @@ class ClipAdam:
                   self.offsets.data_ptr(), len(self.offsets) - 1, float(self.max_norm),
                   self.lr.data_ptr(), float(self.betas[0]), float(self.betas[1]), float(self.eps),
                   self.steps.data_ptr(), _lib.ptr(active), self.workspace.data_ptr(), _lib.stream())
+
+
+class _NoisyLayer(ctypes.Structure):
+    _fields_ = [("eps_in", ctypes.c_void_p), ("eps_out", ctypes.c_void_p), ("weight_epsilon", ctypes.c_void_p),
+                ("bias_epsilon", ctypes.c_void_p), ("in_features", ctypes.c_int64), ("out_features", ctypes.c_int64)]
+
+
+def noisy_reset_(layers: list) -> None:
+    """agx_noisy_reset: ``layers`` = [(eps_in, eps_out, weight_epsilon,
+    bias_epsilon)] — each layer's two N(0, 1) draws and its epsilon buffers
+    (NoisyLinear.reset_noise, custom_components.py:116-131), one launch."""
+    arr = (_NoisyLayer * max(1, len(layers)))()
+    for k, (ei, eo, we, be) in enumerate(layers):
+        n_in, n_out = ei.numel(), eo.numel()
+        _need(ei, "eps_in", _f32)
+        _need(eo, "eps_out", _f32)
+        _need(we, "weight_epsilon", _f32, (n_out, n_in))
+        _need(be, "bias_epsilon", _f32, (n_out,))
+        arr[k] = _NoisyLayer(ei.data_ptr(), eo.data_ptr(), we.data_ptr(), be.data_ptr(), n_in, n_out)
+    _lib.call("agx_noisy_reset", ctypes.cast(arr, ctypes.c_void_p), len(layers), _lib.stream())
 
 
 def polyak_(target: torch.Tensor, online: torch.Tensor, tau: float) -> None:

@@ -21,6 +21,34 @@ class GumbelSoftmax(nn.Module):
         return self.gumbel_softmax(input)
 
 
+@torch.no_grad()
+def reset_noise_layers(layers: list) -> None:
+    """NoisyLinear.reset_noise of each layer in order (custom_components.py:
+    116-131).  Every layer's two torch.randn draws are made in the
+    reference's order; on the GPU the transform sign(x) sqrt(|x|), the outer
+    product and both epsilon writes of up to 16 layers are one agx_noisy_reset
+    launch (bit-identical to the torch ops: one correctly rounded sqrt and
+    one multiply per element)."""
+    if not layers:
+        return
+    if layers[0].weight_mu.device.type != "cuda":
+        for m in layers:
+            eps_in, eps_out = m._scale_noise(m.in_features), m._scale_noise(m.out_features)
+            m.weight_epsilon.copy_(eps_out.ger(eps_in))
+            m.bias_epsilon.copy_(eps_out)
+        return
+    from .. import kernels as K
+
+    for c in range(0, len(layers), 16):
+        batch = []
+        for m in layers[c:c + 16]:
+            dev = m.weight_mu.device
+            eps_in = torch.randn(m.in_features, device=dev)
+            eps_out = torch.randn(m.out_features, device=dev)
+            batch.append((eps_in, eps_out, m.weight_epsilon, m.bias_epsilon))
+        K.noisy_reset_(batch)
+
+
 class NoisyLinear(nn.Module):
     """Factorised-Gaussian noisy linear layer (custom_components.py:38-131):
     mu ~ U(+-1/sqrt(in)), sigma = std_init/sqrt(in) (weights) and
@@ -53,9 +81,7 @@ class NoisyLinear(nn.Module):
 
     @torch.no_grad()
     def reset_noise(self) -> None:
-        eps_in, eps_out = self._scale_noise(self.in_features), self._scale_noise(self.out_features)
-        self.weight_epsilon.copy_(eps_out.ger(eps_in))
-        self.bias_epsilon.copy_(eps_out)
+        reset_noise_layers([self])
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.training:

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 from torch import nn
 
-from .custom_components import GumbelSoftmax, NoisyLinear
+from .custom_components import GumbelSoftmax, NoisyLinear, reset_noise_layers
 
 
 class NewGELU(nn.Module):
@@ -168,9 +168,7 @@ class EvolvableMLP(nn.Module):
         return getattr(self.model, f"{self.name}_linear_layer_output")
 
     def reset_noise(self) -> None:
-        for m in self.modules():
-            if isinstance(m, NoisyLinear):
-                m.reset_noise()
+        reset_noise_layers([m for m in self.modules() if isinstance(m, NoisyLinear)])
 
     @staticmethod
     def _init_gaussian(module: nn.Module, std_coeff: float) -> None:

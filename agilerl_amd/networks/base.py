@@ -287,8 +287,6 @@ class EvolvableNetwork(nn.Module):
                 mod.change_activation(activation, output=True if name == "encoder" else output)
 
     def reset_noise(self) -> None:
-        from ..modules.custom_components import NoisyLinear
+        from ..modules.custom_components import NoisyLinear, reset_noise_layers
 
-        for m in self.modules():
-            if isinstance(m, NoisyLinear):
-                m.reset_noise()
+        reset_noise_layers([m for m in self.modules() if isinstance(m, NoisyLinear)])

@@ -417,6 +417,19 @@ int agx_clip_adam(float *params, float *grads, float *exp_avg, float *exp_avg_sq
 /* Polyak soft update target <- tau*online + (1-tau)*target
  * (dqn.py:349-358, dqn_rainbow.py:492-501). */
 int agx_polyak(float *target, const float *online, int64_t n, float tau, void *stream);
+/* NoisyLinear.reset_noise (agilerl/modules/custom_components.py:116-131) for
+ * up to 16 noisy layers of a network in one launch.  eps_in [in_features] and
+ * eps_out [out_features] are the layer's two torch.randn draws (the caller
+ * draws them in the reference's order); with f(x) = sign(x) * sqrt(|x|):
+ * weight_epsilon [out][in] = f(eps_out) outer f(eps_in), bias_epsilon = f(eps_out). */
+typedef struct agx_noisy_layer {
+    const float *eps_in;
+    const float *eps_out;
+    float *weight_epsilon;
+    float *bias_epsilon;
+    int64_t in_features, out_features;
+} agx_noisy_layer;
+int agx_noisy_reset(const agx_noisy_layer *layers, int n_layers, void *stream);
 
 /* ---- convolutional encoder (EvolvableCNN) -----------------------------------
  * Conv2d layers of agilerl/modules/cnn.py:224-552 (create_cnn,
