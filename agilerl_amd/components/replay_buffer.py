@@ -229,7 +229,9 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         """p = max(priority, 1e-5) ** alpha per index, in order (:411-428)."""
         idx = _to_tensor(indices, self.device).reshape(-1).to(torch.int64)
         pri = _to_tensor(priorities, self.device).reshape(-1).to(torch.float32)
-        if idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= self.max_size):
-            raise AssertionError("priority index out of range")
+        if idx.numel():
+            lo, hi = torch.stack(torch.aminmax(idx)).tolist()  # one device->host read
+            if lo < 0 or hi >= self.max_size:
+                raise AssertionError("priority index out of range")
         K.per_update(self.sum_tree.tree, self.min_tree.tree, self.tree_capacity, self.max_size, idx.contiguous(),
                      pri.contiguous(), self.alpha, self._max_priority, floor=1e-5, workspace=self._ws)

@@ -19,6 +19,7 @@ every GPU, a shard of an N x 8 population) is reported as an extra key.
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import os
 import sys
@@ -971,7 +972,7 @@ def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15):
     the P agents' samples in one draw (the same torch.rand stream as P
     draws), one batched learn, the P priority updates in agent order.  The
     per-agent loop of the reference (sample, agent.learn, update per agent)
-    is timed on the same agents beside it."""
+    is timed on copies of the same agents beside it."""
     from agilerl_amd.algorithms import RainbowDQN
     from agilerl_amd.algorithms.rainbow_pop import RainbowPopulationLearner
     from agilerl_amd.components import PrioritizedReplayBuffer
@@ -991,6 +992,10 @@ def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15):
                     "reward": torch.randn(n, device=dev, generator=g),
                     "next_obs": torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g),
                     "done": (torch.rand(n, device=dev, generator=g) < 0.02).float()})
+    # the per-agent leg runs on its own copies: the population learner takes the
+    # agents' tensors over as rows of its flat buffers, which the entry point's
+    # agents never are (their own learn keeps its flat state, flat_state.py)
+    solo = [copy.deepcopy(a) for a in agents]
     learner = RainbowPopulationLearner(agents)
 
     def batched():
@@ -1001,7 +1006,7 @@ def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15):
                                  np.concatenate([o[2].reshape(-1) for o in outs]))
 
     def per_agent():
-        for a in agents:
+        for a in solo:
             s = memory.sample(B, beta=0.4)
             _, idxs, pri = a.learn(s, per=True)
             memory.update_priorities(idxs, pri)
@@ -1025,7 +1030,7 @@ def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15):
     # sampling) is reported beside it as an extra, not as the config-3 number
     out["learner_updates_per_s"] = out["per_agent"]["learner_updates_per_s"]
     out["entry_point"] = "per_agent (train_off_policy); batched = algorithms/rainbow_pop.py, not on the entry point"
-    del learner, agents, memory
+    del learner, agents, solo, memory
     torch.cuda.empty_cache()
     return out
 
