@@ -52,6 +52,8 @@ SIGNATURES = {
     "agx_rollout_args_bytes": (_SZ, [_I]),
     "agx_ppo_rollout_persistent": (_INT, [_P, _I, _I, _P, _P, _I, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                           _P, _P, _D, _P]),
+    "agx_ppo_eval_persistent": (_INT, [_P, _I, _I, _P, _P, _P, _P, _P, _I, ctypes.c_uint32, ctypes.c_uint64,
+                                       ctypes.c_uint64, _P, _P, _D, _P]),
     "agx_host_alloc": (_P, [_SZ]),
     "agx_host_free": (_INT, [_P]),
     "agx_host_signal": (_INT, [_P, ctypes.c_uint32]),

@@ -50,8 +50,10 @@ class EvolvableAgentMixin:
             # a population sharded over ranks replays every global agent's draws
             # on every rank (hpo/shard.py RemoteAgent); the module and init draws
             # of a Q-network mutation are not replayed: not applied anywhere.
-            # (Ranks that each train a population of their own, create_population
-            # shard=False, mutate as a single process does.)
+            # The flag is set by create_population and, for agents built any
+            # other way, by the entry points' sharded mutation / selection
+            # steps (hpo/shard.py mark_sharded): the off-policy loops treat
+            # every multi-rank run as one population split over the ranks.
             return False
         from ..modules.cnn import EvolvableCNN
 

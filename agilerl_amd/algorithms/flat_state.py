@@ -33,8 +33,10 @@ def _plain_adam(opt) -> bool:
     if not isinstance(opt, torch.optim.Adam) or len(opt.param_groups) != 1:
         return False
     g = opt.param_groups[0]
+    # fused Adam keeps its 'step' tensors on the device; the flat state swaps
+    # in CPU step tensors, which a later torch step would then mix with device ones
     return not (g.get("amsgrad") or g.get("maximize") or g.get("weight_decay", 0.0) or g.get("capturable")
-                or g.get("differentiable"))
+                or g.get("differentiable") or g.get("fused"))
 
 
 class FlatLearnState:
@@ -142,9 +144,14 @@ def flat_state(agent) -> FlatLearnState | None:
     actor, target, opt = agent.actor, agent.actor_target, agent.optimizer
     if agent.device.type != "cuda" or not _plain_adam(opt):
         return None
-    owned = agent.__dict__.get("_pop_rows_ptr")  # rows of a RainbowPopulationLearner: it owns the tensors
-    if owned is not None and next(iter(actor.parameters())).data_ptr() == owned:
-        return None
+    # rows of a live RainbowPopulationLearner: it owns the tensors (a learner
+    # that was released, or tensors the agent has since replaced, do not count)
+    owned = agent.__dict__.get("_pop_rows")
+    if owned is not None:
+        learner, ptrs = owned[0](), owned[1]
+        if learner is not None and tuple(p.data_ptr() for p in actor.parameters()) == ptrs:
+            return None
+        agent.__dict__.pop("_pop_rows", None)
     fs = agent.__dict__.get("_flat")
     if fs is not None and fs.valid(actor, target, opt):
         return fs

@@ -36,6 +36,7 @@ learned in groups of equal settings.
 from __future__ import annotations
 
 import warnings
+import weakref
 
 import numpy as np
 import torch
@@ -72,6 +73,16 @@ class _Rows:
         b = self.data if buf is None else buf
         k = int(np.prod(shape)) if len(shape) else 1
         return b[p, off:off + k].view(shape)
+
+
+def _backward(loss: torch.Tensor) -> None:
+    """loss.backward() with autograd's gradient-layout notice silenced: the
+    stacked leaves are strided row views whose preset .grad is a strided view
+    of the flat gradient rows by design (AccumulateGrad adds into it in place,
+    no copy).  Scoped to this call, so the notice stays on for other modules."""
+    with warnings.catch_warnings():
+        warnings.filterwarnings("ignore", message="grad and param do not obey the gradient layout contract")
+        loss.backward()
 
 
 def _module_ops(net: nn.Module) -> list[tuple[str, nn.Module]]:
@@ -128,11 +139,9 @@ class RainbowPopulationLearner:
                                      device=self.device)
         self.offsets = torch.tensor([0, n], dtype=torch.int64)
         # stacked leaf views ([P, *shape]) of the online parameters, their
-        # gradients accumulating in place into the flat gradient rows.  The
-        # leaves are strided row views by design, so autograd's "gradient layout
-        # contract" notice (AccumulateGrad adds into the preset strided .grad in
-        # place; no copy) is expected here and silenced for this message only
-        warnings.filterwarnings("ignore", message="grad and param do not obey the gradient layout contract")
+        # gradients accumulating in place into the flat gradient rows (the
+        # layout-contract notice this raises is silenced around backward only,
+        # _backward)
         self.leaf: dict[str, torch.Tensor] = {}
         for k in self.pnames:
             t = self.prm.view(k).detach().requires_grad_(True)
@@ -173,7 +182,7 @@ class RainbowPopulationLearner:
         self.steps[p] = step
         # the agent's own flat learner state (flat_state.py) stands aside while its
         # tensors are rows here
-        a.__dict__["_pop_rows_ptr"] = next(iter(a.actor.parameters())).data_ptr()
+        a.__dict__["_pop_rows"] = (weakref.ref(self), tuple(q.data_ptr() for q in a.actor.parameters()))
 
     def sync_optimizers(self) -> None:
         """Write the device step counts into the agents' torch Adam states
@@ -308,7 +317,7 @@ class RainbowPopulationLearner:
         done = self._stack(experiences, "done").reshape(self.P, -1).float()
         self.grad.zero_()
         loss = self._td_losses(obs, acts, rew, done, next_obs, a0.gamma)
-        loss.sum().backward()
+        _backward(loss.sum())
         self._adam(0.0)
         K.polyak_(self.tgt.data.view(-1), self.prm.data.view(-1), float(a0.tau))
         return [float(x) for x in loss.detach().cpu().tolist()]
@@ -346,7 +355,7 @@ class RainbowPopulationLearner:
                 loss = (el * w.reshape(self.P, -1)).mean(1)
         else:
             loss = el.mean(1)
-        loss.sum().backward()
+        _backward(loss.sum())
         self._adam(10.0)
         K.polyak_(self.tgt.data.view(-1), self.prm.data.view(-1), float(a0.tau))
         for a in self.agents:  # the reference's per-agent noise draws, in agent order

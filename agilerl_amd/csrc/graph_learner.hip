@@ -41,7 +41,8 @@ __global__ void ppo_gather_kernel(const float *__restrict__ obs, const long long
                                   const double *__restrict__ adv_stats, const long long *__restrict__ perms,
                                   const unsigned char *__restrict__ masks, int A, long long S, int D, int P,
                                   float *__restrict__ gobs, int *__restrict__ gact, unsigned *__restrict__ gmask,
-                                  float *__restrict__ grow, unsigned *__restrict__ counters, int ncounters);
+                                  float *__restrict__ grow, unsigned *__restrict__ counters, int ncounters,
+                                  const int *__restrict__ epochs_p, unsigned *__restrict__ err);
 
 namespace {
 
@@ -1381,7 +1382,8 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
     ppo_gather_kernel<<<ggrid, 256, 0, s>>>(x->obs, reinterpret_cast<const long long *>(x->actions), x->old_logp,
                                             x->adv, x->ret, x->old_value, x->adv_stats,
                                             reinterpret_cast<const long long *>(x->perms), x->action_masks, a.A, S,
-                                            a.D, (int)P, gobs, gact, gmask, grow, nullptr, 0);
+                                            a.D, (int)P, gobs, gact, gmask, grow, nullptr, 0, x->epochs_per_agent,
+                                            x->error_word);
     const int rc2 = check_launch("agx_ppo_learn_graph gather");
     if (rc2) return rc2;
     a.ws = reinterpret_cast<float *>(ws + w.agents);

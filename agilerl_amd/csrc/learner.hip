@@ -1811,7 +1811,8 @@ __global__ void ppo_gather_kernel(const float *__restrict__ obs, const long long
                                   const unsigned char *__restrict__ masks, int A,
                                   long long S, int D, int P, float *__restrict__ gobs, int *__restrict__ gact,
                                   unsigned *__restrict__ gmask, float *__restrict__ grow,
-                                  unsigned *__restrict__ counters, int ncounters) {
+                                  unsigned *__restrict__ counters, int ncounters, const int *__restrict__ epochs_p,
+                                  unsigned *__restrict__ err) {
     const int ep = blockIdx.y;  // e * P + p
     const int p = ep % P;
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1820,7 +1821,17 @@ __global__ void ppo_gather_kernel(const float *__restrict__ obs, const long long
     if (blockIdx.x == 0 && blockIdx.y == 0)
         for (int i = threadIdx.x; i < ncounters; i += blockDim.x) counters[i] = 0u;
     if (j >= S) return;
-    const long long src = perms[(size_t)ep * S + j];
+    // epochs beyond an agent's own update_epochs: the learner never reads
+    // them, and their perms rows are not part of the contract (agx.h)
+    if (epochs_p && ep / P >= epochs_p[p]) return;
+    long long src = perms[(size_t)ep * S + j];
+    if (src < 0 || src >= S) {
+        // a host-side slip must not become a device fault: flag it in the
+        // caller's sticky error word (bit 2; PPOPopulation.check_errors raises
+        // AgxError) and gather row 0 in its place
+        if (err) __hip_atomic_fetch_or(err, AGX_LEARN_ERR_PERM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        src = 0;
+    }
     const size_t sp = (size_t)p * S + src;
     for (int d = 0; d < D; ++d) gobs[((size_t)ep * S + j) * D + d] = obs[sp * D + d];
     gact[(size_t)ep * S + j] = (int)act[sp];
@@ -2055,6 +2066,10 @@ __global__ __launch_bounds__(kNT, 1) void ppo_rollout_persistent_kernel(const Ac
                 if (v == AGX_ROLLOUT_ABORT) {  // host exception: the rollout is partial
                     go = 0;
                     __hip_atomic_store(&ctl->timeout, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                if (v == AGX_ROLLOUT_STOP) {  // clean early end (an evaluation whose episodes all finished)
+                    go = 0;
                     break;
                 }
                 if (v >= base + (unsigned)(t + 1)) break;
@@ -2361,7 +2376,7 @@ extern "C" int agx_ppo_learn(const agx_ppo_net *net, const agx_ppo_learn_args *x
                                             x->adv, x->ret, x->old_value, x->adv_stats,
                                             reinterpret_cast<const long long *>(x->perms), x->action_masks, pl.A, S,
                                             pl.D, (int)P, gobs, gact, gmask, grow, reinterpret_cast<unsigned *>(ws),
-                                            (int)(w.gobs / sizeof(unsigned)));
+                                            (int)(w.gobs / sizeof(unsigned)), x->epochs_per_agent, x->error_word);
     const int rc2 = check_launch("agx_ppo_learn gather");
     if (rc2) return rc2;
     LearnArgs a;
@@ -2535,29 +2550,74 @@ extern "C" size_t agx_rollout_ctl_bytes(int64_t P, int64_t N) {
 }
 extern "C" size_t agx_rollout_args_bytes(int64_t nsteps) { return (size_t)nsteps * sizeof(ActArgs); }
 
+static int persistent_fits(const Launcher &L, int64_t P, int64_t N, const char *who) {
+    const int64_t nwg = agx_rollout_workgroups(P, N);
+    const int64_t cap = (int64_t)L.persist_occupancy((size_t)L.plan->act_floats * sizeof(float)) * cu_count();
+    if (nwg > cap) {
+        set_error("%s: %lld workgroups cannot all be resident (the GPU holds %lld of this kernel at once); use "
+                  "per-step launches", who, (long long)nwg, (long long)cap);
+        return AGX_EUNSUPPORTED;
+    }
+    return AGX_OK;
+}
+
+extern "C" int agx_ppo_eval_persistent(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
+                                       const float *stage_obs, const uint8_t *stage_mask, int64_t *actions_flat,
+                                       const int64_t *agent_env_base, int64_t nsteps, uint32_t base, uint64_t seed,
+                                       uint64_t counter0, void *args_host, agx_rollout_ctl *ctl, double timeout_s,
+                                       void *stream) {
+    AGX_REQUIRE(net && params && stage_obs && actions_flat && args_host && ctl && P > 0 && N > 0 && P <= 65535 &&
+                    nsteps >= 1,
+                "agx_ppo_eval_persistent: bad arguments");
+    AGX_REQUIRE((uint64_t)base + (uint64_t)nsteps < AGX_ROLLOUT_STOP, "agx_ppo_eval_persistent: base wraps");
+    AGX_REQUIRE(timeout_s > 0 && timeout_s < 3600, "agx_ppo_eval_persistent: timeout_s out of range");
+    Launcher L;
+    if (!find_launcher(net, L)) {
+        set_error("agx_ppo_eval_persistent: network shape not instantiated");
+        return AGX_EUNSUPPORTED;
+    }
+    if (int rc = persistent_fits(L, P, N, "agx_ppo_eval_persistent")) return rc;
+    const LearnPlan &pl = *L.plan;
+    ActArgs *steps = static_cast<ActArgs *>(args_host);
+    for (int64_t t = 0; t < nsteps; ++t) {
+        ActArgs a{};
+        a.params = params;
+        a.obs = stage_obs;
+        a.obs_pstride = N * (int64_t)pl.D;
+        a.N = (int)N;
+        a.P = (int)P;
+        a.sample = 1;
+        a.seed = seed;
+        a.counter = counter0 + (uint64_t)t;
+        a.act_flat = reinterpret_cast<long long *>(actions_flat);
+        a.act = 1;
+        a.mask = stage_mask;
+        a.mask_pstride = N * (int64_t)pl.A;
+        a.env_base = reinterpret_cast<const long long *>(agent_env_base);
+        steps[t] = a;
+    }
+    const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    ctl->nwg = (uint32_t)agx_rollout_workgroups(P, N);
+    dim3 grid((unsigned)ceil_div(N, kSB), (unsigned)P);
+    L.persist(steps, (int)nsteps, ctl, ticks, base, nullptr, grid, (size_t)pl.act_floats * sizeof(float),
+              as_stream(stream));
+    return check_launch("agx_ppo_eval_persistent");
+}
+
 extern "C" int agx_ppo_rollout_persistent(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
                                           const agx_rollout_io *ios, int64_t nsteps, uint32_t base, uint64_t seed,
                                           uint64_t counter0, void *args_host, agx_rollout_ctl *ctl,
                                           double timeout_s, void *stream) {
     AGX_REQUIRE(net && ios && params && args_host && ctl && P > 0 && N > 0 && P <= 65535 && nsteps >= 1,
                 "agx_ppo_rollout_persistent: bad arguments");
-    AGX_REQUIRE((uint64_t)base + (uint64_t)nsteps < AGX_ROLLOUT_ABORT, "agx_ppo_rollout_persistent: base wraps");
+    AGX_REQUIRE((uint64_t)base + (uint64_t)nsteps < AGX_ROLLOUT_STOP, "agx_ppo_rollout_persistent: base wraps");
     AGX_REQUIRE(timeout_s > 0 && timeout_s < 3600, "agx_ppo_rollout_persistent: timeout_s out of range");
     Launcher L;
     if (!find_launcher(net, L)) {
         set_error("agx_ppo_rollout_persistent: network shape not instantiated");
         return AGX_EUNSUPPORTED;
     }
-    {
-        const int64_t nwg = agx_rollout_workgroups(P, N);
-        const int64_t cap = (int64_t)L.persist_occupancy((size_t)L.plan->act_floats * sizeof(float)) * cu_count();
-        if (nwg > cap) {
-            set_error("agx_ppo_rollout_persistent: %lld workgroups cannot all be resident (the GPU holds %lld of "
-                      "this kernel at once); use per-step launches (agx_ppo_rollout_step)",
-                      (long long)nwg, (long long)cap);
-            return AGX_EUNSUPPORTED;
-        }
-    }
+    if (int rc = persistent_fits(L, P, N, "agx_ppo_rollout_persistent")) return rc;
     ActArgs *steps = static_cast<ActArgs *>(args_host);
     for (int64_t t = 0; t < nsteps; ++t) {
         const bool last = t + 1 == nsteps;

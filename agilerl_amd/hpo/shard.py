@@ -114,7 +114,10 @@ def host_record(agent) -> dict:
     if hasattr(agent, "population"):  # a PPO view: what a clone of it on another rank is made of
         rec["_spec"] = agent.spec
         rec["_adam_step"] = int(agent.population.opt.steps[agent.row])
-        rec["_arch_rngs"] = (agent.module_rng.bit_generator.state, agent.critic_rng.bit_generator.state)
+        rngs = [agent.module_rng, agent.critic_rng]
+        if hasattr(agent, "kernel_rng"):  # image actor-critics also draw kernel sizes (image_arch.mutate)
+            rngs += [agent.kernel_rng, agent.critic_kernel_rng]
+        rec["_arch_rngs"] = tuple(g.bit_generator.state for g in rngs)
     return rec
 
 
@@ -174,21 +177,30 @@ class RemoteAgent:
         return self.__dict__.get("_spec") is not None
 
     def architecture_mutation(self, new_layer_prob: float, rng):
-        """The draws of a PPO view's architecture mutation (population/arch.py):
-        the method from ``rng`` (Mutations.rng), the module generators' node /
-        layer draws, and torch's global CPU generator for the fresh weights
-        (the same modules built on zeros)."""
+        """The draws of a PPO view's architecture mutation (population/arch.py
+        for MLP actor-critics, population/image_arch.py for CNN ones): the
+        method from ``rng`` (Mutations.rng), the module generators' node /
+        layer / kernel draws, and torch's global CPU generator for the fresh
+        weights (the same modules built on zeros)."""
         if self._spec is None:
             raise AttributeError("architecture_mutation")
-        from ..population import arch
+        from ..population import arch, image_arch
+        from ..population.image_nets import ImageActorCriticSpec
 
-        method = arch.sample_method(new_layer_prob, rng)
         gens = []
         for st in self._arch_rngs:
             g = np.random.default_rng()
             g.bit_generator.state = st
             gens.append(g)
-        _, _, applied, _ = arch.mutate(self._spec, torch.zeros(self._spec.n_params), method, gens[0], gens[1])
+        zeros = torch.zeros(self._spec.n_params)
+        if isinstance(self._spec, ImageActorCriticSpec):
+            if len(gens) != 4:
+                raise ValueError("an image actor-critic record carries four architecture generators")
+            method = image_arch.sample_method(new_layer_prob, rng)
+            _, _, applied, _ = image_arch.mutate(self._spec, zeros, method, gens[0], gens[2], gens[1], gens[3])
+        else:
+            method = arch.sample_method(new_layer_prob, rng)
+            _, _, applied, _ = arch.mutate(self._spec, zeros, method, gens[0], gens[1])
         return applied
 
 
@@ -248,12 +260,27 @@ def global_view(pop, records: list[dict], group=None) -> list:
     return out
 
 
+def mark_sharded(pop) -> None:
+    """Flag every local object-level agent as one shard of a global
+    population.  The entry points treat any run with more than one rank as
+    one population split over the ranks (the draws are replayed globally,
+    selection is the sharded tournament), so an agent built outside
+    ``create_population`` — directly, by ``load()``, or with
+    ``shard=False`` — must take the sharded rules too: otherwise it would
+    mutate its architecture on its own rank while the other ranks' stand-ins
+    draw nothing, and the ranks' streams would diverge."""
+    for a in pop:
+        if hasattr(type(a), "sharded"):
+            a.sharded = True
+
+
 def mutate_population(mutation, pop, pre_training_mut: bool = False, group=None):
     """``mutation.mutation(pop)`` over the global population; returns this
     rank's slice (the real agents, mutated)."""
     world, rank = world_rank(group)
     if world == 1:
         return mutation.mutation(pop, pre_training_mut=pre_training_mut)
+    mark_sharded(pop)
     sync_host_rngs(group)
     records = gather_records(pop, group)
     glob = global_view(pop, records, group)

@@ -226,5 +226,8 @@ def select_population(tournament: TournamentSelection, population):
     """The entry points' selection step: the per-process tournament, or the
     sharded one when a torch.distributed group of more than one rank is up."""
     if dist.is_initialized() and dist.get_world_size() > 1:
+        from .shard import mark_sharded
+
+        mark_sharded(population)
         return ShardedTournamentSelection(tournament).select(population)
     return tournament.select(population)

@@ -243,11 +243,27 @@ class PopulationEngine:
         return r_sum, r_cnt
 
     def evaluate(self, loop: int, max_steps) -> list[float]:
+        """agent.test for every agent (train_on_policy.py:363-373): each
+        group's pass as PopulationRunner.evaluate, all groups stepped in lock
+        step (runner.run_lockstep) so a population split into several groups
+        by mutations still evaluates in one pass's time, not one per group.
+        A group's samples depend only on its agents' counters, so the result
+        equals evaluating the groups one after another."""
+        from .runner import _EvalDriver, run_lockstep
+
         out = [0.0] * self.P
         self._eval_calls += 1
+        acc = {id(g): np.zeros(g.pop.P) for g in self.groups}
         for g in self.groups:
-            g.pop.eval_rounds = self._eval_calls - 1  # runner.evaluate counts this round in
-            f = g.runner.evaluate(loop=loop, max_steps=max_steps)
+            g.pop.eval_rounds = self._eval_calls
+        for k in range(loop):
+            drivers = [(g, _EvalDriver(g.runner, k, max_steps)) for g in self.groups]
+            run_lockstep([d for _, d in drivers])
+            for g, d in drivers:
+                acc[id(g)] += d.result()
+        for g in self.groups:
+            g.runner.after_evaluation()
+            f = acc[id(g)] / loop
             for r, slot in enumerate(g.slots):
                 out[slot] = float(f[r])
         return out

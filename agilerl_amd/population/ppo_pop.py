@@ -361,10 +361,17 @@ class PPOPopulation:
         """Raise AgxError if a fused learn() since the last check left an agent's
         update incomplete (a partner workgroup timed out); resets the word.
         Synchronises with the device."""
-        if int(self.err_word.item()) != 0:
+        w = int(self.err_word.item())
+        if w != 0:
             self.err_word.zero_()
-            raise _lib.AgxError("agx_ppo_learn: a partner workgroup timed out; the population's parameters are "
-                                "incomplete for this learn()")
+            why = []
+            if w & 1:  # AGX_LEARN_ERR_TIMEOUT
+                why.append("a partner workgroup timed out; the population's parameters are incomplete for this "
+                           "learn()")
+            if w & 2:  # AGX_LEARN_ERR_PERM
+                why.append("a minibatch permutation index was outside [0, S) (the gather prologue substituted "
+                           "row 0; this learn() is invalid)")
+            raise _lib.AgxError("agx_ppo_learn: " + "; ".join(why or [f"error word {w:#x}"]))
 
     # ------------------------------------------------------------------ #
     @property

@@ -367,65 +367,46 @@ class PopulationRunner:
     def evaluate(self, loop: int = 1, max_steps: int | None = None) -> np.ndarray:
         """Fitness of every agent at once: PPO.test (ppo.py:1113-1289) run for
         the whole population on its env slices — agent p acts on envs
-        [p*N, (p+1)*N) with the sampled policy step (one agx_ppo_act launch per
-        vector step for all P agents); each env's first finished episode score
-        counts, ``max_steps`` ends the pass; mean over envs, then over ``loop``
-        passes.  The env is reset per pass (as test() does), so the next
-        rollout starts from a fresh reset like the reference's next
-        collect_rollouts (on_policy.py:50-56).  -> float64 [P]."""
-        pop, env = self.pop, self.env
-        P, N, D = pop.P, pop.N, pop.spec.obs_dim
-        desc = pop.fused_descriptor()
-        gdesc = pop.learn_descriptor() if desc is None else None
-        act_d = torch.empty(P * N, dtype=torch.int64, device=pop.device)
-        act_h = torch.empty(P * N, dtype=torch.int64, pin_memory=True)
-        obs_h = torch.empty(P * N * D, dtype=pop.obs.dtype, pin_memory=True)
-        obs_d = torch.empty(P, N, D, dtype=pop.obs.dtype, device=pop.device)
-        out = np.zeros((loop, P))
+        [p*N, (p+1)*N) with the sampled policy step; each env's first finished
+        episode score counts, ``max_steps`` ends the pass; mean over envs, then
+        over ``loop`` passes.  The env is reset per pass (as test() does), so
+        the next rollout starts from a fresh reset like the reference's next
+        collect_rollouts (on_policy.py:50-56).  -> float64 [P].
+
+        Compiled shapes on a device-free env run the pass as ONE persistent
+        launch (agx_ppo_eval_persistent, paced like the rollout); other
+        shapes launch the policy step per vector step (_EvalDriver)."""
+        pop = self.pop
         pop.eval_rounds = getattr(pop, "eval_rounds", 0) + 1
-        eval_base = (1 << 41) + (pop.eval_rounds << 24)
+        out = np.zeros((loop, pop.P))
         for k in range(loop):
-            obs, _ = env.reset()
-            scores = np.zeros(P * N)
-            completed = np.zeros(P * N)
-            finished = np.zeros(P * N, dtype=bool)
-            step = 0
-            while not finished.all():
-                obs_h.numpy()[:] = np.asarray(obs).reshape(-1)
-                obs_d.view(-1).copy_(obs_h, non_blocking=True)
-                if desc is not None:
-                    from .learner import policy_step
+            d = _EvalDriver(self, k, max_steps)
+            run_lockstep([d])
+            out[k] = d.result()
+        self.after_evaluation()
+        return out.mean(0)
 
-                    # evaluation draws from its own counter space, one block per
-                    # evaluate() call: the rollout counters of an agent then depend
-                    # only on its own rollouts, never on how long the other agents of
-                    # its group take to finish their evaluation episodes
-                    policy_step(pop, desc, obs_d, N * D, sample=True, counter=eval_base + (k << 20) + step,
-                                out_agent_stride=N, actions_flat=act_d)
-                elif gdesc is not None:  # a mutated shape: agx_ppo_act_graph, same counters
-                    from .learner import policy_step_graph
+    def _eval_staging(self):
+        """Coherent host buffers of the persistent evaluation (allocated on
+        first use): packed obs / reward / done staging, actions, a control
+        block of its own and the per-step arguments of one launch, plus the
+        side stream its launches run on (groups evaluated in lock step each
+        keep a persistent launch resident, so they cannot share a stream)."""
+        if getattr(self, "_eval_bufs", None) is None:
+            pop = self.pop
+            P, N, D = pop.P, pop.N, pop.spec.obs_dim
+            lib = _lib.load()
+            _, obs, rew, done = _packed(P, N, D, owner=self)
+            act = _coherent(self, P * N * 8).view(torch.int64)
+            ctl = _coherent(self, int(lib.agx_rollout_ctl_bytes(P, N)))
+            args = _coherent(self, int(lib.agx_rollout_args_bytes(_EVAL_CHUNK)))
+            self._eval_bufs = (obs, rew, done, act, ctl, args, torch.cuda.Stream(device=pop.device))
+        return self._eval_bufs
 
-                    policy_step_graph(pop, gdesc, obs_d, N * D, sample=True, counter=eval_base + (k << 20) + step,
-                                      out_agent_stride=N, actions_flat=act_d)
-                else:
-                    act_d.copy_(pop.act(obs_d, counter=eval_base + (k << 20) + step)[0].view(-1))
-                act_h.copy_(act_d, non_blocking=True)
-                self.ev.record()
-                self.ev.synchronize()
-                obs, reward, term, trunc, _ = env.step(act_h.numpy().copy())
-                step += 1
-                scores += np.asarray(reward, dtype=np.float64).reshape(-1)
-                done = np.logical_or(term, trunc if trunc is not None else False).reshape(-1)
-                if max_steps is not None and step == max_steps:
-                    done = np.ones(P * N, dtype=bool)
-                new = done & ~finished
-                completed[new] = scores[new]
-                finished |= done
-            out[k] = completed.reshape(P, N).mean(1)
+    def after_evaluation(self) -> None:
         self.started = False  # the next collect() starts from env.reset()
         self.last_value_valid = False
         self.scores.zero_()
-        return out.mean(0)
 
     def iteration(self) -> torch.Tensor:
         """collect -> bootstrap + GAE -> learn; returns per-agent mean loss (device)."""
@@ -470,3 +451,194 @@ class PopulationRunner:
         if self.pop.prefetch_perms:  # next learn's minibatch orders: host work while the GPU learns
             self.pop.prefetch_permutations()
         return loss
+
+
+# ---------------------------------------------------------------------- #
+# evaluation (PPO.test, ppo.py:1113-1289) for one group, steppable in lock
+# step with other groups' passes
+# ---------------------------------------------------------------------- #
+#: vector steps per persistent evaluation launch (a pass that needs more takes
+#: another launch); the per-step arguments of a launch sit in coherent host memory
+_EVAL_CHUNK = 1024
+
+
+class _EvalDriver:
+    """One evaluation pass of one group: reset, then per vector step the
+    sampled policy step of every agent (evaluation counters
+    ``(1 << 41) + (eval_round << 24) + (k << 20) + step``, the agent's own
+    Philox stream), the env step, and each env's first finished episode
+    score.  Persistent mode keeps ONE launch resident for the pass
+    (agx_ppo_eval_persistent) and paces it through its own control block;
+    otherwise one policy-step launch + event wait per step."""
+
+    def __init__(self, runner: "PopulationRunner", k: int, max_steps: int | None):
+        self.runner, self.pop, self.env = runner, runner.pop, runner.env
+        pop = self.pop
+        P, N, D = pop.P, pop.N, pop.spec.obs_dim
+        self.P, self.N, self.D = P, N, D
+        self.max_steps = max_steps
+        self.counter0 = (1 << 41) + (int(pop.eval_rounds) << 24) + (k << 20)
+        self.desc = pop.fused_descriptor()
+        self.gdesc = pop.learn_descriptor() if self.desc is None else None
+        self.persistent = bool(runner.persistent and self.desc is not None)
+        self.step = 0
+        self.scores = np.zeros(P * N)
+        self.completed = np.zeros(P * N)
+        self.finished = np.zeros(P * N, dtype=bool)
+        if self.persistent:
+            st = runner._eval_staging()
+            self.obs_h, self.rew_h, self.done_h, self.act_h, self.ctl_h, self.args_h, self.stream = st
+            self.launched_to = 0  # steps covered by launches so far (0: no launch resident)
+        else:
+            self.act_d = torch.empty(P * N, dtype=torch.int64, device=pop.device)
+            self.act_h = torch.empty(P * N, dtype=torch.int64, pin_memory=True)
+            self.obs_h = torch.empty(P * N * D, dtype=pop.obs.dtype, pin_memory=True)
+            self.obs_d = torch.empty(P, N, D, dtype=pop.obs.dtype, device=pop.device)
+            self.ev = torch.cuda.Event()
+        self.obs = None
+
+    # -- lock-step protocol -------------------------------------------------
+    def begin(self) -> None:
+        if self.persistent:
+            self.env.reset(out_obs=self.obs_h.numpy())
+        else:
+            self.obs, _ = self.env.reset()
+
+    def _launch(self) -> None:
+        """A persistent launch covering the next chunk of steps.  Each launch
+        starts on a freshly zeroed control block (the previous launch has
+        exited: it either ran all its steps or was stopped and synchronised)."""
+        lib = _lib.load()
+        pop = self.pop
+        n = _EVAL_CHUNK if self.max_steps is None else min(_EVAL_CHUNK, int(self.max_steps) - self.step)
+        self.ctl_h.zero_()
+        # the side stream starts after everything queued so far (the learner
+        # that wrote the parameters)
+        self.stream.wait_stream(torch.cuda.current_stream(pop.device))
+        _lib.check(lib.agx_ppo_eval_persistent(ctypes.byref(self.desc), self.P, self.N, pop.params.data.data_ptr(),
+                                               self.obs_h.data_ptr(), None, self.act_h.data_ptr(),
+                                               pop.env_base_d.data_ptr(), n, 0, pop.act_seed,
+                                               self.counter0 + self.step, self.args_h.data_ptr(),
+                                               self.ctl_h.data_ptr(), self.runner.timeout_s,
+                                               self.stream.cuda_stream),
+                   "agx_ppo_eval_persistent")
+        _pacing_begin()
+        self.launch_step0 = self.step
+        self.launched_to = self.step + n
+
+    def request(self) -> None:
+        """Start the policy step of vector step self.step."""
+        if self.persistent:
+            if self.step >= self.launched_to:
+                if self.launched_to > 0:  # the previous launch ran all its steps and ends by itself
+                    self._drain()
+                self._launch()
+            _lib.load().agx_host_signal(self.ctl_h.data_ptr(), self.step - self.launch_step0 + 1)
+            return
+        pop, P, N, D = self.pop, self.P, self.N, self.D
+        self.obs_h.numpy()[:] = np.asarray(self.obs).reshape(-1)
+        self.obs_d.view(-1).copy_(self.obs_h, non_blocking=True)
+        counter = self.counter0 + self.step
+        if self.desc is not None:
+            from .learner import policy_step
+
+            policy_step(pop, self.desc, self.obs_d, N * D, sample=True, counter=counter, out_agent_stride=N,
+                        actions_flat=self.act_d)
+        elif self.gdesc is not None:  # a mutated shape: agx_ppo_act_graph, same counters
+            from .learner import policy_step_graph
+
+            policy_step_graph(pop, self.gdesc, self.obs_d, N * D, sample=True, counter=counter,
+                              out_agent_stride=N, actions_flat=self.act_d)
+        else:
+            self.act_d.copy_(pop.act(self.obs_d, counter=counter)[0].view(-1))
+        self.act_h.copy_(self.act_d, non_blocking=True)
+        self.ev.record()
+
+    def wait(self) -> None:
+        if self.persistent:
+            t = self.step - self.launch_step0 + 1
+            try:
+                _lib.check(_lib.load().agx_host_wait(self.ctl_h.data_ptr(), self.runner.n_wg, t, self.runner.timeout_s),
+                           "agx_host_wait")
+            except BaseException:
+                self.abort()
+                raise
+            return
+        self.ev.synchronize()
+
+    def env_step(self) -> bool:
+        """The env step on the actions; -> True once every env has finished."""
+        if self.persistent:
+            act = self.act_h.numpy()
+            try:
+                _, _, term, trunc, _ = self.env.step(act, out_obs=self.obs_h.numpy(), out_rew=self.rew_h.numpy(),
+                                                     out_done=self.done_h.numpy())
+            except BaseException:
+                self.abort()
+                raise
+            reward = self.rew_h.numpy()
+        else:
+            self.obs, reward, term, trunc, _ = self.env.step(self.act_h.numpy().copy())
+        self.step += 1
+        self.scores += np.asarray(reward, dtype=np.float64).reshape(-1)
+        done = np.asarray(term).reshape(-1)
+        if trunc is not None:
+            done = np.logical_or(done, np.asarray(trunc).reshape(-1))
+        if self.max_steps is not None and self.step == self.max_steps:
+            done = np.ones(self.P * self.N, dtype=bool)
+        new = done & ~self.finished
+        if new.any():
+            self.completed[new] = self.scores[new]
+            self.finished |= new
+        return bool(self.finished.all())
+
+    def _drain(self) -> None:
+        _pacing_end()
+        self.stream.synchronize()  # only this pass's launch: other groups' stay resident
+        self.launched_to = 0
+
+    def end(self) -> None:
+        """The pass is over: a persistent launch still waiting for its next
+        step is stopped cleanly (AGX_ROLLOUT_STOP) and drained."""
+        if self.persistent and self.launched_to > 0:
+            if self.step < self.launched_to:
+                _lib.load().agx_host_signal(self.ctl_h.data_ptr(), AGX_ROLLOUT_STOP)
+            self._drain()
+
+    def abort(self) -> None:
+        if self.persistent and self.launched_to > 0:
+            _lib.load().agx_host_signal(self.ctl_h.data_ptr(), AGX_ROLLOUT_STOP)
+            self._drain()
+
+    def result(self) -> np.ndarray:
+        return self.completed.reshape(self.P, self.N).mean(1)
+
+
+AGX_ROLLOUT_STOP = 0xFFFFFFFE  # include/agx.h
+
+
+def run_lockstep(drivers: list) -> None:
+    """Step several groups' evaluation passes together: every vector step
+    releases all groups' policy steps, waits for all, then steps all envs, so
+    the groups' device work and host env steps overlap instead of running
+    one pass after another."""
+    active = list(drivers)
+    try:
+        for d in active:
+            d.begin()
+        while active:
+            for d in active:
+                d.request()
+            for d in active:
+                d.wait()
+            still = []
+            for d in active:
+                if d.env_step():
+                    d.end()
+                else:
+                    still.append(d)
+            active = still
+    except BaseException:
+        for d in active:
+            d.abort()
+        raise

@@ -53,6 +53,26 @@ from ..hpo.shard import all_ranks, gather_records, mutate_population
 from ..population.engine import PopulationEngine
 
 
+#: host wall seconds per phase of the generation loop, accumulated over calls
+#: (diagnostic; bench.py reads and clears it): "train" (collect + learn
+#: iterations), "evaluate" (agent.test of every agent), "select" (tournament,
+#: parent clone, host attributes), "mutate" (mutations), "regroup" (moving
+#: mutated agents to their groups)
+PHASE_TIMES: dict[str, float] = {}
+
+
+class _Phase:
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        self.t0 = time.perf_counter()
+
+    def __exit__(self, *exc):
+        PHASE_TIMES[self.name] = PHASE_TIMES.get(self.name, 0.0) + time.perf_counter() - self.t0
+        return False
+
+
 def _population_env(env, P: int, N: int, offset: int = 0):
     if env.num_envs == P * N:
         return env
@@ -196,11 +216,12 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
     while all_ranks(all(agent.steps[-1] < max_steps for agent in pop)):
         # the generation's minibatch shuffles, agent after agent as the reference's
         # agents learn (train_on_policy.py:210-248 -> ppo.py:836-842)
-        engine.draw_generation_perms(evo_steps)
-        if collect_rollouts_fn is None:
-            losses = engine.train(evo_steps)
-        else:
-            losses = _train_with_collector(engine, pop, user_env, evo_steps, collect_rollouts_fn)
+        with _Phase("train"):
+            engine.draw_generation_perms(evo_steps)
+            if collect_rollouts_fn is None:
+                losses = engine.train(evo_steps)
+            else:
+                losses = _train_with_collector(engine, pop, user_env, evo_steps, collect_rollouts_fn)
         for j, agent in enumerate(pop):
             agent.steps[-1] += engine.steps_per_generation(j, evo_steps)
         engine.resync_numpy_after_generation(evo_steps)
@@ -208,7 +229,8 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
         r_sum, r_cnt = engine.episode_stats()
         # ... then the population's fitness: agent.test for every agent
         # (train_on_policy.py:363-373), batched on device over the env slices
-        fitness = engine.evaluate(eval_loop, eval_steps)
+        with _Phase("evaluate"):
+            fitness = engine.evaluate(eval_loop, eval_steps)
         for i, agent in enumerate(pop):
             if r_cnt[i] > 0 and collect_rollouts_fn is None:
                 agent.scores.append(float(r_sum[i] / r_cnt[i]))
@@ -224,23 +246,26 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
                 and len(pop[0].steps) >= 100:
             return pop, pop_fitnesses
         if sync is not None:  # tournament_selection_and_mutation (utils.py:1137-1225)
-            records = gather_records(pop)  # every global agent's host attributes, before the clone
-            sync.fitness_override = np.asarray(fitness)  # reduced on the host already: hand it over
-            if _all_one_group(engine):
-                # one network shape and rollout length everywhere: parent rows move in HBM
-                sync.pop, sync.runner = engine.groups[0].pop, engine.groups[0].runner
-                parents = sync.generation()
-            else:
-                parents = sync.select()
-                engine.regroup(engine.clone_states(parents, records))
-            _clone_host_attributes(pop, parents, tournament.elitism, records, rank)
+            with _Phase("select"):
+                records = gather_records(pop)  # every global agent's host attributes, before the clone
+                sync.fitness_override = np.asarray(fitness)  # reduced on the host already: hand it over
+                if _all_one_group(engine):
+                    # one network shape and rollout length everywhere: parent rows move in HBM
+                    sync.pop, sync.runner = engine.groups[0].pop, engine.groups[0].runner
+                    parents = sync.generation()
+                else:
+                    parents = sync.select()
+                    engine.regroup(engine.clone_states(parents, records))
+                _clone_host_attributes(pop, parents, tournament.elitism, records, rank)
             if save_elite and tournament.elitism and rank == 0:
                 # the reference saves ``elite``, the unmutated clone of the best agent
                 # (utils.py:1214-1223): slot 0 holds exactly that until mutation runs
                 elite_save_path = elite_path.split(".pt")[0] if elite_path is not None else f"{env_name}-elite_{algo}"
                 pop[0].save_checkpoint(f"{elite_save_path}.pt")
-            pop = mutate_population(mutation, pop)
-            _apply_mutations(engine)
+            with _Phase("mutate"):
+                pop = mutate_population(mutation, pop)
+            with _Phase("regroup"):
+                _apply_mutations(engine)
         if verbose:
             fps = sum(a.steps[-1] for a in pop) / max(time.time() - t0, 1e-9)
             print(f"--- {env_name} {algo}: steps {[a.steps[-1] for a in pop]}, fitness "

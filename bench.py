@@ -886,9 +886,12 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
     parameters, architecture, learn_step) and the regroup.  Timed over
     ``generations`` generations after one warm-up generation; env-steps are
     the training steps the reference counts (agent.steps), evaluation steps
-    not included.  Reported with ARCH_MUT = 0 (every agent stays on the fused
-    kernels; the other mutation kinds as ppo.yaml), and with AGX_BENCH_E2E_ARCH=1
-    also with ppo.yaml's ARCH_MUT 0.2."""
+    not included.  Reported with ppo.yaml's MUTATION_PARAMS as they are
+    (ARCH_MUT 0.2) and with ARCH_MUT = 0 (every agent stays on the compiled
+    kernels; the other mutation kinds as ppo.yaml); each also over
+    AGX_BENCH_E2E_LONG (default 10) generations, with the milliseconds per
+    generation split by phase (train / evaluate / select / mutate / regroup)
+    and the count of agents on each kernel family at the end."""
     from agilerl_amd.envs import SyntheticVecEnv
     from agilerl_amd.hpo.mutation import Mutations
     from agilerl_amd.hpo.registry import HyperparameterConfig, RLParameter
@@ -946,20 +949,37 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
     variants = [("ppo_yaml", 0.2), ("no_arch_mutation", 0.0)]
     if os.environ.get("AGX_BENCH_E2E_NO_ARCH_ONLY"):
         variants = variants[1:]
+    from agilerl_amd.training import train_on_policy as top_mod
+
+    def one(arch: float, gens: int, seed: int) -> dict:
+        top_mod.PHASE_TIMES.clear()
+        dt, pop = run(arch, gens, seed)
+        steps = sum(a.steps[-1] for a in pop)
+        fused = sum(a.population.fused_descriptor() is not None for a in pop)
+        hip = sum(a.population.learn_descriptor() is not None for a in pop)
+        phases = {k: round(v / gens * 1e3, 2) for k, v in sorted(top_mod.PHASE_TIMES.items())}
+        phases["other"] = round(dt / gens * 1e3 - sum(phases.values()), 2)
+        return {"env_steps_per_s": round(steps / dt, 1), "ms_per_generation": round(dt / gens * 1e3, 2),
+                "ms_per_generation_by_phase": phases, "env_steps": int(steps),
+                "agents_on_compiled_kernels_at_end": int(fused),
+                "agents_on_runtime_shape_kernels_at_end": int(hip - fused),
+                "agents_on_pytorch_learner_at_end": int(len(pop) - hip),
+                "groups_at_end": len({id(a.population) for a in pop}),
+                "final_shapes": sorted({str(a.spec.shape_key()[2:6]) for a in pop})}
+
+    long_gens = int(os.environ.get("AGX_BENCH_E2E_LONG", 10))
     for name, arch in variants:
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
             run(arch, 1, 5)  # warm-up (first-use allocations, library start-up)
             log(f"train_on_policy {name}: warm-up done")
-            dt, pop = run(arch, generations, 6)
-            log(f"train_on_policy {name}: {generations} generations in {dt:.1f} s")
-        steps = sum(a.steps[-1] for a in pop)
-        fused = sum(a.population.fused_descriptor() is not None for a in pop)
-        hip = sum(a.population.learn_descriptor() is not None for a in pop)
-        out[name] = {"env_steps_per_s": round(steps / dt, 1), "ms_per_generation": round(dt / generations * 1e3, 2),
-                     "env_steps": int(steps), "agents_on_compiled_kernels_at_end": int(fused),
-                     "agents_on_hip_kernels_at_end": int(hip),
-                     "final_shapes": sorted({str(a.spec.shape_key()[2:6]) for a in pop})}
+            out[name] = one(arch, generations, 6)
+            log(f"train_on_policy {name}: {generations} generations: {out[name]['ms_per_generation']} ms each")
+            if long_gens > generations:
+                # the decay as mutations move agents to other groups / kernels
+                out[name][f"{long_gens}_generations"] = one(arch, long_gens, 7)
+                log(f"train_on_policy {name}: {long_gens} generations: "
+                    f"{out[name][f'{long_gens}_generations']['ms_per_generation']} ms each")
     return out
 
 

@@ -132,10 +132,16 @@ int agx_ppo_learn_prepare(const agx_ppo_net *net, void *workspace, void *stream)
  *   loss_out    [P] f32 = sum of minibatch losses / (S * epochs) (ppo.py:920);
  *   kl_out      [P] f32 mean approx_kl over the minibatches run, or NULL;
  *   epochs_out  [P] int32 epochs run, or NULL;
- *   error_word  one uint32, sticky: the kernel ORs in 1 when a partner
- *               workgroup gave up waiting (the agent's update is then
- *               incomplete); never cleared by the library — the caller
- *               checks and resets it (PPOPopulation raises AgxError). */
+ *   error_word  one uint32, sticky: the kernel ORs in
+ *               AGX_LEARN_ERR_TIMEOUT (1) when a partner workgroup gave up
+ *               waiting (the agent's update is then incomplete) and the
+ *               gather prologue ORs in AGX_LEARN_ERR_PERM (2) when a perms
+ *               entry it reads lies outside [0, S) (row 0 is gathered in
+ *               its place: the update is then invalid, but nothing faults);
+ *               never cleared by the library — the caller checks and resets
+ *               it (PPOPopulation raises AgxError). */
+#define AGX_LEARN_ERR_TIMEOUT 1u
+#define AGX_LEARN_ERR_PERM 2u
 typedef struct agx_ppo_learn_args {
     int64_t P, S, epochs, batch;
     float *params, *exp_avg, *exp_avg_sq;
@@ -263,6 +269,10 @@ typedef struct agx_rollout_ctl {
     /* followed by nwg uint32 done words, then (64-byte aligned) one 64-byte
      * release line per workgroup: each workgroup polls its own copy of seq */
 } agx_rollout_ctl;
+/* seq value that ends a persistent launch early and cleanly (an evaluation
+ * whose episodes have all finished): every workgroup waiting for its next
+ * step exits without touching ctl->timeout. */
+#define AGX_ROLLOUT_STOP 0xfffffffeu
 int64_t agx_rollout_workgroups(int64_t P, int64_t N);
 /* Workgroups of the persistent rollout kernel for `net` the GPU holds at once
  * (occupancy x CUs; 0: shape not instantiated).  Every workgroup of a
@@ -277,6 +287,22 @@ int agx_ppo_rollout_persistent(const agx_ppo_net *net, int64_t P, int64_t N, con
                                const agx_rollout_io *ios, int64_t nsteps, uint32_t base, uint64_t seed,
                                uint64_t counter0, void *args_host, agx_rollout_ctl *ctl, double timeout_s,
                                void *stream);
+/* Persistent evaluation: PPO.test's loop (agilerl/algorithms/ppo.py:1113-
+ * 1289) for P agents x N envs in ONE launch of the persistent rollout kernel,
+ * paced like agx_ppo_rollout_persistent.  Step t reads the observations from
+ * stage_obs (coherent host memory, [P*N][D]; legal-action masks from
+ * stage_mask [P*N][A] or NULL), samples with Philox counter counter0 + t
+ * (agx_ppo_act's stream) and writes the P*N actions to actions_flat (host).
+ * Nothing else is stored: no rollout slots, no episode accounting (the host
+ * tallies the evaluation episodes from its env step).  The host ends the
+ * launch early with agx_host_signal(ctl, AGX_ROLLOUT_STOP) once every episode
+ * has finished; a launch that runs all nsteps ends by itself.
+ * args_host: agx_rollout_args_bytes(nsteps) of agx_host_alloc memory. */
+int agx_ppo_eval_persistent(const agx_ppo_net *net, int64_t P, int64_t N, const float *params,
+                            const float *stage_obs, const uint8_t *stage_mask, int64_t *actions_flat,
+                            const int64_t *agent_env_base, int64_t nsteps, uint32_t base, uint64_t seed,
+                            uint64_t counter0, void *args_host, agx_rollout_ctl *ctl, double timeout_s,
+                            void *stream);
 /* ---- reference RNG streams (host) ----------------------------------------
  * The minibatch permutations PPO._learn_from_rollout_buffer_flat draws from
  * numpy's global legacy MT19937 (ppo.py:836-842: indices = arange(S) once

@@ -385,3 +385,30 @@ def test_target_kl_resyncs_global_numpy_stream():
     np.random.seed(77)
     numpy_shuffle_perms(1, int(ran.sum()), pop.S)
     assert np.array_equal(got, np.random.randint(0, 2**31 - 1, 8))
+
+
+@pytest.mark.parametrize("bad", [2048 + 7, -3])
+def test_bad_permutation_index_raises(bad):
+    """A permutation index outside [0, S) (a host-side slip: the round-4
+    fault was stale rows of the pinned shuffle buffer) is caught by the
+    gather prologue on the device: the sticky error word gets
+    AGX_LEARN_ERR_PERM, nothing is read out of bounds, and
+    PPOPopulation.check_errors raises AgxError."""
+    from agilerl_amd import _lib
+    from agilerl_amd.population.learner import fused_learn
+
+    pop, _, _ = _config2_population()
+    E, P, S = pop.update_epochs, pop.P, pop.S
+    block = np.stack([np.stack([np.random.default_rng(e * P + p).permutation(S) for p in range(P)])
+                      for e in range(E)])[None].astype(np.int64)
+    block[0, 1, 3, 17] = bad
+    pop.set_generation_perms(block)
+    fused_learn(pop)
+    torch.cuda.synchronize()
+    with pytest.raises(_lib.AgxError, match="permutation"):
+        pop.check_errors()
+    pop.check_errors()  # reset
+    pop.set_generation_perms(None)
+    fused_learn(pop)  # the next learn with valid shuffles runs clean
+    torch.cuda.synchronize()
+    pop.check_errors()

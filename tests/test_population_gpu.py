@@ -612,3 +612,59 @@ def test_env_that_synchronizes_the_device_completes(monkeypatch):
     pop.check_errors()
     assert time.perf_counter() - t0 < 4.0
     assert torch.isfinite(pop.params.data).all()
+
+
+@pytest.mark.parametrize("max_steps", [None, 13])
+def test_persistent_evaluation_matches_per_step_launches(monkeypatch, max_steps):
+    """The evaluation pass as ONE persistent launch (agx_ppo_eval_persistent,
+    host-paced, ended by AGX_ROLLOUT_STOP once every env has finished) gives
+    the fitness of one policy-step launch per vector step bit for bit — the
+    same Philox counters, the same first-finished-episode tally — also when
+    a pass needs several launches (chunk of 7 steps here); the rollout after
+    it starts from a reset, as after the per-step pass."""
+    from agilerl_amd.population import runner as R
+
+    monkeypatch.setattr(R, "_EVAL_CHUNK", 7)
+    out = []
+    for persistent in (True, False):
+        pop, run = _runner_pair(monkeypatch, persistent)
+        run.env.max_episode_steps = 30
+        run.iteration()
+        fit = run.evaluate(loop=2, max_steps=max_steps)
+        run.iteration()
+        torch.cuda.synchronize()
+        out.append((fit, pop.params.data.clone(), pop.obs.clone()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
+    assert np.all(np.isfinite(out[0][0]))
+
+
+def test_engine_evaluates_groups_in_lockstep(monkeypatch):
+    """A population split into groups (a learn_step mutation here) is
+    evaluated with every group's pass stepped together; each group's fitness
+    equals its own runner's pass run alone (the groups' samples depend only
+    on their agents' counters)."""
+    from agilerl_amd.envs import StackedVecEnv, SyntheticVecEnv
+    from agilerl_amd.population.engine import PopulationEngine
+
+    P, N = 4, 32
+    pop, _ = _runner_pair(monkeypatch, True, P=P, N=N)
+    envs = [SyntheticVecEnv(N, seed=10 + j, p_done=0.1, max_episode_steps=25) for j in range(P)]
+    views = [type("V", (), {"learn_step": pop.learn_step})() for _ in range(P)]
+    eng = PopulationEngine(pop, views, StackedVecEnv(envs))
+    states = eng.local_states()
+    states[1].learn_step = states[1].learn_step // 2
+    states[3].learn_step = states[3].learn_step // 2
+    eng.regroup(states)
+    assert len(eng.groups) == 2
+    eng.train(2 * pop.learn_step)
+    fit = eng.evaluate(1, None)
+    # the same evaluation round, group by group
+    eng._eval_calls -= 1
+    alone = [0.0] * P
+    for g in eng.groups:
+        g.pop.eval_rounds = eng._eval_calls  # runner.evaluate counts this round in
+        f = g.runner.evaluate(loop=1, max_steps=None)
+        for r, slot in enumerate(g.slots):
+            alone[slot] = float(f[r])
+    assert fit == alone
