@@ -56,6 +56,7 @@ SIGNATURES = {
                                        ctypes.c_uint64, _P, _P, _D, _P]),
     "agx_host_alloc": (_P, [_SZ]),
     "agx_host_free": (_INT, [_P]),
+    "agx_stream_create": (_P, []),
     "agx_host_signal": (_INT, [_P, ctypes.c_uint32]),
     "agx_host_wait": (_INT, [_P, _I, ctypes.c_uint32, _D]),
     "agx_per_workspace_bytes": (_SZ, [_I, _I]),
@@ -117,6 +118,8 @@ def load(require_gpu: bool = True):
             )
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("AGX_LIB") and not hasattr(lib, name):
+                continue  # an A/B build of an older revision: only what it exports
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -69,6 +69,16 @@ struct GArgs {
     GLay L[kGL];
     int nl, aout, cout, A, D, n, cstart, bp;
     long long oc, dzr, dzc, dzr1, dzc1, t1, t2, gr, ws_agent;  // dZ buffers by layer parity
+    // partnered learner (ppo_learn_graph_part_kernel): K workgroups per agent,
+    // R rows of each minibatch per partner; agent stride Q of the block index
+    long long ws_part, wt0, wt_agent;  // a partner's scratch, the transposed weights' plan offset / size
+    int K, R, Q;
+    long long nslab;       // floats per exchange slab: gradient row, loss chunk, partial norms
+    float *slabs, *sums;   // [P][2][K][nslab] partial gradients, [P][2][nslab] summed gradients
+    float *wtb;            // [P][wt_agent] transposed weights shared by an agent's partners
+    unsigned *cnt;         // barrier counters, timeout word, XCC ids (zeroed by the gather)
+    unsigned *err;         // caller's sticky error word
+    int write_through;     // test hook: the cross-XCD (release-fence) publish form always
     float *ws;
     float *params, *m, *v;
     const float *lr;
@@ -702,6 +712,244 @@ __device__ __forceinline__ void forward_layers(const GLay *Ls, int nl, const flo
     }
 }
 
+// One minibatch's forward, PPO loss and backward over `bsz` rows (rows
+// s0 .. s0 + bsz - 1 of the epoch's minibatch-ordered rollout, observations at
+// xobs), accumulating the gradient row G (every entry written: dW by GEMM
+// epilogues, bias / LN-affine sums by the column passes) and the loss / approx_kl
+// partial sums.  inv_b = 1 / the whole minibatch's size (the loss is a mean over
+// it).  base: this workgroup's activation scratch; wb: where the transposed
+// weights live (wb + L.wt).  Shared by the one-workgroup-per-agent learner and
+// the partnered one (each partner over its slice of the rows).
+__device__ __forceinline__ void minibatch_grads(const GArgs &g, float *base, const float *wb, const float *pr, float *G,
+                                                const float *xobs, const int *gact_e, const unsigned *gmask_e,
+                                                const float *grow_e, long long s0, int bsz, float inv_b, float entp,
+                                                float *lds, float *colp, float *colo, float &lsum, float &klsum) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = lane & 15, rq = lane >> 4;
+    const int bp = g.bp, A = g.A, D = g.D;
+    const long long S = g.S;
+    (void)wave;
+    // observation, feature-major (the first layer's dW operand)
+    for (int i = tid; i < bsz * D; i += kGT) {
+        const int b = i / D, d = i - b * D;
+        base[g.oc + (size_t)d * bp + b] = xobs[i];
+    }
+
+    // ---- forward, layer by layer ------------------------------------
+    forward_layers(g.L, g.nl, xobs, bsz, base, pr, bp, lds, g.dbg);
+
+    // ---- loss row pass: logits / value -> d(logits), d(value) (ppo.py:876-908)
+    if (!(g.dbg & 8)) {
+        const GLay &La = g.L[g.aout];
+        const GLay &Lc = g.L[g.cout];
+        const float *lgp = base + La.yr;
+        const float *vp = base + Lc.yr;
+        float *dla = base + La.dy;
+        float *dlac = base + La.dyc;
+        float *dlv = base + Lc.dy;
+        const int a0 = sub, a1 = sub + 16;
+        float cb0 = 0.f, cb1 = 0.f, cbv = 0.f;  // output-layer bias gradients (column partials)
+        // four rows per 16-lane group at once: every input of the 128-row
+        // block is loaded before the first reduction
+        constexpr int R = 4;
+        for (int rb = 0; rb < bsz; rb += R * 4 * kGW) {
+            unsigned pbits[R];
+            int pact[R];
+            float plg0[R], plg1[R], polp[R], pad[R], pret[R], pov[R], pv[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int row0 = rb + 4 * wave + rq + 4 * kGW * u;
+                const int row = row0 < bsz ? row0 : 0;
+                pbits[u] = gmask_e ? gmask_e[s0 + row] : 0xffffffffu;
+                plg0[u] = lgp[(size_t)row * A + (a0 < A ? a0 : 0)];
+                plg1[u] = lgp[(size_t)row * A + (a1 < A ? a1 : 0)];
+                pact[u] = gact_e[s0 + row];
+                polp[u] = grow_e[s0 + row];
+                pad[u] = grow_e[S + s0 + row];
+                pret[u] = grow_e[2 * S + s0 + row];
+                pov[u] = grow_e[3 * S + s0 + row];
+                pv[u] = vp[row];
+            }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+            const int row0 = rb + 4 * wave + rq + 4 * kGW * u;
+            const bool live = row0 < bsz;
+            const int row = live ? row0 : 0;
+            const unsigned bits = pbits[u];
+            const bool ok0 = (bits >> a0) & 1u, ok1 = (bits >> a1) & 1u;
+            const float lg0 = a0 < A ? (ok0 ? plg0[u] : -1.0e8f) : -3.0e38f;
+            const float lg1 = a1 < A ? (ok1 ? plg1[u] : -1.0e8f) : -3.0e38f;
+            const float mx = rmax16(fmaxf(lg0, lg1));
+            const float ex0 = a0 < A ? expf(lg0 - mx) : 0.f, ex1 = a1 < A ? expf(lg1 - mx) : 0.f;
+            const float lse = mx + logf(rsum16(ex0 + ex1));
+            const float p0 = a0 < A ? expf(lg0 - lse) : 0.f, p1 = a1 < A ? expf(lg1 - lse) : 0.f;
+            const float lpe0 = logf(p0 + 1e-8f), lpe1 = logf(p1 + 1e-8f);
+            const float Hs = -rsum16((a0 < A ? p0 * lpe0 : 0.f) + (a1 < A ? p1 * lpe1 : 0.f));
+            const float gh0 = -(lpe0 + p0 / (p0 + 1e-8f)), gh1 = -(lpe1 + p1 / (p1 + 1e-8f));
+            const float pg = rsum16((a0 < A ? p0 * gh0 : 0.f) + (a1 < A ? p1 * gh1 : 0.f));
+            const int a_t = pact[u];
+            const int srcl = (lane & ~15) + (a_t & 15);
+            const float t0 = bperm(srcl, lg0), t1 = bperm(srcl, lg1);
+            const float logp = (a_t < 16 ? t0 : t1) - lse;
+            const float olp = polp[u], Ad = pad[u], Rt = pret[u], ov = pov[u];
+            const float lo = 1.f - g.clip, hi = 1.f + g.clip;
+            const float lrt = logp - olp;
+            const float ratio = expf(lrt);
+            const float rcl = fminf(fmaxf(ratio, lo), hi);
+            const float q1 = -Ad * ratio, q2 = -Ad * rcl;
+            const float g1 = q1 > q2 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
+            const float g2 = q2 > q1 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
+            const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+            const float g_logp = ((g1 * -Ad + g2 * -Ad * inr) * inv_b) * ratio;
+            const float v = pv[u];
+            const float dv = v - ov;
+            const float vcl = ov + fminf(fmaxf(dv, -g.clip), g.clip);
+            const float eu = v - Rt, ec = vcl - Rt;
+            const float lu = eu * eu, lc = ec * ec;
+            const float gu = lu > lc ? 1.f : (lu == lc ? 0.5f : 0.f);
+            const float gc = lc > lu ? 1.f : (lu == lc ? 0.5f : 0.f);
+            const float inv = (dv >= -g.clip && dv <= g.clip) ? 1.f : 0.f;
+            const float g_H = -entp * inv_b;
+            const float dl0 = g_logp * ((a0 == a_t ? 1.f : 0.f) - p0) + g_H * p0 * (gh0 - pg);
+            const float dl1 = g_logp * ((a1 == a_t ? 1.f : 0.f) - p1) + g_H * p1 * (gh1 - pg);
+            if (live) {
+                const float d0 = ok0 ? dl0 : 0.f, d1 = ok1 ? dl1 : 0.f;
+                if (a0 < A) {
+                    dla[(size_t)row * A + a0] = d0;
+                    dlac[(size_t)a0 * bp + row] = d0;
+                    cb0 += d0;
+                }
+                if (a1 < A) {
+                    dla[(size_t)row * A + a1] = d1;
+                    dlac[(size_t)a1 * bp + row] = d1;
+                    cb1 += d1;
+                }
+                if (sub == 0) {
+                    const float dvv = g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv);
+                    dlv[row] = dvv;
+                    cbv += dvv;
+                    lsum += (fmaxf(q1, q2) + g.vf * 0.5f * fmaxf(lu, lc) - entp * Hs) * inv_b;
+                    klsum += ((ratio - 1.f) - lrt) * inv_b;  // approx_kl (ppo.py:899-902)
+                }
+            }
+            }
+        }
+        // bias gradients of the output layers: the wave's four row groups,
+        // then per wave into LDS (summed over the waves in order below)
+        cb0 += __shfl_xor(cb0, 16, 64);
+        cb0 += __shfl_xor(cb0, 32, 64);
+        cb1 += __shfl_xor(cb1, 16, 64);
+        cb1 += __shfl_xor(cb1, 32, 64);
+        cbv += __shfl_xor(cbv, 16, 64);
+        cbv += __shfl_xor(cbv, 32, 64);
+        if (rq == 0) {
+            colo[wave * 33 + a0] = cb0;
+            colo[wave * 33 + a1] = cb1;
+            if (sub == 0) colo[wave * 33 + 32] = cbv;
+        }
+    }
+    __syncthreads();
+    if (!(g.dbg & 8) && tid <= A) {
+        float sb = 0.f;
+        for (int w = 0; w < kGW; ++w) sb += colo[w * 33 + (tid < A ? tid : 32)];
+        G[tid < A ? g.L[g.aout].b + tid : g.L[g.cout].b] = sb;
+    }
+
+    // ---- backward, layer by layer (reverse) ----------------------------
+    float *t1c = base + g.t1, *t2c = base + g.t2;
+    for (int l = g.nl - 1; l >= 0; --l) {
+        const GLay &L = g.L[l];
+        const int F = L.fout;
+        float *dzr = base + ((l & 1) ? g.dzr1 : g.dzr), *dzc = base + ((l & 1) ? g.dzc1 : g.dzc);
+        float *colp_l = colp + (l & 1) * 3 * kGW * 128;
+        // output layers: the loss pass wrote dZ in both layouts and the bias gradient;
+        // fused layers: the consumer's dX epilogue wrote dZ and the column partials
+        const bool outl = L.dyc >= 0;
+        // dY -> dZ through ReLU and LayerNorm(+affine)
+        if (!(g.dbg & 8) && !outl && !L.fused) {
+            if (F <= 128) bwd_rows<8>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c, colp_l);
+            else bwd_rows<0>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
+        }
+        if (!outl && !L.fused) __syncthreads();
+        // bias / LN-affine gradients: column sums over the rows (fixed order);
+        // up to 8 feature groups summed before the first store
+        if (F <= 128 && !(g.dbg & 24) && !outl) {  // the row pass left per-wave partials in LDS
+            for (int o = tid; o < F; o += kGT) {
+                float sb = 0.f, sg = 0.f, sbe = 0.f;
+                for (int w = 0; w < kGW; ++w) {
+                    sb += colp_l[w * F + o];
+                    sg += colp_l[(kGW + w) * F + o];
+                    sbe += colp_l[(2 * kGW + w) * F + o];
+                }
+                G[L.b + o] = sb;
+                if (L.ln == 2) {
+                    G[L.g + o] = sg;
+                    G[L.be + o] = sbe;
+                }
+            }
+        }
+        for (int ob = 0; ob < ((g.dbg & 16) || F <= 128 || outl ? 0 : F); ob += 8 * 4 * kGW) {
+            float rb_[8], rg_[8], rbe_[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int o = ob + 4 * kGW * k + 4 * wave + rq;
+                const bool on = o < F;
+                float sb = 0.f, sg = 0.f, sbe = 0.f;
+                if (ob + 4 * kGW * k < F) {  // wave-uniform
+                    for (int b = sub; b < bsz; b += 16) {
+                        const size_t x = (size_t)(on ? o : 0) * bp + b;
+                        const float v0 = dzc[x];
+                        sb += on ? v0 : 0.f;
+                        if (L.ln == 2) {
+                            const float v1 = t1c[x], v2 = t2c[x];
+                            sg += on ? v1 : 0.f;
+                            sbe += on ? v2 : 0.f;
+                        }
+                    }
+                }
+                rb_[k] = rsum16(sb);
+                rg_[k] = L.ln == 2 ? rsum16(sg) : 0.f;
+                rbe_[k] = L.ln == 2 ? rsum16(sbe) : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int o = ob + 4 * kGW * k + 4 * wave + rq;
+                if (o < F && sub == 0) {
+                    G[L.b + o] = rb_[k];
+                    if (L.ln == 2) {
+                        G[L.g + o] = rg_[k];
+                        G[L.be + o] = rbe_[k];
+                    }
+                }
+            }
+        }
+        // dW = dZ^T X (contraction over the rows), then dX = dZ W into the
+        // source's dY (one GEMM call site for both: instruction-cache footprint)
+        const float *xc = L.src < 0 ? base + g.oc : base + g.L[L.src].yc;
+        const int fin = L.fin;
+        for (int job = 0; job < (L.src >= 0 ? 2 : 1); ++job) {
+            if (job) __syncthreads();  // the dW GEMM's last panels are still being read
+            if (g.dbg & (job ? 4 : 2)) continue;
+            const float *ga = job ? (outl ? base + L.dy : dzr) : (outl ? base + L.dyc : dzc);
+            const float *gb = job ? wb + L.wt : xc;
+            const int lda = job ? F : bp, ldb = job ? F : bp;
+            const int M = job ? bsz : F, K = job ? F : bsz;
+            float *dst = job ? base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy) : G + L.w;
+            if (job && L.fuse) {  // the source's dZ (other parity) from the epilogue
+                const int s_ = L.src;
+                gemm_nt<2>(ga, lda, gb, ldb, M, fin, K, lds, nullptr, [](int, int, float) {}, g.L[s_], base, pr,
+                           bp, base + ((s_ & 1) ? g.dzr1 : g.dzr), base + ((s_ & 1) ? g.dzc1 : g.dzc),
+                           colp + (s_ & 1) * 3 * kGW * 128);
+            } else {
+                gemm_nt(ga, lda, gb, ldb, M, fin, K, lds, nullptr,
+                        [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; }, L);
+            }
+        }
+        __syncthreads();
+    }
+
+}
+
 __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
     __shared__ float red[2 * kGW];
     __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
@@ -709,14 +957,13 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
     __shared__ float colo[kGW * 33];       // per-wave output-layer bias partials (32 logits + the value)
     if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const int p = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int sub = lane & 15, rq = lane >> 4;
+    const int tid = threadIdx.x;
     float *const pr = g.params + (size_t)p * g.n;
     float *const gm = g.m + (size_t)p * g.n;
     float *const gv = g.v + (size_t)p * g.n;
     float *const base = g.ws + (size_t)p * g.ws_agent;
     float *const G = base + g.gr;
-    const int bp = g.bp, A = g.A, D = g.D;
+    const int D = g.D;
     const long long S = g.S;
 
     // transposed weight copies (the dX operand)
@@ -755,226 +1002,9 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
             const float inv_b = 1.f / (float)bsz;
             const float *xobs = gobs_e + s0 * D;
 
-            // observation, feature-major (the first layer's dW operand)
-            for (int i = tid; i < bsz * D; i += kGT) {
-                const int b = i / D, d = i - b * D;
-                base[g.oc + (size_t)d * bp + b] = xobs[i];
-            }
-
-            // ---- forward, layer by layer ------------------------------------
-            forward_layers(g.L, g.nl, xobs, bsz, base, pr, bp, lds, g.dbg);
-
-            // ---- loss row pass: logits / value -> d(logits), d(value) (ppo.py:876-908)
             float lsum = 0.f, klsum = 0.f;
-            if (!(g.dbg & 8)) {
-                const GLay &La = g.L[g.aout];
-                const GLay &Lc = g.L[g.cout];
-                const float *lgp = base + La.yr;
-                const float *vp = base + Lc.yr;
-                float *dla = base + La.dy;
-                float *dlac = base + La.dyc;
-                float *dlv = base + Lc.dy;
-                const int a0 = sub, a1 = sub + 16;
-                float cb0 = 0.f, cb1 = 0.f, cbv = 0.f;  // output-layer bias gradients (column partials)
-                // four rows per 16-lane group at once: every input of the 128-row
-                // block is loaded before the first reduction
-                constexpr int R = 4;
-                for (int rb = 0; rb < bsz; rb += R * 4 * kGW) {
-                    unsigned pbits[R];
-                    int pact[R];
-                    float plg0[R], plg1[R], polp[R], pad[R], pret[R], pov[R], pv[R];
-#pragma unroll
-                    for (int u = 0; u < R; ++u) {
-                        const int row0 = rb + 4 * wave + rq + 4 * kGW * u;
-                        const int row = row0 < bsz ? row0 : 0;
-                        pbits[u] = gmask_e ? gmask_e[s0 + row] : 0xffffffffu;
-                        plg0[u] = lgp[(size_t)row * A + (a0 < A ? a0 : 0)];
-                        plg1[u] = lgp[(size_t)row * A + (a1 < A ? a1 : 0)];
-                        pact[u] = gact_e[s0 + row];
-                        polp[u] = grow_e[s0 + row];
-                        pad[u] = grow_e[S + s0 + row];
-                        pret[u] = grow_e[2 * S + s0 + row];
-                        pov[u] = grow_e[3 * S + s0 + row];
-                        pv[u] = vp[row];
-                    }
-#pragma unroll
-                    for (int u = 0; u < R; ++u) {
-                    const int row0 = rb + 4 * wave + rq + 4 * kGW * u;
-                    const bool live = row0 < bsz;
-                    const int row = live ? row0 : 0;
-                    const unsigned bits = pbits[u];
-                    const bool ok0 = (bits >> a0) & 1u, ok1 = (bits >> a1) & 1u;
-                    const float lg0 = a0 < A ? (ok0 ? plg0[u] : -1.0e8f) : -3.0e38f;
-                    const float lg1 = a1 < A ? (ok1 ? plg1[u] : -1.0e8f) : -3.0e38f;
-                    const float mx = rmax16(fmaxf(lg0, lg1));
-                    const float ex0 = a0 < A ? expf(lg0 - mx) : 0.f, ex1 = a1 < A ? expf(lg1 - mx) : 0.f;
-                    const float lse = mx + logf(rsum16(ex0 + ex1));
-                    const float p0 = a0 < A ? expf(lg0 - lse) : 0.f, p1 = a1 < A ? expf(lg1 - lse) : 0.f;
-                    const float lpe0 = logf(p0 + 1e-8f), lpe1 = logf(p1 + 1e-8f);
-                    const float Hs = -rsum16((a0 < A ? p0 * lpe0 : 0.f) + (a1 < A ? p1 * lpe1 : 0.f));
-                    const float gh0 = -(lpe0 + p0 / (p0 + 1e-8f)), gh1 = -(lpe1 + p1 / (p1 + 1e-8f));
-                    const float pg = rsum16((a0 < A ? p0 * gh0 : 0.f) + (a1 < A ? p1 * gh1 : 0.f));
-                    const int a_t = pact[u];
-                    const int srcl = (lane & ~15) + (a_t & 15);
-                    const float t0 = bperm(srcl, lg0), t1 = bperm(srcl, lg1);
-                    const float logp = (a_t < 16 ? t0 : t1) - lse;
-                    const float olp = polp[u], Ad = pad[u], Rt = pret[u], ov = pov[u];
-                    const float lo = 1.f - g.clip, hi = 1.f + g.clip;
-                    const float lrt = logp - olp;
-                    const float ratio = expf(lrt);
-                    const float rcl = fminf(fmaxf(ratio, lo), hi);
-                    const float q1 = -Ad * ratio, q2 = -Ad * rcl;
-                    const float g1 = q1 > q2 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
-                    const float g2 = q2 > q1 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
-                    const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
-                    const float g_logp = ((g1 * -Ad + g2 * -Ad * inr) * inv_b) * ratio;
-                    const float v = pv[u];
-                    const float dv = v - ov;
-                    const float vcl = ov + fminf(fmaxf(dv, -g.clip), g.clip);
-                    const float eu = v - Rt, ec = vcl - Rt;
-                    const float lu = eu * eu, lc = ec * ec;
-                    const float gu = lu > lc ? 1.f : (lu == lc ? 0.5f : 0.f);
-                    const float gc = lc > lu ? 1.f : (lu == lc ? 0.5f : 0.f);
-                    const float inv = (dv >= -g.clip && dv <= g.clip) ? 1.f : 0.f;
-                    const float g_H = -entp * inv_b;
-                    const float dl0 = g_logp * ((a0 == a_t ? 1.f : 0.f) - p0) + g_H * p0 * (gh0 - pg);
-                    const float dl1 = g_logp * ((a1 == a_t ? 1.f : 0.f) - p1) + g_H * p1 * (gh1 - pg);
-                    if (live) {
-                        const float d0 = ok0 ? dl0 : 0.f, d1 = ok1 ? dl1 : 0.f;
-                        if (a0 < A) {
-                            dla[(size_t)row * A + a0] = d0;
-                            dlac[(size_t)a0 * bp + row] = d0;
-                            cb0 += d0;
-                        }
-                        if (a1 < A) {
-                            dla[(size_t)row * A + a1] = d1;
-                            dlac[(size_t)a1 * bp + row] = d1;
-                            cb1 += d1;
-                        }
-                        if (sub == 0) {
-                            const float dvv = g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv);
-                            dlv[row] = dvv;
-                            cbv += dvv;
-                            lsum += (fmaxf(q1, q2) + g.vf * 0.5f * fmaxf(lu, lc) - entp * Hs) * inv_b;
-                            klsum += ((ratio - 1.f) - lrt) * inv_b;  // approx_kl (ppo.py:899-902)
-                        }
-                    }
-                    }
-                }
-                // bias gradients of the output layers: the wave's four row groups,
-                // then per wave into LDS (summed over the waves in order below)
-                cb0 += __shfl_xor(cb0, 16, 64);
-                cb0 += __shfl_xor(cb0, 32, 64);
-                cb1 += __shfl_xor(cb1, 16, 64);
-                cb1 += __shfl_xor(cb1, 32, 64);
-                cbv += __shfl_xor(cbv, 16, 64);
-                cbv += __shfl_xor(cbv, 32, 64);
-                if (rq == 0) {
-                    colo[wave * 33 + a0] = cb0;
-                    colo[wave * 33 + a1] = cb1;
-                    if (sub == 0) colo[wave * 33 + 32] = cbv;
-                }
-            }
-            __syncthreads();
-            if (!(g.dbg & 8) && tid <= A) {
-                float sb = 0.f;
-                for (int w = 0; w < kGW; ++w) sb += colo[w * 33 + (tid < A ? tid : 32)];
-                G[tid < A ? g.L[g.aout].b + tid : g.L[g.cout].b] = sb;
-            }
-
-            // ---- backward, layer by layer (reverse) ----------------------------
-            float *t1c = base + g.t1, *t2c = base + g.t2;
-            for (int l = g.nl - 1; l >= 0; --l) {
-                const GLay &L = g.L[l];
-                const int F = L.fout;
-                float *dzr = base + ((l & 1) ? g.dzr1 : g.dzr), *dzc = base + ((l & 1) ? g.dzc1 : g.dzc);
-                float *colp_l = colp + (l & 1) * 3 * kGW * 128;
-                // output layers: the loss pass wrote dZ in both layouts and the bias gradient;
-                // fused layers: the consumer's dX epilogue wrote dZ and the column partials
-                const bool outl = L.dyc >= 0;
-                // dY -> dZ through ReLU and LayerNorm(+affine)
-                if (!(g.dbg & 8) && !outl && !L.fused) {
-                    if (F <= 128) bwd_rows<8>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c, colp_l);
-                    else bwd_rows<0>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
-                }
-                if (!outl && !L.fused) __syncthreads();
-                // bias / LN-affine gradients: column sums over the rows (fixed order);
-                // up to 8 feature groups summed before the first store
-                if (F <= 128 && !(g.dbg & 24) && !outl) {  // the row pass left per-wave partials in LDS
-                    for (int o = tid; o < F; o += kGT) {
-                        float sb = 0.f, sg = 0.f, sbe = 0.f;
-                        for (int w = 0; w < kGW; ++w) {
-                            sb += colp_l[w * F + o];
-                            sg += colp_l[(kGW + w) * F + o];
-                            sbe += colp_l[(2 * kGW + w) * F + o];
-                        }
-                        G[L.b + o] = sb;
-                        if (L.ln == 2) {
-                            G[L.g + o] = sg;
-                            G[L.be + o] = sbe;
-                        }
-                    }
-                }
-                for (int ob = 0; ob < ((g.dbg & 16) || F <= 128 || outl ? 0 : F); ob += 8 * 4 * kGW) {
-                    float rb_[8], rg_[8], rbe_[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int o = ob + 4 * kGW * k + 4 * wave + rq;
-                        const bool on = o < F;
-                        float sb = 0.f, sg = 0.f, sbe = 0.f;
-                        if (ob + 4 * kGW * k < F) {  // wave-uniform
-                            for (int b = sub; b < bsz; b += 16) {
-                                const size_t x = (size_t)(on ? o : 0) * bp + b;
-                                const float v0 = dzc[x];
-                                sb += on ? v0 : 0.f;
-                                if (L.ln == 2) {
-                                    const float v1 = t1c[x], v2 = t2c[x];
-                                    sg += on ? v1 : 0.f;
-                                    sbe += on ? v2 : 0.f;
-                                }
-                            }
-                        }
-                        rb_[k] = rsum16(sb);
-                        rg_[k] = L.ln == 2 ? rsum16(sg) : 0.f;
-                        rbe_[k] = L.ln == 2 ? rsum16(sbe) : 0.f;
-                    }
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int o = ob + 4 * kGW * k + 4 * wave + rq;
-                        if (o < F && sub == 0) {
-                            G[L.b + o] = rb_[k];
-                            if (L.ln == 2) {
-                                G[L.g + o] = rg_[k];
-                                G[L.be + o] = rbe_[k];
-                            }
-                        }
-                    }
-                }
-                // dW = dZ^T X (contraction over the rows), then dX = dZ W into the
-                // source's dY (one GEMM call site for both: instruction-cache footprint)
-                const float *xc = L.src < 0 ? base + g.oc : base + g.L[L.src].yc;
-                const int fin = L.fin;
-                for (int job = 0; job < (L.src >= 0 ? 2 : 1); ++job) {
-                    if (job) __syncthreads();  // the dW GEMM's last panels are still being read
-                    if (g.dbg & (job ? 4 : 2)) continue;
-                    const float *ga = job ? (outl ? base + L.dy : dzr) : (outl ? base + L.dyc : dzc);
-                    const float *gb = job ? base + L.wt : xc;
-                    const int lda = job ? F : bp, ldb = job ? F : bp;
-                    const int M = job ? bsz : F, K = job ? F : bsz;
-                    float *dst = job ? base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy) : G + L.w;
-                    if (job && L.fuse) {  // the source's dZ (other parity) from the epilogue
-                        const int s_ = L.src;
-                        gemm_nt<2>(ga, lda, gb, ldb, M, fin, K, lds, nullptr, [](int, int, float) {}, g.L[s_], base, pr,
-                                   bp, base + ((s_ & 1) ? g.dzr1 : g.dzr), base + ((s_ & 1) ? g.dzc1 : g.dzc),
-                                   colp + (s_ & 1) * 3 * kGW * 128);
-                    } else {
-                        gemm_nt(ga, lda, gb, ldb, M, fin, K, lds, nullptr,
-                                [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; }, L);
-                    }
-                }
-                __syncthreads();
-            }
-
+            minibatch_grads(g, base, base, pr, G, xobs, gact_e, gmask_e, grow_e, s0, bsz, inv_b, entp, lds, colp,
+                            colo, lsum, klsum);
             // ---- loss / kl, clip, Adam ------------------------------------------
             block_sum2(lsum, klsum, red);
             if (tid == 0) loss_total += lsum;
@@ -1045,6 +1075,302 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
         if (g.target_kl > 0.0 && kl_total / (double)n_done > g.target_kl) break;  // ppo.py:917-918
     }  // epochs
     if (tid == 0) {
+        if (g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)Ep);
+        if (g.kl_out) g.kl_out[p] = n_done ? (float)(kl_total / (double)n_done) : 0.f;
+        if (g.epochs_out) g.epochs_out[p] = epochs_done;
+        g.step[p] = step0 + n_done;
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Partnered runtime-shape learner: an agent's minibatch is split over K
+// workgroups ("partners", R rows each) that exchange gradients through L2,
+// the compiled learner's scheme (learner.hip) on a runtime layer list:
+//   1. each partner runs minibatch_grads over its rows into its own slab of
+//      the agent's exchange area (partial gradient row + loss / approx_kl);
+//   2. barrier 1, then reduce-scatter: partner kk sums the float4 chunks it
+//      owns ([kk cs, (kk + 1) cs)) over the K slabs in partner order, keeps the
+//      sums in the agent's sum slab and publishes per-wave partial two-group
+//      squared norms;
+//   3. barrier 2: every partner sums the K x 4 partial norms in one fixed
+//      order (identical clip coefficients everywhere) and runs Adam on its own
+//      chunks, writing the parameters, both Adam moments and the transposed
+//      weight copy (the dX operand, shared by the agent's partners);
+//   4. barrier 3 and an agent-scope acquire: the next update's plain loads of
+//      the parameters see every partner's chunks.
+// The K partners of an agent are placed on one XCD (block b -> agent b % Q,
+// partner b / Q, Q a multiple of 8); that is checked at run time from
+// HW_REG_XCC_ID, and a split placement publishes with an agent release (the
+// L2 write-back) before every ticket.  Barriers are tickets with bounded spins;
+// a timeout sets the caller's error word (AGX_LEARN_ERR_TIMEOUT) and the
+// partner exits.  An agent's result depends on K (the row split), never on
+// which other agents share the launch.
+// ---------------------------------------------------------------------------
+constexpr int kMaxGK = 16;
+constexpr unsigned kGSpinMax = 1u << 23;
+
+__device__ __forceinline__ bool gpart_sync(unsigned *ctr, unsigned target, bool release, unsigned *tmo,
+                                           unsigned *err, int *s_ok) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores have left
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (release) {  // partners on other XCDs: write this L2's dirty lines back first
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const unsigned before = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        int ok = 1;
+        while (before + 1u < target && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kGSpinMax) {
+                __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (err) __hip_atomic_fetch_or(err, AGX_LEARN_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+        }
+        *s_ok = ok;
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
+
+// this CU's L1 no longer holds lines other partners have rewritten (the
+// parameters after an Adam step): one agent-scope acquire, waited for by the
+// whole workgroup before its next plain loads
+__device__ __forceinline__ void gpart_acquire() {
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+__device__ __forceinline__ float ld_sc1(const float *p) {
+    return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g) {
+    __shared__ float red[2 * kGW];
+    __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
+    __shared__ float colp[2 * 3 * kGW * 128];
+    __shared__ float colo[kGW * 33];
+    __shared__ int s_ok;
+    if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
+    const int b = blockIdx.x;
+    const int p = b % g.Q, kk = b / g.Q;
+    if (p >= g.P) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int K = g.K, P = g.P, n = g.n, D = g.D;
+    const long long S = g.S;
+    float *const pr = g.params + (size_t)p * n;
+    float *const gm = g.m + (size_t)p * n;
+    float *const gv = g.v + (size_t)p * n;
+    float *const base = g.ws + ((size_t)p * K + kk) * g.ws_part;
+    float *const wsh = g.wtb + (size_t)p * g.wt_agent;  // the agent's shared transposed weights
+    float *const wb = wsh - g.wt0;                      // wb + L.wt lands in wsh
+    unsigned *const c0 = g.cnt + p, *const c1 = g.cnt + P + p, *const c2 = g.cnt + 2 * P + p;
+    unsigned *const c3 = g.cnt + 3 * P + p, *const tmo = g.cnt + 4 * P;
+    unsigned *const xcc = g.cnt + 4 * P + 1 + (size_t)p * kMaxGK;
+    // float4 ownership: chunks [own0, own1) of the n4s = n4 + 1 chunks (the
+    // gradient row padded to n4 chunks, then the loss / approx_kl chunk)
+    const int n4 = (n + 3) / 4, n4s = n4 + 1, nal = 4 * n4;
+    const int cs = (n4s + K - 1) / K;
+    const int own0 = kk * cs < n4s ? kk * cs : n4s, own1 = own0 + cs < n4s ? own0 + cs : n4s;
+    const int f0 = 4 * own0, f1 = 4 * own1 < n ? 4 * own1 : n;  // owned parameter floats
+
+    // placement id + the transposed copies of the owned weights, one setup barrier
+    if (tid == 0) {
+        int x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        __hip_atomic_store(xcc + kk, (unsigned)(x & 15) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (int l = 0; l < g.nl; ++l) {
+        const GLay &L = g.L[l];
+        if (L.wt < 0) continue;
+        const int cnt = L.fout * L.fin;
+        const int i0 = f0 - L.w > 0 ? f0 - L.w : 0, i1 = f1 - L.w < cnt ? f1 - L.w : cnt;
+        float *wt = wb + L.wt;
+        for (int i = i0 + tid; i < i1; i += kGT) {
+            const int o = i / L.fin, c = i - o * L.fin;
+            wt[(size_t)c * L.fout + o] = pr[L.w + i];
+        }
+    }
+    if (!gpart_sync(c0, (unsigned)K, true, tmo, g.err, &s_ok)) return;
+    bool local;
+    {
+        const unsigned v = lane < K ? __hip_atomic_load(xcc + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const unsigned v0 = __builtin_amdgcn_readlane(v, 0);
+        bool same = v0 != 0u;
+        for (int q = 1; q < K; ++q) same = same && __builtin_amdgcn_readlane(v, q) == v0;
+        local = same && !g.write_through;
+    }
+    gpart_acquire();
+
+    int Bp = g.batch_p ? g.batch_p[p] : g.B;
+    if (Bp > g.B) Bp = g.B;
+    const int Ep = g.epochs_p ? g.epochs_p[p] : g.E;
+    const float entp = g.ent_p ? g.ent_p[p] : g.ent;
+    const int nmb = (int)((S + Bp - 1) / Bp);
+    float loss_total = 0.f;
+    double kl_total = 0.0;
+    int n_done = 0, epochs_done = 0;
+    const long long step0 = g.step[p];
+    double pb1 = pow((double)g.b1, (double)step0), pb2 = pow((double)g.b2, (double)step0);
+    const float lr_p = g.lr[p];
+
+    for (int e = 0; e < Ep; ++e) {
+        const size_t ge = (size_t)e * P + p;
+        const float *gobs_e = g.gobs + ge * S * D;
+        const int *gact_e = g.gact + ge * S;
+        const unsigned *gmask_e = g.gmask ? g.gmask + ge * S : nullptr;
+        const float *grow_e = g.grow + ge * 4 * S;
+        for (int mb = 0; mb < nmb; ++mb) {
+            const long long s0 = (long long)mb * Bp;
+            const int bsz = (int)((s0 + Bp <= S) ? Bp : S - s0);
+            const float inv_b = 1.f / (float)bsz;
+            const int r0 = kk * g.R, rk = bsz - r0 < 0 ? 0 : (bsz - r0 < g.R ? bsz - r0 : g.R);
+            const int upd = e * nmb + mb;
+            float *const slab0 = g.slabs + ((size_t)p * 2 + (upd & 1)) * K * g.nslab;  // partner 0's slab
+            float *const G = slab0 + (size_t)kk * g.nslab;
+            float *const sum = g.sums + ((size_t)p * 2 + (upd & 1)) * g.nslab;
+
+            // ---- 1. this partner's rows -> its partial gradient row ----------------
+            float lsum = 0.f, klsum = 0.f;
+            if (rk > 0) {
+                minibatch_grads(g, base, wb, pr, G, gobs_e + (s0 + r0) * D, gact_e, gmask_e, grow_e, s0 + r0, rk,
+                                inv_b, entp, lds, colp, colo, lsum, klsum);
+            } else {  // no rows this minibatch (a short last minibatch): publish zeros
+                for (int i = tid; i < n; i += kGT) G[i] = 0.f;
+            }
+            block_sum2(lsum, klsum, red);
+            if (tid == 0) {
+                G[nal] = lsum;
+                G[nal + 1] = klsum;
+            }
+            if (!gpart_sync(c1, (unsigned)(K * (upd + 1)), !local, tmo, g.err, &s_ok)) return;
+
+            // ---- 2. reduce-scatter of the owned chunks + partial norms ---------------
+            float q0 = 0.f, q1 = 0.f;
+            {
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab0, 0, __builtin_amdgcn_readfirstlane(
+                                                                                 (int)(K * g.nslab * 4)), 0x00020000);
+                for (int c = own0 + tid; c < own1; c += kGT) {
+                    // partner order, 8 loads in flight at a time
+                    f4 t = f4{0.f, 0.f, 0.f, 0.f};
+                    for (int q0_ = 0; q0_ < K; q0_ += 8) {  // uniform
+                        f4 x[8];
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) {
+                            const int qq = q0_ + q, qs = qq < K ? qq : K - 1;
+                            const f4 v = __builtin_bit_cast(
+                                f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((qs * g.nslab + 4 * c) * 4), 0, 16));
+                            x[q] = qq < K ? v : f4{0.f, 0.f, 0.f, 0.f};
+                        }
+                        if (q0_ == 0) {
+                            t = x[0];
+#pragma unroll
+                            for (int q = 1; q < 8; ++q) t += x[q];
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) t += x[q];
+                        }
+                    }
+                    *reinterpret_cast<f4 *>(sum + 4 * c) = t;
+#pragma unroll
+                    for (int cc = 0; cc < 4; ++cc) {
+                        const int f = 4 * c + cc;
+                        const float x2 = f < n ? t[cc] * t[cc] : 0.f;
+                        if (f < g.cstart) q0 += x2;
+                        else q1 += x2;
+                    }
+                }
+                q0 = wave_sum(q0);
+                q1 = wave_sum(q1);
+                if (lane < 2) sum[nal + 4 + (kk * kGW + wave) * 2 + lane] = lane ? q1 : q0;
+            }
+            if (!gpart_sync(c2, (unsigned)(K * (upd + 1)), !local, tmo, g.err, &s_ok)) return;
+
+            // ---- 3. norms (fixed order), loss words, Adam on the owned floats ---------
+            float t0, t1, lmb, klmb;
+            {
+                const int np = 2 * kGW * K;  // <= 128 words: lanes l and l + 64
+                float v = 0.f;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int w = lane + 64 * h;
+                    const float x = ld_sc1(sum + nal + 4 + (w < np ? w : 0));
+                    v += w < np ? x : 0.f;
+                }
+                const float lw = ld_sc1(sum + nal), kw = ld_sc1(sum + nal + 1);
+                t0 = wave_sum((lane & 1) ? 0.f : v);
+                t1 = wave_sum((lane & 1) ? v : 0.f);
+                lmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(unsigned, lw)));
+                klmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(unsigned, kw)));
+            }
+            if (tid == 0) loss_total += lmb;
+            kl_total += (double)klmb;
+            ++n_done;
+            const float cl0 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t0) + 1e-6f), 1.f) : 1.f;
+            const float cl1 = g.max_norm > 0.f ? fminf(g.max_norm / (sqrtf(t1) + 1e-6f), 1.f) : 1.f;
+            pb1 *= (double)g.b1;
+            pb2 *= (double)g.b2;
+            const float bc1 = (float)(1.0 - pb1);
+            const float bc2s = (float)sqrt(1.0 - pb2);
+            const float step_size = lr_p / bc1;
+            const float ob1 = 1.f - g.b1, ob2 = 1.f - g.b2;
+            // the owned float range [f0, f1), region by region (per layer W with its
+            // transposed copy, b, LN weight, LN bias): all loads of a round first
+            auto adam_range = [&](int r0_, int cnt, long long wt, int fin, int fout) {
+                const int lo = f0 - r0_ > 0 ? f0 - r0_ : 0, hi = f1 - r0_ < cnt ? f1 - r0_ : cnt;
+                constexpr int U = 8;
+                for (int i0 = lo + tid; i0 < hi; i0 += U * kGT) {
+                    float gg[U], mm[U], vv[U], pp[U];
+#pragma unroll
+                    for (int k = 0; k < U; ++k) {
+                        const int i = i0 + k * kGT;
+                        const int f = r0_ + (i < hi ? i : lo);
+                        gg[k] = sum[f];  // this partner's own reduce-scatter stores
+                        mm[k] = gm[f];
+                        vv[k] = gv[f];
+                        pp[k] = pr[f];
+                    }
+#pragma unroll
+                    for (int k = 0; k < U; ++k) {
+                        const int i = i0 + k * kGT;
+                        if (i >= hi) break;
+                        const int f = r0_ + i;
+                        const float gc = gg[k] * (f < g.cstart ? cl0 : cl1);
+                        const float m = mm[k] + ob1 * (gc - mm[k]);
+                        const float v = vv[k] * g.b2 + ob2 * gc * gc;
+                        const float np_ = pp[k] - step_size * (m / (sqrtf(v) / bc2s + g.eps));
+                        gm[f] = m;
+                        gv[f] = v;
+                        pr[f] = np_;
+                        if (wt >= 0) {
+                            const int o = i / fin, c = i - o * fin;
+                            wb[wt + (size_t)c * fout + o] = np_;
+                        }
+                    }
+                }
+            };
+            for (int rg = 0; rg < 4 * g.nl; ++rg) {
+                const GLay &L = g.L[rg >> 2];
+                const int kind = rg & 3;
+                if (kind >= 2 && L.ln != 2) continue;
+                const int rf = kind == 0 ? L.w : kind == 1 ? L.b : kind == 2 ? L.g : L.be;
+                const int cnt = kind == 0 ? L.fout * L.fin : L.fout;
+                if (rf >= f1 || rf + cnt <= f0) continue;  // uniform: no owned float in the region
+                adam_range(rf, cnt, kind == 0 ? L.wt : -1, kind == 0 ? L.fin : 1, kind == 0 ? L.fout : 1);
+            }
+            // ---- 4. every partner's chunks visible to this one's next plain loads ---------
+            if (!gpart_sync(c3, (unsigned)(K * (upd + 1)), !local, tmo, g.err, &s_ok)) return;
+            gpart_acquire();
+        }  // minibatches
+        ++epochs_done;
+        if (g.target_kl > 0.0 && kl_total / (double)n_done > g.target_kl) break;  // ppo.py:917-918
+    }  // epochs
+    if (tid == 0 && kk == 0) {
         if (g.loss_out) g.loss_out[p] = loss_total / ((float)S * (float)Ep);
         if (g.kl_out) g.kl_out[p] = n_done ? (float)(kl_total / (double)n_done) : 0.f;
         if (g.epochs_out) g.epochs_out[p] = epochs_done;
@@ -1244,11 +1570,7 @@ int plan_graph(const agx_ppo_graph *net, int64_t batch, GArgs &a) {
             L.dy2 = off;
             off = r4(off + bp * x.fout);
         }
-        L.wt = -1;
-        if (x.src >= 0) {
-            L.wt = off;
-            off = r4(off + (long long)x.fin * x.fout);
-        }
+        L.wt = -1;  // allocated after the gradient row (below)
         L.dyc = -1;
         if (l == net->actor_out) {  // the value layer's (width 1) row- and feature-major forms coincide
             L.dyc = off;
@@ -1287,6 +1609,19 @@ int plan_graph(const agx_ppo_graph *net, int64_t batch, GArgs &a) {
     off = r4(off + bp * maxw);
     a.gr = off;
     off = r4(off + net->n_params);
+    // the transposed weights last: a partner's scratch is everything before the
+    // gradient row (its gradient goes to the exchange slab, the transposed
+    // weights are shared by the agent's partners)
+    a.ws_part = (a.gr + 63) & ~63ll;
+    a.wt0 = off;
+    for (int l = 0; l < nl; ++l) {
+        const agx_ppo_layer &x = net->layers[l];
+        if (x.src >= 0) {
+            a.L[l].wt = off;
+            off = r4(off + (long long)x.fin * x.fout);
+        }
+    }
+    a.wt_agent = ((off - a.wt0) + 63) & ~63ll;
     a.ws_agent = (off + 63) & ~63ll;  // 256-byte aligned agent blocks
     a.nl = nl;
     a.aout = net->actor_out;
@@ -1340,6 +1675,67 @@ GraphWs graph_ws(const GArgs &a, int64_t P, int64_t S, int64_t epochs) {
     return w;
 }
 
+// The partnered learner's split of a minibatch: K partners of R rows
+// (AGX_GRAPH_ROWS, default 16) while the whole grid (Q x K workgroups, Q = P
+// rounded up to the 8 XCDs) stays co-resident; K = 1: the one-workgroup-per-
+// agent kernel.  AGX_GRAPH_SPLIT caps K (tests, diagnostics).
+int cu_count_g() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                ? prop.multiProcessorCount
+                : 256;
+        if (n <= 0) n = 256;
+    }
+    return n;
+}
+int part_occupancy() {  // co-resident partner workgroups per CU (queried once)
+    static int n = -1;
+    if (n < 0) {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_learn_graph_part_kernel, kGT, 0) != hipSuccess) v = 1;
+        n = v < 1 ? 1 : v;
+    }
+    return n;
+}
+void graph_split(int64_t P, int64_t batch, int &K, int &R, int &Q) {
+    int rows = 16;
+    if (const char *e = getenv("AGX_GRAPH_ROWS")) rows = atoi(e) >= 1 ? atoi(e) : 16;
+    int k = (int)((batch + rows - 1) / rows);
+    int cap = kMaxGK;
+    if (const char *e = getenv("AGX_GRAPH_SPLIT")) cap = atoi(e) >= 1 ? atoi(e) : 1;
+    if (k > cap) k = cap;
+    Q = (int)((P + 7) / 8 * 8);
+    const int64_t resident = (int64_t)part_occupancy() * cu_count_g();
+    while (k > 1 && (int64_t)Q * k > resident) --k;
+    if (k > 1 && (int64_t)P * k > resident) k = 1;
+    K = k < 1 ? 1 : k;
+    R = (int)((batch + K - 1) / K);
+}
+struct PartWs {
+    size_t cnt, gobs, gact, gmask, grow, scratch, wt, slabs, sums, total;
+    long long nslab;
+};
+PartWs part_ws(const GArgs &a, int64_t P, int64_t S, int64_t epochs, int K) {
+    PartWs w;
+    const size_t per = (size_t)epochs * P * S;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    w.cnt = 0;
+    w.gobs = up(((size_t)4 * P + 1 + (size_t)kMaxGK * P) * 4);
+    w.gact = w.gobs + up(per * a.D * 4);
+    w.gmask = w.gact + up(per * 4);
+    w.grow = w.gmask + up(per * 4);
+    w.scratch = w.grow + up(per * 4 * 4);
+    w.wt = w.scratch + up((size_t)P * K * a.ws_part * 4);
+    w.nslab = ((long long)(a.n + 3) / 4 * 4 + 4 + 2 * kGW * K + 63) / 64 * 64;
+    w.slabs = w.wt + up((size_t)P * a.wt_agent * 4);
+    w.sums = w.slabs + up((size_t)P * 2 * K * w.nslab * 4);
+    w.total = w.sums + (size_t)P * 2 * w.nslab * 4;
+    return w;
+}
+
 }  // namespace
 }  // namespace agx
 
@@ -1354,8 +1750,18 @@ extern "C" size_t agx_ppo_learn_graph_workspace_bytes(const agx_ppo_graph *net, 
                                                       int64_t epochs, int64_t batch) {
     GArgs a{};
     if (P <= 0 || S <= 0 || epochs <= 0 || batch <= 0) return 0;
-    if (plan_graph(net, batch < S ? batch : S, a) != AGX_OK) return 0;
-    return graph_ws(a, P, S, epochs).total;
+    const int64_t bb = batch < S ? batch : S;
+    if (plan_graph(net, bb, a) != AGX_OK) return 0;
+    size_t total = graph_ws(a, P, S, epochs).total;
+    int K, R, Q;
+    graph_split(P, bb, K, R, Q);
+    if (K > 1) {  // room for either kernel: the split may change with the call's batch
+        GArgs ap{};
+        if (plan_graph(net, R, ap) != AGX_OK) return 0;
+        const size_t t = part_ws(ap, P, S, epochs, K).total;
+        total = t > total ? t : total;
+    }
+    return total;
 }
 
 extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn_args *x, void *workspace,
@@ -1368,25 +1774,41 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
     AGX_REQUIRE(P > 0 && P <= 65535 && S > 0 && S < (1ll << 31) && epochs > 0 && batch > 0 && epochs * P <= 65535,
                 "agx_ppo_learn_graph: bad sizes P=%lld S=%lld epochs=%lld batch=%lld", (long long)P, (long long)S,
                 (long long)epochs, (long long)batch);
+    const int64_t bb = batch < S ? batch : S;
+    int K = 1, R = (int)bb, Q = (int)P;
+    graph_split(P, bb, K, R, Q);
     GArgs a{};
-    const int rc = plan_graph(net, batch < S ? batch : S, a);
+    const int rc = plan_graph(net, K > 1 ? R : bb, a);
     if (rc != AGX_OK) return rc;
-    const GraphWs w = graph_ws(a, P, S, epochs);
     char *ws = static_cast<char *>(workspace);
     hipStream_t s = as_stream(stream);
-    float *gobs = reinterpret_cast<float *>(ws + w.gobs);
-    int *gact = reinterpret_cast<int *>(ws + w.gact);
-    unsigned *gmask = x->action_masks ? reinterpret_cast<unsigned *>(ws + w.gmask) : nullptr;
-    float *grow = reinterpret_cast<float *>(ws + w.grow);
+    size_t o_gobs, o_gact, o_gmask, o_grow;
+    unsigned *counters = nullptr;
+    int ncounters = 0;
+    PartWs pw{};
+    GraphWs w{};
+    if (K > 1) {
+        pw = part_ws(a, P, S, epochs, K);
+        o_gobs = pw.gobs, o_gact = pw.gact, o_gmask = pw.gmask, o_grow = pw.grow;
+        counters = reinterpret_cast<unsigned *>(ws + pw.cnt);
+        ncounters = (int)(pw.gobs / sizeof(unsigned));
+    } else {
+        w = graph_ws(a, P, S, epochs);
+        o_gobs = w.gobs, o_gact = w.gact, o_gmask = w.gmask, o_grow = w.grow;
+    }
+    float *gobs = reinterpret_cast<float *>(ws + o_gobs);
+    int *gact = reinterpret_cast<int *>(ws + o_gact);
+    unsigned *gmask = x->action_masks ? reinterpret_cast<unsigned *>(ws + o_gmask) : nullptr;
+    float *grow = reinterpret_cast<float *>(ws + o_grow);
     dim3 ggrid((unsigned)ceil_div(S, 256), (unsigned)(epochs * P));
     ppo_gather_kernel<<<ggrid, 256, 0, s>>>(x->obs, reinterpret_cast<const long long *>(x->actions), x->old_logp,
                                             x->adv, x->ret, x->old_value, x->adv_stats,
                                             reinterpret_cast<const long long *>(x->perms), x->action_masks, a.A, S,
-                                            a.D, (int)P, gobs, gact, gmask, grow, nullptr, 0, x->epochs_per_agent,
-                                            x->error_word);
+                                            a.D, (int)P, gobs, gact, gmask, grow, counters, ncounters,
+                                            x->epochs_per_agent, x->error_word);
     const int rc2 = check_launch("agx_ppo_learn_graph gather");
     if (rc2) return rc2;
-    a.ws = reinterpret_cast<float *>(ws + w.agents);
+    a.ws = reinterpret_cast<float *>(ws + (K > 1 ? pw.scratch : w.agents));
     a.params = x->params;
     a.m = x->exp_avg;
     a.v = x->exp_avg_sq;
@@ -1419,7 +1841,26 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
         const char *d = getenv("AGX_GRAPH_DEBUG");
         a.dbg = d ? atoi(d) : 0;
     }
-    ppo_learn_graph_kernel<<<(unsigned)P, kGT, 0, s>>>(a);
+    a.err = x->error_word;
+    if (K > 1) {
+        a.dbg = 0;  // phase skips: the one-workgroup kernel only
+        a.K = K;
+        a.R = R;
+        a.Q = Q;
+        a.nslab = pw.nslab;
+        a.wtb = reinterpret_cast<float *>(ws + pw.wt);
+        a.slabs = reinterpret_cast<float *>(ws + pw.slabs);
+        a.sums = reinterpret_cast<float *>(ws + pw.sums);
+        a.cnt = counters;
+        {
+            const char *wt = getenv("AGX_LEARN_WRITETHROUGH");
+            a.write_through = wt && atoi(wt) != 0;
+        }
+        AGX_REQUIRE((int64_t)Q * K <= 65535, "agx_ppo_learn_graph: too many workgroups");
+        ppo_learn_graph_part_kernel<<<(unsigned)(Q * K), kGT, 0, s>>>(a);
+    } else {
+        ppo_learn_graph_kernel<<<(unsigned)P, kGT, 0, s>>>(a);
+    }
     return check_launch("agx_ppo_learn_graph");
 }
 

@@ -52,6 +52,18 @@
 
 namespace agx {
 
+// Partner ownership of the parameter image: uniform chunks (1, default) or the
+// proportional n4s * kk / K split of rounds 2-4 (0; A/B builds)
+#ifndef AGX_LEARN_UNIFORM
+#define AGX_LEARN_UNIFORM 1
+#endif
+// Reduce-scatter over all 8 waves (two partner halves per owned chunk, summed
+// lower + upper through LDS; 1) or one thread per owned chunk over all K
+// partners (0, default: measured 1.116 vs 1.133 ms per learn() on one box)
+#ifndef AGX_LEARN_RS2
+#define AGX_LEARN_RS2 0
+#endif
+
 constexpr int kNT = 512;
 constexpr int kNW = kNT / kWave;  // 8 waves
 constexpr int kSB = 32;           // rows per sub-batch
@@ -750,7 +762,15 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
     // i.e. slot i is float (i & 3) of chunk oc0 + tid + kNT*(i >> 2).  K == 1:
     // every chunk, thread t owning t, t + kNT, ...
     constexpr int n4 = pl.param_end / 4, n4s = n4 + 1;
+#if AGX_LEARN_UNIFORM
+    // uniform chunks of cs = ceil(n4s / K): chunk c belongs to partner c / cs,
+    // which the parameter hand-off computes per chunk without a table
+    const int cs = (n4s + g.K - 1) / g.K;
+    int oc0 = kk * cs < n4s ? kk * cs : n4s, oc1 = oc0 + cs < n4s ? oc0 + cs : n4s;
+    const float inv_cs = 1.f / (float)cs;  // c / cs = floor((c + 0.5) * inv_cs) exactly for c < 2^16
+#else
     int oc0 = n4s * kk / g.K, oc1 = n4s * (kk + 1) / g.K;
+#endif
     int pc1 = oc1 < n4 ? oc1 : n4;  // own parameter chunks [oc0, pc1)
     constexpr int kUsed4 = JN > 0 ? JN : (n4 + kNT - 1) / kNT;  // owned chunk rounds per thread, at most
     static_assert(pl.param_end % 4 == 0 && pl.slab >= pl.param_end + 4 + 2 * kNW * kMaxK, "sum slab layout");
@@ -1528,6 +1548,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 block_sum2(lmb, klmb, stat, 2, lane, wave);
             }
             float gr[kMaxPT];  // summed gradients of the owned slots
+            constexpr int NQ = (2 * kNW * KM + 63) / 64;
+            float vq[NQ];  // partners: this lane's words of the published partial norms
             if (g.K > 1) {
                 // ---- P9b: exchange partial gradients with the agent's partners --------
                 // every gradient word went out as a write-through (sc1) store from the
@@ -1548,8 +1570,49 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     // one buffer descriptor over the K consecutive slabs
                     const auto rs = __builtin_amdgcn_make_buffer_rsrc(
                         base, 0, __builtin_amdgcn_readfirstlane(g.K * pl.slab * 4), 0x00020000);
+                    bool rs_done = false;
+#if AGX_LEARN_RS2
+                    // all 8 waves load: thread t sums chunk oc0 + (t mod kNT/2) over one
+                    // half of the partners (half t / (kNT/2): partners [KM/2 h, KM/2 h +
+                    // KM/2), in order), the upper half hands its sum over through the
+                    // dead activation region of LDS, and the owner adds the two halves
+                    // (fixed order: lower + upper)
+                    if constexpr (JN == 1) {
+                        if (oc1 - oc0 <= kNT / 2) {  // workgroup-uniform
+                            constexpr int KH = KM / 2;
+                            const int h = tid >= kNT / 2 ? 1 : 0;
+                            const int c = oc0 + (tid & (kNT / 2 - 1));
+                            const int cl = c < oc1 ? c : oc0;
+                            f4 x[KH];
+#pragma unroll
+                            for (int q = 0; q < KH; ++q) {
+                                const int qq = KH * h + q, qs = qq < g.K ? qq : g.K - 1;
+                                const f4 v = __builtin_bit_cast(
+                                    f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (qs * pl.slab + 4 * cl) * 4, 0, 16));
+                                x[q] = qq < g.K ? v : f4{0.f, 0.f, 0.f, 0.f};
+                            }
+                            f4 t = x[0];
+#pragma unroll
+                            for (int q = 1; q < KH; ++q) t += x[q];
+                            f4 *xch = reinterpret_cast<f4 *>(sm + pl.l_x0);
+                            if (h) xch[tid - kNT / 2] = t;
+                            __syncthreads();
+                            if (!h) {
+                                t += xch[tid];
+                                if (c == n4) {  // the loss / approx_kl chunk: every partner reads it
+                                    if (local) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 0);
+                                    else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, t), sum_rsrc, c * 16, 0, 16);
+                                }
+                            }
+#pragma unroll
+                            for (int cc = 0; cc < 4; ++cc) gr[cc] = (!h && c < pc1) ? t[cc] : 0.f;
+                            rs_done = true;
+                        }
+                    }
+#endif
 #pragma unroll
                     for (int j = 0; j < kUsed4; ++j) {
+                        if (rs_done) break;  // uniform
                         const int c = oc0 + tid + kNT * j;
                         f4 t = f4{0.f, 0.f, 0.f, 0.f};
                         if (j >= jn_own) {  // uniform: no thread owns round j
@@ -1601,12 +1664,26 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 }
                 AGX_STAMP(64 + 13);
                 if (!partner_sync(ctr2, (unsigned)(g.K * (upd + 1)), 64 + 8, 64 + 15)) return;
+                // ONE round trip for everything the second barrier published: the
+                // K x kNW per-wave partial norms (unconditional loads; the slab
+                // always holds the kMaxK-partner area, words past this split's are
+                // masked) and the minibatch loss / approx_kl words
+                {
+                    const int lane = vlane();
+                    const int np = 2 * kNW * g.K;  // <= 256: word lane + 64 q holds [partner][wave][group]
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const float x = __builtin_bit_cast(
+                            float, __builtin_amdgcn_raw_buffer_load_b32(sum_rsrc, (pl.param_end + 4 + 64 * q + lane) * 4, 0, 16));
+                        vq[q] = lane + 64 * q < np ? x : 0.f;
+                    }
+                }
                 // the minibatch loss and approx_kl: partner-order sums of the K words
                 // (uniform: the early-stop branch depends on it)
-                lmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
-                                                    __builtin_amdgcn_raw_buffer_load_b32(sum_rsrc, pl.param_end * 4, 0, 16)));
-                klmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b32(
-                                                     sum_rsrc, (pl.param_end + 1) * 4, 0, 16)));
+                const unsigned lw = __builtin_amdgcn_raw_buffer_load_b32(sum_rsrc, pl.param_end * 4, 0, 16);
+                const unsigned kw = __builtin_amdgcn_raw_buffer_load_b32(sum_rsrc, (pl.param_end + 1) * 4, 0, 16);
+                lmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(lw));
+                klmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(kw));
             }
 
             // ---- P10: two-group norm, Adam from registers -------------------------
@@ -1651,19 +1728,13 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 }
             } else {
                 // the K x kNW per-wave partials of both groups from the sum slab
-                // ([partner][wave][group]: group = index parity), summed in one
-                // fixed order by every wave of every partner -> identical clip
+                // ([partner][wave][group]: group = index parity, loaded right after the
+                // second barrier), summed in one fixed order by every wave of every
+                // partner -> identical clip
                 const int lane = vlane();
-                const int np = 2 * kNW * g.K;  // <= 256: word lane + 64 q holds [partner][wave][group]
-                float vq[(2 * kNW * KM + 63) / 64];
-#pragma unroll
-                for (int q = 0; q < (2 * kNW * KM + 63) / 64; ++q)
-                    vq[q] = lane + 64 * q < np ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                                            sum_rsrc, (pl.param_end + 4 + 64 * q + lane) * 4, 0, 16))
-                                               : 0.f;
                 float v = vq[0];
 #pragma unroll
-                for (int q = 1; q < (2 * kNW * KM + 63) / 64; ++q) v += vq[q];
+                for (int q = 1; q < NQ; ++q) v += vq[q];
                 const float x0 = row_sum((lane & 1) ? 0.f : v), x1 = row_sum((lane & 1) ? v : 0.f);
                 t0 = readlane_f(x0, 0) + readlane_f(x0, 16) + readlane_f(x0, 32) + readlane_f(x0, 48);
                 t1 = readlane_f(x1, 0) + readlane_f(x1, 16) + readlane_f(x1, 32) + readlane_f(x1, 48);
@@ -1741,6 +1812,26 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                 const int tid = vtid();
                 const auto rs = __builtin_amdgcn_make_buffer_rsrc(
                     base, 0, __builtin_amdgcn_readfirstlane(g.K * pl.slab * 4), 0x00020000);
+#if AGX_LEARN_UNIFORM
+                // every thread of the workgroup takes chunks tid, tid + kNT, ...
+                // of the whole image from their owners' slabs: all loads issued
+                // unconditionally (the clamped chunk of a thread past the image
+                // re-reads a valid word), then the other partners' chunks -> LDS
+                constexpr int NR = (n4 + kNT - 1) / kNT;
+                f4 x[NR];
+#pragma unroll
+                for (int j = 0; j < NR; ++j) {
+                    const int c0 = tid + kNT * j, c = c0 < n4 ? c0 : n4 - 1;
+                    const int q = (int)(((float)c + 0.5f) * inv_cs);
+                    x[j] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (q * pl.slab + 4 * c) * 4, 0, 16));
+                }
+#pragma unroll
+                for (int j = 0; j < NR; ++j) {
+                    const int c = tid + kNT * j;
+                    const int q = (int)(((float)c + 0.5f) * inv_cs);
+                    if (c < n4 && q != kk) sm4[c] = x[j];
+                }
+#else
                 // round r: chunk qc0 + tid + kNT*r of every other partner q, all loads in flight
                 const int span = (n4s + g.K - 1) / g.K + 1;
                 for (int r0 = 0; r0 < span; r0 += kNT) {
@@ -1759,6 +1850,7 @@ __global__ __launch_bounds__(kNT, 1) void ppo_learn_kernel(LearnArgs g) {
                     for (int q = 0; q < KM; ++q)
                         if (cq[q] >= 0) sm4[cq[q]] = x[q];
                 }
+#endif
                 AGX_STAMP(64 + 2);
             }
             __syncthreads();
@@ -2182,13 +2274,22 @@ static void launch_act(const ActArgs &a, dim3 grid, size_t lds, hipStream_t s) {
     ppo_act_kernel<C><<<grid, kNT, lds, s>>>(a);
 }
 
+// Co-resident persistent workgroups per CU, queried once per shape: a launch
+// may be issued while another persistent launch (a group evaluated in lock
+// step) waits for the host, so the launch path calls nothing that could wait
+// for the device.
 template <class C>
 static int persist_occupancy(size_t lds) {
+    static size_t cached_lds = 0;
+    static int cached = -1;
+    if (cached >= 0 && cached_lds == lds) return cached;
     (void)hipFuncSetAttribute((const void *)ppo_rollout_persistent_kernel<C>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ppo_rollout_persistent_kernel<C>, kNT, lds) != hipSuccess)
         return 0;
+    cached_lds = lds;
+    cached = n;
     return n;
 }
 

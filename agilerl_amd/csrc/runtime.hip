@@ -114,6 +114,16 @@ extern "C" int agx_host_free(void *ptr) {
     return AGX_OK;
 }
 
+extern "C" void *agx_stream_create(void) {
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        agx::set_error("agx_stream_create: hipStreamCreateWithFlags failed");
+        return nullptr;
+    }
+    return s;
+}
+
 extern "C" int agx_host_signal(agx_rollout_ctl *ctl, uint32_t seq) {
     AGX_REQUIRE(ctl, "agx_host_signal: null ctl");
     const unsigned nwg = __atomic_load_n(&ctl->nwg, __ATOMIC_RELAXED);

@@ -256,8 +256,12 @@ class PopulationEngine:
         acc = {id(g): np.zeros(g.pop.P) for g in self.groups}
         for g in self.groups:
             g.pop.eval_rounds = self._eval_calls
+        # a group on the PyTorch policy step allocates while it steps: persistent
+        # launches of the other groups (which wait for the host) only without one
+        allow = all(g.pop.fused_descriptor() is not None or g.pop.learn_descriptor() is not None
+                    for g in self.groups)
         for k in range(loop):
-            drivers = [(g, _EvalDriver(g.runner, k, max_steps)) for g in self.groups]
+            drivers = [(g, _EvalDriver(g.runner, k, max_steps, allow_persistent=allow)) for g in self.groups]
             run_lockstep([d for _, d in drivers])
             for g, d in drivers:
                 acc[id(g)] += d.result()

@@ -256,12 +256,11 @@ def policy_step(pop, desc: AgxPPONet, obs: torch.Tensor, obs_agent_stride: int, 
               _lib.ptr(actions_flat), pop.env_base_d.data_ptr(), _lib.stream())
 
 
-def policy_step_graph(pop, desc: AgxPPOGraph, obs: torch.Tensor, obs_agent_stride: int, *, sample: bool,
-                      counter: int, actions=None, log_probs=None, values=None, entropy=None,
-                      out_agent_stride: int = 0, actions_flat=None, action_mask=None,
-                      mask_agent_stride: int = 0) -> None:
-    """agx_ppo_act_graph over all P agents x N envs: the policy step of
-    policy_step for a mutated (runtime-shape) network, same Philox stream."""
+def graph_act_workspace(pop, desc: AgxPPOGraph):
+    """(desc, scratch) of agx_ppo_act_graph for this population, allocated on
+    first use.  Callers that keep a persistent launch resident (lock-stepped
+    evaluation) take it before launching: an allocation can wait for the
+    device."""
     ws = getattr(pop, "_act_ws", None)
     if ws is None or ws[0] is not desc:
         lib = _lib.load()
@@ -269,6 +268,16 @@ def policy_step_graph(pop, desc: AgxPPOGraph, obs: torch.Tensor, obs_agent_strid
         if nbytes == 0:
             raise _lib.AgxError(f"agx_ppo_act_graph_workspace_bytes: {lib.agx_last_error().decode()}")
         ws = pop._act_ws = (desc, torch.empty(nbytes, dtype=torch.uint8, device=pop.device))
+    return ws
+
+
+def policy_step_graph(pop, desc: AgxPPOGraph, obs: torch.Tensor, obs_agent_stride: int, *, sample: bool,
+                      counter: int, actions=None, log_probs=None, values=None, entropy=None,
+                      out_agent_stride: int = 0, actions_flat=None, action_mask=None,
+                      mask_agent_stride: int = 0) -> None:
+    """agx_ppo_act_graph over all P agents x N envs: the policy step of
+    policy_step for a mutated (runtime-shape) network, same Philox stream."""
+    ws = graph_act_workspace(pop, desc)
     _lib.call("agx_ppo_act_graph", ctypes.byref(desc), pop.P, pop.N, pop.params.data.data_ptr(), obs.data_ptr(),
               obs_agent_stride, _lib.ptr(action_mask), mask_agent_stride, 1 if sample else 0, pop.act_seed, counter,
               _lib.ptr(actions), _lib.ptr(log_probs), _lib.ptr(values), _lib.ptr(entropy), out_agent_stride,

@@ -390,8 +390,7 @@ class PopulationRunner:
         """Coherent host buffers of the persistent evaluation (allocated on
         first use): packed obs / reward / done staging, actions, a control
         block of its own and the per-step arguments of one launch, plus the
-        side stream its launches run on (groups evaluated in lock step each
-        keep a persistent launch resident, so they cannot share a stream)."""
+        stream is assigned by run_lockstep)."""
         if getattr(self, "_eval_bufs", None) is None:
             pop = self.pop
             P, N, D = pop.P, pop.N, pop.spec.obs_dim
@@ -400,7 +399,7 @@ class PopulationRunner:
             act = _coherent(self, P * N * 8).view(torch.int64)
             ctl = _coherent(self, int(lib.agx_rollout_ctl_bytes(P, N)))
             args = _coherent(self, int(lib.agx_rollout_args_bytes(_EVAL_CHUNK)))
-            self._eval_bufs = (obs, rew, done, act, ctl, args, torch.cuda.Stream(device=pop.device))
+            self._eval_bufs = (obs, rew, done, act, ctl, args)
         return self._eval_bufs
 
     def after_evaluation(self) -> None:
@@ -471,7 +470,7 @@ class _EvalDriver:
     (agx_ppo_eval_persistent) and paces it through its own control block;
     otherwise one policy-step launch + event wait per step."""
 
-    def __init__(self, runner: "PopulationRunner", k: int, max_steps: int | None):
+    def __init__(self, runner: "PopulationRunner", k: int, max_steps: int | None, allow_persistent: bool = True):
         self.runner, self.pop, self.env = runner, runner.pop, runner.env
         pop = self.pop
         P, N, D = pop.P, pop.N, pop.spec.obs_dim
@@ -480,14 +479,15 @@ class _EvalDriver:
         self.counter0 = (1 << 41) + (int(pop.eval_rounds) << 24) + (k << 20)
         self.desc = pop.fused_descriptor()
         self.gdesc = pop.learn_descriptor() if self.desc is None else None
-        self.persistent = bool(runner.persistent and self.desc is not None)
+        self.persistent = bool(allow_persistent and runner.persistent and self.desc is not None)
         self.step = 0
         self.scores = np.zeros(P * N)
         self.completed = np.zeros(P * N)
         self.finished = np.zeros(P * N, dtype=bool)
         if self.persistent:
             st = runner._eval_staging()
-            self.obs_h, self.rew_h, self.done_h, self.act_h, self.ctl_h, self.args_h, self.stream = st
+            self.obs_h, self.rew_h, self.done_h, self.act_h, self.ctl_h, self.args_h = st
+            self.stream = None  # a dedicated stream, assigned by run_lockstep
             self.launched_to = 0  # steps covered by launches so far (0: no launch resident)
         else:
             self.act_d = torch.empty(P * N, dtype=torch.int64, device=pop.device)
@@ -495,12 +495,21 @@ class _EvalDriver:
             self.obs_h = torch.empty(P * N * D, dtype=pop.obs.dtype, pin_memory=True)
             self.obs_d = torch.empty(P, N, D, dtype=pop.obs.dtype, device=pop.device)
             self.ev = torch.cuda.Event()
+            if self.gdesc is not None:  # its scratch now: nothing may allocate while a persistent launch waits
+                from .learner import graph_act_workspace
+
+                graph_act_workspace(self.pop, self.gdesc)
         self.obs = None
 
     # -- lock-step protocol -------------------------------------------------
     def begin(self) -> None:
         if self.persistent:
             self.env.reset(out_obs=self.obs_h.numpy())
+            # the side stream starts after everything queued so far (the learner
+            # that wrote the parameters).  Ordered here, before any group's
+            # persistent launch is resident: nothing after a launch may wait for
+            # the device while the host is pacing it
+            self.stream.wait_stream(torch.cuda.current_stream(self.pop.device))
         else:
             self.obs, _ = self.env.reset()
 
@@ -512,9 +521,6 @@ class _EvalDriver:
         pop = self.pop
         n = _EVAL_CHUNK if self.max_steps is None else min(_EVAL_CHUNK, int(self.max_steps) - self.step)
         self.ctl_h.zero_()
-        # the side stream starts after everything queued so far (the learner
-        # that wrote the parameters)
-        self.stream.wait_stream(torch.cuda.current_stream(pop.device))
         _lib.check(lib.agx_ppo_eval_persistent(ctypes.byref(self.desc), self.P, self.N, pop.params.data.data_ptr(),
                                                self.obs_h.data_ptr(), None, self.act_h.data_ptr(),
                                                pop.env_base_d.data_ptr(), n, 0, pop.act_seed,
@@ -616,6 +622,21 @@ class _EvalDriver:
 
 AGX_ROLLOUT_STOP = 0xFFFFFFFE  # include/agx.h
 
+# Dedicated non-blocking streams for persistent evaluation launches, one per
+# lock-stepped group, created once per process (agx_stream_create).  Not from
+# torch's stream pool: its round-robin could hand two groups the same stream,
+# and one resident persistent launch would then hold the other's back.
+_EVAL_STREAMS: list = []
+
+
+def _eval_stream(i: int):
+    while len(_EVAL_STREAMS) <= i:
+        h = _lib.load().agx_stream_create()
+        if not h:
+            raise _lib.AgxError(_lib.load().agx_last_error().decode(errors="replace"))
+        _EVAL_STREAMS.append(torch.cuda.ExternalStream(h))
+    return _EVAL_STREAMS[i]
+
 
 def run_lockstep(drivers: list) -> None:
     """Step several groups' evaluation passes together: every vector step
@@ -623,8 +644,13 @@ def run_lockstep(drivers: list) -> None:
     the groups' device work and host env steps overlap instead of running
     one pass after another."""
     active = list(drivers)
+    k = 0
+    for d in active:
+        if d.persistent:
+            d.stream = _eval_stream(k)
+            k += 1
     try:
-        for d in active:
+        for d in active:  # every group's stream ordering first, then the launches
             d.begin()
         while active:
             for d in active:

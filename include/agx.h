@@ -320,6 +320,11 @@ int agx_host_shuffle_perms(uint32_t *mt_key, int32_t *mt_pos, int64_t P, int64_t
  * address; NULL on failure. */
 void *agx_host_alloc(size_t bytes);
 int agx_host_free(void *ptr);
+/* A dedicated non-blocking stream (hipStreamNonBlocking: never ordered with
+ * the legacy NULL stream) for a persistent launch that must run beside
+ * others — the groups of an evaluation paced in lock step each keep one
+ * resident, so each needs a stream of its own.  NULL on failure. */
+void *agx_stream_create(void);
 /* release-store seq into ctl->seq and every workgroup's release line */
 int agx_host_signal(agx_rollout_ctl *ctl, uint32_t seq);
 /* spin until every done word >= target; AGX_EHIP on ctl->timeout or after

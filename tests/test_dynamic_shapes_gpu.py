@@ -133,23 +133,27 @@ def test_regroup_keeps_the_mutated_weights():
     assert arch.METHODS  # module imported
 
 
-@pytest.mark.parametrize("learner", ["graph", "torch"])
-def test_grouped_learner_single_update_on_mutated_shape(learner):
-    """The runtime-shape HIP learner (agx_ppo_learn_graph, what learn() runs
-    on a mutated shape) and the autograd learner, each against the oracle."""
-    from agilerl_amd.population.learner import GraphLearner, fused_learn
+# mutated shapes (population/arch.py: encoder / head nodes +-16/32/64, latent
+# +-8/16/32, new layers): (encoder hidden, latent, actor head, critic head)
+_MUTATED = {
+    "three_mutations": ([80], 72, [64, 64], [64, 64]),  # encoder node, latent node, head layer
+    "width_500": ([500], 64, [64], [64]),                 # the node cap (max_mlp_nodes 500)
+    "three_layer_encoder": ([64, 96, 64], 56, [64], [80]),
+}
+
+
+def _mutated_population(shape, P, N, T, batch, epochs, lr, seed=3):
     from agilerl_amd.population.nets import ActorCriticSpec
     from agilerl_amd.population.ppo_pop import PPOPopulation
-    from oracle.ppo_learn import ActorCritic, reference_learn
 
-    # a shape three mutations away from ppo.yaml's: encoder node, latent node, head layer
-    spec = ActorCriticSpec(obs_dim=8, n_actions=4, encoder_hidden=[80], latent_dim=72, actor_hidden=[64, 64],
-                           critic_hidden=[64, 64], encoder_name="encoder")
-    P, N, T, lr = 2, 16, 8, 1e-3
+    enc, lat, ah, ch = shape
+    spec = ActorCriticSpec(obs_dim=8, n_actions=4, encoder_hidden=list(enc), latent_dim=lat, actor_hidden=list(ah),
+                           critic_hidden=list(ch), encoder_name="encoder")
     S = T * N
-    pop = PPOPopulation(spec, P, N, learn_step=S, batch_size=S, update_epochs=1, lr=lr, seeds=[4, 5], device=DEV)
-    assert pop.fused_descriptor() is None  # the grouped autograd learner runs this shape
-    g = torch.Generator(device=DEV).manual_seed(3)
+    pop = PPOPopulation(spec, P, N, learn_step=S, batch_size=batch, update_epochs=epochs, lr=lr,
+                        seeds=[4 + i for i in range(P)], device=DEV)
+    assert pop.fused_descriptor() is None  # not a compiled shape
+    g = torch.Generator(device=DEV).manual_seed(seed)
     pop.obs.copy_(torch.randn(pop.obs.shape, device=DEV, generator=g))
     pop.actions.copy_(torch.randint(0, 4, pop.actions.shape, device=DEV, generator=g))
     pop.log_probs.copy_(-torch.rand(pop.log_probs.shape, device=DEV, generator=g) * 2 - 0.2)
@@ -162,6 +166,44 @@ def test_grouped_learner_single_update_on_mutated_shape(learner):
     pop.opt.exp_avg.copy_(torch.randn(P, n, device=DEV, generator=g) * 1e-3)
     pop.opt.exp_avg_sq.copy_(torch.rand(P, n, device=DEV, generator=g) * 1e-5 + 1e-7)
     pop.opt.steps.fill_(7)
+    return pop
+
+
+def _oracle_learn(pop, shape, p, init, m0, v0, raw_adv, perms, batch, epochs, lr, dtype=torch.float32):
+    from oracle.ppo_learn import ActorCritic, reference_learn
+
+    enc, lat, ah, ch = shape
+    keys = pop.spec.state_dict_keys()
+    S = pop.S
+    net = ActorCritic(8, 4, list(enc), lat, list(ah), list(ch))
+    sd = {k: init[p, o:o + int(np.prod(sh))].view(sh).cpu() for k, (o, sh) in keys.items()
+          if not k.startswith("critic.encoder.")}
+    net.load_reference(sd)
+    if dtype == torch.float64:
+        net = net.double()
+    nd = np.float64 if dtype == torch.float64 else np.float32
+    adam = {k: (m0[p, o:o + int(np.prod(sh))].view(sh).cpu().numpy().astype(nd),
+                v0[p, o:o + int(np.prod(sh))].view(sh).cpu().numpy().astype(nd))
+            for k, (o, sh) in keys.items() if not k.startswith("critic.encoder.")}
+    adam["step"] = 7
+    return reference_learn(net, adam, pop.obs[p].reshape(S, -1).cpu().numpy(), pop.actions[p].reshape(-1).cpu().numpy(),
+                           pop.log_probs[p].reshape(-1).cpu().numpy(), raw_adv[p].reshape(-1).cpu().numpy(),
+                           pop.returns[p].reshape(-1).cpu().numpy(), pop.values[p].reshape(-1).cpu().numpy(),
+                           perms[:, p].cpu().numpy(), batch_size=batch, epochs=epochs, lr=lr, dtype=dtype)
+
+
+@pytest.mark.parametrize("shape", sorted(_MUTATED))
+@pytest.mark.parametrize("learner", ["graph", "torch"])
+def test_grouped_learner_single_update_on_mutated_shape(learner, shape):
+    """The runtime-shape HIP learner (agx_ppo_learn_graph, what learn() runs
+    on a mutated shape) and the autograd learner, each against the oracle
+    (oracle/ppo_learn.reference_learn), on several mutated shapes: one full-
+    batch update from a mid-training Adam state."""
+    from agilerl_amd.population.learner import GraphLearner, fused_learn
+
+    P, N, T, lr = 2, 16, 8, 1e-3
+    S = T * N
+    pop = _mutated_population(_MUTATED[shape], P, N, T, S, 1, lr)
     init, m0, v0 = (x.clone() for x in (pop.params.data, pop.opt.exp_avg, pop.opt.exp_avg_sq))
     raw_adv = pop.advantages.clone()
     perms = torch.arange(S, device=DEV).repeat(1, P, 1).contiguous()
@@ -172,7 +214,7 @@ def test_grouped_learner_single_update_on_mutated_shape(learner):
     else:
         pop._learn_torch(perms)
     torch.cuda.synchronize()
-    keys = spec.state_dict_keys()
+    keys = pop.spec.state_dict_keys()
 
     def close(name, got, want, rtol):
         got, want = got.double().numpy().ravel(), want.double().numpy().ravel()
@@ -180,19 +222,7 @@ def test_grouped_learner_single_update_on_mutated_shape(learner):
         assert bad.mean() <= 1e-4, (name, int(bad.sum()), want.size)
 
     for p in range(P):
-        net = ActorCritic(8, 4, [80], 72, [64, 64], [64, 64])
-        sd = {k: init[p, o:o + int(np.prod(sh))].view(sh).cpu() for k, (o, sh) in keys.items()
-              if not k.startswith("critic.encoder.")}
-        net.load_reference(sd)
-        adam = {k: (m0[p, o:o + int(np.prod(sh))].view(sh).cpu().numpy(),
-                    v0[p, o:o + int(np.prod(sh))].view(sh).cpu().numpy())
-                for k, (o, sh) in keys.items() if not k.startswith("critic.encoder.")}
-        adam["step"] = 7
-        out = reference_learn(net, adam, pop.obs[p].reshape(S, -1).cpu().numpy(),
-                              pop.actions[p].reshape(-1).cpu().numpy(), pop.log_probs[p].reshape(-1).cpu().numpy(),
-                              raw_adv[p].reshape(-1).cpu().numpy(), pop.returns[p].reshape(-1).cpu().numpy(),
-                              pop.values[p].reshape(-1).cpu().numpy(), perms[:, p].cpu().numpy(), batch_size=S,
-                              epochs=1, lr=lr)
+        out = _oracle_learn(pop, _MUTATED[shape], p, init, m0, v0, raw_adv, perms, S, 1, lr)
         assert out["step"] == 8 and int(pop.opt.steps[p]) == 8
         for name, ref in out["state"].items():
             off, sh = keys[name]
@@ -201,6 +231,42 @@ def test_grouped_learner_single_update_on_mutated_shape(learner):
             close(f"{p} {name} m", pop.opt.exp_avg[p, off:off + k].cpu(), out["exp_avg"][name].reshape(-1), 1e-4)
             close(f"{p} {name} v", pop.opt.exp_avg_sq[p, off:off + k].cpu(), out["exp_avg_sq"][name].reshape(-1),
                   1e-4)
+
+
+@pytest.mark.parametrize("shape", ["three_mutations", "three_layer_encoder"])
+def test_graph_learner_multi_epoch_learn_matches_oracle(shape):
+    """A whole multi-epoch, minibatched learn() of the runtime-shape learner
+    (4 minibatches x 3 epochs = 12 updates, shuffled minibatch order) against
+    the oracle's learn on the same shuffles: within 4x the oracle's own
+    fp32-vs-fp64 drift (PPO's clip / max decisions turn last-bit differences
+    into discrete gradient changes; two correct fp32 implementations drift
+    apart as far as fp32 does from fp64)."""
+    from agilerl_amd.population.learner import GraphLearner, fused_learn
+
+    P, N, T, lr, E = 2, 16, 8, 1e-3, 3
+    S = T * N
+    B = S // 4
+    pop = _mutated_population(_MUTATED[shape], P, N, T, B, E, lr, seed=11)
+    init, m0, v0 = (x.clone() for x in (pop.params.data, pop.opt.exp_avg, pop.opt.exp_avg_sq))
+    raw_adv = pop.advantages.clone()
+    rng = np.random.default_rng(5)
+    perms = torch.tensor(np.stack([np.stack([rng.permutation(S) for _ in range(P)]) for _ in range(E)]),
+                         device=DEV)
+    fused_learn(pop, perms)
+    assert isinstance(pop._fused, GraphLearner)
+    torch.cuda.synchronize()
+    keys = pop.spec.state_dict_keys()
+    for p in range(P):
+        o32 = _oracle_learn(pop, _MUTATED[shape], p, init, m0, v0, raw_adv, perms, B, E, lr)
+        o64 = _oracle_learn(pop, _MUTATED[shape], p, init, m0, v0, raw_adv, perms, B, E, lr, dtype=torch.float64)
+        assert o32["step"] == 7 + 4 * E and int(pop.opt.steps[p]) == 7 + 4 * E
+        for name, ref in o32["state"].items():
+            off, sh = keys[name]
+            k = ref.numel()
+            d = np.abs(pop.params.data[p, off:off + k].cpu().double().numpy() - ref.reshape(-1).double().numpy())
+            e = np.abs(o64["state"][name].reshape(-1).double().numpy() - ref.reshape(-1).double().numpy())
+            assert d.max() <= 4 * e.max() + 1e-6, (p, name, d.max(), e.max())
+            assert d.mean() <= 4 * e.mean() + 1e-8, (p, name, d.mean(), e.mean())
 
 
 def test_regroup_does_not_replay_sampling_noise():

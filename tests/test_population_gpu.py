@@ -650,14 +650,14 @@ def test_engine_evaluates_groups_in_lockstep(monkeypatch):
     P, N = 4, 32
     pop, _ = _runner_pair(monkeypatch, True, P=P, N=N)
     envs = [SyntheticVecEnv(N, seed=10 + j, p_done=0.1, max_episode_steps=25) for j in range(P)]
-    views = [type("V", (), {"learn_step": pop.learn_step})() for _ in range(P)]
+    views = [type("V", (), {"learn_step": pop.T * pop.N})() for _ in range(P)]
     eng = PopulationEngine(pop, views, StackedVecEnv(envs))
     states = eng.local_states()
     states[1].learn_step = states[1].learn_step // 2
     states[3].learn_step = states[3].learn_step // 2
     eng.regroup(states)
     assert len(eng.groups) == 2
-    eng.train(2 * pop.learn_step)
+    eng.train(2 * pop.T * pop.N)
     fit = eng.evaluate(1, None)
     # the same evaluation round, group by group
     eng._eval_calls -= 1
