@@ -40,6 +40,14 @@ SIGNATURES = {
     "agx_ppo_learn_graph_workspace_bytes": (_SZ, [_P, _I, _I, _I, _I]),
     "agx_ppo_learn_graph": (_INT, [_P, _P, _P, _P]),
     "agx_ppo_act_graph_workspace_bytes": (_SZ, [_P, _I, _I]),
+    "agx_debug_graph_stamps": (_INT, [_P]),
+    "agx_ppo_rollout_graph_workgroups": (_I, [_I, _I]),
+    "agx_ppo_rollout_graph_max_workgroups": (_I, []),
+    "agx_ppo_rollout_graph_ctl_bytes": (_SZ, [_I, _I]),
+    "agx_ppo_rollout_graph_persistent": (_INT, [_P, _I, _I, _P, _P, _I, ctypes.c_uint32, ctypes.c_uint64,
+                                                ctypes.c_uint64, _P, _P, _D, _P, _P]),
+    "agx_ppo_eval_graph_persistent": (_INT, [_P, _I, _I, _P, _P, _P, _P, _P, _I, ctypes.c_uint32, ctypes.c_uint64,
+                                             ctypes.c_uint64, _P, _P, _D, _P, _P]),
     "agx_ppo_act_graph": (_INT, [_P, _I, _I, _P, _P, _I, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P,
                                  _P, _I, _P, _P, _P, _P]),
     "agx_ppo_learn": (_INT, [_P, _P, _P, _P]),

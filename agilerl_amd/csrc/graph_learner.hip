@@ -29,6 +29,7 @@
 #include <cstdlib>
 
 #include "agx_common.h"
+#include "rollout.h"
 #include "../../include/agx_graph.h"
 
 namespace agx {
@@ -79,6 +80,7 @@ struct GArgs {
     unsigned *cnt;         // barrier counters, timeout word, XCC ids (zeroed by the gather)
     unsigned *err;         // caller's sticky error word
     int write_through;     // test hook: the cross-XCD (release-fence) publish form always
+    long long *stamps;     // diagnostic phase stamps of the partnered learner (agx_debug_graph_stamps), or null
     float *ws;
     float *params, *m, *v;
     const float *lr;
@@ -183,15 +185,21 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 const int k = kc + lk;
                 const bool kin = k < K;
                 const int kk = kin ? k : 0;
-                // unconditional loads from clamped (valid) addresses, then the predicate
+                // unconditional loads from clamped (valid) addresses, then the
+                // predicate; staging rows wholly past the block (a few-row block:
+                // the partnered learner's 8-16 rows) are neither loaded nor
+                // committed (workgroup-uniform: no MFMA tile reads them for an
+                // output row that is kept)
 #pragma unroll
                 for (int i = 0; i < kBM / kRS; ++i) {
+                    if (kRS * i >= BM) break;
                     const int row = lr + kRS * i;
                     const float va = Ab[(size_t)(row < BM ? row : 0) * lda + kk];
                     ra[i] = (row < BM && kin) ? va : 0.f;
                 }
 #pragma unroll
                 for (int i = 0; i < kBN / kRS; ++i) {
+                    if (kRS * i >= BN) break;
                     const int row = lr + kRS * i;
                     const float vb = Bb[(size_t)(row < BN ? row : 0) * ldb + kk];
                     rb[i] = (row < BN && kin) ? vb : 0.f;
@@ -200,9 +208,15 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
             auto commit = [&](int buf) {
                 float *As = lds + buf * kPanel, *Bs = As + kBM * kLdS;
 #pragma unroll
-                for (int i = 0; i < kBM / kRS; ++i) As[(lr + kRS * i) * kLdS + lk] = ra[i];
+                for (int i = 0; i < kBM / kRS; ++i) {
+                    if (kRS * i >= BM) break;
+                    As[(lr + kRS * i) * kLdS + lk] = ra[i];
+                }
 #pragma unroll
-                for (int i = 0; i < kBN / kRS; ++i) Bs[(lr + kRS * i) * kLdS + lk] = rb[i];
+                for (int i = 0; i < kBN / kRS; ++i) {
+                    if (kRS * i >= BN) break;
+                    Bs[(lr + kRS * i) * kLdS + lk] = rb[i];
+                }
             };
             f4 acc[kTPW];
             // per slot: the bias of column n0 + r (and with LNE the LN affine),
@@ -1156,6 +1170,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
     __shared__ float colp[2 * 3 * kGW * 128];
     __shared__ float colo[kGW * 33];
     __shared__ int s_ok;
+    __shared__ long long s_st[16];  // phase stamps (agent 0, partner 0, update 1)
     if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const int b = blockIdx.x;
     const int p = b % g.Q, kk = b / g.Q;
@@ -1235,6 +1250,10 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
             float *const G = slab0 + (size_t)kk * g.nslab;
             float *const sum = g.sums + ((size_t)p * 2 + (upd & 1)) * g.nslab;
 
+            const bool stamp = g.stamps && b == 0 && upd == 1 && tid == 0;
+#define GST(i) \
+    if (stamp) s_st[i] = (long long)__builtin_readcyclecounter()
+            GST(0);
             // ---- 1. this partner's rows -> its partial gradient row ----------------
             float lsum = 0.f, klsum = 0.f;
             if (rk > 0) {
@@ -1243,12 +1262,15 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
             } else {  // no rows this minibatch (a short last minibatch): publish zeros
                 for (int i = tid; i < n; i += kGT) G[i] = 0.f;
             }
+            GST(1);
             block_sum2(lsum, klsum, red);
             if (tid == 0) {
                 G[nal] = lsum;
                 G[nal + 1] = klsum;
             }
+            GST(2);
             if (!gpart_sync(c1, (unsigned)(K * (upd + 1)), !local, tmo, g.err, &s_ok)) return;
+            GST(3);
 
             // ---- 2. reduce-scatter of the owned chunks + partial norms ---------------
             float q0 = 0.f, q1 = 0.f;
@@ -1289,7 +1311,9 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
                 q1 = wave_sum(q1);
                 if (lane < 2) sum[nal + 4 + (kk * kGW + wave) * 2 + lane] = lane ? q1 : q0;
             }
+            GST(4);
             if (!gpart_sync(c2, (unsigned)(K * (upd + 1)), !local, tmo, g.err, &s_ok)) return;
+            GST(5);
 
             // ---- 3. norms (fixed order), loss words, Adam on the owned floats ---------
             float t0, t1, lmb, klmb;
@@ -1308,6 +1332,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
                 lmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(unsigned, lw)));
                 klmb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(unsigned, kw)));
             }
+            GST(6);
             if (tid == 0) loss_total += lmb;
             kl_total += (double)klmb;
             ++n_done;
@@ -1363,9 +1388,13 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
                 if (rf >= f1 || rf + cnt <= f0) continue;  // uniform: no owned float in the region
                 adam_range(rf, cnt, kind == 0 ? L.wt : -1, kind == 0 ? L.fin : 1, kind == 0 ? L.fout : 1);
             }
+            GST(7);
             // ---- 4. every partner's chunks visible to this one's next plain loads ---------
             if (!gpart_sync(c3, (unsigned)(K * (upd + 1)), !local, tmo, g.err, &s_ok)) return;
+            GST(8);
             gpart_acquire();
+            GST(9);
+#undef GST
         }  // minibatches
         ++epochs_done;
         if (g.target_kl > 0.0 && kl_total / (double)n_done > g.target_kl) break;  // ppo.py:917-918
@@ -1376,29 +1405,15 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
         if (g.epochs_out) g.epochs_out[p] = epochs_done;
         g.step[p] = step0 + n_done;
     }
+    if (g.stamps && b == 0 && tid < 10) g.stamps[tid] = s_st[tid];
 }
 
-
-// Philox4x32-10 (Salmon et al., SC'11): the counter-based stream of
-// agx_ppo_act (learner.hip), so an agent's draws are keyed the same way
-// whichever kernel runs its network
-__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-        const unsigned long long p0 = (unsigned long long)0xD2511F53u * c.x;
-        const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c.z;
-        const unsigned h0 = (unsigned)(p0 >> 32), l0 = (unsigned)p0, h1 = (unsigned)(p1 >> 32), l1 = (unsigned)p1;
-        c = make_uint4(h1 ^ c.y ^ k.x, l1, h0 ^ c.w ^ k.y, l0);
-        k.x += 0x9E3779B9u;
-        k.y += 0xBB67AE85u;
-    }
-    return c;
-}
 
 struct GActArgs {
     GLay L[kGL];
     int nl, aout, cout, A, D, n, rows;
     long long ws_block;  // scratch floats per (agent, row block)
+    long long obs_off;   // persistent rollout: the step's observation rows [rows][D] in the block scratch
     float *ws;
     const float *params;
     const float *obs;  // agent p, env n at obs + p*obs_pstride + n*D
@@ -1414,22 +1429,30 @@ struct GActArgs {
     const long long *env_base;
 };
 
-// Rollout policy step (PPO.get_action, ppo.py:567-633) of workgroup (p, row
-// block): forward through the layer list, then the categorical over 16 lanes
-// per row (actions a and a + 16 per lane): masked logits (illegal -> -1e8,
+// The categorical step of rows [0, nrow) of agent p's row block n0 (logits at
+// lgp [nrow][A], values at vp) — masked logits (illegal -> -1e8,
 // distributions.py:16-28), Gumbel-max sample from the Philox stream of
-// agx_ppo_act, log-prob, entropy, value.
-__global__ __launch_bounds__(kGT) void ppo_act_graph_kernel(const GActArgs g) {
-    __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
-    const int p = blockIdx.y, n0 = blockIdx.x * g.rows;
+// agx_ppo_act, log-prob, entropy, value; 16 lanes per row, actions a and a + 16
+// per lane.  HOST_MASK: the mask is host staging (system-scope loads), copied to
+// mask_copy when that is set.
+struct GSample {
+    int A, N, sample;
+    unsigned long long seed, counter;
+    const long long *env_base;
+    const unsigned char *mask;
+    long long mask_pstride;
+    unsigned char *mask_copy;
+    long long mask_copy_pstride;
+    long long *act_out;
+    float *logp_out, *value_out, *ent_out;
+    long long out_pstride;
+    long long *act_flat;
+};
+template <bool HOST_MASK>
+__device__ __forceinline__ void graph_sample(const GSample &g, const float *lgp, const float *vp, int p, int n0,
+                                             int nrow) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane & 15, rq = lane >> 4;
-    const int nrow = g.N - n0 < g.rows ? g.N - n0 : g.rows;
-    float *base = g.ws + ((size_t)p * gridDim.x + blockIdx.x) * g.ws_block;
-    const float *pr = g.params + (size_t)p * g.n;
-    forward_layers(g.L, g.nl, g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * g.D, nrow, base, pr, g.rows, lds);
-    const float *lgp = base + g.L[g.aout].yr;
-    const float *vp = base + g.L[g.cout].yr;
     const int A = g.A;
     const int a0 = sub, a1 = sub + 16;
     for (int r0 = 0; r0 < nrow; r0 += 4 * kGW) {
@@ -1439,9 +1462,17 @@ __global__ __launch_bounds__(kGT) void ppo_act_graph_kernel(const GActArgs g) {
         float lg0 = a0 < A ? lgp[(size_t)rr * A + a0] : -3.0e38f;
         float lg1 = a1 < A ? lgp[(size_t)rr * A + a1] : -3.0e38f;
         if (g.mask && live) {
-            const unsigned char *mk = g.mask + (size_t)p * g.mask_pstride + (size_t)(n0 + r) * A;
-            if (a0 < A && !mk[a0]) lg0 = -1.0e8f;
-            if (a1 < A && !mk[a1]) lg1 = -1.0e8f;
+            const size_t mo = (size_t)p * g.mask_pstride + (size_t)(n0 + r) * A;
+            unsigned char ok0 = 1, ok1 = 1;
+            if (a0 < A) ok0 = HOST_MASK ? ld_sys_u8(g.mask + mo + a0) : g.mask[mo + a0];
+            if (a1 < A) ok1 = HOST_MASK ? ld_sys_u8(g.mask + mo + a1) : g.mask[mo + a1];
+            if (HOST_MASK && g.mask_copy) {
+                const size_t co = (size_t)p * g.mask_copy_pstride + (size_t)(n0 + r) * A;
+                if (a0 < A) g.mask_copy[co + a0] = ok0;
+                if (a1 < A) g.mask_copy[co + a1] = ok1;
+            }
+            if (a0 < A && !ok0) lg0 = -1.0e8f;
+            if (a1 < A && !ok1) lg1 = -1.0e8f;
         }
         const float mx = rmax16(fmaxf(lg0, lg1));
         const float lse = mx + logf(rsum16((a0 < A ? expf(lg0 - mx) : 0.f) + (a1 < A ? expf(lg1 - mx) : 0.f)));
@@ -1480,6 +1511,116 @@ __global__ __launch_bounds__(kGT) void ppo_act_graph_kernel(const GActArgs g) {
                 __hip_atomic_store(g.act_flat + (size_t)p * g.N + n0 + r, (long long)choice, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
         }
+    }
+}
+
+// Rollout policy step (PPO.get_action, ppo.py:567-633) of workgroup (p, row
+// block): forward through the layer list, then graph_sample.
+__global__ __launch_bounds__(kGT) void ppo_act_graph_kernel(const GActArgs g) {
+    __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
+    const int p = blockIdx.y, n0 = blockIdx.x * g.rows;
+    const int nrow = g.N - n0 < g.rows ? g.N - n0 : g.rows;
+    float *base = g.ws + ((size_t)p * gridDim.x + blockIdx.x) * g.ws_block;
+    const float *pr = g.params + (size_t)p * g.n;
+    forward_layers(g.L, g.nl, g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * g.D, nrow, base, pr, g.rows, lds);
+    GSample s{g.A, g.N, g.sample, g.seed, g.counter, g.env_base, g.mask, g.mask_pstride, nullptr, 0,
+              g.act_out, g.logp_out, g.value_out, g.ent_out, g.out_pstride, g.act_flat};
+    graph_sample<false>(s, base + g.L[g.aout].yr, base + g.L[g.cout].yr, p, n0, nrow);
+}
+
+// Persistent rollout of a runtime-shape population (agx_ppo_rollout_graph_
+// persistent / agx_ppo_eval_graph_persistent): agx_ppo_rollout_persistent's
+// host-paced loop (learner.hip) around ppo_act_graph_kernel's step.  Step t:
+// wait for the host's release, then the step's ActArgs (host memory): the
+// observation rows from the host staging (system-scope loads) into this
+// block's scratch and the rollout slot, the previous step's reward / done into
+// slot t-1 with the episode accounting, and (act) the forward + sample; the
+// actions go to the host staging; then this block's done word.
+__global__ __launch_bounds__(kGT) void ppo_rollout_graph_persistent_kernel(const GActArgs ga, const ActArgs *steps,
+                                                                           int nsteps, agx_rollout_ctl *ctl,
+                                                                           unsigned long long timeout_ticks,
+                                                                           unsigned base_seq) {
+    __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
+    __shared__ ActArgs s_args;
+    __shared__ int s_go;
+    const int tid = threadIdx.x;
+    const int p = blockIdx.y, n0 = blockIdx.x * ga.rows;
+    const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+    const int D = ga.D;
+    unsigned *rel = rollout_release_word(ctl, gridDim.x * gridDim.y, blk);
+    float *base = ga.ws + ((size_t)p * gridDim.x + blockIdx.x) * ga.ws_block;
+    float *obs_rows = base + ga.obs_off;  // [rows][D]: this step's observations
+    constexpr int kArgWords = (int)(sizeof(ActArgs) / 4);
+    for (int t = 0; t < nsteps; ++t) {
+        if (tid < kArgWords)
+            reinterpret_cast<unsigned *>(&s_args)[tid] = reinterpret_cast<const unsigned *>(steps + t)[tid];
+        if (tid == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            int go = 1;
+            for (;;) {
+                const unsigned v = __hip_atomic_load(rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (v == AGX_ROLLOUT_ABORT) {
+                    go = 0;
+                    __hip_atomic_store(&ctl->timeout, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                if (v == AGX_ROLLOUT_STOP) {
+                    go = 0;
+                    break;
+                }
+                if (v >= base_seq + (unsigned)(t + 1)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+                    go = 0;
+                    __hip_atomic_store(&ctl->timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) return;
+        const ActArgs g = s_args;
+        const int nrow = g.N - n0 < ga.rows ? g.N - n0 : ga.rows;
+        // the host staging of this block's rows (one round trip), then the
+        // previous step's reward / done and the episode accounting
+        const float *ob = g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * D;
+        for (int i = tid; i < nrow * D; i += kGT) {
+            const float x = ld_sys(ob + i);
+            obs_rows[i] = x;
+            if (g.obs_copy) g.obs_copy[(size_t)p * g.obs_copy_pstride + (size_t)n0 * D + i] = x;
+        }
+        if (g.st_rew && tid < nrow) {
+            const size_t idx = (size_t)p * g.N + n0 + tid;
+            const float rw = ld_sys(g.st_rew + idx);
+            const unsigned char dn = ld_sys_u8(g.st_done + idx);
+            const int env = n0 + tid;
+            g.rew_prev[(size_t)p * g.prev_pstride + env] = rw;
+            g.done_prev[(size_t)p * g.prev_pstride + env] = dn;
+            if (g.scores) {
+                float sc = g.scores[idx] + rw;
+                if (dn) {
+                    g.ret_sum[idx] += (double)sc;
+                    g.episodes[idx] += 1;
+                    sc = 0.f;
+                }
+                g.scores[idx] = sc;
+            }
+        }
+        if (g.act) {
+            __syncthreads();  // the observation rows are in the scratch
+            forward_layers(ga.L, ga.nl, obs_rows, nrow, base, g.params + (size_t)p * ga.n, ga.rows, lds);
+            GSample sp{ga.A, g.N, g.sample, g.seed, g.counter, g.env_base, g.mask, g.mask_pstride, g.mask_copy,
+                       g.mask_copy_pstride, g.act_out, g.logp_out, g.value_out, g.ent_out, g.out_pstride, g.act_flat};
+            graph_sample<true>(sp, base + ga.L[ga.aout].yr, base + ga.L[ga.cout].yr, p, n0, nrow);
+        }
+        // the host-memory stores (actions) are system-scope write-through: wait
+        // for their acknowledgements, then this block's done word
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_store(rollout_done_words(ctl) + blk, base_seq + (unsigned)(t + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1655,6 +1796,8 @@ long long act_plan(const GArgs &full, GActArgs &a) {
     a.D = full.D;
     a.n = full.n;
     a.rows = kActRows;
+    a.obs_off = off;
+    off = r4(off + (long long)kActRows * full.D);
     a.ws_block = (off + 63) & ~63ll;
     return a.ws_block;
 }
@@ -1740,6 +1883,15 @@ PartWs part_ws(const GArgs &a, int64_t P, int64_t S, int64_t epochs, int K) {
 }  // namespace agx
 
 using namespace agx;
+
+static long long *&g_graph_stamps() {
+    static long long *p = nullptr;
+    return p;
+}
+extern "C" int agx_debug_graph_stamps(int64_t *buf) {
+    g_graph_stamps() = reinterpret_cast<long long *>(buf);
+    return AGX_OK;
+}
 
 extern "C" int agx_ppo_graph_check(const agx_ppo_graph *net) {
     GArgs a{};
@@ -1852,6 +2004,7 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
         a.slabs = reinterpret_cast<float *>(ws + pw.slabs);
         a.sums = reinterpret_cast<float *>(ws + pw.sums);
         a.cnt = counters;
+        a.stamps = g_graph_stamps();
         {
             const char *wt = getenv("AGX_LEARN_WRITETHROUGH");
             a.write_through = wt && atoi(wt) != 0;
@@ -1904,4 +2057,103 @@ extern "C" int agx_ppo_act_graph(const agx_ppo_graph *net, int64_t P, int64_t N,
     dim3 grid((unsigned)ceil_div(N, kActRows), (unsigned)P);
     ppo_act_graph_kernel<<<grid, kGT, 0, as_stream(stream)>>>(a);
     return check_launch("agx_ppo_act_graph");
+}
+
+// ---------------------------------------------------------------------------
+// persistent rollout / evaluation of runtime-shape populations
+// ---------------------------------------------------------------------------
+extern "C" int64_t agx_ppo_rollout_graph_workgroups(int64_t P, int64_t N) { return P * ceil_div(N, kActRows); }
+
+extern "C" int64_t agx_ppo_rollout_graph_max_workgroups(void) {
+    static int occ = -1;
+    if (occ < 0) {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_rollout_graph_persistent_kernel, kGT, 0) != hipSuccess)
+            v = 0;
+        occ = v;
+    }
+    return (int64_t)occ * cu_count_g();
+}
+
+extern "C" size_t agx_ppo_rollout_graph_ctl_bytes(int64_t P, int64_t N) {
+    const unsigned nwg = (unsigned)agx_ppo_rollout_graph_workgroups(P, N);
+    return (size_t)rollout_release_offset(nwg, nwg) * sizeof(unsigned);
+}
+
+namespace {
+int launch_graph_persistent(const agx_ppo_graph *net, int64_t P, int64_t N, ActArgs *steps, int64_t nsteps,
+                            uint32_t base, agx_rollout_ctl *ctl, double timeout_s, void *workspace, void *stream,
+                            const char *who) {
+    GArgs full{};
+    const int rc = plan_graph(net, 1, full);
+    if (rc != AGX_OK) return rc;
+    const int64_t nwg = agx_ppo_rollout_graph_workgroups(P, N);
+    if (nwg > agx_ppo_rollout_graph_max_workgroups()) {
+        set_error("%s: %lld workgroups cannot all be resident; use per-step launches", who, (long long)nwg);
+        return AGX_EUNSUPPORTED;
+    }
+    GActArgs a{};
+    act_plan(full, a);
+    a.ws = static_cast<float *>(workspace);
+    a.N = (int)N;
+    a.P = (int)P;
+    const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    ctl->nwg = (uint32_t)nwg;
+    dim3 grid((unsigned)ceil_div(N, kActRows), (unsigned)P);
+    ppo_rollout_graph_persistent_kernel<<<grid, kGT, 0, as_stream(stream)>>>(a, steps, (int)nsteps, ctl, ticks, base);
+    return check_launch(who);
+}
+}  // namespace
+
+extern "C" int agx_ppo_rollout_graph_persistent(const agx_ppo_graph *net, int64_t P, int64_t N, const float *params,
+                                                const agx_rollout_io *ios, int64_t nsteps, uint32_t base,
+                                                uint64_t seed, uint64_t counter0, void *args_host,
+                                                agx_rollout_ctl *ctl, double timeout_s, void *workspace,
+                                                void *stream) {
+    AGX_REQUIRE(net && ios && params && args_host && ctl && workspace && P > 0 && N > 0 && P <= 65535 && nsteps >= 1,
+                "agx_ppo_rollout_graph_persistent: bad arguments");
+    AGX_REQUIRE((uint64_t)base + (uint64_t)nsteps < AGX_ROLLOUT_STOP, "agx_ppo_rollout_graph_persistent: base wraps");
+    AGX_REQUIRE(timeout_s > 0 && timeout_s < 3600, "agx_ppo_rollout_graph_persistent: timeout_s out of range");
+    AGX_REQUIRE(net->obs_dim >= 1, "agx_ppo_rollout_graph_persistent: bad graph");
+    ActArgs *steps = static_cast<ActArgs *>(args_host);
+    for (int64_t t = 0; t < nsteps; ++t) {
+        const bool last = t + 1 == nsteps;
+        if (int rc = check_rollout_io(ios + t, 1, params, "agx_ppo_rollout_graph_persistent")) return rc;
+        fill_rollout_args(steps[t], net->obs_dim, net->n_actions, P, N, params, ios + t, 1, last ? 0 : 1, seed,
+                          last ? 0 : counter0 + 1 + (uint64_t)t);
+    }
+    return launch_graph_persistent(net, P, N, steps, nsteps, base, ctl, timeout_s, workspace, stream,
+                                   "agx_ppo_rollout_graph_persistent");
+}
+
+extern "C" int agx_ppo_eval_graph_persistent(const agx_ppo_graph *net, int64_t P, int64_t N, const float *params,
+                                             const float *stage_obs, const uint8_t *stage_mask,
+                                             int64_t *actions_flat, const int64_t *agent_env_base, int64_t nsteps,
+                                             uint32_t base, uint64_t seed, uint64_t counter0, void *args_host,
+                                             agx_rollout_ctl *ctl, double timeout_s, void *workspace, void *stream) {
+    AGX_REQUIRE(net && params && stage_obs && actions_flat && args_host && ctl && workspace && P > 0 && N > 0 &&
+                    P <= 65535 && nsteps >= 1,
+                "agx_ppo_eval_graph_persistent: bad arguments");
+    AGX_REQUIRE((uint64_t)base + (uint64_t)nsteps < AGX_ROLLOUT_STOP, "agx_ppo_eval_graph_persistent: base wraps");
+    AGX_REQUIRE(timeout_s > 0 && timeout_s < 3600, "agx_ppo_eval_graph_persistent: timeout_s out of range");
+    ActArgs *steps = static_cast<ActArgs *>(args_host);
+    for (int64_t t = 0; t < nsteps; ++t) {
+        ActArgs a{};
+        a.params = params;
+        a.obs = stage_obs;
+        a.obs_pstride = N * (int64_t)net->obs_dim;
+        a.N = (int)N;
+        a.P = (int)P;
+        a.sample = 1;
+        a.seed = seed;
+        a.counter = counter0 + (uint64_t)t;
+        a.act_flat = reinterpret_cast<long long *>(actions_flat);
+        a.act = 1;
+        a.mask = stage_mask;
+        a.mask_pstride = N * (int64_t)net->n_actions;
+        a.env_base = reinterpret_cast<const long long *>(agent_env_base);
+        steps[t] = a;
+    }
+    return launch_graph_persistent(net, P, N, steps, nsteps, base, ctl, timeout_s, workspace, stream,
+                                   "agx_ppo_eval_graph_persistent");
 }

@@ -34,7 +34,10 @@ the identical global sequence.
 from __future__ import annotations
 
 import copy
+import os
+import pickle
 import random
+import time
 
 import numpy as np
 import torch
@@ -42,6 +45,34 @@ import torch.distributed as dist
 
 #: per-agent RL hyperparameters a PPO view exposes as properties (not in vars)
 _PPO_HP = ("lr", "batch_size", "update_epochs", "ent_coef", "learn_step")
+
+
+#: per tag: [calls, seconds, pickled bytes this rank contributed] of the host-object
+#: collectives of the generation step (diagnostic, enabled by AGX_SHARD_STATS=1;
+#: the byte count pickles the payload once more)
+EXCHANGE_STATS: dict[str, list] = {}
+
+
+def _record(tag: str, t0: float, obj) -> None:
+    if os.environ.get("AGX_SHARD_STATS"):
+        st = EXCHANGE_STATS.setdefault(tag, [0, 0.0, 0])
+        st[0] += 1
+        st[1] += time.perf_counter() - t0
+        st[2] += len(pickle.dumps(obj))
+
+
+def all_gather_obj(box: list, obj, group=None, tag: str = "other") -> None:
+    """dist.all_gather_object, timed per tag (EXCHANGE_STATS)."""
+    t0 = time.perf_counter()
+    dist.all_gather_object(box, obj, group=group)
+    _record(tag, t0, obj)
+
+
+def broadcast_obj(box: list, src: int, group=None, tag: str = "other") -> None:
+    """dist.broadcast_object_list, timed per tag (EXCHANGE_STATS)."""
+    t0 = time.perf_counter()
+    dist.broadcast_object_list(box, src=src, group=group)
+    _record(tag, t0, box)
 
 
 def world_rank(group=None) -> tuple[int, int]:
@@ -57,7 +88,7 @@ def all_ranks(flag: bool, group=None) -> bool:
     if world == 1:
         return bool(flag)
     box: list = [None] * world
-    dist.all_gather_object(box, bool(flag), group=group)
+    all_gather_obj(box, bool(flag), group=group, tag="stop_flag")
     return all(box)
 
 
@@ -69,7 +100,7 @@ def sync_host_rngs(group=None) -> None:
         return
     box = [(np.random.get_state(legacy=True), torch.get_rng_state(), random.getstate())] if rank == 0 else [None]
     src = dist.get_global_rank(group, 0) if group is not None else 0
-    dist.broadcast_object_list(box, src=src, group=group)
+    broadcast_obj(box, src=src, group=group, tag="host_rngs")
     if rank != 0:
         np_state, t_state, py_state = box[0]
         np.random.set_state(np_state)
@@ -211,7 +242,7 @@ def gather_records(pop, group=None) -> list[dict]:
     if world == 1:
         return local
     box: list = [None] * world
-    dist.all_gather_object(box, local, group=group)
+    all_gather_obj(box, local, group=group, tag="agent_records")
     if any(len(b) != len(pop) for b in box):
         raise ValueError("every rank must hold the same number of agents")
     return [r for b in box for r in b]
@@ -247,7 +278,7 @@ def global_view(pop, records: list[dict], group=None) -> list:
     flags = [shared is not None]
     if world > 1:
         box: list = [None] * world
-        dist.all_gather_object(box, flags, group=group)
+        all_gather_obj(box, flags, group=group, tag="registry_flags")
         all_shared = all(b[0] for b in box)
     else:
         all_shared = flags[0]

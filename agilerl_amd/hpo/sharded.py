@@ -35,6 +35,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .shard import all_gather_obj
 from .tournament import TournamentSelection, select_parents
 
 _PLAIN = (bool, int, float, str, type(None), np.integer, np.floating)
@@ -156,7 +157,7 @@ class ShardedTournamentSelection:
                 for a in population]
         if world > 1:
             gathered: list = [None] * world
-            dist.all_gather_object(gathered, info, group=self.group)
+            all_gather_obj(gathered, info, group=self.group, tag="tournament_attributes")
         else:
             gathered = [info]
         if any(len(g) != P for g in gathered):

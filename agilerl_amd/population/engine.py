@@ -42,6 +42,7 @@ import torch
 import torch.distributed as dist
 
 from ..envs import StackedVecEnv
+from ..hpo.shard import all_gather_obj
 from ..rng import numpy_shuffle_perms
 from .ppo_pop import PPOPopulation
 from .runner import PopulationRunner
@@ -140,7 +141,7 @@ class PopulationEngine:
             local.append((g.pop.S, int(g.pop.agent_epochs[r]), g.learn_step, int(g.pop.agent_batch[r])))
         if self.world > 1:
             box: list = [None] * self.world
-            dist.all_gather_object(box, local)
+            all_gather_obj(box, local, tag="population_plan")
             plan = [tuple(x) for b in box for x in b]
         else:
             plan = local
@@ -196,7 +197,7 @@ class PopulationEngine:
             # every rank replays the GLOBAL re-advance: each slot's epochs run
             # (a few ints per agent) gathered like refresh_plan's plan
             box: list = [None] * self.world
-            dist.all_gather_object(box, ran_local)
+            all_gather_obj(box, ran_local, tag="epochs_run")
             ran_of = [x for b in box for x in b]
         else:
             ran_of = ran_local
@@ -221,12 +222,17 @@ class PopulationEngine:
             if g.pop.act_counter > base:
                 raise RuntimeError(f"rollout counter {g.pop.act_counter} overran generation {self._generation - 2}")
             g.pop.act_counter = base
+            # no host sync between a group's iterations: the next rollout and
+            # learn are enqueued while the device still learns (the learner
+            # reuses its loss buffer, hence the device-side copies); errors and
+            # losses are read once the group's iterations are queued
+            pending = []
             for _ in range(self.iterations(evo_steps, g.learn_step)):
-                loss = g.runner.iteration()
-                g.pop.check_errors()
-                losses.append(loss.cpu().numpy())
+                pending.append(g.runner.iteration().clone())
                 if on_iteration is not None:
                     on_iteration(g)
+            g.pop.check_errors()
+            losses += [x.cpu().numpy() for x in pending]
         return losses
 
     def steps_per_generation(self, slot: int, evo_steps: int) -> int:

@@ -133,21 +133,23 @@ class PopulationRunner:
         dev = pop.device
         self.zero_copy = os.environ.get("AGX_ZERO_COPY", "1") != "0"
         desc = pop.fused_descriptor()
+        gdesc = pop.learn_descriptor() if desc is None else None  # a mutated (runtime-shape) network
         mode = os.environ.get("AGX_PERSISTENT_ROLLOUT", "auto")
-        self.persistent = (self.zero_copy and mode != "0" and desc is not None
-                           and (mode == "1" or bool(getattr(env, "agx_device_free", False))))
-        if self.persistent:
-            # every workgroup of the persistent launch must be co-resident (the
-            # host paces them in lock step); larger grids take per-step launches
-            lib = _lib.load()
-            if lib.agx_rollout_workgroups(P, N) > lib.agx_rollout_max_workgroups(ctypes.byref(desc)):
-                self.persistent = False
-        if self.persistent:
+        paced = self.zero_copy and mode != "0" and (mode == "1" or bool(getattr(env, "agx_device_free", False)))
+        # every workgroup of a persistent launch must be co-resident (the host
+        # paces them in lock step); larger grids take per-step launches
+        lib = _lib.load()
+        self.persistent = bool(paced and desc is not None and
+                               lib.agx_rollout_workgroups(P, N) <= lib.agx_rollout_max_workgroups(ctypes.byref(desc)))
+        self.graph_persistent = bool(paced and gdesc is not None and pop.obs.dtype == torch.float32 and
+                                     lib.agx_ppo_rollout_graph_workgroups(P, N) <=
+                                     lib.agx_ppo_rollout_graph_max_workgroups())
+        if self.persistent or self.graph_persistent:
             self.stage_h, self.obs_h, self.rew_h, self.done_h = _packed(P, N, D, owner=self)
             self.act_h = _coherent(self, P * N * 8).view(torch.int64)
-            lib = _lib.load()
-            self.n_wg = int(lib.agx_rollout_workgroups(P, N))
-            self.ctl_h = _coherent(self, int(lib.agx_rollout_ctl_bytes(P, N)))
+            self.n_wg = int(lib.agx_ppo_rollout_graph_workgroups(P, N) if self.graph_persistent
+                            else lib.agx_rollout_workgroups(P, N))
+            self.ctl_h = _coherent(self, self._ctl_bytes())
             self.args_h = _coherent(self, int(lib.agx_rollout_args_bytes(pop.T + 1)))
             self.seq_base = 0
             self.timeout_s = float(os.environ.get("AGX_ROLLOUT_TIMEOUT", "20"))
@@ -172,6 +174,11 @@ class PopulationRunner:
         self._ios = None
         self._np = None
         self.stats_event = None
+
+    def _ctl_bytes(self) -> int:
+        lib, P, N = _lib.load(), self.pop.P, self.pop.N
+        return int(lib.agx_ppo_rollout_graph_ctl_bytes(P, N) if self.graph_persistent
+                   else lib.agx_rollout_ctl_bytes(P, N))
 
     # ------------------------------------------------------------------ #
     @property
@@ -238,7 +245,7 @@ class PopulationRunner:
     def collect(self) -> None:
         pop, env = self.pop, self.env
         desc = pop.fused_descriptor()
-        if desc is None:
+        if desc is None and not self.graph_persistent:
             return self._collect_torch()
         P, N, T = pop.P, pop.N, pop.T
         if self._ios is None:
@@ -248,7 +255,7 @@ class PopulationRunner:
             if not self.zero_copy:
                 self.stage_d.copy_(self.stage_h, non_blocking=True)
             self.started = True
-        if self.persistent:
+        if self.persistent or self.graph_persistent:
             return self._collect_persistent(desc)
         lib = _lib.load()
         fn = lib.agx_ppo_rollout_step
@@ -294,10 +301,21 @@ class PopulationRunner:
             torch.cuda.current_stream().synchronize()
             self.ctl_h.zero_()
             base = 0
-        _lib.check(lib.agx_ppo_rollout_persistent(ctypes.byref(desc), P, N, pop.params.data.data_ptr(), self._ios,
-                                                  T + 1, base, pop.act_seed, pop.act_counter,
-                                                  self.args_h.data_ptr(), ctl, self.timeout_s, _lib.stream()),
-                   "agx_ppo_rollout_persistent")
+        if self.graph_persistent:  # a mutated shape: the runtime-shape policy step in the same loop
+            from .learner import graph_act_workspace
+
+            gdesc = pop.learn_descriptor()
+            ws = graph_act_workspace(pop, gdesc)[1]
+            _lib.check(lib.agx_ppo_rollout_graph_persistent(ctypes.byref(gdesc), P, N, pop.params.data.data_ptr(),
+                                                            self._ios, T + 1, base, pop.act_seed, pop.act_counter,
+                                                            self.args_h.data_ptr(), ctl, self.timeout_s,
+                                                            ws.data_ptr(), _lib.stream()),
+                       "agx_ppo_rollout_graph_persistent")
+        else:
+            _lib.check(lib.agx_ppo_rollout_persistent(ctypes.byref(desc), P, N, pop.params.data.data_ptr(),
+                                                      self._ios, T + 1, base, pop.act_seed, pop.act_counter,
+                                                      self.args_h.data_ptr(), ctl, self.timeout_s, _lib.stream()),
+                       "agx_ppo_rollout_persistent")
         self.seq_base = base + T + 1
         self._mark_stats()
         return lib, ctl, base
@@ -359,6 +377,13 @@ class PopulationRunner:
             self.ret_sum_env += torch.where(d, self.scores, 0.0).double()
             self.episodes_env += d.long()
             self.scores.masked_fill_(d, 0.0)
+        gdesc = pop.learn_descriptor()
+        if gdesc is not None:  # a mutated shape: the bootstrap value from the runtime-shape kernel too
+            from .learner import policy_step_graph
+
+            policy_step_graph(pop, gdesc, self.last_obs, N * pop.spec.obs_dim, sample=False, counter=0,
+                              values=self.last_value, out_agent_stride=N)
+            self.last_value_valid = True
         self._mark_stats()
         self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)
         self.env_steps += P * N * T
@@ -397,7 +422,7 @@ class PopulationRunner:
             lib = _lib.load()
             _, obs, rew, done = _packed(P, N, D, owner=self)
             act = _coherent(self, P * N * 8).view(torch.int64)
-            ctl = _coherent(self, int(lib.agx_rollout_ctl_bytes(P, N)))
+            ctl = _coherent(self, self._ctl_bytes())
             args = _coherent(self, int(lib.agx_rollout_args_bytes(_EVAL_CHUNK)))
             self._eval_bufs = (obs, rew, done, act, ctl, args)
         return self._eval_bufs
@@ -410,7 +435,7 @@ class PopulationRunner:
     def iteration(self) -> torch.Tensor:
         """collect -> bootstrap + GAE -> learn; returns per-agent mean loss (device)."""
         desc = self.pop.fused_descriptor()
-        if self.persistent and desc is not None:
+        if (self.persistent and desc is not None) or self.graph_persistent:
             return self._iteration_pipelined(desc)
         self.collect()
         self.pop.finish_rollout(self.last_obs, self.last_done,
@@ -479,7 +504,8 @@ class _EvalDriver:
         self.counter0 = (1 << 41) + (int(pop.eval_rounds) << 24) + (k << 20)
         self.desc = pop.fused_descriptor()
         self.gdesc = pop.learn_descriptor() if self.desc is None else None
-        self.persistent = bool(allow_persistent and runner.persistent and self.desc is not None)
+        self.persistent = bool(allow_persistent and ((runner.persistent and self.desc is not None) or
+                                                     (runner.graph_persistent and self.gdesc is not None)))
         self.step = 0
         self.scores = np.zeros(P * N)
         self.completed = np.zeros(P * N)
@@ -487,7 +513,6 @@ class _EvalDriver:
         if self.persistent:
             st = runner._eval_staging()
             self.obs_h, self.rew_h, self.done_h, self.act_h, self.ctl_h, self.args_h = st
-            self.stream = None  # a dedicated stream, assigned by run_lockstep
             self.launched_to = 0  # steps covered by launches so far (0: no launch resident)
         else:
             self.act_d = torch.empty(P * N, dtype=torch.int64, device=pop.device)
@@ -495,21 +520,22 @@ class _EvalDriver:
             self.obs_h = torch.empty(P * N * D, dtype=pop.obs.dtype, pin_memory=True)
             self.obs_d = torch.empty(P, N, D, dtype=pop.obs.dtype, device=pop.device)
             self.ev = torch.cuda.Event()
-            if self.gdesc is not None:  # its scratch now: nothing may allocate while a persistent launch waits
-                from .learner import graph_act_workspace
+        if self.gdesc is not None:  # its scratch now: nothing may allocate while a persistent launch waits
+            from .learner import graph_act_workspace
 
-                graph_act_workspace(self.pop, self.gdesc)
+            graph_act_workspace(self.pop, self.gdesc)
         self.obs = None
+        self.stream = None  # a dedicated non-blocking stream, assigned by run_lockstep
 
     # -- lock-step protocol -------------------------------------------------
     def begin(self) -> None:
+        # the driver's stream starts after everything queued so far (the learner
+        # that wrote the parameters).  Ordered here, before any group's
+        # persistent launch is resident: nothing after a launch may wait for
+        # the device while the host is pacing it
+        self.stream.wait_stream(torch.cuda.current_stream(self.pop.device))
         if self.persistent:
             self.env.reset(out_obs=self.obs_h.numpy())
-            # the side stream starts after everything queued so far (the learner
-            # that wrote the parameters).  Ordered here, before any group's
-            # persistent launch is resident: nothing after a launch may wait for
-            # the device while the host is pacing it
-            self.stream.wait_stream(torch.cuda.current_stream(self.pop.device))
         else:
             self.obs, _ = self.env.reset()
 
@@ -521,13 +547,23 @@ class _EvalDriver:
         pop = self.pop
         n = _EVAL_CHUNK if self.max_steps is None else min(_EVAL_CHUNK, int(self.max_steps) - self.step)
         self.ctl_h.zero_()
-        _lib.check(lib.agx_ppo_eval_persistent(ctypes.byref(self.desc), self.P, self.N, pop.params.data.data_ptr(),
-                                               self.obs_h.data_ptr(), None, self.act_h.data_ptr(),
-                                               pop.env_base_d.data_ptr(), n, 0, pop.act_seed,
-                                               self.counter0 + self.step, self.args_h.data_ptr(),
-                                               self.ctl_h.data_ptr(), self.runner.timeout_s,
-                                               self.stream.cuda_stream),
-                   "agx_ppo_eval_persistent")
+        if self.desc is not None:
+            _lib.check(lib.agx_ppo_eval_persistent(ctypes.byref(self.desc), self.P, self.N,
+                                                   pop.params.data.data_ptr(), self.obs_h.data_ptr(), None,
+                                                   self.act_h.data_ptr(), pop.env_base_d.data_ptr(), n, 0, pop.act_seed,
+                                                   self.counter0 + self.step, self.args_h.data_ptr(),
+                                                   self.ctl_h.data_ptr(), self.runner.timeout_s,
+                                                   self.stream.cuda_stream),
+                       "agx_ppo_eval_persistent")
+        else:  # a mutated shape (its act workspace was taken at construction)
+            _lib.check(lib.agx_ppo_eval_graph_persistent(ctypes.byref(self.gdesc), self.P, self.N,
+                                                         pop.params.data.data_ptr(), self.obs_h.data_ptr(), None,
+                                                         self.act_h.data_ptr(), pop.env_base_d.data_ptr(), n, 0,
+                                                         pop.act_seed, self.counter0 + self.step,
+                                                         self.args_h.data_ptr(), self.ctl_h.data_ptr(),
+                                                         self.runner.timeout_s, pop._act_ws[1].data_ptr(),
+                                                         self.stream.cuda_stream),
+                       "agx_ppo_eval_graph_persistent")
         _pacing_begin()
         self.launch_step0 = self.step
         self.launched_to = self.step + n
@@ -541,6 +577,10 @@ class _EvalDriver:
                 self._launch()
             _lib.load().agx_host_signal(self.ctl_h.data_ptr(), self.step - self.launch_step0 + 1)
             return
+        with torch.cuda.stream(self.stream):  # never the NULL stream: it would wait for resident launches
+            self._request_step()
+
+    def _request_step(self) -> None:
         pop, P, N, D = self.pop, self.P, self.N, self.D
         self.obs_h.numpy()[:] = np.asarray(self.obs).reshape(-1)
         self.obs_d.view(-1).copy_(self.obs_h, non_blocking=True)
@@ -622,10 +662,11 @@ class _EvalDriver:
 
 AGX_ROLLOUT_STOP = 0xFFFFFFFE  # include/agx.h
 
-# Dedicated non-blocking streams for persistent evaluation launches, one per
+# Dedicated non-blocking streams for the evaluation passes, one per
 # lock-stepped group, created once per process (agx_stream_create).  Not from
 # torch's stream pool: its round-robin could hand two groups the same stream,
-# and one resident persistent launch would then hold the other's back.
+# and one resident persistent launch would then hold the other's back; and not
+# the legacy NULL stream, whose work waits for every blocking stream.
 _EVAL_STREAMS: list = []
 
 
@@ -644,11 +685,10 @@ def run_lockstep(drivers: list) -> None:
     the groups' device work and host env steps overlap instead of running
     one pass after another."""
     active = list(drivers)
-    k = 0
-    for d in active:
-        if d.persistent:
-            d.stream = _eval_stream(k)
-            k += 1
+    # every driver on a stream of its own, none on the legacy NULL stream (work
+    # there would wait for the other groups' resident persistent launches)
+    for k, d in enumerate(active):
+        d.stream = _eval_stream(k)
     try:
         for d in active:  # every group's stream ordering first, then the launches
             d.begin()

@@ -29,7 +29,7 @@ import numpy as np
 
 from ..algorithms.dqn import DQN, RainbowDQN
 from ..components.sampler import Sampler
-from ..hpo.shard import all_ranks, mutate_population, sync_host_rngs, world_rank
+from ..hpo.shard import all_gather_obj, all_ranks, mutate_population, sync_host_rngs, world_rank
 from ..hpo.sharded import select_population
 
 
@@ -113,7 +113,7 @@ def train_off_policy(env, env_name: str, algo: str, pop, memory, INIT_HP=None, M
             import torch.distributed as dist
 
             box: list = [None] * world
-            dist.all_gather_object(box, fitnesses)
+            all_gather_obj(box, fitnesses, tag="fitness")
             pop_fitnesses.append([f for b in box for f in b])
         else:
             pop_fitnesses.append(fitnesses)

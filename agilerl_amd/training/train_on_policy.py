@@ -49,7 +49,7 @@ import torch.distributed as dist
 
 from ..envs import StackedVecEnv
 from ..hpo.population_sync import PopulationSync
-from ..hpo.shard import all_ranks, gather_records, mutate_population
+from ..hpo.shard import all_gather_obj, all_ranks, gather_records, mutate_population
 from ..population.engine import PopulationEngine
 
 
@@ -137,7 +137,7 @@ def _all_one_group(engine) -> bool:
     if engine.world == 1:
         return mine[0]
     box: list = [None] * engine.world
-    dist.all_gather_object(box, mine)
+    all_gather_obj(box, mine, tag="group_shapes")
     return all(b[0] for b in box) and len({(b[1], b[2]) for b in box}) == 1
 
 
@@ -147,7 +147,7 @@ def _apply_mutations(engine) -> None:
     changed = engine.pending()
     if engine.world > 1:
         box: list = [None] * engine.world
-        dist.all_gather_object(box, changed)
+        all_gather_obj(box, changed, tag="mutated_flags")
         changed = any(box)
     if changed:
         engine.regroup(engine.local_states())
@@ -238,7 +238,7 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
             agent.steps.append(agent.steps[-1])
         if world > 1:
             box: list = [None] * world
-            dist.all_gather_object(box, fitness)
+            all_gather_obj(box, fitness, tag="fitness")
             pop_fitnesses.append([f for b in box for f in b])
         else:
             pop_fitnesses.append(fitness)

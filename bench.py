@@ -949,7 +949,9 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
     variants = [("ppo_yaml", 0.2), ("no_arch_mutation", 0.0)]
     if os.environ.get("AGX_BENCH_E2E_NO_ARCH_ONLY"):
         variants = variants[1:]
-    from agilerl_amd.training import train_on_policy as top_mod
+    import importlib
+
+    top_mod = importlib.import_module("agilerl_amd.training.train_on_policy")  # the module (PHASE_TIMES)
 
     def one(arch: float, gens: int, seed: int) -> dict:
         top_mod.PHASE_TIMES.clear()

@@ -65,6 +65,36 @@ int agx_ppo_act_graph(const agx_ppo_graph *net, int64_t P, int64_t N, const floa
                       float *entropy, int64_t out_agent_stride, int64_t *actions_flat,
                       const int64_t *agent_env_base, void *workspace, void *stream);
 
+/* Partnered-learner phase timing: subsequent agx_ppo_learn_graph calls that
+ * split minibatches over partners write shader-cycle stamps of agent 0,
+ * partner 0, update 1 into buf (device int64[10]: start, gradients done,
+ * loss words, barrier 1, reduce-scatter, barrier 2, norms, Adam, barrier 3,
+ * acquire); NULL disables. */
+int agx_debug_graph_stamps(int64_t *buf);
+/* Persistent rollout / evaluation of a runtime-shape population: the
+ * host-paced loops of agx_ppo_rollout_persistent and agx_ppo_eval_persistent
+ * (agx.h: same agx_rollout_io steps, control block protocol, Philox counters,
+ * AGX_ROLLOUT_ABORT / AGX_ROLLOUT_STOP) around agx_ppo_act_graph's step, one
+ * launch per rollout (replaces rollouts/on_policy.py:23-203's per-step
+ * forward for mutated architectures).  The grid is
+ * agx_ppo_rollout_graph_workgroups(P, N) workgroups (16 env rows each), all of
+ * which must be co-resident (AGX_EUNSUPPORTED beyond
+ * agx_ppo_rollout_graph_max_workgroups()); the control block holds
+ * agx_ppo_rollout_graph_ctl_bytes(P, N) bytes; `workspace` as
+ * agx_ppo_act_graph. */
+int64_t agx_ppo_rollout_graph_workgroups(int64_t P, int64_t N);
+int64_t agx_ppo_rollout_graph_max_workgroups(void);
+size_t agx_ppo_rollout_graph_ctl_bytes(int64_t P, int64_t N);
+int agx_ppo_rollout_graph_persistent(const agx_ppo_graph *net, int64_t P, int64_t N, const float *params,
+                                     const agx_rollout_io *ios, int64_t nsteps, uint32_t base, uint64_t seed,
+                                     uint64_t counter0, void *args_host, agx_rollout_ctl *ctl, double timeout_s,
+                                     void *workspace, void *stream);
+int agx_ppo_eval_graph_persistent(const agx_ppo_graph *net, int64_t P, int64_t N, const float *params,
+                                  const float *stage_obs, const uint8_t *stage_mask, int64_t *actions_flat,
+                                  const int64_t *agent_env_base, int64_t nsteps, uint32_t base, uint64_t seed,
+                                  uint64_t counter0, void *args_host, agx_rollout_ctl *ctl, double timeout_s,
+                                  void *workspace, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

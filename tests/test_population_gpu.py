@@ -668,3 +668,40 @@ def test_engine_evaluates_groups_in_lockstep(monkeypatch):
         for r, slot in enumerate(g.slots):
             alone[slot] = float(f[r])
     assert fit == alone
+
+
+@pytest.mark.parametrize("evaluate", [False, True])
+def test_graph_persistent_rollout_matches_per_step_launches(monkeypatch, evaluate):
+    """A mutated (runtime-shape) network: ONE persistent launch per rollout
+    (agx_ppo_rollout_graph_persistent) gives the rollout, bootstrap values,
+    episode statistics and — after the runtime-shape learn() — parameters of
+    one agx_ppo_act_graph launch per step, bit for bit; so does the
+    persistent evaluation (agx_ppo_eval_graph_persistent)."""
+    from agilerl_amd.envs import SyntheticVecEnv
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.ppo_pop import PPOPopulation
+    from agilerl_amd.population.runner import PopulationRunner
+
+    out = []
+    for persistent in (True, False):
+        monkeypatch.setenv("AGX_PERSISTENT_ROLLOUT", "1" if persistent else "0")
+        spec = ActorCriticSpec(obs_dim=8, n_actions=4, encoder_hidden=[80], latent_dim=56, actor_hidden=[64, 64])
+        P, N = 3, 40
+        pop = PPOPopulation(spec, P, N, learn_step=8 * N, batch_size=64, update_epochs=2, device=DEV,
+                            seeds=list(range(P)), fused=True, perm_source="device")
+        assert pop.fused_descriptor() is None and pop.learn_descriptor() is not None
+        run = PopulationRunner(pop, SyntheticVecEnv(P * N, seed=5, p_done=0.2, max_episode_steps=30))
+        assert run.graph_persistent == persistent and not run.persistent
+        fit = None
+        for i in range(3):
+            run.iteration()
+            if evaluate and i == 1:
+                fit = run.evaluate(loop=1, max_steps=None)
+        torch.cuda.synchronize()
+        out.append([pop.obs.clone(), pop.actions.clone(), pop.log_probs.clone(), pop.values.clone(),
+                    pop.rewards.clone(), pop.dones.clone(), run.last_value.clone(), run.episodes.clone(),
+                    pop.params.data.clone(), pop.opt.exp_avg.clone()])
+        if evaluate:
+            out[-1].append(torch.as_tensor(fit))
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
