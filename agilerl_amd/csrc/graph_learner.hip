@@ -80,6 +80,7 @@ struct GArgs {
     unsigned *cnt;         // barrier counters, timeout word, XCC ids (zeroed by the gather)
     unsigned *err;         // caller's sticky error word
     int write_through;     // test hook: the cross-XCD (release-fence) publish form always
+    int lds_act;           // the partner's activation scratch (ws_part floats) in dynamic LDS, not at ws
     long long *stamps;     // diagnostic phase stamps of the partnered learner (agx_debug_graph_stamps), or null
     float *ws;
     float *params, *m, *v;
@@ -151,7 +152,7 @@ constexpr int kGemmLds = 2 * kPanel;        // double-buffered
 // kBN wide: the epilogue runs S's ReLU / LayerNorm(+affine) backward on the
 // whole rows of dY it holds and writes S's dZ (dzr_s / dzc_s) and per-wave
 // bias / LN-affine column partials (colp_s): S needs no row pass of its own.
-template <int MODE = 0, class FE>
+template <int MODE = 0, bool DIRECT = false, class FE>
 __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B, int ldb, int M, int N, int K,
                                         float *lds, const float *bias, FE epi, const GLay &L,
                                         float *base = nullptr, const float *pr = nullptr, int bp = 0,
@@ -185,21 +186,15 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 const int k = kc + lk;
                 const bool kin = k < K;
                 const int kk = kin ? k : 0;
-                // unconditional loads from clamped (valid) addresses, then the
-                // predicate; staging rows wholly past the block (a few-row block:
-                // the partnered learner's 8-16 rows) are neither loaded nor
-                // committed (workgroup-uniform: no MFMA tile reads them for an
-                // output row that is kept)
+                // unconditional loads from clamped (valid) addresses, then the predicate
 #pragma unroll
                 for (int i = 0; i < kBM / kRS; ++i) {
-                    if (kRS * i >= BM) break;
                     const int row = lr + kRS * i;
                     const float va = Ab[(size_t)(row < BM ? row : 0) * lda + kk];
                     ra[i] = (row < BM && kin) ? va : 0.f;
                 }
 #pragma unroll
                 for (int i = 0; i < kBN / kRS; ++i) {
-                    if (kRS * i >= BN) break;
                     const int row = lr + kRS * i;
                     const float vb = Bb[(size_t)(row < BN ? row : 0) * ldb + kk];
                     rb[i] = (row < BN && kin) ? vb : 0.f;
@@ -208,15 +203,9 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
             auto commit = [&](int buf) {
                 float *As = lds + buf * kPanel, *Bs = As + kBM * kLdS;
 #pragma unroll
-                for (int i = 0; i < kBM / kRS; ++i) {
-                    if (kRS * i >= BM) break;
-                    As[(lr + kRS * i) * kLdS + lk] = ra[i];
-                }
+                for (int i = 0; i < kBM / kRS; ++i) As[(lr + kRS * i) * kLdS + lk] = ra[i];
 #pragma unroll
-                for (int i = 0; i < kBN / kRS; ++i) {
-                    if (kRS * i >= BN) break;
-                    Bs[(lr + kRS * i) * kLdS + lk] = rb[i];
-                }
+                for (int i = 0; i < kBN / kRS; ++i) Bs[(lr + kRS * i) * kLdS + lk] = rb[i];
             };
             f4 acc[kTPW];
             // per slot: the bias of column n0 + r (and with LNE the LN affine),
@@ -230,6 +219,36 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 const float v = bias ? bias[nb + (ok ? n0 + r : 0)] : 0.f;
                 bv_[j] = v;
             }
+            if constexpr (DIRECT) {
+                // the partnered learner's few-row minibatch slices: every wave loads
+                // its tiles' operands straight from L2 (operand rows other waves
+                // also read are L1 hits) — no LDS staging and no barriers: one round
+                // trip per 32-deep chunk instead of a staged pipeline per block
+                for (int kc = 0; kc < K; kc += kKC) {
+#pragma unroll
+                    for (int j = 0; j < kTPW; ++j) {
+                        int m0, n0;
+                        if (tile(j, m0, n0)) {  // wave-uniform
+                            float av[8], bv[8];
+                            const int m = m0 + r, n = n0 + r;
+#pragma unroll
+                            for (int kk = 0; kk < 8; ++kk) {
+                                const int k = kc + 4 * kk + q;
+                                const int kq = k < K ? k : 0;
+                                const float xa = Ab[(size_t)(m < BM ? m : 0) * lda + kq];
+                                const float xb = Bb[(size_t)(n < BN ? n : 0) * ldb + kq];
+                                av[kk] = (k < K && m < BM) ? xa : 0.f;
+                                bv[kk] = (k < K && n < BN) ? xb : 0.f;
+                            }
+#pragma unroll
+                            for (int kk = 0; kk < 8; ++kk) {
+                                if (kc + 4 * kk >= K) break;  // uniform: a short last chunk
+                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc[j], 0, 0, 0);
+                            }
+                        }
+                    }
+                }
+            } else {
             fetch(0);
             if (mb | nb) __syncthreads();  // the previous block's last panels may still be read
             commit(0);
@@ -262,6 +281,7 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 }
                 buf ^= 1;
             }
+            }  // staged
             if constexpr (LNE) {
                 const float invF = 1.f / (float)N;
                 // the LN affine of the lane's four columns, loaded before any store
@@ -701,8 +721,9 @@ __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float
 // keeping xhat / rstd / the feature-major copy where the plan has room for
 // them (the learner; the policy step keeps outputs only).  xobs: the
 // observation rows (stride = the first layer's fin).
+template <bool DIRECT = false>
 __device__ __forceinline__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bsz, float *base, const float *pr,
-                               int bp, float *lds, int dbg = 0) {
+                               int bp, float *lds, int dbg = 0, long long *st = nullptr) {
     for (int l = 0; l < nl; ++l) {
         const GLay &L = Ls[l];
         const float *x = L.src < 0 ? xobs : base + Ls[L.src].yr;
@@ -712,17 +733,21 @@ __device__ __forceinline__ void forward_layers(const GLay *Ls, int nl, const flo
         const bool lne = F <= kBN && (L.ln || L.relu);  // LayerNorm / ReLU in the GEMM epilogue
         if (!(dbg & 1)) {
             if (lne)
-                gemm_nt<1>(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
-                              [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; }, L, base, pr, bp);
+                gemm_nt<1, DIRECT>(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
+                                   [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; }, L, base, pr, bp);
             else
-                gemm_nt(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
-                        [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; }, L);
+                gemm_nt<0, DIRECT>(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
+                                   [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; }, L);
         }
         __syncthreads();
-        if (lne || (L.ln == 0 && !L.relu && L.yc < 0) || (dbg & 8)) continue;
+        if (lne || (L.ln == 0 && !L.relu && L.yc < 0) || (dbg & 8)) {
+            if (st) st[1 + l] = (long long)__builtin_readcyclecounter();
+            continue;
+        }
         if (F <= 128) fwd_rows<8>(L, base, pr, bsz, bp);
         else fwd_rows<0>(L, base, pr, bsz, bp);
         __syncthreads();
+        if (st) st[1 + l] = (long long)__builtin_readcyclecounter();
     }
 }
 
@@ -734,10 +759,12 @@ __device__ __forceinline__ void forward_layers(const GLay *Ls, int nl, const flo
 // it).  base: this workgroup's activation scratch; wb: where the transposed
 // weights live (wb + L.wt).  Shared by the one-workgroup-per-agent learner and
 // the partnered one (each partner over its slice of the rows).
+template <bool DIRECT = false>
 __device__ __forceinline__ void minibatch_grads(const GArgs &g, float *base, const float *wb, const float *pr, float *G,
                                                 const float *xobs, const int *gact_e, const unsigned *gmask_e,
                                                 const float *grow_e, long long s0, int bsz, float inv_b, float entp,
-                                                float *lds, float *colp, float *colo, float &lsum, float &klsum) {
+                                                float *lds, float *colp, float *colo, float &lsum, float &klsum,
+                                                long long *st = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int sub = lane & 15, rq = lane >> 4;
     const int bp = g.bp, A = g.A, D = g.D;
@@ -750,7 +777,8 @@ __device__ __forceinline__ void minibatch_grads(const GArgs &g, float *base, con
     }
 
     // ---- forward, layer by layer ------------------------------------
-    forward_layers(g.L, g.nl, xobs, bsz, base, pr, bp, lds, g.dbg);
+    if (st) st[0] = (long long)__builtin_readcyclecounter();
+    forward_layers<DIRECT>(g.L, g.nl, xobs, bsz, base, pr, bp, lds, g.dbg, st);
 
     // ---- loss row pass: logits / value -> d(logits), d(value) (ppo.py:876-908)
     if (!(g.dbg & 8)) {
@@ -868,6 +896,7 @@ __device__ __forceinline__ void minibatch_grads(const GArgs &g, float *base, con
         for (int w = 0; w < kGW; ++w) sb += colo[w * 33 + (tid < A ? tid : 32)];
         G[tid < A ? g.L[g.aout].b + tid : g.L[g.cout].b] = sb;
     }
+    if (st) st[17] = (long long)__builtin_readcyclecounter();
 
     // ---- backward, layer by layer (reverse) ----------------------------
     float *t1c = base + g.t1, *t2c = base + g.t2;
@@ -885,6 +914,7 @@ __device__ __forceinline__ void minibatch_grads(const GArgs &g, float *base, con
             else bwd_rows<0>(L, base, pr, bsz, bp, dzr, dzc, t1c, t2c);
         }
         if (!outl && !L.fused) __syncthreads();
+        if (st) st[18 + 3 * l] = (long long)__builtin_readcyclecounter();
         // bias / LN-affine gradients: column sums over the rows (fixed order);
         // up to 8 feature groups summed before the first store
         if (F <= 128 && !(g.dbg & 24) && !outl) {  // the row pass left per-wave partials in LDS
@@ -943,6 +973,7 @@ __device__ __forceinline__ void minibatch_grads(const GArgs &g, float *base, con
         const int fin = L.fin;
         for (int job = 0; job < (L.src >= 0 ? 2 : 1); ++job) {
             if (job) __syncthreads();  // the dW GEMM's last panels are still being read
+            if (st && job) st[19 + 3 * l] = (long long)__builtin_readcyclecounter();
             if (g.dbg & (job ? 4 : 2)) continue;
             const float *ga = job ? (outl ? base + L.dy : dzr) : (outl ? base + L.dyc : dzc);
             const float *gb = job ? wb + L.wt : xc;
@@ -951,15 +982,16 @@ __device__ __forceinline__ void minibatch_grads(const GArgs &g, float *base, con
             float *dst = job ? base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy) : G + L.w;
             if (job && L.fuse) {  // the source's dZ (other parity) from the epilogue
                 const int s_ = L.src;
-                gemm_nt<2>(ga, lda, gb, ldb, M, fin, K, lds, nullptr, [](int, int, float) {}, g.L[s_], base, pr,
+                gemm_nt<2, DIRECT>(ga, lda, gb, ldb, M, fin, K, lds, nullptr, [](int, int, float) {}, g.L[s_], base, pr,
                            bp, base + ((s_ & 1) ? g.dzr1 : g.dzr), base + ((s_ & 1) ? g.dzc1 : g.dzc),
                            colp + (s_ & 1) * 3 * kGW * 128);
             } else {
-                gemm_nt(ga, lda, gb, ldb, M, fin, K, lds, nullptr,
-                        [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; }, L);
+                gemm_nt<0, DIRECT>(ga, lda, gb, ldb, M, fin, K, lds, nullptr,
+                                   [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; }, L);
             }
         }
         __syncthreads();
+        if (st) st[20 + 3 * l] = (long long)__builtin_readcyclecounter();
     }
 
 }
@@ -1122,6 +1154,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_kernel(const GArgs g) {
 // which other agents share the launch.
 // ---------------------------------------------------------------------------
 constexpr int kMaxGK = 16;
+constexpr size_t kLdsMax = 160 * 1024;  // LDS per CU (gfx950)
 constexpr unsigned kGSpinMax = 1u << 23;
 
 __device__ __forceinline__ bool gpart_sync(unsigned *ctr, unsigned target, bool release, unsigned *tmo,
@@ -1160,6 +1193,17 @@ __device__ __forceinline__ void gpart_acquire() {
     __syncthreads();
 }
 
+// the partner's few-row GEMMs with operands loaded straight from L2 (1) or
+// staged through LDS (0, measured faster: r5 graph_stamps)
+#ifndef AGX_GRAPH_DIRECT
+#define AGX_GRAPH_DIRECT 0
+#endif
+
+// inner stamps of minibatch_grads: [0] forward start, [1 + l] layer l's forward
+// done, [17] loss pass done, [18 + 3l] / [19 + 3l] / [20 + 3l] layer l's row pass,
+// dW and dX done
+constexpr int kGStampsIn = 18 + 3 * kGL;
+
 __device__ __forceinline__ float ld_sc1(const float *p) {
     return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1170,7 +1214,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
     __shared__ float colp[2 * 3 * kGW * 128];
     __shared__ float colo[kGW * 33];
     __shared__ int s_ok;
-    __shared__ long long s_st[16];  // phase stamps (agent 0, partner 0, update 1)
+    __shared__ long long s_st[16 + kGStampsIn];  // phase stamps (agent 0, partner 0, update 1), then per layer
     if (g.skip && __hip_atomic_load(g.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const int b = blockIdx.x;
     const int p = b % g.Q, kk = b / g.Q;
@@ -1181,7 +1225,11 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
     float *const pr = g.params + (size_t)p * n;
     float *const gm = g.m + (size_t)p * n;
     float *const gv = g.v + (size_t)p * n;
-    float *const base = g.ws + ((size_t)p * K + kk) * g.ws_part;
+    // the activation scratch: this workgroup's dynamic LDS when the plan fits
+    // (every row pass, GEMM operand and epilogue store then stays on the CU),
+    // else its block of the global scratch
+    extern __shared__ __attribute__((aligned(16))) float gdyn[];
+    float *const base = g.lds_act ? gdyn : g.ws + ((size_t)p * K + kk) * g.ws_part;
     float *const wsh = g.wtb + (size_t)p * g.wt_agent;  // the agent's shared transposed weights
     float *const wb = wsh - g.wt0;                      // wb + L.wt lands in wsh
     unsigned *const c0 = g.cnt + p, *const c1 = g.cnt + P + p, *const c2 = g.cnt + 2 * P + p;
@@ -1257,8 +1305,8 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
             // ---- 1. this partner's rows -> its partial gradient row ----------------
             float lsum = 0.f, klsum = 0.f;
             if (rk > 0) {
-                minibatch_grads(g, base, wb, pr, G, gobs_e + (s0 + r0) * D, gact_e, gmask_e, grow_e, s0 + r0, rk,
-                                inv_b, entp, lds, colp, colo, lsum, klsum);
+                minibatch_grads<AGX_GRAPH_DIRECT>(g, base, wb, pr, G, gobs_e + (s0 + r0) * D, gact_e, gmask_e, grow_e, s0 + r0, rk,
+                                inv_b, entp, lds, colp, colo, lsum, klsum, stamp ? s_st + 16 : nullptr);
             } else {  // no rows this minibatch (a short last minibatch): publish zeros
                 for (int i = tid; i < n; i += kGT) G[i] = 0.f;
             }
@@ -1277,34 +1325,46 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
             {
                 const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab0, 0, __builtin_amdgcn_readfirstlane(
                                                                                  (int)(K * g.nslab * 4)), 0x00020000);
-                for (int c = own0 + tid; c < own1; c += kGT) {
-                    // partner order, 8 loads in flight at a time
-                    f4 t = f4{0.f, 0.f, 0.f, 0.f};
+                // two chunks per thread per round, partner order, up to 16 loads in flight
+                for (int cb = own0 + tid; cb < own1; cb += 2 * kGT) {
+                    f4 t[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
                     for (int q0_ = 0; q0_ < K; q0_ += 8) {  // uniform
-                        f4 x[8];
+                        f4 x[2][8];
 #pragma unroll
-                        for (int q = 0; q < 8; ++q) {
-                            const int qq = q0_ + q, qs = qq < K ? qq : K - 1;
-                            const f4 v = __builtin_bit_cast(
-                                f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((qs * g.nslab + 4 * c) * 4), 0, 16));
-                            x[q] = qq < K ? v : f4{0.f, 0.f, 0.f, 0.f};
+                        for (int h = 0; h < 2; ++h) {
+                            const int c = cb + h * kGT, cl = c < own1 ? c : own0;
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) {
+                                const int qq = q0_ + q, qs = qq < K ? qq : K - 1;
+                                const f4 v = __builtin_bit_cast(
+                                    f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((qs * g.nslab + 4 * cl) * 4), 0, 16));
+                                x[h][q] = qq < K ? v : f4{0.f, 0.f, 0.f, 0.f};
+                            }
                         }
-                        if (q0_ == 0) {
-                            t = x[0];
 #pragma unroll
-                            for (int q = 1; q < 8; ++q) t += x[q];
-                        } else {
+                        for (int h = 0; h < 2; ++h) {
+                            if (q0_ == 0) {
+                                t[h] = x[h][0];
 #pragma unroll
-                            for (int q = 0; q < 8; ++q) t += x[q];
+                                for (int q = 1; q < 8; ++q) t[h] += x[h][q];
+                            } else {
+#pragma unroll
+                                for (int q = 0; q < 8; ++q) t[h] += x[h][q];
+                            }
                         }
                     }
-                    *reinterpret_cast<f4 *>(sum + 4 * c) = t;
 #pragma unroll
-                    for (int cc = 0; cc < 4; ++cc) {
-                        const int f = 4 * c + cc;
-                        const float x2 = f < n ? t[cc] * t[cc] : 0.f;
-                        if (f < g.cstart) q0 += x2;
-                        else q1 += x2;
+                    for (int h = 0; h < 2; ++h) {
+                        const int c = cb + h * kGT;
+                        if (c >= own1) break;
+                        *reinterpret_cast<f4 *>(sum + 4 * c) = t[h];
+#pragma unroll
+                        for (int cc = 0; cc < 4; ++cc) {
+                            const int f = 4 * c + cc;
+                            const float x2 = f < n ? t[h][cc] * t[h][cc] : 0.f;
+                            if (f < g.cstart) q0 += x2;
+                            else q1 += x2;
+                        }
                     }
                 }
                 q0 = wave_sum(q0);
@@ -1344,17 +1404,18 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
             const float bc2s = (float)sqrt(1.0 - pb2);
             const float step_size = lr_p / bc1;
             const float ob1 = 1.f - g.b1, ob2 = 1.f - g.b2;
-            // the owned float range [f0, f1), region by region (per layer W with its
-            // transposed copy, b, LN weight, LN bias): all loads of a round first
-            auto adam_range = [&](int r0_, int cnt, long long wt, int fin, int fout) {
-                const int lo = f0 - r0_ > 0 ? f0 - r0_ : 0, hi = f1 - r0_ < cnt ? f1 - r0_ : cnt;
+            // the owned float range [f0, f1) in one pass, U elements per thread per
+            // round (all loads of a round first); an element inside a layer's W
+            // also goes to the transposed copy (the layer found by a short scan of
+            // the layer list: contiguous W ranges, at most 16 layers)
+            {
                 constexpr int U = 8;
-                for (int i0 = lo + tid; i0 < hi; i0 += U * kGT) {
+                for (int i0 = f0 + tid; i0 < f1; i0 += U * kGT) {
                     float gg[U], mm[U], vv[U], pp[U];
 #pragma unroll
                     for (int k = 0; k < U; ++k) {
                         const int i = i0 + k * kGT;
-                        const int f = r0_ + (i < hi ? i : lo);
+                        const int f = i < f1 ? i : f0;
                         gg[k] = sum[f];  // this partner's own reduce-scatter stores
                         mm[k] = gm[f];
                         vv[k] = gv[f];
@@ -1362,9 +1423,8 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
                     }
 #pragma unroll
                     for (int k = 0; k < U; ++k) {
-                        const int i = i0 + k * kGT;
-                        if (i >= hi) break;
-                        const int f = r0_ + i;
+                        const int f = i0 + k * kGT;
+                        if (f >= f1) break;
                         const float gc = gg[k] * (f < g.cstart ? cl0 : cl1);
                         const float m = mm[k] + ob1 * (gc - mm[k]);
                         const float v = vv[k] * g.b2 + ob2 * gc * gc;
@@ -1372,21 +1432,17 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
                         gm[f] = m;
                         gv[f] = v;
                         pr[f] = np_;
-                        if (wt >= 0) {
-                            const int o = i / fin, c = i - o * fin;
-                            wb[wt + (size_t)c * fout + o] = np_;
+                        for (int l = 0; l < g.nl; ++l) {
+                            const GLay &L = g.L[l];
+                            const int i = f - L.w;
+                            if (L.wt >= 0 && i >= 0 && i < L.fout * L.fin) {
+                                const int o = i / L.fin, c = i - o * L.fin;
+                                wb[L.wt + (size_t)c * L.fout + o] = np_;
+                                break;
+                            }
                         }
                     }
                 }
-            };
-            for (int rg = 0; rg < 4 * g.nl; ++rg) {
-                const GLay &L = g.L[rg >> 2];
-                const int kind = rg & 3;
-                if (kind >= 2 && L.ln != 2) continue;
-                const int rf = kind == 0 ? L.w : kind == 1 ? L.b : kind == 2 ? L.g : L.be;
-                const int cnt = kind == 0 ? L.fout * L.fin : L.fout;
-                if (rf >= f1 || rf + cnt <= f0) continue;  // uniform: no owned float in the region
-                adam_range(rf, cnt, kind == 0 ? L.wt : -1, kind == 0 ? L.fin : 1, kind == 0 ? L.fout : 1);
             }
             GST(7);
             // ---- 4. every partner's chunks visible to this one's next plain loads ---------
@@ -1405,7 +1461,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
         if (g.epochs_out) g.epochs_out[p] = epochs_done;
         g.step[p] = step0 + n_done;
     }
-    if (g.stamps && b == 0 && tid < 10) g.stamps[tid] = s_st[tid];
+    if (g.stamps && b == 0 && tid < 16 + kGStampsIn) g.stamps[tid] = s_st[tid];
 }
 
 
@@ -1834,28 +1890,70 @@ int cu_count_g() {
     }
     return n;
 }
-int part_occupancy() {  // co-resident partner workgroups per CU (queried once)
-    static int n = -1;
-    if (n < 0) {
+int part_occupancy(size_t dyn) {  // co-resident partner workgroups per CU with dyn bytes of dynamic LDS
+    static size_t last = (size_t)-1;
+    static int n = 1;
+    if (dyn != last) {
         int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_learn_graph_part_kernel, kGT, 0) != hipSuccess) v = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_learn_graph_part_kernel, kGT, dyn) != hipSuccess) v = 1;
         n = v < 1 ? 1 : v;
+        last = dyn;
     }
     return n;
 }
-void graph_split(int64_t P, int64_t batch, int &K, int &R, int &Q) {
-    int rows = 16;
-    if (const char *e = getenv("AGX_GRAPH_ROWS")) rows = atoi(e) >= 1 ? atoi(e) : 16;
-    int k = (int)((batch + rows - 1) / rows);
+// dynamic LDS a partner may take for its activations: the CU's 160 KB less the
+// kernel's static LDS (queried once)
+size_t part_lds_budget() {
+    static size_t b = 0;
+    if (!b) {
+        hipFuncAttributes fa{};
+        const size_t st = hipFuncGetAttributes(&fa, (const void *)ppo_learn_graph_part_kernel) == hipSuccess
+                              ? fa.sharedSizeBytes
+                              : 80 * 1024;
+        b = st < kLdsMax ? kLdsMax - st : 1;
+        (void)hipFuncSetAttribute((const void *)ppo_learn_graph_part_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
+    }
+    return b;
+}
+// The partnered learner's split of a minibatch: K partners of R rows while the
+// whole grid (Q x K workgroups, Q = P rounded up to the 8 XCDs) stays
+// co-resident; K = 1: the one-workgroup-per-agent kernel.  Rows per partner:
+// AGX_GRAPH_ROWS, else 16, or with AGX_GRAPH_LDS=1 the largest of 16 / 8 whose
+// activation scratch fits the workgroup's LDS (dyn = its bytes; 0: the global
+// scratch).  AGX_GRAPH_SPLIT caps K (tests, diagnostics).
+void graph_split(const agx_ppo_graph *net, int64_t P, int64_t batch, int &K, int &R, int &Q, size_t &dyn) {
+    int rows_env = 0;
+    if (const char *e = getenv("AGX_GRAPH_ROWS")) rows_env = atoi(e) >= 1 ? atoi(e) : 16;
     int cap = kMaxGK;
     if (const char *e = getenv("AGX_GRAPH_SPLIT")) cap = atoi(e) >= 1 ? atoi(e) : 1;
-    if (k > cap) k = cap;
+    // off by default: through a generic pointer every scratch access becomes a
+    // flat instruction, measured 5 % slower than the global scratch (r5)
+    bool lds_ok = false;
+    if (const char *e = getenv("AGX_GRAPH_LDS")) lds_ok = atoi(e) != 0;
     Q = (int)((P + 7) / 8 * 8);
-    const int64_t resident = (int64_t)part_occupancy() * cu_count_g();
-    while (k > 1 && (int64_t)Q * k > resident) --k;
-    if (k > 1 && (int64_t)P * k > resident) k = 1;
+    const size_t budget = part_lds_budget();
+    auto fit = [&](int k) -> size_t {  // dynamic LDS bytes of a k-way split, 0 when the scratch is global
+        if (!lds_ok || k <= 1) return 0;
+        GArgs ap{};
+        if (plan_graph(net, (batch + k - 1) / k, ap) != AGX_OK) return 0;
+        const size_t b = (size_t)ap.ws_part * 4;
+        return b <= budget ? b : 0;
+    };
+    auto split_of = [&](int rows) { const int k = (int)((batch + rows - 1) / rows); return k > cap ? cap : k; };
+    int k = split_of(rows_env ? rows_env : 16);
+    size_t d = fit(k);
+    if (!rows_env && !d) {
+        const int k8 = split_of(8);
+        const size_t d8 = fit(k8);
+        if (d8) k = k8, d = d8;
+    }
+    const int64_t cus = cu_count_g();
+    while (k > 1 && (int64_t)Q * k > (int64_t)part_occupancy(d) * cus) d = fit(--k);
+    if (k > 1 && (int64_t)P * k > (int64_t)part_occupancy(d) * cus) k = 1;
     K = k < 1 ? 1 : k;
     R = (int)((batch + K - 1) / K);
+    dyn = K > 1 ? d : 0;
 }
 struct PartWs {
     size_t cnt, gobs, gact, gmask, grow, scratch, wt, slabs, sums, total;
@@ -1906,7 +2004,8 @@ extern "C" size_t agx_ppo_learn_graph_workspace_bytes(const agx_ppo_graph *net, 
     if (plan_graph(net, bb, a) != AGX_OK) return 0;
     size_t total = graph_ws(a, P, S, epochs).total;
     int K, R, Q;
-    graph_split(P, bb, K, R, Q);
+    size_t dyn;
+    graph_split(net, P, bb, K, R, Q, dyn);
     if (K > 1) {  // room for either kernel: the split may change with the call's batch
         GArgs ap{};
         if (plan_graph(net, R, ap) != AGX_OK) return 0;
@@ -1928,7 +2027,8 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
                 (long long)epochs, (long long)batch);
     const int64_t bb = batch < S ? batch : S;
     int K = 1, R = (int)bb, Q = (int)P;
-    graph_split(P, bb, K, R, Q);
+    size_t dyn = 0;
+    graph_split(net, P, bb, K, R, Q, dyn);
     GArgs a{};
     const int rc = plan_graph(net, K > 1 ? R : bb, a);
     if (rc != AGX_OK) return rc;
@@ -1995,7 +2095,6 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
     }
     a.err = x->error_word;
     if (K > 1) {
-        a.dbg = 0;  // phase skips: the one-workgroup kernel only
         a.K = K;
         a.R = R;
         a.Q = Q;
@@ -2010,7 +2109,8 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
             a.write_through = wt && atoi(wt) != 0;
         }
         AGX_REQUIRE((int64_t)Q * K <= 65535, "agx_ppo_learn_graph: too many workgroups");
-        ppo_learn_graph_part_kernel<<<(unsigned)(Q * K), kGT, 0, s>>>(a);
+        a.lds_act = dyn > 0;
+        ppo_learn_graph_part_kernel<<<(unsigned)(Q * K), kGT, dyn, s>>>(a);
     } else {
         ppo_learn_graph_kernel<<<(unsigned)P, kGT, 0, s>>>(a);
     }

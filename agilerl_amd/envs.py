@@ -260,6 +260,7 @@ class StackedVecEnv:
         space = getattr(e0, "single_observation_space", None)
         # uint8 image frames stay uint8; everything else is stacked as f32
         self._obs_dtype = np.uint8 if getattr(space, "dtype", None) == np.uint8 else np.float32
+        self._fz = None  # the stacked rings of a lock-step SyntheticVecEnv stack (_fusable)
 
     @classmethod
     def from_shared(cls, env, copies: int, offset: int = 0) -> "StackedVecEnv":
@@ -317,7 +318,75 @@ class StackedVecEnv:
         obs = self._cat([r[0] for r in res], out_obs, self._obs_dtype)
         return obs, self._infos([r[1] for r in res])
 
+    #: stacked rings above this size are not built (the blocks step one by one)
+    FUSE_BYTES = 256 << 20
+
+    def _fusable(self) -> bool:
+        """Every block a SyntheticVecEnv (the flat-vector kind) in lock-step
+        (same ring position, ring length and time limit): then one vectorized
+        step over stacked copies of the blocks' rings does what stepping each
+        block does, with one copy per output instead of one per block.  The
+        blocks' episode lengths become views into one stacked array, so a
+        block stepped on its own later (after a regroup) stays consistent; a
+        reseeded block, a block stepped on its own, or a block re-stacked
+        elsewhere drops the stacked rings (rebuilt, or the per-block path)."""
+        envs = self.envs
+        fz = self._fz
+        if fz is not None:
+            ids, views = fz[0], fz[4]
+            k = envs[0]._k
+            for e, i, v in zip(envs, ids, views):
+                if e._obs is not i or e._len is not v or e._k != k:
+                    break
+            else:
+                return True
+            self._fz = None
+        e0 = envs[0]
+        if any(type(e) is not SyntheticVecEnv for e in envs):
+            return False
+        if any(e._ring != e0._ring or e.max_episode_steps != e0.max_episode_steps or e._k != e0._k or
+               e._obs_dim != e0._obs_dim for e in envs):
+            return False
+        if sum(e._obs.nbytes + e._rew.nbytes + e._term.nbytes for e in envs) > self.FUSE_BYTES:
+            return False
+        obs = np.concatenate([e._obs for e in envs], axis=1)
+        rew = np.concatenate([e._rew for e in envs], axis=1)
+        term = np.concatenate([e._term for e in envs], axis=1)
+        lens = np.concatenate([e._len for e in envs])
+        views, s = [], 0
+        for e in envs:
+            e._len = lens[s:s + e.num_envs]
+            views.append(e._len)
+            s += e.num_envs
+        self._fz = ([e._obs for e in envs], obs, rew, term, views, lens, np.zeros(self.num_envs, dtype=bool))
+        return True
+
+    def _step_fused(self, out_obs, out_rew, out_done):
+        _, robs, rrew, rterm, _, lens, ztrunc = self._fz
+        e0 = self.envs[0]
+        k = (e0._k + 1) % e0._ring
+        for e in self.envs:
+            e._k = k
+            e.steps += e.num_envs
+        obs, rew, term = robs[k], rrew[k], rterm[k]
+        if out_obs is not None:
+            np.copyto(out_obs.reshape(obs.shape), obs)
+            obs = out_obs
+        if out_rew is not None:
+            np.copyto(out_rew.reshape(rew.shape), rew)
+            rew = out_rew
+        if out_done is not None:
+            np.copyto(out_done.reshape(term.shape), term)
+        trunc = ztrunc
+        if e0.max_episode_steps is not None:
+            lens += 1
+            trunc = (lens >= e0.max_episode_steps) & ~term
+            lens[term | trunc] = 0
+        return obs, rew, term, trunc, {}
+
     def step(self, actions, out_obs=None, out_rew=None, out_done=None):
+        if self._fusable():
+            return self._step_fused(out_obs, out_rew, out_done)
         res = [e.step(a) for e, a in zip(self.envs, self._split(np.asarray(actions)))]
         obs = self._cat([r[0] for r in res], out_obs, self._obs_dtype)
         rew = self._cat([r[1] for r in res], out_rew, np.float32)

@@ -250,11 +250,11 @@ class PopulationEngine:
 
     def evaluate(self, loop: int, max_steps) -> list[float]:
         """agent.test for every agent (train_on_policy.py:363-373): each
-        group's pass as PopulationRunner.evaluate, all groups stepped in lock
-        step (runner.run_lockstep) so a population split into several groups
-        by mutations still evaluates in one pass's time, not one per group.
-        A group's samples depend only on its agents' counters, so the result
-        equals evaluating the groups one after another."""
+        group's pass as PopulationRunner.evaluate — a persistent launch per
+        pass where the group's policy step is a HIP kernel — one group after
+        another; groups on the PyTorch policy step are stepped together
+        (runner.run_lockstep).  A group's samples depend only on its agents'
+        counters, so the order does not change any result."""
         from .runner import _EvalDriver, run_lockstep
 
         out = [0.0] * self.P
@@ -262,15 +262,23 @@ class PopulationEngine:
         acc = {id(g): np.zeros(g.pop.P) for g in self.groups}
         for g in self.groups:
             g.pop.eval_rounds = self._eval_calls
-        # a group on the PyTorch policy step allocates while it steps: persistent
-        # launches of the other groups (which wait for the host) only without one
-        allow = all(g.pop.fused_descriptor() is not None or g.pop.learn_descriptor() is not None
-                    for g in self.groups)
+        # Groups with a HIP policy step run their passes as persistent launches,
+        # ONE resident at a time: a process has few hardware queues
+        # (GPU_MAX_HW_QUEUES, 4 by default), so two resident launches — or a
+        # resident launch and another group's per-step kernels — can share one
+        # queue, the later one waiting behind a launch that waits for the host.
+        # The remaining groups (the PyTorch policy step) step together in lock
+        # step with per-step launches, after the persistent passes.
+        paced = [g for g in self.groups if g.runner.persistent or g.runner.graph_persistent]
+        stepped = [g for g in self.groups if g not in paced]
         for k in range(loop):
-            drivers = [(g, _EvalDriver(g.runner, k, max_steps, allow_persistent=allow)) for g in self.groups]
-            run_lockstep([d for _, d in drivers])
-            for g, d in drivers:
-                acc[id(g)] += d.result()
+            batches = [[g] for g in paced] + ([stepped] if stepped else [])
+            for batch in batches:
+                drivers = [(g, _EvalDriver(g.runner, k, max_steps, allow_persistent=len(batch) == 1))
+                           for g in batch]
+                run_lockstep([d for _, d in drivers])
+                for g, d in drivers:
+                    acc[id(g)] += d.result()
         for g in self.groups:
             g.runner.after_evaluation()
             f = acc[id(g)] / loop

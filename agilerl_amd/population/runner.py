@@ -510,10 +510,16 @@ class _EvalDriver:
         self.scores = np.zeros(P * N)
         self.completed = np.zeros(P * N)
         self.finished = np.zeros(P * N, dtype=bool)
+        self.n_finished = 0
         if self.persistent:
             st = runner._eval_staging()
             self.obs_h, self.rew_h, self.done_h, self.act_h, self.ctl_h, self.args_h = st
             self.launched_to = 0  # steps covered by launches so far (0: no launch resident)
+            # per-step host work kept to the env step: numpy views of the staging
+            # and the control-block entry points, taken once
+            self._views = (self.obs_h.numpy(), self.rew_h.numpy(), self.done_h.numpy(), self.act_h.numpy())
+            lib = _lib.load()
+            self._signal, self._wait_fn, self._ctl = lib.agx_host_signal, lib.agx_host_wait, self.ctl_h.data_ptr()
         else:
             self.act_d = torch.empty(P * N, dtype=torch.int64, device=pop.device)
             self.act_h = torch.empty(P * N, dtype=torch.int64, pin_memory=True)
@@ -575,7 +581,7 @@ class _EvalDriver:
                 if self.launched_to > 0:  # the previous launch ran all its steps and ends by itself
                     self._drain()
                 self._launch()
-            _lib.load().agx_host_signal(self.ctl_h.data_ptr(), self.step - self.launch_step0 + 1)
+            self._signal(self._ctl, self.step - self.launch_step0 + 1)
             return
         with torch.cuda.stream(self.stream):  # never the NULL stream: it would wait for resident launches
             self._request_step()
@@ -603,40 +609,45 @@ class _EvalDriver:
     def wait(self) -> None:
         if self.persistent:
             t = self.step - self.launch_step0 + 1
-            try:
-                _lib.check(_lib.load().agx_host_wait(self.ctl_h.data_ptr(), self.runner.n_wg, t, self.runner.timeout_s),
-                           "agx_host_wait")
-            except BaseException:
+            rc = self._wait_fn(self._ctl, self.runner.n_wg, t, self.runner.timeout_s)
+            if rc != 0:
+                msg = _lib.load().agx_last_error().decode(errors="replace")
+                words = self.ctl_h.view(torch.int32)
+                done = words[4:4 + self.runner.n_wg].tolist()
+                state = (f"{'graph' if self.desc is None else 'compiled'} group P={self.P} N={self.N}: step "
+                         f"{self.step} (launch from {self.launch_step0} to {self.launched_to}), waiting for "
+                         f"{t}; control block seq {int(words[0])} timeout {int(words[1])} nwg {int(words[2])} "
+                         f"(runner {self.runner.n_wg}); done words {done}")
                 self.abort()
-                raise
+                raise _lib.AgxError(f"agx_host_wait failed ({rc}): {msg}; evaluation {state}")
             return
         self.ev.synchronize()
 
     def env_step(self) -> bool:
         """The env step on the actions; -> True once every env has finished."""
         if self.persistent:
-            act = self.act_h.numpy()
+            obs_n, rew_n, done_n, act_n = self._views
             try:
-                _, _, term, trunc, _ = self.env.step(act, out_obs=self.obs_h.numpy(), out_rew=self.rew_h.numpy(),
-                                                     out_done=self.done_h.numpy())
+                _, _, term, trunc, _ = self.env.step(act_n, out_obs=obs_n, out_rew=rew_n, out_done=done_n)
             except BaseException:
                 self.abort()
                 raise
-            reward = self.rew_h.numpy()
+            reward = rew_n
         else:
             self.obs, reward, term, trunc, _ = self.env.step(self.act_h.numpy().copy())
         self.step += 1
-        self.scores += np.asarray(reward, dtype=np.float64).reshape(-1)
-        done = np.asarray(term).reshape(-1)
+        self.scores += np.asarray(reward).reshape(-1)
+        done = np.asarray(term, dtype=bool).reshape(-1)
         if trunc is not None:
-            done = np.logical_or(done, np.asarray(trunc).reshape(-1))
+            done = done | np.asarray(trunc, dtype=bool).reshape(-1)
         if self.max_steps is not None and self.step == self.max_steps:
             done = np.ones(self.P * self.N, dtype=bool)
         new = done & ~self.finished
         if new.any():
             self.completed[new] = self.scores[new]
             self.finished |= new
-        return bool(self.finished.all())
+            self.n_finished = int(self.finished.sum())
+        return self.n_finished == self.finished.size
 
     def _drain(self) -> None:
         _pacing_end()

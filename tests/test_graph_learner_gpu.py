@@ -121,6 +121,9 @@ def test_graph_learner_single_update_tight(shape):
     ("latent_56", 16, 512, 256, 1), ("wide_500", 16, 256, 200, 1)])  # > 128 rows: several GEMM row blocks
 def test_graph_learner_matches_torch_learner(shape, N, learn_step, batch, epochs):
     pop = _pop(shape, N=N, learn_step=learn_step, batch=batch, epochs=epochs)
+    # the minibatch orders come from numpy's global shuffle stream (ppo.py:836-842):
+    # seeded, so the drift bar below sees the same data whatever ran before
+    np.random.seed(1234)
     _compare(pop, pop.permutations())
 
 

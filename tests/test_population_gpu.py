@@ -639,11 +639,10 @@ def test_persistent_evaluation_matches_per_step_launches(monkeypatch, max_steps)
     assert np.all(np.isfinite(out[0][0]))
 
 
-def test_engine_evaluates_groups_in_lockstep(monkeypatch):
-    """A population split into groups (a learn_step mutation here) is
-    evaluated with every group's pass stepped together; each group's fitness
-    equals its own runner's pass run alone (the groups' samples depend only
-    on their agents' counters)."""
+def test_engine_evaluates_groups_like_their_runners(monkeypatch):
+    """A population split into groups (a learn_step mutation here): the
+    engine's evaluation gives each group the fitness of its own runner's
+    pass (the groups' samples depend only on their agents' counters)."""
     from agilerl_amd.envs import StackedVecEnv, SyntheticVecEnv
     from agilerl_amd.population.engine import PopulationEngine
 
