@@ -976,12 +976,14 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
             run(arch, 1, 5)  # warm-up (first-use allocations, library start-up)
             log(f"train_on_policy {name}: warm-up done")
             out[name] = one(arch, generations, 6)
-            log(f"train_on_policy {name}: {generations} generations: {out[name]['ms_per_generation']} ms each")
+            log(f"train_on_policy {name}: {generations} generations: {out[name]['ms_per_generation']} ms each, "
+                f"by phase {out[name]['ms_per_generation_by_phase']}, {out[name]['groups_at_end']} groups")
             if long_gens > generations:
                 # the decay as mutations move agents to other groups / kernels
                 out[name][f"{long_gens}_generations"] = one(arch, long_gens, 7)
-                log(f"train_on_policy {name}: {long_gens} generations: "
-                    f"{out[name][f'{long_gens}_generations']['ms_per_generation']} ms each")
+                lg = out[name][f'{long_gens}_generations']
+                log(f"train_on_policy {name}: {long_gens} generations: {lg['ms_per_generation']} ms each, "
+                    f"by phase {lg['ms_per_generation_by_phase']}, {lg['groups_at_end']} groups")
     return out
 
 
