@@ -64,6 +64,7 @@ struct GLay {
     long long dyc;  // output layers: d(output) feature-major, written by the loss pass (-1 otherwise)
     int fuse;       // this layer's dX GEMM runs its source's LayerNorm / ReLU backward in the epilogue
     int fused;      // this layer's dZ (and column partials) come from its consumer's dX epilogue
+    int ld;         // few-row form: the row stride of the layer's LDS tiles
 };
 
 struct GArgs {
@@ -80,7 +81,8 @@ struct GArgs {
     unsigned *cnt;         // barrier counters, timeout word, XCC ids (zeroed by the gather)
     unsigned *err;         // caller's sticky error word
     int write_through;     // test hook: the cross-XCD (release-fence) publish form always
-    int lds_act;           // the partner's activation scratch (ws_part floats) in dynamic LDS, not at ws
+    int ld0;               // few-row form: the observation tile's row stride (its offset: oc)
+    long long lds_floats;  // few-row form: the LDS tiles' size (dynamic LDS)
     long long *stamps;     // diagnostic phase stamps of the partnered learner (agx_debug_graph_stamps), or null
     float *ws;
     float *params, *m, *v;
@@ -1208,6 +1210,304 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
     return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- the few-row form (ppo_learn_graph_part_kernel<true>) --------------------
+// A partner's slice of at most kFR = 16 minibatch rows stays in LDS for the
+// whole update: the observation tile, every layer's output Y, xhat and rstd,
+// and dY, each a [16][ld] row-major tile (ld = the width rounded up to 16,
+// + 4: float4 row reads spread over the banks).  The padding columns are zero
+// from the kernel's start and never written, so every contraction runs over
+// whole 16-wide chunks with no masks; rows past the slice carry finite values
+// and a zero gradient.  One 16-row MFMA m-tile covers the slice, its n-tiles
+// go round the four waves; LayerNorm / ReLU (forward and backward) are row
+// passes, 16 lanes per row, one row per lane group; bias / LN-affine
+// gradients are column sums over the 16 rows, one thread per column, in row
+// order.  Weights come from L2 (buffer loads, the agent's partners share
+// them): W [out][in] for the forward, the transposed copy for dX.
+constexpr int kFR = 16;
+
+__device__ __forceinline__ f4 bload4(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
+// C[16 x N] = X[16 x K] . W^T, W's row n at byte woff + 4 n K of the buffer
+// wr: lane (r, q) feeds k = 16c + 4q + j to MFMA j of chunk c (float4 reads
+// of X from LDS and of W from L2, four chunks' loads in flight).  epi(row, n,
+// v) for the lane's outputs with n < N.  Rows of W past N read other finite
+// parameters (or zeros past the buffer) and are never stored.
+template <class FE>
+__device__ __forceinline__ void few_gemm(const float *X, int ldx, __amdgpu_buffer_rsrc_t wr, int woff, int K, int N,
+                                         const float *bias, FE epi) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, q = lane >> 4;
+    const int nc = (K + 15) >> 4, ntile = (N + 15) >> 4;
+    const float *xr = X + r * ldx + 4 * q;
+    for (int t = wave; t < ntile; t += kGW) {
+        const int n0 = t << 4;
+        const int wrow = woff + ((n0 + r) * K + 4 * q) * 4;
+        const float bv = bias ? bias[n0 + r < N ? n0 + r : 0] : 0.f;  // in flight under the MFMAs
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int c0 = 0; c0 < nc; c0 += 4) {
+            f4 wv[4], xv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int c = c0 + u < nc ? c0 + u : nc - 1;
+                wv[u] = bload4(wr, wrow + c * 64);
+                xv[u] = *reinterpret_cast<const f4 *>(xr + 16 * c);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (c0 + u >= nc) break;  // uniform
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[u][j], wv[u][j], acc, 0, 0, 0);
+            }
+        }
+        if (n0 + r < N) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) epi(4 * q + j, n0 + r, acc[j] + bv);
+        }
+    }
+}
+
+// dW[o][i] = sum over the 16 rows of dZ[row][o] X[row][i] (o < F, i < fin)
+// straight into the gradient row Gw ([F][fin]); tiles round the waves
+__device__ __forceinline__ void few_dw(const float *dZ, int ldz, const float *X, int ldx, int F, int fin, float *Gw) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, q = lane >> 4;
+    const int tm = (F + 15) >> 4, tn = (fin + 15) >> 4;
+    for (int t = wave; t < tm * tn; t += kGW) {
+        const int o0 = (t % tm) << 4, i0 = (t / tm) << 4;
+        float a[4], b[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            a[kk] = dZ[(4 * kk + q) * ldz + o0 + r];
+            b[kk] = X[(4 * kk + q) * ldx + i0 + r];
+        }
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], b[kk], acc, 0, 0, 0);
+        const int i = i0 + r;
+        if (i < fin) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int o = o0 + 4 * q + j;
+                if (o < F) Gw[o * fin + i] = acc[j];
+            }
+        }
+    }
+}
+
+// One update's gradient of a partner's rows (rk <= 16 of them, observations
+// at xobs, rollout rows s0 ..) into the gradient row G, plus the loss /
+// approx_kl partial sums: the few-row counterpart of minibatch_grads, same
+// float operations per element.  S: the LDS tiles (plan_few).
+__device__ __forceinline__ void few_grads(const GArgs &g, float *S, const float *pr, const float *wb, float *G,
+                                          const float *xobs, const int *gact_e, const unsigned *gmask_e,
+                                          const float *grow_e, long long s0, int rk, float inv_b, float entp,
+                                          float &lsum, float &klsum, long long *st) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = lane & 15, rq = lane >> 4;
+    const int row = 4 * wave + rq;  // the lane group's row in the row passes
+    const int A = g.A, D = g.D;
+    const long long S_ = g.S;
+    const auto prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(pr), 0, __builtin_amdgcn_readfirstlane(g.n * 4),
+                                                       0x00020000);
+    // the agent's transposed weights start at wb + wt0 (wb + L.wt addresses layer L's)
+    const auto wts = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(wb + g.wt0), 0,
+                                                       __builtin_amdgcn_readfirstlane((int)(g.wt_agent * 4)), 0x00020000);
+    // observation rows (zero past the slice)
+    {
+        float *x0 = S + g.oc;
+        for (int i = tid; i < kFR * D; i += kGT) {
+            const int b = i / D, d = i - b * D;
+            float v = 0.f;
+            if (b < rk) v = xobs[i];
+            x0[b * g.ld0 + d] = v;
+        }
+    }
+    __syncthreads();
+    if (st) st[0] = (long long)__builtin_readcyclecounter();
+
+    // ---- forward -------------------------------------------------------
+    for (int l = 0; l < g.nl; ++l) {
+        const GLay &L = g.L[l];
+        const int F = L.fout, ld = L.ld;
+        const float *X = L.src < 0 ? S + g.oc : S + g.L[L.src].yr;
+        const int ldx = L.src < 0 ? g.ld0 : g.L[L.src].ld;
+        float *Y = S + L.yr;
+        few_gemm(X, ldx, prs, L.w * 4, L.fin, F, pr + L.b, [&](int m, int n, float v) { Y[m * ld + n] = v; });
+        __syncthreads();
+        if (L.ln || L.relu) {
+            const float invF = 1.f / (float)F;
+            float *y = Y + row * ld;
+            float mean = 0.f, rstd = 1.f;
+            if (L.ln) {
+                float s = 0.f;
+                for (int j = sub; j < F; j += 16) s += y[j];
+                mean = rsum16(s) * invF;
+                float vs = 0.f;
+                for (int j = sub; j < F; j += 16) {
+                    const float d = y[j] - mean;
+                    vs += d * d;
+                }
+                rstd = 1.f / sqrtf(rsum16(vs) / (float)F + 1e-5f);
+                if (sub == 0) S[L.rs + row] = rstd;
+            }
+            for (int j = sub; j < F; j += 16) {
+                float v = y[j];
+                if (L.ln) {
+                    const float xh = (v - mean) * rstd;
+                    S[L.xh + row * ld + j] = xh;
+                    v = L.ln == 2 ? xh * pr[L.g + j] + pr[L.be + j] : xh;
+                }
+                if (L.relu) v = relu(v);
+                y[j] = v;
+            }
+            __syncthreads();
+        }
+        if (st) st[1 + l] = (long long)__builtin_readcyclecounter();
+    }
+
+    // ---- PPO loss row pass: logits / value -> d(logits), d(value) (ppo.py:876-908)
+    {
+        const GLay &La = g.L[g.aout];
+        const GLay &Lc = g.L[g.cout];
+        const float *lgp = S + La.yr + row * La.ld;
+        float *dla = S + La.dy + row * La.ld;
+        const bool live = row < rk;
+        const int rr = live ? row : 0;
+        const int a0 = sub, a1 = sub + 16;
+        const unsigned bits = gmask_e ? gmask_e[s0 + rr] : 0xffffffffu;
+        const float plg0 = lgp[a0 < A ? a0 : 0], plg1 = lgp[a1 < A ? a1 : 0];
+        const int a_t = gact_e[s0 + rr];
+        const float olp = grow_e[s0 + rr], Ad = grow_e[S_ + s0 + rr];
+        const float Rt = grow_e[2 * S_ + s0 + rr], ov = grow_e[3 * S_ + s0 + rr];
+        const float v = S[Lc.yr + row * Lc.ld];
+        const bool ok0 = (bits >> a0) & 1u, ok1 = (bits >> a1) & 1u;
+        const float lg0 = a0 < A ? (ok0 ? plg0 : -1.0e8f) : -3.0e38f;
+        const float lg1 = a1 < A ? (ok1 ? plg1 : -1.0e8f) : -3.0e38f;
+        const float mx = rmax16(fmaxf(lg0, lg1));
+        const float ex0 = a0 < A ? expf(lg0 - mx) : 0.f, ex1 = a1 < A ? expf(lg1 - mx) : 0.f;
+        const float lse = mx + logf(rsum16(ex0 + ex1));
+        const float p0 = a0 < A ? expf(lg0 - lse) : 0.f, p1 = a1 < A ? expf(lg1 - lse) : 0.f;
+        const float lpe0 = logf(p0 + 1e-8f), lpe1 = logf(p1 + 1e-8f);
+        const float Hs = -rsum16((a0 < A ? p0 * lpe0 : 0.f) + (a1 < A ? p1 * lpe1 : 0.f));
+        const float gh0 = -(lpe0 + p0 / (p0 + 1e-8f)), gh1 = -(lpe1 + p1 / (p1 + 1e-8f));
+        const float pg = rsum16((a0 < A ? p0 * gh0 : 0.f) + (a1 < A ? p1 * gh1 : 0.f));
+        const int srcl = (lane & ~15) + (a_t & 15);
+        const float t0 = bperm(srcl, lg0), t1 = bperm(srcl, lg1);
+        const float logp = (a_t < 16 ? t0 : t1) - lse;
+        const float lo = 1.f - g.clip, hi = 1.f + g.clip;
+        const float lrt = logp - olp;
+        const float ratio = expf(lrt);
+        const float rcl = fminf(fmaxf(ratio, lo), hi);
+        const float q1 = -Ad * ratio, q2 = -Ad * rcl;
+        const float g1 = q1 > q2 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
+        const float g2 = q2 > q1 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
+        const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        const float g_logp = ((g1 * -Ad + g2 * -Ad * inr) * inv_b) * ratio;
+        const float dv = v - ov;
+        const float vcl = ov + fminf(fmaxf(dv, -g.clip), g.clip);
+        const float eu = v - Rt, ec = vcl - Rt;
+        const float lu = eu * eu, lc = ec * ec;
+        const float gu = lu > lc ? 1.f : (lu == lc ? 0.5f : 0.f);
+        const float gc = lc > lu ? 1.f : (lu == lc ? 0.5f : 0.f);
+        const float inv = (dv >= -g.clip && dv <= g.clip) ? 1.f : 0.f;
+        const float g_H = -entp * inv_b;
+        const float dl0 = g_logp * ((a0 == a_t ? 1.f : 0.f) - p0) + g_H * p0 * (gh0 - pg);
+        const float dl1 = g_logp * ((a1 == a_t ? 1.f : 0.f) - p1) + g_H * p1 * (gh1 - pg);
+        // rows past the slice: a zero gradient (their tiles hold the last minibatch's rows)
+        if (a0 < A) dla[a0] = (live && ok0) ? dl0 : 0.f;
+        if (a1 < A) dla[a1] = (live && ok1) ? dl1 : 0.f;
+        if (sub == 0) {
+            const float dvv = g.vf * 0.5f * inv_b * (gu * 2.f * eu + gc * 2.f * ec * inv);
+            S[Lc.dy + row * Lc.ld] = live ? dvv : 0.f;
+            if (live) {
+                lsum += (fmaxf(q1, q2) + g.vf * 0.5f * fmaxf(lu, lc) - entp * Hs) * inv_b;
+                klsum += ((ratio - 1.f) - lrt) * inv_b;  // approx_kl (ppo.py:899-902)
+            }
+        }
+    }
+    __syncthreads();
+    if (st) st[17] = (long long)__builtin_readcyclecounter();
+
+    // ---- backward, layer by layer (reverse) ------------------------------
+    float *T = S + g.t1;  // dY' of the current LN-affine layer (its gamma / beta gradients)
+    for (int l = g.nl - 1; l >= 0; --l) {
+        const GLay &L = g.L[l];
+        const int F = L.fout, ld = L.ld;
+        float *dZ = S + L.dy;  // dY in, dZ out (in place)
+        if (L.ln || L.relu) {
+            float *dy = dZ + row * ld;
+            const float *xh = S + (L.ln ? L.xh : L.yr) + row * ld;  // xhat, or Y for a plain ReLU
+            const float invF = 1.f / (float)F;
+            float m1 = 0.f, m2 = 0.f, rs = 1.f;
+            auto dpre = [&](int j, float &x) {
+                const float d = dy[j];
+                x = xh[j];
+                const float pre = L.ln == 2 ? x * pr[L.g + j] + pr[L.be + j] : x;
+                return (!L.relu || pre > 0.f) ? d : 0.f;
+            };
+            if (L.ln) {
+                float s1 = 0.f, s2 = 0.f;
+                for (int j = sub; j < F; j += 16) {
+                    float x;
+                    const float dx = dpre(j, x) * (L.ln == 2 ? pr[L.g + j] : 1.f);
+                    s1 += dx;
+                    s2 += dx * x;
+                }
+                m1 = rsum16(s1) * invF;
+                m2 = rsum16(s2) * invF;
+                rs = S[L.rs + row];
+            }
+            for (int j = sub; j < F; j += 16) {
+                float x;
+                const float dp = dpre(j, x);
+                if (L.ln == 2) T[row * ld + j] = dp;
+                dy[j] = L.ln ? rs * (dp * (L.ln == 2 ? pr[L.g + j] : 1.f) - m1 - x * m2) : dp;
+            }
+            __syncthreads();
+        }
+        if (st) st[18 + 3 * l] = (long long)__builtin_readcyclecounter();
+        // bias / LN-affine gradients: column sums in row order
+        for (int j = tid; j < F; j += kGT) {
+            float sb = 0.f, sg = 0.f, sbe = 0.f;
+#pragma unroll
+            for (int b = 0; b < kFR; ++b) sb += dZ[b * ld + j];
+            G[L.b + j] = sb;
+            if (L.ln == 2) {
+#pragma unroll
+                for (int b = 0; b < kFR; ++b) {
+                    const float t = T[b * ld + j];
+                    sg += t * S[L.xh + b * ld + j];
+                    sbe += t;
+                }
+                G[L.g + j] = sg;
+                G[L.be + j] = sbe;
+            }
+        }
+        const float *X = L.src < 0 ? S + g.oc : S + g.L[L.src].yr;
+        const int ldx = L.src < 0 ? g.ld0 : g.L[L.src].ld;
+        few_dw(dZ, ld, X, ldx, F, L.fin, G + L.w);
+        if (st) st[19 + 3 * l] = (long long)__builtin_readcyclecounter();
+        if (L.src >= 0) {  // dX = dZ W into the source's dY (the second consumer adds)
+            const GLay &Ls = g.L[L.src];
+            float *dys = S + Ls.dy;
+            const int lds_ = Ls.ld;
+            if (L.acc)
+                few_gemm(dZ, ld, wts, (int)(L.wt - g.wt0) * 4, F, L.fin, nullptr,
+                         [&](int m, int n, float v) { dys[m * lds_ + n] += v; });
+            else
+                few_gemm(dZ, ld, wts, (int)(L.wt - g.wt0) * 4, F, L.fin, nullptr,
+                         [&](int m, int n, float v) { dys[m * lds_ + n] = v; });
+        }
+        __syncthreads();
+        if (st) st[20 + 3 * l] = (long long)__builtin_readcyclecounter();
+    }
+}
+
+// FEW: the few-row form (few_grads, activations in dynamic LDS); else the
+// general form (minibatch_grads over the partner's global scratch)
+template <bool FEW>
 __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g) {
     __shared__ float red[2 * kGW];
     __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
@@ -1225,11 +1525,13 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
     float *const pr = g.params + (size_t)p * n;
     float *const gm = g.m + (size_t)p * n;
     float *const gv = g.v + (size_t)p * n;
-    // the activation scratch: this workgroup's dynamic LDS when the plan fits
-    // (every row pass, GEMM operand and epilogue store then stays on the CU),
-    // else its block of the global scratch
+    // the activation scratch: the few-row form's LDS tiles (zeroed once: their
+    // padding columns stay zero), else this partner's block of the global scratch
     extern __shared__ __attribute__((aligned(16))) float gdyn[];
-    float *const base = g.lds_act ? gdyn : g.ws + ((size_t)p * K + kk) * g.ws_part;
+    float *const base = FEW ? gdyn : g.ws + ((size_t)p * K + kk) * g.ws_part;
+    if constexpr (FEW) {
+        for (int i = tid; i < (int)g.lds_floats; i += kGT) gdyn[i] = 0.f;
+    }
     float *const wsh = g.wtb + (size_t)p * g.wt_agent;  // the agent's shared transposed weights
     float *const wb = wsh - g.wt0;                      // wb + L.wt lands in wsh
     unsigned *const c0 = g.cnt + p, *const c1 = g.cnt + P + p, *const c2 = g.cnt + 2 * P + p;
@@ -1305,8 +1607,13 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
             // ---- 1. this partner's rows -> its partial gradient row ----------------
             float lsum = 0.f, klsum = 0.f;
             if (rk > 0) {
-                minibatch_grads<AGX_GRAPH_DIRECT>(g, base, wb, pr, G, gobs_e + (s0 + r0) * D, gact_e, gmask_e, grow_e, s0 + r0, rk,
-                                inv_b, entp, lds, colp, colo, lsum, klsum, stamp ? s_st + 16 : nullptr);
+                if constexpr (FEW)
+                    few_grads(g, base, pr, wb, G, gobs_e + (s0 + r0) * D, gact_e, gmask_e, grow_e, s0 + r0, rk, inv_b,
+                              entp, lsum, klsum, stamp ? s_st + 16 : nullptr);
+                else
+                    minibatch_grads<AGX_GRAPH_DIRECT>(g, base, wb, pr, G, gobs_e + (s0 + r0) * D, gact_e, gmask_e,
+                                                      grow_e, s0 + r0, rk, inv_b, entp, lds, colp, colo, lsum, klsum,
+                                                      stamp ? s_st + 16 : nullptr);
             } else {  // no rows this minibatch (a short last minibatch): publish zeros
                 for (int i = tid; i < n; i += kGT) G[i] = 0.f;
             }
@@ -1890,70 +2197,114 @@ int cu_count_g() {
     }
     return n;
 }
+template <bool FEW>
 int part_occupancy(size_t dyn) {  // co-resident partner workgroups per CU with dyn bytes of dynamic LDS
     static size_t last = (size_t)-1;
     static int n = 1;
     if (dyn != last) {
         int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_learn_graph_part_kernel, kGT, dyn) != hipSuccess) v = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_learn_graph_part_kernel<FEW>, kGT, dyn) != hipSuccess)
+            v = 1;
         n = v < 1 ? 1 : v;
         last = dyn;
     }
     return n;
 }
-// dynamic LDS a partner may take for its activations: the CU's 160 KB less the
-// kernel's static LDS (queried once)
-size_t part_lds_budget() {
+// dynamic LDS the few-row form may take: the CU's 160 KB less the kernel's
+// static LDS (queried once)
+size_t few_lds_budget() {
     static size_t b = 0;
     if (!b) {
         hipFuncAttributes fa{};
-        const size_t st = hipFuncGetAttributes(&fa, (const void *)ppo_learn_graph_part_kernel) == hipSuccess
+        const size_t st = hipFuncGetAttributes(&fa, (const void *)ppo_learn_graph_part_kernel<true>) == hipSuccess
                               ? fa.sharedSizeBytes
-                              : 80 * 1024;
+                              : 8 * 1024;
         b = st < kLdsMax ? kLdsMax - st : 1;
-        (void)hipFuncSetAttribute((const void *)ppo_learn_graph_part_kernel,
+        (void)hipFuncSetAttribute((const void *)ppo_learn_graph_part_kernel<true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
     }
     return b;
 }
-// The partnered learner's split of a minibatch: K partners of R rows while the
-// whole grid (Q x K workgroups, Q = P rounded up to the 8 XCDs) stays
-// co-resident; K = 1: the one-workgroup-per-agent kernel.  Rows per partner:
-// AGX_GRAPH_ROWS, else 16, or with AGX_GRAPH_LDS=1 the largest of 16 / 8 whose
-// activation scratch fits the workgroup's LDS (dyn = its bytes; 0: the global
-// scratch).  AGX_GRAPH_SPLIT caps K (tests, diagnostics).
-void graph_split(const agx_ppo_graph *net, int64_t P, int64_t batch, int &K, int &R, int &Q, size_t &dyn) {
-    int rows_env = 0;
-    if (const char *e = getenv("AGX_GRAPH_ROWS")) rows_env = atoi(e) >= 1 ? atoi(e) : 16;
+// the few-row form's plan: the general plan (validation, parameter offsets,
+// transposed weights, accumulation order) with every activation tile moved to
+// LDS: per layer Y, xhat + rstd (LayerNorm), dY, each [16][ld]; the
+// observation tile; one dY' tile for the LN-affine gradients.  -> LDS bytes
+// (0: the plan does not fit, or the graph is invalid)
+size_t plan_few(const agx_ppo_graph *net, GArgs &a) {
+    if (plan_graph(net, kFR, a) != AGX_OK) return 0;
+    auto ldof = [](int w) { return (w + 15) / 16 * 16 + 4; };
+    long long off = 0;
+    int ldmax = 0;
+    bool affine = false;
+    for (int l = 0; l < a.nl; ++l) {
+        GLay &L = a.L[l];
+        L.ld = ldof(L.fout);
+        L.yr = off;
+        off += (long long)kFR * L.ld;
+        L.xh = L.rs = -1;
+        if (L.ln) {
+            L.xh = off;
+            off += (long long)kFR * L.ld;
+            L.rs = off;
+            off += kFR;
+        }
+        L.dy = off;
+        off += (long long)kFR * L.ld;
+        L.yc = L.dy2 = L.dyc = -1;
+        L.fuse = L.fused = 0;
+        ldmax = L.ld > ldmax ? L.ld : ldmax;
+        affine = affine || L.ln == 2;
+    }
+    a.ld0 = ldof(a.D);
+    a.oc = off;
+    off += (long long)kFR * a.ld0;
+    a.t1 = off;
+    if (affine) off += (long long)kFR * ldmax;
+    a.lds_floats = (off + 3) & ~3ll;
+    a.ws_part = 0;  // no global activation scratch
+    const size_t bytes = (size_t)a.lds_floats * 4;
+    return bytes <= few_lds_budget() ? bytes : 0;
+}
+// How a learn() runs, chosen per call (the workspace query makes the same
+// choice): the few-row partnered form when a minibatch splits into at most
+// kMaxGK slices of at most 16 rows whose tiles fit in LDS (AGX_GRAPH_FEW=0
+// turns it off); else the general partnered form, K partners of R rows
+// (AGX_GRAPH_ROWS, default 16); K = 1: one workgroup per agent.  The whole
+// grid (Q x K workgroups, Q = P rounded up to the 8 XCDs) must be co-resident.
+// AGX_GRAPH_SPLIT caps K (tests, diagnostics).
+struct Split {
+    int K = 1, R = 1, Q = 1;
+    bool few = false;
+    size_t dyn = 0;  // dynamic LDS bytes (few-row form)
+};
+Split graph_split(const agx_ppo_graph *net, int64_t P, int64_t batch) {
+    Split sp;
+    int rows = 16;
+    if (const char *e = getenv("AGX_GRAPH_ROWS")) rows = atoi(e) >= 1 ? atoi(e) : 16;
     int cap = kMaxGK;
     if (const char *e = getenv("AGX_GRAPH_SPLIT")) cap = atoi(e) >= 1 ? atoi(e) : 1;
-    // off by default: through a generic pointer every scratch access becomes a
-    // flat instruction, measured 5 % slower than the global scratch (r5)
-    bool lds_ok = false;
-    if (const char *e = getenv("AGX_GRAPH_LDS")) lds_ok = atoi(e) != 0;
-    Q = (int)((P + 7) / 8 * 8);
-    const size_t budget = part_lds_budget();
-    auto fit = [&](int k) -> size_t {  // dynamic LDS bytes of a k-way split, 0 when the scratch is global
-        if (!lds_ok || k <= 1) return 0;
-        GArgs ap{};
-        if (plan_graph(net, (batch + k - 1) / k, ap) != AGX_OK) return 0;
-        const size_t b = (size_t)ap.ws_part * 4;
-        return b <= budget ? b : 0;
-    };
-    auto split_of = [&](int rows) { const int k = (int)((batch + rows - 1) / rows); return k > cap ? cap : k; };
-    int k = split_of(rows_env ? rows_env : 16);
-    size_t d = fit(k);
-    if (!rows_env && !d) {
-        const int k8 = split_of(8);
-        const size_t d8 = fit(k8);
-        if (d8) k = k8, d = d8;
-    }
+    bool few_ok = true;
+    if (const char *e = getenv("AGX_GRAPH_FEW")) few_ok = atoi(e) != 0;
+    sp.Q = (int)((P + 7) / 8 * 8);
     const int64_t cus = cu_count_g();
-    while (k > 1 && (int64_t)Q * k > (int64_t)part_occupancy(d) * cus) d = fit(--k);
-    if (k > 1 && (int64_t)P * k > (int64_t)part_occupancy(d) * cus) k = 1;
-    K = k < 1 ? 1 : k;
-    R = (int)((batch + K - 1) / K);
-    dyn = K > 1 ? d : 0;
+    int k = (int)((batch + rows - 1) / rows);
+    if (k > cap) k = cap;
+    if (few_ok && k > 1 && (batch + k - 1) / k <= kFR) {
+        GArgs a{};
+        const size_t dyn = plan_few(net, a);
+        if (dyn && (int64_t)sp.Q * k <= (int64_t)part_occupancy<true>(dyn) * cus) {
+            sp.few = true;
+            sp.dyn = dyn;
+            sp.K = k;
+            sp.R = (int)((batch + k - 1) / k);
+            return sp;
+        }
+    }
+    while (k > 1 && (int64_t)sp.Q * k > (int64_t)part_occupancy<false>(0) * cus) --k;
+    if (k > 1 && (int64_t)P * k > (int64_t)part_occupancy<false>(0) * cus) k = 1;
+    sp.K = k < 1 ? 1 : k;
+    sp.R = (int)((batch + sp.K - 1) / sp.K);
+    return sp;
 }
 struct PartWs {
     size_t cnt, gobs, gact, gmask, grow, scratch, wt, slabs, sums, total;
@@ -2003,13 +2354,11 @@ extern "C" size_t agx_ppo_learn_graph_workspace_bytes(const agx_ppo_graph *net, 
     const int64_t bb = batch < S ? batch : S;
     if (plan_graph(net, bb, a) != AGX_OK) return 0;
     size_t total = graph_ws(a, P, S, epochs).total;
-    int K, R, Q;
-    size_t dyn;
-    graph_split(net, P, bb, K, R, Q, dyn);
-    if (K > 1) {  // room for either kernel: the split may change with the call's batch
+    const Split sp = graph_split(net, P, bb);
+    if (sp.K > 1) {  // room for either kernel: the split may change with the call's batch
         GArgs ap{};
-        if (plan_graph(net, R, ap) != AGX_OK) return 0;
-        const size_t t = part_ws(ap, P, S, epochs, K).total;
+        if (sp.few ? !plan_few(net, ap) : plan_graph(net, sp.R, ap) != AGX_OK) return 0;
+        const size_t t = part_ws(ap, P, S, epochs, sp.K).total;
         total = t > total ? t : total;
     }
     return total;
@@ -2026,12 +2375,12 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
                 "agx_ppo_learn_graph: bad sizes P=%lld S=%lld epochs=%lld batch=%lld", (long long)P, (long long)S,
                 (long long)epochs, (long long)batch);
     const int64_t bb = batch < S ? batch : S;
-    int K = 1, R = (int)bb, Q = (int)P;
-    size_t dyn = 0;
-    graph_split(net, P, bb, K, R, Q, dyn);
+    const Split sp = graph_split(net, P, bb);
+    const int K = sp.K, R = sp.R, Q = sp.Q;
     GArgs a{};
     const int rc = plan_graph(net, K > 1 ? R : bb, a);
     if (rc != AGX_OK) return rc;
+    if (sp.few) AGX_REQUIRE(plan_few(net, a) == sp.dyn, "agx_ppo_learn_graph: few-row plan changed");
     char *ws = static_cast<char *>(workspace);
     hipStream_t s = as_stream(stream);
     size_t o_gobs, o_gact, o_gmask, o_grow;
@@ -2109,8 +2458,10 @@ extern "C" int agx_ppo_learn_graph(const agx_ppo_graph *net, const agx_ppo_learn
             a.write_through = wt && atoi(wt) != 0;
         }
         AGX_REQUIRE((int64_t)Q * K <= 65535, "agx_ppo_learn_graph: too many workgroups");
-        a.lds_act = dyn > 0;
-        ppo_learn_graph_part_kernel<<<(unsigned)(Q * K), kGT, dyn, s>>>(a);
+        if (sp.few)
+            ppo_learn_graph_part_kernel<true><<<(unsigned)(Q * K), kGT, sp.dyn, s>>>(a);
+        else
+            ppo_learn_graph_part_kernel<false><<<(unsigned)(Q * K), kGT, 0, s>>>(a);
     } else {
         ppo_learn_graph_kernel<<<(unsigned)P, kGT, 0, s>>>(a);
     }

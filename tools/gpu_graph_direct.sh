@@ -1,5 +1,5 @@
-# Runtime-shape learner: graph/dynamic-shape parity tests (LDS-resident activations, then the global
-# scratch form), partnered-learner phase stamps and graph_bench.
+# Runtime-shape learner: graph/dynamic-shape parity tests (few-row LDS form, then the general
+# form), partnered-learner phase stamps and graph_bench.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest tests/test_graph_learner_gpu.py tests/test
 rc=$?
 tail -15 gpurun_out/pytest_graph.log
 [ $rc -eq 0 ] || exit $rc
-AGX_GRAPH_LDS=1 timeout -k 10 600 python -u -m pytest tests/test_graph_learner_gpu.py tests/test_dynamic_shapes_gpu.py -m gpu -x -q -rf --timeout 200 --timeout-method thread > gpurun_out/pytest_graph_g.log 2>&1
+AGX_GRAPH_FEW=0 timeout -k 10 600 python -u -m pytest tests/test_graph_learner_gpu.py tests/test_dynamic_shapes_gpu.py -m gpu -x -q -rf --timeout 200 --timeout-method thread > gpurun_out/pytest_graph_g.log 2>&1
 rc=$?
 tail -3 gpurun_out/pytest_graph_g.log
 [ $rc -eq 0 ] || exit $rc
