@@ -48,6 +48,10 @@ SIGNATURES = {
                                                 ctypes.c_uint64, _P, _P, _D, _P, _P]),
     "agx_ppo_eval_graph_persistent": (_INT, [_P, _I, _I, _P, _P, _P, _P, _P, _I, ctypes.c_uint32, ctypes.c_uint64,
                                              ctypes.c_uint64, _P, _P, _D, _P, _P]),
+    "agx_ppo_eval_multi_bytes": (_SZ, [_I]),
+    "agx_ppo_eval_multi_supported": (_INT, [_P, _I, _I]),
+    "agx_ppo_eval_multi_persistent": (_INT, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _I, ctypes.c_uint32, _P, _P, _P,
+                                             _D, _P]),
     "agx_ppo_act_graph": (_INT, [_P, _I, _I, _P, _P, _I, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P,
                                  _P, _I, _P, _P, _P, _P]),
     "agx_ppo_learn": (_INT, [_P, _P, _P, _P]),

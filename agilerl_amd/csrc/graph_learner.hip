@@ -65,6 +65,7 @@ struct GLay {
     int fuse;       // this layer's dX GEMM runs its source's LayerNorm / ReLU backward in the epilogue
     int fused;      // this layer's dZ (and column partials) come from its consumer's dX epilogue
     int ld;         // few-row form: the row stride of the layer's LDS tiles
+    long long af;   // few-row form: the LN affine (gamma then beta) copied to LDS, -1: none
 };
 
 struct GArgs {
@@ -1234,7 +1235,10 @@ __device__ __forceinline__ f4 bload4(__amdgpu_buffer_rsrc_t r, int byte_off) {
 // of X from LDS and of W from L2, four chunks' loads in flight).  epi(row, n,
 // v) for the lane's outputs with n < N.  Rows of W past N read other finite
 // parameters (or zeros past the buffer) and are never stored.
-template <class FE>
+// TRANSB: W is [K][N] instead (row k at byte woff + 4 k N): MFMA j of chunk c
+// takes W[16c + 4q + j][n0 + r], one dword per lane, 16 lanes on one 64-byte
+// row segment (the dX of a layer straight from its nn.Linear weight).
+template <bool TRANSB = false, class FE>
 __device__ __forceinline__ void few_gemm(const float *X, int ldx, __amdgpu_buffer_rsrc_t wr, int woff, int K, int N,
                                          const float *bias, FE epi) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1243,7 +1247,7 @@ __device__ __forceinline__ void few_gemm(const float *X, int ldx, __amdgpu_buffe
     const float *xr = X + r * ldx + 4 * q;
     for (int t = wave; t < ntile; t += kGW) {
         const int n0 = t << 4;
-        const int wrow = woff + ((n0 + r) * K + 4 * q) * 4;
+        const int wrow = TRANSB ? woff + (4 * q * N + n0 + r) * 4 : woff + ((n0 + r) * K + 4 * q) * 4;
         const float bv = bias ? bias[n0 + r < N ? n0 + r : 0] : 0.f;  // in flight under the MFMAs
         f4 acc = {0.f, 0.f, 0.f, 0.f};
         for (int c0 = 0; c0 < nc; c0 += 4) {
@@ -1251,7 +1255,14 @@ __device__ __forceinline__ void few_gemm(const float *X, int ldx, __amdgpu_buffe
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int c = c0 + u < nc ? c0 + u : nc - 1;
-                wv[u] = bload4(wr, wrow + c * 64);
+                if constexpr (TRANSB) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        wv[u][j] = __builtin_bit_cast(
+                            float, __builtin_amdgcn_raw_buffer_load_b32(wr, wrow + ((16 * c + j) * N) * 4, 0, 0));
+                } else {
+                    wv[u] = bload4(wr, wrow + c * 64);
+                }
                 xv[u] = *reinterpret_cast<const f4 *>(xr + 16 * c);
             }
 #pragma unroll
@@ -1296,45 +1307,41 @@ __device__ __forceinline__ void few_dw(const float *dZ, int ldz, const float *X,
     }
 }
 
-// One update's gradient of a partner's rows (rk <= 16 of them, observations
-// at xobs, rollout rows s0 ..) into the gradient row G, plus the loss /
-// approx_kl partial sums: the few-row counterpart of minibatch_grads, same
-// float operations per element.  S: the LDS tiles (plan_few).
-__device__ __forceinline__ void few_grads(const GArgs &g, float *S, const float *pr, const float *wb, float *G,
-                                          const float *xobs, const int *gact_e, const unsigned *gmask_e,
-                                          const float *grow_e, long long s0, int rk, float inv_b, float entp,
-                                          float &lsum, float &klsum, long long *st) {
+// Forward of the 16-row LDS tiles through the layer list: the few-row GEMM
+// (+ bias) into Y, then LayerNorm(+affine) / ReLU as a row pass in place,
+// keeping xhat / rstd where the plan has them (the learner; the policy step
+// keeps Y only).  The observation tile is at oc (row stride ld0).
+__device__ __forceinline__ void few_forward(const GLay *Ls, int nl, float *S, const float *pr,
+                                            __amdgpu_buffer_rsrc_t prs, long long oc, int ld0, long long *st) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int sub = lane & 15, rq = lane >> 4;
-    const int row = 4 * wave + rq;  // the lane group's row in the row passes
-    const int A = g.A, D = g.D;
-    const long long S_ = g.S;
-    const auto prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(pr), 0, __builtin_amdgcn_readfirstlane(g.n * 4),
-                                                       0x00020000);
-    // the agent's transposed weights start at wb + wt0 (wb + L.wt addresses layer L's)
-    const auto wts = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(wb + g.wt0), 0,
-                                                       __builtin_amdgcn_readfirstlane((int)(g.wt_agent * 4)), 0x00020000);
-    // observation rows (zero past the slice)
-    {
-        float *x0 = S + g.oc;
-        for (int i = tid; i < kFR * D; i += kGT) {
-            const int b = i / D, d = i - b * D;
-            float v = 0.f;
-            if (b < rk) v = xobs[i];
-            x0[b * g.ld0 + d] = v;
-        }
-    }
-    __syncthreads();
-    if (st) st[0] = (long long)__builtin_readcyclecounter();
-
-    // ---- forward -------------------------------------------------------
-    for (int l = 0; l < g.nl; ++l) {
-        const GLay &L = g.L[l];
+    const int row = 4 * wave + rq;
+    for (int l = 0; l < nl; ++l) {
+        const GLay &L = Ls[l];
         const int F = L.fout, ld = L.ld;
-        const float *X = L.src < 0 ? S + g.oc : S + g.L[L.src].yr;
-        const int ldx = L.src < 0 ? g.ld0 : g.L[L.src].ld;
+        const float *X = L.src < 0 ? S + oc : S + Ls[L.src].yr;
+        const int ldx = L.src < 0 ? ld0 : Ls[L.src].ld;
         float *Y = S + L.yr;
+        // the LN affine for this update's row passes (forward and backward) to
+        // LDS, its loads in flight under the GEMM
+        float ga[2] = {0.f, 0.f}, be[2] = {0.f, 0.f};
+        if (L.ln == 2) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (tid + h * kGT < F) {
+                    ga[h] = pr[L.g + tid + h * kGT];
+                    be[h] = pr[L.be + tid + h * kGT];
+                }
+        }
         few_gemm(X, ldx, prs, L.w * 4, L.fin, F, pr + L.b, [&](int m, int n, float v) { Y[m * ld + n] = v; });
+        if (L.ln == 2) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (tid + h * kGT < F) {
+                    S[L.af + tid + h * kGT] = ga[h];
+                    S[L.af + F + tid + h * kGT] = be[h];
+                }
+        }
         __syncthreads();
         if (L.ln || L.relu) {
             const float invF = 1.f / (float)F;
@@ -1350,14 +1357,14 @@ __device__ __forceinline__ void few_grads(const GArgs &g, float *S, const float 
                     vs += d * d;
                 }
                 rstd = 1.f / sqrtf(rsum16(vs) / (float)F + 1e-5f);
-                if (sub == 0) S[L.rs + row] = rstd;
+                if (sub == 0 && L.rs >= 0) S[L.rs + row] = rstd;
             }
             for (int j = sub; j < F; j += 16) {
                 float v = y[j];
                 if (L.ln) {
                     const float xh = (v - mean) * rstd;
-                    S[L.xh + row * ld + j] = xh;
-                    v = L.ln == 2 ? xh * pr[L.g + j] + pr[L.be + j] : xh;
+                    if (L.xh >= 0) S[L.xh + row * ld + j] = xh;
+                    v = L.ln == 2 ? xh * S[L.af + j] + S[L.af + F + j] : xh;
                 }
                 if (L.relu) v = relu(v);
                 y[j] = v;
@@ -1366,6 +1373,39 @@ __device__ __forceinline__ void few_grads(const GArgs &g, float *S, const float 
         }
         if (st) st[1 + l] = (long long)__builtin_readcyclecounter();
     }
+
+}
+
+// One update's gradient of a partner's rows (rk <= 16 of them, observations
+// at xobs, rollout rows s0 ..) into the gradient row G, plus the loss /
+// approx_kl partial sums: the few-row counterpart of minibatch_grads, same
+// float operations per element.  S: the LDS tiles (plan_few).
+__device__ __forceinline__ void few_grads(const GArgs &g, float *S, const float *pr, const float *wb, float *G,
+                                          const float *xobs, const int *gact_e, const unsigned *gmask_e,
+                                          const float *grow_e, long long s0, int rk, float inv_b, float entp,
+                                          float &lsum, float &klsum, long long *st) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = lane & 15, rq = lane >> 4;
+    const int row = 4 * wave + rq;  // the lane group's row in the row passes
+    const int A = g.A, D = g.D;
+    const long long S_ = g.S;
+    const auto prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(pr), 0, __builtin_amdgcn_readfirstlane(g.n * 4),
+                                                       0x00020000);
+    // observation rows (zero past the slice)
+    {
+        float *x0 = S + g.oc;
+        for (int i = tid; i < kFR * D; i += kGT) {
+            const int b = i / D, d = i - b * D;
+            float v = 0.f;
+            if (b < rk) v = xobs[i];
+            x0[b * g.ld0 + d] = v;
+        }
+    }
+    __syncthreads();
+    if (st) st[0] = (long long)__builtin_readcyclecounter();
+
+    // ---- forward -------------------------------------------------------
+    few_forward(g.L, g.nl, S, pr, prs, g.oc, g.ld0, st);
 
     // ---- PPO loss row pass: logits / value -> d(logits), d(value) (ppo.py:876-908)
     {
@@ -1444,14 +1484,14 @@ __device__ __forceinline__ void few_grads(const GArgs &g, float *S, const float 
             auto dpre = [&](int j, float &x) {
                 const float d = dy[j];
                 x = xh[j];
-                const float pre = L.ln == 2 ? x * pr[L.g + j] + pr[L.be + j] : x;
+                const float pre = L.ln == 2 ? x * S[L.af + j] + S[L.af + F + j] : x;
                 return (!L.relu || pre > 0.f) ? d : 0.f;
             };
             if (L.ln) {
                 float s1 = 0.f, s2 = 0.f;
                 for (int j = sub; j < F; j += 16) {
                     float x;
-                    const float dx = dpre(j, x) * (L.ln == 2 ? pr[L.g + j] : 1.f);
+                    const float dx = dpre(j, x) * (L.ln == 2 ? S[L.af + j] : 1.f);
                     s1 += dx;
                     s2 += dx * x;
                 }
@@ -1463,7 +1503,7 @@ __device__ __forceinline__ void few_grads(const GArgs &g, float *S, const float 
                 float x;
                 const float dp = dpre(j, x);
                 if (L.ln == 2) T[row * ld + j] = dp;
-                dy[j] = L.ln ? rs * (dp * (L.ln == 2 ? pr[L.g + j] : 1.f) - m1 - x * m2) : dp;
+                dy[j] = L.ln ? rs * (dp * (L.ln == 2 ? S[L.af + j] : 1.f) - m1 - x * m2) : dp;
             }
             __syncthreads();
         }
@@ -1494,11 +1534,11 @@ __device__ __forceinline__ void few_grads(const GArgs &g, float *S, const float 
             float *dys = S + Ls.dy;
             const int lds_ = Ls.ld;
             if (L.acc)
-                few_gemm(dZ, ld, wts, (int)(L.wt - g.wt0) * 4, F, L.fin, nullptr,
-                         [&](int m, int n, float v) { dys[m * lds_ + n] += v; });
+                few_gemm<true>(dZ, ld, prs, L.w * 4, F, L.fin, nullptr,
+                               [&](int m, int n, float v) { dys[m * lds_ + n] += v; });
             else
-                few_gemm(dZ, ld, wts, (int)(L.wt - g.wt0) * 4, F, L.fin, nullptr,
-                         [&](int m, int n, float v) { dys[m * lds_ + n] = v; });
+                few_gemm<true>(dZ, ld, prs, L.w * 4, F, L.fin, nullptr,
+                               [&](int m, int n, float v) { dys[m * lds_ + n] = v; });
         }
         __syncthreads();
         if (st) st[20 + 3 * l] = (long long)__builtin_readcyclecounter();
@@ -1550,7 +1590,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
         __hip_atomic_store(xcc + kk, (unsigned)(x & 15) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    for (int l = 0; l < g.nl; ++l) {
+    for (int l = 0; l < (FEW ? 0 : g.nl); ++l) {
         const GLay &L = g.L[l];
         if (L.wt < 0) continue;
         const int cnt = L.fout * L.fin;
@@ -1628,12 +1668,19 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
             GST(3);
 
             // ---- 2. reduce-scatter of the owned chunks + partial norms ---------------
+            // few-row form with at most four owned chunks per thread: the sums stay
+            // in registers for Adam and the chunks' moments / parameters are loaded
+            // before barrier 2 (they land while it waits)
+            const bool regs = FEW && own1 - own0 <= 4 * kGT;
+            f4 tg[2][2];
+            float mg[2][2][4], vg[2][2][4], pg[2][2][4];
             float q0 = 0.f, q1 = 0.f;
             {
                 const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab0, 0, __builtin_amdgcn_readfirstlane(
                                                                                  (int)(K * g.nslab * 4)), 0x00020000);
                 // two chunks per thread per round, partner order, up to 16 loads in flight
-                for (int cb = own0 + tid; cb < own1; cb += 2 * kGT) {
+                int rr = 0;
+                for (int cb = own0 + tid; cb < own1; cb += 2 * kGT, ++rr) {
                     f4 t[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
                     for (int q0_ = 0; q0_ < K; q0_ += 8) {  // uniform
                         f4 x[2][8];
@@ -1660,11 +1707,20 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
                             }
                         }
                     }
+                    if (regs) {
+                        if (rr == 0) {
+                            tg[0][0] = t[0];
+                            tg[0][1] = t[1];
+                        } else {
+                            tg[1][0] = t[0];
+                            tg[1][1] = t[1];
+                        }
+                    }
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int c = cb + h * kGT;
                         if (c >= own1) break;
-                        *reinterpret_cast<f4 *>(sum + 4 * c) = t[h];
+                        if (!regs) *reinterpret_cast<f4 *>(sum + 4 * c) = t[h];
 #pragma unroll
                         for (int cc = 0; cc < 4; ++cc) {
                             const int f = 4 * c + cc;
@@ -1677,6 +1733,20 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
                 q0 = wave_sum(q0);
                 q1 = wave_sum(q1);
                 if (lane < 2) sum[nal + 4 + (kk * kGW + wave) * 2 + lane] = lane ? q1 : q0;
+            }
+            if (regs) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int cc = 0; cc < 4; ++cc) {
+                            const int f = 4 * (own0 + tid + (2 * r + h) * kGT) + cc;
+                            const int fs = f < f1 ? f : f0;
+                            mg[r][h][cc] = gm[fs];
+                            vg[r][h][cc] = gv[fs];
+                            pg[r][h][cc] = pr[fs];
+                        }
             }
             GST(4);
             if (!gpart_sync(c2, (unsigned)(K * (upd + 1)), !local, tmo, g.err, &s_ok)) return;
@@ -1715,7 +1785,23 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
             // round (all loads of a round first); an element inside a layer's W
             // also goes to the transposed copy (the layer found by a short scan of
             // the layer list: contiguous W ranges, at most 16 layers)
-            {
+            if (regs) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int cc = 0; cc < 4; ++cc) {
+                            const int f = 4 * (own0 + tid + (2 * r + h) * kGT) + cc;
+                            if (f >= f1) continue;
+                            const float gc = tg[r][h][cc] * (f < g.cstart ? cl0 : cl1);
+                            const float m = mg[r][h][cc] + ob1 * (gc - mg[r][h][cc]);
+                            const float v = vg[r][h][cc] * g.b2 + ob2 * gc * gc;
+                            gm[f] = m;
+                            gv[f] = v;
+                            pr[f] = pg[r][h][cc] - step_size * (m / (sqrtf(v) / bc2s + g.eps));
+                        }
+            } else {
                 constexpr int U = 8;
                 for (int i0 = f0 + tid; i0 < f1; i0 += U * kGT) {
                     float gg[U], mm[U], vv[U], pp[U];
@@ -1739,13 +1825,15 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
                         gm[f] = m;
                         gv[f] = v;
                         pr[f] = np_;
-                        for (int l = 0; l < g.nl; ++l) {
-                            const GLay &L = g.L[l];
-                            const int i = f - L.w;
-                            if (L.wt >= 0 && i >= 0 && i < L.fout * L.fin) {
-                                const int o = i / L.fin, c = i - o * L.fin;
-                                wb[L.wt + (size_t)c * L.fout + o] = np_;
-                                break;
+                        if constexpr (!FEW) {  // the few-row form's dX reads W itself
+                            for (int l = 0; l < g.nl; ++l) {
+                                const GLay &L = g.L[l];
+                                const int i = f - L.w;
+                                if (L.wt >= 0 && i >= 0 && i < L.fout * L.fin) {
+                                    const int o = i / L.fin, c = i - o * L.fin;
+                                    wb[L.wt + (size_t)c * L.fout + o] = np_;
+                                    break;
+                                }
                             }
                         }
                     }
@@ -1775,6 +1863,8 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
 struct GActArgs {
     GLay L[kGL];
     int nl, aout, cout, A, D, n, rows;
+    int ld0;                 // few-row form: the observation tile's row stride
+    long long oc, lds_floats;  // few-row form: its offset, the LDS tiles' size
     long long ws_block;  // scratch floats per (agent, row block)
     long long obs_off;   // persistent rollout: the step's observation rows [rows][D] in the block scratch
     float *ws;
@@ -1800,6 +1890,7 @@ struct GActArgs {
 // mask_copy when that is set.
 struct GSample {
     int A, N, sample;
+    int lda, ldv;  // row strides of the logits and the values
     unsigned long long seed, counter;
     const long long *env_base;
     const unsigned char *mask;
@@ -1810,6 +1901,7 @@ struct GSample {
     float *logp_out, *value_out, *ent_out;
     long long out_pstride;
     long long *act_flat;
+    long long env_off = -1;  // >= 0: the block's agent's first env (else env_base[p], or p N)
 };
 template <bool HOST_MASK>
 __device__ __forceinline__ void graph_sample(const GSample &g, const float *lgp, const float *vp, int p, int n0,
@@ -1822,8 +1914,8 @@ __device__ __forceinline__ void graph_sample(const GSample &g, const float *lgp,
         const int r = r0 + 4 * wave + rq;
         const bool live = r < nrow;
         const int rr = live ? r : 0;
-        float lg0 = a0 < A ? lgp[(size_t)rr * A + a0] : -3.0e38f;
-        float lg1 = a1 < A ? lgp[(size_t)rr * A + a1] : -3.0e38f;
+        float lg0 = a0 < A ? lgp[(size_t)rr * g.lda + a0] : -3.0e38f;
+        float lg1 = a1 < A ? lgp[(size_t)rr * g.lda + a1] : -3.0e38f;
         if (g.mask && live) {
             const size_t mo = (size_t)p * g.mask_pstride + (size_t)(n0 + r) * A;
             unsigned char ok0 = 1, ok1 = 1;
@@ -1843,8 +1935,10 @@ __device__ __forceinline__ void graph_sample(const GSample &g, const float *lgp,
         const float H = -rsum16((a0 < A ? p0 * logf(p0 + 1e-8f) : 0.f) + (a1 < A ? p1 * logf(p1 + 1e-8f) : 0.f));
         float sc0 = lg0, sc1 = lg1;
         if (g.sample) {
-            const unsigned long long env =
-                (g.env_base ? (unsigned long long)g.env_base[p] : (unsigned long long)p * g.N) + n0 + rr;
+            const unsigned long long env = (g.env_off >= 0   ? (unsigned long long)g.env_off
+                                            : g.env_base ? (unsigned long long)g.env_base[p]
+                                                         : (unsigned long long)p * g.N) +
+                                           n0 + rr;
             auto gumbel = [&](int a, float lg) {
                 const uint4 rnd = philox(make_uint4((unsigned)env, (unsigned)(env >> 32), (unsigned)g.counter,
                                                     (unsigned)(g.counter >> 32) ^ ((unsigned)(a >> 2) << 24)),
@@ -1869,7 +1963,7 @@ __device__ __forceinline__ void graph_sample(const GSample &g, const float *lgp,
             if (g.act_out) g.act_out[o] = choice;
             if (g.logp_out) g.logp_out[o] = (choice < 16 ? c0 : c1) - lse;
             if (g.ent_out) g.ent_out[o] = H;
-            if (g.value_out) g.value_out[o] = vp[r];
+            if (g.value_out) g.value_out[o] = vp[(size_t)r * g.ldv];
             if (g.act_flat)  // host staging: system-scope (write-through) store
                 __hip_atomic_store(g.act_flat + (size_t)p * g.N + n0 + r, (long long)choice, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1879,16 +1973,38 @@ __device__ __forceinline__ void graph_sample(const GSample &g, const float *lgp,
 
 // Rollout policy step (PPO.get_action, ppo.py:567-633) of workgroup (p, row
 // block): forward through the layer list, then graph_sample.
+// FEW: the block's 16 rows through few_forward's LDS tiles (act_plan_few).
+template <bool FEW>
 __global__ __launch_bounds__(kGT) void ppo_act_graph_kernel(const GActArgs g) {
     __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
+    extern __shared__ __attribute__((aligned(16))) float gdyn[];
     const int p = blockIdx.y, n0 = blockIdx.x * g.rows;
     const int nrow = g.N - n0 < g.rows ? g.N - n0 : g.rows;
-    float *base = g.ws + ((size_t)p * gridDim.x + blockIdx.x) * g.ws_block;
     const float *pr = g.params + (size_t)p * g.n;
-    forward_layers(g.L, g.nl, g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * g.D, nrow, base, pr, g.rows, lds);
-    GSample s{g.A, g.N, g.sample, g.seed, g.counter, g.env_base, g.mask, g.mask_pstride, nullptr, 0,
-              g.act_out, g.logp_out, g.value_out, g.ent_out, g.out_pstride, g.act_flat};
-    graph_sample<false>(s, base + g.L[g.aout].yr, base + g.L[g.cout].yr, p, n0, nrow);
+    const float *obs = g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * g.D;
+    const GLay &La = g.L[g.aout], &Lc = g.L[g.cout];
+    if constexpr (FEW) {
+        const int tid = threadIdx.x;
+        for (int i = tid; i < (int)g.lds_floats; i += kGT) gdyn[i] = 0.f;
+        __syncthreads();
+        for (int i = tid; i < nrow * g.D; i += kGT) {
+            const int b = i / g.D, d = i - b * g.D;
+            gdyn[g.oc + b * g.ld0 + d] = obs[i];
+        }
+        __syncthreads();
+        const auto prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(pr), 0,
+                                                           __builtin_amdgcn_readfirstlane(g.n * 4), 0x00020000);
+        few_forward(g.L, g.nl, gdyn, pr, prs, g.oc, g.ld0, nullptr);
+        GSample s{g.A, g.N, g.sample, La.ld, Lc.ld, g.seed, g.counter, g.env_base, g.mask, g.mask_pstride, nullptr, 0,
+                  g.act_out, g.logp_out, g.value_out, g.ent_out, g.out_pstride, g.act_flat};
+        graph_sample<false>(s, gdyn + La.yr, gdyn + Lc.yr, p, n0, nrow);
+    } else {
+        float *base = g.ws + ((size_t)p * gridDim.x + blockIdx.x) * g.ws_block;
+        forward_layers(g.L, g.nl, obs, nrow, base, pr, g.rows, lds);
+        GSample s{g.A, g.N, g.sample, g.A, 1, g.seed, g.counter, g.env_base, g.mask, g.mask_pstride, nullptr, 0,
+                  g.act_out, g.logp_out, g.value_out, g.ent_out, g.out_pstride, g.act_flat};
+        graph_sample<false>(s, base + La.yr, base + Lc.yr, p, n0, nrow);
+    }
 }
 
 // Persistent rollout of a runtime-shape population (agx_ppo_rollout_graph_
@@ -1899,11 +2015,13 @@ __global__ __launch_bounds__(kGT) void ppo_act_graph_kernel(const GActArgs g) {
 // block's scratch and the rollout slot, the previous step's reward / done into
 // slot t-1 with the episode accounting, and (act) the forward + sample; the
 // actions go to the host staging; then this block's done word.
+template <bool FEW>
 __global__ __launch_bounds__(kGT) void ppo_rollout_graph_persistent_kernel(const GActArgs ga, const ActArgs *steps,
                                                                            int nsteps, agx_rollout_ctl *ctl,
                                                                            unsigned long long timeout_ticks,
                                                                            unsigned base_seq) {
     __shared__ __attribute__((aligned(16))) float lds[kGemmLds];
+    extern __shared__ __attribute__((aligned(16))) float gdyn[];
     __shared__ ActArgs s_args;
     __shared__ int s_go;
     const int tid = threadIdx.x;
@@ -1914,6 +2032,9 @@ __global__ __launch_bounds__(kGT) void ppo_rollout_graph_persistent_kernel(const
     float *base = ga.ws + ((size_t)p * gridDim.x + blockIdx.x) * ga.ws_block;
     float *obs_rows = base + ga.obs_off;  // [rows][D]: this step's observations
     constexpr int kArgWords = (int)(sizeof(ActArgs) / 4);
+    if constexpr (FEW) {  // the LDS tiles' padding (and the rows past the block) stay zero
+        for (int i = tid; i < (int)ga.lds_floats; i += kGT) gdyn[i] = 0.f;
+    }
     for (int t = 0; t < nsteps; ++t) {
         if (tid < kArgWords)
             reinterpret_cast<unsigned *>(&s_args)[tid] = reinterpret_cast<const unsigned *>(steps + t)[tid];
@@ -1950,7 +2071,12 @@ __global__ __launch_bounds__(kGT) void ppo_rollout_graph_persistent_kernel(const
         const float *ob = g.obs + (size_t)p * g.obs_pstride + (size_t)n0 * D;
         for (int i = tid; i < nrow * D; i += kGT) {
             const float x = ld_sys(ob + i);
-            obs_rows[i] = x;
+            if constexpr (FEW) {
+                const int b = i / D, d = i - b * D;
+                gdyn[ga.oc + b * ga.ld0 + d] = x;
+            } else {
+                obs_rows[i] = x;
+            }
             if (g.obs_copy) g.obs_copy[(size_t)p * g.obs_copy_pstride + (size_t)n0 * D + i] = x;
         }
         if (g.st_rew && tid < nrow) {
@@ -1972,13 +2098,107 @@ __global__ __launch_bounds__(kGT) void ppo_rollout_graph_persistent_kernel(const
         }
         if (g.act) {
             __syncthreads();  // the observation rows are in the scratch
-            forward_layers(ga.L, ga.nl, obs_rows, nrow, base, g.params + (size_t)p * ga.n, ga.rows, lds);
-            GSample sp{ga.A, g.N, g.sample, g.seed, g.counter, g.env_base, g.mask, g.mask_pstride, g.mask_copy,
-                       g.mask_copy_pstride, g.act_out, g.logp_out, g.value_out, g.ent_out, g.out_pstride, g.act_flat};
-            graph_sample<true>(sp, base + ga.L[ga.aout].yr, base + ga.L[ga.cout].yr, p, n0, nrow);
+            const float *pr = g.params + (size_t)p * ga.n;
+            const GLay &La = ga.L[ga.aout], &Lc = ga.L[ga.cout];
+            if constexpr (FEW) {
+                const auto prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(pr), 0,
+                                                                   __builtin_amdgcn_readfirstlane(ga.n * 4), 0x00020000);
+                few_forward(ga.L, ga.nl, gdyn, pr, prs, ga.oc, ga.ld0, nullptr);
+                GSample sp{ga.A, g.N, g.sample, La.ld, Lc.ld, g.seed, g.counter, g.env_base, g.mask, g.mask_pstride,
+                           g.mask_copy, g.mask_copy_pstride, g.act_out, g.logp_out, g.value_out, g.ent_out,
+                           g.out_pstride, g.act_flat};
+                graph_sample<true>(sp, gdyn + La.yr, gdyn + Lc.yr, p, n0, nrow);
+            } else {
+                forward_layers(ga.L, ga.nl, obs_rows, nrow, base, pr, ga.rows, lds);
+                GSample sp{ga.A, g.N, g.sample, ga.A, 1, g.seed, g.counter, g.env_base, g.mask, g.mask_pstride,
+                           g.mask_copy, g.mask_copy_pstride, g.act_out, g.logp_out, g.value_out, g.ent_out,
+                           g.out_pstride, g.act_flat};
+                graph_sample<true>(sp, base + La.yr, base + Lc.yr, p, n0, nrow);
+            }
         }
         // the host-memory stores (actions) are system-scope write-through: wait
         // for their acknowledgements, then this block's done word
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_store(rollout_done_words(ctl) + blk, base_seq + (unsigned)(t + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// One evaluation pass of a WHOLE population in one persistent launch
+// (agx_ppo_eval_multi_persistent): agent p runs ITS network (its own few-row
+// policy-step plan, agents[p]) on its own parameter row over envs
+// [p N, (p + 1) N) of the packed host staging, whatever group it trains in;
+// the host paces the steps as for ppo_rollout_graph_persistent_kernel.  Step t
+// samples with counter agents[p].counter0 + t from the agent's own Philox
+// stream (seed, env base).
+struct EvalAgent {
+    GLay L[kGL];
+    int nl, aout, cout, n, ld0;
+    long long oc, lds_floats;
+    const float *params;
+    long long env_base;
+    unsigned long long seed, counter0;
+};
+
+__global__ __launch_bounds__(kGT) void ppo_eval_multi_persistent_kernel(const EvalAgent *__restrict__ agents, int N,
+                                                                        int A, int D, const float *stage_obs,
+                                                                        long long *act_flat, int nsteps,
+                                                                        agx_rollout_ctl *ctl,
+                                                                        unsigned long long timeout_ticks,
+                                                                        unsigned base_seq) {
+    extern __shared__ __attribute__((aligned(16))) float gdyn[];
+    __shared__ int s_go;
+    const int tid = threadIdx.x;
+    const int p = blockIdx.y, n0 = blockIdx.x * kFR;
+    const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+    const int nrow = N - n0 < kFR ? N - n0 : kFR;
+    const EvalAgent &ag = agents[p];
+    unsigned *rel = rollout_release_word(ctl, gridDim.x * gridDim.y, blk);
+    const float *pr = ag.params;
+    const auto prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(pr), 0,
+                                                       __builtin_amdgcn_readfirstlane(ag.n * 4), 0x00020000);
+    for (int i = tid; i < (int)ag.lds_floats; i += kGT) gdyn[i] = 0.f;  // padding and rows past the block
+    const GLay &La = ag.L[ag.aout], &Lc = ag.L[ag.cout];
+    for (int t = 0; t < nsteps; ++t) {
+        if (tid == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            int go = 1;
+            for (;;) {
+                const unsigned v = __hip_atomic_load(rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (v == AGX_ROLLOUT_ABORT) {
+                    go = 0;
+                    __hip_atomic_store(&ctl->timeout, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                if (v == AGX_ROLLOUT_STOP) {
+                    go = 0;
+                    break;
+                }
+                if (v >= base_seq + (unsigned)(t + 1)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+                    go = 0;
+                    __hip_atomic_store(&ctl->timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) return;
+        const float *ob = stage_obs + ((size_t)p * N + n0) * D;
+        for (int i = tid; i < nrow * D; i += kGT) {
+            const int b = i / D, d = i - b * D;
+            gdyn[ag.oc + b * ag.ld0 + d] = ld_sys(ob + i);
+        }
+        __syncthreads();
+        few_forward(ag.L, ag.nl, gdyn, pr, prs, ag.oc, ag.ld0, nullptr);
+        GSample sp{A, N, 1, La.ld, Lc.ld, ag.seed, ag.counter0 + (unsigned long long)t, nullptr, nullptr, 0,
+                   nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, act_flat, ag.env_base};
+        graph_sample<true>(sp, gdyn + La.yr, gdyn + Lc.yr, p, n0, nrow);
+        // the actions are system-scope (write-through) stores: their acknowledgements, then the done word
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
         if (tid == 0)
@@ -2165,6 +2385,41 @@ long long act_plan(const GArgs &full, GActArgs &a) {
     return a.ws_block;
 }
 
+// The policy step's few-row form: act_plan's layer table with every output
+// a [16][ld] LDS tile (+ the LN affine copy), and the observation tile.  ->
+// dynamic LDS bytes, 0 when it does not fit beside the kernel's static LDS
+// (or AGX_GRAPH_FEW=0).  The policy-step block is kActRows = 16 rows either way.
+template <class KER>
+size_t act_plan_few(KER kernel, GActArgs &a) {
+    if (const char *e = getenv("AGX_GRAPH_FEW"))
+        if (atoi(e) == 0) return 0;
+    static_assert(kActRows == kFR, "the few-row policy step covers one row block");
+    auto ldof = [](int w) { return (w + 15) / 16 * 16 + 4; };
+    long long off = 0;
+    for (int l = 0; l < a.nl; ++l) {
+        GLay &L = a.L[l];
+        L.ld = ldof(L.fout);
+        L.yr = off;
+        off += (long long)kFR * L.ld;
+        L.af = -1;
+        if (L.ln == 2) {
+            L.af = off;
+            off += 2 * ((L.fout + 3) / 4 * 4);
+        }
+        L.xh = L.rs = -1;
+    }
+    a.ld0 = ldof(a.D);
+    a.oc = off;
+    off += (long long)kFR * a.ld0;
+    a.lds_floats = (off + 3) & ~3ll;
+    hipFuncAttributes fa{};
+    const size_t st = hipFuncGetAttributes(&fa, (const void *)kernel) == hipSuccess ? fa.sharedSizeBytes : 8 * 1024;
+    const size_t bytes = (size_t)a.lds_floats * 4;
+    if (st >= kLdsMax || bytes > kLdsMax - st) return 0;
+    (void)hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsMax - st));
+    return bytes;
+}
+
 struct GraphWs {
     size_t gobs, gact, gmask, grow, agents, total;
 };
@@ -2250,6 +2505,11 @@ size_t plan_few(const agx_ppo_graph *net, GArgs &a) {
         }
         L.dy = off;
         off += (long long)kFR * L.ld;
+        L.af = -1;
+        if (L.ln == 2) {
+            L.af = off;
+            off += 2 * ((L.fout + 3) / 4 * 4);
+        }
         L.yc = L.dy2 = L.dyc = -1;
         L.fuse = L.fused = 0;
         ldmax = L.ld > ldmax ? L.ld : ldmax;
@@ -2506,7 +2766,10 @@ extern "C" int agx_ppo_act_graph(const agx_ppo_graph *net, int64_t P, int64_t N,
     a.mask_pstride = mask_agent_stride;
     a.env_base = reinterpret_cast<const long long *>(agent_env_base);
     dim3 grid((unsigned)ceil_div(N, kActRows), (unsigned)P);
-    ppo_act_graph_kernel<<<grid, kGT, 0, as_stream(stream)>>>(a);
+    if (const size_t dyn = act_plan_few(ppo_act_graph_kernel<true>, a))
+        ppo_act_graph_kernel<true><<<grid, kGT, dyn, as_stream(stream)>>>(a);
+    else
+        ppo_act_graph_kernel<false><<<grid, kGT, 0, as_stream(stream)>>>(a);
     return check_launch("agx_ppo_act_graph");
 }
 
@@ -2519,7 +2782,8 @@ extern "C" int64_t agx_ppo_rollout_graph_max_workgroups(void) {
     static int occ = -1;
     if (occ < 0) {
         int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_rollout_graph_persistent_kernel, kGT, 0) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_rollout_graph_persistent_kernel<false>, kGT, 0) !=
+            hipSuccess)
             v = 0;
         occ = v;
     }
@@ -2551,7 +2815,21 @@ int launch_graph_persistent(const agx_ppo_graph *net, int64_t P, int64_t N, ActA
     const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
     ctl->nwg = (uint32_t)nwg;
     dim3 grid((unsigned)ceil_div(N, kActRows), (unsigned)P);
-    ppo_rollout_graph_persistent_kernel<<<grid, kGT, 0, as_stream(stream)>>>(a, steps, (int)nsteps, ctl, ticks, base);
+    // the few-row form when its tiles fit and the grid stays co-resident with them
+    size_t dyn = act_plan_few(ppo_rollout_graph_persistent_kernel<true>, a);
+    if (dyn) {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_rollout_graph_persistent_kernel<true>, kGT, dyn) !=
+                hipSuccess ||
+            (int64_t)v * cu_count_g() < nwg)
+            dyn = 0;
+    }
+    if (dyn)
+        ppo_rollout_graph_persistent_kernel<true><<<grid, kGT, dyn, as_stream(stream)>>>(a, steps, (int)nsteps, ctl,
+                                                                                         ticks, base);
+    else
+        ppo_rollout_graph_persistent_kernel<false><<<grid, kGT, 0, as_stream(stream)>>>(a, steps, (int)nsteps, ctl,
+                                                                                         ticks, base);
     return check_launch(who);
 }
 }  // namespace
@@ -2607,4 +2885,90 @@ extern "C" int agx_ppo_eval_graph_persistent(const agx_ppo_graph *net, int64_t P
     }
     return launch_graph_persistent(net, P, N, steps, nsteps, base, ctl, timeout_s, workspace, stream,
                                    "agx_ppo_eval_graph_persistent");
+}
+
+// ---------------------------------------------------------------------------
+// evaluation of a whole population, every agent on its own network
+// ---------------------------------------------------------------------------
+extern "C" size_t agx_ppo_eval_multi_bytes(int64_t P) { return P > 0 ? (size_t)P * sizeof(EvalAgent) : 0; }
+
+namespace {
+// agent p's policy-step plan (act_plan + act_plan_few) into x; -> its dynamic
+// LDS bytes (0: the plan does not fit)
+size_t eval_agent_plan(const agx_ppo_graph *net, EvalAgent &x) {
+    GArgs full{};
+    if (plan_graph(net, 1, full) != AGX_OK) return 0;
+    GActArgs a{};
+    act_plan(full, a);
+    const size_t dyn = act_plan_few(ppo_eval_multi_persistent_kernel, a);
+    if (!dyn) return 0;
+    for (int l = 0; l < kGL; ++l) x.L[l] = a.L[l];
+    x.nl = a.nl;
+    x.aout = a.aout;
+    x.cout = a.cout;
+    x.n = a.n;
+    x.ld0 = a.ld0;
+    x.oc = a.oc;
+    x.lds_floats = a.lds_floats;
+    return dyn;
+}
+}  // namespace
+
+extern "C" int agx_ppo_eval_multi_supported(const agx_ppo_graph *const *nets, int64_t P, int64_t N) {
+    if (!nets || P <= 0 || N <= 0 || P > 65535) return 0;
+    if (const char *e = getenv("AGX_GRAPH_FEW"))
+        if (atoi(e) == 0) return 0;
+    size_t dyn = 0;
+    for (int64_t p = 0; p < P; ++p) {
+        EvalAgent x{};
+        if (!nets[p] || nets[p]->obs_dim != nets[0]->obs_dim || nets[p]->n_actions != nets[0]->n_actions) return 0;
+        const size_t d = eval_agent_plan(nets[p], x);
+        if (!d) return 0;
+        dyn = d > dyn ? d : dyn;
+    }
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_eval_multi_persistent_kernel, kGT, dyn) != hipSuccess)
+        return 0;
+    return (int64_t)v * cu_count_g() >= P * ceil_div(N, kFR) ? 1 : 0;
+}
+
+extern "C" int agx_ppo_eval_multi_persistent(const agx_ppo_graph *const *nets, const float *const *params,
+                                             const int64_t *env_base, const uint64_t *seeds,
+                                             const uint64_t *counters, int64_t P, int64_t N, const float *stage_obs,
+                                             int64_t *actions_flat, int64_t nsteps, uint32_t base, void *agents_host,
+                                             void *agents_dev, agx_rollout_ctl *ctl, double timeout_s, void *stream) {
+    AGX_REQUIRE(nets && params && env_base && seeds && counters && stage_obs && actions_flat && agents_host &&
+                    agents_dev && ctl && P > 0 && N > 0 && P <= 65535 && nsteps >= 1,
+                "agx_ppo_eval_multi_persistent: bad arguments");
+    AGX_REQUIRE((uint64_t)base + (uint64_t)nsteps < AGX_ROLLOUT_STOP, "agx_ppo_eval_multi_persistent: base wraps");
+    AGX_REQUIRE(timeout_s > 0 && timeout_s < 3600, "agx_ppo_eval_multi_persistent: timeout_s out of range");
+    AGX_REQUIRE(agx_ppo_eval_multi_supported(nets, P, N), "agx_ppo_eval_multi_persistent: unsupported population");
+    EvalAgent *ag = static_cast<EvalAgent *>(agents_host);
+    size_t dyn = 0;
+    for (int64_t p = 0; p < P; ++p) {
+        AGX_REQUIRE(params[p], "agx_ppo_eval_multi_persistent: agent %lld has no parameters", (long long)p);
+        EvalAgent x{};
+        const size_t d = eval_agent_plan(nets[p], x);
+        dyn = d > dyn ? d : dyn;
+        x.params = params[p];
+        x.env_base = env_base[p];
+        x.seed = seeds[p];
+        x.counter0 = counters[p];
+        ag[p] = x;
+    }
+    hipStream_t s = as_stream(stream);
+    if (hipMemcpyAsync(agents_dev, agents_host, (size_t)P * sizeof(EvalAgent), hipMemcpyHostToDevice, s) !=
+        hipSuccess) {
+        set_error("agx_ppo_eval_multi_persistent: agent table copy failed");
+        return AGX_EHIP;
+    }
+    const int64_t nwg = P * ceil_div(N, kFR);
+    const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    ctl->nwg = (uint32_t)nwg;
+    dim3 grid((unsigned)ceil_div(N, kFR), (unsigned)P);
+    ppo_eval_multi_persistent_kernel<<<grid, kGT, dyn, s>>>(static_cast<const EvalAgent *>(agents_dev), (int)N,
+                                                            nets[0]->n_actions, nets[0]->obs_dim, stage_obs,
+                                                            reinterpret_cast<long long *>(actions_flat), (int)nsteps,
+                                                            ctl, ticks, base);
+    return check_launch("agx_ppo_eval_multi_persistent");
 }

@@ -214,26 +214,67 @@ class PopulationEngine:
     # ------------------------------------------------------------------ #
     def train(self, evo_steps: int, on_iteration=None) -> list:
         """Every group runs its agents' iterations of the generation; ->
-        per-iteration mean losses (host arrays, slot order where known)."""
-        losses = []
+        per-iteration mean losses (host arrays, group by group, slot order
+        where known).
+
+        The groups' iterations interleave, each group on a stream of its own:
+        iteration i of every group, then iteration i + 1, ...  A group's
+        learner (enqueued behind its rollout) then runs on the device while the
+        host paces the NEXT group's rollout, and the groups' learners overlap
+        one another.  At most one persistent launch is ever paced, and the
+        host waits only for the launch it paces (the other streams hold finite
+        kernels), so no hardware-queue ordering can stall it.  No host sync
+        inside the loop: errors and losses are read once every group's
+        iterations are queued (the learner reuses its loss buffer, hence the
+        device-side copies)."""
         base = self._counter0 + (self._generation << 24)
         self._generation += 1
-        for g in self.groups:
+        main = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        iters, pending = [], []
+        for k, g in enumerate(self.groups):
             if g.pop.act_counter > base:
                 raise RuntimeError(f"rollout counter {g.pop.act_counter} overran generation {self._generation - 2}")
             g.pop.act_counter = base
-            # no host sync between a group's iterations: the next rollout and
-            # learn are enqueued while the device still learns (the learner
-            # reuses its loss buffer, hence the device-side copies); errors and
-            # losses are read once the group's iterations are queued
-            pending = []
-            for _ in range(self.iterations(evo_steps, g.learn_step)):
-                pending.append(g.runner.iteration().clone())
-                if on_iteration is not None:
-                    on_iteration(g)
+            iters.append(self.iterations(evo_steps, g.learn_step))
+            pending.append([])
+        streams = [self._train_stream(k) for k in range(len(self.groups))] if main is not None else None
+        if streams is not None:
+            for st in streams:  # parameters / buffers written by selection, mutation, regrouping
+                st.wait_stream(main)
+        try:
+            for i in range(max(iters, default=0)):
+                for k, g in enumerate(self.groups):
+                    if i >= iters[k]:
+                        continue
+                    if streams is not None:
+                        with torch.cuda.stream(streams[k]):
+                            pending[k].append(g.runner.iteration().clone())
+                    else:
+                        pending[k].append(g.runner.iteration().clone())
+                    if on_iteration is not None:
+                        on_iteration(g)
+        finally:
+            if streams is not None:
+                for st in streams:
+                    main.wait_stream(st)
+        losses = []
+        for k, g in enumerate(self.groups):
             g.pop.check_errors()
-            losses += [x.cpu().numpy() for x in pending]
+            losses += [x.cpu().numpy() for x in pending[k]]
         return losses
+
+    def _train_stream(self, k: int):
+        """Group k's training stream: a non-blocking stream of its own
+        (agx_stream_create), made once per engine."""
+        from .. import _lib
+
+        pool = self.__dict__.setdefault("_train_streams", [])
+        while len(pool) <= k:
+            h = _lib.load().agx_stream_create()
+            if not h:
+                raise _lib.AgxError(_lib.load().agx_last_error().decode(errors="replace"))
+            pool.append(torch.cuda.ExternalStream(h, device=self.device))
+        return pool[k]
 
     def steps_per_generation(self, slot: int, evo_steps: int) -> int:
         g, _ = self.group_of(slot)
@@ -249,19 +290,39 @@ class PopulationEngine:
         return r_sum, r_cnt
 
     def evaluate(self, loop: int, max_steps) -> list[float]:
-        """agent.test for every agent (train_on_policy.py:363-373): each
-        group's pass as PopulationRunner.evaluate — a persistent launch per
-        pass where the group's policy step is a HIP kernel — one group after
-        another; groups on the PyTorch policy step are stepped together
-        (runner.run_lockstep).  A group's samples depend only on its agents'
-        counters, so the order does not change any result."""
-        from .runner import _EvalDriver, run_lockstep
+        """agent.test for every agent (train_on_policy.py:363-373).  Where
+        every group paces persistent launches and every network has an
+        evaluation layer list (runner.population_eval_ok), ALL agents run one
+        pass together: ONE persistent launch (agx_ppo_eval_multi_persistent),
+        each agent on its own network, over one stack of all the agents' envs.
+        Otherwise each group's pass as PopulationRunner.evaluate — a
+        persistent launch per pass where the group's policy step is a HIP
+        kernel — one group after another, and groups on the PyTorch policy
+        step stepped together (runner.run_lockstep).  A group's samples depend
+        only on its agents' counters, so neither form changes any result."""
+        from .runner import _EvalDriver, population_eval_ok, run_lockstep
 
-        out = [0.0] * self.P
         self._eval_calls += 1
         acc = {id(g): np.zeros(g.pop.P) for g in self.groups}
         for g in self.groups:
             g.pop.eval_rounds = self._eval_calls
+        runners = [g.runner for g in self.groups]
+        if population_eval_ok(runners) and (len(self.groups) == 1 or self.slot_envs is not None):
+            # every agent of every group in ONE persistent launch per pass
+            # (agx_ppo_eval_multi_persistent) on one stack of all their envs
+            if len(self.groups) == 1:
+                env, staging = runners[0].env, None
+            else:
+                env = StackedVecEnv([self.slot_envs[j] for g in self.groups for j in g.slots])
+                staging = self._eval_staging(sum(g.pop.P for g in self.groups))
+            for k in range(loop):
+                d = _EvalDriver(runners[0], k, max_steps, runners=runners, env=env, staging=staging)
+                run_lockstep([d])
+                res, off = d.result(), 0
+                for g in self.groups:
+                    acc[id(g)] += res[off:off + g.pop.P]
+                    off += g.pop.P
+            return self._fitness(acc, loop)
         # Groups with a HIP policy step run their passes as persistent launches,
         # ONE resident at a time: a process has few hardware queues
         # (GPU_MAX_HW_QUEUES, 4 by default), so two resident launches — or a
@@ -279,12 +340,36 @@ class PopulationEngine:
                 run_lockstep([d for _, d in drivers])
                 for g, d in drivers:
                     acc[id(g)] += d.result()
+        return self._fitness(acc, loop)
+
+    def _fitness(self, acc: dict, loop: int) -> list[float]:
+        out = [0.0] * self.P
         for g in self.groups:
             g.runner.after_evaluation()
             f = acc[id(g)] / loop
             for r, slot in enumerate(g.slots):
                 out[slot] = float(f[r])
         return out
+
+    def _eval_staging(self, P: int):
+        """Coherent host staging of the population-wide evaluation pass (obs /
+        reward / done, actions, control block, per-agent plan table), kept
+        for the population size it was made for."""
+        from .runner import _coherent, _packed
+
+        bufs = getattr(self, "_eval_bufs", None)
+        if bufs is None or bufs[0] != P:
+            from .. import _lib
+
+            lib = _lib.load()
+            pop = self.groups[0].pop
+            N, D = pop.N, pop.spec.obs_dim
+            _, obs, rew, done = _packed(P, N, D, owner=self)
+            act = _coherent(self, P * N * 8).view(torch.int64)
+            ctl = _coherent(self, int(lib.agx_ppo_rollout_graph_ctl_bytes(P, N)))
+            agents = _coherent(self, int(lib.agx_ppo_eval_multi_bytes(P)))
+            bufs = self._eval_bufs = (P, (obs, rew, done, act, ctl, None, agents))
+        return bufs[1]
 
     # ------------------------------------------------------------------ #
     def local_states(self) -> list[AgentState]:

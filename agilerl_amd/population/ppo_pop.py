@@ -139,6 +139,7 @@ class PPOPopulation:
         self.act_counter = 0
         self._desc = None
         self._gdesc = None
+        self._edesc = None
         self._alloc_rollout()
         self.env_base_d = torch.tensor([i * self.N for i in self.agent_ids], dtype=torch.int64, device=self.device)
         self.learn_steps = 0
@@ -224,6 +225,21 @@ class PPOPopulation:
 
             self._gdesc = graph_descriptor(self.spec) or False
         return self._gdesc or None
+
+    def eval_descriptor(self):
+        """agx_ppo_graph of this network for the evaluation passes: every MLP
+        actor-critic, the compiled shapes included, so that a population's
+        agents are evaluated together in one launch whatever kernels they train
+        on (agx_ppo_eval_multi_persistent).  None: the PyTorch policy step."""
+        if not self.fused or not isinstance(self.spec, ActorCriticSpec):
+            return None
+        if self.fused_descriptor() is None:
+            return self.learn_descriptor()  # already the runtime layer list
+        if self._edesc is None:
+            from .learner import graph_descriptor
+
+            self._edesc = graph_descriptor(self.spec) or False
+        return self._edesc or None
 
     @torch.no_grad()
     def act_into(self, t: int, actions_flat: torch.Tensor | None = None) -> None:

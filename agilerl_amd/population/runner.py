@@ -76,9 +76,20 @@ class AgxRolloutIO(ctypes.Structure):
 # the end of the pacing.
 _PACING = 0
 _DEFERRED_FREES: list[int] = []
+# Coherent buffers of retired runners, by size: the population engine rebuilds
+# its groups every generation with the same staging sizes, so a buffer goes
+# back to this pool instead of hipHostFree (which waits for the device) and the
+# next runner of that size takes it instead of a fresh hipHostMalloc.
+_HOST_POOL: dict[int, list[int]] = {}
+_HOST_POOL_MAX = 64  # buffers kept per size; the rest are freed
 
 
-def _host_free(p: int) -> None:
+def _host_free(p: int, nbytes: int | None = None) -> None:
+    if nbytes is not None:
+        pool = _HOST_POOL.setdefault(nbytes, [])
+        if len(pool) < _HOST_POOL_MAX:
+            pool.append(p)
+            return
     if _PACING:
         _DEFERRED_FREES.append(p)
     else:
@@ -100,14 +111,20 @@ def _pacing_end() -> None:
 
 
 def _coherent(owner, nbytes: int) -> torch.Tensor:
-    """uint8 CPU tensor over agx_host_alloc memory (coherent, device-accessible
-    at the same address), freed with its owner (deferred while a persistent
-    rollout is being paced, see _host_free)."""
-    lib = _lib.load()
-    p = lib.agx_host_alloc(nbytes)
-    if not p:
-        raise _lib.AgxError(lib.agx_last_error().decode(errors="replace"))
-    weakref.finalize(owner, _host_free, p)
+    """Zeroed uint8 CPU tensor over agx_host_alloc memory (coherent,
+    device-accessible at the same address), returned to the size pool when its
+    owner is collected (see _host_free)."""
+    pool = _HOST_POOL.get(nbytes)
+    if pool:
+        p = pool.pop()
+        ctypes.memset(p, 0, nbytes)
+    else:
+        lib = _lib.load()
+        p = lib.agx_host_alloc(nbytes)
+        if not p:
+            raise _lib.AgxError(lib.agx_last_error().decode(errors="replace"))
+        ctypes.memset(p, 0, nbytes)
+    weakref.finalize(owner, _host_free, p, nbytes)
     return torch.from_numpy(np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)))
 
 
@@ -422,9 +439,11 @@ class PopulationRunner:
             lib = _lib.load()
             _, obs, rew, done = _packed(P, N, D, owner=self)
             act = _coherent(self, P * N * 8).view(torch.int64)
-            ctl = _coherent(self, self._ctl_bytes())
+            # room for the group's own evaluation launch and the population-wide one
+            ctl = _coherent(self, max(self._ctl_bytes(), int(lib.agx_ppo_rollout_graph_ctl_bytes(P, N))))
             args = _coherent(self, int(lib.agx_rollout_args_bytes(_EVAL_CHUNK)))
-            self._eval_bufs = (obs, rew, done, act, ctl, args)
+            agents = _coherent(self, int(lib.agx_ppo_eval_multi_bytes(P)))
+            self._eval_bufs = (obs, rew, done, act, ctl, args, agents)
         return self._eval_bufs
 
     def after_evaluation(self) -> None:
@@ -486,47 +505,113 @@ class PopulationRunner:
 _EVAL_CHUNK = 1024
 
 
-class _EvalDriver:
-    """One evaluation pass of one group: reset, then per vector step the
-    sampled policy step of every agent (evaluation counters
-    ``(1 << 41) + (eval_round << 24) + (k << 20) + step``, the agent's own
-    Philox stream), the env step, and each env's first finished episode
-    score.  Persistent mode keeps ONE launch resident for the pass
-    (agx_ppo_eval_persistent) and paces it through its own control block;
-    otherwise one policy-step launch + event wait per step."""
+def _eval_nets(runners: list) -> tuple | None:
+    """(per-agent ctypes array of agx_ppo_graph pointers, [edesc per runner])
+    when every runner's network has an evaluation layer list, else None."""
+    descs = [r.pop.eval_descriptor() for r in runners]
+    if any(d is None for d in descs):
+        return None
+    ptrs = [ctypes.cast(ctypes.pointer(d), ctypes.c_void_p).value for r, d in zip(runners, descs) for _ in range(r.pop.P)]
+    return (ctypes.c_void_p * len(ptrs))(*ptrs), descs
 
-    def __init__(self, runner: "PopulationRunner", k: int, max_steps: int | None, allow_persistent: bool = True):
-        self.runner, self.pop, self.env = runner, runner.pop, runner.env
+
+def population_eval_ok(runners: list, paced: bool = True) -> bool:
+    """Whether the runners' agents can be evaluated together in ONE persistent
+    launch (agx_ppo_eval_multi_persistent): every runner paces persistent
+    launches (a device-free env; not asked with paced=False), every network
+    has an evaluation layer list, one env width, and the kernel takes the
+    whole grid."""
+    if not runners or (paced and not all(r.persistent or r.graph_persistent for r in runners)):
+        return False
+    pops = [r.pop for r in runners]
+    if len({(p.N, p.spec.obs_dim, p.spec.n_actions) for p in pops}) != 1:
+        return False
+    if any(p.obs.dtype != torch.float32 for p in pops):
+        return False
+    nets = _eval_nets(runners)
+    if nets is None:
+        return False
+    P = sum(p.P for p in pops)
+    return bool(_lib.load().agx_ppo_eval_multi_supported(nets[0], P, pops[0].N))
+
+
+class _EvalDriver:
+    """One evaluation pass of one group — or of several groups together
+    (``runners``: the population engine's groups, on the stacked ``env``
+    holding their envs in order): reset, then per vector step the sampled
+    policy step of every agent (evaluation counters ``(1 << 41) +
+    (eval_round << 24) + (k << 20) + step``, the agent's own Philox stream),
+    the env step, and each env's first finished episode score.  Persistent
+    mode keeps ONE launch resident for the pass and paces it through its own
+    control block: agx_ppo_eval_multi_persistent (every agent on its own
+    network, all groups at once) where population_eval_ok holds, else the
+    group's agx_ppo_eval_persistent / agx_ppo_eval_graph_persistent;
+    otherwise one policy-step launch + event wait per step (the evaluation
+    layer list when the multi form is available, so both give the same
+    samples)."""
+
+    def __init__(self, runner: "PopulationRunner", k: int, max_steps: int | None, allow_persistent: bool = True,
+                 runners: list | None = None, env=None, staging=None):
+        self.runners = list(runners) if runners else [runner]
+        self.runner, self.pop = runner, runner.pop
+        self.env = env if env is not None else runner.env
+        pops = [r.pop for r in self.runners]
         pop = self.pop
-        P, N, D = pop.P, pop.N, pop.spec.obs_dim
+        P, N, D = sum(p.P for p in pops), pop.N, pop.spec.obs_dim
         self.P, self.N, self.D = P, N, D
         self.max_steps = max_steps
-        self.counter0 = (1 << 41) + (int(pop.eval_rounds) << 24) + (k << 20)
+        self.counter0s = [(1 << 41) + (int(p.eval_rounds) << 24) + (k << 20) for p in pops]
+        self.counter0 = self.counter0s[0]
+        capable = population_eval_ok(self.runners, paced=False)
+        self.multi = bool(allow_persistent and capable and population_eval_ok(self.runners))
+        if len(self.runners) > 1 and not self.multi:
+            raise ValueError("several groups evaluate together only in the population-wide launch")
         self.desc = pop.fused_descriptor()
         self.gdesc = pop.learn_descriptor() if self.desc is None else None
-        self.persistent = bool(allow_persistent and ((runner.persistent and self.desc is not None) or
-                                                     (runner.graph_persistent and self.gdesc is not None)))
+        # the evaluation layer list wherever the multi form can run, per-step
+        # launches included: persistent and per-step passes then sample alike
+        self.edescs = _eval_nets(self.runners)[1] if capable else None
+        self.persistent = bool(self.multi or (allow_persistent and (
+            (runner.persistent and self.desc is not None) or (runner.graph_persistent and self.gdesc is not None))))
         self.step = 0
         self.scores = np.zeros(P * N)
         self.completed = np.zeros(P * N)
         self.finished = np.zeros(P * N, dtype=bool)
         self.n_finished = 0
+        lib = _lib.load()
         if self.persistent:
-            st = runner._eval_staging()
-            self.obs_h, self.rew_h, self.done_h, self.act_h, self.ctl_h, self.args_h = st
+            st = staging if staging is not None else runner._eval_staging()
+            self.obs_h, self.rew_h, self.done_h, self.act_h, self.ctl_h, self.args_h = st[:6]
             self.launched_to = 0  # steps covered by launches so far (0: no launch resident)
             # per-step host work kept to the env step: numpy views of the staging
             # and the control-block entry points, taken once
             self._views = (self.obs_h.numpy(), self.rew_h.numpy(), self.done_h.numpy(), self.act_h.numpy())
-            lib = _lib.load()
             self._signal, self._wait_fn, self._ctl = lib.agx_host_signal, lib.agx_host_wait, self.ctl_h.data_ptr()
+            if self.multi:
+                self.n_wg = int(lib.agx_ppo_rollout_graph_workgroups(P, N))
+                nets = _eval_nets(self.runners)
+                self._nets = nets[0]
+                self._params = (ctypes.c_void_p * P)(*[r.pop.params.data[a].data_ptr()
+                                                       for r in self.runners for a in range(r.pop.P)])
+                self._env_base = (ctypes.c_int64 * P)(*[int(i) * N for r in self.runners for i in r.pop.agent_ids])
+                self._seeds = (ctypes.c_uint64 * P)(*[r.pop.act_seed for r in self.runners for _ in range(r.pop.P)])
+                self._ctr0 = [c for r, c in zip(self.runners, self.counter0s) for _ in range(r.pop.P)]
+                nb = int(lib.agx_ppo_eval_multi_bytes(P))
+                self._agents_h = st[6] if len(st) > 6 else _coherent(self, nb)
+                self._agents_d = torch.empty(nb, dtype=torch.uint8, device=pop.device)  # before any launch
+            else:
+                self.n_wg = runner.n_wg
         else:
             self.act_d = torch.empty(P * N, dtype=torch.int64, device=pop.device)
             self.act_h = torch.empty(P * N, dtype=torch.int64, pin_memory=True)
             self.obs_h = torch.empty(P * N * D, dtype=pop.obs.dtype, pin_memory=True)
             self.obs_d = torch.empty(P, N, D, dtype=pop.obs.dtype, device=pop.device)
             self.ev = torch.cuda.Event()
-        if self.gdesc is not None:  # its scratch now: nothing may allocate while a persistent launch waits
+        if self.edescs is not None and not self.multi:  # per-step launches of the evaluation layer list
+            from .learner import graph_act_workspace
+
+            graph_act_workspace(self.pop, self.edescs[0])
+        elif self.gdesc is not None:  # its scratch now: nothing may allocate while a persistent launch waits
             from .learner import graph_act_workspace
 
             graph_act_workspace(self.pop, self.gdesc)
@@ -553,7 +638,15 @@ class _EvalDriver:
         pop = self.pop
         n = _EVAL_CHUNK if self.max_steps is None else min(_EVAL_CHUNK, int(self.max_steps) - self.step)
         self.ctl_h.zero_()
-        if self.desc is not None:
+        if self.multi:  # every agent of every group on its own network
+            ctr = (ctypes.c_uint64 * self.P)(*[c + self.step for c in self._ctr0])
+            _lib.check(lib.agx_ppo_eval_multi_persistent(self._nets, self._params, self._env_base, self._seeds, ctr,
+                                                         self.P, self.N, self.obs_h.data_ptr(), self.act_h.data_ptr(),
+                                                         n, 0, self._agents_h.data_ptr(), self._agents_d.data_ptr(),
+                                                         self.ctl_h.data_ptr(), self.runner.timeout_s,
+                                                         self.stream.cuda_stream),
+                       "agx_ppo_eval_multi_persistent")
+        elif self.desc is not None:
             _lib.check(lib.agx_ppo_eval_persistent(ctypes.byref(self.desc), self.P, self.N,
                                                    pop.params.data.data_ptr(), self.obs_h.data_ptr(), None,
                                                    self.act_h.data_ptr(), pop.env_base_d.data_ptr(), n, 0, pop.act_seed,
@@ -591,7 +684,12 @@ class _EvalDriver:
         self.obs_h.numpy()[:] = np.asarray(self.obs).reshape(-1)
         self.obs_d.view(-1).copy_(self.obs_h, non_blocking=True)
         counter = self.counter0 + self.step
-        if self.desc is not None:
+        if self.edescs is not None:  # the evaluation layer list (as the multi launch samples)
+            from .learner import policy_step_graph
+
+            policy_step_graph(pop, self.edescs[0], self.obs_d, N * D, sample=True, counter=counter,
+                              out_agent_stride=N, actions_flat=self.act_d)
+        elif self.desc is not None:
             from .learner import policy_step
 
             policy_step(pop, self.desc, self.obs_d, N * D, sample=True, counter=counter, out_agent_stride=N,
@@ -609,15 +707,16 @@ class _EvalDriver:
     def wait(self) -> None:
         if self.persistent:
             t = self.step - self.launch_step0 + 1
-            rc = self._wait_fn(self._ctl, self.runner.n_wg, t, self.runner.timeout_s)
+            rc = self._wait_fn(self._ctl, self.n_wg, t, self.runner.timeout_s)
             if rc != 0:
                 msg = _lib.load().agx_last_error().decode(errors="replace")
                 words = self.ctl_h.view(torch.int32)
-                done = words[4:4 + self.runner.n_wg].tolist()
-                state = (f"{'graph' if self.desc is None else 'compiled'} group P={self.P} N={self.N}: step "
+                done = words[4:4 + self.n_wg].tolist()
+                kind = "population" if self.multi else ("graph" if self.desc is None else "compiled")
+                state = (f"{kind} pass P={self.P} N={self.N}: step "
                          f"{self.step} (launch from {self.launch_step0} to {self.launched_to}), waiting for "
                          f"{t}; control block seq {int(words[0])} timeout {int(words[1])} nwg {int(words[2])} "
-                         f"(runner {self.runner.n_wg}); done words {done}")
+                         f"(driver {self.n_wg}); done words {done}")
                 self.abort()
                 raise _lib.AgxError(f"agx_host_wait failed ({rc}): {msg}; evaluation {state}")
             return

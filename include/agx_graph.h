@@ -95,6 +95,30 @@ int agx_ppo_eval_graph_persistent(const agx_ppo_graph *net, int64_t P, int64_t N
                                   uint64_t counter0, void *args_host, agx_rollout_ctl *ctl, double timeout_s,
                                   void *workspace, void *stream);
 
+/* Evaluation pass of a WHOLE population in ONE persistent launch (replaces
+ * the per-agent agent.test loop of train_on_policy.py:363-373 and PPO.test,
+ * ppo.py:1113-1289, for every group of a population at once): agent p of P
+ * runs its own network nets[p] (any MLP actor-critic, compiled shapes
+ * included; one obs_dim / n_actions for all) on its parameter row params[p]
+ * over envs [p N, (p + 1) N) of the packed host staging (stage_obs [P N][D],
+ * actions_flat [P N], coherent host memory), sampled from its own Philox
+ * stream: seed seeds[p], env env_base[p] + n, counter counters[p] + t at step
+ * t.  Host-paced like agx_ppo_eval_graph_persistent (control block of
+ * agx_ppo_rollout_graph_ctl_bytes(P, N) bytes, release word t + 1 + base,
+ * AGX_ROLLOUT_STOP ends it early).  agents_host / agents_dev:
+ * agx_ppo_eval_multi_bytes(P) bytes of coherent host memory / device memory
+ * for the per-agent plans (copied on `stream` before the launch).
+ * agx_ppo_eval_multi_supported: 1 when every network's policy-step tiles fit
+ * in LDS and the P x ceil(N / 16) workgroups can all be resident (else the
+ * groups' own passes run: agx_ppo_eval_persistent / _graph_persistent). */
+size_t agx_ppo_eval_multi_bytes(int64_t P);
+int agx_ppo_eval_multi_supported(const agx_ppo_graph *const *nets, int64_t P, int64_t N);
+int agx_ppo_eval_multi_persistent(const agx_ppo_graph *const *nets, const float *const *params,
+                                  const int64_t *env_base, const uint64_t *seeds, const uint64_t *counters, int64_t P,
+                                  int64_t N, const float *stage_obs, int64_t *actions_flat, int64_t nsteps,
+                                  uint32_t base, void *agents_host, void *agents_dev, agx_rollout_ctl *ctl,
+                                  double timeout_s, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

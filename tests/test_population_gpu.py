@@ -669,6 +669,55 @@ def test_engine_evaluates_groups_like_their_runners(monkeypatch):
     assert fit == alone
 
 
+def test_engine_evaluates_mixed_shapes_in_one_launch(monkeypatch):
+    """Groups of different networks (the compiled shape and an architecture-
+    mutated one): the engine evaluates all agents in ONE persistent launch
+    (agx_ppo_eval_multi_persistent, each agent on its own network) with the
+    fitness of each group's own pass, and that pass equals one policy-step
+    launch per vector step of the evaluation layer list."""
+    from agilerl_amd.envs import StackedVecEnv, SyntheticVecEnv
+    from agilerl_amd.population.engine import PopulationEngine
+    from agilerl_amd.population.nets import ActorCriticSpec
+    from agilerl_amd.population.runner import population_eval_ok
+
+    P, N = 4, 32
+    pop, _ = _runner_pair(monkeypatch, True, P=P, N=N)
+    envs = [SyntheticVecEnv(N, seed=30 + j, p_done=0.08, max_episode_steps=40) for j in range(P)]
+    views = [type("V", (), {"learn_step": pop.T * pop.N})() for _ in range(P)]
+    eng = PopulationEngine(pop, views, StackedVecEnv(envs))
+    states = eng.local_states()
+    mut = ActorCriticSpec(obs_dim=8, n_actions=4, encoder_hidden=[80], latent_dim=56, actor_hidden=[64, 64])
+    g = torch.Generator(device=DEV).manual_seed(4)
+    for j in (1, 3):
+        st = states[j]
+        st.spec = mut
+        st.params = 0.1 * torch.randn(mut.n_params, device=DEV, generator=g)
+        st.exp_avg = torch.zeros(mut.n_params, device=DEV)
+        st.exp_avg_sq = torch.zeros(mut.n_params, device=DEV)
+    eng.regroup(states)
+    assert len(eng.groups) == 2
+    runners = [gr.runner for gr in eng.groups]
+    assert population_eval_ok(runners)
+    fit = eng.evaluate(1, None)
+    assert all(np.isfinite(fit))
+    eng._eval_calls -= 1
+    alone = [0.0] * P
+    for gr in eng.groups:
+        gr.pop.eval_rounds = eng._eval_calls
+        f = gr.runner.evaluate(loop=1, max_steps=None)
+        for r, slot in enumerate(gr.slots):
+            alone[slot] = float(f[r])
+    assert fit == alone
+    # one group's pass, persistent vs one launch per step
+    gr = eng.groups[1]
+    persistent = gr.runner.evaluate(loop=1, max_steps=None)
+    monkeypatch.setattr(gr.runner, "persistent", False)
+    monkeypatch.setattr(gr.runner, "graph_persistent", False)
+    gr.pop.eval_rounds -= 1
+    stepped = gr.runner.evaluate(loop=1, max_steps=None)
+    np.testing.assert_array_equal(persistent, stepped)
+
+
 @pytest.mark.parametrize("evaluate", [False, True])
 def test_graph_persistent_rollout_matches_per_step_launches(monkeypatch, evaluate):
     """A mutated (runtime-shape) network: ONE persistent launch per rollout
