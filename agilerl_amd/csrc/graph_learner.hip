@@ -155,7 +155,7 @@ constexpr int kGemmLds = 2 * kPanel;        // double-buffered
 // kBN wide: the epilogue runs S's ReLU / LayerNorm(+affine) backward on the
 // whole rows of dY it holds and writes S's dZ (dzr_s / dzc_s) and per-wave
 // bias / LN-affine column partials (colp_s): S needs no row pass of its own.
-template <int MODE = 0, bool DIRECT = false, class FE>
+template <int MODE = 0, class FE>
 __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B, int ldb, int M, int N, int K,
                                         float *lds, const float *bias, FE epi, const GLay &L,
                                         float *base = nullptr, const float *pr = nullptr, int bp = 0,
@@ -222,36 +222,6 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 const float v = bias ? bias[nb + (ok ? n0 + r : 0)] : 0.f;
                 bv_[j] = v;
             }
-            if constexpr (DIRECT) {
-                // the partnered learner's few-row minibatch slices: every wave loads
-                // its tiles' operands straight from L2 (operand rows other waves
-                // also read are L1 hits) — no LDS staging and no barriers: one round
-                // trip per 32-deep chunk instead of a staged pipeline per block
-                for (int kc = 0; kc < K; kc += kKC) {
-#pragma unroll
-                    for (int j = 0; j < kTPW; ++j) {
-                        int m0, n0;
-                        if (tile(j, m0, n0)) {  // wave-uniform
-                            float av[8], bv[8];
-                            const int m = m0 + r, n = n0 + r;
-#pragma unroll
-                            for (int kk = 0; kk < 8; ++kk) {
-                                const int k = kc + 4 * kk + q;
-                                const int kq = k < K ? k : 0;
-                                const float xa = Ab[(size_t)(m < BM ? m : 0) * lda + kq];
-                                const float xb = Bb[(size_t)(n < BN ? n : 0) * ldb + kq];
-                                av[kk] = (k < K && m < BM) ? xa : 0.f;
-                                bv[kk] = (k < K && n < BN) ? xb : 0.f;
-                            }
-#pragma unroll
-                            for (int kk = 0; kk < 8; ++kk) {
-                                if (kc + 4 * kk >= K) break;  // uniform: a short last chunk
-                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc[j], 0, 0, 0);
-                            }
-                        }
-                    }
-                }
-            } else {
             fetch(0);
             if (mb | nb) __syncthreads();  // the previous block's last panels may still be read
             commit(0);
@@ -284,7 +254,6 @@ __device__ __forceinline__ void gemm_nt(const float *A, int lda, const float *B,
                 }
                 buf ^= 1;
             }
-            }  // staged
             if constexpr (LNE) {
                 const float invF = 1.f / (float)N;
                 // the LN affine of the lane's four columns, loaded before any store
@@ -724,7 +693,6 @@ __device__ __forceinline__ void bwd_rows(const GLay &L, float *base, const float
 // keeping xhat / rstd / the feature-major copy where the plan has room for
 // them (the learner; the policy step keeps outputs only).  xobs: the
 // observation rows (stride = the first layer's fin).
-template <bool DIRECT = false>
 __device__ __forceinline__ void forward_layers(const GLay *Ls, int nl, const float *xobs, int bsz, float *base, const float *pr,
                                int bp, float *lds, int dbg = 0, long long *st = nullptr) {
     for (int l = 0; l < nl; ++l) {
@@ -736,10 +704,10 @@ __device__ __forceinline__ void forward_layers(const GLay *Ls, int nl, const flo
         const bool lne = F <= kBN && (L.ln || L.relu);  // LayerNorm / ReLU in the GEMM epilogue
         if (!(dbg & 1)) {
             if (lne)
-                gemm_nt<1, DIRECT>(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
+                gemm_nt<1>(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
                                    [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; }, L, base, pr, bp);
             else
-                gemm_nt<0, DIRECT>(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
+                gemm_nt<0>(x, L.fin, pr + L.w, L.fin, bsz, F, L.fin, lds, bias,
                                    [&](int m, int n, float c) { yr[(size_t)m * F + n] = c; }, L);
         }
         __syncthreads();
@@ -762,7 +730,6 @@ __device__ __forceinline__ void forward_layers(const GLay *Ls, int nl, const flo
 // it).  base: this workgroup's activation scratch; wb: where the transposed
 // weights live (wb + L.wt).  Shared by the one-workgroup-per-agent learner and
 // the partnered one (each partner over its slice of the rows).
-template <bool DIRECT = false>
 __device__ __forceinline__ void minibatch_grads(const GArgs &g, float *base, const float *wb, const float *pr, float *G,
                                                 const float *xobs, const int *gact_e, const unsigned *gmask_e,
                                                 const float *grow_e, long long s0, int bsz, float inv_b, float entp,
@@ -781,7 +748,7 @@ __device__ __forceinline__ void minibatch_grads(const GArgs &g, float *base, con
 
     // ---- forward, layer by layer ------------------------------------
     if (st) st[0] = (long long)__builtin_readcyclecounter();
-    forward_layers<DIRECT>(g.L, g.nl, xobs, bsz, base, pr, bp, lds, g.dbg, st);
+    forward_layers(g.L, g.nl, xobs, bsz, base, pr, bp, lds, g.dbg, st);
 
     // ---- loss row pass: logits / value -> d(logits), d(value) (ppo.py:876-908)
     if (!(g.dbg & 8)) {
@@ -985,11 +952,11 @@ __device__ __forceinline__ void minibatch_grads(const GArgs &g, float *base, con
             float *dst = job ? base + (L.acc ? g.L[L.src].dy2 : g.L[L.src].dy) : G + L.w;
             if (job && L.fuse) {  // the source's dZ (other parity) from the epilogue
                 const int s_ = L.src;
-                gemm_nt<2, DIRECT>(ga, lda, gb, ldb, M, fin, K, lds, nullptr, [](int, int, float) {}, g.L[s_], base, pr,
+                gemm_nt<2>(ga, lda, gb, ldb, M, fin, K, lds, nullptr, [](int, int, float) {}, g.L[s_], base, pr,
                            bp, base + ((s_ & 1) ? g.dzr1 : g.dzr), base + ((s_ & 1) ? g.dzc1 : g.dzc),
                            colp + (s_ & 1) * 3 * kGW * 128);
             } else {
-                gemm_nt<0, DIRECT>(ga, lda, gb, ldb, M, fin, K, lds, nullptr,
+                gemm_nt<0>(ga, lda, gb, ldb, M, fin, K, lds, nullptr,
                                    [&](int m, int n, float c) { dst[(size_t)m * fin + n] = c; }, L);
             }
         }
@@ -1195,12 +1162,6 @@ __device__ __forceinline__ void gpart_acquire() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 }
-
-// the partner's few-row GEMMs with operands loaded straight from L2 (1) or
-// staged through LDS (0, measured faster: r5 graph_stamps)
-#ifndef AGX_GRAPH_DIRECT
-#define AGX_GRAPH_DIRECT 0
-#endif
 
 // inner stamps of minibatch_grads: [0] forward start, [1 + l] layer l's forward
 // done, [17] loss pass done, [18 + 3l] / [19 + 3l] / [20 + 3l] layer l's row pass,
@@ -1651,7 +1612,7 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
                     few_grads(g, base, pr, wb, G, gobs_e + (s0 + r0) * D, gact_e, gmask_e, grow_e, s0 + r0, rk, inv_b,
                               entp, lsum, klsum, stamp ? s_st + 16 : nullptr);
                 else
-                    minibatch_grads<AGX_GRAPH_DIRECT>(g, base, wb, pr, G, gobs_e + (s0 + r0) * D, gact_e, gmask_e,
+                    minibatch_grads(g, base, wb, pr, G, gobs_e + (s0 + r0) * D, gact_e, gmask_e,
                                                       grow_e, s0 + r0, rk, inv_b, entp, lds, colp, colo, lsum, klsum,
                                                       stamp ? s_st + 16 : nullptr);
             } else {  // no rows this minibatch (a short last minibatch): publish zeros
@@ -1720,7 +1681,8 @@ __global__ __launch_bounds__(kGT) void ppo_learn_graph_part_kernel(const GArgs g
                     for (int h = 0; h < 2; ++h) {
                         const int c = cb + h * kGT;
                         if (c >= own1) break;
-                        if (!regs) *reinterpret_cast<f4 *>(sum + 4 * c) = t[h];
+                        // (the loss / approx_kl chunk n4 always: every partner reads it after barrier 2)
+                        if (!regs || c >= n4) *reinterpret_cast<f4 *>(sum + 4 * c) = t[h];
 #pragma unroll
                         for (int cc = 0; cc < 4; ++cc) {
                             const int f = 4 * c + cc;

@@ -68,12 +68,14 @@ class AgentState:
                           self.ent_coef)
 
 
-def export_state(pop: PPOPopulation, row: int, learn_step: int) -> AgentState:
+def export_state(pop: PPOPopulation, row: int, learn_step: int, steps: list | None = None) -> AgentState:
+    """``steps``: the population's Adam step counts read once (host list) by
+    a caller exporting several rows; else this row's is read (a device sync)."""
     n = pop.spec.n_params
     return AgentState(copy.deepcopy(pop.spec), int(learn_step), pop.params.data[row, :n].clone(),
                       pop.opt.exp_avg[row, :n].clone(), pop.opt.exp_avg_sq[row, :n].clone(),
-                      int(pop.opt.steps[row]), float(pop.agent_lr[row]), int(pop.agent_batch[row]),
-                      int(pop.agent_epochs[row]), float(pop.agent_ent[row]))
+                      int(steps[row] if steps is not None else pop.opt.steps[row]), float(pop.agent_lr[row]),
+                      int(pop.agent_batch[row]), int(pop.agent_epochs[row]), float(pop.agent_ent[row]))
 
 
 class _Group:
@@ -374,6 +376,7 @@ class PopulationEngine:
     # ------------------------------------------------------------------ #
     def local_states(self) -> list[AgentState]:
         out = []
+        steps = {}  # each group's Adam step counts: one device read per group
         for j in range(self.P):
             v = self.views[j]
             pending = getattr(v, "_pending_state", None)
@@ -381,7 +384,10 @@ class PopulationEngine:
                 out.append(pending)
                 continue
             g, r = self.group_of(j)
-            out.append(export_state(g.pop, r, getattr(v, "_pending_learn_step", None) or g.learn_step))
+            if id(g) not in steps:
+                steps[id(g)] = g.pop.opt.steps.tolist()
+            out.append(export_state(g.pop, r, getattr(v, "_pending_learn_step", None) or g.learn_step,
+                                    steps[id(g)]))
         return out
 
     def clone_states(self, parents: list[int], records: list[dict]) -> list[AgentState]:
@@ -452,7 +458,7 @@ class PopulationEngine:
                                 update_epochs=max(s.update_epochs for s in st), target_kl=t.target_kl,
                                 device=self.device, fused=t.fused, perm_source=t.perm_source,
                                 action_masks=t.use_action_masks, global_pop_size=t.global_P, seed_base=t.seed_base,
-                                agent_ids=[self.rank * self.P + j for j in slots])
+                                agent_ids=[self.rank * self.P + j for j in slots], init_params=False)
             n = spec.n_params
             with torch.no_grad():
                 for r, s in enumerate(st):

@@ -71,7 +71,7 @@ class PPOPopulation:
                  batch_size=128, lr=1e-3, gamma=0.99, gae_lambda=0.95, clip_coef=0.2, ent_coef=0.01,
                  vf_coef=0.5, max_grad_norm=0.5, update_epochs=4, target_kl=None, seeds=None,
                  device="cuda", fused=True, perm_source="numpy", action_masks=False, agent_offset=0,
-                 global_pop_size=None, seed_base=None, agent_ids=None):
+                 global_pop_size=None, seed_base=None, agent_ids=None, init_params=True):
         self.spec = spec
         self.P, self.N = int(pop_size), int(num_envs)
         # a shard of a population spread over ranks: these P agents are global
@@ -103,7 +103,10 @@ class PPOPopulation:
         # population-level streams key off the global population's first seed
         seed_base = int(seeds[0]) if seed_base is None else int(seed_base)
         self.seed_base = seed_base
-        self.params = torch.nn.Parameter(spec.init_params(self.P, seeds, self.device))
+        # init_params=False: zeros, for a caller that copies every row in (the
+        # population engine's regrouping; the orthogonal init is a host QR per layer)
+        self.params = torch.nn.Parameter(spec.init_params(self.P, seeds, self.device) if init_params else
+                                         torch.zeros(self.P, spec.n_params, dtype=torch.float32, device=self.device))
         self.params.grad = torch.zeros_like(self.params)
         lr_list = [float(lr)] * self.P if not isinstance(lr, (list, tuple)) else [float(x) for x in lr]
         self.opt = K.ClipAdam(self.params.data, spec.group_offsets, lr_list, max_norm=self.max_grad_norm,
