@@ -49,6 +49,7 @@ SIGNATURES = {
     "agx_ppo_eval_graph_persistent": (_INT, [_P, _I, _I, _P, _P, _P, _P, _P, _I, ctypes.c_uint32, ctypes.c_uint64,
                                              ctypes.c_uint64, _P, _P, _D, _P, _P]),
     "agx_ppo_eval_multi_bytes": (_SZ, [_I]),
+    "agx_debug_eval_stamps": (_INT, [_P]),
     "agx_ppo_eval_multi_supported": (_INT, [_P, _I, _I]),
     "agx_ppo_eval_multi_persistent": (_INT, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _I, ctypes.c_uint32, _P, _P, _P,
                                              _D, _P]),
@@ -71,6 +72,8 @@ SIGNATURES = {
     "agx_stream_create": (_P, []),
     "agx_host_signal": (_INT, [_P, ctypes.c_uint32]),
     "agx_host_wait": (_INT, [_P, _I, ctypes.c_uint32, _D]),
+    "agx_host_signal_range": (_INT, [_P, _I, _I, ctypes.c_uint32]),
+    "agx_host_wait_range": (_INT, [_P, _I, _I, ctypes.c_uint32, _D]),
     "agx_per_workspace_bytes": (_SZ, [_I, _I]),
     "agx_per_init": (_INT, [_P, _P, _I, _P]),
     "agx_per_add": (_INT, [_P, _P, _I, _I, _I, _I, _D, _P, _P, _P]),

@@ -2109,7 +2109,7 @@ __global__ __launch_bounds__(kGT) void ppo_eval_multi_persistent_kernel(const Ev
                                                                         long long *act_flat, int nsteps,
                                                                         agx_rollout_ctl *ctl,
                                                                         unsigned long long timeout_ticks,
-                                                                        unsigned base_seq) {
+                                                                        unsigned base_seq, long long *stamps) {
     extern __shared__ __attribute__((aligned(16))) float gdyn[];
     __shared__ int s_go;
     const int tid = threadIdx.x;
@@ -2150,13 +2150,18 @@ __global__ __launch_bounds__(kGT) void ppo_eval_multi_persistent_kernel(const Ev
         }
         __syncthreads();
         if (!s_go) return;
+        const bool stamp = stamps && blk == 0 && tid == 0 && t >= 2 && t < 34;
+        long long *stp = stamp ? stamps + 4 * (t - 2) : nullptr;
+        if (stamp) stp[0] = (long long)__builtin_amdgcn_s_memrealtime();
         const float *ob = stage_obs + ((size_t)p * N + n0) * D;
         for (int i = tid; i < nrow * D; i += kGT) {
             const int b = i / D, d = i - b * D;
             gdyn[ag.oc + b * ag.ld0 + d] = ld_sys(ob + i);
         }
         __syncthreads();
+        if (stamp) stp[1] = (long long)__builtin_amdgcn_s_memrealtime();
         few_forward(ag.L, ag.nl, gdyn, pr, prs, ag.oc, ag.ld0, nullptr);
+        if (stamp) stp[2] = (long long)__builtin_amdgcn_s_memrealtime();
         GSample sp{A, N, 1, La.ld, Lc.ld, ag.seed, ag.counter0 + (unsigned long long)t, nullptr, nullptr, 0,
                    nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, act_flat, ag.env_base};
         graph_sample<true>(sp, gdyn + La.yr, gdyn + Lc.yr, p, n0, nrow);
@@ -2166,6 +2171,7 @@ __global__ __launch_bounds__(kGT) void ppo_eval_multi_persistent_kernel(const Ev
         if (tid == 0)
             __hip_atomic_store(rollout_done_words(ctl) + blk, base_seq + (unsigned)(t + 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
+        if (stamp) stp[3] = (long long)__builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -2852,6 +2858,18 @@ extern "C" int agx_ppo_eval_graph_persistent(const agx_ppo_graph *net, int64_t P
 // ---------------------------------------------------------------------------
 // evaluation of a whole population, every agent on its own network
 // ---------------------------------------------------------------------------
+static long long *&g_eval_stamps() {
+    static long long *p = nullptr;
+    return p;
+}
+// diagnostic: block 0's stamps of steps 2..33 of agx_ppo_eval_multi_persistent
+// (s_memrealtime, 100 MHz): release seen, observations staged, forward done,
+// done word written; int64[128], or null to stop
+extern "C" int agx_debug_eval_stamps(int64_t *buf) {
+    g_eval_stamps() = reinterpret_cast<long long *>(buf);
+    return AGX_OK;
+}
+
 extern "C" size_t agx_ppo_eval_multi_bytes(int64_t P) { return P > 0 ? (size_t)P * sizeof(EvalAgent) : 0; }
 
 namespace {
@@ -2931,6 +2949,6 @@ extern "C" int agx_ppo_eval_multi_persistent(const agx_ppo_graph *const *nets, c
     ppo_eval_multi_persistent_kernel<<<grid, kGT, dyn, s>>>(static_cast<const EvalAgent *>(agents_dev), (int)N,
                                                             nets[0]->n_actions, nets[0]->obs_dim, stage_obs,
                                                             reinterpret_cast<long long *>(actions_flat), (int)nsteps,
-                                                            ctl, ticks, base);
+                                                            ctl, ticks, base, g_eval_stamps());
     return check_launch("agx_ppo_eval_multi_persistent");
 }

@@ -132,6 +132,39 @@ extern "C" int agx_host_signal(agx_rollout_ctl *ctl, uint32_t seq) {
     return AGX_OK;
 }
 
+extern "C" int agx_host_signal_range(agx_rollout_ctl *ctl, int64_t w0, int64_t w1, uint32_t seq) {
+    AGX_REQUIRE(ctl, "agx_host_signal_range: null ctl");
+    const unsigned nwg = __atomic_load_n(&ctl->nwg, __ATOMIC_RELAXED);
+    AGX_REQUIRE(w0 >= 0 && w0 <= w1 && w1 <= (int64_t)nwg, "agx_host_signal_range: [%lld, %lld) outside %u",
+                (long long)w0, (long long)w1, nwg);
+    for (int64_t w = w0; w < w1; ++w)
+        __atomic_store_n(agx::rollout_release_word(ctl, nwg, (unsigned)w), seq, __ATOMIC_RELEASE);
+    return AGX_OK;
+}
+
+extern "C" int agx_host_wait_range(const agx_rollout_ctl *ctl, int64_t w0, int64_t w1, uint32_t target,
+                                   double timeout_s) {
+    AGX_REQUIRE(ctl && w0 >= 0 && w0 < w1, "agx_host_wait_range: bad arguments");
+    const uint32_t *done = agx::rollout_done_words(const_cast<agx_rollout_ctl *>(ctl));
+    const auto t0 = std::chrono::steady_clock::now();
+    int64_t i = w0;
+    for (unsigned spin = 0;; ++spin) {
+        while (i < w1 && __atomic_load_n(done + i, __ATOMIC_ACQUIRE) >= target) ++i;
+        if (i == w1) return AGX_OK;
+        if (__atomic_load_n(&ctl->timeout, __ATOMIC_RELAXED)) {
+            agx::set_error("agx_host_wait_range: a workgroup timed out waiting for the host");
+            return AGX_EHIP;
+        }
+        if ((spin & 1023) == 1023 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+            agx::set_error("agx_host_wait_range: %lld of [%lld, %lld) not done after %.1f s", (long long)(w1 - i),
+                           (long long)w0, (long long)w1, timeout_s);
+            return AGX_EHIP;
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 extern "C" int agx_host_wait(const agx_rollout_ctl *ctl, int64_t nwg, uint32_t target, double timeout_s) {
     AGX_REQUIRE(ctl && nwg > 0, "agx_host_wait: bad arguments");
     const uint32_t *done = agx::rollout_done_words(const_cast<agx_rollout_ctl *>(ctl));

@@ -62,8 +62,10 @@ class AgentState:
     update_epochs: int
     ent_coef: float
 
+    # A network spec is never changed in place (an architecture mutation makes a
+    # new one: population/arch.py, image_arch.py), so states share it.
     def clone(self) -> "AgentState":
-        return AgentState(copy.deepcopy(self.spec), self.learn_step, self.params.clone(), self.exp_avg.clone(),
+        return AgentState(self.spec, self.learn_step, self.params.clone(), self.exp_avg.clone(),
                           self.exp_avg_sq.clone(), self.step, self.lr, self.batch_size, self.update_epochs,
                           self.ent_coef)
 
@@ -72,7 +74,7 @@ def export_state(pop: PPOPopulation, row: int, learn_step: int, steps: list | No
     """``steps``: the population's Adam step counts read once (host list) by
     a caller exporting several rows; else this row's is read (a device sync)."""
     n = pop.spec.n_params
-    return AgentState(copy.deepcopy(pop.spec), int(learn_step), pop.params.data[row, :n].clone(),
+    return AgentState(pop.spec, int(learn_step), pop.params.data[row, :n].clone(),
                       pop.opt.exp_avg[row, :n].clone(), pop.opt.exp_avg_sq[row, :n].clone(),
                       int(steps[row] if steps is not None else pop.opt.steps[row]), float(pop.agent_lr[row]),
                       int(pop.agent_batch[row]), int(pop.agent_epochs[row]), float(pop.agent_ent[row]))
@@ -319,7 +321,10 @@ class PopulationEngine:
                 staging = self._eval_staging(sum(g.pop.P for g in self.groups))
             for k in range(loop):
                 d = _EvalDriver(runners[0], k, max_steps, runners=runners, env=env, staging=staging)
-                run_lockstep([d])
+                if d.can_pipeline():
+                    d.run_pipelined()
+                else:
+                    run_lockstep([d])
                 res, off = d.result(), 0
                 for g in self.groups:
                     acc[id(g)] += res[off:off + g.pop.P]

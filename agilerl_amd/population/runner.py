@@ -423,7 +423,10 @@ class PopulationRunner:
         out = np.zeros((loop, pop.P))
         for k in range(loop):
             d = _EvalDriver(self, k, max_steps)
-            run_lockstep([d])
+            if d.can_pipeline():
+                d.run_pipelined()
+            else:
+                run_lockstep([d])
             out[k] = d.result()
         self.after_evaluation()
         return out.mean(0)
@@ -768,6 +771,83 @@ class _EvalDriver:
 
     def result(self) -> np.ndarray:
         return self.completed.reshape(self.P, self.N).mean(1)
+
+    # -- the pass in two halves ---------------------------------------------
+    def can_pipeline(self) -> bool:
+        """A population-wide launch over a stack of one env per agent can
+        run in two halves (AGX_EVAL_PIPELINE=0 turns it off)."""
+        from ..envs import StackedVecEnv
+
+        return bool(self.multi and self.P >= 2 and isinstance(self.env, StackedVecEnv) and
+                    len(self.env.envs) == self.P and all(int(e.num_envs) == self.N for e in self.env.envs) and
+                    os.environ.get("AGX_EVAL_PIPELINE", "1") != "0")
+
+    def _half_env_step(self, h: int) -> None:
+        lo, hi = self._halves[h]
+        obs_n, rew_n, done_n, act_n = self._views
+        try:
+            _, _, term, trunc, _ = self._half_envs[h].step(act_n[lo:hi], out_obs=obs_n[lo:hi],
+                                                           out_rew=rew_n[lo:hi], out_done=done_n[lo:hi])
+        except BaseException:
+            self.abort()
+            raise
+        sc, fin = self.scores[lo:hi], self.finished[lo:hi]
+        sc += rew_n[lo:hi]
+        done = np.asarray(term, dtype=bool).reshape(-1)
+        if trunc is not None:
+            done = done | np.asarray(trunc, dtype=bool).reshape(-1)
+        if self.max_steps is not None and self.step + 1 == self.max_steps:
+            done = np.ones(hi - lo, dtype=bool)
+        new = done & ~fin
+        if new.any():
+            self.completed[lo:hi][new] = sc[new]
+            fin |= new
+            self.n_finished = int(self.finished.sum())
+
+    def run_pipelined(self) -> None:
+        """The whole pass with the agents in two halves, one half a step ahead:
+        while one half's workgroups compute their policy step, the host steps
+        the other half's envs (agx_host_signal_range / agx_host_wait_range).
+        Same launch, counters, releases and samples as the lock-step loop
+        (run_lockstep); the device latency hides behind half of the env work."""
+        from ..envs import StackedVecEnv
+
+        lib = _lib.load()
+        P, N = self.P, self.N
+        pa = P // 2
+        gx = self.n_wg // P
+        self._halves = [(0, pa * N), (pa * N, P * N)]
+        blocks = [(0, pa * gx), (pa * gx, P * gx)]
+        self._half_envs = [StackedVecEnv(self.env.envs[:pa]), StackedVecEnv(self.env.envs[pa:])]
+        sig, wait = lib.agx_host_signal_range, lib.agx_host_wait_range
+        self.stream = _eval_stream(0)
+        self.begin()
+        try:
+            while True:
+                if self.step >= self.launched_to:
+                    if self.launched_to > 0:  # the previous launch ran all its steps and ends by itself
+                        self._drain()
+                    self._launch()
+                    for w0, w1 in blocks:
+                        sig(self._ctl, w0, w1, 1)
+                rel = self.step - self.launch_step0 + 1
+                for h in (0, 1):
+                    rc = wait(self._ctl, blocks[h][0], blocks[h][1], rel, self.runner.timeout_s)
+                    if rc != 0:
+                        msg = lib.agx_last_error().decode(errors="replace")
+                        self.abort()
+                        raise _lib.AgxError(f"agx_host_wait_range failed ({rc}): {msg}; evaluation half {h} of "
+                                            f"P={P} N={N} at step {self.step}")
+                    self._half_env_step(h)
+                    if self.step + 1 < self.launched_to:  # this half's next step, before the other half waits
+                        sig(self._ctl, blocks[h][0], blocks[h][1], rel + 1)
+                self.step += 1
+                if self.n_finished == P * N or (self.max_steps is not None and self.step >= self.max_steps):
+                    break
+            self.end()
+        except BaseException:
+            self.abort()
+            raise
 
 
 AGX_ROLLOUT_STOP = 0xFFFFFFFE  # include/agx.h

@@ -330,6 +330,11 @@ int agx_host_signal(agx_rollout_ctl *ctl, uint32_t seq);
 /* spin until every done word >= target; AGX_EHIP on ctl->timeout or after
  * timeout_s */
 int agx_host_wait(const agx_rollout_ctl *ctl, int64_t nwg, uint32_t target, double timeout_s);
+/* the same for workgroups [w0, w1) only (ctl->seq untouched): a host that
+ * paces two halves of a launch, stepping one half's envs while the other
+ * half's workgroups run */
+int agx_host_signal_range(agx_rollout_ctl *ctl, int64_t w0, int64_t w1, uint32_t seq);
+int agx_host_wait_range(const agx_rollout_ctl *ctl, int64_t w0, int64_t w1, uint32_t target, double timeout_s);
 
 /* ---- prioritized replay segment trees -----------------------------------
  * Replaces SumSegmentTree / MinSegmentTree (agilerl/components/

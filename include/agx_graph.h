@@ -112,6 +112,11 @@ int agx_ppo_eval_graph_persistent(const agx_ppo_graph *net, int64_t P, int64_t N
  * in LDS and the P x ceil(N / 16) workgroups can all be resident (else the
  * groups' own passes run: agx_ppo_eval_persistent / _graph_persistent). */
 size_t agx_ppo_eval_multi_bytes(int64_t P);
+/* diagnostic: workgroup 0's stamps of steps 2..33 of the next
+ * agx_ppo_eval_multi_persistent launches into buf (int64[128], s_memrealtime
+ * ticks of 10 ns: release seen, observations staged, forward done, done word
+ * written per step); null stops. */
+int agx_debug_eval_stamps(int64_t *buf);
 int agx_ppo_eval_multi_supported(const agx_ppo_graph *const *nets, int64_t P, int64_t N);
 int agx_ppo_eval_multi_persistent(const agx_ppo_graph *const *nets, const float *const *params,
                                   const int64_t *env_base, const uint64_t *seeds, const uint64_t *counters, int64_t P,
