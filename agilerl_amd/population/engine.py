@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import copy
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -221,11 +222,11 @@ class PopulationEngine:
         per-iteration mean losses (host arrays, group by group, slot order
         where known).
 
-        The groups' iterations interleave, each group on a stream of its own:
-        iteration i of every group, then iteration i + 1, ...  A group's
-        learner (enqueued behind its rollout) then runs on the device while the
-        host paces the NEXT group's rollout, and the groups' learners overlap
-        one another.  At most one persistent launch is ever paced, and the
+        The groups' iterations interleave, each group on a stream of its own
+        (the host paces next the group with the most iterations left among
+        those whose learner has finished): a group's learner (enqueued behind
+        its rollout) runs on the device while the host paces ANOTHER group's
+        rollout, and the groups' learners overlap one another.  At most one persistent launch is ever paced, and the
         host waits only for the launch it paces (the other streams hold finite
         kernels), so no hardware-queue ordering can stall it.  No host sync
         inside the loop: errors and losses are read once every group's
@@ -241,25 +242,47 @@ class PopulationEngine:
             g.pop.act_counter = base
             iters.append(self.iterations(evo_steps, g.learn_step))
             pending.append([])
-        streams = [self._train_stream(k) for k in range(len(self.groups))] if main is not None else None
+        streams = [_train_stream(k) for k in range(len(self.groups))] if main is not None else None
         if streams is not None:
-            for st in streams:  # parameters / buffers written by selection, mutation, regrouping
+            for st in set(streams):  # parameters / buffers written by selection, mutation, regrouping
                 st.wait_stream(main)
+        # which group's next iteration the host paces: among the groups whose
+        # previous learner has finished (its event), the one with the most
+        # iterations left — the longest chain first; if none has finished, the
+        # one with the most left anyway (its rollout starts when its learner
+        # ends).  Each group's own iterations keep their order.
+        left = list(iters)
+        done_ev = [None] * len(self.groups)
+        if streams is not None and len(self.groups) > 1 and self._paced_together():
+            try:
+                self._train_paced_together(left, streams, pending, on_iteration)
+            finally:
+                for st in set(streams):
+                    main.wait_stream(st)
+            losses = []
+            for k, g in enumerate(self.groups):
+                g.pop.check_errors()
+                losses += [x.cpu().numpy() for x in pending[k]]
+            return losses
         try:
-            for i in range(max(iters, default=0)):
-                for k, g in enumerate(self.groups):
-                    if i >= iters[k]:
-                        continue
-                    if streams is not None:
-                        with torch.cuda.stream(streams[k]):
-                            pending[k].append(g.runner.iteration().clone())
-                    else:
+            while any(left):
+                cands = [k for k in range(len(self.groups)) if left[k]]
+                ready = [k for k in cands if done_ev[k] is None or done_ev[k].query()]
+                k = max(ready or cands, key=lambda c: (left[c], -c))
+                g = self.groups[k]
+                if streams is not None:
+                    with torch.cuda.stream(streams[k]):
                         pending[k].append(g.runner.iteration().clone())
-                    if on_iteration is not None:
-                        on_iteration(g)
+                        done_ev[k] = torch.cuda.Event()
+                        done_ev[k].record()
+                else:
+                    pending[k].append(g.runner.iteration().clone())
+                left[k] -= 1
+                if on_iteration is not None:
+                    on_iteration(g)
         finally:
             if streams is not None:
-                for st in streams:
+                for st in set(streams):
                     main.wait_stream(st)
         losses = []
         for k, g in enumerate(self.groups):
@@ -267,18 +290,88 @@ class PopulationEngine:
             losses += [x.cpu().numpy() for x in pending[k]]
         return losses
 
-    def _train_stream(self, k: int):
-        """Group k's training stream: a non-blocking stream of its own
-        (agx_stream_create), made once per engine."""
-        from .. import _lib
 
-        pool = self.__dict__.setdefault("_train_streams", [])
-        while len(pool) <= k:
-            h = _lib.load().agx_stream_create()
-            if not h:
-                raise _lib.AgxError(_lib.load().agx_last_error().decode(errors="replace"))
-            pool.append(torch.cuda.ExternalStream(h, device=self.device))
-        return pool[k]
+    def _paced_together(self) -> bool:
+        """Every group runs the pipelined persistent iteration (a device-free
+        env and a HIP policy step), so their rollouts can be paced together
+        (AGX_TRAIN_TOGETHER=0 turns it off)."""
+        if os.environ.get("AGX_TRAIN_TOGETHER", "1") == "0":
+            return False
+        # target-KL learns: drawing the next shuffles waits for a learner's epochs
+        # run (a device sync), which must not happen while launches are resident
+        return all(((g.runner.persistent and g.pop.fused_descriptor() is not None) or g.runner.graph_persistent)
+                   and g.pop.target_kl is None for g in self.groups)
+
+    def _train_paced_together(self, left: list, streams: list, pending: list, on_iteration) -> None:
+        """The groups' iterations with their rollouts paced TOGETHER: each
+        round of the loop releases the next step of every running rollout
+        (each group's persistent launch computes its policy step meanwhile),
+        then waits for each in turn and steps its envs; a group whose rollout
+        has ended starts its next iteration at once (rollout + GAE + learner
+        enqueued on its stream; the launch starts when its learner is done).
+
+        Only launches seen running (agx_rollout_ctl.started) are paced, and the
+        host never waits for one that is not: a launch queued in a hardware
+        queue behind another group's resident launch (a process has few, see
+        GPU_MAX_HW_QUEUES) starts once that one ends, so the loop cannot stall.
+        Each group's env steps, releases and launches are those of its own
+        iteration() loop, in order."""
+        G = len(self.groups)
+        ctx = [None] * G
+        running = [False] * G
+        # first-use work (learner workspaces, pinned staging, the act workspace of
+        # a runtime shape) while no launch is resident: a fresh group (after a
+        # regroup) runs its first iteration alone, the others get their learner
+        # and staging ready; nothing in the loop below may then wait for the device
+        for k, g in enumerate(self.groups):
+            with torch.cuda.stream(streams[k]):
+                if not getattr(g.runner, "_paced_before", False):
+                    if left[k]:
+                        pending[k].append(g.runner.iteration().clone())
+                        left[k] -= 1
+                        if on_iteration is not None:
+                            on_iteration(g)
+                    g.runner._paced_before = True
+                g.pop.prepare_learn()
+        try:
+            while True:
+                for k in range(G):
+                    if ctx[k] is None and left[k]:
+                        with torch.cuda.stream(streams[k]):
+                            ctx[k] = self.groups[k].runner.begin_iteration()
+                        running[k] = False
+                        left[k] -= 1
+                live = [k for k in range(G) if ctx[k] is not None]
+                if not live:
+                    return
+                for k in live:
+                    if not running[k]:
+                        running[k] = self.groups[k].runner.launch_running()
+                go = [k for k in live if running[k]]
+                if not go:
+                    continue  # every launch still waits for its learner (or queue): poll again
+                for k in go:
+                    self.groups[k].runner.pace_release(ctx[k])
+                for k in go:
+                    g = self.groups[k]
+                    g.runner.pace_wait_step(ctx[k])
+                    if ctx[k].t == g.pop.T:
+                        with torch.cuda.stream(streams[k]):
+                            pending[k].append(g.runner.end_iteration(ctx[k]).clone())
+                        ctx[k] = None
+                        if on_iteration is not None:
+                            on_iteration(g)
+        except BaseException:
+            # every launch released with the abort word first (one queued behind
+            # another's would otherwise keep that one waiting), then each drained
+            for k in range(G):
+                if ctx[k] is not None:
+                    ctx[k].lib.agx_host_signal(ctx[k].ctl, 0xFFFFFFFF)
+            for k in range(G):
+                if ctx[k] is not None:
+                    with torch.cuda.stream(streams[k]):
+                        self.groups[k].runner.abort_iteration(ctx[k])
+            raise
 
     def steps_per_generation(self, slot: int, evo_steps: int) -> int:
         g, _ = self.group_of(slot)
@@ -492,3 +585,25 @@ class PopulationEngine:
     def pending(self) -> bool:
         return any(getattr(v, "_pending_state", None) is not None or getattr(v, "_pending_learn_step", None)
                    for v in self.views)
+
+
+
+# The groups' training streams: non-blocking streams (agx_stream_create) made
+# once per process, as many as the process has hardware queues
+# (GPU_MAX_HW_QUEUES, 4 by default): streams are given hardware queues in
+# turn, so consecutive groups land on different queues and a group's rollout
+# does not wait in a queue behind another group's learner.  Group k trains on
+# stream k mod that count.
+_TRAIN_STREAMS: list = []
+
+
+def _train_stream(k: int):
+    from .. import _lib
+
+    n = max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
+    while len(_TRAIN_STREAMS) < n:
+        h = _lib.load().agx_stream_create()
+        if not h:
+            raise _lib.AgxError(_lib.load().agx_last_error().decode(errors="replace"))
+        _TRAIN_STREAMS.append(torch.cuda.ExternalStream(h))
+    return _TRAIN_STREAMS[k % n]

@@ -190,6 +190,7 @@ class PopulationRunner:
         self.episodes_env = torch.zeros(P * N, dtype=torch.int64, device=dev)
         self._ios = None
         self._np = None
+        self._ctl_words = None
         self.stats_event = None
 
     def _ctl_bytes(self) -> int:
@@ -476,12 +477,33 @@ class PopulationRunner:
         timeout word set in the control block; the queued learner reads that
         word first (``skip_if_set``) and returns without touching parameters
         or Adam state, and the exception propagates."""
+        c = self.begin_iteration()
+        try:
+            while c.t < self.pop.T:
+                self.pace_release(c)
+                self.pace_wait_step(c)
+        except BaseException:
+            self.abort_iteration(c)
+            raise
+        return self.end_iteration(c)
+
+    # -- an iteration in parts: a host pacing several groups' rollouts at once
+    # (PopulationEngine.train) interleaves their pace_release / pace_wait_step
+    def begin_iteration(self) -> "_IterCtx":
+        """Everything of the pipelined iteration but the pacing: the persistent
+        rollout launch (its control block's ``started`` word cleared first), the
+        last_done copy, GAE and the learner, enqueued on the current stream.
+        Nothing here waits for the device."""
+        desc = self.pop.fused_descriptor()
         if self._ios is None:
             self._build_ios()
         if not self.started:
             self.env.reset(out_obs=self.obs_h.numpy())
             self.started = True
         self.pop.prepare_learn()  # nothing between the launch and the pacing may wait for the device
+        if self._ctl_words is None:
+            self._ctl_words = self.ctl_h.numpy().view(np.uint32)
+        self._ctl_words[3] = 0  # agx_rollout_ctl.started
         _pacing_begin()
         try:
             lib, ctl, base = self._launch_persistent(desc)
@@ -491,12 +513,55 @@ class PopulationRunner:
             # set by an aborted (host exception) or timed-out rollout, so the
             # partial rollout never updates the parameters or Adam state
             loss = self.pop.learn(prefetch=False, skip_if_set=ctl + 4)
-            self._pace_persistent(lib, ctl, base)
+        except BaseException:
+            _pacing_end()
+            raise
+        return _IterCtx(lib, ctl, base, loss)
+
+    def launch_running(self) -> bool:
+        """The current persistent rollout launch has started on the device."""
+        return bool(self._ctl_words[3])
+
+    def pace_release(self, c: "_IterCtx") -> None:
+        c.lib.agx_host_signal(c.ctl, c.base + c.t + 1)
+
+    def pace_wait_step(self, c: "_IterCtx") -> None:
+        """Wait for released step c.t, step the env; after the last step the
+        release of the final obs / bootstrap value."""
+        _lib.check(c.lib.agx_host_wait(c.ctl, self.n_wg, c.base + c.t + 1, self.timeout_s), "agx_host_wait")
+        self._env_step()
+        c.t += 1
+        if c.t == self.pop.T:
+            c.lib.agx_host_signal(c.ctl, c.base + self.pop.T + 1)  # reward/done of step T-1, final obs, bootstrap value
+
+    def abort_iteration(self, c: "_IterCtx") -> None:
+        """Release the workgroups with the abort word (the queued learner then
+        skips), wait for the stream, reset the control block."""
+        try:
+            c.lib.agx_host_signal(c.ctl, 0xFFFFFFFF)
+            torch.cuda.current_stream().synchronize()
+            self.ctl_h.zero_()
+            self.seq_base = 0
         finally:
             _pacing_end()
+
+    def end_iteration(self, c: "_IterCtx") -> torch.Tensor:
+        self.pop.act_counter += self.pop.T
+        self.env_steps += self.pop.P * self.pop.N * self.pop.T
+        _pacing_end()
         if self.pop.prefetch_perms:  # next learn's minibatch orders: host work while the GPU learns
             self.pop.prefetch_permutations()
-        return loss
+        return c.loss
+
+
+class _IterCtx:
+    """An enqueued pipelined iteration being paced: its control block, release
+    base, the learner's loss tensor and the next step to release."""
+
+    __slots__ = ("lib", "ctl", "base", "loss", "t")
+
+    def __init__(self, lib, ctl, base, loss):
+        self.lib, self.ctl, self.base, self.loss, self.t = lib, ctl, base, loss, 0
 
 
 # ---------------------------------------------------------------------- #

@@ -669,6 +669,52 @@ def test_engine_evaluates_groups_like_their_runners(monkeypatch):
     assert fit == alone
 
 
+@pytest.mark.parametrize("mixed", [False, True])
+def test_groups_paced_together_train_like_one_after_another(monkeypatch, mixed):
+    """Groups of one population (a learn_step split; with ``mixed`` also an
+    architecture-mutated network) trained with their rollouts paced together
+    (PopulationEngine._train_paced_together) end with the parameters, Adam
+    state and losses of the groups trained one iteration after another."""
+    from agilerl_amd.envs import StackedVecEnv, SyntheticVecEnv
+    from agilerl_amd.population.engine import PopulationEngine
+    from agilerl_amd.population.nets import ActorCriticSpec
+
+    out = []
+    for together in ("1", "0"):
+        monkeypatch.setenv("AGX_TRAIN_TOGETHER", together)
+        P, N = 4, 32
+        pop, _ = _runner_pair(monkeypatch, True, P=P, N=N)
+        envs = [SyntheticVecEnv(N, seed=50 + j, p_done=0.05, max_episode_steps=30) for j in range(P)]
+        views = [type("V", (), {"learn_step": pop.T * pop.N})() for _ in range(P)]
+        eng = PopulationEngine(pop, views, StackedVecEnv(envs))
+        states = eng.local_states()
+        states[1].learn_step = states[1].learn_step // 2
+        states[3].learn_step = states[3].learn_step // 2
+        if mixed:
+            mut = ActorCriticSpec(obs_dim=8, n_actions=4, encoder_hidden=[80], latent_dim=56, actor_hidden=[64, 64])
+            g = torch.Generator(device=DEV).manual_seed(9)
+            for j in (2, 3):
+                st = states[j]
+                st.spec = mut
+                st.params = 0.1 * torch.randn(mut.n_params, device=DEV, generator=g)
+                st.exp_avg = torch.zeros(mut.n_params, device=DEV)
+                st.exp_avg_sq = torch.zeros(mut.n_params, device=DEV)
+        eng.regroup(states)
+        assert len(eng.groups) == (4 if mixed else 2)
+        losses = []
+        for _ in range(2):
+            losses += eng.train(4 * pop.T * pop.N)
+        torch.cuda.synchronize()
+        st = eng.local_states()
+        out.append(([s.params.cpu() for s in st], [s.exp_avg.cpu() for s in st], [s.step for s in st],
+                    [np.asarray(x) for x in losses]))
+    (pa, ma, sa, la), (pb, mb, sb, lb) = out
+    assert sa == sb
+    for x, y in zip(pa + ma, pb + mb):
+        assert torch.equal(x, y)
+    assert len(la) == len(lb) and all(np.array_equal(x, y) for x, y in zip(la, lb))
+
+
 def test_engine_evaluates_mixed_shapes_in_one_launch(monkeypatch):
     """Groups of different networks (the compiled shape and an architecture-
     mutated one): the engine evaluates all agents in ONE persistent launch
