@@ -160,6 +160,7 @@ class PPOPopulation:
         # a generation's shuffles drawn ahead by the population engine, agent by
         # agent (set_generation_perms): [K, E, P, S], learn k reads row k
         self._gen_block = None
+        self._gen_block_d = None
         self._gen_k = 0
         self._gen_ran: list[torch.Tensor] = []
 
@@ -513,8 +514,13 @@ class PPOPopulation:
             self._perm_next = None
             self._perm_drawn_state = state
             main = torch.cuda.current_stream(self.device)
-            main.wait_event(ev)
-            perms.record_stream(main)
+            if ev is not None:
+                main.wait_event(ev)
+            perms.record_stream(main)  # (a block row: the block stays allocated until this stream is past it)
+            return perms
+        if self.perm_source == "numpy" and self._gen_block_d is not None:
+            perms = self._next_block_row()
+            perms.record_stream(torch.cuda.current_stream(self.device))
             return perms
         if self.perm_source == "numpy":
             host = self._host_perm_buffer()
@@ -539,6 +545,18 @@ class PPOPopulation:
                 raise ValueError(f"generation shuffles {block.shape}, expected [K, {self.update_epochs}, {self.P}, "
                                  f"{self.S}]")
         self._gen_block, self._gen_k, self._gen_ran = block, 0, []
+        # the whole block in HBM once (one copy at the generation's start, before
+        # any launch): each learn then takes its row without host work
+        self._gen_block_d = (torch.from_numpy(block).to(self.device)
+                             if block is not None and self.device.type == "cuda" else None)
+
+    def _next_block_row(self) -> torch.Tensor:
+        """The next learn's [E, P, S] row of the generation block in HBM."""
+        if self._gen_k >= self._gen_block.shape[0]:
+            raise RuntimeError("more learns than the generation's shuffles were drawn for")
+        row = self._gen_block_d[self._gen_k]
+        self._gen_k += 1
+        return row
 
     def _fill_numpy_perms(self, out: np.ndarray):
         """The next learn's [E, P, S] numpy-stream permutations into ``out``;
@@ -624,6 +642,9 @@ class PPOPopulation:
         side = self._perm_stream
         state = None
         from_block = False
+        if self.perm_source == "numpy" and self._gen_block_d is not None:
+            self._perm_next = (self._next_block_row(), None, None, True)
+            return
         if self.perm_source == "numpy":
             # waits for a target-KL learn's epochs_run (before any rollout launch)
             from_block = self._gen_block is not None

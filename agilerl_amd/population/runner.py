@@ -848,42 +848,48 @@ class _EvalDriver:
                     os.environ.get("AGX_EVAL_PIPELINE", "1") != "0")
 
     def _half_env_step(self, h: int) -> None:
-        lo, hi = self._halves[h]
-        obs_n, rew_n, done_n, act_n = self._views
+        """One part's env step and episode tally, on views of the staging and
+        of the tallies made once per pass (run_pipelined)."""
+        obs, rew, done_st, act, sc, fin, comp, buf = self._part_views[h]
         try:
-            _, _, term, trunc, _ = self._half_envs[h].step(act_n[lo:hi], out_obs=obs_n[lo:hi],
-                                                           out_rew=rew_n[lo:hi], out_done=done_n[lo:hi])
+            _, _, term, trunc, _ = self._half_envs[h].step(act, out_obs=obs, out_rew=rew, out_done=done_st)
         except BaseException:
             self.abort()
             raise
-        sc, fin = self.scores[lo:hi], self.finished[lo:hi]
-        sc += rew_n[lo:hi]
-        done = np.asarray(term, dtype=bool).reshape(-1)
-        if trunc is not None:
-            done = done | np.asarray(trunc, dtype=bool).reshape(-1)
+        sc += rew
         if self.max_steps is not None and self.step + 1 == self.max_steps:
-            done = np.ones(hi - lo, dtype=bool)
-        new = done & ~fin
-        if new.any():
-            self.completed[lo:hi][new] = sc[new]
-            fin |= new
+            buf[:] = True
+        elif trunc is not None:
+            np.logical_or(term, trunc, out=buf)
+        else:
+            np.copyto(buf, term)
+        np.logical_and(buf, ~fin, out=buf)
+        if buf.any():
+            comp[buf] = sc[buf]
+            fin |= buf
             self.n_finished = int(self.finished.sum())
 
     def run_pipelined(self) -> None:
-        """The whole pass with the agents in two halves, one half a step ahead:
-        while one half's workgroups compute their policy step, the host steps
-        the other half's envs (agx_host_signal_range / agx_host_wait_range).
-        Same launch, counters, releases and samples as the lock-step loop
-        (run_lockstep); the device latency hides behind half of the env work."""
+        """The whole pass with the agents in n parts (AGX_EVAL_PARTS, default
+        2: more parts cost more host work than they hide, r5 tools/gpu_eval_parts.sh), each a step ahead of the next: while
+        one part's workgroups compute their policy step, the host steps the
+        other parts' envs (agx_host_signal_range / agx_host_wait_range).  Same
+        launch, counters, releases and samples as the lock-step loop
+        (run_lockstep); the device latency hides behind the other parts' env
+        work."""
         from ..envs import StackedVecEnv
 
         lib = _lib.load()
         P, N = self.P, self.N
-        pa = P // 2
+        n = max(2, min(P, int(os.environ.get("AGX_EVAL_PARTS", "2"))))
         gx = self.n_wg // P
-        self._halves = [(0, pa * N), (pa * N, P * N)]
-        blocks = [(0, pa * gx), (pa * gx, P * gx)]
-        self._half_envs = [StackedVecEnv(self.env.envs[:pa]), StackedVecEnv(self.env.envs[pa:])]
+        cut = [round(i * P / n) for i in range(n + 1)]
+        self._halves = [(cut[i] * N, cut[i + 1] * N) for i in range(n)]
+        blocks = [(cut[i] * gx, cut[i + 1] * gx) for i in range(n)]
+        self._half_envs = [StackedVecEnv(self.env.envs[cut[i]:cut[i + 1]]) for i in range(n)]
+        obs_n, rew_n, done_n, act_n = self._views
+        self._part_views = [(obs_n[a:b], rew_n[a:b], done_n[a:b], act_n[a:b], self.scores[a:b], self.finished[a:b],
+                             self.completed[a:b], np.zeros(b - a, dtype=bool)) for a, b in self._halves]
         sig, wait = lib.agx_host_signal_range, lib.agx_host_wait_range
         self.stream = _eval_stream(0)
         self.begin()
@@ -896,15 +902,15 @@ class _EvalDriver:
                     for w0, w1 in blocks:
                         sig(self._ctl, w0, w1, 1)
                 rel = self.step - self.launch_step0 + 1
-                for h in (0, 1):
+                for h in range(n):
                     rc = wait(self._ctl, blocks[h][0], blocks[h][1], rel, self.runner.timeout_s)
                     if rc != 0:
                         msg = lib.agx_last_error().decode(errors="replace")
                         self.abort()
-                        raise _lib.AgxError(f"agx_host_wait_range failed ({rc}): {msg}; evaluation half {h} of "
-                                            f"P={P} N={N} at step {self.step}")
+                        raise _lib.AgxError(f"agx_host_wait_range failed ({rc}): {msg}; evaluation part {h} of "
+                                            f"{n}, P={P} N={N} at step {self.step}")
                     self._half_env_step(h)
-                    if self.step + 1 < self.launched_to:  # this half's next step, before the other half waits
+                    if self.step + 1 < self.launched_to:  # this part's next step, before the next part waits
                         sig(self._ctl, blocks[h][0], blocks[h][1], rel + 1)
                 self.step += 1
                 if self.n_finished == P * N or (self.max_steps is not None and self.step >= self.max_steps):
