@@ -52,7 +52,7 @@ SIGNATURES = {
     "agx_debug_eval_stamps": (_INT, [_P]),
     "agx_ppo_eval_multi_supported": (_INT, [_P, _I, _I]),
     "agx_ppo_eval_multi_persistent": (_INT, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _I, ctypes.c_uint32, _P, _P, _P,
-                                             _D, _P]),
+                                             _D, _P, _P]),
     "agx_ppo_act_graph": (_INT, [_P, _I, _I, _P, _P, _I, _P, _I, _INT, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P,
                                  _P, _I, _P, _P, _P, _P]),
     "agx_ppo_learn": (_INT, [_P, _P, _P, _P]),

@@ -2106,12 +2106,27 @@ struct EvalAgent {
     unsigned long long seed, counter0;
 };
 
+// The episode tally of an evaluation pass on the device (agx_eval_tally):
+// at each step the previous env step's reward / done from the host staging
+// into the env's running score (f64, as the reference's numpy tally), its
+// first finished episode's score, and each workgroup's count of finished envs
+// for the host's end-of-pass test.
+struct EvalTally {
+    const float *rew;
+    const unsigned char *done;
+    double *scores, *completed;
+    unsigned char *finished;
+    unsigned *fin_words;
+    int prev;  // the staging holds a reward / done when the launch starts
+};
+
 __global__ __launch_bounds__(kGT) void ppo_eval_multi_persistent_kernel(const EvalAgent *__restrict__ agents, int N,
                                                                         int A, int D, const float *stage_obs,
                                                                         long long *act_flat, int nsteps,
                                                                         agx_rollout_ctl *ctl,
                                                                         unsigned long long timeout_ticks,
-                                                                        unsigned base_seq, long long *stamps) {
+                                                                        unsigned base_seq, long long *stamps,
+                                                                        const EvalTally tally) {
     extern __shared__ __attribute__((aligned(16))) float gdyn[];
     __shared__ int s_go;
     const int tid = threadIdx.x;
@@ -2159,6 +2174,24 @@ __global__ __launch_bounds__(kGT) void ppo_eval_multi_persistent_kernel(const Ev
         for (int i = tid; i < nrow * D; i += kGT) {
             const int b = i / D, d = i - b * D;
             gdyn[ag.oc + b * ag.ld0 + d] = ld_sys(ob + i);
+        }
+        if (tally.rew && (t > 0 || tally.prev) && tid < 64) {  // one wave: the block's <= 16 envs
+            int fin = 0;
+            if (tid < nrow) {
+                const size_t idx = (size_t)p * N + n0 + tid;
+                const float rw = ld_sys(tally.rew + idx);
+                const unsigned char dn = ld_sys_u8(tally.done + idx);
+                const double sc = tally.scores[idx] + (double)rw;
+                tally.scores[idx] = sc;
+                fin = tally.finished[idx];
+                if (dn && !fin) {
+                    tally.finished[idx] = 1;
+                    tally.completed[idx] = sc;
+                    fin = 1;
+                }
+            }
+            const unsigned cnt = (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(fin != 0));
+            if (tid == 0) __hip_atomic_store(tally.fin_words + blk, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
         if (stamp) stp[1] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -2918,7 +2951,8 @@ extern "C" int agx_ppo_eval_multi_persistent(const agx_ppo_graph *const *nets, c
                                              const int64_t *env_base, const uint64_t *seeds,
                                              const uint64_t *counters, int64_t P, int64_t N, const float *stage_obs,
                                              int64_t *actions_flat, int64_t nsteps, uint32_t base, void *agents_host,
-                                             void *agents_dev, agx_rollout_ctl *ctl, double timeout_s, void *stream) {
+                                             void *agents_dev, agx_rollout_ctl *ctl, double timeout_s,
+                                             const agx_eval_tally *tally, void *stream) {
     AGX_REQUIRE(nets && params && env_base && seeds && counters && stage_obs && actions_flat && agents_host &&
                     agents_dev && ctl && P > 0 && N > 0 && P <= 65535 && nsteps >= 1,
                 "agx_ppo_eval_multi_persistent: bad arguments");
@@ -2948,9 +2982,17 @@ extern "C" int agx_ppo_eval_multi_persistent(const agx_ppo_graph *const *nets, c
     const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
     ctl->nwg = (uint32_t)nwg;
     dim3 grid((unsigned)ceil_div(N, kFR), (unsigned)P);
+    EvalTally et{};
+    if (tally) {
+        AGX_REQUIRE(tally->stage_rew && tally->stage_done && tally->scores && tally->completed && tally->finished &&
+                        tally->fin_words,
+                    "agx_ppo_eval_multi_persistent: incomplete tally");
+        et = EvalTally{tally->stage_rew, tally->stage_done, tally->scores, tally->completed, tally->finished,
+                       tally->fin_words, tally->prev ? 1 : 0};
+    }
     ppo_eval_multi_persistent_kernel<<<grid, kGT, dyn, s>>>(static_cast<const EvalAgent *>(agents_dev), (int)N,
                                                             nets[0]->n_actions, nets[0]->obs_dim, stage_obs,
                                                             reinterpret_cast<long long *>(actions_flat), (int)nsteps,
-                                                            ctl, ticks, base, g_eval_stamps());
+                                                            ctl, ticks, base, g_eval_stamps(), et);
     return check_launch("agx_ppo_eval_multi_persistent");
 }

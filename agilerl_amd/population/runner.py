@@ -68,6 +68,14 @@ class AgxRolloutIO(ctypes.Structure):
     ]
 
 
+class AgxEvalTally(ctypes.Structure):
+    """Mirror of ``agx_eval_tally`` (include/agx_graph.h)."""
+
+    _fields_ = [("stage_rew", ctypes.c_void_p), ("stage_done", ctypes.c_void_p), ("scores", ctypes.c_void_p),
+                ("completed", ctypes.c_void_p), ("finished", ctypes.c_void_p), ("fin_words", ctypes.c_void_p),
+                ("prev", ctypes.c_int)]
+
+
 # hipHostFree waits for the whole device.  A persistent rollout of this
 # process waits for the host from its launch until the host's final release,
 # so a free in that window (a garbage-collected runner's buffers, finalised in
@@ -632,6 +640,7 @@ class _EvalDriver:
         self.counter0 = self.counter0s[0]
         capable = population_eval_ok(self.runners, paced=False)
         self.multi = bool(allow_persistent and capable and population_eval_ok(self.runners))
+        self.device_tally = False
         if len(self.runners) > 1 and not self.multi:
             raise ValueError("several groups evaluate together only in the population-wide launch")
         self.desc = pop.fused_descriptor()
@@ -667,6 +676,19 @@ class _EvalDriver:
                 nb = int(lib.agx_ppo_eval_multi_bytes(P))
                 self._agents_h = st[6] if len(st) > 6 else _coherent(self, nb)
                 self._agents_d = torch.empty(nb, dtype=torch.uint8, device=pop.device)  # before any launch
+                # the episode tally on the device (a pass to the end of every episode):
+                # the host then only sums the workgroups' finished counts
+                self.device_tally = max_steps is None and os.environ.get("AGX_EVAL_DEVICE_TALLY", "1") != "0"
+                if self.device_tally:
+                    dev = pop.device
+                    self._t_scores = torch.zeros(P * N, dtype=torch.float64, device=dev)
+                    self._t_completed = torch.zeros(P * N, dtype=torch.float64, device=dev)
+                    self._t_finished = torch.zeros(P * N, dtype=torch.uint8, device=dev)
+                    self._t_fin = _coherent(self, 4 * self.n_wg).view(torch.int32)
+                    self._t_fin_np = self._t_fin.numpy()
+                    self._tally = AgxEvalTally(self.rew_h.data_ptr(), self.done_h.data_ptr(),
+                                               self._t_scores.data_ptr(), self._t_completed.data_ptr(),
+                                               self._t_finished.data_ptr(), self._t_fin.data_ptr(), 0)
             else:
                 self.n_wg = runner.n_wg
         else:
@@ -685,6 +707,7 @@ class _EvalDriver:
             graph_act_workspace(self.pop, self.gdesc)
         self.obs = None
         self.stream = None  # a dedicated non-blocking stream, assigned by run_lockstep
+        self._pipelined = False
 
     # -- lock-step protocol -------------------------------------------------
     def begin(self) -> None:
@@ -708,10 +731,14 @@ class _EvalDriver:
         self.ctl_h.zero_()
         if self.multi:  # every agent of every group on its own network
             ctr = (ctypes.c_uint64 * self.P)(*[c + self.step for c in self._ctr0])
+            tally = None
+            if self.device_tally and self._pipelined:
+                self._tally.prev = 1 if self.step > 0 else 0
+                tally = ctypes.byref(self._tally)
             _lib.check(lib.agx_ppo_eval_multi_persistent(self._nets, self._params, self._env_base, self._seeds, ctr,
                                                          self.P, self.N, self.obs_h.data_ptr(), self.act_h.data_ptr(),
                                                          n, 0, self._agents_h.data_ptr(), self._agents_d.data_ptr(),
-                                                         self.ctl_h.data_ptr(), self.runner.timeout_s,
+                                                         self.ctl_h.data_ptr(), self.runner.timeout_s, tally,
                                                          self.stream.cuda_stream),
                        "agx_ppo_eval_multi_persistent")
         elif self.desc is not None:
@@ -856,6 +883,10 @@ class _EvalDriver:
         except BaseException:
             self.abort()
             raise
+        if self.device_tally:  # the launch tallies this step's reward / done at its next step
+            if trunc is not None and np.count_nonzero(trunc):
+                np.logical_or(done_st, trunc, out=done_st)  # done = term | trunc
+            return
         sc += rew
         if self.max_steps is not None and self.step + 1 == self.max_steps:
             buf[:] = True
@@ -892,6 +923,7 @@ class _EvalDriver:
                              self.completed[a:b], np.zeros(b - a, dtype=bool)) for a, b in self._halves]
         sig, wait = lib.agx_host_signal_range, lib.agx_host_wait_range
         self.stream = _eval_stream(0)
+        self._pipelined = True
         self.begin()
         try:
             while True:
@@ -913,12 +945,16 @@ class _EvalDriver:
                     if self.step + 1 < self.launched_to:  # this part's next step, before the next part waits
                         sig(self._ctl, blocks[h][0], blocks[h][1], rel + 1)
                 self.step += 1
+                if self.device_tally:  # the env steps before this one, tallied by the launch
+                    self.n_finished = int(self._t_fin_np.sum())
                 if self.n_finished == P * N or (self.max_steps is not None and self.step >= self.max_steps):
                     break
             self.end()
         except BaseException:
             self.abort()
             raise
+        if self.device_tally:
+            self.completed = self._t_completed.cpu().numpy()
 
 
 AGX_ROLLOUT_STOP = 0xFFFFFFFE  # include/agx.h

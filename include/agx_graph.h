@@ -111,6 +111,22 @@ int agx_ppo_eval_graph_persistent(const agx_ppo_graph *net, int64_t P, int64_t N
  * agx_ppo_eval_multi_supported: 1 when every network's policy-step tiles fit
  * in LDS and the P x ceil(N / 16) workgroups can all be resident (else the
  * groups' own passes run: agx_ppo_eval_persistent / _graph_persistent). */
+/* Optional episode tally of the pass on the device: at each step the
+ * previous env step's reward / done (host staging, P N each) go into the env's
+ * running score (f64, as the reference's numpy tally) and its first finished
+ * episode's score; each workgroup stores its count of finished envs into
+ * fin_words[w] (coherent host memory) before its done word, so the host ends
+ * the pass once they sum to P N (one step after the last episode ended).
+ * prev: the staging already holds a reward / done when the launch starts (a
+ * pass continued by a second launch). */
+typedef struct agx_eval_tally {
+    const float *stage_rew;
+    const uint8_t *stage_done;
+    double *scores, *completed; /* [P N] device, zeroed by the caller */
+    uint8_t *finished;          /* [P N] device, zeroed by the caller */
+    uint32_t *fin_words;        /* [workgroups] coherent host memory */
+    int prev;
+} agx_eval_tally;
 size_t agx_ppo_eval_multi_bytes(int64_t P);
 /* diagnostic: workgroup 0's stamps of steps 2..33 of the next
  * agx_ppo_eval_multi_persistent launches into buf (int64[128], s_memrealtime
@@ -122,7 +138,7 @@ int agx_ppo_eval_multi_persistent(const agx_ppo_graph *const *nets, const float 
                                   const int64_t *env_base, const uint64_t *seeds, const uint64_t *counters, int64_t P,
                                   int64_t N, const float *stage_obs, int64_t *actions_flat, int64_t nsteps,
                                   uint32_t base, void *agents_host, void *agents_dev, agx_rollout_ctl *ctl,
-                                  double timeout_s, void *stream);
+                                  double timeout_s, const agx_eval_tally *tally, void *stream);
 
 #ifdef __cplusplus
 }

@@ -743,7 +743,10 @@ def test_engine_evaluates_mixed_shapes_in_one_launch(monkeypatch):
     eng.regroup(states)
     assert len(eng.groups) == 2
     runners = [gr.runner for gr in eng.groups]
-    assert population_eval_ok(runners)
+    import os
+
+    # AGX_GRAPH_FEW=0 (the general form only): each group's own pass instead
+    assert population_eval_ok(runners) == (os.environ.get("AGX_GRAPH_FEW", "1") != "0")
     fit = eng.evaluate(1, None)
     assert all(np.isfinite(fit))
     eng._eval_calls -= 1
