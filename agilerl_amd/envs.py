@@ -358,11 +358,14 @@ class StackedVecEnv:
             e._len = lens[s:s + e.num_envs]
             views.append(e._len)
             s += e.num_envs
-        self._fz = ([e._obs for e in envs], obs, rew, term, views, lens, np.zeros(self.num_envs, dtype=bool))
+        # [6]: an upper bound of the episode lengths (while it stays below the
+        # time limit no env can be truncated and the step skips that test)
+        self._fz = ([e._obs for e in envs], obs, rew, term, views, lens, np.zeros(self.num_envs, dtype=bool),
+                    [int(lens.max()) if lens.size else 0])
         return True
 
     def _step_fused(self, out_obs, out_rew, out_done):
-        _, robs, rrew, rterm, _, lens, ztrunc = self._fz
+        _, robs, rrew, rterm, _, lens, ztrunc, lmax = self._fz
         e0 = self.envs[0]
         k = (e0._k + 1) % e0._ring
         for e in self.envs:
@@ -380,8 +383,14 @@ class StackedVecEnv:
         trunc = ztrunc
         if e0.max_episode_steps is not None:
             lens += 1
-            trunc = (lens >= e0.max_episode_steps) & ~term
-            lens[term | trunc] = 0
+            lmax[0] += 1
+            if lmax[0] < e0.max_episode_steps:  # no env can reach the limit: only episode ends reset
+                if term.any():
+                    lens[term] = 0
+            else:
+                trunc = (lens >= e0.max_episode_steps) & ~term
+                lens[term | trunc] = 0
+                lmax[0] = int(lens.max())
         return obs, rew, term, trunc, {}
 
     def step(self, actions, out_obs=None, out_rew=None, out_done=None):
