@@ -116,11 +116,13 @@ def _weight_groups(agent) -> list[dict[str, torch.Tensor]]:
     return []
 
 
-def host_record(agent) -> dict:
+def host_record(agent, adam_steps: dict | None = None) -> dict:
     """What another rank needs to replay this agent's mutation draws and to
     clone its host attributes: plain attributes, the hyperparameters the
     registry can mutate, the registry itself, the learning-rate names and the
-    shapes of the policy's weights."""
+    shapes of the policy's weights.  ``adam_steps``: id(population) -> its
+    Adam step counts on the host (one device read per population, not one
+    per agent)."""
     from .sharded import plain_attributes
 
     rec = plain_attributes(agent)
@@ -144,7 +146,8 @@ def host_record(agent) -> dict:
     rec["algo"] = getattr(agent, "algo", None)
     if hasattr(agent, "population"):  # a PPO view: what a clone of it on another rank is made of
         rec["_spec"] = agent.spec
-        rec["_adam_step"] = int(agent.population.opt.steps[agent.row])
+        steps = None if adam_steps is None else adam_steps.get(id(agent.population))
+        rec["_adam_step"] = int(agent.population.opt.steps[agent.row] if steps is None else steps[agent.row])
         rngs = [agent.module_rng, agent.critic_rng]
         if hasattr(agent, "kernel_rng"):  # image actor-critics also draw kernel sizes (image_arch.mutate)
             rngs += [agent.kernel_rng, agent.critic_kernel_rng]
@@ -238,7 +241,11 @@ class RemoteAgent:
 def gather_records(pop, group=None) -> list[dict]:
     """Every rank's agent records, in global agent order."""
     world, _ = world_rank(group)
-    local = [host_record(a) for a in pop]
+    adam_steps = {}
+    for a in pop:
+        if hasattr(getattr(a, "population", None), "opt") and id(a.population) not in adam_steps:
+            adam_steps[id(a.population)] = a.population.opt.steps.cpu().numpy()
+    local = [host_record(a, adam_steps) for a in pop]
     if world == 1:
         return local
     box: list = [None] * world

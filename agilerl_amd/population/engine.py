@@ -171,17 +171,24 @@ class PopulationEngine:
             K = self.iterations(evo_steps, g.learn_step)
             blocks[id(g)] = np.zeros((K, g.pop.update_epochs, g.pop.P, g.pop.S), dtype=np.int64)
         where = {self.rank * self.P + j: self.group_of(j) for j in range(self.P)}
-        scratch = {}
-        for gid, (S, E, ls) in enumerate(self.global_plan):
-            K = self.iterations(evo_steps, ls)
-            buf = scratch.get((E, S))
-            if buf is None:
-                buf = scratch[(E, S)] = np.empty((E, 1, S), dtype=np.int64)
-            for k in range(K):
-                numpy_shuffle_perms(1, E, S, out=buf)
-                if gid in where:
-                    g, r = where[gid]
-                    blocks[id(g)][k, :E, r] = buf[:, 0]
+        # consecutive global agents with the same (S, E, K) draw in one native
+        # call: agent after agent, learn after learn, each learn a fresh
+        # arange(S) shuffled E times -- the same order as one call per learn
+        plan = [(S, E, self.iterations(evo_steps, ls)) for S, E, ls in self.global_plan]
+        i = 0
+        while i < len(plan):
+            j = i + 1
+            while j < len(plan) and plan[j] == plan[i]:
+                j += 1
+            S, E, K = plan[i]
+            if K > 0:
+                buf = numpy_shuffle_perms((j - i) * K, E, S)  # [E, (j-i)*K, S]
+                for gid in range(i, j):
+                    if gid in where:
+                        g, r = where[gid]
+                        o = (gid - i) * K
+                        blocks[id(g)][:, :E, r] = buf[:, o:o + K].transpose(1, 0, 2)
+            i = j
         for g in self.groups:
             g.pop.set_generation_perms(blocks[id(g)])
 

@@ -122,3 +122,70 @@ def test_an_exception_releases_every_launch_before_draining():
     signalled = {e[1] for e in log[:first_abort] if e[0] == "signal" and e[2] == ABORT}
     assert signalled == {"a", "b", "c"}  # every in-flight launch, the unstarted one included
     assert all(r.aborted for r in runners)
+
+
+class _PermPop:
+    perm_source = "numpy"
+
+    def __init__(self, P, S, E):
+        self.P, self.S, self.update_epochs = P, S, E
+        self.block = None
+
+    def discard_prefetch(self):
+        pass
+
+    def set_generation_perms(self, block):
+        self.block = block
+
+
+class _PermGroup:
+    def __init__(self, slots, S, E, learn_step):
+        self.slots, self.learn_step = slots, learn_step
+        self.pop = _PermPop(len(slots), S, E)
+
+
+@pytest.mark.parametrize("rank", [0, 1])
+def test_generation_perms_follow_the_reference_shuffle_order(rank):
+    """draw_generation_perms batches consecutive same-shape agents into one
+    native draw; the rows must equal the reference's loop (global agent after
+    global agent, each learn a fresh arange(S) shuffled E times in place,
+    agilerl/algorithms/ppo.py:836-842) with the global stream left where that
+    loop leaves it."""
+    import numpy as np
+
+    # global plan over 2 ranks x 3 agents: (S, E, learn_step); a run of equal
+    # shapes crosses the rank boundary, one agent has a mutated learn_step
+    gplan = [(8, 2, 4), (8, 2, 4), (8, 2, 4), (8, 2, 4), (12, 3, 4), (4, 2, 2)]
+    evo = 8
+    eng = PopulationEngine.__new__(PopulationEngine)
+    eng.rank, eng.P, eng.world = rank, 3, 2
+    eng.global_plan = gplan
+    local = gplan[3 * rank:3 * rank + 3]
+    # groups: one per distinct shape on this rank, slots in order
+    groups = {}
+    for j, x in enumerate(local):
+        groups.setdefault(x, []).append(j)
+    eng.groups = [_PermGroup(slots, S, E, ls) for (S, E, ls), slots in groups.items()]
+    np.random.seed(99)
+    eng.draw_generation_perms(evo)
+    after = np.random.get_state(legacy=True)[2]
+
+    np.random.seed(99)
+    want = {}
+    for gid, (S, E, ls) in enumerate(gplan):
+        K = max(1, -(evo // -ls))
+        rows = []
+        for _ in range(K):
+            idx = np.arange(S)
+            learn = []
+            for _ in range(E):
+                np.random.shuffle(idx)
+                learn.append(idx.copy())
+            rows.append(learn)
+        want[gid] = rows
+    assert np.random.get_state(legacy=True)[2] == after
+    for g in eng.groups:
+        for r, slot in enumerate(g.slots):
+            for k, learn in enumerate(want[3 * rank + slot]):
+                for e, row in enumerate(learn):
+                    assert np.array_equal(g.pop.block[k, e, r], row)

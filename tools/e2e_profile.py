@@ -25,3 +25,10 @@ if __name__ == "__main__":
         s = io.StringIO()
         pstats.Stats(pr, stream=s).sort_stats(key).print_stats(45)
         print(s.getvalue())
+    s = io.StringIO()
+    st = pstats.Stats(pr, stream=s).sort_stats("tottime")
+    for pat in os.environ.get("CALLERS", "'sum' of|zeros_like|_generate|'item' of|_train_stream").split("|"):
+        st.print_callers(pat)
+    for pat in os.environ.get("CALLEES", "regroup|clone_states|gather_records|_clone_host_attributes|select").split("|"):
+        st.print_callees(pat)
+    print(s.getvalue())
