@@ -1240,6 +1240,43 @@ __device__ __forceinline__ void few_gemm(const float *X, int ldx, __amdgpu_buffe
     }
 }
 
+// few_gemm with W [16-rounded N][ldw] and the bias in LDS, zero padded to
+// whole 16 x 16 tiles (the evaluation pass's resident weights)
+template <class FE>
+__device__ __forceinline__ void few_gemm_l(const float *X, int ldx, const float *W, int ldw, int K, int N,
+                                           const float *bias, FE epi) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, q = lane >> 4;
+    const int nc = (K + 15) >> 4, ntile = (N + 15) >> 4;
+    const float *xr = X + r * ldx + 4 * q;
+    for (int t = wave; t < ntile; t += kGW) {
+        const int n0 = t << 4;
+        const float *wr = W + (n0 + r) * ldw + 4 * q;
+        const float bv = bias[n0 + r];
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int c0 = 0; c0 < nc; c0 += 4) {  // four chunks' reads in flight, then their MFMAs
+            f4 xv[4], wv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int c = c0 + u < nc ? c0 + u : nc - 1;
+                xv[u] = *reinterpret_cast<const f4 *>(xr + 16 * c);
+                wv[u] = *reinterpret_cast<const f4 *>(wr + 16 * c);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (c0 + u >= nc) break;  // uniform
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[u][j], wv[u][j], acc, 0, 0, 0);
+            }
+        }
+        if (n0 + r < N) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) epi(4 * q + j, n0 + r, acc[j] + bv);
+        }
+    }
+}
+
 // dW[o][i] = sum over the 16 rows of dZ[row][o] X[row][i] (o < F, i < fin)
 // straight into the gradient row Gw ([F][fin]); tiles round the waves
 __device__ __forceinline__ void few_dw(const float *dZ, int ldz, const float *X, int ldx, int F, int fin, float *Gw) {
@@ -1268,25 +1305,96 @@ __device__ __forceinline__ void few_dw(const float *dZ, int ldz, const float *X,
     }
 }
 
+// LayerNorm(+affine) / ReLU of one row in place (16 lanes per row, sub =
+// the lane's column phase), the row's values held in M registers per lane
+// (F <= 16 M): every LDS read issued before the first use, the same float
+// operations in the same order as the column loops
+constexpr int kRowRegs = 8;
+// the fields a row pass reads, loaded with the layer's other fields before its
+// GEMM (not re-read from the layer table after the barrier)
+struct LayRow {
+    int ln, relu;
+    long long af, rs, xh;
+};
+template <int M>
+__device__ __forceinline__ void few_row_pass(float *y, float *S, const LayRow &L, int F, int ld, int row, int sub) {
+    // whole 16-column chunks up to the 16-rounded width (a uniform bound: no
+    // per-lane branches); the padding columns read zero and are written zero,
+    // columns >= F enter no sum
+    const int mp = (F + 15) >> 4;
+    float v[M], ga[M], be[M];
+    bool ok[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int j = sub + 16 * i;
+        ok[i] = j < F;
+        v[i] = ga[i] = be[i] = 0.f;
+        if (i < mp) {
+            v[i] = y[j];
+            if (L.ln == 2) {
+                ga[i] = S[L.af + j];
+                be[i] = S[L.af + F + j];
+            }
+        }
+    }
+    float mean = 0.f, rstd = 1.f;
+    if (L.ln) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < M; ++i) s = ok[i] ? s + v[i] : s;
+        mean = rsum16(s) * (1.f / (float)F);
+        float vs = 0.f;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            const float d = v[i] - mean;
+            vs = ok[i] ? vs + d * d : vs;
+        }
+        rstd = 1.f / sqrtf(rsum16(vs) / (float)F + 1e-5f);
+        if (sub == 0 && L.rs >= 0) S[L.rs + row] = rstd;
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        if (i >= mp) break;  // uniform
+        const int j = sub + 16 * i;
+        float x = v[i];
+        if (L.ln) {
+            const float xh = (x - mean) * rstd;
+            if (L.xh >= 0) S[L.xh + row * ld + j] = ok[i] ? xh : 0.f;
+            x = L.ln == 2 ? xh * ga[i] + be[i] : xh;
+        }
+        if (L.relu) x = relu(x);
+        y[j] = ok[i] ? x : 0.f;
+    }
+}
+
 // Forward of the 16-row LDS tiles through the layer list: the few-row GEMM
 // (+ bias) into Y, then LayerNorm(+affine) / ReLU as a row pass in place,
 // keeping xhat / rstd where the plan has them (the learner; the policy step
 // keeps Y only).  The observation tile is at oc (row stride ld0).
+// WLDS: the weights are LDS-resident (layer l's W [16-rounded fout][ldw[l]]
+// at S + wl[l], zero padded, its bias after it; the evaluation pass copies
+// them once per launch); run: the layers to compute (bit l), the others are
+// skipped (the evaluation's forward needs the actor's path only).
+template <bool WLDS = false>
 __device__ __forceinline__ void few_forward(const GLay *Ls, int nl, float *S, const float *pr,
-                                            __amdgpu_buffer_rsrc_t prs, long long oc, int ld0, long long *st) {
+                                            __amdgpu_buffer_rsrc_t prs, long long oc, int ld0, long long *st,
+                                            unsigned run = ~0u, const long long *wl = nullptr,
+                                            const int *ldw = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int sub = lane & 15, rq = lane >> 4;
     const int row = 4 * wave + rq;
     for (int l = 0; l < nl; ++l) {
+        if (!((run >> l) & 1u)) continue;  // uniform
         const GLay &L = Ls[l];
         const int F = L.fout, ld = L.ld;
+        const LayRow lr{L.ln, L.relu, L.af, L.rs, L.xh};
         const float *X = L.src < 0 ? S + oc : S + Ls[L.src].yr;
         const int ldx = L.src < 0 ? ld0 : Ls[L.src].ld;
         float *Y = S + L.yr;
         // the LN affine for this update's row passes (forward and backward) to
         // LDS, its loads in flight under the GEMM
         float ga[2] = {0.f, 0.f}, be[2] = {0.f, 0.f};
-        if (L.ln == 2) {
+        if (!WLDS && L.ln == 2) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 if (tid + h * kGT < F) {
@@ -1294,8 +1402,14 @@ __device__ __forceinline__ void few_forward(const GLay *Ls, int nl, float *S, co
                     be[h] = pr[L.be + tid + h * kGT];
                 }
         }
-        few_gemm(X, ldx, prs, L.w * 4, L.fin, F, pr + L.b, [&](int m, int n, float v) { Y[m * ld + n] = v; });
-        if (L.ln == 2) {
+        if constexpr (WLDS) {
+            const float *W = S + wl[l];
+            few_gemm_l(X, ldx, W, ldw[l], L.fin, F, W + (long long)((F + 15) & ~15) * ldw[l],
+                       [&](int m, int n, float v) { Y[m * ld + n] = v; });
+        } else {
+            few_gemm(X, ldx, prs, L.w * 4, L.fin, F, pr + L.b, [&](int m, int n, float v) { Y[m * ld + n] = v; });
+        }
+        if (!WLDS && L.ln == 2) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 if (tid + h * kGT < F) {
@@ -1304,31 +1418,37 @@ __device__ __forceinline__ void few_forward(const GLay *Ls, int nl, float *S, co
                 }
         }
         __syncthreads();
-        if (L.ln || L.relu) {
-            const float invF = 1.f / (float)F;
+        if (lr.ln || lr.relu) {
             float *y = Y + row * ld;
-            float mean = 0.f, rstd = 1.f;
-            if (L.ln) {
-                float s = 0.f;
-                for (int j = sub; j < F; j += 16) s += y[j];
-                mean = rsum16(s) * invF;
-                float vs = 0.f;
-                for (int j = sub; j < F; j += 16) {
-                    const float d = y[j] - mean;
-                    vs += d * d;
-                }
-                rstd = 1.f / sqrtf(rsum16(vs) / (float)F + 1e-5f);
-                if (sub == 0 && L.rs >= 0) S[L.rs + row] = rstd;
-            }
-            for (int j = sub; j < F; j += 16) {
-                float v = y[j];
+            if (F <= 64) {
+                few_row_pass<4>(y, S, lr, F, ld, row, sub);
+            } else if (F <= 16 * kRowRegs) {
+                few_row_pass<kRowRegs>(y, S, lr, F, ld, row, sub);
+            } else {
+                const float invF = 1.f / (float)F;
+                float mean = 0.f, rstd = 1.f;
                 if (L.ln) {
-                    const float xh = (v - mean) * rstd;
-                    if (L.xh >= 0) S[L.xh + row * ld + j] = xh;
-                    v = L.ln == 2 ? xh * S[L.af + j] + S[L.af + F + j] : xh;
+                    float s = 0.f;
+                    for (int j = sub; j < F; j += 16) s += y[j];
+                    mean = rsum16(s) * invF;
+                    float vs = 0.f;
+                    for (int j = sub; j < F; j += 16) {
+                        const float d = y[j] - mean;
+                        vs += d * d;
+                    }
+                    rstd = 1.f / sqrtf(rsum16(vs) / (float)F + 1e-5f);
+                    if (sub == 0 && L.rs >= 0) S[L.rs + row] = rstd;
                 }
-                if (L.relu) v = relu(v);
-                y[j] = v;
+                for (int j = sub; j < F; j += 16) {
+                    float v = y[j];
+                    if (L.ln) {
+                        const float xh = (v - mean) * rstd;
+                        if (L.xh >= 0) S[L.xh + row * ld + j] = xh;
+                        v = L.ln == 2 ? xh * S[L.af + j] + S[L.af + F + j] : xh;
+                    }
+                    if (L.relu) v = relu(v);
+                    y[j] = v;
+                }
             }
             __syncthreads();
         }
@@ -2101,6 +2221,10 @@ struct EvalAgent {
     GLay L[kGL];
     int nl, aout, cout, n, ld0;
     long long oc, lds_floats;
+    unsigned run;       // the layers on the actor's path (the critic's are not computed)
+    int ldw[kGL];       // LDS-resident weights (the WLDS kernel): row stride of layer l's W,
+    long long wl[kGL];  // its offset in floats (W, then the bias), -1: layer not run
+    long long lds_w;    // floats of LDS with the weights
     const float *params;
     long long env_base;
     unsigned long long seed, counter0;
@@ -2120,6 +2244,9 @@ struct EvalTally {
     int prev;  // the staging holds a reward / done when the launch starts
 };
 
+constexpr int kEvalStamps = 6 + kGL;  // agx_debug_eval_stamps: per step
+
+template <bool WLDS>
 __global__ __launch_bounds__(kGT) void ppo_eval_multi_persistent_kernel(const EvalAgent *__restrict__ agents, int N,
                                                                         int A, int D, const float *stage_obs,
                                                                         long long *act_flat, int nsteps,
@@ -2139,6 +2266,25 @@ __global__ __launch_bounds__(kGT) void ppo_eval_multi_persistent_kernel(const Ev
     const auto prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(pr), 0,
                                                        __builtin_amdgcn_readfirstlane(ag.n * 4), 0x00020000);
     for (int i = tid; i < (int)ag.lds_floats; i += kGT) gdyn[i] = 0.f;  // padding and rows past the block
+    if constexpr (WLDS) {  // the actor path's weights, once for the whole pass (zero padded)
+        __syncthreads();   // the zeroing above before the LN affine copies below
+        for (int l = 0; l < ag.nl; ++l) {
+            if (!((ag.run >> l) & 1u)) continue;
+            const GLay &L = ag.L[l];
+            const int K = L.fin, F = L.fout, ldw = ag.ldw[l], Fp = (F + 15) & ~15;
+            float *W = gdyn + ag.wl[l];
+            for (int i = tid; i < Fp * ldw; i += kGT) {
+                const int n = i / ldw, k = i - n * ldw;
+                W[i] = (n < F && k < K) ? pr[L.w + n * K + k] : 0.f;
+            }
+            for (int i = tid; i < Fp; i += kGT) W[Fp * ldw + i] = i < F ? pr[L.b + i] : 0.f;
+            if (L.ln == 2)  // the LN affine's LDS copy too (few_forward<true> does not reload it)
+                for (int i = tid; i < F; i += kGT) {
+                    gdyn[L.af + i] = pr[L.g + i];
+                    gdyn[L.af + F + i] = pr[L.be + i];
+                }
+        }
+    }
     const GLay &La = ag.L[ag.aout], &Lc = ag.L[ag.cout];
     for (int t = 0; t < nsteps; ++t) {
         if (tid == 0) {
@@ -2168,7 +2314,7 @@ __global__ __launch_bounds__(kGT) void ppo_eval_multi_persistent_kernel(const Ev
         __syncthreads();
         if (!s_go) return;
         const bool stamp = stamps && blk == 0 && tid == 0 && t >= 2 && t < 34;
-        long long *stp = stamp ? stamps + 4 * (t - 2) : nullptr;
+        long long *stp = stamp ? stamps + kEvalStamps * (t - 2) : nullptr;
         if (stamp) stp[0] = (long long)__builtin_amdgcn_s_memrealtime();
         const float *ob = stage_obs + ((size_t)p * N + n0) * D;
         for (int i = tid; i < nrow * D; i += kGT) {
@@ -2194,8 +2340,11 @@ __global__ __launch_bounds__(kGT) void ppo_eval_multi_persistent_kernel(const Ev
             if (tid == 0) __hip_atomic_store(tally.fin_words + blk, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
-        if (stamp) stp[1] = (long long)__builtin_amdgcn_s_memrealtime();
-        few_forward(ag.L, ag.nl, gdyn, pr, prs, ag.oc, ag.ld0, nullptr);
+        if (stamp) {
+            stp[1] = (long long)__builtin_amdgcn_s_memrealtime();
+            stp[4] = (long long)__builtin_readcyclecounter();
+        }
+        few_forward<WLDS>(ag.L, ag.nl, gdyn, pr, prs, ag.oc, ag.ld0, stp ? stp + 5 : nullptr, ag.run, ag.wl, ag.ldw);
         if (stamp) stp[2] = (long long)__builtin_amdgcn_s_memrealtime();
         GSample sp{A, N, 1, La.ld, Lc.ld, ag.seed, ag.counter0 + (unsigned long long)t, nullptr, nullptr, 0,
                    nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, act_flat, ag.env_base};
@@ -2897,9 +3046,11 @@ static long long *&g_eval_stamps() {
     static long long *p = nullptr;
     return p;
 }
-// diagnostic: block 0's stamps of steps 2..33 of agx_ppo_eval_multi_persistent
-// (s_memrealtime, 100 MHz): release seen, observations staged, forward done,
-// done word written; int64[128], or null to stop
+// diagnostic: block 0's stamps of steps 2..33 of agx_ppo_eval_multi_persistent,
+// kEvalStamps per step: release seen, observations staged, forward done, done
+// word written (s_memrealtime, 100 MHz), then the shader clock at the forward's
+// start and after each layer (0: not run); int64[32 * kEvalStamps], or null
+// to stop
 extern "C" int agx_debug_eval_stamps(int64_t *buf) {
     g_eval_stamps() = reinterpret_cast<long long *>(buf);
     return AGX_OK;
@@ -2909,13 +3060,15 @@ extern "C" size_t agx_ppo_eval_multi_bytes(int64_t P) { return P > 0 ? (size_t)P
 
 namespace {
 // agent p's policy-step plan (act_plan + act_plan_few) into x; -> its dynamic
-// LDS bytes (0: the plan does not fit)
-size_t eval_agent_plan(const agx_ppo_graph *net, EvalAgent &x) {
+// LDS bytes (0: the plan does not fit).  Only the layers on the actor's path
+// run; wlds: their weights get LDS tiles after the activation tiles.
+size_t eval_agent_plan(const agx_ppo_graph *net, EvalAgent &x, bool wlds) {
     GArgs full{};
     if (plan_graph(net, 1, full) != AGX_OK) return 0;
     GActArgs a{};
     act_plan(full, a);
-    const size_t dyn = act_plan_few(ppo_eval_multi_persistent_kernel, a);
+    const size_t dyn = wlds ? act_plan_few(ppo_eval_multi_persistent_kernel<true>, a)
+                            : act_plan_few(ppo_eval_multi_persistent_kernel<false>, a);
     if (!dyn) return 0;
     for (int l = 0; l < kGL; ++l) x.L[l] = a.L[l];
     x.nl = a.nl;
@@ -2925,26 +3078,64 @@ size_t eval_agent_plan(const agx_ppo_graph *net, EvalAgent &x) {
     x.ld0 = a.ld0;
     x.oc = a.oc;
     x.lds_floats = a.lds_floats;
-    return dyn;
+    x.run = 0;
+    for (int l = a.aout; l >= 0; l = a.L[l].src) x.run |= 1u << l;
+    long long off = a.lds_floats;
+    for (int l = 0; l < kGL; ++l) {
+        x.wl[l] = -1;
+        x.ldw[l] = 0;
+        if (!wlds || l >= a.nl || !((x.run >> l) & 1u)) continue;
+        const long long fp = (a.L[l].fout + 15) / 16 * 16;
+        x.ldw[l] = (a.L[l].fin + 15) / 16 * 16 + 4;
+        x.wl[l] = off;
+        off += fp * x.ldw[l] + fp;
+    }
+    x.lds_w = (off + 3) & ~3ll;
+    if (!wlds) return dyn;
+    hipFuncAttributes fa{};
+    const size_t st = hipFuncGetAttributes(&fa, (const void *)ppo_eval_multi_persistent_kernel<true>) == hipSuccess
+                          ? fa.sharedSizeBytes
+                          : 8 * 1024;
+    const size_t bytes = (size_t)x.lds_w * 4;
+    return bytes <= kLdsMax - st ? bytes : 0;
+}
+
+// the population's form: 1 LDS-resident weights, 0 weights from L2, -1 none
+// (every workgroup co-resident either way); dyn: the launch's LDS bytes
+int eval_form(const agx_ppo_graph *const *nets, int64_t P, int64_t N, size_t *dyn_out) {
+    if (!nets || P <= 0 || N <= 0 || P > 65535) return -1;
+    if (const char *e = getenv("AGX_GRAPH_FEW"))
+        if (atoi(e) == 0) return -1;
+    bool wl_ok = true;
+    if (const char *e = getenv("AGX_EVAL_WLDS"))
+        if (atoi(e) == 0) wl_ok = false;
+    for (int w = wl_ok ? 1 : 0; w >= 0; --w) {
+        size_t dyn = 0;
+        bool ok = true;
+        for (int64_t p = 0; p < P && ok; ++p) {
+            EvalAgent x{};
+            if (!nets[p] || nets[p]->obs_dim != nets[0]->obs_dim || nets[p]->n_actions != nets[0]->n_actions)
+                return -1;
+            const size_t d = eval_agent_plan(nets[p], x, w == 1);
+            ok = d != 0;
+            dyn = d > dyn ? d : dyn;
+        }
+        if (!ok) continue;
+        int v = 0;
+        const hipError_t e = w ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                     &v, ppo_eval_multi_persistent_kernel<true>, kGT, dyn)
+                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                     &v, ppo_eval_multi_persistent_kernel<false>, kGT, dyn);
+        if (e != hipSuccess || (int64_t)v * cu_count_g() < P * ceil_div(N, kFR)) continue;
+        if (dyn_out) *dyn_out = dyn;
+        return w;
+    }
+    return -1;
 }
 }  // namespace
 
 extern "C" int agx_ppo_eval_multi_supported(const agx_ppo_graph *const *nets, int64_t P, int64_t N) {
-    if (!nets || P <= 0 || N <= 0 || P > 65535) return 0;
-    if (const char *e = getenv("AGX_GRAPH_FEW"))
-        if (atoi(e) == 0) return 0;
-    size_t dyn = 0;
-    for (int64_t p = 0; p < P; ++p) {
-        EvalAgent x{};
-        if (!nets[p] || nets[p]->obs_dim != nets[0]->obs_dim || nets[p]->n_actions != nets[0]->n_actions) return 0;
-        const size_t d = eval_agent_plan(nets[p], x);
-        if (!d) return 0;
-        dyn = d > dyn ? d : dyn;
-    }
-    int v = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, ppo_eval_multi_persistent_kernel, kGT, dyn) != hipSuccess)
-        return 0;
-    return (int64_t)v * cu_count_g() >= P * ceil_div(N, kFR) ? 1 : 0;
+    return eval_form(nets, P, N, nullptr) >= 0 ? 1 : 0;
 }
 
 extern "C" int agx_ppo_eval_multi_persistent(const agx_ppo_graph *const *nets, const float *const *params,
@@ -2958,14 +3149,14 @@ extern "C" int agx_ppo_eval_multi_persistent(const agx_ppo_graph *const *nets, c
                 "agx_ppo_eval_multi_persistent: bad arguments");
     AGX_REQUIRE((uint64_t)base + (uint64_t)nsteps < AGX_ROLLOUT_STOP, "agx_ppo_eval_multi_persistent: base wraps");
     AGX_REQUIRE(timeout_s > 0 && timeout_s < 3600, "agx_ppo_eval_multi_persistent: timeout_s out of range");
-    AGX_REQUIRE(agx_ppo_eval_multi_supported(nets, P, N), "agx_ppo_eval_multi_persistent: unsupported population");
-    EvalAgent *ag = static_cast<EvalAgent *>(agents_host);
     size_t dyn = 0;
+    const int form = eval_form(nets, P, N, &dyn);
+    AGX_REQUIRE(form >= 0, "agx_ppo_eval_multi_persistent: unsupported population");
+    EvalAgent *ag = static_cast<EvalAgent *>(agents_host);
     for (int64_t p = 0; p < P; ++p) {
         AGX_REQUIRE(params[p], "agx_ppo_eval_multi_persistent: agent %lld has no parameters", (long long)p);
         EvalAgent x{};
-        const size_t d = eval_agent_plan(nets[p], x);
-        dyn = d > dyn ? d : dyn;
+        eval_agent_plan(nets[p], x, form == 1);
         x.params = params[p];
         x.env_base = env_base[p];
         x.seed = seeds[p];
@@ -2990,9 +3181,9 @@ extern "C" int agx_ppo_eval_multi_persistent(const agx_ppo_graph *const *nets, c
         et = EvalTally{tally->stage_rew, tally->stage_done, tally->scores, tally->completed, tally->finished,
                        tally->fin_words, tally->prev ? 1 : 0};
     }
-    ppo_eval_multi_persistent_kernel<<<grid, kGT, dyn, s>>>(static_cast<const EvalAgent *>(agents_dev), (int)N,
-                                                            nets[0]->n_actions, nets[0]->obs_dim, stage_obs,
-                                                            reinterpret_cast<long long *>(actions_flat), (int)nsteps,
-                                                            ctl, ticks, base, g_eval_stamps(), et);
+    auto *kern = form == 1 ? ppo_eval_multi_persistent_kernel<true> : ppo_eval_multi_persistent_kernel<false>;
+    kern<<<grid, kGT, dyn, s>>>(static_cast<const EvalAgent *>(agents_dev), (int)N, nets[0]->n_actions,
+                                nets[0]->obs_dim, stage_obs, reinterpret_cast<long long *>(actions_flat), (int)nsteps,
+                                ctl, ticks, base, g_eval_stamps(), et);
     return check_launch("agx_ppo_eval_multi_persistent");
 }

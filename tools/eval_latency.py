@@ -28,7 +28,8 @@ assert R.population_eval_ok([run])
 run.evaluate(max_steps=50)
 torch.cuda.synchronize()
 lib = _lib.load()
-buf = torch.zeros(128, dtype=torch.int64, device="cuda")
+KS = 6 + 16  # kEvalStamps
+buf = torch.zeros(32 * KS, dtype=torch.int64, device="cuda")
 lib.agx_debug_eval_stamps(buf.data_ptr())
 waits, envs = [], []
 orig_wait, orig_env = R._EvalDriver.wait, R._EvalDriver.env_step
@@ -53,10 +54,19 @@ run.evaluate(max_steps=400)
 dt = time.perf_counter() - t0
 torch.cuda.synchronize()
 lib.agx_debug_eval_stamps(None)
-st = buf.cpu().numpy().reshape(32, 4).astype(np.float64) * 10e-3  # us
+raw = buf.cpu().numpy().reshape(32, KS)
+st = raw[:, :4].astype(np.float64) * 10e-3  # us
 d = np.diff(st, axis=1)
+cyc = raw[:, 4:].astype(np.float64)  # shader clock: forward start, then after each layer run
+fwd_cyc = np.array([row[row > 0].max() - row[0] for row in cyc])
+print(f"shader clock over the forward: {np.mean(fwd_cyc / (d[:, 1] * 1e-6)) / 1e9:.2f} GHz equivalent "
+      f"({fwd_cyc.mean():.0f} cycles); per layer run (cycles):",
+      [round(float(x)) for x in np.diff(np.concatenate([[cyc[0, 0]], cyc[0, 1:][cyc[0, 1:] > 0]]))])
+for i in (1, 2, 3):
+    print("   step", i, [round(float(x)) for x in np.diff(np.concatenate([[cyc[i, 0]], cyc[i, 1:][cyc[i, 1:] > 0]]))])
 gap = st[1:, 0] - st[:-1, 3]  # done written -> next release seen (host env step + signal)
 print(f"pass: {dt / 400 * 1e6:.1f} us per step; host wait {np.mean(waits) * 1e6:.1f} us, env step "
       f"{np.mean(envs) * 1e6:.1f} us")
 print(f"device (workgroup 0): obs staged {d[:, 0].mean():.2f} us, forward {d[:, 1].mean():.2f} us, sample + "
       f"actions + done {d[:, 2].mean():.2f} us; done -> next release seen {gap.mean():.2f} us")
+
