@@ -1280,20 +1280,10 @@ __device__ __forceinline__ void few_gemm_l(const float *X, int ldx, const float 
 // dW[o][i] = sum over the 16 rows of dZ[row][o] X[row][i] (o < F, i < fin)
 // straight into the gradient row Gw ([F][fin]); tiles round the waves
 __device__ __forceinline__ void few_dw(const float *dZ, int ldz, const float *X, int ldx, int F, int fin, float *Gw) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane & 15, q = lane >> 4;
-    const int tm = (F + 15) >> 4, tn = (fin + 15) >> 4;
-    for (int t = wave; t < tm * tn; t += kGW) {
-        const int o0 = (t % tm) << 4, i0 = (t / tm) << 4;
-        float a[4], b[4];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            a[kk] = dZ[(4 * kk + q) * ldz + o0 + r];
-            b[kk] = X[(4 * kk + q) * ldx + i0 + r];
-        }
-        f4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], b[kk], acc, 0, 0, 0);
+    const int tm = (F + 15) >> 4, tn = (fin + 15) >> 4, nt = tm * tn;
+    auto put = [&](int o0, int i0, const f4 &acc) {
         const int i = i0 + r;
         if (i < fin) {
 #pragma unroll
@@ -1302,6 +1292,30 @@ __device__ __forceinline__ void few_dw(const float *dZ, int ldz, const float *X,
                 if (o < F) Gw[o * fin + i] = acc[j];
             }
         }
+    };
+    // two tiles per pass (t and t + kGW): both tiles' LDS reads in flight,
+    // then two independent MFMA chains; each tile's sum order unchanged
+    for (int t = wave; t < nt; t += 2 * kGW) {
+        const int t2 = t + kGW;
+        const bool two = t2 < nt;  // uniform
+        const int o0 = (t % tm) << 4, i0 = (t / tm) << 4;
+        const int o1 = two ? (t2 % tm) << 4 : o0, i1 = two ? (t2 / tm) << 4 : i0;
+        float a[4], b[4], a2[4], b2[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            a[kk] = dZ[(4 * kk + q) * ldz + o0 + r];
+            b[kk] = X[(4 * kk + q) * ldx + i0 + r];
+            a2[kk] = dZ[(4 * kk + q) * ldz + o1 + r];
+            b2[kk] = X[(4 * kk + q) * ldx + i1 + r];
+        }
+        f4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], b[kk], acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[kk], b2[kk], acc2, 0, 0, 0);
+        }
+        put(o0, i0, acc);
+        if (two) put(o1, i1, acc2);
     }
 }
 
@@ -1364,6 +1378,60 @@ __device__ __forceinline__ void few_row_pass(float *y, float *S, const LayRow &L
         }
         if (L.relu) x = relu(x);
         y[j] = ok[i] ? x : 0.f;
+    }
+}
+
+// The backward of few_row_pass for one row: dY -> dZ in place through the
+// ReLU mask and the LayerNorm(+affine) backward, dY' (the affine's input
+// gradient) to T for the gamma / beta sums; registers as in few_row_pass, the
+// same float operations in the same order as the column loops.
+template <int M>
+__device__ __forceinline__ void few_row_back(float *dy, const float *xh, float *T, const float *S, const LayRow &L,
+                                             int F, int row, int sub) {
+    const int mp = (F + 15) >> 4;
+    float d[M], x[M], ga[M], be[M];
+    bool ok[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int j = sub + 16 * i;
+        ok[i] = j < F;
+        d[i] = x[i] = ga[i] = be[i] = 0.f;
+        if (i < mp) {
+            d[i] = dy[j];
+            x[i] = xh[j];
+            if (L.ln == 2) {
+                ga[i] = S[L.af + j];
+                be[i] = S[L.af + F + j];
+            }
+        }
+    }
+    const float rs = L.ln ? S[L.rs + row] : 1.f;
+    float dp[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const float pre = L.ln == 2 ? x[i] * ga[i] + be[i] : x[i];
+        dp[i] = (!L.relu || pre > 0.f) ? d[i] : 0.f;
+    }
+    float m1 = 0.f, m2 = 0.f;
+    if (L.ln) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            const float dx = dp[i] * (L.ln == 2 ? ga[i] : 1.f);
+            s1 = ok[i] ? s1 + dx : s1;
+            s2 = ok[i] ? s2 + dx * x[i] : s2;
+        }
+        const float invF = 1.f / (float)F;
+        m1 = rsum16(s1) * invF;
+        m2 = rsum16(s2) * invF;
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        if (i >= mp) break;  // uniform
+        const int j = sub + 16 * i;
+        if (L.ln == 2) T[j] = ok[i] ? dp[i] : 0.f;
+        const float v = L.ln ? rs * (dp[i] * (L.ln == 2 ? ga[i] : 1.f) - m1 - x[i] * m2) : dp[i];
+        dy[j] = ok[i] ? v : 0.f;
     }
 }
 
@@ -1560,50 +1628,58 @@ __device__ __forceinline__ void few_grads(const GArgs &g, float *S, const float 
         if (L.ln || L.relu) {
             float *dy = dZ + row * ld;
             const float *xh = S + (L.ln ? L.xh : L.yr) + row * ld;  // xhat, or Y for a plain ReLU
-            const float invF = 1.f / (float)F;
-            float m1 = 0.f, m2 = 0.f, rs = 1.f;
-            auto dpre = [&](int j, float &x) {
-                const float d = dy[j];
-                x = xh[j];
-                const float pre = L.ln == 2 ? x * S[L.af + j] + S[L.af + F + j] : x;
-                return (!L.relu || pre > 0.f) ? d : 0.f;
-            };
-            if (L.ln) {
-                float s1 = 0.f, s2 = 0.f;
+            const LayRow lr{L.ln, L.relu, L.af, L.rs, L.xh};
+            if (F <= 64) {
+                few_row_back<4>(dy, xh, T + row * ld, S, lr, F, row, sub);
+            } else if (F <= 16 * kRowRegs) {
+                few_row_back<kRowRegs>(dy, xh, T + row * ld, S, lr, F, row, sub);
+            } else {
+                const float invF = 1.f / (float)F;
+                float m1 = 0.f, m2 = 0.f, rs = 1.f;
+                auto dpre = [&](int j, float &x) {
+                    const float d = dy[j];
+                    x = xh[j];
+                    const float pre = L.ln == 2 ? x * S[L.af + j] + S[L.af + F + j] : x;
+                    return (!L.relu || pre > 0.f) ? d : 0.f;
+                };
+                if (L.ln) {
+                    float s1 = 0.f, s2 = 0.f;
+                    for (int j = sub; j < F; j += 16) {
+                        float x;
+                        const float dx = dpre(j, x) * (L.ln == 2 ? S[L.af + j] : 1.f);
+                        s1 += dx;
+                        s2 += dx * x;
+                    }
+                    m1 = rsum16(s1) * invF;
+                    m2 = rsum16(s2) * invF;
+                    rs = S[L.rs + row];
+                }
                 for (int j = sub; j < F; j += 16) {
                     float x;
-                    const float dx = dpre(j, x) * (L.ln == 2 ? S[L.af + j] : 1.f);
-                    s1 += dx;
-                    s2 += dx * x;
+                    const float dp = dpre(j, x);
+                    if (L.ln == 2) T[row * ld + j] = dp;
+                    dy[j] = L.ln ? rs * (dp * (L.ln == 2 ? S[L.af + j] : 1.f) - m1 - x * m2) : dp;
                 }
-                m1 = rsum16(s1) * invF;
-                m2 = rsum16(s2) * invF;
-                rs = S[L.rs + row];
-            }
-            for (int j = sub; j < F; j += 16) {
-                float x;
-                const float dp = dpre(j, x);
-                if (L.ln == 2) T[row * ld + j] = dp;
-                dy[j] = L.ln ? rs * (dp * (L.ln == 2 ? S[L.af + j] : 1.f) - m1 - x * m2) : dp;
             }
             __syncthreads();
         }
         if (st) st[18 + 3 * l] = (long long)__builtin_readcyclecounter();
-        // bias / LN-affine gradients: column sums in row order
-        for (int j = tid; j < F; j += kGT) {
-            float sb = 0.f, sg = 0.f, sbe = 0.f;
-#pragma unroll
-            for (int b = 0; b < kFR; ++b) sb += dZ[b * ld + j];
-            G[L.b + j] = sb;
-            if (L.ln == 2) {
+        // bias / LN-affine gradients: column sums in row order, one sum per
+        // wave (0: bias, 1: gamma, 2: beta), the 16 rows' terms loaded first
+        if (wave < (L.ln == 2 ? 3 : 1)) {
+            const float *src = wave == 0 ? dZ : T;
+            const long long go = wave == 0 ? L.b : wave == 1 ? L.g : L.be;
+            for (int j = lane; j < F; j += kWave) {
+                float v[kFR];
 #pragma unroll
                 for (int b = 0; b < kFR; ++b) {
-                    const float t = T[b * ld + j];
-                    sg += t * S[L.xh + b * ld + j];
-                    sbe += t;
+                    v[b] = src[b * ld + j];
+                    if (wave == 1) v[b] = v[b] * S[L.xh + b * ld + j];
                 }
-                G[L.g + j] = sg;
-                G[L.be + j] = sbe;
+                float sum = 0.f;
+#pragma unroll
+                for (int b = 0; b < kFR; ++b) sum += v[b];
+                G[go + j] = sum;
             }
         }
         const float *X = L.src < 0 ? S + g.oc : S + g.L[L.src].yr;

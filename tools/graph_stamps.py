@@ -36,25 +36,21 @@ for i, n in enumerate(names):
 
 # inside the gradient pass (minibatch_grads' inner stamps)
 inner = st[16:]
-nl = len(pop.desc_layers) if hasattr(pop, "desc_layers") else None
+from agilerl_amd.population.learner import graph_descriptor  # noqa: E402
+d = graph_descriptor(pop.spec)
 print(f"  obs transpose                    {inner[0] - st[0]}")
 prev = inner[0]
 L = 0
-while L < 16 and inner[1 + L] > 0:
+while L < d.n_layers:
     print(f"  fwd layer {L:2d}                     {inner[1 + L] - prev}")
     prev = inner[1 + L]
     L += 1
 print(f"  loss pass                        {inner[17] - prev}")
 prev = inner[17]
 for l in range(L - 1, -1, -1):
-    rows, dw, dx = inner[18 + 3 * l], inner[19 + 3 * l], inner[20 + 3 * l]
-    if dw <= 0:
-        print(f"  bwd layer {l:2d}: rows {rows - prev:6d}  dW {dx - rows:6d}")
-    else:
-        print(f"  bwd layer {l:2d}: rows {rows - prev:6d}  dW {dw - rows:6d}  dX {dx - dw:6d}")
-    prev = dx
-from agilerl_amd.population.learner import graph_descriptor  # noqa: E402
-d = graph_descriptor(pop.spec)
+    rows, dx, dw = inner[18 + 3 * l], inner[19 + 3 * l], inner[20 + 3 * l]
+    print(f"  bwd layer {l:2d}: rows {rows - prev:6d}  dW (+ column sums) {dx - rows:6d}  dX {dw - dx:6d}")
+    prev = dw
 for i in range(d.n_layers):
     x = d.layers[i]
     print(f"  layer {i:2d}: src {x.src:2d} {x.fin:3d} -> {x.fout:3d} ln {x.ln} relu {x.relu}")
