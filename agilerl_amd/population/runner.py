@@ -686,6 +686,10 @@ class _EvalDriver:
                     self._t_finished = torch.zeros(P * N, dtype=torch.uint8, device=dev)
                     self._t_fin = _coherent(self, 4 * self.n_wg).view(torch.int32)
                     self._t_fin_np = self._t_fin.numpy()
+                    # every workgroup's env count: the pass ends when the counts reach
+                    # them (one byte compare per step instead of a numpy sum)
+                    gx = self.n_wg // P
+                    self._fin_all = np.array([min(16, N - 16 * x) for x in range(gx)] * P, dtype=np.int32).tobytes()
                     self._tally = AgxEvalTally(self.rew_h.data_ptr(), self.done_h.data_ptr(),
                                                self._t_scores.data_ptr(), self._t_completed.data_ptr(),
                                                self._t_finished.data_ptr(), self._t_fin.data_ptr(), 0)
@@ -945,8 +949,8 @@ class _EvalDriver:
                     if self.step + 1 < self.launched_to:  # this part's next step, before the next part waits
                         sig(self._ctl, blocks[h][0], blocks[h][1], rel + 1)
                 self.step += 1
-                if self.device_tally:  # the env steps before this one, tallied by the launch
-                    self.n_finished = int(self._t_fin_np.sum())
+                if self.device_tally and self._t_fin_np.tobytes() == self._fin_all:  # tallied by the launch
+                    self.n_finished = P * N
                 if self.n_finished == P * N or (self.max_steps is not None and self.step >= self.max_steps):
                     break
             self.end()
