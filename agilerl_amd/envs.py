@@ -360,12 +360,14 @@ class StackedVecEnv:
             s += e.num_envs
         # [6]: an upper bound of the episode lengths (while it stays below the
         # time limit no env can be truncated and the step skips that test)
+        # [8]: per ring slot, whether any env's episode ends there (a lookup
+        # instead of a test of the slot's terminations every step)
         self._fz = ([e._obs for e in envs], obs, rew, term, views, lens, np.zeros(self.num_envs, dtype=bool),
-                    [int(lens.max()) if lens.size else 0])
+                    [int(lens.max()) if lens.size else 0], term.any(axis=1).tolist())
         return True
 
     def _step_fused(self, out_obs, out_rew, out_done):
-        _, robs, rrew, rterm, _, lens, ztrunc, lmax = self._fz
+        _, robs, rrew, rterm, _, lens, ztrunc, lmax, rany = self._fz
         e0 = self.envs[0]
         k = (e0._k + 1) % e0._ring
         for e in self.envs:
@@ -385,7 +387,7 @@ class StackedVecEnv:
             lens += 1
             lmax[0] += 1
             if lmax[0] < e0.max_episode_steps:  # no env can reach the limit: only episode ends reset
-                if term.any():
+                if rany[k]:
                     lens[term] = 0
             else:
                 trunc = (lens >= e0.max_episode_steps) & ~term
