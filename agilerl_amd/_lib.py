@@ -74,6 +74,7 @@ SIGNATURES = {
     "agx_host_wait": (_INT, [_P, _I, ctypes.c_uint32, _D]),
     "agx_host_signal_range": (_INT, [_P, _I, _I, ctypes.c_uint32]),
     "agx_host_wait_range": (_INT, [_P, _I, _I, ctypes.c_uint32, _D]),
+    "agx_host_signal_wait_range": (_INT, [_P, _I, _I, ctypes.c_uint32, _I, _I, ctypes.c_uint32, _D]),
     "agx_per_workspace_bytes": (_SZ, [_I, _I]),
     "agx_per_init": (_INT, [_P, _P, _I, _P]),
     "agx_per_add": (_INT, [_P, _P, _I, _I, _I, _I, _D, _P, _P, _P]),

@@ -165,6 +165,14 @@ extern "C" int agx_host_wait_range(const agx_rollout_ctl *ctl, int64_t w0, int64
     }
 }
 
+// release [s0, s1) to seq, then wait until [w0, w1) reach target: one call
+// for the pipelined pass's hand-over from one part to the next
+extern "C" int agx_host_signal_wait_range(agx_rollout_ctl *ctl, int64_t s0, int64_t s1, uint32_t seq, int64_t w0,
+                                          int64_t w1, uint32_t target, double timeout_s) {
+    const int rc = agx_host_signal_range(ctl, s0, s1, seq);
+    return rc != AGX_OK ? rc : agx_host_wait_range(ctl, w0, w1, target, timeout_s);
+}
+
 extern "C" int agx_host_wait(const agx_rollout_ctl *ctl, int64_t nwg, uint32_t target, double timeout_s) {
     AGX_REQUIRE(ctl && nwg > 0, "agx_host_wait: bad arguments");
     const uint32_t *done = agx::rollout_done_words(const_cast<agx_rollout_ctl *>(ctl));

@@ -925,10 +925,19 @@ class _EvalDriver:
         obs_n, rew_n, done_n, act_n = self._views
         self._part_views = [(obs_n[a:b], rew_n[a:b], done_n[a:b], act_n[a:b], self.scores[a:b], self.finished[a:b],
                              self.completed[a:b], np.zeros(b - a, dtype=bool)) for a, b in self._halves]
-        sig, wait = lib.agx_host_signal_range, lib.agx_host_wait_range
+        sig, wait, sigwait = lib.agx_host_signal_range, lib.agx_host_wait_range, lib.agx_host_signal_wait_range
+        tmo = self.runner.timeout_s
         self.stream = _eval_stream(0)
         self._pipelined = True
         self.begin()
+
+        def _failed(rc, h):
+            msg = lib.agx_last_error().decode(errors="replace")
+            self.abort()
+            raise _lib.AgxError(f"agx_host_wait_range failed ({rc}): {msg}; evaluation part {h} of "
+                                f"{n}, P={P} N={N} at step {self.step}")
+
+        waited0 = False  # part 0's wait for this step done by the previous step's last hand-over
         try:
             while True:
                 if self.step >= self.launched_to:
@@ -937,21 +946,37 @@ class _EvalDriver:
                     self._launch()
                     for w0, w1 in blocks:
                         sig(self._ctl, w0, w1, 1)
+                    waited0 = False
                 rel = self.step - self.launch_step0 + 1
-                for h in range(n):
-                    rc = wait(self._ctl, blocks[h][0], blocks[h][1], rel, self.runner.timeout_s)
+                more = self.step + 1 < self.launched_to  # the launch covers the next step
+                if not waited0:
+                    rc = wait(self._ctl, blocks[0][0], blocks[0][1], rel, tmo)
                     if rc != 0:
-                        msg = lib.agx_last_error().decode(errors="replace")
-                        self.abort()
-                        raise _lib.AgxError(f"agx_host_wait_range failed ({rc}): {msg}; evaluation part {h} of "
-                                            f"{n}, P={P} N={N} at step {self.step}")
+                        _failed(rc, 0)
+                waited0 = False
+                for h in range(n):
                     self._half_env_step(h)
-                    if self.step + 1 < self.launched_to:  # this part's next step, before the next part waits
-                        sig(self._ctl, blocks[h][0], blocks[h][1], rel + 1)
+                    if h + 1 < n:
+                        # this part's next step released, then the next part's wait: one call
+                        rc = (sigwait(self._ctl, blocks[h][0], blocks[h][1], rel + 1, blocks[h + 1][0],
+                                      blocks[h + 1][1], rel, tmo) if more
+                              else wait(self._ctl, blocks[h + 1][0], blocks[h + 1][1], rel, tmo))
+                        if rc != 0:
+                            _failed(rc, h + 1)
                 self.step += 1
                 if self.device_tally and self._t_fin_np.tobytes() == self._fin_all:  # tallied by the launch
                     self.n_finished = P * N
-                if self.n_finished == P * N or (self.max_steps is not None and self.step >= self.max_steps):
+                done = self.n_finished == P * N or (self.max_steps is not None and self.step >= self.max_steps)
+                if more:  # the last part's next step, and (going on) part 0's wait for it
+                    if done:
+                        sig(self._ctl, blocks[-1][0], blocks[-1][1], rel + 1)
+                    else:
+                        rc = sigwait(self._ctl, blocks[-1][0], blocks[-1][1], rel + 1, blocks[0][0], blocks[0][1],
+                                     rel + 1, tmo)
+                        if rc != 0:
+                            _failed(rc, 0)
+                        waited0 = True
+                if done:
                     break
             self.end()
         except BaseException:

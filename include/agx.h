@@ -337,6 +337,11 @@ int agx_host_wait(const agx_rollout_ctl *ctl, int64_t nwg, uint32_t target, doub
  * half's workgroups run */
 int agx_host_signal_range(agx_rollout_ctl *ctl, int64_t w0, int64_t w1, uint32_t seq);
 int agx_host_wait_range(const agx_rollout_ctl *ctl, int64_t w0, int64_t w1, uint32_t target, double timeout_s);
+/* agx_host_signal_range(ctl, s0, s1, seq) then agx_host_wait_range(ctl, w0, w1,
+ * target, timeout_s): one call where a part's release hands over to the next
+ * part's wait */
+int agx_host_signal_wait_range(agx_rollout_ctl *ctl, int64_t s0, int64_t s1, uint32_t seq, int64_t w0, int64_t w1,
+                               uint32_t target, double timeout_s);
 
 /* ---- prioritized replay segment trees -----------------------------------
  * Replaces SumSegmentTree / MinSegmentTree (agilerl/components/
