@@ -125,43 +125,52 @@ __global__ __launch_bounds__(256) void rowpass(long long *out, float *sink, cons
     for (int rep = 0; rep < 4; ++rep) {
         t[2 * rep] = __builtin_readcyclecounter();
         float *y = S + row * ld;
-        float v[8], ga[8], be[8];
+        constexpr int M = 4;
+        const int mp = (F + 15) >> 4;
+        float v[M], ga[M], be[M];
+        bool ok[M];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < M; ++i) {
             const int j = sub + 16 * i;
-            v[i] = j < F ? y[j] : 0.f;
-            ga[i] = ln == 2 && j < F ? S[af + j] : 0.f;
-            be[i] = ln == 2 && j < F ? S[af + F + j] : 0.f;
+            ok[i] = j < F;
+            v[i] = ga[i] = be[i] = 0.f;
+            if (i < mp) {
+                v[i] = y[j];
+                if (ln == 2) {
+                    ga[i] = S[af + j];
+                    be[i] = S[af + F + j];
+                }
+            }
         }
+        long long ta = __builtin_readcyclecounter();
         float mean = 0.f, rstd = 1.f;
         if (ln) {
             float s = 0.f;
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (sub + 16 * i < F) s += v[i];
+            for (int i = 0; i < M; ++i) s = ok[i] ? s + v[i] : s;
             mean = rsum16(s) * (1.f / (float)F);
             float vs = 0.f;
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (sub + 16 * i < F) {
-                    const float d = v[i] - mean;
-                    vs += d * d;
-                }
+            for (int i = 0; i < M; ++i) {
+                const float d = v[i] - mean;
+                vs = ok[i] ? vs + d * d : vs;
+            }
             rstd = 1.f / sqrtf(rsum16(vs) / (float)F + 1e-5f);
         }
+        long long tb = __builtin_readcyclecounter() + (rstd == 7.f);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < M; ++i) {
+            if (i >= mp) break;
             const int j = sub + 16 * i;
-            if (j < F) {
-                float x = v[i];
-                if (ln) {
-                    const float xh = (x - mean) * rstd;
-                    x = ln == 2 ? xh * ga[i] + be[i] : xh;
-                }
-                if (relu) x = fmaxf(x, 0.f);
-                y[j] = x * 0.5f;
+            float x = v[i];
+            if (ln) {
+                const float xh = (x - mean) * rstd;
+                x = ln == 2 ? xh * ga[i] + be[i] : xh;
             }
+            if (relu) x = fmaxf(x, 0.f);
+            y[j] = ok[i] ? x * 0.5f : 0.f;
         }
+        if (rep == 3 && tid == 0) { out[20] = ta - t[2 * rep]; out[21] = tb - ta; }
         t[2 * rep + 1] = __builtin_readcyclecounter();
         __syncthreads();
     }
@@ -198,9 +207,11 @@ int main() {
     for (int rep = 0; rep < 2; ++rep) {
         rowpass<<<1, 256>>>(out, sink, chase);
         if (hipDeviceSynchronize() != hipSuccess) return 2;
-        if (hipMemcpy(h, out, 8 * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess) return 3;
+        long long h2[22];
+        if (hipMemcpy(h2, out, sizeof(h2), hipMemcpyDeviceToHost) != hipSuccess) return 3;
         printf("row pass (F 64, LN + affine + ReLU): row pass / barrier cycles:");
-        for (int i = 0; i < 8; ++i) printf(" %lld", h[i]);
+        for (int i = 0; i < 8; ++i) printf(" %lld", h2[i]);
+        printf("; last rep: loads %lld, stats %lld", h2[20], h2[21]);
         printf("\n");
     }
     return 0;
