@@ -2190,8 +2190,8 @@ __global__ __launch_bounds__(kGT) void ppo_rollout_graph_persistent_kernel(const
     float *base = ga.ws + ((size_t)p * gridDim.x + blockIdx.x) * ga.ws_block;
     float *obs_rows = base + ga.obs_off;  // [rows][D]: this step's observations
     constexpr int kArgWords = (int)(sizeof(ActArgs) / 4);
-    if (blk == 0 && tid == 0)  // the launch runs (agx_rollout_ctl.started)
-        __hip_atomic_store(&ctl->started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0)  // this workgroup is resident (agx_rollout_ctl.started counts them)
+        __hip_atomic_fetch_add(&ctl->started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if constexpr (FEW) {  // the LDS tiles' padding (and the rows past the block) stay zero
         for (int i = tid; i < (int)ga.lds_floats; i += kGT) gdyn[i] = 0.f;
     }

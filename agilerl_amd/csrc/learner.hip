@@ -2081,8 +2081,8 @@ __global__ __launch_bounds__(kNT, 1) void ppo_rollout_persistent_kernel(const Ac
     const int blk = blockIdx.y * gridDim.x + blockIdx.x;
     unsigned *rel = rollout_release_word(ctl, gridDim.x * gridDim.y, blk);  // this workgroup's own line
     constexpr int kArgWords = (int)(sizeof(ActArgs) / 4);
-    if (blk == 0 && tid == 0)  // the launch runs (agx_rollout_ctl.started): a host pacing several can tell
-        __hip_atomic_store(&ctl->started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0)  // this workgroup is resident (agx_rollout_ctl.started counts them): a host pacing
+        __hip_atomic_fetch_add(&ctl->started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // several can tell
     for (int t = 0; t < nsteps; ++t) {
         long long *st = stamps && blk == 0 && t < 32 ? stamps + 8 * t : nullptr;
         if (st && tid == 0) st[0] = (long long)__builtin_amdgcn_s_memrealtime();

@@ -333,12 +333,17 @@ class StackedVecEnv:
         envs = self.envs
         fz = self._fz
         if fz is not None:
-            ids, views = fz[0], fz[4]
+            ids, views, seen = fz[0], fz[4], fz[9]
             k = envs[0]._k
             for e, i, v in zip(envs, ids, views):
                 if e._obs is not i or e._len is not v or e._k != k:
                     break
             else:
+                if any(e.steps != n for e, n in zip(envs, seen)):
+                    # blocks stepped on their own in lock step (ring positions still
+                    # agree): their lengths grew in place, the cached bound did not
+                    fz[7][0] = int(fz[5].max()) if fz[5].size else 0
+                    seen[:] = [e.steps for e in envs]
                 return True
             self._fz = None
         e0 = envs[0]
@@ -362,17 +367,20 @@ class StackedVecEnv:
         # time limit no env can be truncated and the step skips that test)
         # [8]: per ring slot, whether any env's episode ends there (a lookup
         # instead of a test of the slot's terminations every step)
+        # [9]: each block's step count as of the last fused step (a block stepped
+        # on its own invalidates [6]'s bound)
         self._fz = ([e._obs for e in envs], obs, rew, term, views, lens, np.zeros(self.num_envs, dtype=bool),
-                    [int(lens.max()) if lens.size else 0], term.any(axis=1).tolist())
+                    [int(lens.max()) if lens.size else 0], term.any(axis=1).tolist(), [e.steps for e in envs])
         return True
 
     def _step_fused(self, out_obs, out_rew, out_done):
-        _, robs, rrew, rterm, _, lens, ztrunc, lmax, rany = self._fz
+        _, robs, rrew, rterm, _, lens, ztrunc, lmax, rany, seen = self._fz
         e0 = self.envs[0]
         k = (e0._k + 1) % e0._ring
-        for e in self.envs:
+        for j, e in enumerate(self.envs):
             e._k = k
             e.steps += e.num_envs
+            seen[j] = e.steps
         obs, rew, term = robs[k], rrew[k], rterm[k]
         if out_obs is not None:
             np.copyto(out_obs.reshape(obs.shape), obs)

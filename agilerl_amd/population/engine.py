@@ -36,6 +36,7 @@ from __future__ import annotations
 import copy
 import math
 import os
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -306,8 +307,30 @@ class PopulationEngine:
             return False
         # target-KL learns: drawing the next shuffles waits for a learner's epochs
         # run (a device sync), which must not happen while launches are resident
-        return all(((g.runner.persistent and g.pop.fused_descriptor() is not None) or g.runner.graph_persistent)
-                   and g.pop.target_kl is None for g in self.groups)
+        if not all(((g.runner.persistent and g.pop.fused_descriptor() is not None) or g.runner.graph_persistent)
+                   and g.pop.target_kl is None for g in self.groups):
+            return False
+        return self.co_resident_demand() <= self._cu_count()
+
+    # partner workgroups per agent of either learner, at most (learner.hip kMaxK,
+    # graph_learner.hip kMaxGK): an agent's learn holds at most this many CUs
+    _MAX_PARTNERS = 16
+
+    def co_resident_demand(self) -> int:
+        """Workgroups that may have to be resident at the same time when the
+        groups run together: every group's persistent rollout (all of whose
+        workgroups wait on the host) and every group's partnered learner (whose
+        partners spin on each other), one CU each at most.  Within the CU count,
+        every such workgroup finds a CU however the launches interleave (the
+        other kernels all finish); above it a rollout partly resident and a
+        learner whose partners wait for its CUs could wait on each other, so
+        the groups then run one after another."""
+        return sum(int(g.runner.n_wg) + self._MAX_PARTNERS * g.pop.P for g in self.groups)
+
+    def _cu_count(self) -> int:
+        if not hasattr(self, "_cus"):
+            self._cus = int(torch.cuda.get_device_properties(self.groups[0].pop.device).multi_processor_count)
+        return self._cus
 
     def _train_paced_together(self, left: list, streams: list, pending: list, on_iteration) -> None:
         """The groups' iterations with their rollouts paced TOGETHER: each
@@ -356,7 +379,10 @@ class PopulationEngine:
                         running[k] = self.groups[k].runner.launch_running()
                 go = [k for k in live if running[k]]
                 if not go:
-                    continue  # every launch still waits for its learner (or queue): poll again
+                    # every launch still waits for its learner (or queue): yield the core
+                    # (env worker threads may need it) and poll again
+                    time.sleep(0)
+                    continue
                 for k in go:
                     self.groups[k].runner.pace_release(ctx[k])
                 for k in go:

@@ -118,12 +118,23 @@ def _pacing_end() -> None:
             lib.agx_host_free(_DEFERRED_FREES.pop())
 
 
+def _device_sync() -> None:
+    torch.cuda.synchronize()
+
+
 def _coherent(owner, nbytes: int) -> torch.Tensor:
     """Zeroed uint8 CPU tensor over agx_host_alloc memory (coherent,
     device-accessible at the same address), returned to the size pool when its
-    owner is collected (see _host_free)."""
-    pool = _HOST_POOL.get(nbytes)
+    owner is collected (see _host_free).
+
+    A pooled buffer's previous owner may still have device work queued that
+    reads or writes it (a launch's control words, a learner's skip word, a
+    tally's fin words): it is reused only after the device has drained, and
+    never inside a pacing window (where the device waits for this thread), in
+    which case a fresh buffer is allocated instead."""
+    pool = _HOST_POOL.get(nbytes) if not _PACING else None
     if pool:
+        _device_sync()
         p = pool.pop()
         ctypes.memset(p, 0, nbytes)
     else:
@@ -527,8 +538,10 @@ class PopulationRunner:
         return _IterCtx(lib, ctl, base, loss)
 
     def launch_running(self) -> bool:
-        """The current persistent rollout launch has started on the device."""
-        return bool(self._ctl_words[3])
+        """Every workgroup of the current persistent rollout launch is resident
+        (agx_rollout_ctl.started counts them): a launch only partly resident is
+        not paced, so the host never waits on workgroups that cannot start."""
+        return int(self._ctl_words[3]) >= self.n_wg
 
     def pace_release(self, c: "_IterCtx") -> None:
         c.lib.agx_host_signal(c.ctl, c.base + c.t + 1)

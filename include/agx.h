@@ -265,9 +265,10 @@ typedef struct agx_rollout_ctl {
     uint32_t timeout; /* device -> host: a workgroup stopped waiting (1:
                          timeout, 2: abort); agx_ppo_learn_args.skip_if_set */
     uint32_t nwg;     /* workgroups (set by agx_ppo_rollout_persistent)    */
-    uint32_t started; /* device -> host: set by workgroup 0 when the launch
-                         starts (the host clears it before launching): a host
-                         pacing several launches paces only running ones */
+    uint32_t started; /* device -> host: workgroups resident so far (each
+                         adds 1 when it starts; the host clears it before
+                         launching): a host pacing several launches paces
+                         only those whose nwg workgroups all run */
     /* followed by nwg uint32 done words, then (64-byte aligned) one 64-byte
      * release line per workgroup: each workgroup polls its own copy of seq */
 } agx_rollout_ctl;

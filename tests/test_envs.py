@@ -65,3 +65,31 @@ def test_restacked_blocks_keep_their_episode_lengths():
         np.testing.assert_array_equal(x[3], y[3])
         np.testing.assert_array_equal(x[0], y[0])
     assert not a._fusable() or all(e._len is v for e, v in zip(a.envs, a._fz[4]))
+
+
+def test_blocks_stepped_directly_in_lock_step_keep_truncations():
+    """Every block stepped on its own, all together (ring positions still
+    agree, so the stacked rings stay valid): the episode lengths grow in place
+    and the fused step's cached length bound must follow, or it would skip the
+    time-limit test and miss truncations."""
+    a, b = _pair(9)
+    n = a.num_envs
+    act = np.zeros(n, dtype=np.int64)
+    for s in (a, b):
+        s.reset()
+        s.step(act)
+    assert a._fz is not None
+    for _ in range(6):
+        for s in (a, b):
+            for e in s.envs:
+                e.step(np.zeros(e.num_envs, dtype=np.int64))
+    truncs = 0
+    for _ in range(12):
+        x, y = a.step(act), b.step(act)
+        assert a._fz is not None  # still the fused path
+        np.testing.assert_array_equal(x[2], y[2])
+        np.testing.assert_array_equal(x[3], y[3])
+        truncs += int(np.count_nonzero(y[3]))
+    assert truncs > 0
+    for ea, eb in zip(a.envs, b.envs):
+        np.testing.assert_array_equal(ea._len, eb._len)

@@ -10,6 +10,14 @@ import pytest
 class _FakeLib:
     def __init__(self):
         self.freed = []
+        self.bufs = []
+
+    def agx_host_alloc(self, nbytes):
+        import ctypes
+
+        b = ctypes.create_string_buffer(nbytes)
+        self.bufs.append(b)
+        return ctypes.addressof(b)
 
     def agx_host_free(self, p):
         self.freed.append(p)
@@ -24,6 +32,13 @@ def runner_mod(monkeypatch):
     monkeypatch.setattr(runner._lib, "load", lambda *a, **k: fake)
     monkeypatch.setattr(runner, "_PACING", 0)
     monkeypatch.setattr(runner, "_DEFERRED_FREES", [])
+    monkeypatch.setattr(runner, "_HOST_POOL", {})
+    fake.syncs = 0
+
+    def sync():
+        fake.syncs += 1
+
+    monkeypatch.setattr(runner, "_device_sync", sync)
     return runner, fake
 
 
@@ -64,3 +79,31 @@ def test_finalizer_of_a_collected_owner_is_deferred(runner_mod):
     assert fake.freed == []
     runner._pacing_end()
     assert fake.freed == [42]
+
+
+def test_pooled_buffer_reused_only_after_the_device_drains(runner_mod):
+    """A retired runner's staging goes back to the size pool; the next owner
+    takes it only after a device sync (queued work of the old owner may still
+    touch it), zeroed, and never while a rollout is being paced."""
+    import gc
+
+    runner, fake = runner_mod
+
+    class Owner:
+        pass
+
+    a = Owner()
+    t = runner._coherent(a, 64)
+    addr = t.data_ptr()
+    t.fill_(7)
+    del t, a
+    gc.collect()
+    assert runner._HOST_POOL[64] == [addr] and fake.syncs == 0
+    runner._pacing_begin()
+    b = Owner()
+    tb = runner._coherent(b, 64)  # inside a pacing window: a fresh buffer, no sync
+    assert tb.data_ptr() != addr and fake.syncs == 0 and runner._HOST_POOL[64] == [addr]
+    runner._pacing_end()
+    c = Owner()
+    tc = runner._coherent(c, 64)
+    assert tc.data_ptr() == addr and fake.syncs == 1 and int(tc.sum()) == 0

@@ -802,3 +802,86 @@ def test_graph_persistent_rollout_matches_per_step_launches(monkeypatch, evaluat
             out[-1].append(torch.as_tensor(fit))
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
+
+
+def _many_group_states(eng, pop):
+    """Mutate a population of 8 slots into 7 groups: the compiled shape at
+    two learn_steps and five runtime shapes (more groups than the process's
+    GPU_MAX_HW_QUEUES = 4 hardware queues)."""
+    from agilerl_amd.population.nets import ActorCriticSpec
+
+    states = eng.local_states()
+    shapes = [dict(encoder_hidden=[80], latent_dim=56, actor_hidden=[64, 64]),
+              dict(encoder_hidden=[48], latent_dim=32),
+              dict(encoder_hidden=[64, 32], latent_dim=40),
+              dict(encoder_hidden=[96], latent_dim=24, critic_hidden=[48]),
+              dict(encoder_hidden=[40], latent_dim=64, actor_hidden=[32])]
+    g = torch.Generator(device=DEV).manual_seed(17)
+    for j, kw in zip((2, 3, 4, 5, 6), shapes):
+        spec = ActorCriticSpec(obs_dim=8, n_actions=4, **kw)
+        st = states[j]
+        st.spec = spec
+        st.params = 0.1 * torch.randn(spec.n_params, device=DEV, generator=g)
+        st.exp_avg = torch.zeros(spec.n_params, device=DEV)
+        st.exp_avg_sq = torch.zeros(spec.n_params, device=DEV)
+    states[1].learn_step = states[1].learn_step // 2
+    states[7].learn_step = states[7].learn_step // 2
+    return states
+
+
+@pytest.mark.parametrize("budget", ["fits", "exceeded"])
+def test_more_groups_than_hardware_queues_train_and_evaluate(monkeypatch, budget):
+    """7 groups (5 runtime shapes + the compiled shape at two rollout lengths)
+    > GPU_MAX_HW_QUEUES: one generation's training with the groups' persistent
+    rollouts paced together (or, when the co-resident budget of rollouts +
+    partnered learners exceeds the CUs, one group after another) and the
+    population-wide evaluation complete (no agx_host_wait timeout: only
+    launches whose workgroups are ALL resident are paced) and equal the
+    one-group-after-another run bit for bit."""
+    from agilerl_amd.envs import StackedVecEnv, SyntheticVecEnv
+    from agilerl_amd.population.engine import PopulationEngine
+
+    out = []
+    for together in ("1", "0"):
+        monkeypatch.setenv("AGX_TRAIN_TOGETHER", together)
+        P, N = 8, 32
+        pop, _ = _runner_pair(monkeypatch, True, P=P, N=N)
+        envs = [SyntheticVecEnv(N, seed=70 + j, p_done=0.05, max_episode_steps=30) for j in range(P)]
+        views = [type("V", (), {"learn_step": pop.T * pop.N})() for _ in range(P)]
+        eng = PopulationEngine(pop, views, StackedVecEnv(envs))
+        eng.regroup(_many_group_states(eng, pop))
+        assert len(eng.groups) == 7
+        if budget == "exceeded":
+            monkeypatch.setattr(eng, "_cus", eng.co_resident_demand() - 1, raising=False)
+        if together == "1":
+            assert eng._paced_together() == (budget == "fits")
+        losses = eng.train(2 * pop.T * pop.N)
+        fit = eng.evaluate(1, None)
+        torch.cuda.synchronize()
+        for gr in eng.groups:
+            gr.pop.check_errors()
+        st = eng.local_states()
+        out.append(([s.params.cpu() for s in st], [s.step for s in st], [np.asarray(x) for x in losses], fit))
+    (pa, sa, la, fa), (pb, sb, lb, fb) = out
+    assert sa == sb and fa == fb and all(np.isfinite(fa))
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))
+    assert len(la) == len(lb) and all(np.array_equal(x, y) for x, y in zip(la, lb))
+
+
+def test_compiled_shape_evaluation_layer_list_matches_compiled_kernel(monkeypatch):
+    """Where the population-wide launch can run, a compiled-shape group
+    evaluates on its evaluation layer list (agx_ppo_act_graph); a full pass
+    gives the fitness of the compiled policy step (agx_ppo_act) on the same
+    counters — the samples agree (a tie within rounding between two logits
+    would be the only way to differ)."""
+    from agilerl_amd.population import runner as runner_mod
+
+    pop, run = _runner_pair(monkeypatch, False, P=4, N=32)
+    run.iteration()
+    torch.cuda.synchronize()
+    layer_list = run.evaluate(loop=2, max_steps=None)
+    pop.eval_rounds -= 1
+    monkeypatch.setattr(runner_mod, "population_eval_ok", lambda runners, paced=True: False)
+    compiled = run.evaluate(loop=2, max_steps=None)
+    assert np.all(np.isfinite(layer_list))
+    np.testing.assert_array_equal(layer_list, compiled)
