@@ -21,6 +21,7 @@ import torch
 from .. import kernels as K
 from . import checkpoint as C
 from .evolvable import EvolvableAgentMixin
+from . import learn_graph
 from .flat_state import flat_state
 from ..networks import QNetwork, RainbowQNetwork
 from ..networks.base import image_norm_bounds, is_image_space, mlp_net_config
@@ -353,45 +354,62 @@ class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
     def test(self, env, swap_channels: bool = False, max_steps: int | None = None, loop: int = 3) -> float:
         return _evaluate(self, env, lambda o: self.get_action(o, training=False), max_steps, loop)
 
-    def learn(self, experiences, n_experiences=None, per: bool = False):
-        """-> (loss, idxs, new_priorities) (dqn_rainbow.py:369-490)."""
-        to = lambda x: torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x).to(self.device)
-        get = lambda e, k: e[k]
-        n_step = n_experiences is not None
-        ex = [self._obs(get(experiences, "obs")), to(get(experiences, "action")), to(get(experiences, "reward")),
-              self._obs(get(experiences, "next_obs")), to(get(experiences, "done"))]
+    def _losses(self, xs: list, n_step: bool, per: bool):
+        """The update's loss and backward pass over xs = [obs, action, reward,
+        next_obs, done] (+ the n-step batch's five) (+ PER weights)."""
         el = None
         if self.combined_reward or not n_step:
-            el = self._dqn_loss(*ex, self.gamma)
+            el = self._dqn_loss(*xs[:5], self.gamma)
         if n_step:
-            nx = [self._obs(get(n_experiences, "obs")), to(get(n_experiences, "action")),
-                  to(get(n_experiences, "reward")), self._obs(get(n_experiences, "next_obs")),
-                  to(get(n_experiences, "done"))]
-            nl = self._dqn_loss(*nx, self.gamma ** self.n_step)
+            nl = self._dqn_loss(*xs[5:10], self.gamma ** self.n_step)
             el = el + nl if self.combined_reward else nl
-        idxs = new_priorities = None
         if per:
-            weights = to(get(experiences, "weights"))
-            idxs = get(experiences, "idxs")
             # (B,) * (B,1) broadcasts to (B,B) in the reference: mean = mean(loss) * mean(w)
-            loss = torch.mean(el * weights)
+            loss = torch.mean(el * xs[-1])
         else:
-            if n_step:
-                idxs = get(experiences, "idxs")
             loss = torch.mean(el)
         self.optimizer.zero_grad()
         loss.backward()
-        fs = flat_state(self)
-        if fs is not None and fs.step(10.0):  # clip_grad_norm_(10) + Adam: one launch (flat_state.py)
-            fs.polyak(self.tau)
-        else:
-            torch.nn.utils.clip_grad_norm_(self.actor.parameters(), 10.0)
-            self.optimizer.step()
-            self.soft_update()
-        self.actor.reset_noise()
-        self.actor_target.reset_noise()
+        return loss, el
+
+    def learn(self, experiences, n_experiences=None, per: bool = False):
+        """-> (loss, idxs, new_priorities) (dqn_rainbow.py:369-490).  The
+        device work is replayed from a captured graph from the second update
+        of a given shape on (learn_graph.py)."""
+        to = lambda x: torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x).to(self.device)
+        get = lambda e, k: e[k]
+        n_step = n_experiences is not None
+        xs = [self._obs(get(experiences, "obs")), to(get(experiences, "action")), to(get(experiences, "reward")),
+              self._obs(get(experiences, "next_obs")), to(get(experiences, "done"))]
+        if n_step:
+            xs += [self._obs(get(n_experiences, "obs")), to(get(n_experiences, "action")),
+                   to(get(n_experiences, "reward")), self._obs(get(n_experiences, "next_obs")),
+                   to(get(n_experiences, "done"))]
         if per:
-            new_priorities = el.detach().cpu().numpy() + self.prior_eps
+            xs.append(to(get(experiences, "weights")))
+        idxs = get(experiences, "idxs") if (per or n_step) else None
+        fs = flat_state(self)
+        nets = (self.actor, self.actor_target)
+        g = self.optimizer.param_groups[0]
+        key = ("rainbow", n_step, per, bool(self.combined_reward), float(self.gamma), int(self.n_step),
+               float(self.v_min), float(self.v_max), int(self.num_atoms), float(self.tau), tuple(g["betas"]),
+               float(g["eps"]))
+        out = learn_graph.run(fs, key, xs, lambda s: self._losses(s, n_step, per), nets, 10.0, self.tau)
+        if out is None:
+            loss, el = self._losses(xs, n_step, per)
+            flat_ok = fs is not None and fs.step(10.0)  # clip_grad_norm_(10) + Adam: one launch (flat_state.py)
+            if flat_ok:
+                fs.polyak(self.tau)
+            else:
+                torch.nn.utils.clip_grad_norm_(self.actor.parameters(), 10.0)
+                self.optimizer.step()
+                self.soft_update()
+            self.actor.reset_noise()
+            self.actor_target.reset_noise()
+            learn_graph.note_eager(fs, key, xs, nets, flat_ok)
+        else:
+            loss, el = out
+        new_priorities = el.detach().cpu().numpy() + self.prior_eps if per else None
         return loss.item(), idxs, new_priorities
 
     def _fresh_optimizer(self, lr_name: str):

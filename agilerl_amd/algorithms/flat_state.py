@@ -113,25 +113,42 @@ class FlatLearnState:
         unclipped ones, which nothing reads before the next zero_grad.
         False (nothing done) when a parameter has no gradient: torch's Adam
         skips such a parameter, so the caller steps the torch optimizer."""
-        grads = [p.grad for p in self.params]
-        if any(g is None for g in grads):
+        if any(p.grad is None for p in self.params):
             return False
-        torch.cat([g.reshape(-1) for g in grads], out=self.grad)
+        self.sync()
+        self.launch(max_norm)
+        self.advance()
+        return True
+
+    # step() in three parts, for a captured update (learn_graph.py): the host
+    # bookkeeping runs around every replay, only launch() is in the graph
+    def sync(self) -> None:
+        """Host -> device: a mutated learning rate, and the Adam step count when
+        the torch optimizer stepped these parameters itself."""
         g = self.opt.param_groups[0]
         lr = float(g["lr"])
         if lr != self.lr:
             self.lr = lr
             self.lr_dev.fill_(lr)
-        b1, b2 = g["betas"]
         t = int(self.step_ts[0])
         if t != self.host_step:  # the torch optimizer stepped these parameters itself
             self.steps.fill_(t)
+            self.host_step = t
+
+    def launch(self, max_norm: float) -> None:
+        """The device work: gradient gather + agx_clip_adam (its step count and
+        learning rate read from device memory)."""
+        torch.cat([p.grad.reshape(-1) for p in self.params], out=self.grad)
+        g = self.opt.param_groups[0]
+        b1, b2 = g["betas"]
         _lib.call("agx_clip_adam", self.prm.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                   1, self.n, self.offsets.data_ptr(), 1, float(max_norm), self.lr_dev.data_ptr(), float(b1),
                   float(b2), float(g["eps"]), self.steps.data_ptr(), None, self.workspace.data_ptr(), _lib.stream())
+
+    def advance(self) -> None:
+        """The torch optimizer's step tensors follow the device count."""
         torch._foreach_add_(self.step_ts, 1.0)
-        self.host_step = t + 1
-        return True
+        self.host_step += 1
 
     def polyak(self, tau: float) -> None:
         _lib.call("agx_polyak", self.tgt.data_ptr(), self.prm.data_ptr(), self.n, float(tau), _lib.stream())

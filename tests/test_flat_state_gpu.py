@@ -155,3 +155,66 @@ def test_flat_state_across_clone_checkpoint_and_lr_change(tmp_path, monkeypatch)
     for x, y in zip(d.actor.parameters(), rc.actor.parameters()):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=5e-5)
         assert int(d.optimizer.state[x]["step"]) == int(rc.optimizer.state[y]["step"]) == 6
+
+
+@pytest.mark.parametrize("per,n_step", [(True, True), (False, False)])
+def test_rainbow_cnn_update_replayed_from_graph_equals_eager(per, n_step, monkeypatch):
+    """The config-3 network (uint8 84x84x4 frames, CNN 32/64/128, dueling noisy
+    heads): updates replayed from the captured graph (learn_graph.py) equal the
+    eager updates of a twin agent bit for bit — losses, priorities,
+    parameters, Adam moments and step counts, target parameters and the noise
+    buffers — across a learning-rate mutation and a torch optimizer step
+    taken outside learn (both applied around the replay)."""
+    from agilerl_amd.algorithms import RainbowDQN, learn_graph
+    from agilerl_amd.envs import Box, Discrete
+
+    torch.manual_seed(3)
+    net = {"latent_dim": 64, "encoder_config": {"channel_size": [32, 64, 128], "kernel_size": [8, 4, 3],
+                                                "stride_size": [4, 2, 1]}, "head_config": {"hidden_size": [64]}}
+    a = RainbowDQN(Box(0, 255, (4, 84, 84), dtype=np.uint8), Discrete(6), batch_size=16, lr=1e-4, gamma=0.99,
+                   tau=1e-3, v_min=-10, v_max=10, n_step=3, net_config=net)
+    r = copy.deepcopy(a)
+    rng = np.random.default_rng(8)
+    B = 16
+
+    def batch():
+        e = {"obs": torch.as_tensor(rng.integers(0, 256, (B, 4, 84, 84), dtype=np.uint8), device="cuda"),
+             "action": torch.as_tensor(rng.integers(0, 6, (B, 1)), device="cuda"),
+             "reward": torch.as_tensor(rng.standard_normal((B, 1)).astype(np.float32), device="cuda"),
+             "next_obs": torch.as_tensor(rng.integers(0, 256, (B, 4, 84, 84), dtype=np.uint8), device="cuda"),
+             "done": torch.as_tensor((rng.random((B, 1)) < 0.2).astype(np.float32), device="cuda")}
+        if per:
+            e["weights"] = torch.as_tensor(rng.random((B, 1)).astype(np.float32), device="cuda")
+        e["idxs"] = np.arange(B)
+        return e
+
+    for it in range(5):
+        e, ne = batch(), (batch() if n_step else None)
+        if it == 3:  # a learning-rate mutation and a torch step outside learn
+            for x in (a, r):
+                for g in x.optimizer.param_groups:
+                    g["lr"] = 3e-4
+                x.optimizer.zero_grad(set_to_none=False)
+                x.optimizer.step()
+        torch.cuda.manual_seed(100 + it)
+        l1, _, p1 = a.learn(e, ne, per=per)
+        with monkeypatch.context() as mp:
+            mp.setenv("AGX_LEARN_GRAPH", "0")
+            torch.cuda.manual_seed(100 + it)
+            l2, _, p2 = r.learn(e, ne, per=per)
+        assert l1 == l2, (it, l1, l2)
+        if per:
+            np.testing.assert_array_equal(p1, p2)
+    fs = a.__dict__["_flat"]
+    assert any(ent.graph is not None for ent in learn_graph._GRAPHS.get(fs, {}).values())  # replayed
+    for (k, x), y in zip(a.actor.named_parameters(), r.actor.parameters()):
+        assert torch.equal(x, y), k
+        assert torch.equal(x.grad, y.grad), k
+        sa, sr = a.optimizer.state[x], r.optimizer.state[y]
+        assert torch.equal(sa["exp_avg"], sr["exp_avg"]) and torch.equal(sa["exp_avg_sq"], sr["exp_avg_sq"]), k
+        assert int(sa["step"]) == int(sr["step"]) == 6
+    for x, y in zip(a.actor_target.parameters(), r.actor_target.parameters()):
+        assert torch.equal(x, y)
+    for x, y in zip(list(a.actor.buffers()) + list(a.actor_target.buffers()),
+                    list(r.actor.buffers()) + list(r.actor_target.buffers())):
+        assert torch.equal(x, y)  # the same noise draws
