@@ -7,6 +7,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+import agilerl_amd  # noqa: E402,F401  (before any device call: its hardware-queue setting, agilerl_amd/__init__.py)
+
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 

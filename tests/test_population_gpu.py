@@ -806,8 +806,8 @@ def test_graph_persistent_rollout_matches_per_step_launches(monkeypatch, evaluat
 
 def _many_group_states(eng, pop):
     """Mutate a population of 8 slots into 7 groups: the compiled shape at
-    two learn_steps and five runtime shapes (more groups than the process's
-    GPU_MAX_HW_QUEUES = 4 hardware queues)."""
+    two learn_steps and five runtime shapes (more groups than HIP's default 4
+    hardware queues per process)."""
     from agilerl_amd.population.nets import ActorCriticSpec
 
     states = eng.local_states()
@@ -832,7 +832,8 @@ def _many_group_states(eng, pop):
 @pytest.mark.parametrize("budget", ["fits", "exceeded"])
 def test_more_groups_than_hardware_queues_train_and_evaluate(monkeypatch, budget):
     """7 groups (5 runtime shapes + the compiled shape at two rollout lengths)
-    > GPU_MAX_HW_QUEUES: one generation's training with the groups' persistent
+    > HIP's default 4 hardware queues (the package raises it to 8; either way
+    groups share queues with the main and evaluation streams): one generation's training with the groups' persistent
     rollouts paced together (or, when the co-resident budget of rollouts +
     partnered learners exceeds the CUs, one group after another) and the
     population-wide evaluation complete (no agx_host_wait timeout: only

@@ -13,6 +13,8 @@
 // hipcc --offload-arch=gfx950 -O2 tools/host_signal_latency.hip -o /tmp/hsl && /tmp/hsl host 4096 && /tmp/hsl vram 4096
 #include <hip/hip_runtime.h>
 
+#include <immintrin.h>
+
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -87,7 +89,9 @@ int main(int argc, char **argv) {
     for (int i = 1; i <= iters && ok; ++i) {
         if (i == 101) t0 = std::chrono::steady_clock::now();  // 100 warm-up steps
         memcpy(payload, stage, pay_bytes);
+        if (vram) _mm_sfence();  // write-combined BAR: the payload lands before the release word
         std::atomic_ref<unsigned>(*rel).store((unsigned)i, std::memory_order_release);
+        if (vram) _mm_sfence();  // ... and the release word leaves the write-combining buffer now
         const auto w0 = std::chrono::steady_clock::now();
         for (;;) {
             const unsigned d = std::atomic_ref<unsigned>(*done_h).load(std::memory_order_acquire);
