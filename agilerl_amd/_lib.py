@@ -159,8 +159,12 @@ def ptr(t) -> int | None:
 
 
 def stream(s=None) -> int:
-    s = torch.cuda.current_stream() if s is None else s
-    return s.cuda_stream
+    """hipStream_t of ``s`` (default: torch's current stream on the current
+    device).  Read through torch's raw accessor: torch.cuda.current_stream()
+    builds a Stream object per call (~2 us of host time on every launch)."""
+    if s is not None:
+        return s.cuda_stream
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def call(name: str, *args) -> None:

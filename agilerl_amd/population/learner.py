@@ -194,7 +194,7 @@ class FusedLearner:
             self.dref = ctypes.byref(self.desc)
         self.args.perms = perms.data_ptr()
         self.args.skip_if_set = skip_if_set
-        rc = self.fn(self.dref, self.aref, self.ws.data_ptr(), torch.cuda.current_stream(pop.device).cuda_stream)
+        rc = self.fn(self.dref, self.aref, self.ws.data_ptr(), _lib.stream())
         if rc != 0:
             _lib.check(rc, "agx_ppo_learn")
         return self.loss

@@ -286,20 +286,23 @@ class PPOPopulation:
         self.values[:, t].copy_(value, non_blocking=True)
         self.log_probs[:, t].copy_(logp, non_blocking=True)
 
-    @torch.no_grad()
     def finish_rollout(self, last_obs: torch.Tensor, last_done: torch.Tensor,
                        last_value: torch.Tensor | None = None):
         """Bootstrap value + GAE (+ per-agent advantage statistics).  The fused
         runner computes last_value in its final rollout-step launch."""
         self.rollout_id += 1
         if last_value is None:
-            _, last_value = self.spec.forward(self.params.data, last_obs)
-        last_value, last_done = last_value.contiguous(), last_done.contiguous()
+            with torch.no_grad():
+                _, last_value = self.spec.forward(self.params.data, last_obs)
+        if not last_value.is_contiguous():
+            last_value = last_value.contiguous()
+        if not last_done.is_contiguous():
+            last_done = last_done.contiguous()
         key = (last_value.data_ptr(), last_done.data_ptr(), last_value.shape, last_done.dtype,
                *(t.data_ptr() for t in (self.rewards, self.dones, self.values, self.advantages, self.returns,
                                         self.adv_stats, self.gae_ws)))
         if self._gae_launch is not None and self._gae_launch[0] == key:
-            self._gae_launch[1](torch.cuda.current_stream(self.device).cuda_stream)
+            self._gae_launch[1](_lib.stream())  # the runner's steady state: one cached launch
             return
         launch = K.gae_launcher(self.rewards, self.dones, self.values, last_value, last_done, self.gamma,
                                 self.gae_lambda, True, self.advantages, self.returns, self.adv_stats, self.gae_ws)
@@ -513,7 +516,7 @@ class PPOPopulation:
             perms, ev, state = self._perm_next[:3]
             self._perm_next = None
             self._perm_drawn_state = state
-            main = torch.cuda.current_stream(self.device)
+            main = torch.cuda.current_stream()
             if ev is not None:
                 main.wait_event(ev)
             perms.record_stream(main)  # (a block row: the block stays allocated until this stream is past it)

@@ -386,7 +386,10 @@ class PopulationRunner:
         # stream-ordered after the rollout kernel, which ends only after the
         # host's final release — by then the last env step has written term_h
         self.last_value_valid = True
-        self.last_done.view(-1).copy_(self.term_h.view(torch.uint8), non_blocking=True)  # last_done = term (:196)
+        v = self.__dict__.get("_done_views")
+        if v is None:
+            v = self._done_views = (self.last_done.view(-1), self.term_h.view(torch.uint8))
+        v[0].copy_(v[1], non_blocking=True)  # last_done = term (:196)
 
     @torch.no_grad()
     def _collect_torch(self) -> None:

@@ -50,6 +50,10 @@ wrap(R.PopulationRunner, "begin_iteration", "begin_iteration")
 wrap(R.PopulationRunner, "end_iteration", "end_iteration")
 wrap(R.PopulationRunner, "pace_wait_step", "pace_wait_step")
 wrap(R.PopulationRunner, "_env_step", "env_step")
+wrap(R.PopulationRunner, "_finish_persistent", "finish_persistent")
+wrap(R.PopulationRunner, "_mark_stats", "mark_stats")
+wrap(R.PopulationRunner, "launch_running", "launch_running")
+wrap(R.PopulationRunner, "pace_release", "pace_release")
 
 if __name__ == "__main__":
     out = bench.train_on_policy_leg(generations=3)

@@ -28,3 +28,16 @@ span = (k[-1][1] - k[0][0]) if k else 0
 print(f"learn kernels {len(learn)}, total {sum(e - s for s, e, _, _ in learn) / 1e6:.2f} ms, pairwise overlap "
       f"{ov / 1e6:.2f} ms, trace span {span / 1e6:.1f} ms; queues {sorted({q for _, _, q, _ in learn})}, "
       f"streams {sorted({st for _, _, _, st in learn})}")
+# per queue: kernel-busy time, the persistent rollouts' share, and the idle gaps
+byq = collections.defaultdict(list)
+for s, e, n, q, st in k:
+    byq[q].append((s, e, n))
+for q in sorted(byq):
+    ks = byq[q]
+    busy = sum(e - s for s, e, _ in ks)
+    roll = sum(e - s for s, e, n in ks if "persistent" in n)
+    lrn = sum(e - s for s, e, n in ks if "learn" in n and "gather" not in n)
+    gaps = sorted(ks[i + 1][0] - ks[i][1] for i in range(len(ks) - 1))
+    big = sum(g for g in gaps if g > 20000)
+    print(f"queue {q}: {len(ks)} kernels, busy {busy / 1e6:.1f} ms (rollout {roll / 1e6:.1f}, learn {lrn / 1e6:.1f}), "
+          f"span {(ks[-1][1] - ks[0][0]) / 1e6:.1f} ms, gaps > 20 us {big / 1e6:.1f} ms")
