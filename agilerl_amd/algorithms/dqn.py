@@ -23,6 +23,7 @@ from . import checkpoint as C
 from .evolvable import EvolvableAgentMixin
 from . import learn_graph
 from .flat_state import flat_state
+from ..modules.custom_components import noisy_scope
 from ..networks import QNetwork, RainbowQNetwork
 from ..networks.base import image_norm_bounds, is_image_space, mlp_net_config
 
@@ -358,11 +359,12 @@ class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
         """The update's loss and backward pass over xs = [obs, action, reward,
         next_obs, done] (+ the n-step batch's five) (+ PER weights)."""
         el = None
-        if self.combined_reward or not n_step:
-            el = self._dqn_loss(*xs[:5], self.gamma)
-        if n_step:
-            nl = self._dqn_loss(*xs[5:10], self.gamma ** self.n_step)
-            el = el + nl if self.combined_reward else nl
+        with noisy_scope():  # each noisy layer's mu + sigma * eps formed once for the update's forwards
+            if self.combined_reward or not n_step:
+                el = self._dqn_loss(*xs[:5], self.gamma)
+            if n_step:
+                nl = self._dqn_loss(*xs[5:10], self.gamma ** self.n_step)
+                el = el + nl if self.combined_reward else nl
         if per:
             # (B,) * (B,1) broadcasts to (B,B) in the reference: mean = mean(loss) * mean(w)
             loss = torch.mean(el * xs[-1])

@@ -118,8 +118,7 @@ def run(fs, key: tuple, inputs: list, body, nets: tuple, max_norm: float, tau: f
         ent.graph, ent.inputs, ent.outputs = g, statics, outs
         ent.grads = [p.grad for p in fs.params]
     else:
-        for s, x in zip(ent.inputs, inputs):
-            s.copy_(x, non_blocking=True)
+        torch._foreach_copy_(ent.inputs, inputs)  # the batch into the static inputs: one launch for all
     fs.sync()
     ent.graph.replay()
     fs.advance()

@@ -49,6 +49,44 @@ def reset_noise_layers(layers: list) -> None:
         K.noisy_reset_(batch)
 
 
+# noisy weights formed once per update (noisy_scope): NoisyLinear -> (W, b)
+_SCOPE: dict | None = None
+
+
+class noisy_scope:
+    """Within one update the parameters and noise of every NoisyLinear are
+    fixed, and the reference's update runs the online network twice (on s'
+    for a*, on s for the loss) and the target once: inside this scope each
+    layer forms mu + sigma * eps once and reuses it (the same tensors the
+    repeated forwards would compute, so results are bit-identical; the
+    gradient path goes through _NoisyParam).  RainbowDQN._losses opens it."""
+
+    def __enter__(self):
+        global _SCOPE
+        self._prev, _SCOPE = _SCOPE, {}
+        return self
+
+    def __exit__(self, *exc):
+        global _SCOPE
+        _SCOPE = self._prev
+        return False
+
+
+class _NoisyParam(torch.autograd.Function):
+    """mu + sigma * eps already formed (``w``): forward returns it; backward is
+    autograd's for the expression (d mu = g, d sigma = g * eps)."""
+
+    @staticmethod
+    def forward(ctx, mu, sigma, eps, w):
+        ctx.save_for_backward(eps)
+        return w.view_as(w)
+
+    @staticmethod
+    def backward(ctx, g):
+        (eps,) = ctx.saved_tensors
+        return g, g * eps, None, None
+
+
 class NoisyLinear(nn.Module):
     """Factorised-Gaussian noisy linear layer (custom_components.py:38-131):
     mu ~ U(+-1/sqrt(in)), sigma = std_init/sqrt(in) (weights) and
@@ -85,6 +123,16 @@ class NoisyLinear(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.training:
-            return F.linear(x, self.weight_mu + self.weight_sigma * self.weight_epsilon,
-                            self.bias_mu + self.bias_sigma * self.bias_epsilon)
+            if _SCOPE is None:
+                return F.linear(x, self.weight_mu + self.weight_sigma * self.weight_epsilon,
+                                self.bias_mu + self.bias_sigma * self.bias_epsilon)
+            wb = _SCOPE.get(id(self))
+            if wb is None:
+                with torch.no_grad():
+                    wb = _SCOPE[id(self)] = (self.weight_mu + self.weight_sigma * self.weight_epsilon,
+                                             self.bias_mu + self.bias_sigma * self.bias_epsilon)
+            if torch.is_grad_enabled():
+                return F.linear(x, _NoisyParam.apply(self.weight_mu, self.weight_sigma, self.weight_epsilon, wb[0]),
+                                _NoisyParam.apply(self.bias_mu, self.bias_sigma, self.bias_epsilon, wb[1]))
+            return F.linear(x, wb[0], wb[1])
         return F.linear(x, self.weight_mu, self.bias_mu)

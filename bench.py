@@ -988,7 +988,7 @@ def train_on_policy_leg(generations: int = 3, P: int = 8, N: int = 128):
     return out
 
 
-def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15):
+def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15, on_timed=None):
     """Config 3 (Atari Pong Rainbow DQN, pop 8): learner updates/s of the
     population-batched learner (algorithms/rainbow_pop.py) on uint8 4x84x84
     frames, CNN 32/64/128 -> 256, dueling noisy heads [256], A = 6, Z = 51 on
@@ -997,7 +997,9 @@ def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15):
     the P agents' samples in one draw (the same torch.rand stream as P
     draws), one batched learn, the P priority updates in agent order.  The
     per-agent loop of the reference (sample, agent.learn, update per agent)
-    is timed on copies of the same agents beside it."""
+    is timed on copies of the same agents beside it.  ``on_timed(name,
+    start)``: called right before / after each timed loop (profiling markers,
+    tools/prof_config3.py)."""
     from agilerl_amd.algorithms import RainbowDQN
     from agilerl_amd.algorithms.rainbow_pop import RainbowPopulationLearner
     from agilerl_amd.components import PrioritizedReplayBuffer
@@ -1043,11 +1045,15 @@ def config3_leg(iters: int = 10, P: int = 8, B: int = 64, fill: int = 1 << 15):
         for _ in range(2):
             fn()
         torch.cuda.synchronize()
+        if on_timed is not None:
+            on_timed(name, True)
         t0 = time.perf_counter()
         for _ in range(iters):
             fn()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        if on_timed is not None:
+            on_timed(name, False)
         out[name] = {"learner_updates_per_s": round(P * iters / dt, 1), "ms_per_iteration": round(dt / iters * 1e3, 3)}
     # the headline is what the drop-in entry point runs: train_off_policy learns
     # agent after agent (the reference's train_off_policy.py:355-429); the
