@@ -51,8 +51,11 @@ __global__ void pong(unsigned *rel, const float *payload, int pay_n, unsigned *d
             if (threadIdx.x == 0) __hip_atomic_store(done, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
-        for (int j = threadIdx.x; j < pay_n; j += blockDim.x)
-            acc += __hip_atomic_load(payload + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // the payload of step i is (float)(i + j): count reads that are not (stale data)
+        for (int j = threadIdx.x; j < pay_n; j += blockDim.x) {
+            const float v = __hip_atomic_load(payload + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            acc += v != (float)(i + j) ? 1.f : 0.f;
+        }
         __syncthreads();
         if (threadIdx.x == 0) __hip_atomic_store(done, (unsigned)i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -88,6 +91,7 @@ int main(int argc, char **argv) {
     bool ok = true;
     for (int i = 1; i <= iters && ok; ++i) {
         if (i == 101) t0 = std::chrono::steady_clock::now();  // 100 warm-up steps
+        for (int j = 0; j < pay_n; ++j) stage[j] = (float)(i + j);
         memcpy(payload, stage, pay_bytes);
         if (vram) _mm_sfence();  // write-combined BAR: the payload lands before the release word
         std::atomic_ref<unsigned>(*rel).store((unsigned)i, std::memory_order_release);
@@ -109,7 +113,12 @@ int main(int argc, char **argv) {
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (!ok) std::atomic_ref<unsigned>(*rel).store(0x7FFFFFFFu, std::memory_order_release);  // let the kernel finish
     CK(hipDeviceSynchronize());
-    printf("mode %s payload %d B: %s, %.2f us per round trip over %d steps\n", vram ? "vram" : "host", pay_bytes,
-           ok ? "ok" : "TIMEOUT", 1e6 * dt / (iters - 100), iters - 100);
+    float hs[256];
+    CK(hipMemcpy(hs, sink, sizeof(hs), hipMemcpyDeviceToHost));
+    double stale = 0;
+    for (int t = 0; t < 256; ++t) stale += hs[t];
+    printf("mode %s payload %d B: %s, %.2f us per round trip over %d steps (host step includes writing the payload); "
+           "stale payload words read: %.0f\n", vram ? "vram" : "host", pay_bytes, ok ? "ok" : "TIMEOUT",
+           1e6 * dt / (iters - 100), iters - 100, stale);
     return ok ? 0 : 1;
 }
