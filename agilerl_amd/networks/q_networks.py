@@ -14,6 +14,7 @@ import torch
 from torch.nn import functional as F
 
 from ..modules.mlp import EvolvableMLP, create_mlp
+from ..modules.noisy_streams import head_streams
 from .base import EvolvableNetwork, as_config, flatdim, is_image_space, mlp_net_config
 
 
@@ -142,8 +143,12 @@ class DuelingDistributionalMLP(EvolvableMLP):
 
     def forward(self, x: torch.Tensor, q: bool = True, log: bool = False, rows: torch.Tensor | None = None):
         """rows (int64 [B], q=False): only action rows[b]'s distribution, [B, Z]."""
-        value = self.model(x)
-        advantage = self.advantage_net(x)
+        fused = head_streams([self.model, self.advantage_net], x)  # both streams, one launch per depth
+        if fused is not None:
+            value, advantage = fused
+        else:
+            value = self.model(x)
+            advantage = self.advantage_net(x)
         if rows is not None and q:
             raise ValueError("rows selects distributions: pass q=False")
         if rows is not None and value.is_cuda and self.num_atoms <= 64 and value.dtype == torch.float32:

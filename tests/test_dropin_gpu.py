@@ -3,6 +3,8 @@ test), create_population + train_on_policy with tournament selection, and
 DQN.learn against a plain-PyTorch DQN update from the same weights
 (dqn.py:274-348)."""
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -205,7 +207,21 @@ def test_dqn_learn_matches_torch_update():
 
 def _rainbow_reference_loss(agent, actor, target, exp, gamma, per):
     """The reference's _dqn_loss + learn loss in plain PyTorch
-    (dqn_rainbow.py:284-367, 369-440) on the given networks."""
+    (dqn_rainbow.py:284-367, 369-440) on the given networks (their head
+    streams as torch modules: AGX_NOISY_STREAMS=0 for the forward; autograd
+    keeps the torch ops it recorded)."""
+    old = os.environ.get("AGX_NOISY_STREAMS")
+    os.environ["AGX_NOISY_STREAMS"] = "0"
+    try:
+        return _rainbow_reference_loss_torch(agent, actor, target, exp, gamma, per)
+    finally:
+        if old is None:
+            del os.environ["AGX_NOISY_STREAMS"]
+        else:
+            os.environ["AGX_NOISY_STREAMS"] = old
+
+
+def _rainbow_reference_loss_torch(agent, actor, target, exp, gamma, per):
     dev = agent.device
     o = torch.as_tensor(exp["obs"], device=dev)
     no = torch.as_tensor(exp["next_obs"], device=dev)
