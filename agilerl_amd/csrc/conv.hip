@@ -35,7 +35,10 @@ namespace agx {
 
 namespace conv {
 
-constexpr int BK = 16, NT = 256, kTab = 1024, kTapMax = 16;
+#ifndef AGX_CONV_BK
+#define AGX_CONV_BK 16
+#endif
+constexpr int BK = AGX_CONV_BK, NT = 256, kTab = 1024, kTapMax = 16;
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 struct Shape {
@@ -129,9 +132,13 @@ struct FwdOps {
             rb[i] = (c.xbase >= 0 && kk < k1) ? ld_xt<U8>(x, c.xbase + sm.tabB[kk - kc], sm) : 0.f;
         }
     }
-    __device__ void store(int m, int n, float v, int) const {
+    // the epilogue reads a lane's eight row biases up front (unconditional,
+    // clamped), not one dependent load per stored element
+    static constexpr bool kBias = true;
+    __device__ float row_bias(int m) const { return bias ? bias[m < M ? m : M - 1] : 0.f; }
+    __device__ void store(int m, int n, float v, int, float b) const {
         if (m >= M || n >= N) return;
-        if (bias) v += bias[m];
+        if (bias) v += b;
         if (relu) v = v > 0.f ? v : 0.f;
         const int ow = n % s.OW, t2 = n / s.OW, oh = t2 % s.OH, bb = t2 / s.OH;
         y[(((size_t)bb * s.Cout + m) * s.OH + oh) * s.OW + ow] = v;
@@ -161,7 +168,8 @@ struct WgradOps {
     // db (column N - 1) is the row sum of the A operand (dZ), taken from LDS by
     // the n_blk == 0 tiles: a GEMM ones column would cost a whole extra column
     // tile (re-gathering all of A) when Cin*KH*KW is a multiple of the tile width
-    static constexpr bool kRowSum = true, kCols = false, kLut = U8;
+    static constexpr bool kRowSum = true, kCols = false, kLut = U8, kBias = false;
+    __device__ float row_bias(int) const { return 0.f; }
     static constexpr int kTabN = kTab;
     struct Ctx {
         int koff;  // im2col offset of this thread's weight column, -1 past the weights
@@ -255,7 +263,8 @@ struct DgradOps {
         return o;
     }
     __device__ int kend(int) const { return K; }  // this phase's taps (0: zeros)
-    static constexpr bool kRowSum = false, kCols = true, kLut = false;
+    static constexpr bool kRowSum = false, kCols = true, kLut = false, kBias = false;
+    __device__ float row_bias(int) const { return 0.f; }
     static constexpr int kTabN = kTab / 2;  // with the tap table: 4 (32x128) / 5 (64x64) workgroups per CU
     struct Ctx {
         int dbase;  // dy offset of this thread's image (channel 0), -1 past N
@@ -364,9 +373,13 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
     typename Ops::Ctx ctx;
     ops.setup(ctx, sm, tid % BN, n_blk + tid % BN, tid);
     float ra[NA], rb[NB];
+    // As columns are XOR-swizzled by k (swz): the stash writes (16 k rows x 4
+    // columns per wave) and the MFMA operand reads (4 k rows x 16 columns) both
+    // land in 64 distinct banks
+    auto swz = [](int k) { return ((k >> 2) & 3) << 2; };
     auto stash = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < NA; ++i) sm.As[buf][tid % BK][tid / BK + i * (NT / BK)] = ra[i];
+        for (int i = 0; i < NA; ++i) sm.As[buf][tid % BK][(tid / BK + i * (NT / BK)) ^ swz(tid % BK)] = ra[i];
 #pragma unroll
         for (int i = 0; i < NB; ++i) sm.Bs[buf][tid / BN + i * (NT / BN)][tid % BN] = rb[i];
     };
@@ -393,7 +406,8 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
             if (more) ops.template gather<NA, NB, BN>(ctx, sm, m_blk, kc, kb + BK, kce, tid, ra, rb);
 #pragma unroll
             for (int kk = 0; kk < BK; kk += 4) {
-                const float a0 = sm.As[buf][kk + q][wm + r], a1 = sm.As[buf][kk + q][wm + 16 + r];
+                const int sw = swz(kk + q);
+                const float a0 = sm.As[buf][kk + q][(wm + r) ^ sw], a1 = sm.As[buf][kk + q][(wm + 16 + r) ^ sw];
                 const float b0 = sm.Bs[buf][kk + q][wn + r], b1 = sm.Bs[buf][kk + q][wn + 16 + r];
                 acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
                 acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
@@ -403,7 +417,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
             if constexpr (Ops::kRowSum)
                 if (rsum) {
 #pragma unroll
-                    for (int kk = 0; kk < BK; ++kk) rs += sm.As[buf][kk][tid];
+                    for (int kk = 0; kk < BK; ++kk) rs += sm.As[buf][kk][tid ^ swz(kk)];
                 }
             if (more) {
                 stash(buf ^ 1);
@@ -413,6 +427,11 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
         }
     }
     // C layout: lane holds rows 4q + i, column r of each 16x16 tile
+    float rb_[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) rb_[i][e] = ops.row_bias(m_blk + wm + 16 * i + 4 * q + e);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -420,8 +439,11 @@ __global__ __launch_bounds__(NT) void igemm_kernel(Ops ops_g, int k0, int k1, in
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int n = n_blk + wn + 16 * j + r;
-                if (!Ops::kRowSum || n < ops.N - 1)  // column N - 1 (db) belongs to the row sums
+                if constexpr (Ops::kBias) {
+                    ops.store(m_blk + wm + 16 * i + 4 * q + e, n, acc[i][j][e], split, rb_[i][e]);
+                } else if (!Ops::kRowSum || n < ops.N - 1) {  // column N - 1 (db) belongs to the row sums
                     ops.store(m_blk + wm + 16 * i + 4 * q + e, n, acc[i][j][e], split);
+                }
             }
     if constexpr (Ops::kRowSum)
         if (rsum) ops.store(m_blk + tid, ops.N - 1, rs, split);

@@ -22,9 +22,15 @@
 //   LayerNorm + ReLU backward of the gradient of its activation, recomputed
 //   in the loads from per-row statistics (mean, rstd and the two row sums
 //   of the LayerNorm backward).
-// Row statistics are always computed by one wave over the row in the same
-// order (row_stats / row_bwd_sums), and y = xhat * gamma + beta is rounded
-// explicitly, so the ReLU mask the backward recomputes is the forward's.
+// Row statistics never take a pass over a row: the workgroup that writes a
+// 16-feature tile of a hidden output also writes that tile's mean and sum of
+// squared deviations per row (ln_part), and the role-X workgroup that writes
+// a tile of a hidden activation's gradient writes that tile's two
+// LayerNorm-backward sums; a consumer combines a row's tiles in tile order
+// (Chan's pairwise update for the moments).  Forward and backward read the
+// same partials through the same code, and y = xhat * gamma + beta is
+// rounded explicitly, so the ReLU mask the backward recomputes is the
+// forward's.
 #include <cstdint>
 
 #include "agx_common.h"
@@ -40,12 +46,16 @@ constexpr int kRows = AGX_NOISY_MAX_ROWS;
 
 struct Layer {
     const float *in, *in_g, *in_b;  // input [B][K]; in_g: the input is relu(LN(in) * in_g + in_b)
+    const float *in_part;           // LN statistics tiles of in [B][ceil(K/16)][2] (with in_g)
     const float *w_mu, *w_sig, *w_eps, *b_mu, *b_sig, *b_eps;
     float *out;                     // [B][N]
+    float *out_part;                // hidden layers: LN statistics tiles of out [B][ceil(N/16)][2]
     const float *dsrc;              // backward: d/d out (out_g == null) or d/d relu(LN(out)) [B][N]
     const float *out_g, *out_b;     // LayerNorm affine of this layer's output (hidden layers)
+    const float *s_part;            // backward, hidden layers: LN-backward sum tiles of dsrc [B][ceil(N/16)][2]
     float *gw_mu, *gw_sig, *gb_mu, *gb_sig, *g_g, *g_b;
     float *din;                     // role X output [B][K] (null: none)
+    float *din_part;                // role X, with in_g: LN-backward sum tiles of din [B][ceil(K/16)][2]
     int K, N, tiles_w, tiles_x;
 };
 
@@ -68,47 +78,88 @@ __device__ __forceinline__ float bval(const Layer &L, int n) {
 __device__ __forceinline__ float ln_xhat(float h, float mu, float rs) { return __fmul_rn(__fsub_rn(h, mu), rs); }
 __device__ __forceinline__ float ln_y(float xhat, float g, float b) { return __fadd_rn(__fmul_rn(xhat, g), b); }
 
-// mean and rstd of one row of length K, by one wave (every lane returns lane 0's values)
-__device__ __forceinline__ void row_stats(const float *row, int K, float eps, int lane, float &mu, float &rs) {
-    float s = 0.f;
-    for (int k = lane; k < K; k += 64) s += row[k];
-    mu = __shfl(wave_sum(s), 0, 64) / (float)K;
-    float v = 0.f;
-    for (int k = lane; k < K; k += 64) {
-        const float d = __fsub_rn(row[k], mu);
-        v = __fmaf_rn(d, d, v);
+// a row's mean and rstd from its tiles' (mean, M2), combined in tile order
+// (eight tiles' loads in flight at a time)
+__device__ __forceinline__ void ln_stats(const float *part, int N, float eps, float &mu, float &rs) {
+    const int T = (N + 15) >> 4;
+    float na = 0.f, ma = 0.f, qa = 0.f;
+    for (int t0 = 0; t0 < T; t0 += 8) {
+        float mb[8], qb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int t = min(t0 + j, T - 1);
+            mb[j] = part[2 * t];
+            qb[j] = part[2 * t + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int t = t0 + j;
+            if (t >= T) break;
+            const float nb = (float)min(16, N - 16 * t);
+            if (t == 0) {
+                na = nb;
+                ma = mb[j];
+                qa = qb[j];
+            } else {
+                const float n = na + nb, d = mb[j] - ma;
+                ma = ma + d * (nb / n);
+                qa = (qa + qb[j]) + (d * d) * (na * nb / n);
+                na = n;
+            }
+        }
     }
-    v = __shfl(wave_sum(v), 0, 64) / (float)K;
-    rs = __frsqrt_rn(__fadd_rn(v, eps));
+    mu = ma;
+    rs = __frsqrt_rn(qa / (float)N + eps);
 }
 
-// LayerNorm + ReLU backward of a row: with g = da * [y > 0] * gamma, s1 = sum g, s2 = sum g * xhat
-__device__ __forceinline__ void row_bwd_sums(const float *h, const float *da, const float *gam, const float *bet, int N,
-                                             float mu, float rs, int lane, float &s1, float &s2) {
-    float a1 = 0.f, a2 = 0.f;
-    for (int n = lane; n < N; n += 64) {
-        const float xh = ln_xhat(h[n], mu, rs);
-        const float gx = ln_y(xh, gam[n], bet[n]) > 0.f ? __fmul_rn(da[n], gam[n]) : 0.f;
-        a1 += gx;
-        a2 = __fmaf_rn(gx, xh, a2);
+// a row's LayerNorm-backward sums (s1 = sum g, s2 = sum g * xhat, g = da * [y > 0] * gamma) from its tiles
+__device__ __forceinline__ void ln_sums(const float *part, int N, float &s1, float &s2) {
+    const int T = (N + 15) >> 4;
+    float a = 0.f, b = 0.f;
+    for (int t0 = 0; t0 < T; t0 += 8) {
+        float pa[8], pb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int t = min(t0 + j, T - 1);
+            pa[j] = part[2 * t];
+            pb[j] = part[2 * t + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (t0 + j >= T) break;
+            a += pa[j];
+            b += pb[j];
+        }
     }
-    s1 = __shfl(wave_sum(a1), 0, 64);
-    s2 = __shfl(wave_sum(a2), 0, 64);
+    s1 = a;
+    s2 = b;
+}
+
+__device__ __forceinline__ float ln_relu_g(float xh, float da, float gam, float bet) {
+    return ln_y(xh, gam, bet) > 0.f ? __fmul_rn(da, gam) : 0.f;
 }
 
 // d/d out[b][n] of a hidden layer from the gradient of its activation
 __device__ __forceinline__ float ln_relu_bwd(float h, float da, float gam, float bet, float mu, float rs, float s1,
                                              float s2, float invN) {
     const float xh = ln_xhat(h, mu, rs);
-    const float gx = ln_y(xh, gam, bet) > 0.f ? __fmul_rn(da, gam) : 0.f;
+    const float gx = ln_relu_g(xh, da, gam, bet);
     return rs * ((gx - s1 * invN) - xh * (s2 * invN));
+}
+
+// one 16-lane group's tile partials of a row (lane group = lanes with equal lane >> 4), value v valid if ok
+__device__ __forceinline__ void tile_moments(float v, bool ok, int cnt, int lane, float &m, float &q2) {
+    const float s = group_sum<16>(ok ? v : 0.f);
+    m = __shfl(s, lane & ~15, 64) / (float)cnt;
+    const float d = ok ? v - m : 0.f;
+    q2 = __shfl(group_sum<16>(d * d), lane & ~15, 64);
 }
 
 __device__ __forceinline__ Layer pick(const Level &lv, int s) { return s == 0 ? lv.s[0] : lv.s[1]; }
 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
-    __shared__ float st_mu[16], st_rs[16];
+    __shared__ float st[2][16];
     __shared__ f32x4 red[3][64];
     int blk = blockIdx.x, si = 0;
     if (blk >= lv.s[0].tiles_w) {
@@ -122,35 +173,58 @@ __global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool ln = L.in_g != nullptr;
     if (ln) {
-        for (int i = wave * 4; i < wave * 4 + 4; ++i) {
+        if (threadIdx.x < 16) {
+            const int b = b0 + threadIdx.x;
             float mu = 0.f, rs = 0.f;
-            if (b0 + i < B) row_stats(L.in + (int64_t)(b0 + i) * K, K, lv.eps, lane, mu, rs);
-            if (lane == 0) {
-                st_mu[i] = mu;
-                st_rs[i] = rs;
-            }
+            if (b < B) ln_stats(L.in_part + (int64_t)b * (((K + 15) >> 4) * 2), K, lv.eps, mu, rs);
+            st[0][threadIdx.x] = mu;
+            st[1][threadIdx.x] = rs;
         }
         __syncthreads();
     }
     const int r = b0 + (lane & 15), n = n0 + (lane & 15), q = lane >> 4;
     const bool rok = r < B, nok = n < N;
-    const float mu = ln ? st_mu[lane & 15] : 0.f, rs = ln ? st_rs[lane & 15] : 0.f;
+    const float mu = ln ? st[0][lane & 15] : 0.f, rs = ln ? st[1][lane & 15] : 0.f;
+    // every load below is unconditional (indices clamped, pointers selected
+    // uniformly), so a wave issues all of them before the first wait
     const float *xrow = L.in + (int64_t)(rok ? r : 0) * K;
     const int64_t wrow = (int64_t)(nok ? n : 0) * K;
+    const bool noisy = L.w_sig != nullptr;
+    const float *wsig = noisy ? L.w_sig : L.w_mu, *weps = noisy ? L.w_eps : L.w_mu;
+    const float *ing = ln ? L.in_g : L.w_mu, *inb = ln ? L.in_b : L.w_mu;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int kb = wave * 16; kb < K; kb += 64) {
-        float a[4], w[4];
+    for (int kc = wave * 16; kc < K; kc += 256) {  // four 16-deep k blocks of this wave in flight
+        float xv[4][4], wm[4][4], ws[4][4], we[4][4], gg[4][4], gb[4][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int k = kb + 4 * q + j;
-            const bool kok = k < K;
-            float xv = (rok && kok) ? xrow[k] : 0.f;
-            if (ln && rok && kok) xv = fmaxf(ln_y(ln_xhat(xv, mu, rs), L.in_g[k], L.in_b[k]), 0.f);
-            a[j] = xv;
-            w[j] = (nok && kok) ? wval(L, wrow + k) : 0.f;
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kk = min(kc + 64 * u + 4 * q + j, K - 1);
+                xv[u][j] = xrow[kk];
+                wm[u][j] = L.w_mu[wrow + kk];
+                ws[u][j] = wsig[wrow + kk];
+                we[u][j] = weps[wrow + kk];
+                gg[u][j] = ing[kk];
+                gb[u][j] = inb[kk];
+            }
+        }
+        float a[4][4], w[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool kok = kc + 64 * u + 4 * q + j < K;
+                float x = xv[u][j];
+                if (ln) x = fmaxf(ln_y(ln_xhat(x, mu, rs), gg[u][j], gb[u][j]), 0.f);
+                a[u][j] = (rok && kok) ? x : 0.f;
+                const float wf = noisy ? __fadd_rn(wm[u][j], __fmul_rn(ws[u][j], we[u][j])) : wm[u][j];
+                w[u][j] = (nok && kok) ? wf : 0.f;
+            }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], w[j], acc, 0, 0, 0);
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][j], w[u][j], acc, 0, 0, 0);
     }
     if (wave) red[wave - 1][lane] = acc;
     __syncthreads();
@@ -158,12 +232,22 @@ __global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
 #pragma unroll
         for (int w = 0; w < 3; ++w) acc += red[w][lane];
         const int col = n0 + (lane & 15);
-        if (col < N) {
-            const float bias = bval(L, col);
+        const bool cok = col < N;
+        const float bias = cok ? bval(L, col) : 0.f;
+        const int T = (N + 15) >> 4, cnt = min(16, N - n0);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = b0 + 4 * q + i;
-                if (row < B) L.out[(int64_t)row * N + col] = acc[i] + bias;
+        for (int i = 0; i < 4; ++i) {
+            const int row = b0 + 4 * q + i;
+            const float v = acc[i] + bias;
+            if (row < B && cok) L.out[(int64_t)row * N + col] = v;
+            if (L.out_part) {
+                float m, q2;
+                tile_moments(v, cok, cnt, lane, m, q2);
+                if ((lane & 15) == 0 && row < B) {
+                    float *p = L.out_part + ((int64_t)row * T + (n0 >> 4)) * 2;
+                    p[0] = m;
+                    p[1] = q2;
+                }
             }
         }
     }
@@ -173,32 +257,29 @@ __global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
 // role W: 16 output features x 64 input features of one stream's layer
 __device__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
     __shared__ float tab[6][kRows];  // out-LN mean, rstd, s1, s2 | in-LN mean, rstd
+    __shared__ float bred[3][3][64];
     const int B = lv.B, K = L.K, N = L.N;
     const int nkt = (K + 63) >> 6;
     const int n0 = (blk / nkt) * 16, kt = blk % nkt;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool oln = L.out_g != nullptr, iln = L.in_g != nullptr;
     if (oln || iln) {
-        for (int b = wave; b < B; b += 4) {
+        for (int b = threadIdx.x; b < B; b += 256) {
             if (oln) {
+                const int64_t o = (int64_t)b * (((N + 15) >> 4) * 2);
                 float mu, rs, s1, s2;
-                row_stats(L.out + (int64_t)b * N, N, lv.eps, lane, mu, rs);
-                row_bwd_sums(L.out + (int64_t)b * N, L.dsrc + (int64_t)b * N, L.out_g, L.out_b, N, mu, rs, lane, s1,
-                             s2);
-                if (lane == 0) {
-                    tab[0][b] = mu;
-                    tab[1][b] = rs;
-                    tab[2][b] = s1;
-                    tab[3][b] = s2;
-                }
+                ln_stats(L.out_part + o, N, lv.eps, mu, rs);
+                ln_sums(L.s_part + o, N, s1, s2);
+                tab[0][b] = mu;
+                tab[1][b] = rs;
+                tab[2][b] = s1;
+                tab[3][b] = s2;
             }
             if (iln) {
                 float mu, rs;
-                row_stats(L.in + (int64_t)b * K, K, lv.eps, lane, mu, rs);
-                if (lane == 0) {
-                    tab[4][b] = mu;
-                    tab[5][b] = rs;
-                }
+                ln_stats(L.in_part + (int64_t)b * (((K + 15) >> 4) * 2), K, lv.eps, mu, rs);
+                tab[4][b] = mu;
+                tab[5][b] = rs;
             }
         }
         __syncthreads();
@@ -210,25 +291,46 @@ __device__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
         return ln_relu_bwd(L.out[i], L.dsrc[i], L.out_g[n], L.out_b[n], tab[0][b], tab[1][b], tab[2][b], tab[3][b],
                            invN);
     };
-    auto act = [&](int b, int k) -> float {
-        const float v = L.in[(int64_t)b * K + k];
-        return iln ? fmaxf(ln_y(ln_xhat(v, tab[4][b], tab[5][b]), L.in_g[k], L.in_b[k]), 0.f) : v;
-    };
     const int q = lane >> 4;
     const int n = n0 + (lane & 15), k = kt * 64 + wave * 16 + (lane & 15);
     const bool nok = n < N, kok = k < K;
+    const int nc_ = nok ? n : N - 1, kc_ = kok ? k : K - 1;
+    const float *og = oln ? L.out_g : L.dsrc, *ob = oln ? L.out_b : L.dsrc, *oh = oln ? L.out : L.dsrc;
+    const float *ig = iln ? L.in_g : L.in, *ib = iln ? L.in_b : L.in;
+    const float gn = og[nc_], bn = ob[nc_], gk = ig[kc_], bk = ib[kc_];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int bb = 0; bb < B; bb += 16) {
-        float a[4], x[4];
+    for (int bc = 0; bc < B; bc += 64) {  // four 16-row blocks in flight, loads unconditional
+        float dv[4][4], hv[4][4], xv[4][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int b = bb + 4 * q + j;
-            const bool bok = b < B;
-            a[j] = (bok && nok) ? dy(b, n) : 0.f;
-            x[j] = (bok && kok) ? act(b, k) : 0.f;
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int bb = min(bc + 16 * u + 4 * q + j, B - 1);
+                dv[u][j] = L.dsrc[(int64_t)bb * N + nc_];
+                hv[u][j] = oh[(int64_t)bb * N + nc_];
+                xv[u][j] = L.in[(int64_t)bb * K + kc_];
+            }
+        }
+        float a[4][4], x[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int b = bc + 16 * u + 4 * q + j;
+                const int bb = min(b, B - 1);
+                const bool bok = b < B;
+                float d = dv[u][j];
+                if (oln) d = ln_relu_bwd(hv[u][j], d, gn, bn, tab[0][bb], tab[1][bb], tab[2][bb], tab[3][bb], invN);
+                float xa = xv[u][j];
+                if (iln) xa = fmaxf(ln_y(ln_xhat(xa, tab[4][bb], tab[5][bb]), gk, bk), 0.f);
+                a[u][j] = (bok && nok) ? d : 0.f;
+                x[u][j] = (bok && kok) ? xa : 0.f;
+            }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], x[j], acc, 0, 0, 0);
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][j], x[u][j], acc, 0, 0, 0);
     }
     // lane: dW[n0 + 4q + i][k]
     if (kok) {
@@ -242,10 +344,11 @@ __device__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
             }
         }
     }
-    if (kt == 0 && wave == 0) {  // bias (and LayerNorm affine) gradients of the 16 features
+    if (kt == 0) {  // bias (and LayerNorm affine) gradients of the 16 features: rows split over 16 lane groups
+        const int grp = wave * 4 + q;
         float sb = 0.f, sg = 0.f, sbeta = 0.f;
         if (nok) {
-            for (int b = q; b < B; b += 4) {
+            for (int b = grp; b < B; b += 16) {
                 sb += dy(b, n);
                 if (oln) {
                     const int64_t i = (int64_t)b * N + n;
@@ -262,7 +365,19 @@ __device__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
         sg += __shfl_xor(sg, 32, 64);
         sbeta += __shfl_xor(sbeta, 16, 64);
         sbeta += __shfl_xor(sbeta, 32, 64);
-        if (q == 0 && nok) {
+        if (wave) {
+            bred[wave - 1][0][lane] = sb;
+            bred[wave - 1][1][lane] = sg;
+            bred[wave - 1][2][lane] = sbeta;
+        }
+        __syncthreads();
+        if (wave == 0 && q == 0 && nok) {
+#pragma unroll
+            for (int w = 0; w < 3; ++w) {
+                sb += bred[w][0][lane];
+                sg += bred[w][1][lane];
+                sbeta += bred[w][2][lane];
+            }
             L.gb_mu[n] = sb;
             if (L.b_sig) L.gb_sig[n] = __fmul_rn(sb, L.b_eps[n]);
             if (oln) {
@@ -275,7 +390,7 @@ __device__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
 
 // role X: d act(in) for 16 rows x 16 input features, over streams [s_lo, s_hi)
 __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
-    __shared__ float rt[4][16];
+    __shared__ float rt[6][16];  // out-LN mean, rstd, s1, s2 of the stream in hand | in-LN mean, rstd
     __shared__ f32x4 red[3][64];
     const Layer L0 = pick(lv, s_lo);
     const int B = lv.B, K = L0.K;
@@ -285,6 +400,14 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
     const int q = lane >> 4;
     const int r = b0 + (lane & 15), k = k0 + (lane & 15);
     const bool rok = r < B, kok = k < K;
+    const bool dpart = L0.din_part != nullptr;
+    if (dpart && threadIdx.x < 16) {  // the input's LN statistics of the 16 rows (for din's backward sums)
+        const int b = b0 + threadIdx.x;
+        float mu = 0.f, rs = 0.f;
+        if (b < B) ln_stats(L0.in_part + (int64_t)b * (((K + 15) >> 4) * 2), K, lv.eps, mu, rs);
+        rt[4][threadIdx.x] = mu;
+        rt[5][threadIdx.x] = rs;
+    }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int s = s_lo; s < s_hi; ++s) {
         const Layer L = pick(lv, s);
@@ -293,19 +416,18 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
         float mu = 0.f, rs = 0.f, s1 = 0.f, s2 = 0.f;
         if (oln) {
             __syncthreads();  // rt of the previous stream consumed
-            for (int i = wave * 4; i < wave * 4 + 4; ++i) {
+            if (threadIdx.x < 16) {
+                const int b = b0 + threadIdx.x;
                 float m = 0.f, v = 0.f, a1 = 0.f, a2 = 0.f;
-                if (b0 + i < B) {
-                    const int64_t o = (int64_t)(b0 + i) * N;
-                    row_stats(L.out + o, N, lv.eps, lane, m, v);
-                    row_bwd_sums(L.out + o, L.dsrc + o, L.out_g, L.out_b, N, m, v, lane, a1, a2);
+                if (b < B) {
+                    const int64_t o = (int64_t)b * (((N + 15) >> 4) * 2);
+                    ln_stats(L.out_part + o, N, lv.eps, m, v);
+                    ln_sums(L.s_part + o, N, a1, a2);
                 }
-                if (lane == 0) {
-                    rt[0][i] = m;
-                    rt[1][i] = v;
-                    rt[2][i] = a1;
-                    rt[3][i] = a2;
-                }
+                rt[0][threadIdx.x] = m;
+                rt[1][threadIdx.x] = v;
+                rt[2][threadIdx.x] = a1;
+                rt[3][threadIdx.x] = a2;
             }
             __syncthreads();
             mu = rt[0][lane & 15];
@@ -315,19 +437,44 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
         }
         const float invN = 1.f / (float)N;
         const int64_t drow = (int64_t)(rok ? r : 0) * N;
-        for (int nb = wave * 16; nb < N; nb += 64) {
-            float a[4], w[4];
+        const int kc_ = kok ? k : K - 1;
+        const bool noisy = L.w_sig != nullptr;
+        const float *wsig = noisy ? L.w_sig : L.w_mu, *weps = noisy ? L.w_eps : L.w_mu;
+        const float *oh = oln ? L.out : L.dsrc, *og = oln ? L.out_g : L.dsrc, *ob = oln ? L.out_b : L.dsrc;
+        for (int nc = wave * 16; nc < N; nc += 256) {  // four 16-deep n blocks in flight, loads unconditional
+            float dv[4][4], hv[4][4], gv[4][4], bv[4][4], wm[4][4], ws[4][4], we[4][4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int n = nb + 4 * q + j;
-                const bool nok = n < N;
-                float d = (rok && nok) ? L.dsrc[drow + n] : 0.f;
-                if (oln && rok && nok) d = ln_relu_bwd(L.out[drow + n], d, L.out_g[n], L.out_b[n], mu, rs, s1, s2, invN);
-                a[j] = d;
-                w[j] = (nok && kok) ? wval(L, (int64_t)n * K + k) : 0.f;
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int nn = min(nc + 64 * u + 4 * q + j, N - 1);
+                    dv[u][j] = L.dsrc[drow + nn];
+                    hv[u][j] = oh[drow + nn];
+                    gv[u][j] = og[nn];
+                    bv[u][j] = ob[nn];
+                    const int64_t wi = (int64_t)nn * K + kc_;
+                    wm[u][j] = L.w_mu[wi];
+                    ws[u][j] = wsig[wi];
+                    we[u][j] = weps[wi];
+                }
+            }
+            float a[4][4], w[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bool nok = nc + 64 * u + 4 * q + j < N;
+                    float d = dv[u][j];
+                    if (oln) d = ln_relu_bwd(hv[u][j], d, gv[u][j], bv[u][j], mu, rs, s1, s2, invN);
+                    a[u][j] = (rok && nok) ? d : 0.f;
+                    const float wf = noisy ? __fadd_rn(wm[u][j], __fmul_rn(ws[u][j], we[u][j])) : wm[u][j];
+                    w[u][j] = (nok && kok) ? wf : 0.f;
+                }
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], w[j], acc, 0, 0, 0);
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][j], w[u][j], acc, 0, 0, 0);
         }
     }
     if (wave) red[wave - 1][lane] = acc;
@@ -335,11 +482,24 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
     if (wave == 0) {
 #pragma unroll
         for (int w = 0; w < 3; ++w) acc += red[w][lane];
-        if (kok) {
+        const int Tk = (K + 15) >> 4;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = b0 + 4 * q + i;
-                if (row < B) L0.din[(int64_t)row * K + k] = acc[i];
+        for (int i = 0; i < 4; ++i) {
+            const int ri = 4 * q + i, row = b0 + ri;
+            if (row < B && kok) L0.din[(int64_t)row * K + k] = acc[i];
+            if (dpart) {  // this tile's LayerNorm-backward sums of din (the level below reads them)
+                float gx = 0.f, xh = 0.f;
+                if (row < B && kok) {
+                    xh = ln_xhat(L0.in[(int64_t)row * K + k], rt[4][ri], rt[5][ri]);
+                    gx = ln_relu_g(xh, acc[i], L0.in_g[k], L0.in_b[k]);
+                }
+                const float a1 = __shfl(group_sum<16>(gx), lane & ~15, 64);
+                const float a2 = __shfl(group_sum<16>(__fmul_rn(gx, xh)), lane & ~15, 64);
+                if ((lane & 15) == 0 && row < B) {
+                    float *p = L0.din_part + ((int64_t)row * Tk + (k0 >> 4)) * 2;
+                    p[0] = a1;
+                    p[1] = a2;
+                }
             }
         }
     }
@@ -387,9 +547,11 @@ static int check_layers(const agx_noisy_stream_layer *layers, int32_t S, int32_t
                             (L.w_sigma == nullptr) == (L.b_sigma == nullptr),
                         "%s: stream %d layer %d: sigma and eps come together, for weight and bias", who, s, l);
             const bool hidden = l < NL - 1;
-            AGX_REQUIRE(hidden == (L.ln_gamma != nullptr) && hidden == (L.ln_beta != nullptr),
-                        "%s: stream %d layer %d: hidden layers (only) carry the LayerNorm affine", who, s, l);
-            AGX_REQUIRE(l == 0 ? L.fin == layers[l].fin : L.fin == layers[s * NL + l - 1].fout,
+            AGX_REQUIRE(hidden == (L.ln_gamma != nullptr) && hidden == (L.ln_beta != nullptr) &&
+                            hidden == (L.ln_part != nullptr),
+                        "%s: stream %d layer %d: hidden layers (only) carry the LayerNorm affine and ln_part", who, s,
+                        l);
+            AGX_REQUIRE(l == 0 ? L.fin == layers[0].fin : L.fin == layers[s * NL + l - 1].fout,
                         "%s: stream %d layer %d: fin %d does not match its input", who, s, l, L.fin);
         }
     }
@@ -406,6 +568,7 @@ static nmlp::Layer make_layer(const agx_noisy_stream_layer *layers, int NL, int 
         d.in = P.out;
         d.in_g = P.ln_gamma;
         d.in_b = P.ln_beta;
+        d.in_part = P.ln_part;
     }
     d.w_mu = L.w_mu;
     d.w_sig = L.w_sigma;
@@ -414,10 +577,13 @@ static nmlp::Layer make_layer(const agx_noisy_stream_layer *layers, int NL, int 
     d.b_sig = L.b_sigma;
     d.b_eps = L.b_eps;
     d.out = L.out;
+    d.out_part = L.ln_part;
     d.K = L.fin;
     d.N = L.fout;
     return d;
 }
+
+static int64_t part_floats(int64_t B, int32_t n) { return B * ceil_div(n, 16) * 2; }
 
 extern "C" int agx_noisy_streams_forward(const agx_noisy_stream_layer *layers, int32_t S, int32_t NL, const float *x,
                                          int64_t B, float ln_eps, void *stream) {
@@ -442,12 +608,13 @@ extern "C" int agx_noisy_streams_forward(const agx_noisy_stream_layer *layers, i
     return AGX_OK;
 }
 
-extern "C" size_t agx_noisy_streams_workspace_bytes(const agx_noisy_stream_layer *layers, int32_t S, int32_t NL, int64_t B) {
+extern "C" size_t agx_noisy_streams_workspace_bytes(const agx_noisy_stream_layer *layers, int32_t S, int32_t NL,
+                                                    int64_t B) {
     if (!layers || S < 1 || S > AGX_NOISY_MAX_STREAMS || NL < 1 || NL > AGX_NOISY_MAX_LAYERS || B < 0) return 0;
-    size_t n = 0;
+    int64_t n = 0;
     for (int s = 0; s < S; ++s)
-        for (int l = 0; l + 1 < NL; ++l) n += (size_t)B * (size_t)layers[s * NL + l].fout;
-    return n * sizeof(float);
+        for (int l = 0; l + 1 < NL; ++l) n += B * layers[s * NL + l].fout + part_floats(B, layers[s * NL + l].fout);
+    return (size_t)n * sizeof(float);
 }
 
 extern "C" int agx_noisy_streams_backward(const agx_noisy_stream_layer *layers, int32_t S, int32_t NL, const float *x,
@@ -466,13 +633,18 @@ extern "C" int agx_noisy_streams_backward(const agx_noisy_stream_layer *layers, 
         }
     }
     if (B == 0) return AGX_OK;
-    // da[s][l]: d loss / d relu(LN(out of layer l)) of stream s, hidden layers l < NL - 1
+    // da[s][l]: d loss / d relu(LN(out of layer l)) of stream s, hidden layers l < NL - 1;
+    // sp[s][l]: its tiles' LayerNorm-backward sums
     float *da[AGX_NOISY_MAX_STREAMS][AGX_NOISY_MAX_LAYERS] = {};
+    float *sp[AGX_NOISY_MAX_STREAMS][AGX_NOISY_MAX_LAYERS] = {};
     float *p = static_cast<float *>(workspace);
     for (int s = 0; s < S; ++s)
         for (int l = 0; l + 1 < NL; ++l) {
+            const int32_t f = layers[s * NL + l].fout;
             da[s][l] = p;
-            p += B * layers[s * NL + l].fout;
+            p += B * f;
+            sp[s][l] = p;
+            p += part_floats(B, f);
         }
     const int nrb = (int)ceil_div(B, 16);
     for (int l = NL - 1; l >= 0; --l) {
@@ -489,6 +661,7 @@ extern "C" int agx_noisy_streams_backward(const agx_noisy_stream_layer *layers, 
             d.dsrc = l == NL - 1 ? grad_out[s] : da[s][l];
             d.out_g = L.ln_gamma;
             d.out_b = L.ln_beta;
+            d.s_part = l == NL - 1 ? nullptr : sp[s][l];
             d.gw_mu = L.grad_w_mu;
             d.gw_sig = L.grad_w_sigma;
             d.gb_mu = L.grad_b_mu;
@@ -496,6 +669,7 @@ extern "C" int agx_noisy_streams_backward(const agx_noisy_stream_layer *layers, 
             d.g_g = L.grad_ln_gamma;
             d.g_b = L.grad_ln_beta;
             d.din = l == 0 ? grad_x : da[s][l - 1];
+            d.din_part = l == 0 ? nullptr : sp[s][l - 1];
             d.tiles_w = (int)ceil_div(d.N, 16) * (int)ceil_div(d.K, 64);
             d.tiles_x = d.din ? (int)ceil_div(d.K, 16) * nrb : 0;
             grid += d.tiles_w;

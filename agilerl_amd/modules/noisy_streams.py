@@ -33,8 +33,8 @@ from .custom_components import NoisyLinear
 
 _MAX_LAYERS = 4
 _MAX_ROWS = 1024
-_PTRS = ("w_mu", "w_sigma", "w_eps", "b_mu", "b_sigma", "b_eps", "ln_gamma", "ln_beta", "out", "grad_w_mu",
-         "grad_w_sigma", "grad_b_mu", "grad_b_sigma", "grad_ln_gamma", "grad_ln_beta")
+_PTRS = ("w_mu", "w_sigma", "w_eps", "b_mu", "b_sigma", "b_eps", "ln_gamma", "ln_beta", "out", "ln_part",
+         "grad_w_mu", "grad_w_sigma", "grad_b_mu", "grad_b_sigma", "grad_ln_gamma", "grad_ln_beta")
 
 
 class AgxNoisyStreamLayer(ctypes.Structure):
@@ -124,7 +124,7 @@ def _params(plans: list) -> tuple[_Meta, list] | None:
     return meta, ts
 
 
-def _layer_array(meta: _Meta, ts, outs, grads=None) -> ctypes.Array:
+def _layer_array(meta: _Meta, ts, outs, parts, grads=None) -> ctypes.Array:
     arr = (AgxNoisyStreamLayer * len(meta.layers))()
     for j, d in enumerate(meta.layers):
         e = arr[j]
@@ -138,6 +138,8 @@ def _layer_array(meta: _Meta, ts, outs, grads=None) -> ctypes.Array:
             if k in d:
                 setattr(e, k, d[k].data_ptr())
         e.out = outs[j].data_ptr()
+        if parts[j] is not None:
+            e.ln_part = parts[j].data_ptr()
     return arr
 
 
@@ -149,18 +151,26 @@ class NoisyStreamsFn(torch.autograd.Function):
         x = x.contiguous()
         B = x.shape[0]
         outs = [torch.empty(B, d["fout"], dtype=torch.float32, device=x.device) for d in meta.layers]
-        arr = _layer_array(meta, ts, outs)
+        # hidden layers: per-tile LayerNorm statistics of out (read by the next depth and the backward)
+        parts = [torch.empty(B, (d["fout"] + 15) // 16, 2, dtype=torch.float32, device=x.device)
+                 if "ln_gamma" in d else None for d in meta.layers]
+        arr = _layer_array(meta, ts, outs, parts)
         _lib.call("agx_noisy_streams_forward", ctypes.cast(arr, ctypes.c_void_p), meta.S, meta.NL, x.data_ptr(), B,
                   meta.eps, _lib.stream())
         ctx.meta = meta
-        ctx.save_for_backward(x, *ts, *outs)
+        ctx.parts = [p is not None for p in parts]
+        ctx.save_for_backward(x, *ts, *outs, *[p for p in parts if p is not None])
         return tuple(outs[s * meta.NL + meta.NL - 1] for s in range(meta.S))
 
     @staticmethod
     def backward(ctx, *gouts):
         meta = ctx.meta
         saved = ctx.saved_tensors
-        x, ts, outs = saved[0], saved[1:1 + meta.n_tensors], saved[1 + meta.n_tensors:]
+        nl = len(meta.layers)
+        x, ts = saved[0], saved[1:1 + meta.n_tensors]
+        outs = saved[1 + meta.n_tensors:1 + meta.n_tensors + nl]
+        rest = iter(saved[1 + meta.n_tensors + nl:])
+        parts = [next(rest) if has else None for has in ctx.parts]
         B = x.shape[0]
         grads = [torch.empty_like(t) for t in ts]
         gx = torch.empty_like(x) if ctx.needs_input_grad[1] else None
@@ -169,7 +179,7 @@ class NoisyStreamsFn(torch.autograd.Function):
             fout = meta.layers[s * meta.NL + meta.NL - 1]["fout"]
             gs.append(torch.zeros(B, fout, dtype=torch.float32, device=x.device) if g is None else
                       g.to(torch.float32).contiguous())
-        arr = _layer_array(meta, ts, outs, grads)
+        arr = _layer_array(meta, ts, outs, parts, grads)
         lib = _lib.load()
         nws = lib.agx_noisy_streams_workspace_bytes(ctypes.cast(arr, ctypes.c_void_p), meta.S, meta.NL, B)
         ws = torch.empty(max(16, nws), dtype=torch.uint8, device=x.device)

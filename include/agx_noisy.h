@@ -40,13 +40,17 @@ extern "C" {
  * LayerNorm(fout) affine (ln_gamma, ln_beta), applied with ReLU before the
  * next layer; the output layer has ln_gamma == NULL.  out [B][fout]: the
  * layer's output before normalisation — written by the forward, read by the
- * backward.  grad_*: backward outputs (grad_w_sigma / grad_b_sigma only with
- * w_sigma, grad_ln_* only on hidden layers). */
+ * backward.  ln_part [B][ceil(fout / 16)][2] (hidden layers): the forward's
+ * LayerNorm statistics of out per 16-feature tile (mean, sum of squared
+ * deviations), combined in tile order wherever a row's mean / rstd is needed
+ * (forward and backward alike).  grad_*: backward outputs (grad_w_sigma /
+ * grad_b_sigma only with w_sigma, grad_ln_* only on hidden layers). */
 typedef struct agx_noisy_stream_layer {
     const float *w_mu, *w_sigma, *w_eps;
     const float *b_mu, *b_sigma, *b_eps;
     const float *ln_gamma, *ln_beta;
     float *out;
+    float *ln_part;
     float *grad_w_mu, *grad_w_sigma, *grad_b_mu, *grad_b_sigma, *grad_ln_gamma, *grad_ln_beta;
     int32_t fin, fout;
 } agx_noisy_stream_layer;
@@ -57,13 +61,14 @@ int agx_noisy_streams_forward(const agx_noisy_stream_layer *layers, int32_t n_st
                               int64_t B, float ln_eps, void *stream);
 
 /* Bytes of device workspace agx_noisy_streams_backward needs (the gradients
- * of the hidden activations). */
+ * of the hidden activations and their per-tile LayerNorm-backward sums). */
 size_t agx_noisy_streams_workspace_bytes(const agx_noisy_stream_layer *layers, int32_t n_streams, int32_t n_layers,
                                          int64_t B);
 
 /* grad_out[s] [B][fout of the last layer]: d loss / d (stream s's output);
  * grad_x [B][fin] (NULL: not needed): d loss / d x summed over the streams.
- * Reads the forward's out buffers; writes every grad_* of every layer. */
+ * Reads the forward's out and ln_part buffers; writes every grad_* of
+ * every layer. */
 int agx_noisy_streams_backward(const agx_noisy_stream_layer *layers, int32_t n_streams, int32_t n_layers, const float *x,
                                int64_t B, float ln_eps, const float *const *grad_out, float *grad_x, void *workspace,
                                void *stream);
