@@ -96,6 +96,7 @@ SIGNATURES = {
     "agx_polyak": (_INT, [_P, _P, _I, _F, _P]),
     "agx_noisy_reset": (_INT, [_P, _INT, _P]),
     "agx_noisy_streams_forward": (_INT, [_P, _INT, _INT, _P, _I, _F, _P]),
+    "agx_noisy_streams_forward_each": (_INT, [_P, _INT, _INT, _P, _I, _F, _P]),
     "agx_noisy_streams_workspace_bytes": (_SZ, [_P, _INT, _INT, _I]),
     "agx_noisy_streams_backward": (_INT, [_P, _INT, _INT, _P, _I, _F, _P, _P, _P, _P]),
     "agx_conv2d_forward": (_INT, [_P, _P, _INT, _F, _F, _P, _P, _INT, _P, _P]),

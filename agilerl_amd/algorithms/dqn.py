@@ -258,6 +258,78 @@ class _C51RowsLoss(torch.autograd.Function):
         return (-proj * g.unsqueeze(1),) + (None,) * 7
 
 
+@torch.no_grad()
+def _next_pair(agent, next_obs):
+    """The two no-grad forwards of a Rainbow update on s' (dqn_rainbow.py:
+    284-367: a* = argmax_a Q_online(s'), then the target network's
+    distribution of a*) with both networks in one launch per layer: the flat
+    state keeps online and target parameters as the two rows of one buffer,
+    so every convolution is a grouped launch over (online, target) reading
+    the same frames, the encoder's Linear one batched GEMM, and the four head
+    streams one agx_noisy_streams_forward_each launch per depth.  -> (a*,
+    target rows [B, Z]), or None where the network is not the CNN + dueling
+    head this covers (the caller runs the reference's two forwards)."""
+    import ctypes
+
+    from torch import nn
+
+    from .. import _lib
+    from ..modules.cnn import AgxConv2d, EvolvableCNN, _FusedIdentity, _shape
+    from ..modules.noisy_streams import head_streams_each
+    from ..networks.q_networks import DuelingDistributionalMLP, DuelingHeadFn, DuelingRowsFn
+    from .learn_graph import _hooked
+
+    actor, target = agent.actor, agent.actor_target
+    enc = getattr(actor, "encoder", None)
+    if (not isinstance(enc, EvolvableCNN) or not isinstance(getattr(actor, "head_net", None), DuelingDistributionalMLP)
+            or getattr(actor, "flatten_obs", False) or not isinstance(next_obs, torch.Tensor) or not next_obs.is_cuda
+            or next_obs.dim() != 4 or agent.num_atoms > 64 or _hooked(actor, target)):
+        return None
+    fs = flat_state(agent)
+    if fs is None:
+        return None
+    B = next_obs.shape[0]
+    x, first = next_obs.contiguous(), True
+    for _, mod in enc.model.named_children():
+        if type(mod) is AgxConv2d:
+            u8 = x.dtype == torch.uint8
+            if (u8 and mod.image_norm is None) or (not u8 and x.dtype != torch.float32) or mod.bias is None:
+                return None
+            xs = x if first else x[0]
+            sh = _shape(xs, mod.weight, int(mod.stride[0]))
+            OH = (sh.height - sh.kernel_h) // sh.stride + 1
+            OW = (sh.width - sh.kernel_w) // sh.stride + 1
+            y = torch.empty(2, B, mod.out_channels, OH, OW, dtype=torch.float32, device=x.device)
+            w2, b2 = fs.pair_view(mod.weight), fs.pair_view(mod.bias)
+            lo, hi = (float(mod.image_norm[0]), float(mod.image_norm[1])) if u8 else (0.0, 1.0)
+            _lib.call("agx_conv2d_forward_grouped", ctypes.byref(sh), 2, x.data_ptr(), 0 if first else x[0].numel(),
+                      int(u8), lo, hi, w2.data_ptr(), w2.stride(0), b2.data_ptr(), b2.stride(0), int(mod.fuse_relu),
+                      y.data_ptr(), y[0].numel(), _lib.stream())
+            x, first = y, False
+        elif type(mod) is _FusedIdentity or type(mod) is nn.Identity:
+            pass
+        elif type(mod) is nn.ReLU:
+            x = torch.relu(x)
+        elif type(mod) is nn.Flatten and not first:
+            x = x.reshape(2, B, -1)
+        elif type(mod) is nn.Linear and not first and x.dim() == 3 and mod.bias is not None:
+            w2, b2 = fs.pair_view(mod.weight), fs.pair_view(mod.bias)
+            x = torch.baddbmm(b2.unsqueeze(1), x, w2.transpose(1, 2))
+        else:
+            return None
+    if first or x.dim() != 3:
+        return None
+    ha, ht = actor.head_net, target.head_net
+    out = head_streams_each([ha.model, ha.advantage_net, ht.model, ht.advantage_net], [x[0], x[0], x[1], x[1]])
+    if out is None:
+        return None
+    v_on, a_on, v_tg, a_tg = out
+    A, Z = agent.action_dim, agent.num_atoms
+    q = DuelingHeadFn.apply(v_on, a_on, ha.support, A, Z, 0)
+    a_star = q.argmax(1)  # first maximum, as the reference's argmax
+    return a_star, DuelingRowsFn.apply(v_tg, a_tg, a_star, A, Z, 1)
+
+
 class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
     """Drop-in RainbowDQN (agilerl/algorithms/dqn_rainbow.py:77-501) with the
     C51 projection + loss in agx_c51_project_loss and Polyak in agx_polyak."""
@@ -339,8 +411,12 @@ class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
             # the heads emit only the selected rows (target_dist[range(B), a*],
             # log_p[range(B), action]); the C51 step streams them contiguously
             with torch.no_grad():
-                a_star = self.actor(next_obs).argmax(1)     # first maximum, as the reference's argmax
-                target_rows = self.actor_target(next_obs, q=False, rows=a_star)
+                pair = _next_pair(self, next_obs)
+                if pair is not None:
+                    a_star, target_rows = pair
+                else:
+                    a_star = self.actor(next_obs).argmax(1)     # first maximum, as the reference's argmax
+                    target_rows = self.actor_target(next_obs, q=False, rows=a_star)
             logp_rows = self.actor(obs, q=False, log=True, rows=acts)
             return _C51RowsLoss.apply(logp_rows, target_rows, rew, done, self.support, float(self.v_min),
                                       float(self.v_max), float(gamma))

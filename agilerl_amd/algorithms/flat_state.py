@@ -52,8 +52,12 @@ class FlatLearnState:
         dev = self.params[0].device
         sizes = [p.numel() for p in self.params]
         self.n = n = sum(sizes)
-        self.prm = torch.empty(n, dtype=torch.float32, device=dev)
-        self.tgt = torch.empty(n, dtype=torch.float32, device=dev)
+        # online and target parameters as the two rows of one [2, n] buffer: a
+        # tensor's online and target copies sit n elements apart, so the
+        # no-grad forwards on s' take both networks in one grouped launch
+        # (pair_view, dqn.py)
+        self.pair = torch.empty(2, n, dtype=torch.float32, device=dev)
+        self.prm, self.tgt = self.pair[0], self.pair[1]
         self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
         self.m = torch.zeros(n, dtype=torch.float32, device=dev)
         self.v = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -83,6 +87,11 @@ class FlatLearnState:
                     vv.copy_(st["exp_avg_sq"])
                 opt.state[p] = {"step": st_t, "exp_avg": mv, "exp_avg_sq": vv}
                 off += k
+        self.offs = {}
+        off = 0
+        for p, k in zip(self.params, sizes):
+            self.offs[id(p)] = (off, k)
+            off += k
         self.ptrs = [p.data_ptr() for p in self.params]
         self.tptrs = [q.data_ptr() for q in self.tparams]
         self.mptrs = [opt.state[p]["exp_avg"].data_ptr() for p in self.params]
@@ -91,6 +100,11 @@ class FlatLearnState:
         self.offsets = torch.tensor([0, n], dtype=torch.int64)
         lib = _lib.load()
         self.workspace = torch.empty(max(16, lib.agx_adam_workspace_bytes(1, n)), dtype=torch.uint8, device=dev)
+
+    def pair_view(self, p: torch.Tensor) -> torch.Tensor:
+        """[2, *p.shape]: online parameter p and its target copy, one view."""
+        off, k = self.offs[id(p)]
+        return self.pair[:, off:off + k].view(2, *p.shape)
 
     def valid(self, actor, target, opt) -> bool:
         if actor is not self.actor or target is not self.target or opt is not self.opt or not _plain_adam(opt):

@@ -155,17 +155,21 @@ __device__ __forceinline__ void tile_moments(float v, bool ok, int cnt, int lane
     q2 = __shfl(group_sum<16>(d * d), lane & ~15, 64);
 }
 
-__device__ __forceinline__ Layer pick(const Level &lv, int s) { return s == 0 ? lv.s[0] : lv.s[1]; }
+__device__ __forceinline__ Layer pick(const Level &lv, int s) {
+    switch (s) {
+        case 0: return lv.s[0];
+        case 1: return lv.s[1];
+        case 2: return lv.s[2];
+        default: return lv.s[3];
+    }
+}
 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
     __shared__ float st[2][16];
     __shared__ f32x4 red[3][64];
     int blk = blockIdx.x, si = 0;
-    if (blk >= lv.s[0].tiles_w) {
-        blk -= lv.s[0].tiles_w;
-        si = 1;
-    }
+    while (si + 1 < lv.S && blk >= pick(lv, si).tiles_w) blk -= pick(lv, si++).tiles_w;
     const Layer L = pick(lv, si);
     const int B = lv.B, K = L.K, N = L.N;
     const int nrb = (B + 15) >> 4;
@@ -508,7 +512,7 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
 __global__ __launch_bounds__(256) void bwd_kernel(Level lv) {
     int blk = blockIdx.x;
     for (int s = 0; s < lv.S; ++s) {
-        const int t = s == 0 ? lv.s[0].tiles_w : lv.s[1].tiles_w;
+        const int t = pick(lv, s).tiles_w;
         if (blk < t) {
             bwd_weights(lv, pick(lv, s), blk);
             return;
@@ -520,7 +524,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(Level lv) {
         return;
     }
     for (int s = 0; s < lv.S; ++s) {
-        const int t = s == 0 ? lv.s[0].tiles_x : lv.s[1].tiles_x;
+        const int t = pick(lv, s).tiles_x;
         if (blk < t) {
             bwd_inputs(lv, s, s + 1, blk);
             return;
@@ -585,11 +589,8 @@ static nmlp::Layer make_layer(const agx_noisy_stream_layer *layers, int NL, int 
 
 static int64_t part_floats(int64_t B, int32_t n) { return B * ceil_div(n, 16) * 2; }
 
-extern "C" int agx_noisy_streams_forward(const agx_noisy_stream_layer *layers, int32_t S, int32_t NL, const float *x,
-                                         int64_t B, float ln_eps, void *stream) {
-    if (int rc = check_layers(layers, S, NL, B, "agx_noisy_streams_forward")) return rc;
-    AGX_REQUIRE(x, "agx_noisy_streams_forward: x is NULL");
-    if (B == 0) return AGX_OK;
+static int forward_streams(const agx_noisy_stream_layer *layers, int32_t S, int32_t NL, const float *const *xs,
+                           int64_t B, float ln_eps, void *stream) {
     const int nrb = (int)ceil_div(B, 16);
     for (int l = 0; l < NL; ++l) {
         nmlp::Level lv{};
@@ -598,7 +599,7 @@ extern "C" int agx_noisy_streams_forward(const agx_noisy_stream_layer *layers, i
         lv.eps = ln_eps;
         int grid = 0;
         for (int s = 0; s < S; ++s) {
-            lv.s[s] = make_layer(layers, NL, s, l, x);
+            lv.s[s] = make_layer(layers, NL, s, l, xs[s]);
             lv.s[s].tiles_w = (int)ceil_div(lv.s[s].N, 16) * nrb;
             grid += lv.s[s].tiles_w;
         }
@@ -606,6 +607,24 @@ extern "C" int agx_noisy_streams_forward(const agx_noisy_stream_layer *layers, i
         if (int rc = check_launch("agx_noisy_streams_forward")) return rc;
     }
     return AGX_OK;
+}
+
+extern "C" int agx_noisy_streams_forward(const agx_noisy_stream_layer *layers, int32_t S, int32_t NL, const float *x,
+                                         int64_t B, float ln_eps, void *stream) {
+    if (int rc = check_layers(layers, S, NL, B, "agx_noisy_streams_forward")) return rc;
+    AGX_REQUIRE(x, "agx_noisy_streams_forward: x is NULL");
+    if (B == 0) return AGX_OK;
+    const float *xs[AGX_NOISY_MAX_STREAMS] = {x, x, x, x};
+    return forward_streams(layers, S, NL, xs, B, ln_eps, stream);
+}
+
+extern "C" int agx_noisy_streams_forward_each(const agx_noisy_stream_layer *layers, int32_t S, int32_t NL,
+                                              const float *const *xs, int64_t B, float ln_eps, void *stream) {
+    if (int rc = check_layers(layers, S, NL, B, "agx_noisy_streams_forward_each")) return rc;
+    AGX_REQUIRE(xs, "agx_noisy_streams_forward_each: xs is NULL");
+    for (int s = 0; s < S; ++s) AGX_REQUIRE(xs[s], "agx_noisy_streams_forward_each: xs[%d] is NULL", s);
+    if (B == 0) return AGX_OK;
+    return forward_streams(layers, S, NL, xs, B, ln_eps, stream);
 }
 
 extern "C" size_t agx_noisy_streams_workspace_bytes(const agx_noisy_stream_layer *layers, int32_t S, int32_t NL,

@@ -207,3 +207,36 @@ def head_streams(streams: list, x: torch.Tensor):
         return None
     meta, ts = got
     return NoisyStreamsFn.apply(meta, x, *ts)
+
+
+@torch.no_grad()
+def head_streams_each(streams: list, xs: list):
+    """No-grad outputs of ``streams`` where stream s reads xs[s] (several
+    networks' heads in one launch per depth, agx_noisy_streams_forward_each),
+    or None where the fused kernels do not apply."""
+    if not enabled() or len(streams) > 4 or len(xs) != len(streams):
+        return None
+    x0 = xs[0]
+    if any(not isinstance(x, torch.Tensor) or not x.is_cuda or x.dtype != torch.float32 or x.dim() != 2 or
+           x.shape != x0.shape or not x.is_contiguous() for x in xs) or x0.shape[0] > _MAX_ROWS:
+        return None
+    from ..algorithms.learn_graph import _hooked
+
+    plans = [_stream_plan(s) for s in streams]
+    if any(p is None for p in plans) or len({len(p) for p in plans}) != 1 or _hooked(*streams):
+        return None
+    if any(p[0][0].in_features != x0.shape[1] for p in plans):
+        return None
+    got = _params(plans)
+    if got is None:
+        return None
+    meta, ts = got
+    B = x0.shape[0]
+    outs = [torch.empty(B, d["fout"], dtype=torch.float32, device=x0.device) for d in meta.layers]
+    parts = [torch.empty(B, (d["fout"] + 15) // 16, 2, dtype=torch.float32, device=x0.device)
+             if "ln_gamma" in d else None for d in meta.layers]
+    arr = _layer_array(meta, ts, outs, parts)
+    xp = (ctypes.c_void_p * len(xs))(*[x.data_ptr() for x in xs])
+    _lib.call("agx_noisy_streams_forward_each", ctypes.cast(arr, ctypes.c_void_p), meta.S, meta.NL,
+              ctypes.cast(xp, ctypes.c_void_p), B, meta.eps, _lib.stream())
+    return tuple(outs[s * meta.NL + meta.NL - 1] for s in range(meta.S))

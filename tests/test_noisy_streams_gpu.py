@@ -199,3 +199,34 @@ def test_dueling_head_rows_with_and_without_fused_streams():
     _check(x1.grad, x2.grad, 1e-4, "d latent")
     for (n, p), q in zip(head.named_parameters(), twin.parameters()):
         _check(p.grad, q.grad, 1e-4, n)
+
+
+def test_rainbow_next_pair_matches_the_two_forwards():
+    """RainbowDQN's no-grad forwards on s' (a* from the online network, the
+    target network's distribution of a*) as one grouped launch per layer
+    (dqn._next_pair) against the two separate forwards of the reference's
+    _dqn_loss (dqn_rainbow.py:284-367)."""
+    import numpy as np
+
+    from agilerl_amd.algorithms import RainbowDQN
+    from agilerl_amd.algorithms.dqn import _next_pair
+    from agilerl_amd.algorithms.flat_state import flat_state
+    from agilerl_amd.envs import Box, Discrete
+
+    torch.manual_seed(3)
+    net = {"latent_dim": 256, "max_latent_dim": 512, "encoder_config": {"channel_size": [32, 64, 128], "kernel_size": [8, 4, 3],
+                                                 "stride_size": [4, 2, 1]}, "head_config": {"hidden_size": [256]}}
+    agent = RainbowDQN(Box(0, 255, (4, 84, 84), dtype=np.uint8), Discrete(6), net_config=net, v_min=-200.0,
+                       v_max=200.0)
+    assert flat_state(agent) is not None
+    with torch.no_grad():  # target != online
+        for p in agent.actor_target.parameters():
+            p.add_(0.02 * torch.randn_like(p))
+    obs = torch.randint(0, 256, (64, 4, 84, 84), dtype=torch.uint8, device=DEV)
+    pair = _next_pair(agent, obs)
+    assert pair is not None, "the paired forward did not take the config-3 network"
+    with torch.no_grad():
+        a_ref = agent.actor(obs).argmax(1)
+        rows_ref = agent.actor_target(obs, q=False, rows=a_ref)
+    assert torch.equal(pair[0], a_ref)
+    _check(pair[1], rows_ref, 1e-5, "target rows")
