@@ -155,27 +155,44 @@ __device__ __forceinline__ void tile_moments(float v, bool ok, int cnt, int lane
     q2 = __shfl(group_sum<16>(d * d), lane & ~15, 64);
 }
 
-__device__ __forceinline__ Layer pick(const Level &lv, int s) {
-    switch (s) {
-        case 0: return lv.s[0];
-        case 1: return lv.s[1];
-        case 2: return lv.s[2];
-        default: return lv.s[3];
-    }
-}
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
+__device__ __forceinline__ void fwd_body(const Level &lv, const Layer &L, int blk) {
     __shared__ float st[2][16];
     __shared__ f32x4 red[3][64];
-    int blk = blockIdx.x, si = 0;
-    while (si + 1 < lv.S && blk >= pick(lv, si).tiles_w) blk -= pick(lv, si++).tiles_w;
-    const Layer L = pick(lv, si);
     const int B = lv.B, K = L.K, N = L.N;
     const int nrb = (B + 15) >> 4;
     const int n0 = (blk / nrb) * 16, b0 = (blk % nrb) * 16;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool ln = L.in_g != nullptr;
+    const int r = b0 + (lane & 15), n = n0 + (lane & 15), q = lane >> 4;
+    const bool rok = r < B, nok = n < N;
+    // every load is unconditional (indices clamped, pointers selected
+    // uniformly), and the first K chunk's operands and the epilogue's bias are
+    // requested before the LayerNorm statistics are combined: one memory
+    // round trip ahead of the MFMAs instead of three in a row
+    const float *xrow = L.in + (int64_t)(rok ? r : 0) * K;
+    const int64_t wrow = (int64_t)(nok ? n : 0) * K;
+    const bool noisy = L.w_sig != nullptr;
+    const float *wsig = noisy ? L.w_sig : L.w_mu, *weps = noisy ? L.w_eps : L.w_mu;
+    const float *ing = ln ? L.in_g : L.w_mu, *inb = ln ? L.in_b : L.w_mu;
+    const float *bsig = noisy ? L.b_sig : L.b_mu, *beps = noisy ? L.b_eps : L.b_mu;
+    const int nb_ = nok ? n : N - 1;
+    const float bmu = L.b_mu[nb_], bs = bsig[nb_], be = beps[nb_];
+    float xv[4][4], wm[4][4], ws[4][4], we[4][4], gg[4][4], gb[4][4];
+#define NMLP_LOAD(KC)                                                   \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                     \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j) {                 \
+            const int kk = min((KC) + 64 * u + 4 * q + j, K - 1);       \
+            xv[u][j] = xrow[kk];                                        \
+            wm[u][j] = L.w_mu[wrow + kk];                               \
+            ws[u][j] = wsig[wrow + kk];                                 \
+            we[u][j] = weps[wrow + kk];                                 \
+            gg[u][j] = ing[kk];                                         \
+            gb[u][j] = inb[kk];                                         \
+        }                                                               \
+    }
+    NMLP_LOAD(wave * 16)
     if (ln) {
         if (threadIdx.x < 16) {
             const int b = b0 + threadIdx.x;
@@ -186,32 +203,9 @@ __global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
         }
         __syncthreads();
     }
-    const int r = b0 + (lane & 15), n = n0 + (lane & 15), q = lane >> 4;
-    const bool rok = r < B, nok = n < N;
     const float mu = ln ? st[0][lane & 15] : 0.f, rs = ln ? st[1][lane & 15] : 0.f;
-    // every load below is unconditional (indices clamped, pointers selected
-    // uniformly), so a wave issues all of them before the first wait
-    const float *xrow = L.in + (int64_t)(rok ? r : 0) * K;
-    const int64_t wrow = (int64_t)(nok ? n : 0) * K;
-    const bool noisy = L.w_sig != nullptr;
-    const float *wsig = noisy ? L.w_sig : L.w_mu, *weps = noisy ? L.w_eps : L.w_mu;
-    const float *ing = ln ? L.in_g : L.w_mu, *inb = ln ? L.in_b : L.w_mu;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int kc = wave * 16; kc < K; kc += 256) {  // four 16-deep k blocks of this wave in flight
-        float xv[4][4], wm[4][4], ws[4][4], we[4][4], gg[4][4], gb[4][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int kk = min(kc + 64 * u + 4 * q + j, K - 1);
-                xv[u][j] = xrow[kk];
-                wm[u][j] = L.w_mu[wrow + kk];
-                ws[u][j] = wsig[wrow + kk];
-                we[u][j] = weps[wrow + kk];
-                gg[u][j] = ing[kk];
-                gb[u][j] = inb[kk];
-            }
-        }
+    for (int kc = wave * 16; kc < K; kc += 256) {  // four 16-deep k blocks of this wave per chunk
         float a[4][4], w[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -229,7 +223,11 @@ __global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][j], w[u][j], acc, 0, 0, 0);
+        if (kc + 256 < K) {
+            NMLP_LOAD(kc + 256)
+        }
     }
+#undef NMLP_LOAD
     if (wave) red[wave - 1][lane] = acc;
     __syncthreads();
     if (wave == 0) {
@@ -237,7 +235,7 @@ __global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
         for (int w = 0; w < 3; ++w) acc += red[w][lane];
         const int col = n0 + (lane & 15);
         const bool cok = col < N;
-        const float bias = cok ? bval(L, col) : 0.f;
+        const float bias = noisy ? __fadd_rn(bmu, __fmul_rn(bs, be)) : bmu;
         const int T = (N + 15) >> 4, cnt = min(16, N - n0);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -257,16 +255,51 @@ __global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
     }
 }
 
+// stream dispatch with constant indices into the kernel argument (a
+// runtime-indexed Level would be copied to scratch)
+__global__ __launch_bounds__(256) void fwd_kernel(Level lv) {
+    int blk = blockIdx.x;
+#pragma unroll
+    for (int s = 0; s < AGX_NOISY_MAX_STREAMS; ++s) {
+        if (s < lv.S) {
+            if (blk < lv.s[s].tiles_w || s + 1 == lv.S) {
+                fwd_body(lv, lv.s[s], blk);
+                return;
+            }
+            blk -= lv.s[s].tiles_w;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // role W: 16 output features x 64 input features of one stream's layer
-__device__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
+__device__ __forceinline__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
     __shared__ float tab[6][kRows];  // out-LN mean, rstd, s1, s2 | in-LN mean, rstd
-    __shared__ float bred[3][3][64];
     const int B = lv.B, K = L.K, N = L.N;
     const int nkt = (K + 63) >> 6;
     const int n0 = (blk / nkt) * 16, kt = blk % nkt;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool oln = L.out_g != nullptr, iln = L.in_g != nullptr;
+    const int q = lane >> 4;
+    const int n = n0 + (lane & 15), k = kt * 64 + wave * 16 + (lane & 15);
+    const bool nok = n < N, kok = k < K;
+    const int nc_ = nok ? n : N - 1, kc_ = kok ? k : K - 1;
+    const float *og = oln ? L.out_g : L.dsrc, *ob = oln ? L.out_b : L.dsrc, *oh = oln ? L.out : L.dsrc;
+    const float *ig = iln ? L.in_g : L.in, *ib = iln ? L.in_b : L.in;
+    // the first 64 rows' operands are requested before the row statistics are
+    // combined (unconditional loads, clamped indices)
+    const float gn = og[nc_], bn = ob[nc_], gk = ig[kc_], bk = ib[kc_];
+    float dv[4][4], hv[4][4], xv[4][4];
+#define NMLP_LOADW(BC)                                                  \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                     \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j) {                 \
+            const int bb = min((BC) + 16 * u + 4 * q + j, B - 1);       \
+            dv[u][j] = L.dsrc[(int64_t)bb * N + nc_];                   \
+            hv[u][j] = oh[(int64_t)bb * N + nc_];                       \
+            xv[u][j] = L.in[(int64_t)bb * K + kc_];                     \
+        }                                                               \
+    }
+    NMLP_LOADW(0)
     if (oln || iln) {
         for (int b = threadIdx.x; b < B; b += 256) {
             if (oln) {
@@ -289,32 +322,11 @@ __device__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
         __syncthreads();
     }
     const float invN = 1.f / (float)N;
-    auto dy = [&](int b, int n) -> float {
-        const int64_t i = (int64_t)b * N + n;
-        if (!oln) return L.dsrc[i];
-        return ln_relu_bwd(L.out[i], L.dsrc[i], L.out_g[n], L.out_b[n], tab[0][b], tab[1][b], tab[2][b], tab[3][b],
-                           invN);
-    };
-    const int q = lane >> 4;
-    const int n = n0 + (lane & 15), k = kt * 64 + wave * 16 + (lane & 15);
-    const bool nok = n < N, kok = k < K;
-    const int nc_ = nok ? n : N - 1, kc_ = kok ? k : K - 1;
-    const float *og = oln ? L.out_g : L.dsrc, *ob = oln ? L.out_b : L.dsrc, *oh = oln ? L.out : L.dsrc;
-    const float *ig = iln ? L.in_g : L.in, *ib = iln ? L.in_b : L.in;
-    const float gn = og[nc_], bn = ob[nc_], gk = ig[kc_], bk = ib[kc_];
+    // every wave reduces the whole batch for its 16 features: the bias and
+    // LayerNorm-affine sums ride along (reduced over the four lane groups after)
+    float sb = 0.f, sg = 0.f, sbeta = 0.f;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int bc = 0; bc < B; bc += 64) {  // four 16-row blocks in flight, loads unconditional
-        float dv[4][4], hv[4][4], xv[4][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int bb = min(bc + 16 * u + 4 * q + j, B - 1);
-                dv[u][j] = L.dsrc[(int64_t)bb * N + nc_];
-                hv[u][j] = oh[(int64_t)bb * N + nc_];
-                xv[u][j] = L.in[(int64_t)bb * K + kc_];
-            }
-        }
+    for (int bc = 0; bc < B; bc += 64) {  // four 16-row blocks in flight
         float a[4][4], x[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -324,18 +336,29 @@ __device__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
                 const int bb = min(b, B - 1);
                 const bool bok = b < B;
                 float d = dv[u][j];
-                if (oln) d = ln_relu_bwd(hv[u][j], d, gn, bn, tab[0][bb], tab[1][bb], tab[2][bb], tab[3][bb], invN);
+                if (oln) {
+                    const float xh = ln_xhat(hv[u][j], tab[0][bb], tab[1][bb]);
+                    const float gm = (bok && ln_y(xh, gn, bn) > 0.f) ? dv[u][j] : 0.f;
+                    sbeta += gm;
+                    sg = __fmaf_rn(gm, xh, sg);
+                    d = ln_relu_bwd(hv[u][j], d, gn, bn, tab[0][bb], tab[1][bb], tab[2][bb], tab[3][bb], invN);
+                }
                 float xa = xv[u][j];
                 if (iln) xa = fmaxf(ln_y(ln_xhat(xa, tab[4][bb], tab[5][bb]), gk, bk), 0.f);
                 a[u][j] = (bok && nok) ? d : 0.f;
                 x[u][j] = (bok && kok) ? xa : 0.f;
+                sb += a[u][j];
             }
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][j], x[u][j], acc, 0, 0, 0);
+        if (bc + 64 < B) {
+            NMLP_LOADW(bc + 64)
+        }
     }
+#undef NMLP_LOADW
     // lane: dW[n0 + 4q + i][k]
     if (kok) {
 #pragma unroll
@@ -348,40 +371,14 @@ __device__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
             }
         }
     }
-    if (kt == 0) {  // bias (and LayerNorm affine) gradients of the 16 features: rows split over 16 lane groups
-        const int grp = wave * 4 + q;
-        float sb = 0.f, sg = 0.f, sbeta = 0.f;
-        if (nok) {
-            for (int b = grp; b < B; b += 16) {
-                sb += dy(b, n);
-                if (oln) {
-                    const int64_t i = (int64_t)b * N + n;
-                    const float xh = ln_xhat(L.out[i], tab[0][b], tab[1][b]);
-                    const float g = ln_y(xh, L.out_g[n], L.out_b[n]) > 0.f ? L.dsrc[i] : 0.f;
-                    sbeta += g;
-                    sg = __fmaf_rn(g, xh, sg);
-                }
-            }
-        }
+    if (kt == 0 && wave == 0) {  // bias (and LayerNorm affine) gradients of the 16 features
         sb += __shfl_xor(sb, 16, 64);
         sb += __shfl_xor(sb, 32, 64);
         sg += __shfl_xor(sg, 16, 64);
         sg += __shfl_xor(sg, 32, 64);
         sbeta += __shfl_xor(sbeta, 16, 64);
         sbeta += __shfl_xor(sbeta, 32, 64);
-        if (wave) {
-            bred[wave - 1][0][lane] = sb;
-            bred[wave - 1][1][lane] = sg;
-            bred[wave - 1][2][lane] = sbeta;
-        }
-        __syncthreads();
-        if (wave == 0 && q == 0 && nok) {
-#pragma unroll
-            for (int w = 0; w < 3; ++w) {
-                sb += bred[w][0][lane];
-                sg += bred[w][1][lane];
-                sbeta += bred[w][2][lane];
-            }
+        if (q == 0 && nok) {
             L.gb_mu[n] = sb;
             if (L.b_sig) L.gb_sig[n] = __fmul_rn(sb, L.b_eps[n]);
             if (oln) {
@@ -393,10 +390,9 @@ __device__ void bwd_weights(const Level &lv, const Layer &L, int blk) {
 }
 
 // role X: d act(in) for 16 rows x 16 input features, over streams [s_lo, s_hi)
-__device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
+__device__ __forceinline__ void bwd_inputs(const Level &lv, const Layer &L0, int s_lo, int s_hi, int blk) {
     __shared__ float rt[6][16];  // out-LN mean, rstd, s1, s2 of the stream in hand | in-LN mean, rstd
     __shared__ f32x4 red[3][64];
-    const Layer L0 = pick(lv, s_lo);
     const int B = lv.B, K = L0.K;
     const int nrb = (B + 15) >> 4;
     const int k0 = (blk / nrb) * 16, b0 = (blk % nrb) * 16;
@@ -405,6 +401,13 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
     const int r = b0 + (lane & 15), k = k0 + (lane & 15);
     const bool rok = r < B, kok = k < K;
     const bool dpart = L0.din_part != nullptr;
+    // the epilogue's operands (din's LayerNorm inputs), requested up front
+    const int kx = kok ? k : K - 1;
+    const float *pin = dpart ? L0.in : L0.din, *pig = dpart ? L0.in_g : L0.din, *pib = dpart ? L0.in_b : L0.din;
+    float hin[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hin[i] = pin[(int64_t)min(b0 + 4 * q + i, B - 1) * K + kx];
+    const float gin = pig[kx], bin = pib[kx];
     if (dpart && threadIdx.x < 16) {  // the input's LN statistics of the 16 rows (for din's backward sums)
         const int b = b0 + threadIdx.x;
         float mu = 0.f, rs = 0.f;
@@ -413,10 +416,34 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
         rt[5][threadIdx.x] = rs;
     }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int s = s_lo; s < s_hi; ++s) {
-        const Layer L = pick(lv, s);
+#pragma unroll
+    for (int s = 0; s < AGX_NOISY_MAX_STREAMS; ++s) {
+        if (s < s_lo || s >= s_hi) continue;
+        const Layer &L = lv.s[s];
         const int N = L.N;
         const bool oln = L.out_g != nullptr;
+        const int64_t drow = (int64_t)(rok ? r : 0) * N;
+        const int kc_ = kok ? k : K - 1;
+        const bool noisy = L.w_sig != nullptr;
+        const float *wsig = noisy ? L.w_sig : L.w_mu, *weps = noisy ? L.w_eps : L.w_mu;
+        const float *oh = oln ? L.out : L.dsrc, *og = oln ? L.out_g : L.dsrc, *ob = oln ? L.out_b : L.dsrc;
+        // the stream's first n chunk is requested before its row statistics are combined
+        float dv[4][4], hv[4][4], gv[4][4], bv[4][4], wm[4][4], ws[4][4], we[4][4];
+#define NMLP_LOADX(NC)                                                  \
+        _Pragma("unroll") for (int u = 0; u < 4; ++u) {                 \
+            _Pragma("unroll") for (int j = 0; j < 4; ++j) {             \
+                const int nn = min((NC) + 64 * u + 4 * q + j, N - 1);   \
+                dv[u][j] = L.dsrc[drow + nn];                           \
+                hv[u][j] = oh[drow + nn];                               \
+                gv[u][j] = og[nn];                                      \
+                bv[u][j] = ob[nn];                                      \
+                const int64_t wi = (int64_t)nn * K + kc_;               \
+                wm[u][j] = L.w_mu[wi];                                  \
+                ws[u][j] = wsig[wi];                                    \
+                we[u][j] = weps[wi];                                    \
+            }                                                           \
+        }
+        NMLP_LOADX(wave * 16)
         float mu = 0.f, rs = 0.f, s1 = 0.f, s2 = 0.f;
         if (oln) {
             __syncthreads();  // rt of the previous stream consumed
@@ -440,28 +467,7 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
             s2 = rt[3][lane & 15];
         }
         const float invN = 1.f / (float)N;
-        const int64_t drow = (int64_t)(rok ? r : 0) * N;
-        const int kc_ = kok ? k : K - 1;
-        const bool noisy = L.w_sig != nullptr;
-        const float *wsig = noisy ? L.w_sig : L.w_mu, *weps = noisy ? L.w_eps : L.w_mu;
-        const float *oh = oln ? L.out : L.dsrc, *og = oln ? L.out_g : L.dsrc, *ob = oln ? L.out_b : L.dsrc;
         for (int nc = wave * 16; nc < N; nc += 256) {  // four 16-deep n blocks in flight, loads unconditional
-            float dv[4][4], hv[4][4], gv[4][4], bv[4][4], wm[4][4], ws[4][4], we[4][4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int nn = min(nc + 64 * u + 4 * q + j, N - 1);
-                    dv[u][j] = L.dsrc[drow + nn];
-                    hv[u][j] = oh[drow + nn];
-                    gv[u][j] = og[nn];
-                    bv[u][j] = ob[nn];
-                    const int64_t wi = (int64_t)nn * K + kc_;
-                    wm[u][j] = L.w_mu[wi];
-                    ws[u][j] = wsig[wi];
-                    we[u][j] = weps[wi];
-                }
-            }
             float a[4][4], w[4][4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -479,7 +485,11 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
             for (int u = 0; u < 4; ++u)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][j], w[u][j], acc, 0, 0, 0);
+            if (nc + 256 < N) {
+                NMLP_LOADX(nc + 256)
+            }
         }
+#undef NMLP_LOADX
     }
     if (wave) red[wave - 1][lane] = acc;
     __syncthreads();
@@ -494,8 +504,8 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
             if (dpart) {  // this tile's LayerNorm-backward sums of din (the level below reads them)
                 float gx = 0.f, xh = 0.f;
                 if (row < B && kok) {
-                    xh = ln_xhat(L0.in[(int64_t)row * K + k], rt[4][ri], rt[5][ri]);
-                    gx = ln_relu_g(xh, acc[i], L0.in_g[k], L0.in_b[k]);
+                    xh = ln_xhat(hin[i], rt[4][ri], rt[5][ri]);
+                    gx = ln_relu_g(xh, acc[i], gin, bin);
                 }
                 const float a1 = __shfl(group_sum<16>(gx), lane & ~15, 64);
                 const float a2 = __shfl(group_sum<16>(__fmul_rn(gx, xh)), lane & ~15, 64);
@@ -511,25 +521,29 @@ __device__ void bwd_inputs(const Level &lv, int s_lo, int s_hi, int blk) {
 
 __global__ __launch_bounds__(256) void bwd_kernel(Level lv) {
     int blk = blockIdx.x;
-    for (int s = 0; s < lv.S; ++s) {
-        const int t = pick(lv, s).tiles_w;
-        if (blk < t) {
-            bwd_weights(lv, pick(lv, s), blk);
-            return;
+#pragma unroll
+    for (int s = 0; s < AGX_NOISY_MAX_STREAMS; ++s) {
+        if (s < lv.S) {
+            if (blk < lv.s[s].tiles_w) {
+                bwd_weights(lv, lv.s[s], blk);
+                return;
+            }
+            blk -= lv.s[s].tiles_w;
         }
-        blk -= t;
     }
     if (lv.sum_din) {
-        bwd_inputs(lv, 0, lv.S, blk);
+        bwd_inputs(lv, lv.s[0], 0, lv.S, blk);
         return;
     }
-    for (int s = 0; s < lv.S; ++s) {
-        const int t = pick(lv, s).tiles_x;
-        if (blk < t) {
-            bwd_inputs(lv, s, s + 1, blk);
-            return;
+#pragma unroll
+    for (int s = 0; s < AGX_NOISY_MAX_STREAMS; ++s) {
+        if (s < lv.S) {
+            if (blk < lv.s[s].tiles_x) {
+                bwd_inputs(lv, lv.s[s], s, s + 1, blk);
+                return;
+            }
+            blk -= lv.s[s].tiles_x;
         }
-        blk -= t;
     }
 }
 

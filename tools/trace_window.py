@@ -2,7 +2,8 @@
 kernel trace, between marker launches (agx_debug_stream's stream_kernel<1>,
 tools/prof_config3.py): window k = the kernels between markers 2k and 2k + 1
 (k = 0: the batched loop, 1: the per-agent loop).  Writes CSV to stdout and
-the agx:: share of the window's kernel time to stderr."""
+the agx:: share of the window's kernel time to stderr; SEQ=n also lists the
+window's first n kernels in launch order (name, duration) on stderr."""
 import collections
 import csv
 import sys
@@ -28,3 +29,7 @@ span = win[-1][1] - win[0][0] if win else 0
 print(f"window {sys.argv[2] if len(sys.argv) > 2 else 'per_agent'}: {len(win)} kernels, {tot / 1e6:.2f} ms kernel time "
       f"over a {span / 1e6:.2f} ms span; agx:: kernels {agx / 1e6:.2f} ms = {100.0 * agx / max(tot, 1):.1f} %",
       file=sys.stderr)
+import os  # noqa: E402
+
+for s_, e_, n_ in win[:int(os.environ.get("SEQ", "0"))]:
+    print(f"{(e_ - s_) / 1e3:8.1f} us  {n_[:100]}", file=sys.stderr)
