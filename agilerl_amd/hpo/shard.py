@@ -238,14 +238,33 @@ class RemoteAgent:
         return applied
 
 
-def gather_records(pop, group=None) -> list[dict]:
-    """Every rank's agent records, in global agent order."""
-    world, _ = world_rank(group)
+def _local_records(pop) -> list[dict]:
     adam_steps = {}
     for a in pop:
         if hasattr(getattr(a, "population", None), "opt") and id(a.population) not in adam_steps:
             adam_steps[id(a.population)] = a.population.opt.steps.cpu().numpy()
-    local = [host_record(a, adam_steps) for a in pop]
+    return [host_record(a, adam_steps) for a in pop]
+
+
+def gather_fitness_records(pop, fitness: list, with_records: bool, group=None) -> tuple[list, list | None]:
+    """The generation's fitness scalars of every rank (global order) and, when
+    the generation step follows, every rank's agent records — one collective
+    instead of two.  -> (global fitness, global records or None)."""
+    world, _ = world_rank(group)
+    local = (list(fitness), _local_records(pop) if with_records else None)
+    if world == 1:
+        return local
+    box: list = [None] * world
+    all_gather_obj(box, local, group=group, tag="fitness_records" if with_records else "fitness")
+    if with_records and any(len(b[1]) != len(pop) for b in box):
+        raise ValueError("every rank must hold the same number of agents")
+    return [f for b in box for f in b[0]], ([r for b in box for r in b[1]] if with_records else None)
+
+
+def gather_records(pop, group=None) -> list[dict]:
+    """Every rank's agent records, in global agent order."""
+    world, _ = world_rank(group)
+    local = _local_records(pop)
     if world == 1:
         return local
     box: list = [None] * world
@@ -276,19 +295,22 @@ def _locally_shared_registry(pop):
     return None
 
 
-def global_view(pop, records: list[dict], group=None) -> list:
+def global_view(pop, records: list[dict], group=None, all_shared: bool | None = None) -> list:
     """The global population as seen from this rank: its own agents in their
-    global slots, RemoteAgent stand-ins elsewhere."""
+    global slots, RemoteAgent stand-ins elsewhere.  ``all_shared``: whether
+    every rank's agents share one registry by construction (gathered here
+    when not given)."""
     world, rank = world_rank(group)
     P = len(pop)
     shared = _locally_shared_registry(pop)
-    flags = [shared is not None]
-    if world > 1:
-        box: list = [None] * world
-        all_gather_obj(box, flags, group=group, tag="registry_flags")
-        all_shared = all(b[0] for b in box)
-    else:
-        all_shared = flags[0]
+    if all_shared is None:
+        flags = [shared is not None]
+        if world > 1:
+            box: list = [None] * world
+            all_gather_obj(box, flags, group=group, tag="registry_flags")
+            all_shared = all(b[0] for b in box)
+        else:
+            all_shared = flags[0]
     out = []
     for g, rec in enumerate(records):
         if g // P == rank:
@@ -319,9 +341,23 @@ def mutate_population(mutation, pop, pre_training_mut: bool = False, group=None)
     if world == 1:
         return mutation.mutation(pop, pre_training_mut=pre_training_mut)
     mark_sharded(pop)
-    sync_host_rngs(group)
-    records = gather_records(pop, group)
-    glob = global_view(pop, records, group)
+    # one collective for the three things the global draws need: rank 0's host
+    # generator states (every rank takes them, as sync_host_rngs would), every
+    # rank's agent records (gather_records) and its shared-registry flag
+    # (global_view) — one exchange latency per generation instead of three
+    rngs = (np.random.get_state(legacy=True), torch.get_rng_state(), random.getstate()) if rank == 0 else None
+    local = (rngs, _local_records(pop), _locally_shared_registry(pop) is not None)
+    box: list = [None] * world
+    all_gather_obj(box, local, group=group, tag="mutation_state")
+    if any(len(b[1]) != len(pop) for b in box):
+        raise ValueError("every rank must hold the same number of agents")
+    if rank != 0:
+        np_state, t_state, py_state = box[0][0]
+        np.random.set_state(np_state)
+        torch.set_rng_state(t_state)
+        random.setstate(py_state)
+    records = [r for b in box for r in b[1]]
+    glob = global_view(pop, records, group, all_shared=all(b[2] for b in box))
     out = mutation.mutation(glob, pre_training_mut=pre_training_mut)
     P = len(pop)
     mine = out[rank * P:(rank + 1) * P]

@@ -49,7 +49,7 @@ import torch.distributed as dist
 
 from ..envs import StackedVecEnv
 from ..hpo.population_sync import PopulationSync
-from ..hpo.shard import all_gather_obj, all_ranks, gather_records, mutate_population
+from ..hpo.shard import all_gather_obj, all_ranks, gather_fitness_records, mutate_population
 from ..population.engine import PopulationEngine
 
 
@@ -236,18 +236,16 @@ def train_on_policy(env, env_name: str, algo: str, pop, INIT_HP=None, MUT_P=None
                 agent.scores.append(float(r_sum[i] / r_cnt[i]))
             agent.fitness.append(fitness[i])
             agent.steps.append(agent.steps[-1])
-        if world > 1:
-            box: list = [None] * world
-            all_gather_obj(box, fitness, tag="fitness")
-            pop_fitnesses.append([f for b in box for f in b])
-        else:
-            pop_fitnesses.append(fitness)
+        # the fitness scalars and, when a generation step follows, the agents'
+        # host records it clones from: one exchange
+        global_fit, gathered = gather_fitness_records(pop, fitness, sync is not None)
+        pop_fitnesses.append(global_fit if world > 1 else fitness)
         if target is not None and all_ranks(np.all(np.greater([np.mean(a.fitness[-10:]) for a in pop], target))) \
                 and len(pop[0].steps) >= 100:
             return pop, pop_fitnesses
         if sync is not None:  # tournament_selection_and_mutation (utils.py:1137-1225)
             with _Phase("select"):
-                records = gather_records(pop)  # every global agent's host attributes, before the clone
+                records = gathered  # every global agent's host attributes, before the clone
                 sync.fitness_override = np.asarray(fitness)  # reduced on the host already: hand it over
                 if _all_one_group(engine):
                     # one network shape and rollout length everywhere: parent rows move in HBM
