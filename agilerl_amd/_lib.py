@@ -109,6 +109,8 @@ SIGNATURES = {
     "agx_dueling_head_forward_rows": (_INT, [_P, _P, _P, _I, _I, _I, _INT, _P, _P]),
     "agx_dueling_head_backward_rows": (_INT, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "agx_conv2d_forward_grouped": (_INT, [_P, _I, _P, _I, _INT, _F, _F, _P, _I, _P, _I, _INT, _P, _I, _P]),
+    "agx_conv2d_forward_grouped2": (_INT, [_P, _I, _I, _P, _I, _I, _INT, _F, _F, _P, _I, _I, _P, _I, _I, _INT, _P,
+                                           _I, _I, _P]),
     "agx_conv2d_wgrad_workspace_bytes_grouped": (_SZ, [_P, _I]),
     "agx_conv2d_backward_grouped": (_INT, [_P, _I, _P, _I, _INT, _F, _F, _P, _I, _P, _P, _I, _P, _P, _P,
                                            _INT, _P, _P]),

@@ -330,6 +330,140 @@ def _next_pair(agent, next_obs):
     return a_star, DuelingRowsFn.apply(v_tg, a_tg, a_star, A, Z, 1)
 
 
+class _TripleConvFn(torch.autograd.Function):
+    """One encoder layer of a Rainbow update's three forwards in one launch
+    (agx_conv2d_forward_grouped2, group g = g1 + 2 g2): g = 0 the online
+    network on s', 1 the online network on s (the one the loss
+    differentiates), 2 the target network on s'; g1 picks the frames, g2 the
+    network (online and target parameters are the rows of the flat state's
+    pair buffer, n elements apart).  -> (y3 [3, B, C, OH, OW] without
+    gradient, y3[1] with it); the backward is group 1's convolution backward
+    alone (Conv2dFn.backward)."""
+
+    @staticmethod
+    def forward(ctx, x1, w, b, x3, x_strides, n, stride, relu, norm):
+        import ctypes
+
+        from .. import _lib
+        from ..modules.cnn import _shape
+
+        u8 = x1.dtype == torch.uint8
+        sh = _shape(x1, w, stride)
+        OH = (sh.height - sh.kernel_h) // stride + 1
+        OW = (sh.width - sh.kernel_w) // stride + 1
+        B = x1.shape[0]
+        y3 = torch.empty(3, B, w.shape[0], OH, OW, dtype=torch.float32, device=x1.device)
+        Y = y3[0].numel()
+        lo, hi = (float(norm[0]), float(norm[1])) if u8 else (0.0, 1.0)
+        _lib.call("agx_conv2d_forward_grouped2", ctypes.byref(sh), 3, 2, x3.data_ptr(), x_strides[0], x_strides[1],
+                  int(u8), lo, hi, w.data_ptr(), 0, n, b.data_ptr(), 0, n, int(relu), y3.data_ptr(), Y, 2 * Y,
+                  _lib.stream())
+        y1 = y3[1]
+        ctx.save_for_backward(x1, w, y1 if relu else None)
+        ctx.meta = (stride, relu, u8, lo, hi)
+        ctx.mark_non_differentiable(y3)
+        return y3, y1
+
+    @staticmethod
+    def backward(ctx, _g3, dy):
+        import ctypes
+
+        from .. import _lib
+        from ..modules.cnn import _shape
+
+        x, w, y = ctx.saved_tensors
+        stride, relu, u8, lo, hi = ctx.meta
+        sh = _shape(x, w, stride)
+        dy = dy.contiguous()
+        dw = torch.empty_like(w)
+        db = torch.empty(w.shape[0], dtype=torch.float32, device=w.device)
+        dx = torch.empty_like(x) if (ctx.needs_input_grad[0] and not u8) else None
+        ws = torch.empty(max(16, _lib.load().agx_conv2d_wgrad_workspace_bytes(ctypes.byref(sh))), dtype=torch.uint8,
+                         device=w.device)
+        _lib.call("agx_conv2d_backward", ctypes.byref(sh), x.data_ptr(), int(u8), lo, hi, w.data_ptr(), _lib.ptr(y),
+                  dy.data_ptr(), _lib.ptr(dx), dw.data_ptr(), db.data_ptr(), 0, ws.data_ptr(), _lib.stream())
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def _triple_pass(agent, obs, acts, next_obs):
+    """A Rainbow update's three network passes (dqn_rainbow.py:284-367: the
+    online network on s' for a*, the target network on s' for the target
+    distribution, the online network on s for log p) with every encoder layer
+    one grouped launch over all three (_TripleConvFn), the pair's Linear one
+    batched GEMM, the pair's four head streams one launch per depth and the
+    online head on s the autograd head streams.  -> (log p rows [B, Z] with
+    gradient, target rows [B, Z]), or None where the network is not the CNN +
+    dueling head this covers (the caller runs the three forwards)."""
+    from torch import nn
+    from torch.nn import functional as F
+
+    from ..modules.cnn import AgxConv2d, EvolvableCNN, _FusedIdentity
+    from ..modules.noisy_streams import head_streams_each
+    from ..networks.q_networks import DuelingDistributionalMLP, DuelingHeadFn, DuelingRowsFn
+    from .learn_graph import _hooked
+
+    actor, target = agent.actor, agent.actor_target
+    enc = getattr(actor, "encoder", None)
+    if (not isinstance(enc, EvolvableCNN) or not isinstance(getattr(actor, "head_net", None), DuelingDistributionalMLP)
+            or getattr(actor, "flatten_obs", False) or not isinstance(next_obs, torch.Tensor)
+            or not isinstance(obs, torch.Tensor) or not next_obs.is_cuda or next_obs.dim() != 4
+            or obs.shape != next_obs.shape or obs.dtype != next_obs.dtype or agent.num_atoms > 64
+            or _hooked(actor, target) or not torch.is_grad_enabled()):
+        return None
+    fs = flat_state(agent)
+    if fs is None:
+        return None
+    mods = list(enc.model.children())
+    convs = [m for m in mods if type(m) is AgxConv2d]
+    if not convs or any(m.bias is None for m in convs):
+        return None
+    if obs.dtype == torch.uint8 and convs[0].image_norm is None:
+        return None
+    if obs.dtype not in (torch.uint8, torch.float32):
+        return None
+    B = obs.shape[0]
+    frames = torch.stack([next_obs, obs])  # g1 = 0: s', g1 = 1: s
+    x1, x3, xs, first = frames[1], frames, (frames[0].numel(), 0), True
+    y3 = None
+    lat_pair = lat_s = None
+    for mod in mods:
+        if type(mod) is AgxConv2d:
+            y3, x1 = _TripleConvFn.apply(x1, mod.weight, mod.bias, x3, xs, fs.n, int(mod.stride[0]), mod.fuse_relu,
+                                         mod.image_norm if x1.dtype == torch.uint8 else None)
+            x3, xs, first = y3, (y3[0].numel(), 2 * y3[0].numel()), False
+        elif type(mod) is _FusedIdentity or type(mod) is nn.Identity:
+            pass
+        elif type(mod) is nn.Flatten and not first and lat_pair is None:
+            pass  # flattened below with the Linear
+        elif type(mod) is nn.Linear and not first and lat_pair is None and mod.bias is not None:
+            F_ = y3[0].numel() // B
+            pair = y3.reshape(3, B, F_)[0::2]  # online and target on s'
+            w2, b2 = fs.pair_view(mod.weight), fs.pair_view(mod.bias)
+            with torch.no_grad():
+                lat_pair = torch.baddbmm(b2.unsqueeze(1), pair, w2.transpose(1, 2))
+            lat_s = F.linear(x1.reshape(B, F_), mod.weight, mod.bias)
+        elif type(mod) is nn.ReLU and lat_pair is not None:
+            with torch.no_grad():
+                lat_pair = torch.relu(lat_pair)
+            lat_s = torch.relu(lat_s)
+        else:
+            return None
+    if lat_pair is None:
+        return None
+    ha, ht = actor.head_net, target.head_net
+    with torch.no_grad():
+        out = head_streams_each([ha.model, ha.advantage_net, ht.model, ht.advantage_net],
+                                [lat_pair[0], lat_pair[0], lat_pair[1], lat_pair[1]])
+        if out is None:
+            return None
+        v_on, a_on, v_tg, a_tg = out
+        A, Z = agent.action_dim, agent.num_atoms
+        a_star = DuelingHeadFn.apply(v_on, a_on, ha.support, A, Z, 0).argmax(1)  # first maximum, as the reference
+        target_rows = DuelingRowsFn.apply(v_tg, a_tg, a_star, A, Z, 1)
+    logp_rows = actor.head_net(lat_s, q=False, log=True, rows=acts)
+    return logp_rows, target_rows
+
+
 class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
     """Drop-in RainbowDQN (agilerl/algorithms/dqn_rainbow.py:77-501) with the
     C51 projection + loss in agx_c51_project_loss and Polyak in agx_polyak."""
@@ -410,6 +544,11 @@ class RainbowDQN(EvolvableAgentMixin, C.TorchCheckpointMixin):
         if self.num_atoms == 51 and self.device.type == "cuda":
             # the heads emit only the selected rows (target_dist[range(B), a*],
             # log_p[range(B), action]); the C51 step streams them contiguously
+            fused = _triple_pass(self, obs, acts, next_obs)
+            if fused is not None:
+                logp_rows, target_rows = fused
+                return _C51RowsLoss.apply(logp_rows, target_rows, rew, done, self.support, float(self.v_min),
+                                          float(self.v_max), float(gamma))
             with torch.no_grad():
                 pair = _next_pair(self, next_obs)
                 if pair is not None:

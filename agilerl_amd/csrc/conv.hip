@@ -86,12 +86,17 @@ struct FwdOps {
     Shape s;
     int M, N, K;
     long long gx, gw, gb, gy;  // per-group element strides (population-batched launch)
+    // two-level group index (agx_conv2d_forward_grouped2): g = g1 + G1 * g2,
+    // the g2 strides below; G1 <= 0: one level (g1 = g)
+    long long gx2, gw2, gb2, gy2;
+    int G1;
     __device__ FwdOps at(int g) const {
+        const long long g1 = G1 > 0 ? g % G1 : g, g2 = G1 > 0 ? g / G1 : 0;
         FwdOps o = *this;
-        o.x = static_cast<const char *>(x) + (size_t)g * gx * (U8 ? 1 : 4);
-        o.w = w + (size_t)g * gw;
-        o.bias = bias ? bias + (size_t)g * gb : nullptr;
-        o.y = y + (size_t)g * gy;
+        o.x = static_cast<const char *>(x) + (g1 * gx + g2 * gx2) * (U8 ? 1 : 4);
+        o.w = w + (g1 * gw + g2 * gw2);
+        o.bias = bias ? bias + (g1 * gb + g2 * gb2) : nullptr;
+        o.y = y + (g1 * gy + g2 * gy2);
         return o;
     }
     __device__ int kend(int k1) const { return k1; }
@@ -593,6 +598,30 @@ extern "C" int agx_conv2d_forward_grouped(const agx_conv2d_shape *shape, int64_t
         launch(o, M, N, 0, K, 0, 1, (int)groups, st);
     }
     return check_launch("agx_conv2d_forward");
+}
+
+extern "C" int agx_conv2d_forward_grouped2(const agx_conv2d_shape *shape, int64_t groups, int64_t g1_count,
+                                           const void *x, int64_t x_stride1, int64_t x_stride2, int x_is_u8,
+                                           float x_low, float x_high, const float *w, int64_t w_stride1,
+                                           int64_t w_stride2, const float *bias, int64_t b_stride1, int64_t b_stride2,
+                                           int relu, float *y, int64_t y_stride1, int64_t y_stride2, void *stream) {
+    Shape s;
+    if (int rc = check_shape(shape, s, "agx_conv2d_forward_grouped2")) return rc;
+    AGX_REQUIRE(x && w && y && groups >= 1 && groups < 65536 && g1_count >= 1 && g1_count <= groups,
+                "agx_conv2d_forward_grouped2: null pointer or bad groups");
+    AGX_REQUIRE(!x_is_u8 || x_high > x_low, "agx_conv2d_forward_grouped2: u8 input needs high > low");
+    const int M = s.Cout, N = s.B * s.OH * s.OW, K = s.Cin * s.KH * s.KW;
+    hipStream_t st = as_stream(stream);
+    if (x_is_u8) {
+        FwdOps<true> o{w, x, bias, y, x_low, x_high - x_low, relu, s, M, N, K, x_stride1, w_stride1, b_stride1,
+                       y_stride1, x_stride2, w_stride2, b_stride2, y_stride2, (int)g1_count};
+        launch(o, M, N, 0, K, 0, 1, (int)groups, st);
+    } else {
+        FwdOps<false> o{w, x, bias, y, 0.f, 1.f, relu, s, M, N, K, x_stride1, w_stride1, b_stride1, y_stride1,
+                        x_stride2, w_stride2, b_stride2, y_stride2, (int)g1_count};
+        launch(o, M, N, 0, K, 0, 1, (int)groups, st);
+    }
+    return check_launch("agx_conv2d_forward_grouped2");
 }
 
 extern "C" int agx_conv2d_forward(const agx_conv2d_shape *shape, const void *x, int x_is_u8, float x_low,

@@ -511,6 +511,16 @@ int agx_conv2d_forward_grouped(const agx_conv2d_shape *shape, int64_t groups, co
                                int x_is_u8, float x_low, float x_high, const float *w, int64_t w_gstride,
                                const float *bias, int64_t b_gstride, int relu, float *y, int64_t y_gstride,
                                void *stream);
+/* The grouped forward over a two-level group index g = g1 + g1_count * g2
+ * (g1 < g1_count): group g reads x + g1*x_stride1 + g2*x_stride2 and likewise
+ * w, bias, y.  RainbowDQN's update runs its three no-padding CNN forwards
+ * (online on s', online on s, target on s': g1 picks the frames, g2 the
+ * network) as one launch per layer (dqn_rainbow.py:284-367). */
+int agx_conv2d_forward_grouped2(const agx_conv2d_shape *shape, int64_t groups, int64_t g1_count, const void *x,
+                                int64_t x_stride1, int64_t x_stride2, int x_is_u8, float x_low, float x_high,
+                                const float *w, int64_t w_stride1, int64_t w_stride2, const float *bias,
+                                int64_t b_stride1, int64_t b_stride2, int relu, float *y, int64_t y_stride1,
+                                int64_t y_stride2, void *stream);
 size_t agx_conv2d_wgrad_workspace_bytes_grouped(const agx_conv2d_shape *shape, int64_t groups);
 int agx_conv2d_backward_grouped(const agx_conv2d_shape *shape, int64_t groups, const void *x, int64_t x_gstride,
                                 int x_is_u8, float x_low, float x_high, const float *w, int64_t w_gstride,

@@ -230,3 +230,48 @@ def test_rainbow_next_pair_matches_the_two_forwards():
         rows_ref = agent.actor_target(obs, q=False, rows=a_ref)
     assert torch.equal(pair[0], a_ref)
     _check(pair[1], rows_ref, 1e-5, "target rows")
+
+
+def test_rainbow_triple_pass_matches_the_three_forwards():
+    """The update's three passes as one grouped launch per encoder layer
+    (dqn._triple_pass: online on s', target on s', online on s with gradient)
+    against the reference's three separate forwards: the target rows, the
+    taken actions' log-probabilities and the gradient of every online
+    parameter."""
+    import numpy as np
+
+    from agilerl_amd.algorithms import RainbowDQN
+    from agilerl_amd.algorithms.dqn import _triple_pass
+    from agilerl_amd.algorithms.flat_state import flat_state
+    from agilerl_amd.envs import Box, Discrete
+
+    torch.manual_seed(4)
+    net = {"latent_dim": 256, "max_latent_dim": 512, "encoder_config": {
+        "channel_size": [32, 64, 128], "kernel_size": [8, 4, 3], "stride_size": [4, 2, 1]},
+        "head_config": {"hidden_size": [256]}}
+    agent = RainbowDQN(Box(0, 255, (4, 84, 84), dtype=np.uint8), Discrete(6), net_config=net, v_min=-200.0,
+                       v_max=200.0)
+    assert flat_state(agent) is not None
+    with torch.no_grad():
+        for p in agent.actor_target.parameters():
+            p.add_(0.02 * torch.randn_like(p))
+    obs = torch.randint(0, 256, (64, 4, 84, 84), dtype=torch.uint8, device=DEV)
+    nxt = torch.randint(0, 256, (64, 4, 84, 84), dtype=torch.uint8, device=DEV)
+    acts = torch.randint(0, 6, (64,), device=DEV)
+    g = torch.randn(64, 51, device=DEV)
+    params = list(agent.actor.parameters())
+
+    out = _triple_pass(agent, obs, acts, nxt)
+    assert out is not None, "the triple pass did not take the config-3 network"
+    logp, trows = out
+    grads = torch.autograd.grad((logp * g).sum(), params)
+
+    with torch.no_grad():
+        a_ref = agent.actor(nxt).argmax(1)
+        trows_ref = agent.actor_target(nxt, q=False, rows=a_ref)
+    logp_ref = agent.actor(obs, q=False, log=True, rows=acts)
+    grads_ref = torch.autograd.grad((logp_ref * g).sum(), params)
+    _check(trows, trows_ref, 1e-5, "target rows")
+    _check(logp, logp_ref, 1e-5, "log p rows")
+    for (n, _), a, b in zip(agent.actor.named_parameters(), grads, grads_ref):
+        _check(a, b, 1e-4, n)
