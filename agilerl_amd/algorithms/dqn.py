@@ -362,6 +362,7 @@ class _TripleConvFn(torch.autograd.Function):
         ctx.save_for_backward(x1, w, y1 if relu else None)
         ctx.meta = (stride, relu, u8, lo, hi)
         ctx.mark_non_differentiable(y3)
+        ctx.set_materialize_grads(False)  # no zero-filled [3, B, C, OH, OW] gradient for y3
         return y3, y1
 
     @staticmethod
@@ -373,6 +374,8 @@ class _TripleConvFn(torch.autograd.Function):
 
         x, w, y = ctx.saved_tensors
         stride, relu, u8, lo, hi = ctx.meta
+        if dy is None:
+            return (None,) * 9
         sh = _shape(x, w, stride)
         dy = dy.contiguous()
         dw = torch.empty_like(w)
