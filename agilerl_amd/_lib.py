@@ -111,6 +111,7 @@ SIGNATURES = {
     "agx_conv2d_forward_grouped": (_INT, [_P, _I, _P, _I, _INT, _F, _F, _P, _I, _P, _I, _INT, _P, _I, _P]),
     "agx_conv2d_forward_grouped2": (_INT, [_P, _I, _I, _P, _I, _I, _INT, _F, _F, _P, _I, _I, _P, _I, _I, _INT, _P,
                                            _I, _I, _P]),
+    "agx_replay_gather": (_INT, [_P, _P, _P, _INT, _P, _I, _I, _P, _P]),
     "agx_conv2d_wgrad_workspace_bytes_grouped": (_SZ, [_P, _I]),
     "agx_conv2d_backward_grouped": (_INT, [_P, _I, _P, _I, _INT, _F, _F, _P, _I, _P, _P, _I, _P, _P, _P,
                                            _INT, _P, _P]),

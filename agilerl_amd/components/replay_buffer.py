@@ -104,9 +104,32 @@ class ReplayBuffer:
         idx = indices.to(self.device)
         return {k: v.index_select(0, idx) for k, v in self._storage.items()}
 
+    def _gather_sampled(self, indices: torch.Tensor) -> dict[str, torch.Tensor]:
+        """The sampler's own (in-range) indices: every field's rows in one
+        agx_replay_gather launch on the GPU (one index op per field on the CPU)."""
+        st = self._storage
+        if (self.device.type != "cuda" or not st or len(st) > 8
+                or any(not v.is_contiguous() or v.shape[0] != self.max_size for v in st.values())):
+            return self._gather(indices)
+        import ctypes
+
+        from .. import _lib
+
+        idx = indices.to(device=self.device, dtype=torch.int64).contiguous()
+        B = idx.numel()
+        outs = {k: torch.empty((B, *v.shape[1:]), dtype=v.dtype, device=self.device) for k, v in st.items()}
+        vals = list(st.values())
+        n = len(vals)
+        srcs = (ctypes.c_void_p * n)(*[v.data_ptr() for v in vals])
+        dsts = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs.values()])
+        rbytes = (ctypes.c_int64 * n)(*[v[0].numel() * v.element_size() for v in vals])
+        _lib.call("agx_replay_gather", ctypes.cast(srcs, ctypes.c_void_p), ctypes.cast(dsts, ctypes.c_void_p),
+                  ctypes.cast(rbytes, ctypes.c_void_p), n, idx.data_ptr(), B, self.max_size, None, _lib.stream())
+        return outs
+
     def sample(self, batch_size: int, return_idx: bool = False) -> dict[str, torch.Tensor]:
         indices = torch.randperm(self.size)[:batch_size]  # global CPU generator, as the reference
-        samples = self._gather(indices)
+        samples = self._gather_sampled(indices)
         if return_idx:
             samples["idxs"] = indices.to(self.device)
         return samples
@@ -220,7 +243,7 @@ class PrioritizedReplayBuffer(ReplayBuffer):
                               beta=beta, weights=True, err=err)
         if int(err.item()) != 0:  # segment_tree.py:145
             raise AssertionError("upperbound outside [0, sum + 1e-5]")
-        samples = self._gather(idx)
+        samples = self._gather_sampled(idx)
         samples["weights"] = w.unsqueeze(1)
         samples["idxs"] = idx.unsqueeze(1)
         return samples
