@@ -40,6 +40,27 @@ from ..modules.cnn import Conv2dGroupedFn
 from .nets import ActorCriticSpec, Layer
 
 
+class BatchedLinearFn(torch.autograd.Function):
+    """y [P, B, out] = x [P, B, in] @ W[p]^T + b[p] for every agent p (the
+    population's Linear layers, one batched GEMM), with the backward's weight
+    gradient formed directly in W's own [P, out, in] layout (dy^T x): autograd
+    of ``baddbmm(b, x, W.transpose(1, 2))`` builds it as the transpose of
+    x^T dy and copies it back into the parameter chunk's layout."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        return torch.baddbmm(b.unsqueeze(1), x, W.transpose(1, 2))
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dx = torch.bmm(dy, W) if ctx.needs_input_grad[0] else None
+        dW = torch.bmm(dy.transpose(1, 2), x) if ctx.needs_input_grad[1] else None
+        db = dy.sum(1) if ctx.needs_input_grad[2] else None
+        return dx, dW, db
+
+
 @dataclass
 class ImageActorCriticSpec:
     obs_shape: tuple[int, int, int]
@@ -164,7 +185,7 @@ class ImageActorCriticSpec:
         P = x.shape[0]
         for lay in layers:
             W, b = self._chunk(parts, lay.w, P), self._chunk(parts, lay.b, P)
-            x = torch.baddbmm(b.unsqueeze(1), x, W.transpose(1, 2))
+            x = BatchedLinearFn.apply(x, W, b)
             if lay.ln is not None:
                 x = F.layer_norm(x, (lay.fout,), eps=1e-5)
                 if lay.ln == "affine":
@@ -204,8 +225,7 @@ class ImageActorCriticSpec:
         parts = self._split(flat)
         feat = self.features(flat, obs, parts, rows)
         lo = self.lin_out
-        lat = torch.relu(torch.baddbmm(self._chunk(parts, lo.b, P).unsqueeze(1), feat,
-                                       self._chunk(parts, lo.w, P).transpose(1, 2)))
+        lat = torch.relu(BatchedLinearFn.apply(feat, self._chunk(parts, lo.w, P), self._chunk(parts, lo.b, P)))
         logits = self._head(parts, lat, self.actor)
         value = self._head(parts, lat, self.critic).squeeze(-1)
         return logits, value
