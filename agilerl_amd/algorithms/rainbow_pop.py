@@ -48,6 +48,7 @@ from ..modules.cnn import AgxConv2d, Conv2dGroupedFn, _FusedIdentity
 from ..modules.custom_components import NoisyLinear
 from ..modules.mlp import EvolvableMLP
 from ..modules.cnn import EvolvableCNN
+from ..population.image_nets import BatchedLinearFn
 
 
 class _Rows:
@@ -202,7 +203,7 @@ class RainbowPopulationLearner:
             b = P_(f"{name}.bias_mu") + P_(f"{name}.bias_sigma") * noise.view(f"{name}.bias_epsilon")
         else:
             w, b = P_(f"{name}.weight"), P_(f"{name}.bias")
-        return torch.baddbmm(b.unsqueeze(1), x, w.transpose(1, 2))
+        return BatchedLinearFn.apply(x, w, b)
 
     def _seq(self, x, ops, params, rows, noise):
         for name, mod in ops:
