@@ -129,9 +129,12 @@ class Conv2dGroupedFn(torch.autograd.Function):
         stride, relu, u8, lo, hi = ctx.meta
         G = x.shape[0]
         sh = _shape(x[0], w[0], stride)
-        # dZ = dY * relu'(Y) once (one elementwise pass) instead of a second
-        # (mask) load per gathered element in both the wgrad and the dgrad GEMM
-        dy = (dy * (y > 0)).contiguous() if y is not None else dy.contiguous()
+        # dZ = dY * relu'(Y) once (one elementwise pass: ReLU's own backward
+        # kernel, not a compare + cast + product) instead of a second (mask)
+        # load per gathered element in both the wgrad and the dgrad GEMM
+        dy = dy.contiguous()
+        if y is not None:
+            dy = torch.ops.aten.threshold_backward(dy, y, 0.0)
         dw = torch.empty((G, *w.shape[1:]), dtype=torch.float32, device=w.device)
         db = torch.empty(G, w.shape[1], dtype=torch.float32, device=w.device)
         need_dx = ctx.needs_input_grad[0] and not u8
