@@ -401,7 +401,7 @@ def _triple_pass(agent, obs, acts, next_obs):
     from torch.nn import functional as F
 
     from ..modules.cnn import AgxConv2d, EvolvableCNN, _FusedIdentity
-    from ..modules.noisy_streams import head_streams_each
+    from ..modules.noisy_streams import head_streams_each, mixed_streams
     from ..networks.q_networks import DuelingDistributionalMLP, DuelingHeadFn, DuelingRowsFn
     from .learn_graph import _hooked
 
@@ -454,16 +454,25 @@ def _triple_pass(agent, obs, acts, next_obs):
     if lat_pair is None:
         return None
     ha, ht = actor.head_net, target.head_net
-    with torch.no_grad():
-        out = head_streams_each([ha.model, ha.advantage_net, ht.model, ht.advantage_net],
-                                [lat_pair[0], lat_pair[0], lat_pair[1], lat_pair[1]])
+    A, Z = agent.action_dim, agent.num_atoms
+    # the pair's four streams (no gradient) and the online head on s (with
+    # it) in one launch per depth
+    out = mixed_streams([ha.model, ha.advantage_net, ht.model, ht.advantage_net],
+                        [lat_pair[0], lat_pair[0], lat_pair[1], lat_pair[1]], [ha.model, ha.advantage_net], lat_s)
+    if out is not None:
+        v_on, a_on, v_tg, a_tg, v_s, a_s = out
+        logp_rows = DuelingRowsFn.apply(v_s, a_s, acts, A, Z, 2)
+    else:
+        with torch.no_grad():
+            out = head_streams_each([ha.model, ha.advantage_net, ht.model, ht.advantage_net],
+                                    [lat_pair[0], lat_pair[0], lat_pair[1], lat_pair[1]])
         if out is None:
             return None
         v_on, a_on, v_tg, a_tg = out
-        A, Z = agent.action_dim, agent.num_atoms
+        logp_rows = actor.head_net(lat_s, q=False, log=True, rows=acts)
+    with torch.no_grad():
         a_star = DuelingHeadFn.apply(v_on, a_on, ha.support, A, Z, 0).argmax(1)  # first maximum, as the reference
         target_rows = DuelingRowsFn.apply(v_tg, a_tg, a_star, A, Z, 1)
-    logp_rows = actor.head_net(lat_s, q=False, log=True, rows=acts)
     return logp_rows, target_rows
 
 

@@ -628,7 +628,8 @@ extern "C" int agx_noisy_streams_forward(const agx_noisy_stream_layer *layers, i
     if (int rc = check_layers(layers, S, NL, B, "agx_noisy_streams_forward")) return rc;
     AGX_REQUIRE(x, "agx_noisy_streams_forward: x is NULL");
     if (B == 0) return AGX_OK;
-    const float *xs[AGX_NOISY_MAX_STREAMS] = {x, x, x, x};
+    const float *xs[AGX_NOISY_MAX_STREAMS];
+    for (int s = 0; s < AGX_NOISY_MAX_STREAMS; ++s) xs[s] = x;
     return forward_streams(layers, S, NL, xs, B, ln_eps, stream);
 }
 

@@ -164,29 +164,34 @@ class NoisyStreamsFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *gouts):
-        meta = ctx.meta
-        saved = ctx.saved_tensors
-        nl = len(meta.layers)
-        x, ts = saved[0], saved[1:1 + meta.n_tensors]
-        outs = saved[1 + meta.n_tensors:1 + meta.n_tensors + nl]
-        rest = iter(saved[1 + meta.n_tensors + nl:])
-        parts = [next(rest) if has else None for has in ctx.parts]
-        B = x.shape[0]
-        grads = [torch.empty_like(t) for t in ts]
-        gx = torch.empty_like(x) if ctx.needs_input_grad[1] else None
-        gs = []
-        for s, g in enumerate(gouts):
-            fout = meta.layers[s * meta.NL + meta.NL - 1]["fout"]
-            gs.append(torch.zeros(B, fout, dtype=torch.float32, device=x.device) if g is None else
-                      g.to(torch.float32).contiguous())
-        arr = _layer_array(meta, ts, outs, parts, grads)
-        lib = _lib.load()
-        nws = lib.agx_noisy_streams_workspace_bytes(ctypes.cast(arr, ctypes.c_void_p), meta.S, meta.NL, B)
-        ws = torch.empty(max(16, nws), dtype=torch.uint8, device=x.device)
-        gptr = (ctypes.c_void_p * meta.S)(*[g.data_ptr() for g in gs])
-        _lib.call("agx_noisy_streams_backward", ctypes.cast(arr, ctypes.c_void_p), meta.S, meta.NL, x.data_ptr(), B,
-                  meta.eps, ctypes.cast(gptr, ctypes.c_void_p), _lib.ptr(gx), ws.data_ptr(), _lib.stream())
-        return (None, gx, *[g if ctx.needs_input_grad[2 + i] else None for i, g in enumerate(grads)])
+        return (None, *_streams_backward(ctx, ctx.meta, gouts, 1))
+
+
+def _streams_backward(ctx, meta, gouts, first: int) -> list:
+    """Gradients of x and of every stream tensor from the saved (x, ts, outs,
+    parts); ``first``: index of x among the Function's inputs."""
+    saved = ctx.saved_tensors
+    nl = len(meta.layers)
+    x, ts = saved[0], saved[1:1 + meta.n_tensors]
+    outs = saved[1 + meta.n_tensors:1 + meta.n_tensors + nl]
+    rest = iter(saved[1 + meta.n_tensors + nl:])
+    parts = [next(rest) if has else None for has in ctx.parts]
+    B = x.shape[0]
+    grads = [torch.empty_like(t) for t in ts]
+    gx = torch.empty_like(x) if ctx.needs_input_grad[first] else None
+    gs = []
+    for s, g in enumerate(gouts):
+        fout = meta.layers[s * meta.NL + meta.NL - 1]["fout"]
+        gs.append(torch.zeros(B, fout, dtype=torch.float32, device=x.device) if g is None else
+                  g.to(torch.float32).contiguous())
+    arr = _layer_array(meta, ts, outs, parts, grads)
+    lib = _lib.load()
+    nws = lib.agx_noisy_streams_workspace_bytes(ctypes.cast(arr, ctypes.c_void_p), meta.S, meta.NL, B)
+    ws = torch.empty(max(16, nws), dtype=torch.uint8, device=x.device)
+    gptr = (ctypes.c_void_p * meta.S)(*[g.data_ptr() for g in gs])
+    _lib.call("agx_noisy_streams_backward", ctypes.cast(arr, ctypes.c_void_p), meta.S, meta.NL, x.data_ptr(), B,
+              meta.eps, ctypes.cast(gptr, ctypes.c_void_p), _lib.ptr(gx), ws.data_ptr(), _lib.stream())
+    return [gx, *[g if ctx.needs_input_grad[first + 1 + i] else None for i, g in enumerate(grads)]]
 
 
 def head_streams(streams: list, x: torch.Tensor):
@@ -240,3 +245,67 @@ def head_streams_each(streams: list, xs: list):
     _lib.call("agx_noisy_streams_forward_each", ctypes.cast(arr, ctypes.c_void_p), meta.S, meta.NL,
               ctypes.cast(xp, ctypes.c_void_p), B, meta.eps, _lib.stream())
     return tuple(outs[s * meta.NL + meta.NL - 1] for s in range(meta.S))
+
+
+class MixedStreamsFn(torch.autograd.Function):
+    """No-grad streams (each on its own input) and grad streams (on x) in one
+    launch per depth (agx_noisy_streams_forward_each): -> the no-grad
+    streams' outputs (without gradient), then the grad streams' outputs; the
+    backward is the grad streams' alone (NoisyStreamsFn's)."""
+
+    @staticmethod
+    def forward(ctx, meta_g, meta_ng, ts_ng, xs_ng, x, *ts):
+        x = x.contiguous()
+        B = x.shape[0]
+        S_ng, S_g = meta_ng.S, meta_g.S
+        out_ng = [torch.empty(B, d["fout"], dtype=torch.float32, device=x.device) for d in meta_ng.layers]
+        out_g = [torch.empty(B, d["fout"], dtype=torch.float32, device=x.device) for d in meta_g.layers]
+        part = lambda d: (torch.empty(B, (d["fout"] + 15) // 16, 2, dtype=torch.float32, device=x.device)
+                          if "ln_gamma" in d else None)
+        part_ng = [part(d) for d in meta_ng.layers]
+        part_g = [part(d) for d in meta_g.layers]
+        a_ng = _layer_array(meta_ng, ts_ng, out_ng, part_ng)
+        a_g = _layer_array(meta_g, ts, out_g, part_g)
+        arr = (AgxNoisyStreamLayer * (len(a_ng) + len(a_g)))(*a_ng, *a_g)
+        xp = (ctypes.c_void_p * (S_ng + S_g))(*[t.data_ptr() for t in xs_ng], *([x.data_ptr()] * S_g))
+        _lib.call("agx_noisy_streams_forward_each", ctypes.cast(arr, ctypes.c_void_p), S_ng + S_g, meta_g.NL,
+                  ctypes.cast(xp, ctypes.c_void_p), B, meta_g.eps, _lib.stream())
+        ctx.meta = meta_g
+        ctx.parts = [p is not None for p in part_g]
+        ctx.save_for_backward(x, *ts, *out_g, *[p for p in part_g if p is not None])
+        outs_ng = tuple(out_ng[s * meta_ng.NL + meta_ng.NL - 1] for s in range(S_ng))
+        ctx.mark_non_differentiable(*outs_ng)
+        return outs_ng + tuple(out_g[s * meta_g.NL + meta_g.NL - 1] for s in range(S_g))
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        meta = ctx.meta
+        return (None, None, None, None, *_streams_backward(ctx, meta, gouts[len(gouts) - meta.S:], 4))
+
+
+def mixed_streams(nograd_streams: list, nograd_xs: list, grad_streams: list, x: torch.Tensor):
+    """(no-grad outputs..., grad outputs...) of RainbowDQN's update heads in
+    one launch per depth (MixedStreamsFn), or None where the kernels do not
+    apply (every stream a create_mlp stack of one depth, one LayerNorm eps,
+    at most six streams)."""
+    if not enabled() or len(nograd_streams) + len(grad_streams) > 6 or not grad_streams:
+        return None
+    if (not isinstance(x, torch.Tensor) or not x.is_cuda or x.dtype != torch.float32 or x.dim() != 2
+            or x.shape[0] > _MAX_ROWS):
+        return None
+    if any(t.shape != x.shape or t.dtype != x.dtype or not t.is_cuda or not t.is_contiguous() for t in nograd_xs):
+        return None
+    from ..algorithms.learn_graph import _hooked
+
+    plans_ng = [_stream_plan(s) for s in nograd_streams]
+    plans_g = [_stream_plan(s) for s in grad_streams]
+    plans = plans_ng + plans_g
+    if any(p is None for p in plans) or len({len(p) for p in plans}) != 1 or _hooked(*nograd_streams, *grad_streams):
+        return None
+    if any(p[0][0].in_features != x.shape[1] for p in plans):
+        return None
+    got_ng, got_g = _params(plans_ng), _params(plans_g)
+    if got_ng is None or got_g is None or got_ng[0].eps != got_g[0].eps:
+        return None
+    (meta_ng, ts_ng), (meta_g, ts_g) = got_ng, got_g
+    return MixedStreamsFn.apply(meta_g, meta_ng, [t.detach() for t in ts_ng], list(nograd_xs), x, *ts_g)

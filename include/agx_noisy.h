@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AGX_NOISY_MAX_STREAMS 4
+#define AGX_NOISY_MAX_STREAMS 6
 #define AGX_NOISY_MAX_LAYERS 4
 #define AGX_NOISY_MAX_ROWS 1024
 
@@ -56,13 +56,14 @@ typedef struct agx_noisy_stream_layer {
 } agx_noisy_stream_layer;
 
 /* layers [n_streams][n_layers]; every stream's layer 0 reads x [B][fin].
- * 1 <= n_streams <= 4, 1 <= n_layers <= 4, 0 <= B <= 1024. */
+ * 1 <= n_streams <= 6, 1 <= n_layers <= 4, 0 <= B <= 1024. */
 int agx_noisy_streams_forward(const agx_noisy_stream_layer *layers, int32_t n_streams, int32_t n_layers, const float *x,
                               int64_t B, float ln_eps, void *stream);
 
 /* The same forward with stream s's layer 0 reading xs[s] [B][fin] (no-grad
  * passes over several networks at once: RainbowDQN's online and target
- * heads on the next observations, each on its own network's latent). */
+ * heads on the next observations, each on its own network's latent, and
+ * the online head on the observations whose backward follows). */
 int agx_noisy_streams_forward_each(const agx_noisy_stream_layer *layers, int32_t n_streams, int32_t n_layers,
                                    const float *const *xs, int64_t B, float ln_eps, void *stream);
 
