@@ -246,13 +246,18 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         samples = self._gather_sampled(idx)
         samples["weights"] = w.unsqueeze(1)
         samples["idxs"] = idx.unsqueeze(1)
+        self._sampled = (idx.data_ptr(), idx.numel(), idx._version)  # in range by construction (err checked)
         return samples
 
     def update_priorities(self, indices, priorities) -> None:
         """p = max(priority, 1e-5) ** alpha per index, in order (:411-428)."""
         idx = _to_tensor(indices, self.device).reshape(-1).to(torch.int64)
         pri = _to_tensor(priorities, self.device).reshape(-1).to(torch.float32)
-        if idx.numel():
+        # the indices sample() itself handed out (same storage, unmodified) are
+        # in range by construction: no device -> host read of their min / max
+        trusted = (isinstance(indices, torch.Tensor) and getattr(self, "_sampled", None) is not None
+                   and (idx.data_ptr(), idx.numel(), indices._version) == self._sampled)
+        if idx.numel() and not trusted:
             lo, hi = torch.stack(torch.aminmax(idx)).tolist()  # one device->host read
             if lo < 0 or hi >= self.max_size:
                 raise AssertionError("priority index out of range")
