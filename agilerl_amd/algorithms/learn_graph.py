@@ -12,7 +12,7 @@ graph (``torch.cuda.CUDAGraph``) and replayed on every later call:
 
 * the first call with a key runs eagerly (it also makes every lazily created
   library handle and workspace); the second captures and replays;
-* inputs are copied into the graph's static tensors; ``.grad`` of every
+* inputs are copied into the graph's static tensors (one launch); ``.grad`` of every
   parameter is re-pointed at the captured gradient tensors after a replay;
 * the host bookkeeping of the flat tail (a mutated learning rate, a torch
   optimizer step taken outside ``learn``, the torch ``step`` tensors) runs
@@ -44,10 +44,50 @@ _CAPTURE_AFTER = 1  # eager calls of a key before it is captured
 
 
 class _Entry:
-    __slots__ = ("eager", "graph", "inputs", "outputs", "grads", "failed")
+    __slots__ = ("eager", "graph", "inputs", "outputs", "grads", "failed", "copy")
 
     def __init__(self):
         self.eager, self.graph, self.inputs, self.outputs, self.grads, self.failed = 0, None, None, None, None, False
+        self.copy = None  # _copy_plan's result once the graph exists
+
+
+def _copy_plan(statics: list):
+    """The static inputs as one batched copy: when every one is contiguous
+    with the same leading (batch) dimension B, agx_replay_gather over
+    idx = arange(B) moves all of them in one launch (torch's _foreach_copy_
+    is one blit per tensor here).  -> (idx, dst array, row-byte array) or
+    False."""
+    import ctypes
+
+    if not statics or len(statics) > 8 or any(x.dim() == 0 for x in statics):
+        return False
+    B = statics[0].shape[0]
+    if not 1 <= B < 65536 or any(x.shape[0] != B or not x.is_contiguous() or x[0].numel() == 0 for x in statics):
+        return False
+    n = len(statics)
+    idx = torch.arange(B, dtype=torch.int64, device=statics[0].device)
+    dsts = (ctypes.c_void_p * n)(*[x.data_ptr() for x in statics])
+    rbytes = (ctypes.c_int64 * n)(*[x[0].numel() * x.element_size() for x in statics])
+    return idx, dsts, rbytes
+
+
+def _copy_inputs(ent, inputs: list) -> None:
+    """The batch into the static inputs (same shapes and dtypes: the key)."""
+    if ent.copy is None:
+        ent.copy = _copy_plan(ent.inputs)
+    if ent.copy is False or not all(x.is_contiguous() for x in inputs):
+        torch._foreach_copy_(ent.inputs, inputs)
+        return
+    import ctypes
+
+    from .. import _lib
+
+    idx, dsts, rbytes = ent.copy
+    n = len(inputs)
+    srcs = (ctypes.c_void_p * n)(*[x.data_ptr() for x in inputs])
+    B = idx.numel()
+    _lib.call("agx_replay_gather", ctypes.cast(srcs, ctypes.c_void_p), ctypes.cast(dsts, ctypes.c_void_p),
+              ctypes.cast(rbytes, ctypes.c_void_p), n, idx.data_ptr(), B, B, None, _lib.stream())
 
 
 def enabled() -> bool:
@@ -118,7 +158,7 @@ def run(fs, key: tuple, inputs: list, body, nets: tuple, max_norm: float, tau: f
         ent.graph, ent.inputs, ent.outputs = g, statics, outs
         ent.grads = [p.grad for p in fs.params]
     else:
-        torch._foreach_copy_(ent.inputs, inputs)  # the batch into the static inputs: one launch for all
+        _copy_inputs(ent, inputs)
     fs.sync()
     ent.graph.replay()
     fs.advance()
